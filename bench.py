@@ -1,0 +1,181 @@
+"""bench.py — eval_g + eval_jac_g throughput of the MI355X engine on the ANYmal trot (2.4 s) batch.
+
+Contract (see the task's bench section): `python bench.py --gpus N --steps K --warmup W`; for N>1
+launched by torch.distributed.run, one rank per GPU. A "step" is one fused launch computing g and
+every Jacobian nonzero for the rank's batch of B independent ANYmal problems (BASELINE configs[2],
+randomised start/goal/terrain as configs[4] describes). Inputs are resident in HBM before the timed
+region; K steps are bracketed by barrier + synchronize, the max over ranks is taken, rank 0 prints
+one JSON line. Weak scaling: B problems per GPU, no collective on the data path.
+
+roofline: algorithmic bytes per launch = B * 8 * (n + m + nnz) (+ terrain record), over the
+kernel's average duration measured with HIP events on the launch stream.
+cpu_baseline: the CPU oracle (oracle/, a faithful C restatement of the reference path; kind
+"port"), rank 0 at N=1 only, on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+SEED = 20261015
+N_X = 4          # pre-generated x sets cycled over (every step reads a different x)
+
+
+def make_batch(prob, B, first_id):
+    """Randomised instances: start xy ~ U(-0.5,0.5), yaw ~ U(-0.3,0.3);
+    goal = start + (U(1.5,2.5), U(-0.3,0.3)); terrain Flat(h~U(0,0.3)) or Stairs(start~U(0.8,1.4),
+    heights~U(0.1,0.25)); x = x0 + sigma * N(0,1) per variable-set kind."""
+    from towr2025_amd import formulation as F
+    from towr2025_amd import _capi as capi
+    sig_kind = {capi.VAR_BASE_LIN: 0.05, capi.VAR_BASE_ANG: 0.1, capi.VAR_EE_MOTION: 0.05,
+                capi.VAR_EE_ANG: 0.1, capi.VAR_EE_FORCE: 20.0, capi.VAR_EE_TORQUE: 1.0}
+    sigma = np.zeros(prob.n)
+    for kind, _ee, c0, n in prob.varset_info():
+        sigma[c0:c0 + n] = sig_kind[kind]
+    X = np.zeros((N_X, B, prob.n))
+    terrains = []
+    for b in range(B):
+        rng = np.random.default_rng(SEED + first_id + b)
+        sx, sy = rng.uniform(-0.5, 0.5, 2)
+        syaw = rng.uniform(-0.3, 0.3)
+        gx, gy = sx + rng.uniform(1.5, 2.5), sy + rng.uniform(-0.3, 0.3)
+        if rng.uniform() < 0.5:
+            ter = F.HeightMap.Flat(rng.uniform(0.0, 0.3))
+        else:
+            ter = F.HeightMap(F.HeightMap.StairsID, (rng.uniform(0.8, 1.4), 0.4, rng.uniform(0.1, 0.25),
+                                                     rng.uniform(0.1, 0.25), 1.0))
+        f = F.anymal_trot(goal=(gx, gy, 0.0), terrain=ter, start_xy=(sx, sy), start_yaw=syaw, goal_yaw=syaw)
+        d = f.to_desc()
+        x0 = prob.initial_x_for(d.init, d.terrain)
+        for k in range(N_X):
+            X[k, b] = x0 + sigma * rng.standard_normal(prob.n)
+        terrains.append(d.terrain)
+    return X, terrains
+
+
+def cpu_baseline(desc, X, seconds):
+    """The oracle timed on this host's cores, one independent problem per thread."""
+    from oracle import oracle as O
+    O.build()
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    t1, _ = O.bench(desc, 1, 3, X)                         # per-call time estimate (1 thread)
+    per_call = t1 / 3
+    calls = max(4, int(seconds / per_call))
+    secs, done = O.bench(desc, threads, calls, X)
+    return {"value": done / secs, "unit": "calls/s", "cores": threads, "kind": "port",
+            "sample": f"{done} calls ({calls}/thread x {threads} threads) of the CPU oracle "
+                      f"(oracle/towr_oracle.c) on ANYmal trot x-vectors, {secs:.1f} s wall; "
+                      f"1-thread {1.0 / per_call:.1f} calls/s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=4096, help="problems per GPU (weak scaling)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--tiles-per-block", type=int, default=0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from towr2025_amd import TowrGpuProblem
+    from towr2025_amd import formulation as F
+    desc = F.anymal_trot().to_desc()
+    prob = TowrGpuProblem(desc, device=local)
+    if args.tiles_per_block:
+        prob.set_tiles_per_block(args.tiles_per_block)
+    B = args.batch
+    Xh, terrains = make_batch(prob, B, first_id=rank * B)
+    prob.set_batch_terrain(terrains)
+    ldv = (prob.nnz + 15) // 16 * 16
+    ldg = (prob.m + 15) // 16 * 16
+    X = torch.from_numpy(Xh).to(dev)
+    G = torch.empty((B, ldg), dtype=torch.float64, device=dev)
+    V = torch.empty((B, ldv), dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step(i):
+        prob.eval_batch_device(X[i % N_X], G, V, stream=stream)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for i in range(args.steps):
+        step(i)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern_ms = e0.elapsed_time(e1) / args.steps
+    if world > 1:
+        t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall, kern_ms = float(t[0]), float(t[1])
+
+    calls = B * world * args.steps
+    value = calls / wall
+    bytes_call = prob.algorithmic_bytes_per_call()
+    achieved = B * bytes_call / (kern_ms * 1e-3) / 1e9
+    peak = 8000.0
+    out = {
+        "metric": "full eval_g+eval_jac_g calls/sec, ANYmal trot 2.4s horizon; 1/2/4/8-GPU batch",
+        "value": value, "unit": "calls/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic: randomised ANYmal trot instances (start/goal/terrain), x = x0 + seeded noise",
+        "config": {"workload": "ANYmal trot 2.4s (quadruped C1), NlpFormulation defaults, batch of independent problems",
+                   "problems_per_gpu": B, "n": prob.n, "m": prob.m, "nnz": prob.nnz,
+                   "calls_per_step": B * world, "terrains": "Flat(h~U(0,0.3)) | Stairs(randomised)",
+                   "parallelism": f"dp{world} (problem shards, no collective)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
+                     "frac": achieved / peak, "traffic": None,
+                     "kernel_ms": kern_ms, "bytes_per_launch": B * bytes_call},
+    }
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            with open(pmc) as fh:
+                rec = json.load(fh)
+            if rec.get("problems_per_launch") == B:
+                out["roofline"]["traffic"] = rec["hbm_bytes_per_launch"]
+                out["roofline"]["traffic_source"] = rec.get("source")
+        except Exception:
+            pass
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(desc, Xh[0, :8], args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,221 @@
+/*
+ * towr_gpu.h — C-ABI of the MI355X (gfx950) constraint/Jacobian evaluation engine for towr's NLP.
+ *
+ * This is the drop-in boundary for the reference's eval_g / eval_jac_g hot path
+ * (hexb66/towr2025). In the reference, IPOPT calls ifopt's IpoptAdapter::eval_g /
+ * eval_jac_g, which call ifopt::Problem::EvalConstraints / EvalNonzerosOfJacobian, which call
+ * every ifopt::ConstraintSet's GetValues() and FillJacobianBlock(var_set, jac)
+ * (towr/include/towr/constraints/time_discretization_constraint.h:50-73,
+ *  towr/src/constraints/time_discretization_constraint.cc:65-96). Those callbacks are what
+ * this library replaces; IPOPT keeps running on the host.
+ *
+ * Plain C: POD structs, plain pointers and sizes, int status codes (0 = ok, < 0 = error),
+ * no exceptions cross the boundary, no torch types. One handle per host thread; calls on a
+ * handle are serialised on that handle's HIP stream.
+ *
+ * Numbers: every value is IEEE binary64, as in the reference (Eigen double throughout).
+ * Jacobian layout: CSR in ifopt order — rows = constraint sets in the order given, each set's
+ * rows contiguous; columns = variable sets in the order given; within a row, columns ascend
+ * (Eigen::SparseMatrix<double,RowMajor> after setFromTriplets/makeCompressed, which is the
+ * (iRow, jCol) order ifopt's IpoptAdapter::eval_jac_g emits).
+ */
+#ifndef TOWR_GPU_H_
+#define TOWR_GPU_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TOWR_GPU_ABI_VERSION 1
+
+#define TOWR_MAX_EE          4
+#define TOWR_MAX_PHASES      48
+#define TOWR_MAX_VARSETS     (2 + 5 * TOWR_MAX_EE)
+#define TOWR_MAX_CONSTRAINTS 64
+
+/* ---- status codes ---------------------------------------------------------------------- */
+#define TOWR_OK                  0
+#define TOWR_ERR_INVALID        -1   /* malformed description / argument                       */
+#define TOWR_ERR_UNSUPPORTED    -2   /* valid for the reference, not (yet) for this engine     */
+#define TOWR_ERR_HIP            -3   /* HIP runtime failure (message in towr_gpu_last_error)    */
+#define TOWR_ERR_NO_DEVICE      -4   /* no gfx950 device / extension not loadable on this host  */
+
+/* ---- terrain: HeightMap::TerrainID (towr/include/towr/terrain/height_map.h:79-86) --------- */
+enum towr_terrain_id {
+  TOWR_TERRAIN_FLAT       = 0, /* FlatGround   p[0]=height                                  (height_map_examples.h:45-52)  */
+  TOWR_TERRAIN_BLOCK      = 1, /* Block        p[0]=block_start p[1]=length p[2]=height p[3]=eps (:57-69)            */
+  TOWR_TERRAIN_STAIRS     = 2, /* Stairs       p[0]=first_step_start p[1]=first_step_width
+                                  p[2]=height_first_step p[3]=height_second_step p[4]=width_top   (:74-84)           */
+  TOWR_TERRAIN_GAP        = 3, /* Gap          p[0]=gap_start p[1]=w p[2]=h                  (:89-112)                */
+  TOWR_TERRAIN_SLOPE      = 4, /* Slope        p[0]=slope_start p[1]=up_length p[2]=down_length p[3]=height_center (:117-131) */
+  TOWR_TERRAIN_CHIMNEY    = 5, /* Chimney      p[0]=x_start p[1]=length p[2]=y_start p[3]=slope (:136-148)             */
+  TOWR_TERRAIN_CHIMNEY_LR = 6, /* ChimneyLR    p[0]=x_start p[1]=length p[2]=y_start p[3]=slope (:153-166)             */
+  TOWR_TERRAIN_STEPS      = 7  /* FiveStepStairs of towr/test/hopper_example.cc:53-86:
+                                  p[0]=stairs_start p[1]=step_depth p[2]=step_height p[3]=num_steps              */
+};
+
+typedef struct {
+  int32_t id;              /* towr_terrain_id                                                  */
+  int32_t reserved;
+  double  friction_coeff;  /* HeightMap::friction_coeff_ = 0.5 (height_map.h:136)             */
+  double  p[8];            /* per-type parameters, see enum                                    */
+} towr_terrain_t;
+
+/* ---- robot: SingleRigidBodyDynamics + KinematicModel (models/examples/ *.h) ---------------- */
+typedef struct {
+  double  mass;                       /* DynamicModel::m_                                       */
+  double  gravity;                    /* DynamicModel::g_ = 9.80665 (dynamic_model.cc:37)        */
+  double  inertia[6];                 /* Ixx Iyy Izz Ixy Ixz Iyz, BuildInertiaTensor convention
+                                         (single_rigid_body_dynamics.cc:36-44)                   */
+  int32_t n_ee;
+  int32_t reserved;
+  double  nominal_stance[TOWR_MAX_EE][3];  /* KinematicModel::nominal_stance_                  */
+  double  max_dev[TOWR_MAX_EE][3];         /* KinematicModel::max_dev_from_nominal_            */
+  double  min_dev[TOWR_MAX_EE][3];         /* KinematicModel::min_dev_from_nominal_            */
+} towr_robot_t;
+
+/* ---- variable sets: ids of towr/include/towr/variables/variable_names.h:43-75 ------------- */
+enum towr_varset_kind {
+  TOWR_VAR_BASE_LIN    = 0,  /* "base-lin"      NodesVariablesAll                              */
+  TOWR_VAR_BASE_ANG    = 1,  /* "base-ang"      NodesVariablesAll (Euler ZYX)                  */
+  TOWR_VAR_EE_MOTION   = 2,  /* "ee-motion_i"   NodesVariablesEEMotion                         */
+  TOWR_VAR_EE_ANG      = 3,  /* "ee-ang_i"      NodesVariablesEEAng                            */
+  TOWR_VAR_EE_FORCE    = 4,  /* "ee-force_i"    NodesVariablesEEForce                          */
+  TOWR_VAR_EE_TORQUE   = 5,  /* "ee-torque_i"   NodesVariablesEETorque                         */
+  TOWR_VAR_EE_SCHEDULE = 6   /* "ee-schedule_i" PhaseDurations (only with optimize_timings)    */
+};
+
+typedef struct {
+  int32_t kind;  /* towr_varset_kind           */
+  int32_t ee;    /* endeffector id (ee sets)   */
+} towr_varset_t;
+
+/* ---- constraint sets: Parameters::ConstraintName (parameters.h:141-152) --------------------- */
+enum towr_constraint_kind {
+  TOWR_C_DYNAMIC          = 0, /* DynamicConstraint            dt; T                  (dynamic_constraint.cc:38-148)             */
+  TOWR_C_RANGE_OF_MOTION  = 1, /* RangeOfMotionConstraint      dt; T; ee              (range_of_motion_constraint.cc:37-131)     */
+  TOWR_C_FORCE            = 2, /* ForceConstraint (node-based) ee; p[0]=force limit   (force_constraint.cc:37-171)               */
+  TOWR_C_FORCE_DISCRETIZED= 3, /* ForceConstraintDiscretized   dt; T; ee; p[0]=limit  (force_constraint_discretized.cc:71-221)   */
+  TOWR_C_TERRAIN          = 4, /* TerrainConstraint            ee; p[0]=min p[1]=max  (terrain_constraint.cc:36-111)             */
+  TOWR_C_BASE_MOTION      = 5, /* BaseMotionConstraint         dt; T; p[0..5]=ax,ay,lz bounds (base_motion_constraint.cc:38-91)  */
+  TOWR_C_SPLINE_ACC       = 6, /* SplineAccConstraint          ee=0 base-lin, ee=1 base-ang (spline_acc_constraint.cc:34-86)     */
+  TOWR_C_BASE_HEIGHT      = 7, /* BaseHeightConstraint         p[0]=safety distance   (base_height_constraint.cc:35-110)         */
+  TOWR_C_SWING            = 8, /* SwingConstraint              ee; p[0]=t_swing_avg (0.3, swing_constraint.h:68)                  */
+  TOWR_C_TOTAL_DURATION   = 9  /* TotalDurationConstraint      ee; T                  (total_duration_constraint.cc:36-72)       */
+};
+
+typedef struct {
+  int32_t kind;   /* towr_constraint_kind                                                       */
+  int32_t ee;     /* endeffector id, or spline id for TOWR_C_SPLINE_ACC                        */
+  double  T;      /* total horizon the constraint was constructed with                         */
+  double  dt;     /* discretisation step of TimeDiscretizationConstraint subclasses            */
+  double  p[6];   /* per-kind parameters (see enum)                                            */
+} towr_constraint_t;
+
+/* ---- initial guess (NlpFormulation::MakeBaseVariables etc., nlp_formulation.cc:121-346) ---- */
+enum towr_init_mode {
+  TOWR_INIT_FORMULATION = 0,  /* NlpFormulation::GetVariableSets initialisation                  */
+  TOWR_INIT_PROCEDURAL  = 1   /* plain SetByLinearInterpolation of towr/test/procedural_example.cc:134-166 */
+};
+
+typedef struct {
+  int32_t mode;                   /* towr_init_mode                                             */
+  int32_t reserved;
+  double  base_lin_p0[3], base_lin_v0[3], base_ang_p0[3], base_ang_v0[3];  /* initial_base_     */
+  double  base_lin_p1[3], base_lin_v1[3], base_ang_p1[3], base_ang_v1[3];  /* final_base_       */
+  double  ee_p0[TOWR_MAX_EE][3];  /* initial_ee_W_                                              */
+  double  ee_p1[TOWR_MAX_EE][3];  /* procedural mode only: goal footholds                        */
+} towr_init_t;
+
+/* ---- full problem description --------------------------------------------------------------- */
+typedef struct {
+  int32_t        abi_version;               /* TOWR_GPU_ABI_VERSION                                */
+  int32_t        angular_rep;               /* 0 = EulerZYX (Parameters::AngularRepresentation)    */
+  towr_robot_t   robot;
+  towr_terrain_t terrain;
+  /* Parameters (parameters.cc:40-105)                                                            */
+  double   total_time;                      /* Parameters::GetTotalTime()                          */
+  double   duration_base_polynomial;        /* 0.1                                                  */
+  int32_t  ee_polynomials_per_swing_phase;  /* 2                                                    */
+  int32_t  force_polynomials_per_stance_phase;   /* 3                                               */
+  int32_t  torque_polynomials_per_stance_phase;  /* 3                                               */
+  int32_t  optimize_timings;                /* Parameters::IsOptimizeTimings()                     */
+  double   bound_phase_duration[2];         /* (0.2, 1.0)                                          */
+  int32_t  n_phases[TOWR_MAX_EE];
+  int32_t  contact_at_start[TOWR_MAX_EE];   /* ee_in_contact_at_start_                              */
+  double   phase_durations[TOWR_MAX_EE][TOWR_MAX_PHASES];  /* ee_phase_durations_                 */
+  int32_t  n_varsets;                       /* order = ifopt AddVariableSet order                   */
+  int32_t  n_constraints;                   /* order = ifopt AddConstraintSet order                 */
+  towr_varset_t     varsets[TOWR_MAX_VARSETS];
+  towr_constraint_t constraints[TOWR_MAX_CONSTRAINTS];
+  towr_init_t       init;
+} towr_problem_desc_t;
+
+typedef struct towr_gpu_handle_s* towr_gpu_handle;
+
+/* ---- lifecycle ------------------------------------------------------------------------------- */
+/* Builds the layout (variable maps, time grids, CSR pattern, per-item slot tables) on the host and
+ * uploads it to `device`. device < 0 creates a layout-only handle (sizes, structure, x0; every
+ * evaluation entry point then returns TOWR_ERR_NO_DEVICE) — used by host-side structure checks. Replaces NlpFormulation::GetVariableSets/GetConstraints + ifopt
+ * Problem::AddVariableSet/AddConstraintSet (nlp_formulation.cc:76-378, hopper_example.cc:154-161). */
+int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle* out);
+int towr_gpu_destroy(towr_gpu_handle h);
+const char* towr_gpu_last_error(towr_gpu_handle h);   /* h may be NULL: last global error         */
+int towr_gpu_abi_version(void);
+
+/* n = ifopt Problem::GetNumberOfOptimizationVariables, m = GetNumberOfConstraints,
+ * nnz = nonzeros of GetJacobianOfConstraints (what IpoptAdapter::get_nlp_info reports).          */
+int towr_gpu_sizes(towr_gpu_handle h, int32_t* n, int32_t* m, int64_t* nnz);
+
+/* Jacobian structure, 0-based (IpoptAdapter::eval_jac_g with values == NULL; C_STYLE indexing). */
+int towr_gpu_jac_structure(towr_gpu_handle h, int32_t* iRow, int32_t* jCol);
+/* Same pattern as CSR: row_ptr[m+1], col[nnz].                                                   */
+int towr_gpu_jac_csr(towr_gpu_handle h, int64_t* row_ptr, int32_t* col);
+
+/* Starting point x0 = ifopt Problem::GetVariableValues() after NlpFormulation initialisation.    */
+int towr_gpu_initial_x(towr_gpu_handle h, double* x0);
+
+/* x0 of another instance that shares this layout (same robot, gait, horizon, constraint list):
+ * only the start/goal states and the terrain differ (BASELINE config 5's randomised batch).      */
+int towr_gpu_initial_x_for(towr_gpu_handle h, const towr_init_t* init, const towr_terrain_t* terrain, double* x0);
+/* Column range of variable set i (AddVariableSet order): kind, ee, first column, size.          */
+int towr_gpu_varset_info(towr_gpu_handle h, int32_t i, int32_t* kind, int32_t* ee, int32_t* col0, int32_t* n);
+
+/* ---- single-problem host callbacks (what IpoptAdapter calls) -------------------------------- */
+/* g = ifopt Problem::EvalConstraints(x)          (IpoptAdapter::eval_g)                         */
+int towr_gpu_eval_g(towr_gpu_handle h, const double* x, double* g);
+/* values = ifopt Problem::EvalNonzerosOfJacobian(x)  (IpoptAdapter::eval_jac_g, values != NULL) */
+int towr_gpu_eval_jac_values(towr_gpu_handle h, const double* x, double* values);
+/* both at once (one fused launch)                                                                */
+int towr_gpu_eval_g_jac(towr_gpu_handle h, const double* x, double* g, double* values);
+
+/* ---- batched evaluation over independent problems that share the layout ---------------------- */
+/* Per-problem terrain parameters (the only per-instance input to g/J besides x). `terrains` is a
+ * host array of B entries; all entries must keep the Jacobian pattern identical. */
+int towr_gpu_set_batch_terrain(towr_gpu_handle h, int32_t B, const towr_terrain_t* terrains);
+
+/* Device-resident batch: X[b*ldx + j], G[b*ldg + i], V[b*ldv + k] are DEVICE pointers (HBM);
+ * `stream` is a hipStream_t (NULL = the handle's stream). want_g / want_jac select outputs.
+ * Asynchronous with respect to the host.                                                         */
+int towr_gpu_eval_batch_device(towr_gpu_handle h, int32_t B,
+                               const double* X, int64_t ldx,
+                               double* G, int64_t ldg,
+                               double* V, int64_t ldv,
+                               int32_t want_g, int32_t want_jac, void* stream);
+
+/* Host batch (H2D of X, D2H of G and V through pinned staging; contiguous lds = n, m, nnz).      */
+int towr_gpu_eval_batch(towr_gpu_handle h, int32_t B, const double* X, double* G, double* V);
+
+/* Sets the launch geometry (tiles per workgroup); 0 = automatic. For benchmarking.              */
+int towr_gpu_set_tiles_per_block(towr_gpu_handle h, int32_t tiles_per_block);
+
+/* Per-launch algorithmic byte count used for the roofline: 8*(n + m + nnz) + terrain bytes.     */
+int64_t towr_gpu_algorithmic_bytes_per_call(towr_gpu_handle h);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TOWR_GPU_H_ */

@@ -1,0 +1,41 @@
+"""The BASELINE.json configurations as ProblemDescs (+ extra parity cases)."""
+from towr2025_amd import formulation as F
+
+
+def config_descs():
+    """name -> ProblemDesc. configs[0..3] of BASELINE.json (gait optimisation excluded: next tier)."""
+    return {
+        "monoped_hopper_flat": F.monoped_hopper().to_desc(),                       # configs[0]
+        "monoped_procedural": F.procedural_desc(),                                 # procedural_example.cc
+        "biped_walk_2s": F.biped_walk().to_desc(),                                 # configs[1]
+        "anymal_trot_2p4s": F.anymal_trot().to_desc(),                             # configs[2]
+        "anymal_trot_stairs": F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.StairsID)).to_desc(),
+        "hopper_five_steps": _hopper_steps(),
+        "anymal_slope_yaw": F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.SlopeID),
+                                          goal=(1.8, 0.3, 0.0), goal_yaw=0.3).to_desc(),
+        "hyq_chimney": _hyq(F.HeightMap.ChimneyID),
+        "hyq_gap": _hyq(F.HeightMap.GapID),
+        "anymal_block_baserom": _anymal_baserom(),
+    }
+
+
+def _hopper_steps():
+    f = F.monoped_hopper()
+    f.terrain_ = F.HeightMap.MakeTerrain(F.HeightMap.StepsID)
+    return f.to_desc()
+
+
+def _hyq(tid):
+    f = F.anymal_trot(terrain=F.HeightMap.MakeTerrain(tid))
+    f.model_ = F.RobotModel(F.RobotModel.Hyq)
+    nominal = f.model_.kinematic_model.nominal_stance
+    f.initial_ee_W_ = [(p[0], p[1], 0.0) for p in nominal]
+    f.initial_base_ = F.BaseState(lin_p=(0.0, 0.0, -nominal[0][2]))
+    return f.to_desc()
+
+
+def _anymal_baserom():
+    f = F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.BlockID))
+    f.params_.constraints_.append(F.Parameters.BaseRom)
+    f.params_.dt_constraint_force_ = 0.0   # node-based ForceConstraint instead of the discretised one
+    return f.to_desc()

@@ -1,0 +1,36 @@
+// TEST INFRASTRUCTURE ONLY — host emulation of towr_eval_kernel's per-item loop, used by the
+// CPU test suite to check engine_math.h values against the oracle before GPU runs. It is built
+// into tests/host_emu/build/libemu.so and is never linked into or loaded by the product.
+#include "../../towr2025_amd/csrc/layout.h"
+
+#include <cstring>
+#include <string>
+
+using namespace tg;
+
+namespace {
+struct AccEmit {
+  const int32_t* slot; int j; double* v; double* gout;
+  void g(int row, double val) { gout[row] = val; }
+  void operator()(int, int col, double val, bool) {
+    if (col >= 0) { int s = slot[j]; if (s >= 0) v[s] += val; }
+    ++j;
+  }
+};
+}
+
+extern "C" int emu_eval(const towr_problem_desc_t* d, const double* x, double* g, double* v, char* err, int errlen) {
+  Layout L; std::string e;
+  int rc = build_layout(*d, L, e);
+  if (rc) { if (err) std::snprintf(err, errlen, "%s", e.c_str()); return rc; }
+  std::memset(g, 0, sizeof(double) * L.m);
+  std::memset(v, 0, sizeof(double) * L.nnz);
+  Ctx c{};
+  c.x = x; c.nodecol = L.nodecol.data(); c.spl = L.spl.data(); c.dur = L.dur.data();
+  c.ter = &L.terrain; c.rb = L.rb; c.fdisc_motion = L.fdisc_motion;
+  for (const ItemDesc& it : L.items) {
+    AccEmit em{L.slots.data() + it.slot, 0, v, g};
+    eval_item(c, it, em);
+  }
+  return 0;
+}

@@ -1,0 +1,91 @@
+"""GPU parity: the HIP engine through the C-ABI vs the CPU oracle (pattern bit-exact, values within
+the tolerance of tests/parity.py), on every configuration and on seeded perturbations of x0."""
+import numpy as np
+import pytest
+
+from oracle.oracle import Oracle
+from tests.configs import config_descs
+from tests.parity import assert_close
+from towr2025_amd import TowrGpuProblem
+
+pytestmark = pytest.mark.gpu
+
+CONFIGS = config_descs()
+
+
+def _perturb(x0, seed, scale=0.05):
+    return x0 + scale * np.random.default_rng(seed).standard_normal(x0.shape)
+
+
+@pytest.mark.parametrize("name", sorted(CONFIGS))
+def test_pattern_and_values(name):
+    desc = CONFIGS[name]
+    o = Oracle(desc)
+    p = TowrGpuProblem(desc, device=0)
+    x0 = o.initial_x()
+    np.testing.assert_array_equal(p.initial_x(), x0)
+    r, c, _ = o.eval_jac(x0)
+    pr, pc = p.jac_structure()
+    np.testing.assert_array_equal(pr, r)
+    np.testing.assert_array_equal(pc, c)
+    for seed in (0, 1, 2):
+        x = x0 if seed == 0 else _perturb(x0, 20261015 + seed)
+        g_ref = o.eval_g(x)
+        rr, cc, v_ref = o.eval_jac(x)
+        if len(rr) != len(r) or not (np.array_equal(rr, r) and np.array_equal(cc, c)):
+            continue   # reference pattern moved at this x (only Gap terrain): out of contract
+        g = p.eval_g(x)
+        v = p.eval_jac_values(x)
+        assert_close(g_ref, g, r, v_ref, v, o.m, f"{name} seed {seed} (separate calls)")
+        g2, v2 = p.eval_g_jac(x)
+        np.testing.assert_array_equal(g2, g)
+        np.testing.assert_array_equal(v2, v)
+
+
+def test_batch_host_matches_single():
+    desc = CONFIGS["anymal_trot_2p4s"]
+    o = Oracle(desc)
+    p = TowrGpuProblem(desc)
+    x0 = o.initial_x()
+    X = np.stack([_perturb(x0, 100 + b) for b in range(7)])
+    G, V = p.eval_batch(X)
+    r, _, _ = o.eval_jac(x0)
+    for b in range(7):
+        assert_close(o.eval_g(X[b]), G[b], r, o.eval_jac(X[b])[2], V[b], o.m, f"batch {b}")
+
+
+def test_batch_device_per_problem_terrain():
+    import torch
+    from towr2025_amd import formulation as F
+    base = F.anymal_trot()
+    desc = base.to_desc()
+    p = TowrGpuProblem(desc)
+    B = 33
+    rng = np.random.default_rng(7)
+    terrains, X = [], []
+    for b in range(B):
+        if b % 2:
+            t = F.HeightMap.Flat(rng.uniform(0, 0.3))
+        else:
+            t = F.HeightMap(F.HeightMap.StairsID, (rng.uniform(0.8, 1.4), 0.4, rng.uniform(0.1, 0.25), rng.uniform(0.1, 0.25), 1.0))
+        f = F.anymal_trot(terrain=t)
+        terrains.append(f.terrain_.to_c())
+        o = Oracle(f.to_desc())
+        X.append(_perturb(o.initial_x(), 500 + b))
+    X = np.stack(X)
+    p.set_batch_terrain(terrains)
+    ldv = (p.nnz + 15) // 16 * 16
+    dev = torch.device("cuda:0")
+    Xd = torch.from_numpy(X).to(dev)
+    Gd = torch.full((B, p.m), np.nan, dtype=torch.float64, device=dev)
+    Vd = torch.full((B, ldv), np.nan, dtype=torch.float64, device=dev)
+    p.eval_batch_device(Xd, Gd, Vd)
+    torch.cuda.synchronize()
+    G, V = Gd.cpu().numpy(), Vd.cpu().numpy()[:, :p.nnz]
+    for b in range(B):
+        d = F.anymal_trot(terrain=None).to_desc()
+        d.terrain = terrains[b]
+        o = Oracle(d)
+        rr, _, v_ref = o.eval_jac(X[b])
+        assert_close(o.eval_g(X[b]), G[b], rr, v_ref, V[b], o.m, f"device batch {b}")
+    assert np.isnan(Vd.cpu().numpy()[:, p.nnz:]).all()   # padding untouched

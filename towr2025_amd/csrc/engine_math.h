@@ -1,0 +1,705 @@
+// engine_math.h — per-work-item evaluation of towr's constraint values and Jacobian entries.
+//
+// Single source for two instantiations:
+//   * device (towr_gpu.hip): the fused eval kernel, Emit = LDS accumulator indexed by slot table;
+//   * host   (layout.hip):   the structure pass at the starting point x0, Emit = recorder of the
+//                            (row, col) of every candidate entry (IPOPT's eval_jac_g(values=NULL)).
+// The host instantiation's values are discarded; g/J values are only ever produced on the GPU.
+//
+// A "work item" is one (constraint set, instance, group) triple. Each item emits its g rows and an
+// ordered list of Jacobian candidates (row, col, value, present). The ORDER of candidates is the
+// contract between the two instantiations: candidate j of an item lands in slot_table[item.slot + j].
+//
+// Math follows the reference formulas (file:line cited per function); Jacobians are formed by the
+// chain rule through the cubic-Hermite basis (polynomial.cc:135-214), which is exactly the
+// structure the reference builds with NodeSpline::GetJacobianWrtNodes + Eigen sparse products.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/towr_gpu.h"
+
+#define TG_HD __host__ __device__ __forceinline__
+
+namespace tg {
+
+enum { kPos = 0, kVel = 1, kAcc = 2 };
+enum { X = 0, Y = 1, Z = 2 };
+enum { AX = 0, AY = 1, AZ = 2, LX = 3, LY = 4, LZ = 5 };
+
+// spline ids: 0 base-lin, 1 base-ang, 2 + 4*ee + {0 motion, 1 ang, 2 force, 3 torque}
+enum { SP_BASE_LIN = 0, SP_BASE_ANG = 1 };
+TG_HD int sp_motion(int ee) { return 2 + 4 * ee + 0; }
+TG_HD int sp_force(int ee)  { return 2 + 4 * ee + 2; }
+TG_HD int sp_torque(int ee) { return 2 + 4 * ee + 3; }
+
+// work item types
+enum ItemType {
+  IT_DYN = 0,    // DynamicConstraint instant; group 0: base-lin + g, 1: base-ang, 2+ee: ee blocks
+  IT_ROM = 1,    // RangeOfMotionConstraint instant; group 0: base-lin + g, 1: base-ang, 2: motion
+  IT_FDISC = 2,  // ForceConstraintDiscretized instant
+  IT_FNODE = 3,  // ForceConstraint node
+  IT_TERR = 4,   // TerrainConstraint node
+  IT_BMOT = 5,   // BaseMotionConstraint instant
+  IT_SACC = 6,   // SplineAccConstraint junction
+  IT_BHGT = 7,   // BaseHeightConstraint node
+  IT_SWING = 8,  // SwingConstraint node
+  IT_COUNT = 9
+};
+
+struct SplineMeta {
+  int32_t node_off;  // first node's index into nodecol (6 ints per node: [deriv][dim])
+  int32_t n_polys;
+  int32_t dur_off;   // first polynomial duration in the durations table
+  int32_t reserved;
+};
+
+struct RobotC {
+  double m, g;
+  double Ib[9];      // BuildInertiaTensor (single_rigid_body_dynamics.cc:36-44), row-major
+  int32_t n_ee, reserved;
+};
+
+// 48-byte work-item descriptor, shared by all problems of a batch
+struct ItemDesc {
+  int32_t type, group, ee, k;   // k: instance index inside the constraint set
+  int32_t row0;                 // global row of the item's first row
+  int32_t a0, a1;               // node ids (FNODE: force node, motion node at phase start; ...)
+  int32_t slot;                 // first candidate's index into the slot table
+  double t;                     // time of the instant (time-discretised sets)
+  double p0;                    // scalar parameter (safety distance, t_swing_avg, T_poly, ...)
+};
+
+struct Ctx {
+  const double* x;              // this problem's decision vector (LDS on the device)
+  const int32_t* nodecol;       // node value -> global column of x, or -1 (constant 0)
+  const SplineMeta* spl;
+  const double* dur;            // polynomial durations
+  const towr_terrain_t* ter;    // this problem's terrain
+  RobotC rb;
+  int32_t fdisc_motion;         // ForceConstraintDiscretized motion block enabled (terrain has d2h)
+};
+
+// ----------------------------------------------------------------------------------------------
+// cubic Hermite polynomial (towr/src/helpers/polynomial.cc)
+// ----------------------------------------------------------------------------------------------
+struct SplinePt {
+  int poly;
+  double T, tl;
+  double p[3], v[3], a[3];
+};
+
+// Spline::GetSegmentID + GetLocalTime (spline.cc:48-78): eps = 1e-10, junction -> previous poly
+TG_HD int seg_lookup(const double* d, int n, double tg, double* tl) {
+  const double eps = 1e-10;
+  double t = 0.0;
+  int id = n - 1;   // the reference falls off an assert here; clamp to the last polynomial
+  for (int i = 0; i < n; ++i) {
+    t += d[i];
+    if (t >= tg - eps) { id = i; break; }
+  }
+  double l = tg;
+  for (int i = 0; i < id; ++i) l -= d[i];
+  *tl = l;
+  return id;
+}
+
+TG_HD double xval(const Ctx& c, int col) { return col >= 0 ? c.x[col] : 0.0; }
+TG_HD int node_col(const Ctx& c, int s, int node, int deriv, int dim) {
+  return c.nodecol[(c.spl[s].node_off + node) * 6 + deriv * 3 + dim];
+}
+// column of Hermite basis function b (0 n0.p, 1 n0.v, 2 n1.p, 3 n1.v) of polynomial `poly`, dim e
+TG_HD int basis_col(const Ctx& c, int s, int poly, int b, int e) {
+  return node_col(c, s, poly + (b >> 1), b & 1, e);
+}
+
+// CubicHermitePolynomial::UpdateCoeff (:97-104) + Polynomial::GetPoint (:47-58)
+TG_HD void poly_state(const Ctx& c, int s, int poly, double T, double tl, SplinePt& o) {
+  const double T2 = T * T, T3 = T2 * T, t2 = tl * tl, t3 = t2 * tl;
+  for (int e = 0; e < 3; ++e) {
+    const double p0 = xval(c, node_col(c, s, poly, kPos, e)), v0 = xval(c, node_col(c, s, poly, kVel, e));
+    const double p1 = xval(c, node_col(c, s, poly + 1, kPos, e)), v1 = xval(c, node_col(c, s, poly + 1, kVel, e));
+    const double ca = p0, cb = v0;
+    const double cc = -(3 * (p0 - p1) + T * (2 * v0 + v1)) / T2;
+    const double cd = (2 * (p0 - p1) + T * (v0 + v1)) / T3;
+    o.p[e] = ca + tl * cb + t2 * cc + t3 * cd;
+    o.v[e] = cb + 2 * tl * cc + 3 * t2 * cd;
+    o.a[e] = 2 * cc + 6 * tl * cd;
+  }
+}
+
+// Spline::GetPoint(t_global) (spline.cc:80-93)
+TG_HD void spline_eval(const Ctx& c, int s, double t, SplinePt& o) {
+  const SplineMeta m = c.spl[s];
+  o.poly = seg_lookup(c.dur + m.dur_off, m.n_polys, t, &o.tl);
+  o.T = c.dur[m.dur_off + o.poly];
+  poly_state(c, s, o.poly, o.T, o.tl, o);
+}
+
+// GetDerivativeOf{Pos,Vel,Acc}Wrt{Start,End}Node (polynomial.cc:135-234); b = 0 n0.p, 1 n0.v, 2 n1.p, 3 n1.v
+TG_HD void hermite_dpos(double T, double t, double H[4]) {
+  const double T2 = T * T, T3 = T2 * T, t2 = t * t, t3 = t2 * t;
+  H[0] = (2 * t3) / T3 - (3 * t2) / T2 + 1;
+  H[1] = t - (2 * t2) / T + t3 / T2;
+  H[2] = (3 * t2) / T2 - (2 * t3) / T3;
+  H[3] = t3 / T2 - t2 / T;
+}
+TG_HD void hermite_dvel(double T, double t, double H[4]) {
+  const double T2 = T * T, T3 = T2 * T, t2 = t * t;
+  H[0] = (6 * t2) / T3 - (6 * t) / T2;
+  H[1] = (3 * t2) / T2 - (4 * t) / T + 1;
+  H[2] = (6 * t) / T2 - (6 * t2) / T3;
+  H[3] = (3 * t2) / T2 - (2 * t) / T;
+}
+TG_HD void hermite_dacc(double T, double t, double H[4]) {
+  const double T2 = T * T, T3 = T2 * T;
+  H[0] = (12 * t) / T3 - 6 / T2;
+  H[1] = (6 * t) / T2 - 4 / T;
+  H[2] = 6 / T2 - (12 * t) / T3;
+  H[3] = (6 * t) / T2 - 2 / T;
+}
+
+// ----------------------------------------------------------------------------------------------
+// Euler ZYX (towr/src/helpers/euler_converter.cc)
+// ----------------------------------------------------------------------------------------------
+struct Trig { double sx, cx, sy, cy, sz, cz; };
+TG_HD Trig trig(const double a[3]) {
+  Trig r;
+  r.sx = sin(a[0]); r.cx = cos(a[0]);
+  r.sy = sin(a[1]); r.cy = cos(a[1]);
+  r.sz = sin(a[2]); r.cz = cos(a[2]);
+  return r;
+}
+// GetRotationMatrixBaseToWorld (:207-221)
+TG_HD void euler_R(const Trig& q, double R[3][3]) {
+  R[0][0] = q.cy * q.cz; R[0][1] = q.cz * q.sx * q.sy - q.cx * q.sz; R[0][2] = q.sx * q.sz + q.cx * q.cz * q.sy;
+  R[1][0] = q.cy * q.sz; R[1][1] = q.cx * q.cz + q.sx * q.sy * q.sz; R[1][2] = q.cx * q.sy * q.sz - q.cz * q.sx;
+  R[2][0] = -q.sy;       R[2][1] = q.cy * q.sx;                       R[2][2] = q.cx * q.cy;
+}
+// dR[e][i][j] = d R[i][j] / d theta_e  (GetDerivativeOfRotationMatrixWrtNodes, :241-268)
+TG_HD void euler_dR(const Trig& q, double dR[3][3][3]) {
+  const double sx = q.sx, cx = q.cx, sy = q.sy, cy = q.cy, sz = q.sz, cz = q.cz;
+  // wrt x (roll)
+  dR[0][0][0] = 0.0; dR[0][0][1] = sx * sz + cx * cz * sy; dR[0][0][2] = cx * sz - cz * sx * sy;
+  dR[0][1][0] = 0.0; dR[0][1][1] = cx * sy * sz - cz * sx; dR[0][1][2] = -cx * cz - sx * sy * sz;
+  dR[0][2][0] = 0.0; dR[0][2][1] = cx * cy;                dR[0][2][2] = -cy * sx;
+  // wrt y (pitch)
+  dR[1][0][0] = -cz * sy; dR[1][0][1] = cy * cz * sx; dR[1][0][2] = cx * cy * cz;
+  dR[1][1][0] = -sy * sz; dR[1][1][1] = cy * sx * sz; dR[1][1][2] = cx * cy * sz;
+  dR[1][2][0] = -cy;      dR[1][2][1] = -sx * sy;     dR[1][2][2] = -cx * sy;
+  // wrt z (yaw)
+  dR[2][0][0] = -cy * sz; dR[2][0][1] = -cx * cz - sx * sy * sz; dR[2][0][2] = cz * sx - cx * sy * sz;
+  dR[2][1][0] = cy * cz;  dR[2][1][1] = cz * sx * sy - cx * sz;  dR[2][1][2] = sx * sz + cx * cz * sy;
+  dR[2][2][0] = 0.0;      dR[2][2][1] = 0.0;                     dR[2][2][2] = 0.0;
+}
+
+// M (GetM :133-148), Mdot (GetMdot :150-166) as dense 3x3; dM[e] = dM/dtheta_e, dMd[e] = dMdot/dtheta_e
+struct EulerKin {
+  double M[3][3], Md[3][3], dM[3][3][3], dMd[3][3][3];
+  double w[3], wd[3];   // omega = M thd, omega_dot = Md thd + M thdd (:58-83)
+};
+TG_HD void euler_kin(const Trig& q, const double thd[3], const double thdd[3], EulerKin& k) {
+  const double sy = q.sy, cy = q.cy, sz = q.sz, cz = q.cz, yd = thd[1], zd = thd[2];
+  for (int a = 0; a < 3; ++a)
+    for (int b = 0; b < 3; ++b) {
+      k.M[a][b] = 0.0; k.Md[a][b] = 0.0;
+      for (int e = 0; e < 3; ++e) { k.dM[e][a][b] = 0.0; k.dMd[e][a][b] = 0.0; }
+    }
+  k.M[0][0] = cy * cz; k.M[0][1] = -sz;
+  k.M[1][0] = cy * sz; k.M[1][1] = cz;
+  k.M[2][0] = -sy;     k.M[2][2] = 1.0;
+  k.Md[0][0] = -cz * sy * yd - cy * sz * zd; k.Md[0][1] = -cz * zd;
+  k.Md[1][0] = cy * cz * zd - sy * sz * yd;  k.Md[1][1] = -sz * zd;
+  k.Md[2][0] = -cy * yd;
+  // dM / dy, dM / dz (GetDerivMwrtNodes :168-198)
+  k.dM[1][0][0] = -sy * cz; k.dM[1][1][0] = -sy * sz; k.dM[1][2][0] = -cy;
+  k.dM[2][0][0] = -cy * sz; k.dM[2][1][0] = cy * cz;  k.dM[2][0][1] = -cz; k.dM[2][1][1] = -sz;
+  // dMdot / dy, dMdot / dz (GetDerivMdotwrtNodes :270-304, position part)
+  k.dMd[1][0][0] = -cy * cz * yd + sy * sz * zd; k.dMd[1][1][0] = -cy * sz * yd - sy * cz * zd; k.dMd[1][2][0] = sy * yd;
+  k.dMd[2][0][0] = sy * sz * yd - cy * cz * zd;  k.dMd[2][1][0] = -sy * cz * yd - cy * sz * zd;
+  k.dMd[2][0][1] = sz * zd;                      k.dMd[2][1][1] = -cz * zd;
+  for (int a = 0; a < 3; ++a) {
+    k.w[a] = k.M[a][0] * thd[0] + k.M[a][1] * thd[1] + k.M[a][2] * thd[2];
+    k.wd[a] = (k.Md[a][0] * thd[0] + k.Md[a][1] * thd[1] + k.Md[a][2] * thd[2])
+            + (k.M[a][0] * thdd[0] + k.M[a][1] * thdd[1] + k.M[a][2] * thdd[2]);
+  }
+}
+
+TG_HD void cross3(const double a[3], const double b[3], double o[3]) {
+  o[0] = a[1] * b[2] - a[2] * b[1]; o[1] = a[2] * b[0] - a[0] * b[2]; o[2] = a[0] * b[1] - a[1] * b[0];
+}
+// Cross(in)[r][e]: in x v = Cross(in) v  (single_rigid_body_dynamics.cc:47-57)
+TG_HD double cross_el(const double in[3], int r, int e) {
+  const int d = (e - r + 3) % 3;     // 0 diag, 1 (r, r+1), 2 (r, r+2)
+  if (d == 0) return 0.0;
+  const int o = 3 - r - e;           // the remaining index
+  return d == 1 ? -in[o] : in[o];
+}
+TG_HD void mat3_vec(const double A[3][3], const double v[3], double o[3]) {
+  for (int i = 0; i < 3; ++i) o[i] = A[i][0] * v[0] + A[i][1] * v[1] + A[i][2] * v[2];
+}
+
+// ----------------------------------------------------------------------------------------------
+// terrain (towr/src/terrain/height_map.cc, height_map_examples.cc)
+// ----------------------------------------------------------------------------------------------
+TG_HD double ter_h(const towr_terrain_t& T, double x, double y) {
+  const double* p = T.p;
+  switch (T.id) {
+    case TOWR_TERRAIN_FLAT: return p[0];
+    case TOWR_TERRAIN_BLOCK: {
+      double bs = p[0], len = p[1], hh = p[2], eps = p[3], h = 0.0;
+      if (bs <= x && x <= bs + eps) h = hh / eps * (x - bs);
+      if (bs + eps <= x && x <= bs + len) h = hh;
+      return h;
+    }
+    case TOWR_TERRAIN_STAIRS: {
+      double h = 0.0;
+      if (x >= p[0]) h = p[2];
+      if (x >= p[0] + p[1]) h = p[3];
+      if (x >= p[0] + p[1] + p[4]) h = 0.0;
+      return h;
+    }
+    case TOWR_TERRAIN_GAP: {
+      double gs = p[0], w = p[1], hh = p[2], xc = gs + w / 2.0, ge = gs + w;
+      double a = (4 * hh) / (w * w), b = -(8 * hh * xc) / (w * w), cc = -(hh * (w - 2 * xc) * (w + 2 * xc)) / (w * w);
+      return (gs <= x && x <= ge) ? a * x * x + b * x + cc : 0.0;
+    }
+    case TOWR_TERRAIN_SLOPE: {
+      double ss = p[0], xd = ss + p[1], xf = xd + p[2], hc = p[3], sl = hc / p[1], z = 0.0;
+      if (x >= ss) z = sl * (x - ss);
+      if (x >= xd) z = hc - sl * (x - xd);
+      if (x >= xf) z = 0.0;
+      return z;
+    }
+    case TOWR_TERRAIN_CHIMNEY: return (p[0] <= x && x <= p[0] + p[1]) ? p[3] * (y - p[2]) : 0.0;
+    case TOWR_TERRAIN_CHIMNEY_LR: {
+      double z = 0.0, e1 = p[0] + p[1], e2 = p[0] + 2 * p[1];
+      if (p[0] <= x && x <= e1) z = p[3] * (y - p[2]);
+      if (e1 <= x && x <= e2) z = -p[3] * (y + p[2]);
+      return z;
+    }
+    case TOWR_TERRAIN_STEPS: {
+      if (x < p[0]) return 0.0;
+      int step = (int)((x - p[0]) / p[1]);
+      return step >= (int)p[3] ? p[3] * p[2] : (step + 1) * p[2];
+    }
+  }
+  return 0.0;
+}
+TG_HD double ter_dh(const towr_terrain_t& T, int dim, double x, double y) {
+  const double* p = T.p;
+  if (dim == X) {
+    switch (T.id) {
+      case TOWR_TERRAIN_BLOCK: return (p[0] <= x && x <= p[0] + p[3]) ? p[2] / p[3] : 0.0;
+      case TOWR_TERRAIN_GAP: {
+        double gs = p[0], w = p[1], hh = p[2], xc = gs + w / 2.0;
+        double a = (4 * hh) / (w * w), b = -(8 * hh * xc) / (w * w);
+        return (gs <= x && x <= gs + w) ? 2 * a * x + b : 0.0;
+      }
+      case TOWR_TERRAIN_SLOPE: {
+        double ss = p[0], xd = ss + p[1], xf = xd + p[2], sl = p[3] / p[1], d = 0.0;
+        if (x >= ss) d = sl;
+        if (x >= xd) d = -sl;
+        if (x >= xf) d = 0.0;
+        return d;
+      }
+    }
+    return 0.0;
+  }
+  switch (T.id) {
+    case TOWR_TERRAIN_CHIMNEY: return (p[0] <= x && x <= p[0] + p[1]) ? p[3] : 0.0;
+    case TOWR_TERRAIN_CHIMNEY_LR: {
+      double e1 = p[0] + p[1], e2 = p[0] + 2 * p[1], d = 0.0;
+      if (p[0] <= x && x <= e1) d = p[3];
+      if (e1 <= x && x <= e2) d = -p[3];
+      return d;
+    }
+  }
+  return 0.0;
+}
+// GetSecondDerivativeOfHeightWrt (:150-163): only Gap has a nonzero (XX) second derivative
+TG_HD double ter_d2h(const towr_terrain_t& T, int d1, int d2, double x, double y) {
+  if (T.id == TOWR_TERRAIN_GAP && d1 == X && d2 == X) {
+    double gs = T.p[0], w = T.p[1], hh = T.p[2];
+    return (gs <= x && x <= gs + w) ? 2 * ((4 * hh) / (w * w)) : 0.0;
+  }
+  return 0.0;
+}
+TG_HD bool ter_has_curvature(int id) { return id == TOWR_TERRAIN_GAP; }
+
+// GetBasis (:68-139); deriv < 0: the basis itself
+TG_HD void ter_basis(const towr_terrain_t& T, int basis, double x, double y, int deriv, double v[3]) {
+  const bool req = deriv < 0;
+  if (basis == 0) {
+    for (int d = 0; d < 2; ++d) v[d] = req ? -ter_dh(T, d, x, y) : -ter_d2h(T, d, deriv, x, y);
+    v[2] = req ? 1.0 : 0.0;
+  } else if (basis == 1) {
+    v[0] = req ? 1.0 : 0.0; v[1] = 0.0;
+    v[2] = req ? ter_dh(T, X, x, y) : ter_d2h(T, X, deriv, x, y);
+  } else {
+    v[0] = 0.0; v[1] = req ? 1.0 : 0.0;
+    v[2] = req ? ter_dh(T, Y, x, y) : ter_d2h(T, Y, deriv, x, y);
+  }
+}
+TG_HD void normalize3(const double v[3], double o[3]) {
+  const double z = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+  if (z > 0) { const double s = sqrt(z); o[0] = v[0] / s; o[1] = v[1] / s; o[2] = v[2] / s; }
+  else { o[0] = v[0]; o[1] = v[1]; o[2] = v[2]; }
+}
+// GetNormalizedBasis (:62-66)
+TG_HD void ter_nbasis(const towr_terrain_t& T, int basis, double x, double y, double o[3]) {
+  double v[3]; ter_basis(T, basis, x, y, -1, v); normalize3(v, o);
+}
+// GetDerivativeOfNormalizedBasisWrt (:80-91, 141-148)
+TG_HD void ter_d_nbasis(const towr_terrain_t& T, int basis, int dim, double x, double y, double o[3]) {
+  double dv[3], v[3], vn[3];
+  ter_basis(T, basis, x, y, dim, dv);
+  ter_basis(T, basis, x, y, -1, v);
+  const double sq = v[0] * v[0] + v[1] * v[1] + v[2] * v[2], nrm = sqrt(sq);
+  normalize3(v, vn);
+  for (int k = 0; k < 3; ++k) o[k] = (1 / sq * ((k == dim ? nrm : 0.0) - v[dim] * vn[k])) * dv[k];
+}
+// friction-pyramid directions b0..b4 = n, t1-mu n, t1+mu n, t2-mu n, t2+mu n
+TG_HD void pyramid(const double n[3], const double t1[3], const double t2[3], double mu, double b[5][3]) {
+  for (int q = 0; q < 3; ++q) {
+    b[0][q] = n[q];
+    b[1][q] = t1[q] - mu * n[q]; b[2][q] = t1[q] + mu * n[q];
+    b[3][q] = t2[q] - mu * n[q]; b[4][q] = t2[q] + mu * n[q];
+  }
+}
+TG_HD double dot3(const double a[3], const double b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+
+// ----------------------------------------------------------------------------------------------
+// work items
+// ----------------------------------------------------------------------------------------------
+
+// DynamicConstraint instant (dynamic_constraint.cc:63-148, single_rigid_body_dynamics.cc:76-204)
+template <class Emit>
+TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
+  const double t = it.t;
+  const int r0 = it.row0, E = c.rb.n_ee;
+  SplinePt L;
+  spline_eval(c, SP_BASE_LIN, t, L);
+  if (it.group == 0) {
+    // g (GetDynamicViolation :76-102) + d/d base-lin (GetJacobianWrtBaseLin :104-122)
+    SplinePt A; spline_eval(c, SP_BASE_ANG, t, A);
+    const Trig q = trig(A.p);
+    double R[3][3]; euler_R(q, R);
+    EulerKin k; euler_kin(q, A.v, A.a, k);
+    double fs[3] = {0, 0, 0}, ts[3] = {0, 0, 0};
+    for (int ee = 0; ee < E; ++ee) {
+      SplinePt F, Tq, P;
+      spline_eval(c, sp_force(ee), t, F);
+      spline_eval(c, sp_torque(ee), t, Tq);
+      spline_eval(c, sp_motion(ee), t, P);
+      double rr[3] = {L.p[0] - P.p[0], L.p[1] - P.p[1], L.p[2] - P.p[2]}, cr[3];
+      cross3(F.p, rr, cr);
+      for (int e = 0; e < 3; ++e) { ts[e] += cr[e] + Tq.p[e]; fs[e] += F.p[e]; }
+    }
+    // I_w = R I_b R^T
+    double RI[3][3], Iw[3][3];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) RI[i][j] = R[i][0] * c.rb.Ib[0 * 3 + j] + R[i][1] * c.rb.Ib[1 * 3 + j] + R[i][2] * c.rb.Ib[2 * 3 + j];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) Iw[i][j] = RI[i][0] * R[j][0] + RI[i][1] * R[j][1] + RI[i][2] * R[j][2];
+    double a[3], Iww[3], b[3];
+    mat3_vec(Iw, k.wd, a); mat3_vec(Iw, k.w, Iww); cross3(k.w, Iww, b);
+    for (int e = 0; e < 3; ++e) em.g(r0 + AX + e, a[e] + b[e] - ts[e]);
+    const double grav[3] = {0.0, 0.0, -c.rb.m * c.rb.g};
+    for (int e = 0; e < 3; ++e) em.g(r0 + LX + e, c.rb.m * L.a[e] - fs[e] - grav[e]);
+    double Hp[4], Ha[4];
+    hermite_dpos(L.T, L.tl, Hp); hermite_dacc(L.T, L.tl, Ha);
+    for (int r = 0; r < 3; ++r)
+      for (int d = 1; d <= 2; ++d) {
+        const int e = (r + d) % 3;
+        const double s = -cross_el(fs, r, e);  // -(sum_ee Cross(f_ee))[r][e]
+        for (int bb = 0; bb < 4; ++bb) em(r0 + AX + r, basis_col(c, SP_BASE_LIN, L.poly, bb, e), s * Hp[bb], true);
+      }
+    for (int e = 0; e < 3; ++e)
+      for (int bb = 0; bb < 4; ++bb) em(r0 + LX + e, basis_col(c, SP_BASE_LIN, L.poly, bb, e), c.rb.m * Ha[bb], true);
+    return;
+  }
+  if (it.group == 1) {
+    // d/d base-ang (GetJacobianWrtBaseAng :124-166), chain rule through theta, theta_dot, theta_ddot
+    SplinePt A; spline_eval(c, SP_BASE_ANG, t, A);
+    const Trig q = trig(A.p);
+    double R[3][3], dR[3][3][3];
+    euler_R(q, R); euler_dR(q, dR);
+    EulerKin k; euler_kin(q, A.v, A.a, k);
+    double RI[3][3], Iw[3][3];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) RI[i][j] = R[i][0] * c.rb.Ib[0 * 3 + j] + R[i][1] * c.rb.Ib[1 * 3 + j] + R[i][2] * c.rb.Ib[2 * 3 + j];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) Iw[i][j] = RI[i][0] * R[j][0] + RI[i][1] * R[j][1] + RI[i][2] * R[j][2];
+    double Iww[3]; mat3_vec(Iw, k.w, Iww);
+    double Ap[3][3], Av[3][3], Aa[3][3];   // [row][e]
+    for (int e = 0; e < 3; ++e) {
+      // dI_w/dtheta_e = dR_e I_b R^T + R I_b dR_e^T
+      double dRI[3][3], dIw[3][3];
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) dRI[i][j] = dR[e][i][0] * c.rb.Ib[0 * 3 + j] + dR[e][i][1] * c.rb.Ib[1 * 3 + j] + dR[e][i][2] * c.rb.Ib[2 * 3 + j];
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+          dIw[i][j] = (dRI[i][0] * R[j][0] + dRI[i][1] * R[j][1] + dRI[i][2] * R[j][2])
+                    + (RI[i][0] * dR[e][j][0] + RI[i][1] * dR[e][j][1] + RI[i][2] * dR[e][j][2]);
+      double dw[3], dwd[3], t1[3], t2[3], t3[3], t4[3], t5[3], t6[3];
+      mat3_vec(k.dM[e], A.v, dw);
+      mat3_vec(k.dMd[e], A.v, t1); mat3_vec(k.dM[e], A.a, t2);
+      for (int i = 0; i < 3; ++i) dwd[i] = t1[i] + t2[i];
+      mat3_vec(dIw, k.wd, t1);              // dI_w wd
+      mat3_vec(Iw, dwd, t2);                // I_w dwd
+      cross3(dw, Iww, t3);                  // dw x (I_w w)
+      mat3_vec(dIw, k.w, t4); mat3_vec(Iw, dw, t5);
+      for (int i = 0; i < 3; ++i) t4[i] += t5[i];
+      cross3(k.w, t4, t6);                  // w x (dI_w w + I_w dw)
+      for (int i = 0; i < 3; ++i) Ap[i][e] = t1[i] + t2[i] + t3[i] + t6[i];
+      // theta_dot_e: dw = M[:,e], dwd = dM_e thd + Md[:,e]
+      double Me[3] = {k.M[0][e], k.M[1][e], k.M[2][e]}, dwv[3];
+      mat3_vec(k.dM[e], A.v, dwv);
+      for (int i = 0; i < 3; ++i) dwv[i] += k.Md[i][e];
+      mat3_vec(Iw, dwv, t1); cross3(Me, Iww, t3); mat3_vec(Iw, Me, t5); cross3(k.w, t5, t6);
+      for (int i = 0; i < 3; ++i) Av[i][e] = t1[i] + t3[i] + t6[i];
+      // theta_ddot_e: dwd = M[:,e]
+      for (int i = 0; i < 3; ++i) Aa[i][e] = t5[i];
+    }
+    double Hp[4], Hv[4], Ha[4];
+    hermite_dpos(A.T, A.tl, Hp); hermite_dvel(A.T, A.tl, Hv); hermite_dacc(A.T, A.tl, Ha);
+    for (int r = 0; r < 3; ++r)
+      for (int e = 0; e < 3; ++e)
+        for (int bb = 0; bb < 4; ++bb)
+          em(r0 + AX + r, basis_col(c, SP_BASE_ANG, A.poly, bb, e), Ap[r][e] * Hp[bb] + Av[r][e] * Hv[bb] + Aa[r][e] * Ha[bb], true);
+    return;
+  }
+  // group 2 + ee: force (GetJacobianWrtForce :168-180), torque (:182-191), motion (:193-204)
+  const int ee = it.group - 2;
+  SplinePt F, Tq, P;
+  spline_eval(c, sp_force(ee), t, F);
+  spline_eval(c, sp_torque(ee), t, Tq);
+  spline_eval(c, sp_motion(ee), t, P);
+  const double rv[3] = {L.p[0] - P.p[0], L.p[1] - P.p[1], L.p[2] - P.p[2]};
+  double H[4];
+  hermite_dpos(F.T, F.tl, H);
+  for (int r = 0; r < 3; ++r)
+    for (int d = 1; d <= 2; ++d) {
+      const int e = (r + d) % 3;
+      const double s = cross_el(rv, r, e);
+      for (int bb = 0; bb < 4; ++bb) {
+        const int col = basis_col(c, sp_force(ee), F.poly, bb, e);
+        em(r0 + AX + r, col, s * H[bb], col >= 0);
+      }
+    }
+  for (int e = 0; e < 3; ++e)
+    for (int bb = 0; bb < 4; ++bb) {
+      const int col = basis_col(c, sp_force(ee), F.poly, bb, e);
+      em(r0 + LX + e, col, -H[bb], col >= 0);
+    }
+  hermite_dpos(Tq.T, Tq.tl, H);
+  for (int e = 0; e < 3; ++e)
+    for (int bb = 0; bb < 4; ++bb) {
+      const int col = basis_col(c, sp_torque(ee), Tq.poly, bb, e);
+      em(r0 + AX + e, col, -H[bb], col >= 0);
+    }
+  hermite_dpos(P.T, P.tl, H);
+  for (int r = 0; r < 3; ++r)
+    for (int d = 1; d <= 2; ++d) {
+      const int e = (r + d) % 3;
+      const double s = cross_el(F.p, r, e);
+      for (int bb = 0; bb < 4; ++bb) {
+        const int col = basis_col(c, sp_motion(ee), P.poly, bb, e);
+        em(r0 + AX + r, col, s * H[bb], col >= 0);
+      }
+    }
+}
+
+// RangeOfMotionConstraint instant (range_of_motion_constraint.cc:72-131)
+template <class Emit>
+TG_HD void eval_rom(const Ctx& c, const ItemDesc& it, Emit& em) {
+  const double t = it.t;
+  const int r0 = it.row0, ee = it.ee;
+  SplinePt L, A, P;
+  spline_eval(c, SP_BASE_LIN, t, L);
+  spline_eval(c, SP_BASE_ANG, t, A);
+  spline_eval(c, sp_motion(ee), t, P);
+  const Trig q = trig(A.p);
+  double R[3][3]; euler_R(q, R);
+  const double rW[3] = {P.p[0] - L.p[0], P.p[1] - L.p[1], P.p[2] - L.p[2]};
+  double H[4];
+  if (it.group == 0) {
+    for (int i = 0; i < 3; ++i) em.g(r0 + i, R[0][i] * rW[0] + R[1][i] * rW[1] + R[2][i] * rW[2]);
+    hermite_dpos(L.T, L.tl, H);
+    for (int r = 0; r < 3; ++r)
+      for (int e = 0; e < 3; ++e)
+        for (int bb = 0; bb < 4; ++bb) em(r0 + r, basis_col(c, SP_BASE_LIN, L.poly, bb, e), -R[e][r] * H[bb], true);
+  } else if (it.group == 1) {
+    // DerivOfRotVecMult(t, r_W, inverse=true): row r = sum_c rW[c] dR[c][r]; row X has no roll terms
+    double dR[3][3][3]; euler_dR(q, dR);
+    hermite_dpos(A.T, A.tl, H);
+    for (int r = 0; r < 3; ++r)
+      for (int e = (r == 0 ? 1 : 0); e < 3; ++e) {
+        const double s = rW[0] * dR[e][0][r] + rW[1] * dR[e][1][r] + rW[2] * dR[e][2][r];
+        for (int bb = 0; bb < 4; ++bb) em(r0 + r, basis_col(c, SP_BASE_ANG, A.poly, bb, e), s * H[bb], true);
+      }
+  } else {
+    hermite_dpos(P.T, P.tl, H);
+    for (int r = 0; r < 3; ++r)
+      for (int e = 0; e < 3; ++e)
+        for (int bb = 0; bb < 4; ++bb) {
+          const int col = basis_col(c, sp_motion(ee), P.poly, bb, e);
+          em(r0 + r, col, R[e][r] * H[bb], col >= 0);
+        }
+  }
+}
+
+// ForceConstraintDiscretized instant (force_constraint_discretized.cc:97-221)
+template <class Emit>
+TG_HD void eval_fdisc(const Ctx& c, const ItemDesc& it, Emit& em) {
+  const double t = it.t, mu = c.ter->friction_coeff;
+  const int r0 = it.row0, ee = it.ee;
+  SplinePt P, F;
+  spline_eval(c, sp_motion(ee), t, P);
+  spline_eval(c, sp_force(ee), t, F);
+  double n[3], t1[3], t2[3], b[5][3];
+  ter_nbasis(*c.ter, 0, P.p[0], P.p[1], n);
+  ter_nbasis(*c.ter, 1, P.p[0], P.p[1], t1);
+  ter_nbasis(*c.ter, 2, P.p[0], P.p[1], t2);
+  pyramid(n, t1, t2, mu, b);
+  for (int i = 0; i < 5; ++i) em.g(r0 + i, dot3(F.p, b[i]));
+  double H[4];
+  hermite_dpos(F.T, F.tl, H);
+  for (int i = 0; i < 5; ++i)
+    for (int e = 0; e < 3; ++e)
+      for (int bb = 0; bb < 4; ++bb) {
+        const int col = basis_col(c, sp_force(ee), F.poly, bb, e);
+        em(r0 + i, col, b[i][e] * H[bb], col >= 0);
+      }
+  if (c.fdisc_motion) {   // AccumulateScaledRowJacobian: skipped when scale == 0.0 (:58)
+    hermite_dpos(P.T, P.tl, H);
+    for (int dim = 0; dim < 2; ++dim) {
+      double dn[3], dt1[3], dt2[3], db[5][3];
+      ter_d_nbasis(*c.ter, 0, dim, P.p[0], P.p[1], dn);
+      ter_d_nbasis(*c.ter, 1, dim, P.p[0], P.p[1], dt1);
+      ter_d_nbasis(*c.ter, 2, dim, P.p[0], P.p[1], dt2);
+      pyramid(dn, dt1, dt2, mu, db);
+      for (int i = 0; i < 5; ++i) {
+        const double s = dot3(F.p, db[i]);
+        for (int bb = 0; bb < 4; ++bb) {
+          const int col = basis_col(c, sp_motion(ee), P.poly, bb, dim);
+          em(r0 + i, col, s * H[bb], col >= 0 && s != 0.0);
+        }
+      }
+    }
+  }
+}
+
+// ForceConstraint node (force_constraint.cc:62-171); a0 = force node, a1 = motion node at phase start
+template <class Emit>
+TG_HD void eval_fnode(const Ctx& c, const ItemDesc& it, Emit& em) {
+  const double mu = c.ter->friction_coeff;
+  const int r0 = it.row0, ee = it.ee, fs = sp_force(ee), ms = sp_motion(ee);
+  double p[3], f[3];
+  for (int e = 0; e < 3; ++e) { p[e] = xval(c, node_col(c, ms, it.a1, kPos, e)); f[e] = xval(c, node_col(c, fs, it.a0, kPos, e)); }
+  double n[3], t1[3], t2[3], b[5][3];
+  ter_nbasis(*c.ter, 0, p[0], p[1], n);
+  ter_nbasis(*c.ter, 1, p[0], p[1], t1);
+  ter_nbasis(*c.ter, 2, p[0], p[1], t2);
+  pyramid(n, t1, t2, mu, b);
+  for (int i = 0; i < 5; ++i) em.g(r0 + i, dot3(f, b[i]));
+  for (int e = 0; e < 3; ++e) {
+    const int col = node_col(c, fs, it.a0, kPos, e);
+    for (int i = 0; i < 5; ++i) em(r0 + i, col, b[i][e], true);
+  }
+  for (int dim = 0; dim < 2; ++dim) {
+    double dn[3], dt1[3], dt2[3], db[5][3];
+    ter_d_nbasis(*c.ter, 0, dim, p[0], p[1], dn);
+    ter_d_nbasis(*c.ter, 1, dim, p[0], p[1], dt1);
+    ter_d_nbasis(*c.ter, 2, dim, p[0], p[1], dt2);
+    pyramid(dn, dt1, dt2, mu, db);
+    const int col = node_col(c, ms, it.a1, kPos, dim);
+    for (int i = 0; i < 5; ++i) em(r0 + i, col, dot3(f, db[i]), true);
+  }
+}
+
+// TerrainConstraint node (terrain_constraint.cc:61-111); BaseHeightConstraint node (:58-110)
+template <class Emit>
+TG_HD void eval_height(const Ctx& c, const ItemDesc& it, int s, double offset, Emit& em) {
+  double p[3];
+  for (int e = 0; e < 3; ++e) p[e] = xval(c, node_col(c, s, it.a0, kPos, e));
+  em.g(it.row0, p[2] - ter_h(*c.ter, p[0], p[1]) - offset);
+  em(it.row0, node_col(c, s, it.a0, kPos, Z), 1.0, true);
+  for (int dim = 0; dim < 2; ++dim)
+    em(it.row0, node_col(c, s, it.a0, kPos, dim), -ter_dh(*c.ter, dim, p[0], p[1]), true);
+}
+
+// BaseMotionConstraint instant (base_motion_constraint.cc:60-85)
+template <class Emit>
+TG_HD void eval_bmot(const Ctx& c, const ItemDesc& it, Emit& em) {
+  SplinePt L, A;
+  spline_eval(c, SP_BASE_LIN, it.t, L);
+  spline_eval(c, SP_BASE_ANG, it.t, A);
+  for (int e = 0; e < 3; ++e) { em.g(it.row0 + LX + e, L.p[e]); em.g(it.row0 + AX + e, A.p[e]); }
+  double H[4];
+  hermite_dpos(A.T, A.tl, H);
+  for (int e = 0; e < 3; ++e)
+    for (int bb = 0; bb < 4; ++bb) em(it.row0 + AX + e, basis_col(c, SP_BASE_ANG, A.poly, bb, e), H[bb], true);
+  hermite_dpos(L.T, L.tl, H);
+  for (int e = 0; e < 3; ++e)
+    for (int bb = 0; bb < 4; ++bb) em(it.row0 + LX + e, basis_col(c, SP_BASE_LIN, L.poly, bb, e), H[bb], true);
+}
+
+// SplineAccConstraint junction j = it.k (spline_acc_constraint.cc:48-80); it.ee = spline id
+template <class Emit>
+TG_HD void eval_sacc(const Ctx& c, const ItemDesc& it, Emit& em) {
+  const int s = it.ee, j = it.k;
+  const SplineMeta m = c.spl[s];
+  const double Tp = c.dur[m.dur_off + j], Tn = c.dur[m.dur_off + j + 1];
+  SplinePt a, b;
+  poly_state(c, s, j, Tp, Tp, a);
+  poly_state(c, s, j + 1, Tn, 0.0, b);
+  for (int e = 0; e < 3; ++e) em.g(it.row0 + e, a.a[e] - b.a[e]);
+  double Hp[4], Hn[4];
+  hermite_dacc(Tp, Tp, Hp); hermite_dacc(Tn, 0.0, Hn);
+  for (int e = 0; e < 3; ++e) {
+    for (int bb = 0; bb < 4; ++bb) em(it.row0 + e, basis_col(c, s, j, bb, e), Hp[bb], true);
+    for (int bb = 0; bb < 4; ++bb) em(it.row0 + e, basis_col(c, s, j + 1, bb, e), -Hn[bb], true);
+  }
+}
+
+// SwingConstraint node (swing_constraint.cc:54-108); it.p0 = t_swing_avg
+template <class Emit>
+TG_HD void eval_swing(const Ctx& c, const ItemDesc& it, Emit& em) {
+  const int s = sp_motion(it.ee), id = it.a0;
+  const double tsw = it.p0;
+  int row = it.row0;
+  for (int dim = 0; dim < 2; ++dim) {
+    const double prev = xval(c, node_col(c, s, id - 1, kPos, dim)), next = xval(c, node_col(c, s, id + 1, kPos, dim));
+    const double dist = next - prev, center = prev + 0.5 * dist, vdes = dist / tsw;
+    em.g(row, xval(c, node_col(c, s, id, kPos, dim)) - center);
+    em(row, node_col(c, s, id, kPos, dim), 1.0, true);
+    em(row, node_col(c, s, id + 1, kPos, dim), -0.5, true);
+    em(row, node_col(c, s, id - 1, kPos, dim), -0.5, true);
+    ++row;
+    em.g(row, xval(c, node_col(c, s, id, kVel, dim)) - vdes);
+    em(row, node_col(c, s, id, kVel, dim), 1.0, true);
+    em(row, node_col(c, s, id + 1, kPos, dim), -1.0 / tsw, true);
+    em(row, node_col(c, s, id - 1, kPos, dim), +1.0 / tsw, true);
+    ++row;
+  }
+}
+
+template <class Emit>
+TG_HD void eval_item(const Ctx& c, const ItemDesc& it, Emit& em) {
+  switch (it.type) {
+    case IT_DYN: eval_dyn(c, it, em); break;
+    case IT_ROM: eval_rom(c, it, em); break;
+    case IT_FDISC: eval_fdisc(c, it, em); break;
+    case IT_FNODE: eval_fnode(c, it, em); break;
+    case IT_TERR: eval_height(c, it, sp_motion(it.ee), 0.0, em); break;
+    case IT_BMOT: eval_bmot(c, it, em); break;
+    case IT_SACC: eval_sacc(c, it, em); break;
+    case IT_BHGT: eval_height(c, it, SP_BASE_LIN, it.p0, em); break;
+    case IT_SWING: eval_swing(c, it, em); break;
+  }
+}
+
+}  // namespace tg

@@ -1,0 +1,523 @@
+// layout.hip — host-side problem builder (see layout.h). Compiled by hipcc as host code; it
+// instantiates engine_math.h's item evaluators with a recording emitter to obtain the exact
+// candidate (row, col) list of every work item (the structure pass) — no g/J values leave here.
+#include "layout.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+
+namespace tg {
+namespace {
+
+struct Nvi { int id, deriv, dim; };
+struct PolyInfo { int phase, poly_in_phase, n_polys_in_phase, is_constant; };
+
+// NodesVariables state needed at setup: index maps and (initial) node values.
+struct NodeSet {
+  int kind = 0, ee = 0, n_nodes = 0, n_rows = 0, col0 = -1;
+  bool all = false;
+  std::vector<PolyInfo> pinfo;
+  std::vector<std::vector<Nvi>> map;   // opt index -> node values
+  std::vector<double> val;             // [node][deriv][dim]
+
+  std::vector<Nvi> info(int idx) const {   // GetNodeValuesInfo
+    if (all) { int in = idx % 6; return {Nvi{idx / 6, in < 3 ? kPos : kVel, in % 3}}; }
+    return map[idx];
+  }
+  double& v(int node, int deriv, int dim) { return val[(node * 2 + deriv) * 3 + dim]; }
+  bool is_constant_node(int node) const {   // nodes_variables_phase_based.cc:101-113
+    int last = n_nodes - 1;
+    if (node == 0) return pinfo[0].is_constant;
+    if (node == last) return pinfo[last - 1].is_constant;
+    return pinfo[node - 1].is_constant || pinfo[node].is_constant;
+  }
+  int phase_of(int node) const {            // GetPhase :133-140
+    int poly = node == 0 ? 0 : (node == n_nodes - 1 ? n_nodes - 2 : node - 1);
+    return pinfo[poly].phase;
+  }
+  int node_at_start_of_phase(int phase) const {   // :142-165
+    for (int i = 0; i < (int)pinfo.size(); ++i) if (pinfo[i].phase == phase) return i;
+    return -1;
+  }
+};
+
+NodeSet make_all(int kind, int n_nodes) {           // nodes_variables_all.cc:34-43
+  NodeSet s; s.kind = kind; s.all = true; s.n_nodes = n_nodes; s.n_rows = n_nodes * 6;
+  s.val.assign((size_t)n_nodes * 6, 0.0);
+  return s;
+}
+
+// nodes_variables_phase_based.cc:39-73 + GetPhaseBasedEEParameterization (:201-396)
+NodeSet make_phase_based(int kind, int ee, int phase_count, bool contact_at_start, int n_changing) {
+  NodeSet s; s.kind = kind; s.ee = ee;
+  bool first_constant = (kind == TOWR_VAR_EE_MOTION || kind == TOWR_VAR_EE_ANG) ? contact_at_start : !contact_at_start;
+  bool c = first_constant;
+  for (int i = 0; i < phase_count; ++i) {
+    if (c) s.pinfo.push_back({i, 0, 1, 1});
+    else for (int j = 0; j < n_changing; ++j) s.pinfo.push_back({i, j, n_changing, 0});
+    c = !c;
+  }
+  s.n_nodes = (int)s.pinfo.size() + 1;
+  s.val.assign((size_t)s.n_nodes * 6, 0.0);
+  int idx = 0;
+  auto push = [&](int i, int id, int deriv, int dim) {
+    if ((int)s.map.size() <= i) s.map.resize(i + 1);
+    s.map[i].push_back(Nvi{id, deriv, dim});
+  };
+  for (int id = 0; id < s.n_nodes; ++id) {
+    if (!s.is_constant_node(id)) {
+      for (int dim = 0; dim < 3; ++dim) {
+        push(idx++, id, kPos, dim);
+        if (kind == TOWR_VAR_EE_MOTION && dim == Z) continue;   // swing z-velocity fixed to 0
+        push(idx++, id, kVel, dim);
+      }
+    } else {
+      if (kind == TOWR_VAR_EE_MOTION || kind == TOWR_VAR_EE_ANG) {
+        for (int dim = 0; dim < 3; ++dim) { push(idx, id, kPos, dim); push(idx, id + 1, kPos, dim); ++idx; }
+      }
+      id += 1;   // the next (constant) node is handled with this one
+    }
+  }
+  s.n_rows = idx;
+  return s;
+}
+
+void set_linear(NodeSet& s, const double ini[3], const double fin[3], double T) {   // nodes_variables.cc:131-154
+  double dp[3], avg[3];
+  for (int k = 0; k < 3; ++k) { dp[k] = fin[k] - ini[k]; avg[k] = dp[k] / T; }
+  for (int idx = 0; idx < s.n_rows; ++idx)
+    for (const Nvi& q : s.info(idx)) {
+      if (q.deriv == kPos) s.v(q.id, kPos, q.dim) = ini[q.dim] + q.id / (double)(s.n_nodes - 1) * dp[q.dim];
+      if (q.deriv == kVel) s.v(q.id, kVel, q.dim) = avg[q.dim];
+    }
+}
+
+void rot(const double rpy[3], double R[3][3]) { euler_R(trig(rpy), R); }
+
+std::vector<double> get_values(const NodeSet& s) {   // nodes_variables.cc:56-66
+  std::vector<double> x((size_t)s.n_rows);
+  NodeSet& m = const_cast<NodeSet&>(s);
+  for (int idx = 0; idx < s.n_rows; ++idx)
+    for (const Nvi& q : s.info(idx)) x[idx] = m.v(q.id, q.deriv, q.dim);
+  return x;
+}
+void set_values(NodeSet& s, const std::vector<double>& x) {
+  for (int idx = 0; idx < s.n_rows; ++idx)
+    for (const Nvi& q : s.info(idx)) s.v(q.id, q.deriv, q.dim) = x[idx];
+}
+
+// nodes_variables.cc:157-217
+void set_linear_rel_base(NodeSet& s, const double ee0[3], const double ee1[3], const double b0[3], const double b1[3],
+                         const double rpy0[3], const double rpy1[3], double T) {
+  const int N = s.n_nodes;
+  if (N < 2) return;
+  double R0[3][3], RT[3][3], r0B[3], rTB[3], dpB[3], avgB[3], bavg[3], d0[3], dT[3];
+  rot(rpy0, R0); rot(rpy1, RT);
+  for (int k = 0; k < 3; ++k) { d0[k] = ee0[k] - b0[k]; dT[k] = ee1[k] - b1[k]; }
+  for (int i = 0; i < 3; ++i) {
+    r0B[i] = R0[0][i] * d0[0] + R0[1][i] * d0[1] + R0[2][i] * d0[2];
+    rTB[i] = RT[0][i] * dT[0] + RT[1][i] * dT[1] + RT[2][i] * dT[2];
+  }
+  for (int k = 0; k < 3; ++k) { dpB[k] = rTB[k] - r0B[k]; avgB[k] = dpB[k] / T; bavg[k] = (b1[k] - b0[k]) / T; }
+  for (int idx = 0; idx < s.n_rows; ++idx)
+    for (const Nvi& q : s.info(idx)) {
+      double a = q.id / (double)(N - 1), bp[3], rpy[3], R[3][3], rB[3];
+      for (int k = 0; k < 3; ++k) {
+        bp[k] = (1.0 - a) * b0[k] + a * b1[k];
+        rpy[k] = (1.0 - a) * rpy0[k] + a * rpy1[k];
+        rB[k] = r0B[k] + a * dpB[k];
+      }
+      rot(rpy, R);
+      const int d = q.dim;
+      if (q.deriv == kPos) s.v(q.id, kPos, d) = bp[d] + (R[d][0] * rB[0] + R[d][1] * rB[1] + R[d][2] * rB[2]);
+      if (q.deriv == kVel) s.v(q.id, kVel, d) = bavg[d] + (R[d][0] * avgB[0] + R[d][1] * avgB[1] + R[d][2] * avgB[2]);
+    }
+  set_values(s, get_values(s));   // SetVariables(GetValues())
+}
+
+// recording emitter of the structure pass
+struct RecordEmit {
+  std::vector<int32_t>* rows;
+  std::vector<int32_t>* cols;
+  std::vector<uint8_t>* present;
+  int g_rows_lo = 0, g_rows_hi = 0;
+  bool bad_g = false;
+  void g(int row, double) { if (row < g_rows_lo || row >= g_rows_hi) bad_g = true; }
+  void operator()(int row, int col, double, bool pres) {
+    rows->push_back(row); cols->push_back(col); present->push_back(pres && col >= 0 ? 1 : 0);
+  }
+};
+
+
+// NodesVariables of every spline, in spline order: base-lin, base-ang, per ee {motion, ang, force, torque}
+int make_sets(const towr_problem_desc_t& d, std::vector<double>& base_d, std::vector<NodeSet>& sets, std::string& err) {
+  const int E = d.robot.n_ee;
+  const double T = d.total_time;
+  // ---- base polynomial durations (parameters.cc:114-130)
+  { double dt = d.duration_base_polynomial, tl = T;
+    while (tl > 1e-10) { base_d.push_back(tl > dt ? dt : tl); tl -= dt; } }
+
+  // ---- node sets
+  sets.push_back(make_all(TOWR_VAR_BASE_LIN, (int)base_d.size() + 1));
+  sets.push_back(make_all(TOWR_VAR_BASE_ANG, (int)base_d.size() + 1));
+  for (int ee = 0; ee < E; ++ee) {
+    const int np = d.n_phases[ee];
+    if (np < 1 || np > TOWR_MAX_PHASES) { err = "n_phases out of range"; return TOWR_ERR_INVALID; }
+    const bool cs = d.contact_at_start[ee] != 0;
+    sets.push_back(make_phase_based(TOWR_VAR_EE_MOTION, ee, np, cs, d.ee_polynomials_per_swing_phase));
+    sets.push_back(make_phase_based(TOWR_VAR_EE_ANG, ee, np, cs, d.ee_polynomials_per_swing_phase));
+    sets.push_back(make_phase_based(TOWR_VAR_EE_FORCE, ee, np, cs, d.force_polynomials_per_stance_phase));
+    sets.push_back(make_phase_based(TOWR_VAR_EE_TORQUE, ee, np, cs, d.torque_polynomials_per_stance_phase));
+  }
+  return TOWR_OK;
+}
+
+// initial node values (nlp_formulation.cc:121-346, or procedural_example.cc:134-166)
+int init_values(const towr_problem_desc_t& d, const towr_init_t& in, const towr_terrain_t& ter, std::vector<NodeSet>& sets, std::string& err) {
+  const int E = d.robot.n_ee;
+  const double T = d.total_time;
+  const towr_robot_t& rb = d.robot;
+  const double z3[3] = {0, 0, 0};
+  if (in.mode == TOWR_INIT_FORMULATION) {
+    double fp[3] = {in.base_lin_p1[0], in.base_lin_p1[1], 0.0};
+    fp[2] = ter_h(ter, fp[0], fp[1]) - rb.nominal_stance[0][2];
+    set_linear(sets[0], in.base_lin_p0, fp, T);
+    set_linear(sets[1], in.base_ang_p0, in.base_ang_p1, T);
+    for (int ee = 0; ee < E; ++ee) {
+      double yaw[3] = {0.0, 0.0, in.base_ang_p1[2]}, R[3][3], fe[3];
+      rot(yaw, R);
+      for (int q = 0; q < 3; ++q)
+        fe[q] = in.base_lin_p1[q] + (R[q][0] * rb.nominal_stance[ee][0] + R[q][1] * rb.nominal_stance[ee][1] + R[q][2] * rb.nominal_stance[ee][2]);
+      double tgt[3] = {fe[0], fe[1], ter_h(ter, fe[0], fe[1])};
+      set_linear_rel_base(sets[2 + 4 * ee], in.ee_p0[ee], tgt, in.base_lin_p0, in.base_lin_p1, in.base_ang_p0, in.base_ang_p1, T);
+      set_linear(sets[3 + 4 * ee], in.base_ang_p0, in.base_ang_p1, T);
+      double fs[3] = {0.0, 0.0, rb.mass * rb.gravity / E};
+      set_linear(sets[4 + 4 * ee], fs, fs, T);
+      set_linear(sets[5 + 4 * ee], z3, z3, T);
+    }
+  } else if (in.mode == TOWR_INIT_PROCEDURAL) {
+    set_linear(sets[0], in.base_lin_p0, in.base_lin_p1, T);
+    set_linear(sets[1], in.base_ang_p0, in.base_ang_p1, T);
+    for (int ee = 0; ee < E; ++ee) {
+      set_linear(sets[2 + 4 * ee], in.ee_p0[ee], in.ee_p1[ee], T);
+      set_linear(sets[3 + 4 * ee], in.base_ang_p0, in.base_ang_p1, T);
+      double fs[3] = {0.0, 0.0, rb.mass * rb.gravity / E};
+      set_linear(sets[4 + 4 * ee], fs, fs, T);
+      set_linear(sets[5 + 4 * ee], z3, z3, T);
+    }
+  } else { err = "unknown init mode"; return TOWR_ERR_INVALID; }
+  return TOWR_OK;
+}
+
+int item_rows(int type) {
+  switch (type) {
+    case IT_DYN: case IT_BMOT: return 6;
+    case IT_ROM: case IT_SACC: return 3;
+    case IT_FDISC: case IT_FNODE: return 5;
+    case IT_TERR: case IT_BHGT: return 1;
+    case IT_SWING: return 4;
+  }
+  return 0;
+}
+
+}  // namespace
+
+int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
+  if (d.abi_version != TOWR_GPU_ABI_VERSION) { err = "abi version mismatch"; return TOWR_ERR_INVALID; }
+  if (d.angular_rep != 0) { err = "only EulerZYX angular representation is supported (RotVec is next-tier)"; return TOWR_ERR_UNSUPPORTED; }
+  const int E = d.robot.n_ee;
+  if (E < 1 || E > TOWR_MAX_EE) { err = "robot.n_ee out of range"; return TOWR_ERR_INVALID; }
+  if (d.optimize_timings) { err = "phase-duration optimisation (gait optimisation) is not supported yet"; return TOWR_ERR_UNSUPPORTED; }
+  if (!(d.total_time > 0) || !(d.duration_base_polynomial > 0)) { err = "bad total_time / duration_base_polynomial"; return TOWR_ERR_INVALID; }
+  const double T = d.total_time;
+
+  std::vector<double> base_d;
+  std::vector<NodeSet> sets;
+  if (int rc = make_sets(d, base_d, sets, err)) return rc;
+  auto set_index = [&](int kind, int ee) -> int {
+    if (kind == TOWR_VAR_BASE_LIN) return 0;
+    if (kind == TOWR_VAR_BASE_ANG) return 1;
+    if (ee < 0 || ee >= E) return -1;
+    switch (kind) {
+      case TOWR_VAR_EE_MOTION: return 2 + 4 * ee;
+      case TOWR_VAR_EE_ANG: return 3 + 4 * ee;
+      case TOWR_VAR_EE_FORCE: return 4 + 4 * ee;
+      case TOWR_VAR_EE_TORQUE: return 5 + 4 * ee;
+    }
+    return -1;
+  };
+
+  // ---- variable sets in AddVariableSet order
+  int col = 0;
+  L.varsets.clear();
+  for (int i = 0; i < d.n_varsets; ++i) {
+    const int si = set_index(d.varsets[i].kind, d.varsets[i].ee);
+    if (si < 0) { err = "unsupported or malformed variable set " + std::to_string(i); return si == -1 ? TOWR_ERR_INVALID : TOWR_ERR_UNSUPPORTED; }
+    if (sets[si].col0 >= 0) { err = "variable set listed twice"; return TOWR_ERR_INVALID; }
+    sets[si].col0 = col;
+    L.varsets.push_back({d.varsets[i].kind, d.varsets[i].ee, col, sets[si].n_rows});
+    col += sets[si].n_rows;
+  }
+  for (auto& s : sets)
+    if (s.col0 < 0) { err = "every node variable set (base-lin, base-ang, ee motion/ang/force/torque) must be in the problem"; return TOWR_ERR_INVALID; }
+  L.n = col;
+
+  // ---- node -> column table, spline metadata, polynomial durations
+  L.spl.clear(); L.nodecol.clear(); L.dur.clear();
+  for (size_t si = 0; si < sets.size(); ++si) {
+    NodeSet& s = sets[si];
+    SplineMeta m{};
+    m.node_off = (int32_t)(L.nodecol.size() / 6);
+    m.n_polys = s.n_nodes - 1;
+    m.dur_off = (int32_t)L.dur.size();
+    std::vector<int32_t> nc((size_t)s.n_nodes * 6, -1);
+    for (int idx = 0; idx < s.n_rows; ++idx)
+      for (const Nvi& q : s.info(idx)) nc[(q.id * 2 + q.deriv) * 3 + q.dim] = s.col0 + idx;
+    L.nodecol.insert(L.nodecol.end(), nc.begin(), nc.end());
+    if (si < 2) L.dur.insert(L.dur.end(), base_d.begin(), base_d.end());
+    else {
+      const int ee = (int)(si - 2) / 4;
+      for (const PolyInfo& p : s.pinfo) L.dur.push_back(d.phase_durations[ee][p.phase] / p.n_polys_in_phase);  // :75-86
+    }
+    L.spl.push_back(m);
+  }
+
+  if (int rc = init_values(d, d.init, d.terrain, sets, err)) return rc;
+  L.x0.assign((size_t)L.n, 0.0);
+  for (auto& s : sets) { auto v = get_values(s); std::copy(v.begin(), v.end(), L.x0.begin() + s.col0); }
+  L.desc = d;
+
+  // ---- robot & terrain
+  {
+    const double* I = d.robot.inertia;
+    const double Ib[9] = {I[0], -I[3], -I[4], -I[3], I[1], -I[5], -I[4], -I[5], I[2]};
+    std::memcpy(L.rb.Ib, Ib, sizeof Ib);
+    L.rb.m = d.robot.mass; L.rb.g = d.robot.gravity; L.rb.n_ee = E;
+    L.terrain = d.terrain;
+    L.fdisc_motion = ter_has_curvature(d.terrain.id) ? 1 : 0;
+  }
+
+  // ---- constraint sets and work items (AddConstraintSet order)
+  L.cons.clear(); L.items.clear();
+  std::vector<int> item_inst;   // instance id (items of one instance share rows)
+  int row = 0, inst = 0;
+  auto dts_of = [](double Tc, double dt) {   // time_discretization_constraint.cc:37-50
+    std::vector<double> v; double t = 0.0; v.push_back(t);
+    for (int i = 0; i < (int)std::floor(Tc / dt); ++i) { t += dt; v.push_back(t); }
+    v.push_back(Tc);
+    return v;
+  };
+  for (int ci = 0; ci < d.n_constraints; ++ci) {
+    const towr_constraint_t& c = d.constraints[ci];
+    ConsInfo info{c.kind, c.ee, row, 0};
+    auto add = [&](int type, int group, int ee, int k, int row0, double t, int a0, int a1, double p0) {
+      ItemDesc it{}; it.type = type; it.group = group; it.ee = ee; it.k = k; it.row0 = row0;
+      it.t = t; it.a0 = a0; it.a1 = a1; it.p0 = p0;
+      L.items.push_back(it); item_inst.push_back(inst);
+    };
+    const bool timed = c.kind == TOWR_C_DYNAMIC || c.kind == TOWR_C_RANGE_OF_MOTION ||
+                       c.kind == TOWR_C_FORCE_DISCRETIZED || c.kind == TOWR_C_BASE_MOTION;
+    if (timed && !(c.dt > 0 && c.T > 0)) { err = "time-discretised constraint needs T > 0 and dt > 0"; return TOWR_ERR_INVALID; }
+    const bool ee_c = c.kind == TOWR_C_RANGE_OF_MOTION || c.kind == TOWR_C_FORCE || c.kind == TOWR_C_FORCE_DISCRETIZED ||
+                      c.kind == TOWR_C_TERRAIN || c.kind == TOWR_C_SWING;
+    if (ee_c && (c.ee < 0 || c.ee >= E)) { err = "constraint endeffector out of range"; return TOWR_ERR_INVALID; }
+    switch (c.kind) {
+      case TOWR_C_DYNAMIC: {
+        auto ts = dts_of(c.T, c.dt);
+        for (int k = 0; k < (int)ts.size(); ++k, ++inst)
+          for (int g = 0; g < 2 + E; ++g) add(IT_DYN, g, 0, k, row + 6 * k, ts[k], 0, 0, 0.0);
+        info.rows = 6 * (int)ts.size();
+        break;
+      }
+      case TOWR_C_RANGE_OF_MOTION: {
+        auto ts = dts_of(c.T, c.dt);
+        for (int k = 0; k < (int)ts.size(); ++k, ++inst)
+          for (int g = 0; g < 3; ++g) add(IT_ROM, g, c.ee, k, row + 3 * k, ts[k], 0, 0, 0.0);
+        info.rows = 3 * (int)ts.size();
+        break;
+      }
+      case TOWR_C_FORCE_DISCRETIZED: {
+        auto ts = dts_of(c.T, c.dt);
+        for (int k = 0; k < (int)ts.size(); ++k, ++inst) add(IT_FDISC, 0, c.ee, k, row + 5 * k, ts[k], 0, 0, 0.0);
+        info.rows = 5 * (int)ts.size();
+        break;
+      }
+      case TOWR_C_BASE_MOTION: {
+        auto ts = dts_of(c.T, c.dt);
+        for (int k = 0; k < (int)ts.size(); ++k, ++inst) add(IT_BMOT, 0, 0, k, row + 6 * k, ts[k], 0, 0, 0.0);
+        info.rows = 6 * (int)ts.size();
+        break;
+      }
+      case TOWR_C_FORCE: {         // force_constraint.cc:50-60
+        const NodeSet& fv = sets[4 + 4 * c.ee];
+        const NodeSet& mv = sets[2 + 4 * c.ee];
+        int k = 0;
+        for (int id = 0; id < fv.n_nodes; ++id)
+          if (!fv.is_constant_node(id)) {
+            const int mn = mv.node_at_start_of_phase(fv.phase_of(id));
+            if (mn < 0) { err = "force node phase has no motion node"; return TOWR_ERR_INVALID; }
+            add(IT_FNODE, 0, c.ee, k, row + 5 * k, 0.0, id, mn, 0.0); ++k; ++inst;
+          }
+        info.rows = 5 * k;
+        break;
+      }
+      case TOWR_C_TERRAIN: {       // terrain_constraint.cc:48-59
+        const NodeSet& mv = sets[2 + 4 * c.ee];
+        for (int id = 1; id < mv.n_nodes; ++id, ++inst) add(IT_TERR, 0, c.ee, id - 1, row + id - 1, 0.0, id, 0, 0.0);
+        info.rows = mv.n_nodes - 1;
+        break;
+      }
+      case TOWR_C_BASE_HEIGHT: {   // base_height_constraint.cc:45-56
+        const NodeSet& bv = sets[0];
+        for (int id = 1; id < bv.n_nodes; ++id, ++inst) add(IT_BHGT, 0, 0, id - 1, row + id - 1, 0.0, id, 0, c.p[0]);
+        info.rows = bv.n_nodes - 1;
+        break;
+      }
+      case TOWR_C_SWING: {         // swing_constraint.cc:41-52
+        const NodeSet& mv = sets[2 + 4 * c.ee];
+        int k = 0;
+        for (int id = 0; id < mv.n_nodes; ++id)
+          if (!mv.is_constant_node(id)) {
+            if (id == 0 || id == mv.n_nodes - 1) { err = "swing node at trajectory boundary (the reference indexes out of range)"; return TOWR_ERR_INVALID; }
+            add(IT_SWING, 0, c.ee, k, row + 4 * k, 0.0, id, 0, c.p[0] > 0 ? c.p[0] : 0.3); ++k; ++inst;
+          }
+        info.rows = 4 * k;
+        break;
+      }
+      case TOWR_C_SPLINE_ACC: {    // spline_acc_constraint.cc:34-46
+        if (c.ee != 0 && c.ee != 1) { err = "SplineAcc: ee must be 0 (base-lin) or 1 (base-ang)"; return TOWR_ERR_INVALID; }
+        const int nj = L.spl[c.ee].n_polys - 1;
+        for (int j = 0; j < nj; ++j, ++inst) add(IT_SACC, 0, c.ee, j, row + 3 * j, 0.0, 0, 0, 0.0);
+        info.rows = 3 * (nj > 0 ? nj : 0);
+        break;
+      }
+      case TOWR_C_TOTAL_DURATION:
+        err = "TotalDurationConstraint requires phase-duration optimisation (not supported yet)"; return TOWR_ERR_UNSUPPORTED;
+      default: err = "unknown constraint kind"; return TOWR_ERR_INVALID;
+    }
+    row += info.rows;
+    L.cons.push_back(info);
+  }
+  L.m = row;
+
+  // ---- structure pass at x0: candidate (row, col) of every item
+  std::vector<int32_t> crow, ccol; std::vector<uint8_t> cpres;
+  std::vector<int32_t> item_cand_begin(L.items.size() + 1, 0);
+  {
+    Ctx cx{};
+    cx.x = L.x0.data(); cx.nodecol = L.nodecol.data(); cx.spl = L.spl.data(); cx.dur = L.dur.data();
+    cx.ter = &L.terrain; cx.rb = L.rb; cx.fdisc_motion = L.fdisc_motion;
+    for (size_t i = 0; i < L.items.size(); ++i) {
+      item_cand_begin[i] = (int32_t)crow.size();
+      RecordEmit em{&crow, &ccol, &cpres};
+      em.g_rows_lo = L.items[i].row0; em.g_rows_hi = L.items[i].row0 + item_rows(L.items[i].type);
+      eval_item(cx, L.items[i], em);
+      if (em.bad_g) { err = "internal: item wrote g outside its rows"; return TOWR_ERR_INVALID; }
+    }
+    item_cand_begin[L.items.size()] = (int32_t)crow.size();
+  }
+
+  // ---- CSR pattern (setFromTriplets: sorted columns, duplicates merged)
+  std::vector<std::vector<int32_t>> rc((size_t)L.m);
+  for (size_t q = 0; q < crow.size(); ++q)
+    if (cpres[q]) {
+      if (crow[q] < 0 || crow[q] >= L.m || ccol[q] < 0 || ccol[q] >= L.n) { err = "internal: candidate out of range"; return TOWR_ERR_INVALID; }
+      rc[crow[q]].push_back(ccol[q]);
+    }
+  L.row_ptr.assign((size_t)L.m + 1, 0);
+  L.col.clear();
+  for (int r = 0; r < L.m; ++r) {
+    auto& v = rc[r];
+    std::sort(v.begin(), v.end());
+    v.erase(std::unique(v.begin(), v.end()), v.end());
+    L.col.insert(L.col.end(), v.begin(), v.end());
+    L.row_ptr[r + 1] = (int64_t)L.col.size();
+  }
+  L.nnz = (int64_t)L.col.size();
+  if (L.nnz >= (int64_t)INT32_MAX) { err = "too many nonzeros"; return TOWR_ERR_UNSUPPORTED; }
+
+  // ---- slot table: candidate -> CSR position (or -1)
+  L.slots.resize(crow.size());
+  for (size_t q = 0; q < crow.size(); ++q) {
+    if (!cpres[q]) { L.slots[q] = -1; continue; }
+    const int r = crow[q];
+    const int32_t* b = L.col.data() + L.row_ptr[r];
+    const int32_t* e = L.col.data() + L.row_ptr[r + 1];
+    L.slots[q] = (int32_t)(L.row_ptr[r] + (std::lower_bound(b, e, ccol[q]) - b));
+  }
+  for (size_t i = 0; i < L.items.size(); ++i) L.items[i].slot = item_cand_begin[i];
+
+  // ---- tiles: consecutive instances of one constraint set, bounded by the LDS caps
+  L.tiles.clear();
+  L.max_tile_values = 0; L.max_tile_rows = 0;
+  size_t i = 0;
+  while (i < L.items.size()) {
+    TileDesc t{};
+    t.i0 = (int32_t)i; t.type = L.items[i].type;
+    const int set_row0 = [&] { for (auto& c : L.cons) if (L.items[i].row0 >= c.row0 && L.items[i].row0 < c.row0 + c.rows) return c.row0; return 0; }();
+    const int set_row1 = [&] { for (auto& c : L.cons) if (L.items[i].row0 >= c.row0 && L.items[i].row0 < c.row0 + c.rows) return c.row0 + c.rows; return L.m; }();
+    t.r0 = L.items[i].row0;
+    size_t j = i;
+    while (j < L.items.size()) {
+      // extent of the next instance
+      size_t k = j;
+      while (k < L.items.size() && item_inst[k] == item_inst[j]) ++k;
+      const int r1 = L.items[j].row0 + item_rows(L.items[j].type);
+      if (L.items[j].row0 < set_row0 || r1 > set_row1) break;   // next constraint set
+      const int64_t nv = L.row_ptr[r1] - L.row_ptr[t.r0];
+      const int nr = r1 - t.r0;
+      if (j > i && (nv > kTileValueCap || nr > kTileRowCap || (int)(k - i) > kTileItemCap)) break;
+      if (nv > kTileValueCap || nr > kTileRowCap) { err = "internal: one instance exceeds the LDS tile"; return TOWR_ERR_UNSUPPORTED; }
+      j = k;
+      t.r1 = r1;
+    }
+    t.i1 = (int32_t)j;
+    t.v0 = (int32_t)L.row_ptr[t.r0]; t.v1 = (int32_t)L.row_ptr[t.r1];
+    L.max_tile_values = std::max(L.max_tile_values, t.v1 - t.v0);
+    L.max_tile_rows = std::max(L.max_tile_rows, t.r1 - t.r0);
+    L.tiles.push_back(t);
+    i = j;
+  }
+  // rows without items (empty sets) are fine; every row with an item is covered by exactly one tile
+  return TOWR_OK;
+}
+
+int initial_x_for(const towr_problem_desc_t& d, const towr_init_t& init, const towr_terrain_t& ter,
+                  std::vector<double>& x0, std::string& err) {
+  std::vector<double> base_d;
+  std::vector<NodeSet> sets;
+  if (int rc = make_sets(d, base_d, sets, err)) return rc;
+  int col = 0;
+  for (int i = 0; i < d.n_varsets; ++i) {   // same column layout as build_layout
+    const int k = d.varsets[i].kind, ee = d.varsets[i].ee;
+    int si = k == TOWR_VAR_BASE_LIN ? 0 : k == TOWR_VAR_BASE_ANG ? 1 : k == TOWR_VAR_EE_MOTION ? 2 + 4 * ee :
+             k == TOWR_VAR_EE_ANG ? 3 + 4 * ee : k == TOWR_VAR_EE_FORCE ? 4 + 4 * ee : 5 + 4 * ee;
+    sets[si].col0 = col; col += sets[si].n_rows;
+  }
+  if (int rc = init_values(d, init, ter, sets, err)) return rc;
+  x0.assign((size_t)col, 0.0);
+  for (auto& s : sets) { auto v = get_values(s); std::copy(v.begin(), v.end(), x0.begin() + s.col0); }
+  return TOWR_OK;
+}
+
+void group_tiles(const Layout& L, int n_groups, std::vector<int32_t>& out) {
+  const int nt = (int)L.tiles.size();
+  if (n_groups < 1) n_groups = 1;
+  if (n_groups > nt) n_groups = nt;
+  out.assign((size_t)n_groups + 1, nt);
+  out[0] = 0;
+  // greedy: equal share of (values + rows) per group
+  int64_t total = 0;
+  for (auto& t : L.tiles) total += (t.v1 - t.v0) + (t.r1 - t.r0) + 64;
+  int64_t acc = 0; int g = 1;
+  for (int ti = 0; ti < nt && g < n_groups; ++ti) {
+    acc += (L.tiles[ti].v1 - L.tiles[ti].v0) + (L.tiles[ti].r1 - L.tiles[ti].r0) + 64;
+    if (acc * n_groups >= total * g && (nt - (ti + 1)) >= (n_groups - g)) out[g++] = ti + 1;
+  }
+  while (g < n_groups) { out[g] = std::min(nt, out[g - 1] + 1); ++g; }
+  out[n_groups] = nt;
+}
+
+}  // namespace tg

@@ -1,0 +1,453 @@
+// towr_gpu.hip — gfx950 kernel and C-ABI (include/towr_gpu.h) of the eval_g / eval_jac_g engine.
+//
+// One fused launch evaluates, for a batch of B problems sharing one layout, every constraint value
+// g and every Jacobian nonzero of ifopt's RowMajor CSR (what IpoptAdapter::eval_g / eval_jac_g
+// return). Work decomposition:
+//   * block = (problem, group of LDS tiles); blocks of one problem are placed on one XCD
+//     (blockIdx % 8 round-robin), so x is fetched from HBM once per problem;
+//   * the problem's x (NodesVariables / PhaseDurations values) is staged in LDS;
+//   * a tile = consecutive instances of one constraint set whose CSR value range fits in LDS;
+//     lanes evaluate work items (node-per-lane Hermite splines, SRBD, terrain) and accumulate
+//     Jacobian candidates into LDS at precomputed slots; then the tile's contiguous CSR range and
+//     g range are written with 16-byte coalesced stores.
+// No MFMA: there is no dense contraction; the kernel is HBM-write bound.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "engine_math.h"
+#include "layout.h"
+
+using namespace tg;
+
+namespace {
+
+constexpr int kBlock = 256;
+
+struct KParams {
+  const double* X; int64_t ldx;
+  double* G; int64_t ldg;
+  double* V; int64_t ldv;
+  const ItemDesc* items;
+  const int32_t* slots;
+  const TileDesc* tiles;
+  const int32_t* gtile;         // tile range of each group [gtile[g], gtile[g+1])
+  const int32_t* nodecol;
+  const SplineMeta* spl;
+  const double* dur;
+  const towr_terrain_t* terrains;
+  int32_t terrain_per_problem;
+  int32_t n, n_pad, B, n_groups;
+  int32_t want_g, want_jac, fdisc_motion, reserved;
+  RobotC rb;
+};
+
+struct LdsEmit {
+  const int32_t* slot;
+  int j;
+  double* vt;
+  int v0;
+  double* gt;
+  int r0;
+  __device__ __forceinline__ void g(int row, double v) { gt[row - r0] = v; }
+  __device__ __forceinline__ void operator()(int row, int col, double v, bool) {
+    if (col >= 0) {
+      const int s = slot[j];
+      if (s >= 0) vt[s - v0] += v;
+    }
+    ++j;
+  }
+};
+
+// LDS -> HBM, 16-byte stores where the destination allows it
+__device__ __forceinline__ void copy_out(const double* __restrict__ src, double* __restrict__ dst, int n) {
+  const int head = (reinterpret_cast<uintptr_t>(dst) & 15) ? 1 : 0;
+  if (n <= 0) return;
+  if (head && threadIdx.x == 0) dst[0] = src[0];
+  const int m = (n - head) >> 1;
+  double2* d2 = reinterpret_cast<double2*>(dst + head);
+  for (int i = threadIdx.x; i < m; i += blockDim.x) {
+    double2 v;
+    v.x = src[head + 2 * i];
+    v.y = src[head + 2 * i + 1];
+    d2[i] = v;
+  }
+  if (((n - head) & 1) && threadIdx.x == 0) dst[n - 1] = src[n - 1];
+}
+
+__global__ void __launch_bounds__(kBlock) towr_eval_kernel(KParams P) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int total = P.B * P.n_groups;
+  const int per = (total + 7) / 8;
+  // XCD-aware mapping: consecutive work ids (the groups of one problem) share blockIdx % 8
+  const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+  if (w >= total) return;
+  const int b = w / P.n_groups, grp = w % P.n_groups;
+  double* xs = smem;
+  double* vt = smem + P.n_pad;
+  double* gt = vt + kTileValueCap;
+
+  // stage x (NodesVariables / PhaseDurations of this problem) in LDS
+  const double* xb = P.X + (int64_t)b * P.ldx;
+  if ((reinterpret_cast<uintptr_t>(xb) & 15) == 0) {
+    const double2* x2 = reinterpret_cast<const double2*>(xb);
+    for (int i = threadIdx.x; i < (P.n >> 1); i += blockDim.x) {
+      const double2 v = x2[i];
+      xs[2 * i] = v.x; xs[2 * i + 1] = v.y;
+    }
+    if ((P.n & 1) && threadIdx.x == 0) xs[P.n - 1] = xb[P.n - 1];
+  } else {
+    for (int i = threadIdx.x; i < P.n; i += blockDim.x) xs[i] = xb[i];
+  }
+  __syncthreads();
+
+  Ctx c;
+  c.x = xs; c.nodecol = P.nodecol; c.spl = P.spl; c.dur = P.dur;
+  c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
+  c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
+
+  double* Vb = P.V + (int64_t)b * P.ldv;
+  double* Gb = P.G + (int64_t)b * P.ldg;
+  for (int ti = P.gtile[grp]; ti < P.gtile[grp + 1]; ++ti) {
+    const TileDesc T = P.tiles[ti];
+    const int nv = T.v1 - T.v0, nr = T.r1 - T.r0;
+    for (int i = threadIdx.x; i < nv; i += blockDim.x) vt[i] = 0.0;
+    __syncthreads();
+    for (int i = T.i0 + (int)threadIdx.x; i < T.i1; i += blockDim.x) {
+      const ItemDesc it = P.items[i];
+      LdsEmit em{P.slots + it.slot, 0, vt, T.v0, gt, T.r0};
+      eval_item(c, it, em);
+    }
+    __syncthreads();
+    if (P.want_jac) copy_out(vt, Vb + T.v0, nv);
+    if (P.want_g) for (int i = threadIdx.x; i < nr; i += blockDim.x) Gb[T.r0 + i] = gt[i];
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+// =================================================================================================
+// handle
+// =================================================================================================
+struct towr_gpu_handle_s {
+  Layout L;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  // device tables
+  ItemDesc* d_items = nullptr;
+  int32_t* d_slots = nullptr;
+  TileDesc* d_tiles = nullptr;
+  int32_t* d_nodecol = nullptr;
+  SplineMeta* d_spl = nullptr;
+  double* d_dur = nullptr;
+  towr_terrain_t* d_terrain = nullptr;      // base terrain (1 entry)
+  towr_terrain_t* d_bterrain = nullptr;     // per-problem batch terrains
+  int32_t bterrain_n = 0;
+  int32_t* d_gtile = nullptr;
+  int32_t gtile_groups = 0;
+  int32_t tiles_per_block = 0;              // 0 = automatic
+  // staging for host-pointer entry points
+  double *d_x = nullptr, *d_g = nullptr, *d_v = nullptr;
+  double *h_x = nullptr, *h_g = nullptr, *h_v = nullptr;
+  int32_t stage_B = 0;
+};
+
+namespace {
+std::mutex g_err_mu;
+std::string g_last_error;
+
+int fail(towr_gpu_handle h, int code, const std::string& msg) {
+  if (h) h->err = msg;
+  std::lock_guard<std::mutex> lk(g_err_mu);
+  g_last_error = msg;
+  return code;
+}
+
+#define HIPCHK(h, expr)                                                                         \
+  do {                                                                                          \
+    hipError_t e_ = (expr);                                                                     \
+    if (e_ != hipSuccess) return fail((h), TOWR_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+template <class T>
+int upload(towr_gpu_handle h, T** dst, const std::vector<T>& src) {
+  const size_t bytes = sizeof(T) * (src.empty() ? 1 : src.size());
+  HIPCHK(h, hipMalloc(reinterpret_cast<void**>(dst), bytes));
+  if (!src.empty()) HIPCHK(h, hipMemcpy(*dst, src.data(), sizeof(T) * src.size(), hipMemcpyHostToDevice));
+  return TOWR_OK;
+}
+
+int ensure_groups(towr_gpu_handle h, int n_groups) {
+  if (n_groups == h->gtile_groups && h->d_gtile) return TOWR_OK;
+  std::vector<int32_t> gt;
+  group_tiles(h->L, n_groups, gt);
+  if (h->d_gtile) { (void)hipFree(h->d_gtile); h->d_gtile = nullptr; }
+  if (int rc = upload(h, &h->d_gtile, gt)) return rc;
+  h->gtile_groups = (int32_t)gt.size() - 1;
+  return TOWR_OK;
+}
+
+int auto_groups(towr_gpu_handle h, int B) {
+  const int nt = (int)h->L.tiles.size();
+  if (h->tiles_per_block > 0) return std::max(1, (nt + h->tiles_per_block - 1) / h->tiles_per_block);
+  // enough blocks to fill 256 CUs several times over; one group per problem at large batches
+  int g = (4096 + B - 1) / B;
+  if (g < 1) g = 1;
+  if (g > nt) g = nt;
+  return g;
+}
+
+int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, int64_t ldg, double* V, int64_t ldv,
+           int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem) {
+  if (B <= 0) return TOWR_OK;
+  int ng = auto_groups(h, B);
+  if (int rc = ensure_groups(h, ng)) return rc;
+  ng = h->gtile_groups;
+  const Layout& L = h->L;
+  KParams P{};
+  P.X = X; P.ldx = ldx; P.G = G; P.ldg = ldg; P.V = V; P.ldv = ldv;
+  P.items = h->d_items; P.slots = h->d_slots; P.tiles = h->d_tiles; P.gtile = h->d_gtile;
+  P.nodecol = h->d_nodecol; P.spl = h->d_spl; P.dur = h->d_dur;
+  P.terrains = terrains; P.terrain_per_problem = per_problem;
+  P.n = L.n; P.n_pad = (L.n + 1) & ~1; P.B = B; P.n_groups = ng;
+  P.want_g = want_g; P.want_jac = want_jac; P.fdisc_motion = L.fdisc_motion;
+  P.rb = L.rb;
+  const size_t lds = sizeof(double) * ((size_t)P.n_pad + kTileValueCap + kTileRowCap);
+  const int64_t total = (int64_t)B * ng;
+  const int64_t grid = ((total + 7) / 8) * 8;
+  if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
+  hipLaunchKernelGGL(towr_eval_kernel, dim3((unsigned)grid), dim3(kBlock), lds, s, P);
+  HIPCHK(h, hipGetLastError());
+  return TOWR_OK;
+}
+
+int ensure_stage(towr_gpu_handle h, int B) {
+  if (B <= h->stage_B) return TOWR_OK;
+  const Layout& L = h->L;
+  if (h->d_x) { (void)hipFree(h->d_x); (void)hipFree(h->d_g); (void)hipFree(h->d_v); }
+  if (h->h_x) { (void)hipHostFree(h->h_x); (void)hipHostFree(h->h_g); (void)hipHostFree(h->h_v); }
+  h->d_x = h->d_g = h->d_v = h->h_x = h->h_g = h->h_v = nullptr;
+  HIPCHK(h, hipMalloc(&h->d_x, sizeof(double) * (size_t)B * L.n));
+  HIPCHK(h, hipMalloc(&h->d_g, sizeof(double) * (size_t)B * std::max(1, L.m)));
+  HIPCHK(h, hipMalloc(&h->d_v, sizeof(double) * (size_t)B * std::max<int64_t>(1, L.nnz)));
+  HIPCHK(h, hipHostMalloc(&h->h_x, sizeof(double) * (size_t)B * L.n, hipHostMallocDefault));
+  HIPCHK(h, hipHostMalloc(&h->h_g, sizeof(double) * (size_t)B * std::max(1, L.m), hipHostMallocDefault));
+  HIPCHK(h, hipHostMalloc(&h->h_v, sizeof(double) * (size_t)B * std::max<int64_t>(1, L.nnz), hipHostMallocDefault));
+  h->stage_B = B;
+  return TOWR_OK;
+}
+
+int host_eval(towr_gpu_handle h, int B, const double* X, double* G, double* V) {
+  if (h->device < 0) return fail(h, TOWR_ERR_NO_DEVICE, "layout-only handle (created with device < 0) cannot evaluate");
+  if (int rc = ensure_stage(h, B)) return rc;
+  const Layout& L = h->L;
+  const size_t xb = sizeof(double) * (size_t)B * L.n, gb = sizeof(double) * (size_t)B * L.m,
+               vb = sizeof(double) * (size_t)B * L.nnz;
+  std::memcpy(h->h_x, X, xb);
+  HIPCHK(h, hipMemcpyAsync(h->d_x, h->h_x, xb, hipMemcpyHostToDevice, h->stream));
+  const bool per = h->d_bterrain && h->bterrain_n >= B && B > 1;
+  if (int rc = launch(h, B, h->d_x, L.n, h->d_g, L.m, h->d_v, L.nnz, G != nullptr, V != nullptr, h->stream,
+                      per ? h->d_bterrain : h->d_terrain, per ? 1 : 0))
+    return rc;
+  if (G) HIPCHK(h, hipMemcpyAsync(h->h_g, h->d_g, gb, hipMemcpyDeviceToHost, h->stream));
+  if (V) HIPCHK(h, hipMemcpyAsync(h->h_v, h->d_v, vb, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (G) std::memcpy(G, h->h_g, gb);
+  if (V) std::memcpy(V, h->h_v, vb);
+  return TOWR_OK;
+}
+
+}  // namespace
+
+// =================================================================================================
+// C-ABI
+// =================================================================================================
+extern "C" {
+
+int towr_gpu_abi_version(void) { return TOWR_GPU_ABI_VERSION; }
+
+const char* towr_gpu_last_error(towr_gpu_handle h) {
+  if (h) return h->err.c_str();
+  std::lock_guard<std::mutex> lk(g_err_mu);
+  return g_last_error.c_str();
+}
+
+int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle* out) {
+  if (!desc || !out) return fail(nullptr, TOWR_ERR_INVALID, "null argument");
+  *out = nullptr;
+  towr_gpu_handle h = new towr_gpu_handle_s();
+  std::string err;
+  const int rc = build_layout(*desc, h->L, err);
+  if (rc != TOWR_OK) { fail(nullptr, rc, err); delete h; return rc; }
+  if (device < 0) {   // layout-only handle: sizes / structure / x0, no evaluation (CPU-side tests)
+    h->device = -1;
+    *out = h;
+    return TOWR_OK;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device >= ndev) {
+    fail(nullptr, TOWR_ERR_NO_DEVICE, "no HIP device available for towr_gpu_create");
+    delete h;
+    return TOWR_ERR_NO_DEVICE;
+  }
+  h->device = device;
+  auto bail = [&](int code) { std::string m = h->err; towr_gpu_destroy(h); fail(nullptr, code, m); return code; };
+  if (hipSetDevice(device) != hipSuccess) { h->err = "hipSetDevice failed"; return bail(TOWR_ERR_HIP); }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    h->err = std::string("device is ") + prop.gcnArchName + ", this build targets gfx950 only";
+    return bail(TOWR_ERR_NO_DEVICE);
+  }
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) { h->err = "hipStreamCreate failed"; return bail(TOWR_ERR_HIP); }
+  const Layout& L = h->L;
+  std::vector<towr_terrain_t> ter(1, L.terrain);
+  int r;
+  if ((r = upload(h, &h->d_items, L.items)) || (r = upload(h, &h->d_slots, L.slots)) ||
+      (r = upload(h, &h->d_tiles, L.tiles)) || (r = upload(h, &h->d_nodecol, L.nodecol)) ||
+      (r = upload(h, &h->d_spl, L.spl)) || (r = upload(h, &h->d_dur, L.dur)) || (r = upload(h, &h->d_terrain, ter)))
+    return bail(r);
+  const size_t lds = sizeof(double) * ((size_t)((L.n + 1) & ~1) + kTileValueCap + kTileRowCap);
+  if (lds > 160 * 1024) { h->err = "problem too large for the LDS layout"; return bail(TOWR_ERR_UNSUPPORTED); }
+  if (lds > 64 * 1024 &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(towr_eval_kernel), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+    h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
+  }
+  *out = h;
+  return TOWR_OK;
+}
+
+int towr_gpu_destroy(towr_gpu_handle h) {
+  if (!h) return TOWR_OK;
+  void* dev[] = {h->d_items, h->d_slots, h->d_tiles, h->d_nodecol, h->d_spl, h->d_dur, h->d_terrain,
+                 h->d_bterrain, h->d_gtile, h->d_x, h->d_g, h->d_v};
+  if (h->device >= 0) for (void* p : dev) if (p) (void)hipFree(p);
+  void* host[] = {h->h_x, h->h_g, h->h_v};
+  for (void* p : host) if (p) (void)hipHostFree(p);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+  return TOWR_OK;
+}
+
+int towr_gpu_sizes(towr_gpu_handle h, int32_t* n, int32_t* m, int64_t* nnz) {
+  if (!h) return fail(nullptr, TOWR_ERR_INVALID, "null handle");
+  if (n) *n = h->L.n;
+  if (m) *m = h->L.m;
+  if (nnz) *nnz = h->L.nnz;
+  return TOWR_OK;
+}
+
+int towr_gpu_jac_structure(towr_gpu_handle h, int32_t* iRow, int32_t* jCol) {
+  if (!h || !iRow || !jCol) return fail(h, TOWR_ERR_INVALID, "null argument");
+  const Layout& L = h->L;
+  for (int r = 0; r < L.m; ++r)
+    for (int64_t k = L.row_ptr[r]; k < L.row_ptr[r + 1]; ++k) { iRow[k] = r; jCol[k] = L.col[k]; }
+  return TOWR_OK;
+}
+
+int towr_gpu_jac_csr(towr_gpu_handle h, int64_t* row_ptr, int32_t* col) {
+  if (!h || !row_ptr || !col) return fail(h, TOWR_ERR_INVALID, "null argument");
+  std::memcpy(row_ptr, h->L.row_ptr.data(), sizeof(int64_t) * h->L.row_ptr.size());
+  if (h->L.nnz) std::memcpy(col, h->L.col.data(), sizeof(int32_t) * h->L.col.size());
+  return TOWR_OK;
+}
+
+int towr_gpu_initial_x(towr_gpu_handle h, double* x0) {
+  if (!h || !x0) return fail(h, TOWR_ERR_INVALID, "null argument");
+  std::memcpy(x0, h->L.x0.data(), sizeof(double) * h->L.x0.size());
+  return TOWR_OK;
+}
+
+int towr_gpu_initial_x_for(towr_gpu_handle h, const towr_init_t* init, const towr_terrain_t* terrain, double* x0) {
+  if (!h || !init || !terrain || !x0) return fail(h, TOWR_ERR_INVALID, "null argument");
+  std::vector<double> v;
+  std::string err;
+  if (int rc = initial_x_for(h->L.desc, *init, *terrain, v, err)) return fail(h, rc, err);
+  std::memcpy(x0, v.data(), sizeof(double) * v.size());
+  return TOWR_OK;
+}
+
+int towr_gpu_varset_info(towr_gpu_handle h, int32_t i, int32_t* kind, int32_t* ee, int32_t* col0, int32_t* n) {
+  if (!h || i < 0 || i >= (int32_t)h->L.varsets.size()) return fail(h, TOWR_ERR_INVALID, "bad variable set index");
+  const VarSetInfo& v = h->L.varsets[i];
+  if (kind) *kind = v.kind;
+  if (ee) *ee = v.ee;
+  if (col0) *col0 = v.col0;
+  if (n) *n = v.n;
+  return TOWR_OK;
+}
+
+int towr_gpu_eval_g(towr_gpu_handle h, const double* x, double* g) {
+  if (!h || !x || !g) return fail(h, TOWR_ERR_INVALID, "null argument");
+  if (hipSetDevice(h->device) != hipSuccess) return fail(h, TOWR_ERR_HIP, "hipSetDevice");
+  return host_eval(h, 1, x, g, nullptr);
+}
+
+int towr_gpu_eval_jac_values(towr_gpu_handle h, const double* x, double* values) {
+  if (!h || !x || !values) return fail(h, TOWR_ERR_INVALID, "null argument");
+  if (hipSetDevice(h->device) != hipSuccess) return fail(h, TOWR_ERR_HIP, "hipSetDevice");
+  return host_eval(h, 1, x, nullptr, values);
+}
+
+int towr_gpu_eval_g_jac(towr_gpu_handle h, const double* x, double* g, double* values) {
+  if (!h || !x || !g || !values) return fail(h, TOWR_ERR_INVALID, "null argument");
+  if (hipSetDevice(h->device) != hipSuccess) return fail(h, TOWR_ERR_HIP, "hipSetDevice");
+  return host_eval(h, 1, x, g, values);
+}
+
+int towr_gpu_set_batch_terrain(towr_gpu_handle h, int32_t B, const towr_terrain_t* terrains) {
+  if (!h || B < 0 || (B > 0 && !terrains)) return fail(h, TOWR_ERR_INVALID, "bad argument");
+  // The shared pattern holds only while every terrain keeps the base terrain's curvature class:
+  // ForceConstraintDiscretized inserts motion entries only where f . d(basis) != 0 (quirk A22 iv).
+  for (int i = 0; i < B; ++i) {
+    if (ter_has_curvature(terrains[i].id) != ter_has_curvature(h->L.terrain.id))
+      return fail(h, TOWR_ERR_UNSUPPORTED, "batch terrain changes the Jacobian pattern (curvature class differs from the base terrain)");
+    if (ter_has_curvature(terrains[i].id) && B > 1)
+      return fail(h, TOWR_ERR_UNSUPPORTED, "Gap terrain has an x-dependent pattern; batch it one problem per handle");
+  }
+  if (h->device < 0) return fail(h, TOWR_ERR_NO_DEVICE, "layout-only handle (created with device < 0) cannot evaluate");
+  if (hipSetDevice(h->device) != hipSuccess) return fail(h, TOWR_ERR_HIP, "hipSetDevice");
+  if (h->d_bterrain) { (void)hipFree(h->d_bterrain); h->d_bterrain = nullptr; h->bterrain_n = 0; }
+  if (B == 0) return TOWR_OK;
+  std::vector<towr_terrain_t> v(terrains, terrains + B);
+  if (int rc = upload(h, &h->d_bterrain, v)) return rc;
+  h->bterrain_n = B;
+  return TOWR_OK;
+}
+
+int towr_gpu_eval_batch_device(towr_gpu_handle h, int32_t B, const double* X, int64_t ldx, double* G, int64_t ldg,
+                               double* V, int64_t ldv, int32_t want_g, int32_t want_jac, void* stream) {
+  if (!h || B < 0 || !X) return fail(h, TOWR_ERR_INVALID, "bad argument");
+  const Layout& L = h->L;
+  if (ldx < L.n || (want_g && (!G || ldg < L.m)) || (want_jac && (!V || ldv < L.nnz)))
+    return fail(h, TOWR_ERR_INVALID, "leading dimension smaller than n / m / nnz, or missing output");
+  if (h->device < 0) return fail(h, TOWR_ERR_NO_DEVICE, "layout-only handle (created with device < 0) cannot evaluate");
+  if (hipSetDevice(h->device) != hipSuccess) return fail(h, TOWR_ERR_HIP, "hipSetDevice");
+  const bool per = h->d_bterrain && h->bterrain_n >= B;
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : h->stream;
+  return launch(h, B, X, ldx, G, ldg, V, ldv, want_g, want_jac, s, per ? h->d_bterrain : h->d_terrain, per ? 1 : 0);
+}
+
+int towr_gpu_eval_batch(towr_gpu_handle h, int32_t B, const double* X, double* G, double* V) {
+  if (!h || B < 0 || !X) return fail(h, TOWR_ERR_INVALID, "bad argument");
+  if (hipSetDevice(h->device) != hipSuccess) return fail(h, TOWR_ERR_HIP, "hipSetDevice");
+  return host_eval(h, B, X, G, V);
+}
+
+int towr_gpu_set_tiles_per_block(towr_gpu_handle h, int32_t tiles_per_block) {
+  if (!h || tiles_per_block < 0) return fail(h, TOWR_ERR_INVALID, "bad argument");
+  h->tiles_per_block = tiles_per_block;
+  return TOWR_OK;
+}
+
+int64_t towr_gpu_algorithmic_bytes_per_call(towr_gpu_handle h) {
+  if (!h) return 0;
+  return 8 * ((int64_t)h->L.n + h->L.m + h->L.nnz) + (int64_t)sizeof(towr_terrain_t);
+}
+
+}  // extern "C"

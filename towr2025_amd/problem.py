@@ -1,0 +1,137 @@
+"""ifopt::Problem-shaped host API over the HIP engine's C-ABI (include/towr_gpu.h).
+
+Mirrors what IPOPT reaches through ifopt's IpoptAdapter for the hot path:
+  GetNumberOfOptimizationVariables / GetNumberOfConstraints / nonzeros  -> sizes()
+  GetVariableValues (starting point)                                    -> initial_x()
+  EvalConstraints(x)                         (IpoptAdapter::eval_g)     -> eval_g(x)
+  GetJacobianOfConstraints structure         (eval_jac_g, values=NULL)  -> jac_structure()
+  EvalNonzerosOfJacobian(x)                  (eval_jac_g, values!=NULL) -> eval_jac_values(x)
+plus the batched, device-resident entry point used by bench.py.
+
+Every evaluation runs on the GPU through libtowr_gpu.so; there is no CPU path. A missing or
+unloadable extension raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _capi as capi
+
+
+class TowrGpuError(RuntimeError):
+    pass
+
+
+class TowrGpuProblem:
+    def __init__(self, desc: capi.ProblemDesc, device: int = 0):
+        self._lib = capi.load_library()
+        self.desc = desc
+        h = C.c_void_p()
+        rc = self._lib.towr_gpu_create(C.byref(desc), device, C.byref(h))
+        if rc != capi.TOWR_OK:
+            raise TowrGpuError(f"towr_gpu_create failed ({rc}): {self._lib.towr_gpu_last_error(None).decode()}")
+        self._h = h
+        n, m, nnz = C.c_int32(), C.c_int32(), C.c_int64()
+        self._check(self._lib.towr_gpu_sizes(h, C.byref(n), C.byref(m), C.byref(nnz)))
+        self.n, self.m, self.nnz = n.value, m.value, nnz.value
+
+    def _check(self, rc):
+        if rc != capi.TOWR_OK:
+            raise TowrGpuError(f"towr_gpu error {rc}: {self._lib.towr_gpu_last_error(self._h).decode()}")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.towr_gpu_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -------------------------------------------------------------------- structure ----------
+    def sizes(self):
+        return self.n, self.m, self.nnz
+
+    def initial_x(self) -> np.ndarray:
+        x = np.zeros(self.n)
+        self._check(self._lib.towr_gpu_initial_x(self._h, capi.dptr(x)))
+        return x
+
+    def initial_x_for(self, init: capi.InitDesc, terrain: capi.Terrain) -> np.ndarray:
+        """x0 of another start/goal/terrain instance on this layout (batch harness)."""
+        x = np.zeros(self.n)
+        self._check(self._lib.towr_gpu_initial_x_for(self._h, C.byref(init), C.byref(terrain), capi.dptr(x)))
+        return x
+
+    def varset_info(self):
+        out = []
+        for i in range(self.desc.n_varsets):
+            k, e, c0, n = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int32()
+            self._check(self._lib.towr_gpu_varset_info(self._h, i, C.byref(k), C.byref(e), C.byref(c0), C.byref(n)))
+            out.append((k.value, e.value, c0.value, n.value))
+        return out
+
+    def jac_structure(self):
+        r = np.zeros(self.nnz, dtype=np.int32)
+        c = np.zeros(self.nnz, dtype=np.int32)
+        self._check(self._lib.towr_gpu_jac_structure(self._h, capi.iptr(r), capi.iptr(c)))
+        return r, c
+
+    def jac_csr(self):
+        rp = np.zeros(self.m + 1, dtype=np.int64)
+        c = np.zeros(self.nnz, dtype=np.int32)
+        self._check(self._lib.towr_gpu_jac_csr(self._h, capi.lptr(rp), capi.iptr(c)))
+        return rp, c
+
+    # -------------------------------------------------------------------- evaluation ---------
+    def eval_g(self, x) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        g = np.zeros(self.m)
+        self._check(self._lib.towr_gpu_eval_g(self._h, capi.dptr(x), capi.dptr(g)))
+        return g
+
+    def eval_jac_values(self, x) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        v = np.zeros(self.nnz)
+        self._check(self._lib.towr_gpu_eval_jac_values(self._h, capi.dptr(x), capi.dptr(v)))
+        return v
+
+    def eval_g_jac(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        g, v = np.zeros(self.m), np.zeros(self.nnz)
+        self._check(self._lib.towr_gpu_eval_g_jac(self._h, capi.dptr(x), capi.dptr(g), capi.dptr(v)))
+        return g, v
+
+    def set_batch_terrain(self, terrains):
+        arr = (capi.Terrain * len(terrains))(*terrains)
+        self._check(self._lib.towr_gpu_set_batch_terrain(self._h, len(terrains), arr))
+
+    def eval_batch(self, X):
+        """Host batch: X (B, n) -> G (B, m), V (B, nnz)."""
+        X = np.ascontiguousarray(X, dtype=np.float64)
+        B = X.shape[0]
+        G, V = np.zeros((B, self.m)), np.zeros((B, self.nnz))
+        self._check(self._lib.towr_gpu_eval_batch(self._h, B, capi.dptr(X), capi.dptr(G), capi.dptr(V)))
+        return G, V
+
+    def eval_batch_device(self, X, G, V, want_g=True, want_jac=True, stream=None):
+        """Device batch on torch CUDA (HIP) tensors: X (B, ldx), G (B, ldg), V (B, ldv) float64.
+        `stream`: a torch.cuda.Stream (default: torch's current stream)."""
+        import torch
+        B = X.shape[0]
+        if stream is None:
+            stream = torch.cuda.current_stream(X.device)
+        self._check(self._lib.towr_gpu_eval_batch_device(
+            self._h, B, C.c_void_p(X.data_ptr()), X.stride(0),
+            C.c_void_p(G.data_ptr()), G.stride(0), C.c_void_p(V.data_ptr()), V.stride(0),
+            int(want_g), int(want_jac), C.c_void_p(stream.cuda_stream)))
+
+    def set_tiles_per_block(self, t: int):
+        self._check(self._lib.towr_gpu_set_tiles_per_block(self._h, t))
+
+    def algorithmic_bytes_per_call(self) -> int:
+        return int(self._lib.towr_gpu_algorithmic_bytes_per_call(self._h))
