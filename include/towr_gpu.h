@@ -197,7 +197,8 @@ int towr_gpu_eval_g_jac(towr_gpu_handle h, const double* x, double* g, double* v
 int towr_gpu_set_batch_terrain(towr_gpu_handle h, int32_t B, const towr_terrain_t* terrains);
 
 /* Device-resident batch: X[b*ldx + j], G[b*ldg + i], V[b*ldv + k] are DEVICE pointers (HBM);
- * `stream` is a hipStream_t (NULL = the handle's stream). want_g / want_jac select outputs.
+ * `stream` is the hipStream_t to launch on (NULL = HIP's default stream, as in the HIP API).
+ * want_g / want_jac select outputs.
  * Asynchronous with respect to the host.                                                         */
 int towr_gpu_eval_batch_device(towr_gpu_handle h, int32_t B,
                                const double* X, int64_t ldx,
@@ -207,6 +208,16 @@ int towr_gpu_eval_batch_device(towr_gpu_handle h, int32_t B,
 
 /* Host batch (H2D of X, D2H of G and V through pinned staging; contiguous lds = n, m, nnz).      */
 int towr_gpu_eval_batch(towr_gpu_handle h, int32_t B, const double* X, double* G, double* V);
+
+/* The engine launches one kernel per constraint kind ("kernel" 0..towr_gpu_num_kernels()-1).
+ * For roofline accounting: its name, tile count, and algorithmic bytes per problem (CSR values
+ * and g rows written + distinct x entries read), and a launch of that kernel alone.             */
+int towr_gpu_kernel_info(towr_gpu_handle h, int32_t kernel, const char** name, int32_t* n_tiles,
+                         int64_t* bytes_per_problem);
+int towr_gpu_eval_batch_device_kernel(towr_gpu_handle h, int32_t kernel, int32_t B,
+                                      const double* X, int64_t ldx, double* G, int64_t ldg,
+                                      double* V, int64_t ldv, void* stream);
+int towr_gpu_num_kernels(void);
 
 /* Sets the launch geometry (tiles per workgroup); 0 = automatic. For benchmarking.              */
 int towr_gpu_set_tiles_per_block(towr_gpu_handle h, int32_t tiles_per_block);

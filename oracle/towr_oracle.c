@@ -1723,3 +1723,60 @@ double oracle_bench(const towr_problem_desc_t* d, int threads, int calls_per_thr
   if (calls_done) *calls_done = total;
   return t1 - t0;
 }
+
+/* ------------------------------------------------------------- unit-level KAT entry points -- */
+/* Hermite polynomial state at t and the 3x4 basis (d{pos,vel,acc}/d{n0.p,n0.v,n1.p,n1.v}),
+ * via CubicHermitePolynomial::UpdateCoeff/GetPoint/GetDerivativeWrt{Start,End}Node.           */
+void oracle_kat_hermite(double T, double t, const double n0[2], const double n1[2], double state[3], double basis[12]) {
+  Poly p; memset(&p, 0, sizeof p);
+  p.T = T;
+  p.n0[kPos][0] = n0[0]; p.n0[kVel][0] = n0[1]; p.n1[kPos][0] = n1[0]; p.n1[kVel][0] = n1[1];
+  poly_update_coeff(&p);
+  double st[3][3]; poly_get_point(&p, t, st);
+  for (int d = 0; d < 3; ++d) state[d] = st[d][0];
+  for (int d = 0; d < 3; ++d) {
+    basis[4 * d + 0] = poly_d_start(&p, d, kPos, t); basis[4 * d + 1] = poly_d_start(&p, d, kVel, t);
+    basis[4 * d + 2] = poly_d_end(&p, d, kPos, t);   basis[4 * d + 3] = poly_d_end(&p, d, kVel, t);
+  }
+}
+/* d pos / d T of the Hermite polynomial (GetDerivativeOfPosWrtDuration) */
+double oracle_kat_hermite_dT(double T, double t, const double n0[2], const double n1[2]) {
+  Poly p; memset(&p, 0, sizeof p);
+  p.T = T;
+  p.n0[kPos][0] = n0[0]; p.n0[kVel][0] = n0[1]; p.n1[kPos][0] = n1[0]; p.n1[kVel][0] = n1[1];
+  poly_update_coeff(&p);
+  double o[3]; poly_d_pos_wrt_duration(&p, t, o);
+  return o[0];
+}
+/* Euler ZYX: R (row-major), omega = M thd, omega_dot = Mdot thd + M thdd */
+void oracle_kat_euler(const double th[3], const double thd[3], const double thdd[3], double R[9], double w[3], double wd[3]) {
+  double Rm[3][3]; euler_R(th, Rm); memcpy(R, Rm, sizeof Rm);
+  spmat M = eu_M(th), Md = eu_Mdot(th, thd);
+  double a[3], b[3];
+  sp_mul_vec(&M, thd, w); sp_mul_vec(&Md, thd, a); sp_mul_vec(&M, thdd, b);
+  for (int k = 0; k < 3; ++k) wd[k] = a[k] + b[k];
+  sp_free(&M); sp_free(&Md);
+}
+/* SingleRigidBodyDynamics::GetDynamicViolation for n_ee contacts */
+void oracle_kat_srbd(double m, double g, const double inertia[6], int n_ee, const double com[3], const double com_acc[3],
+                     const double th[3], const double thd[3], const double thdd[3],
+                     const double* f, const double* p, const double* tau, double out[6]) {
+  Model M; memset(&M, 0, sizeof M);
+  M.m = m; M.g = g; M.n_ee = n_ee;
+  const double* I = inertia;
+  double Ib[9] = {I[0], -I[3], -I[4], -I[3], I[1], -I[5], -I[4], -I[5], I[2]};
+  M.I_b = sp_from_dense(3, 3, Ib, 0);
+  memcpy(M.com_pos, com, sizeof(double[3])); memcpy(M.com_acc, com_acc, sizeof(double[3]));
+  double R9[9], w[3], wd[3];
+  oracle_kat_euler(th, thd, thdd, R9, w, wd);
+  memcpy(M.R, R9, sizeof R9); memcpy(M.omega, w, sizeof w); memcpy(M.omega_dot, wd, sizeof wd);
+  for (int e = 0; e < n_ee; ++e) for (int k = 0; k < 3; ++k) { M.f[e][k] = f[3 * e + k]; M.p[e][k] = p[3 * e + k]; M.tau[e][k] = tau[3 * e + k]; }
+  model_violation(&M, out);
+  sp_free(&M.I_b);
+}
+/* HeightMap: h, dh/dx, dh/dy, normalized basis (3x3, rows n t1 t2), d basis / d{x,y} (2x3x3) */
+void oracle_kat_terrain(const towr_terrain_t* T, double x, double y, double out_h[3], double basis[9], double dbasis[18]) {
+  out_h[0] = ter_h(T, x, y); out_h[1] = ter_dh(T, X, x, y); out_h[2] = ter_dh(T, Y, x, y);
+  for (int b = 0; b < 3; ++b) ter_nbasis(T, b, x, y, basis + 3 * b);
+  for (int d = 0; d < 2; ++d) for (int b = 0; b < 3; ++b) ter_d_nbasis(T, b, d, x, y, dbasis + 9 * d + 3 * b);
+}

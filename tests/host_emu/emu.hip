@@ -10,10 +10,10 @@ using namespace tg;
 
 namespace {
 struct AccEmit {
-  const int32_t* slot; int j; double* v; double* gout;
+  const int32_t* slot; int stride; int j; double* v; double* gout;
   void g(int row, double val) { gout[row] = val; }
-  void operator()(int, int col, double val, bool) {
-    if (col >= 0) { int s = slot[j]; if (s >= 0) v[s] += val; }
+  void operator()(int, int, double val, bool) {
+    int s = slot[j * stride]; if (s >= 0) v[s] += val;
     ++j;
   }
 };
@@ -29,7 +29,9 @@ extern "C" int emu_eval(const towr_problem_desc_t* d, const double* x, double* g
   c.x = x; c.nodecol = L.nodecol.data(); c.spl = L.spl.data(); c.dur = L.dur.data();
   c.ter = &L.terrain; c.rb = L.rb; c.fdisc_motion = L.fdisc_motion;
   for (const ItemDesc& it : L.items) {
-    AccEmit em{L.slots.data() + it.slot, 0, v, g};
+    if (it.type == IT_NONE) continue;
+    AccEmit em{L.slots.data() + it.slot, L.type_block[it.type], 0, v, g};
+    c.seg = it.seg >= 0 ? L.segs.data() + (size_t)it.seg * L.spl.size() : nullptr;
     eval_item(c, it, em);
   }
   return 0;

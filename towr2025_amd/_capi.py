@@ -107,6 +107,10 @@ SYMBOLS = {
                                               C.c_void_p, C.c_int64, C.c_void_p, C.c_int64,
                                               C.c_int32, C.c_int32, C.c_void_p]),
     "towr_gpu_eval_batch": (C.c_int, [_HANDLE, C.c_int32, _DP, _DP, _DP]),
+    "towr_gpu_kernel_info": (C.c_int, [_HANDLE, C.c_int32, C.POINTER(C.c_char_p), _IP, _LP]),
+    "towr_gpu_eval_batch_device_kernel": (C.c_int, [_HANDLE, C.c_int32, C.c_int32, C.c_void_p, C.c_int64,
+                                                     C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p]),
+    "towr_gpu_num_kernels": (C.c_int, []),
     "towr_gpu_set_tiles_per_block": (C.c_int, [_HANDLE, C.c_int32]),
     "towr_gpu_algorithmic_bytes_per_call": (C.c_int64, [_HANDLE]),
 }
@@ -124,6 +128,12 @@ def load_library(path: str = LIB_PATH):
     if not os.path.exists(path):
         raise RuntimeError(
             f"towr2025_amd: HIP extension not built ({path} missing). Run __graft_entry__.build().")
+    # One HIP runtime per process: torch bundles libamdhip64.so.7 (same SONAME as /opt/rocm's);
+    # whichever loads first serves everyone, so when torch is present let its runtime load first.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(path)
     for name, (res, args) in SYMBOLS.items():
         fn = getattr(lib, name)

@@ -36,6 +36,7 @@ TG_HD int sp_torque(int ee) { return 2 + 4 * ee + 3; }
 
 // work item types
 enum ItemType {
+  IT_NONE = -1,  // padding lane of a tile
   IT_DYN = 0,    // DynamicConstraint instant; group 0: base-lin + g, 1: base-ang, 2+ee: ee blocks
   IT_ROM = 1,    // RangeOfMotionConstraint instant; group 0: base-lin + g, 1: base-ang, 2: motion
   IT_FDISC = 2,  // ForceConstraintDiscretized instant
@@ -61,18 +62,29 @@ struct RobotC {
   int32_t n_ee, reserved;
 };
 
-// 48-byte work-item descriptor, shared by all problems of a batch
+// 64-byte work-item descriptor, shared by all problems of a batch
 struct ItemDesc {
   int32_t type, group, ee, k;   // k: instance index inside the constraint set
   int32_t row0;                 // global row of the item's first row
   int32_t a0, a1;               // node ids (FNODE: force node, motion node at phase start; ...)
-  int32_t slot;                 // first candidate's index into the slot table
+  int32_t slot;                 // candidate j of this item is slot_table[slot + j * stride]
+  int32_t seg;                  // row of the segment table (time-discretised items), else -1
+  int32_t ncand;                // number of candidates the item emits
+  int32_t reserved[2];
   double t;                     // time of the instant (time-discretised sets)
-  double p0;                    // scalar parameter (safety distance, t_swing_avg, T_poly, ...)
+  double p0;                    // scalar parameter (safety distance, t_swing_avg, ...)
+};
+
+// Spline::GetLocalTime result of one spline at one instant (precomputed on the host for fixed
+// polynomial durations: the reference's scan, spline.cc:48-78, run once at setup)
+struct SegRec {
+  double tl, T;
+  int32_t poly, reserved;
 };
 
 struct Ctx {
-  const double* x;              // this problem's decision vector (LDS on the device)
+  const SegRec* seg;            // this item's segment row (one SegRec per spline), or nullptr
+  const double* x;              // this problem's decision vector
   const int32_t* nodecol;       // node value -> global column of x, or -1 (constant 0)
   const SplineMeta* spl;
   const double* dur;            // polynomial durations
@@ -116,6 +128,23 @@ TG_HD int basis_col(const Ctx& c, int s, int poly, int b, int e) {
 
 // CubicHermitePolynomial::UpdateCoeff (:97-104) + Polynomial::GetPoint (:47-58)
 TG_HD void poly_state(const Ctx& c, int s, int poly, double T, double tl, SplinePt& o) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+  // Host structure pass: the reference's own operation order (std::pow, sum over coefficients),
+  // so that data-dependent structure predicates (ForceConstraintDiscretized's `scale == 0.0`,
+  // force_constraint_discretized.cc:58) resolve floating-point ties exactly as the source does.
+  for (int e = 0; e < 3; ++e) {
+    const double p0 = xval(c, node_col(c, s, poly, kPos, e)), v0 = xval(c, node_col(c, s, poly, kVel, e));
+    const double p1 = xval(c, node_col(c, s, poly + 1, kPos, e)), v1 = xval(c, node_col(c, s, poly + 1, kVel, e));
+    const double cf[4] = {p0, v0, -(3 * (p0 - p1) + T * (2 * v0 + v1)) / pow(T, 2),
+                          (2 * (p0 - p1) + T * (v0 + v1)) / pow(T, 3)};
+    double pp = 0.0, vv = 0.0, aa = 0.0;
+    for (int k = 0; k < 4; ++k) pp += pow(tl, k) * cf[k];
+    for (int k = 0; k < 4; ++k) vv += (k >= 1 ? k * pow(tl, k - 1) : 0.0) * cf[k];
+    for (int k = 0; k < 4; ++k) aa += (k >= 2 ? k * (k - 1) * pow(tl, k - 2) : 0.0) * cf[k];
+    o.p[e] = pp; o.v[e] = vv; o.a[e] = aa;
+  }
+  return;
+#endif
   const double T2 = T * T, T3 = T2 * T, t2 = tl * tl, t3 = t2 * tl;
   for (int e = 0; e < 3; ++e) {
     const double p0 = xval(c, node_col(c, s, poly, kPos, e)), v0 = xval(c, node_col(c, s, poly, kVel, e));
@@ -131,9 +160,14 @@ TG_HD void poly_state(const Ctx& c, int s, int poly, double T, double tl, Spline
 
 // Spline::GetPoint(t_global) (spline.cc:80-93)
 TG_HD void spline_eval(const Ctx& c, int s, double t, SplinePt& o) {
-  const SplineMeta m = c.spl[s];
-  o.poly = seg_lookup(c.dur + m.dur_off, m.n_polys, t, &o.tl);
-  o.T = c.dur[m.dur_off + o.poly];
+  if (c.seg) {
+    const SegRec r = c.seg[s];
+    o.poly = r.poly; o.tl = r.tl; o.T = r.T;
+  } else {
+    const SplineMeta m = c.spl[s];
+    o.poly = seg_lookup(c.dur + m.dur_off, m.n_polys, t, &o.tl);
+    o.T = c.dur[m.dur_off + o.poly];
+  }
   poly_state(c, s, o.poly, o.T, o.tl, o);
 }
 
@@ -177,52 +211,35 @@ TG_HD void euler_R(const Trig& q, double R[3][3]) {
   R[1][0] = q.cy * q.sz; R[1][1] = q.cx * q.cz + q.sx * q.sy * q.sz; R[1][2] = q.cx * q.sy * q.sz - q.cz * q.sx;
   R[2][0] = -q.sy;       R[2][1] = q.cy * q.sx;                       R[2][2] = q.cx * q.cy;
 }
-// dR[e][i][j] = d R[i][j] / d theta_e  (GetDerivativeOfRotationMatrixWrtNodes, :241-268)
-TG_HD void euler_dR(const Trig& q, double dR[3][3][3]) {
+// dR[i][j] = d R[i][j] / d theta_e for one Euler axis e (GetDerivativeOfRotationMatrixWrtNodes :241-268)
+TG_HD void euler_dR_axis(const Trig& q, int e, double dR[3][3]) {
   const double sx = q.sx, cx = q.cx, sy = q.sy, cy = q.cy, sz = q.sz, cz = q.cz;
-  // wrt x (roll)
-  dR[0][0][0] = 0.0; dR[0][0][1] = sx * sz + cx * cz * sy; dR[0][0][2] = cx * sz - cz * sx * sy;
-  dR[0][1][0] = 0.0; dR[0][1][1] = cx * sy * sz - cz * sx; dR[0][1][2] = -cx * cz - sx * sy * sz;
-  dR[0][2][0] = 0.0; dR[0][2][1] = cx * cy;                dR[0][2][2] = -cy * sx;
-  // wrt y (pitch)
-  dR[1][0][0] = -cz * sy; dR[1][0][1] = cy * cz * sx; dR[1][0][2] = cx * cy * cz;
-  dR[1][1][0] = -sy * sz; dR[1][1][1] = cy * sx * sz; dR[1][1][2] = cx * cy * sz;
-  dR[1][2][0] = -cy;      dR[1][2][1] = -sx * sy;     dR[1][2][2] = -cx * sy;
-  // wrt z (yaw)
-  dR[2][0][0] = -cy * sz; dR[2][0][1] = -cx * cz - sx * sy * sz; dR[2][0][2] = cz * sx - cx * sy * sz;
-  dR[2][1][0] = cy * cz;  dR[2][1][1] = cz * sx * sy - cx * sz;  dR[2][1][2] = sx * sz + cx * cz * sy;
-  dR[2][2][0] = 0.0;      dR[2][2][1] = 0.0;                     dR[2][2][2] = 0.0;
+  if (e == 0) {
+    dR[0][0] = 0.0; dR[0][1] = sx * sz + cx * cz * sy; dR[0][2] = cx * sz - cz * sx * sy;
+    dR[1][0] = 0.0; dR[1][1] = cx * sy * sz - cz * sx; dR[1][2] = -cx * cz - sx * sy * sz;
+    dR[2][0] = 0.0; dR[2][1] = cx * cy;                dR[2][2] = -cy * sx;
+  } else if (e == 1) {
+    dR[0][0] = -cz * sy; dR[0][1] = cy * cz * sx; dR[0][2] = cx * cy * cz;
+    dR[1][0] = -sy * sz; dR[1][1] = cy * sx * sz; dR[1][2] = cx * cy * sz;
+    dR[2][0] = -cy;      dR[2][1] = -sx * sy;     dR[2][2] = -cx * sy;
+  } else {
+    dR[0][0] = -cy * sz; dR[0][1] = -cx * cz - sx * sy * sz; dR[0][2] = cz * sx - cx * sy * sz;
+    dR[1][0] = cy * cz;  dR[1][1] = cz * sx * sy - cx * sz;  dR[1][2] = sx * sz + cx * cz * sy;
+    dR[2][0] = 0.0;      dR[2][1] = 0.0;                     dR[2][2] = 0.0;
+  }
 }
 
-// M (GetM :133-148), Mdot (GetMdot :150-166) as dense 3x3; dM[e] = dM/dtheta_e, dMd[e] = dMdot/dtheta_e
-struct EulerKin {
-  double M[3][3], Md[3][3], dM[3][3][3], dMd[3][3][3];
-  double w[3], wd[3];   // omega = M thd, omega_dot = Md thd + M thdd (:58-83)
-};
-TG_HD void euler_kin(const Trig& q, const double thd[3], const double thdd[3], EulerKin& k) {
-  const double sy = q.sy, cy = q.cy, sz = q.sz, cz = q.cz, yd = thd[1], zd = thd[2];
-  for (int a = 0; a < 3; ++a)
-    for (int b = 0; b < 3; ++b) {
-      k.M[a][b] = 0.0; k.Md[a][b] = 0.0;
-      for (int e = 0; e < 3; ++e) { k.dM[e][a][b] = 0.0; k.dMd[e][a][b] = 0.0; }
-    }
-  k.M[0][0] = cy * cz; k.M[0][1] = -sz;
-  k.M[1][0] = cy * sz; k.M[1][1] = cz;
-  k.M[2][0] = -sy;     k.M[2][2] = 1.0;
-  k.Md[0][0] = -cz * sy * yd - cy * sz * zd; k.Md[0][1] = -cz * zd;
-  k.Md[1][0] = cy * cz * zd - sy * sz * yd;  k.Md[1][1] = -sz * zd;
-  k.Md[2][0] = -cy * yd;
-  // dM / dy, dM / dz (GetDerivMwrtNodes :168-198)
-  k.dM[1][0][0] = -sy * cz; k.dM[1][1][0] = -sy * sz; k.dM[1][2][0] = -cy;
-  k.dM[2][0][0] = -cy * sz; k.dM[2][1][0] = cy * cz;  k.dM[2][0][1] = -cz; k.dM[2][1][1] = -sz;
-  // dMdot / dy, dMdot / dz (GetDerivMdotwrtNodes :270-304, position part)
-  k.dMd[1][0][0] = -cy * cz * yd + sy * sz * zd; k.dMd[1][1][0] = -cy * sz * yd - sy * cz * zd; k.dMd[1][2][0] = sy * yd;
-  k.dMd[2][0][0] = sy * sz * yd - cy * cz * zd;  k.dMd[2][1][0] = -sy * cz * yd - cy * sz * zd;
-  k.dMd[2][0][1] = sz * zd;                      k.dMd[2][1][1] = -cz * zd;
-  for (int a = 0; a < 3; ++a) {
-    k.w[a] = k.M[a][0] * thd[0] + k.M[a][1] * thd[1] + k.M[a][2] * thd[2];
-    k.wd[a] = (k.Md[a][0] * thd[0] + k.Md[a][1] * thd[1] + k.Md[a][2] * thd[2])
-            + (k.M[a][0] * thdd[0] + k.M[a][1] * thdd[1] + k.M[a][2] * thdd[2]);
+// omega = M thd, omega_dot = Mdot thd + M thdd (GetAngularVelocityInWorld / ...AccelerationInWorld,
+// euler_converter.cc:58-83 with GetM :133-148, GetMdot :150-166)
+TG_HD void euler_w_wd(const Trig& q, const double thd[3], const double thdd[3], double w[3], double wd[3]) {
+  const double sy = q.sy, cy = q.cy, sz = q.sz, cz = q.cz, xd = thd[0], yd = thd[1], zd = thd[2];
+  const double M0[3] = {cy * cz, cy * sz, -sy}, M1[3] = {-sz, cz, 0.0};
+  const double Md0[3] = {-cz * sy * yd - cy * sz * zd, cy * cz * zd - sy * sz * yd, -cy * yd};
+  const double Md1[3] = {-cz * zd, -sz * zd, 0.0};
+  for (int i = 0; i < 3; ++i) {
+    const double M2i = i == 2 ? 1.0 : 0.0;
+    w[i] = M0[i] * xd + M1[i] * yd + M2i * zd;
+    wd[i] = (Md0[i] * xd + Md1[i] * yd) + (M0[i] * thdd[0] + M1[i] * thdd[1] + M2i * thdd[2]);
   }
 }
 
@@ -386,8 +403,9 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
     SplinePt A; spline_eval(c, SP_BASE_ANG, t, A);
     const Trig q = trig(A.p);
     double R[3][3]; euler_R(q, R);
-    EulerKin k; euler_kin(q, A.v, A.a, k);
+    double w[3], wd[3]; euler_w_wd(q, A.v, A.a, w, wd);
     double fs[3] = {0, 0, 0}, ts[3] = {0, 0, 0};
+#pragma unroll 1
     for (int ee = 0; ee < E; ++ee) {
       SplinePt F, Tq, P;
       spline_eval(c, sp_force(ee), t, F);
@@ -404,7 +422,7 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
     for (int i = 0; i < 3; ++i)
       for (int j = 0; j < 3; ++j) Iw[i][j] = RI[i][0] * R[j][0] + RI[i][1] * R[j][1] + RI[i][2] * R[j][2];
     double a[3], Iww[3], b[3];
-    mat3_vec(Iw, k.wd, a); mat3_vec(Iw, k.w, Iww); cross3(k.w, Iww, b);
+    mat3_vec(Iw, wd, a); mat3_vec(Iw, w, Iww); cross3(w, Iww, b);
     for (int e = 0; e < 3; ++e) em.g(r0 + AX + e, a[e] + b[e] - ts[e]);
     const double grav[3] = {0.0, 0.0, -c.rb.m * c.rb.g};
     for (int e = 0; e < 3; ++e) em.g(r0 + LX + e, c.rb.m * L.a[e] - fs[e] - grav[e]);
@@ -421,54 +439,78 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
     return;
   }
   if (it.group == 1) {
-    // d/d base-ang (GetJacobianWrtBaseAng :124-166), chain rule through theta, theta_dot, theta_ddot
+    // d/d base-ang (GetJacobianWrtBaseAng :124-166): chain rule through (theta, theta_dot,
+    // theta_ddot) of the Euler spline, one Euler axis e at a time to keep the live set small.
+    //   A(.) = I_w wd + w x (I_w w);  I_w = R I_b R^T,  w = M thd,  wd = Mdot thd + M thdd
     SplinePt A; spline_eval(c, SP_BASE_ANG, t, A);
     const Trig q = trig(A.p);
-    double R[3][3], dR[3][3][3];
-    euler_R(q, R); euler_dR(q, dR);
-    EulerKin k; euler_kin(q, A.v, A.a, k);
+    const double sy = q.sy, cy = q.cy, sz = q.sz, cz = q.cz;
+    const double xd = A.v[0], yd = A.v[1], zd = A.v[2];
+    double R[3][3]; euler_R(q, R);
+    // M columns (GetM :133-148) and Mdot columns (GetMdot :150-166)
+    const double M0[3] = {cy * cz, cy * sz, -sy}, M1[3] = {-sz, cz, 0.0};
+    const double Md0[3] = {-cz * sy * yd - cy * sz * zd, cy * cz * zd - sy * sz * yd, -cy * yd};
+    const double Md1[3] = {-cz * zd, -sz * zd, 0.0};
+    double w[3], wd[3];
+    for (int i = 0; i < 3; ++i) {
+      const double M2i = i == 2 ? 1.0 : 0.0;
+      w[i] = M0[i] * xd + M1[i] * yd + M2i * zd;
+      wd[i] = (Md0[i] * xd + Md1[i] * yd) + (M0[i] * A.a[0] + M1[i] * A.a[1] + M2i * A.a[2]);
+    }
     double RI[3][3], Iw[3][3];
     for (int i = 0; i < 3; ++i)
       for (int j = 0; j < 3; ++j) RI[i][j] = R[i][0] * c.rb.Ib[0 * 3 + j] + R[i][1] * c.rb.Ib[1 * 3 + j] + R[i][2] * c.rb.Ib[2 * 3 + j];
     for (int i = 0; i < 3; ++i)
       for (int j = 0; j < 3; ++j) Iw[i][j] = RI[i][0] * R[j][0] + RI[i][1] * R[j][1] + RI[i][2] * R[j][2];
-    double Iww[3]; mat3_vec(Iw, k.w, Iww);
-    double Ap[3][3], Av[3][3], Aa[3][3];   // [row][e]
-    for (int e = 0; e < 3; ++e) {
-      // dI_w/dtheta_e = dR_e I_b R^T + R I_b dR_e^T
-      double dRI[3][3], dIw[3][3];
-      for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) dRI[i][j] = dR[e][i][0] * c.rb.Ib[0 * 3 + j] + dR[e][i][1] * c.rb.Ib[1 * 3 + j] + dR[e][i][2] * c.rb.Ib[2 * 3 + j];
-      for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j)
-          dIw[i][j] = (dRI[i][0] * R[j][0] + dRI[i][1] * R[j][1] + dRI[i][2] * R[j][2])
-                    + (RI[i][0] * dR[e][j][0] + RI[i][1] * dR[e][j][1] + RI[i][2] * dR[e][j][2]);
-      double dw[3], dwd[3], t1[3], t2[3], t3[3], t4[3], t5[3], t6[3];
-      mat3_vec(k.dM[e], A.v, dw);
-      mat3_vec(k.dMd[e], A.v, t1); mat3_vec(k.dM[e], A.a, t2);
-      for (int i = 0; i < 3; ++i) dwd[i] = t1[i] + t2[i];
-      mat3_vec(dIw, k.wd, t1);              // dI_w wd
-      mat3_vec(Iw, dwd, t2);                // I_w dwd
-      cross3(dw, Iww, t3);                  // dw x (I_w w)
-      mat3_vec(dIw, k.w, t4); mat3_vec(Iw, dw, t5);
-      for (int i = 0; i < 3; ++i) t4[i] += t5[i];
-      cross3(k.w, t4, t6);                  // w x (dI_w w + I_w dw)
-      for (int i = 0; i < 3; ++i) Ap[i][e] = t1[i] + t2[i] + t3[i] + t6[i];
-      // theta_dot_e: dw = M[:,e], dwd = dM_e thd + Md[:,e]
-      double Me[3] = {k.M[0][e], k.M[1][e], k.M[2][e]}, dwv[3];
-      mat3_vec(k.dM[e], A.v, dwv);
-      for (int i = 0; i < 3; ++i) dwv[i] += k.Md[i][e];
-      mat3_vec(Iw, dwv, t1); cross3(Me, Iww, t3); mat3_vec(Iw, Me, t5); cross3(k.w, t5, t6);
-      for (int i = 0; i < 3; ++i) Av[i][e] = t1[i] + t3[i] + t6[i];
-      // theta_ddot_e: dwd = M[:,e]
-      for (int i = 0; i < 3; ++i) Aa[i][e] = t5[i];
-    }
+    double Iww[3]; mat3_vec(Iw, w, Iww);
     double Hp[4], Hv[4], Ha[4];
     hermite_dpos(A.T, A.tl, Hp); hermite_dvel(A.T, A.tl, Hv); hermite_dacc(A.T, A.tl, Ha);
-    for (int r = 0; r < 3; ++r)
-      for (int e = 0; e < 3; ++e)
+#pragma unroll 1
+    for (int e = 0; e < 3; ++e) {
+      double dR[3][3]; euler_dR_axis(q, e, dR);
+      // dw = dM_e thd; dwd = dMdot_e thd + dM_e thdd (GetDerivMwrtNodes :168-198, GetDerivMdotwrtNodes :270-304)
+      double dw[3] = {0.0, 0.0, 0.0}, dwd[3] = {0.0, 0.0, 0.0};
+      if (e == 1) {
+        const double dM0[3] = {-sy * cz, -sy * sz, -cy};
+        const double dMd0[3] = {-cy * cz * yd + sy * sz * zd, -cy * sz * yd - sy * cz * zd, sy * yd};
+        for (int i = 0; i < 3; ++i) { dw[i] = dM0[i] * xd; dwd[i] = dMd0[i] * xd + dM0[i] * A.a[0]; }
+      } else if (e == 2) {
+        const double dM0[3] = {-cy * sz, cy * cz, 0.0}, dM1[3] = {-cz, -sz, 0.0};
+        const double dMd0[3] = {sy * sz * yd - cy * cz * zd, -sy * cz * yd - cy * sz * zd, 0.0};
+        const double dMd1[3] = {sz * zd, -cz * zd, 0.0};
+        for (int i = 0; i < 3; ++i) {
+          dw[i] = dM0[i] * xd + dM1[i] * yd;
+          dwd[i] = (dMd0[i] * xd + dMd1[i] * yd) + (dM0[i] * A.a[0] + dM1[i] * A.a[1]);
+        }
+      }
+      // dI_w/dtheta_e = dR I_b R^T + R I_b dR^T, applied to wd and w
+      double dRI[3][3];
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) dRI[i][j] = dR[i][0] * c.rb.Ib[0 * 3 + j] + dR[i][1] * c.rb.Ib[1 * 3 + j] + dR[i][2] * c.rb.Ib[2 * 3 + j];
+      double dIwd[3], dIw_w[3];
+      {
+        double u[3], v[3];   // R^T wd, dR^T wd (and the same for w)
+        for (int j = 0; j < 3; ++j) { u[j] = R[0][j] * wd[0] + R[1][j] * wd[1] + R[2][j] * wd[2]; v[j] = dR[0][j] * wd[0] + dR[1][j] * wd[1] + dR[2][j] * wd[2]; }
+        for (int i = 0; i < 3; ++i) dIwd[i] = (dRI[i][0] * u[0] + dRI[i][1] * u[1] + dRI[i][2] * u[2]) + (RI[i][0] * v[0] + RI[i][1] * v[1] + RI[i][2] * v[2]);
+        for (int j = 0; j < 3; ++j) { u[j] = R[0][j] * w[0] + R[1][j] * w[1] + R[2][j] * w[2]; v[j] = dR[0][j] * w[0] + dR[1][j] * w[1] + dR[2][j] * w[2]; }
+        for (int i = 0; i < 3; ++i) dIw_w[i] = (dRI[i][0] * u[0] + dRI[i][1] * u[1] + dRI[i][2] * u[2]) + (RI[i][0] * v[0] + RI[i][1] * v[1] + RI[i][2] * v[2]);
+      }
+      double Ap[3], Av[3], Aa[3], t1[3], t2[3], t3[3];
+      // theta_e: dI_w wd + I_w dwd + dw x (I_w w) + w x (dI_w w + I_w dw)
+      mat3_vec(Iw, dwd, t1); cross3(dw, Iww, t2); mat3_vec(Iw, dw, t3);
+      for (int i = 0; i < 3; ++i) t3[i] += dIw_w[i];
+      double t4[3]; cross3(w, t3, t4);
+      for (int i = 0; i < 3; ++i) Ap[i] = dIwd[i] + t1[i] + t2[i] + t4[i];
+      // theta_dot_e: dw = M[:,e], dwd = dM_e thd + Mdot[:,e]
+      const double Me[3] = {e == 0 ? M0[0] : e == 1 ? M1[0] : 0.0, e == 0 ? M0[1] : e == 1 ? M1[1] : 0.0, e == 0 ? M0[2] : e == 1 ? M1[2] : 1.0};
+      double dwv[3];
+      for (int i = 0; i < 3; ++i) dwv[i] = dw[i] + (e == 0 ? Md0[i] : e == 1 ? Md1[i] : 0.0);
+      mat3_vec(Iw, dwv, t1); cross3(Me, Iww, t2); mat3_vec(Iw, Me, t3); cross3(w, t3, t4);
+      for (int i = 0; i < 3; ++i) { Av[i] = t1[i] + t2[i] + t4[i]; Aa[i] = t3[i]; }   // theta_ddot_e: I_w M[:,e]
+      for (int r = 0; r < 3; ++r)
         for (int bb = 0; bb < 4; ++bb)
-          em(r0 + AX + r, basis_col(c, SP_BASE_ANG, A.poly, bb, e), Ap[r][e] * Hp[bb] + Av[r][e] * Hv[bb] + Aa[r][e] * Ha[bb], true);
+          em(r0 + AX + r, basis_col(c, SP_BASE_ANG, A.poly, bb, e), Ap[r] * Hp[bb] + Av[r] * Hv[bb] + Aa[r] * Ha[bb], true);
+    }
     return;
   }
   // group 2 + ee: force (GetJacobianWrtForce :168-180), torque (:182-191), motion (:193-204)
@@ -533,13 +575,14 @@ TG_HD void eval_rom(const Ctx& c, const ItemDesc& it, Emit& em) {
         for (int bb = 0; bb < 4; ++bb) em(r0 + r, basis_col(c, SP_BASE_LIN, L.poly, bb, e), -R[e][r] * H[bb], true);
   } else if (it.group == 1) {
     // DerivOfRotVecMult(t, r_W, inverse=true): row r = sum_c rW[c] dR[c][r]; row X has no roll terms
-    double dR[3][3][3]; euler_dR(q, dR);
     hermite_dpos(A.T, A.tl, H);
-    for (int r = 0; r < 3; ++r)
-      for (int e = (r == 0 ? 1 : 0); e < 3; ++e) {
-        const double s = rW[0] * dR[e][0][r] + rW[1] * dR[e][1][r] + rW[2] * dR[e][2][r];
+    for (int e = 0; e < 3; ++e) {
+      double dR[3][3]; euler_dR_axis(q, e, dR);
+      for (int r = (e == 0 ? 1 : 0); r < 3; ++r) {
+        const double s = rW[0] * dR[0][r] + rW[1] * dR[1][r] + rW[2] * dR[2][r];
         for (int bb = 0; bb < 4; ++bb) em(r0 + r, basis_col(c, SP_BASE_ANG, A.poly, bb, e), s * H[bb], true);
       }
+    }
   } else {
     hermite_dpos(P.T, P.tl, H);
     for (int r = 0; r < 3; ++r)
@@ -690,6 +733,7 @@ TG_HD void eval_swing(const Ctx& c, const ItemDesc& it, Emit& em) {
 template <class Emit>
 TG_HD void eval_item(const Ctx& c, const ItemDesc& it, Emit& em) {
   switch (it.type) {
+    case IT_NONE: break;
     case IT_DYN: eval_dyn(c, it, em); break;
     case IT_ROM: eval_rom(c, it, em); break;
     case IT_FDISC: eval_fdisc(c, it, em); break;

@@ -19,7 +19,7 @@
 namespace tg {
 
 struct TileDesc {
-  int32_t i0, i1;   // items [i0, i1)
+  int32_t i0, i1;   // items [i0, i1): exactly one item (or IT_NONE padding) per thread of the block
   int32_t r0, r1;   // rows  [r0, r1)
   int32_t v0, v1;   // values (CSR positions) [v0, v1)
   int32_t type, reserved;
@@ -36,6 +36,7 @@ struct Layout {
   std::vector<SplineMeta> spl;
   std::vector<int32_t> nodecol;
   std::vector<double> dur;
+  std::vector<SegRec> segs;     // (2 + 4 n_ee) records per time instant
   std::vector<ItemDesc> items;
   std::vector<int32_t> slots;
   std::vector<int64_t> row_ptr;
@@ -45,14 +46,27 @@ struct Layout {
   RobotC rb{};
   towr_terrain_t terrain{};
   int32_t fdisc_motion = 0;
-  int max_tile_values = 0, max_tile_rows = 0;
   towr_problem_desc_t desc{};
+  // tiles are grouped by item type: tiles [type_tile0[t], type_tile0[t+1]) run in one launch of
+  // the type's kernel with type_block[t] threads and type_lds[t] doubles of dynamic LDS
+  int32_t type_tile0[IT_COUNT + 1] = {};
+  int32_t type_block[IT_COUNT] = {};
+  int32_t type_lds[IT_COUNT] = {};
+  int32_t type_lds_rows_off[IT_COUNT] = {};   // start of the g buffer inside the type's LDS
+  // algorithmic bytes per problem of each type's launch: CSR values + g rows written, distinct
+  // x columns read (= the columns of its Jacobian rows)
+  int64_t type_bytes[IT_COUNT] = {};
 };
 
-// Limits of one LDS tile (doubles) — the kernel's dynamic LDS is sized from these.
-constexpr int kTileValueCap = 3072;
+// LDS tile caps (doubles of CSR values / rows per tile)
+constexpr int kTileValueCap = 8192;
 constexpr int kTileRowCap = 512;
-constexpr int kTileItemCap = 256;
+
+// Launch geometry of each item type (wave-uniform: each wave of a block runs one code path)
+struct TypeSpec { int block; int max_inst; };
+TypeSpec type_spec(int type, int n_ee);
+// thread (lane) of the block that evaluates group `g` of the k-th of n instances in a tile
+int type_lane(int type, int group, int k, int n, int n_ee);
 
 // Returns TOWR_OK or an error code with a message in `err`.
 int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err);
@@ -61,7 +75,5 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err);
 int initial_x_for(const towr_problem_desc_t& d, const towr_init_t& init, const towr_terrain_t& ter,
                   std::vector<double>& x0, std::string& err);
 
-// Tile groups: contiguous tile ranges of roughly equal value counts; out has n_groups + 1 entries.
-void group_tiles(const Layout& L, int n_groups, std::vector<int32_t>& out);
 
 }  // namespace tg

@@ -231,7 +231,6 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
   if (E < 1 || E > TOWR_MAX_EE) { err = "robot.n_ee out of range"; return TOWR_ERR_INVALID; }
   if (d.optimize_timings) { err = "phase-duration optimisation (gait optimisation) is not supported yet"; return TOWR_ERR_UNSUPPORTED; }
   if (!(d.total_time > 0) || !(d.duration_base_polynomial > 0)) { err = "bad total_time / duration_base_polynomial"; return TOWR_ERR_INVALID; }
-  const double T = d.total_time;
 
   std::vector<double> base_d;
   std::vector<NodeSet> sets;
@@ -313,7 +312,7 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
     const towr_constraint_t& c = d.constraints[ci];
     ConsInfo info{c.kind, c.ee, row, 0};
     auto add = [&](int type, int group, int ee, int k, int row0, double t, int a0, int a1, double p0) {
-      ItemDesc it{}; it.type = type; it.group = group; it.ee = ee; it.k = k; it.row0 = row0;
+      ItemDesc it{}; it.type = type; it.group = group; it.ee = ee; it.k = k; it.row0 = row0; it.seg = -1;
       it.t = t; it.a0 = a0; it.a1 = a1; it.p0 = p0;
       L.items.push_back(it); item_inst.push_back(inst);
     };
@@ -402,6 +401,29 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
   }
   L.m = row;
 
+  // ---- segment table: the reference's GetLocalTime scan for every (timed instance, spline)
+  {
+    const int nspl = (int)L.spl.size();
+    L.segs.clear();
+    int last_inst = -1, last_row = -1;
+    for (size_t q = 0; q < L.items.size(); ++q) {
+      ItemDesc& it = L.items[q];
+      const bool timed = it.type == IT_DYN || it.type == IT_ROM || it.type == IT_FDISC || it.type == IT_BMOT;
+      if (!timed) { it.seg = -1; continue; }
+      if (item_inst[q] != last_inst) {
+        last_inst = item_inst[q];
+        last_row = (int)(L.segs.size() / nspl);
+        for (int sp = 0; sp < nspl; ++sp) {
+          SegRec r{};
+          r.poly = seg_lookup(L.dur.data() + L.spl[sp].dur_off, L.spl[sp].n_polys, it.t, &r.tl);
+          r.T = L.dur[L.spl[sp].dur_off + r.poly];
+          L.segs.push_back(r);
+        }
+      }
+      it.seg = last_row;
+    }
+  }
+
   // ---- structure pass at x0: candidate (row, col) of every item
   std::vector<int32_t> crow, ccol; std::vector<uint8_t> cpres;
   std::vector<int32_t> item_cand_begin(L.items.size() + 1, 0);
@@ -413,6 +435,7 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
       item_cand_begin[i] = (int32_t)crow.size();
       RecordEmit em{&crow, &ccol, &cpres};
       em.g_rows_lo = L.items[i].row0; em.g_rows_hi = L.items[i].row0 + item_rows(L.items[i].type);
+      cx.seg = L.items[i].seg >= 0 ? L.segs.data() + (size_t)L.items[i].seg * L.spl.size() : nullptr;
       eval_item(cx, L.items[i], em);
       if (em.bad_g) { err = "internal: item wrote g outside its rows"; return TOWR_ERR_INVALID; }
     }
@@ -447,41 +470,141 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
     const int32_t* e = L.col.data() + L.row_ptr[r + 1];
     L.slots[q] = (int32_t)(L.row_ptr[r] + (std::lower_bound(b, e, ccol[q]) - b));
   }
-  for (size_t i = 0; i < L.items.size(); ++i) L.items[i].slot = item_cand_begin[i];
-
-  // ---- tiles: consecutive instances of one constraint set, bounded by the LDS caps
-  L.tiles.clear();
-  L.max_tile_values = 0; L.max_tile_rows = 0;
-  size_t i = 0;
-  while (i < L.items.size()) {
-    TileDesc t{};
-    t.i0 = (int32_t)i; t.type = L.items[i].type;
-    const int set_row0 = [&] { for (auto& c : L.cons) if (L.items[i].row0 >= c.row0 && L.items[i].row0 < c.row0 + c.rows) return c.row0; return 0; }();
-    const int set_row1 = [&] { for (auto& c : L.cons) if (L.items[i].row0 >= c.row0 && L.items[i].row0 < c.row0 + c.rows) return c.row0 + c.rows; return L.m; }();
-    t.r0 = L.items[i].row0;
-    size_t j = i;
-    while (j < L.items.size()) {
-      // extent of the next instance
-      size_t k = j;
-      while (k < L.items.size() && item_inst[k] == item_inst[j]) ++k;
-      const int r1 = L.items[j].row0 + item_rows(L.items[j].type);
-      if (L.items[j].row0 < set_row0 || r1 > set_row1) break;   // next constraint set
-      const int64_t nv = L.row_ptr[r1] - L.row_ptr[t.r0];
-      const int nr = r1 - t.r0;
-      if (j > i && (nv > kTileValueCap || nr > kTileRowCap || (int)(k - i) > kTileItemCap)) break;
-      if (nv > kTileValueCap || nr > kTileRowCap) { err = "internal: one instance exceeds the LDS tile"; return TOWR_ERR_UNSUPPORTED; }
-      j = k;
-      t.r1 = r1;
-    }
-    t.i1 = (int32_t)j;
-    t.v0 = (int32_t)L.row_ptr[t.r0]; t.v1 = (int32_t)L.row_ptr[t.r1];
-    L.max_tile_values = std::max(L.max_tile_values, t.v1 - t.v0);
-    L.max_tile_rows = std::max(L.max_tile_rows, t.r1 - t.r0);
-    L.tiles.push_back(t);
-    i = j;
+  for (size_t i = 0; i < L.items.size(); ++i) {
+    L.items[i].slot = item_cand_begin[i];
+    L.items[i].ncand = item_cand_begin[i + 1] - item_cand_begin[i];
   }
-  // rows without items (empty sets) are fine; every row with an item is covered by exactly one tile
+
+  // ---- tiles: consecutive instances of one constraint set, bounded by the LDS caps, one block
+  // per (problem, tile); items are laid out per lane so that each wave runs a single code path
+  {
+    struct Inst { int32_t first, count; };
+    std::vector<std::vector<TileDesc>> per_type(IT_COUNT);
+    std::vector<std::vector<ItemDesc>> per_type_items(IT_COUNT);
+    size_t i = 0;
+    while (i < L.items.size()) {
+      // one constraint set = maximal run of items with the same constraint row block
+      const int type = L.items[i].type;
+      int ci = -1;
+      for (int q = 0; q < (int)L.cons.size(); ++q)
+        if (L.items[i].row0 >= L.cons[q].row0 && L.items[i].row0 < L.cons[q].row0 + L.cons[q].rows) { ci = q; break; }
+      if (ci < 0) { err = "internal: item outside every constraint set"; return TOWR_ERR_INVALID; }
+      const int set_end_row = L.cons[ci].row0 + L.cons[ci].rows;
+      std::vector<Inst> insts;
+      size_t j = i;
+      while (j < L.items.size() && L.items[j].type == type && L.items[j].row0 < set_end_row && L.items[j].row0 >= L.cons[ci].row0) {
+        size_t k = j;
+        while (k < L.items.size() && item_inst[k] == item_inst[j]) ++k;
+        insts.push_back({(int32_t)j, (int32_t)(k - j)});
+        j = k;
+      }
+      const TypeSpec sp = type_spec(type, E);
+      const int n_inst = (int)insts.size();
+      auto inst_rows = [&](int a, int b) {   // rows of instances [a, b)
+        const int r0 = L.items[insts[a].first].row0;
+        const ItemDesc& last = L.items[insts[b - 1].first];
+        return std::make_pair(r0, last.row0 + item_rows(last.type));
+      };
+      int n_tiles = (n_inst + sp.max_inst - 1) / sp.max_inst;
+      for (;; ++n_tiles) {
+        bool ok = true;
+        for (int t = 0; t < n_tiles && ok; ++t) {
+          const int a = (int)((int64_t)t * n_inst / n_tiles), b = (int)((int64_t)(t + 1) * n_inst / n_tiles);
+          if (b <= a) continue;
+          auto rr = inst_rows(a, b);
+          if (L.row_ptr[rr.second] - L.row_ptr[rr.first] > kTileValueCap || rr.second - rr.first > kTileRowCap) ok = false;
+        }
+        if (ok) break;
+        if (n_tiles >= n_inst) { err = "internal: one instance exceeds the LDS tile"; return TOWR_ERR_UNSUPPORTED; }
+      }
+      for (int t = 0; t < n_tiles; ++t) {
+        const int a = (int)((int64_t)t * n_inst / n_tiles), b = (int)((int64_t)(t + 1) * n_inst / n_tiles);
+        if (b <= a) continue;
+        auto rr = inst_rows(a, b);
+        TileDesc td{};
+        td.type = type;
+        td.r0 = rr.first; td.r1 = rr.second;
+        td.v0 = (int32_t)L.row_ptr[td.r0]; td.v1 = (int32_t)L.row_ptr[td.r1];
+        std::vector<ItemDesc> lanes((size_t)sp.block);
+        for (auto& it : lanes) { it = ItemDesc{}; it.type = IT_NONE; it.seg = -1; }
+        for (int k = a; k < b; ++k)
+          for (int q = 0; q < insts[k].count; ++q) {
+            const ItemDesc& it = L.items[insts[k].first + q];
+            const int lane = type_lane(type, it.group, k - a, b - a, E);
+            if (lane < 0 || lane >= sp.block || lanes[lane].type != IT_NONE) { err = "internal: lane assignment"; return TOWR_ERR_INVALID; }
+            lanes[lane] = it;
+          }
+        td.i0 = (int32_t)per_type_items[type].size();   // relative; rebased below
+        per_type_items[type].insert(per_type_items[type].end(), lanes.begin(), lanes.end());
+        td.i1 = td.i0 + sp.block;
+        per_type[type].push_back(td);
+      }
+      i = j;
+    }
+    std::vector<ItemDesc> items;
+    L.tiles.clear();
+    for (int t = 0; t < IT_COUNT; ++t) {
+      L.type_tile0[t] = (int32_t)L.tiles.size();
+      const int base = (int)items.size();
+      int maxv = 0, maxr = 0;
+      for (TileDesc td : per_type[t]) {
+        td.i0 += base; td.i1 += base;
+        maxv = std::max(maxv, td.v1 - td.v0); maxr = std::max(maxr, td.r1 - td.r0);
+        L.tiles.push_back(td);
+      }
+      items.insert(items.end(), per_type_items[t].begin(), per_type_items[t].end());
+      L.type_block[t] = type_spec(t, E).block;
+      L.type_lds_rows_off[t] = (maxv + 1) & ~1;
+      L.type_lds[t] = L.type_lds_rows_off[t] + ((maxr + 1) & ~1);
+    }
+    L.type_tile0[IT_COUNT] = (int32_t)L.tiles.size();
+    // slot table per tile, transposed: candidate j of lane l at base + j * block + l, so that one
+    // wave's j-th slot load is a single coalesced 256-byte access
+    std::vector<int32_t> slots;
+    for (const TileDesc& td : L.tiles) {
+      const int block = td.i1 - td.i0;
+      int maxc = 0;
+      for (int l = 0; l < block; ++l) maxc = std::max(maxc, items[td.i0 + l].type == IT_NONE ? 0 : items[td.i0 + l].ncand);
+      const size_t base = slots.size();
+      slots.resize(base + (size_t)maxc * block, -1);
+      for (int l = 0; l < block; ++l) {
+        ItemDesc& it = items[td.i0 + l];
+        if (it.type == IT_NONE) { it.slot = (int32_t)base + l; continue; }
+        for (int j = 0; j < it.ncand; ++j) slots[base + (size_t)j * block + l] = L.slots[it.slot + j];
+        it.slot = (int32_t)(base + l);
+      }
+    }
+    if (slots.size() >= (size_t)INT32_MAX) { err = "slot table too large"; return TOWR_ERR_UNSUPPORTED; }
+    L.slots.swap(slots);
+    L.items.swap(items);
+    for (int t = 0; t < IT_COUNT; ++t) {
+      int64_t nv = 0, nr = 0;
+      std::vector<uint8_t> used((size_t)L.n, 0);
+      for (int ti = L.type_tile0[t]; ti < L.type_tile0[t + 1]; ++ti) {
+        const TileDesc& td = L.tiles[ti];
+        nv += td.v1 - td.v0; nr += td.r1 - td.r0;
+        for (int32_t k = td.v0; k < td.v1; ++k) used[L.col[k]] = 1;
+      }
+      int64_t nx = 0;
+      for (uint8_t u : used) nx += u;
+      L.type_bytes[t] = 8 * (nv + nr + nx);
+    }
+  }
   return TOWR_OK;
+}
+
+TypeSpec type_spec(int type, int n_ee) {
+  switch (type) {
+    case IT_DYN: return {256, std::max(1, std::min(64, 128 / std::max(1, n_ee)))};  // waves: g0 | g1 | ee, ee
+    case IT_ROM: return {192, 64};                                                      // waves: g0 | g1 | g2
+    default: return {64, 64};
+  }
+}
+
+int type_lane(int type, int group, int k, int n, int n_ee) {
+  if (type == IT_DYN) return group == 0 ? k : group == 1 ? 64 + k : 128 + (group - 2) * n + k;
+  if (type == IT_ROM) return 64 * group + k;
+  return k;
 }
 
 int initial_x_for(const towr_problem_desc_t& d, const towr_init_t& init, const towr_terrain_t& ter,
@@ -500,24 +623,6 @@ int initial_x_for(const towr_problem_desc_t& d, const towr_init_t& init, const t
   x0.assign((size_t)col, 0.0);
   for (auto& s : sets) { auto v = get_values(s); std::copy(v.begin(), v.end(), x0.begin() + s.col0); }
   return TOWR_OK;
-}
-
-void group_tiles(const Layout& L, int n_groups, std::vector<int32_t>& out) {
-  const int nt = (int)L.tiles.size();
-  if (n_groups < 1) n_groups = 1;
-  if (n_groups > nt) n_groups = nt;
-  out.assign((size_t)n_groups + 1, nt);
-  out[0] = 0;
-  // greedy: equal share of (values + rows) per group
-  int64_t total = 0;
-  for (auto& t : L.tiles) total += (t.v1 - t.v0) + (t.r1 - t.r0) + 64;
-  int64_t acc = 0; int g = 1;
-  for (int ti = 0; ti < nt && g < n_groups; ++ti) {
-    acc += (L.tiles[ti].v1 - L.tiles[ti].v0) + (L.tiles[ti].r1 - L.tiles[ti].r0) + 64;
-    if (acc * n_groups >= total * g && (nt - (ti + 1)) >= (n_groups - g)) out[g++] = ti + 1;
-  }
-  while (g < n_groups) { out[g] = std::min(nt, out[g - 1] + 1); ++g; }
-  out[n_groups] = nt;
 }
 
 }  // namespace tg

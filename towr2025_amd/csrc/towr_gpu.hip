@@ -26,8 +26,6 @@ using namespace tg;
 
 namespace {
 
-constexpr int kBlock = 256;
-
 struct KParams {
   const double* X; int64_t ldx;
   double* G; int64_t ldg;
@@ -35,17 +33,22 @@ struct KParams {
   const ItemDesc* items;
   const int32_t* slots;
   const TileDesc* tiles;
-  const int32_t* gtile;         // tile range of each group [gtile[g], gtile[g+1])
   const int32_t* nodecol;
   const SplineMeta* spl;
   const double* dur;
+  const SegRec* segs;
+  int32_t n_spl;
   const towr_terrain_t* terrains;
   int32_t terrain_per_problem;
-  int32_t n, n_pad, B, n_groups;
-  int32_t want_g, want_jac, fdisc_motion, reserved;
+  int32_t B, tile0, ntiles;
+  int32_t lds_rows_off;          // start of the g buffer in the dynamic LDS (doubles)
+  int32_t want_g, want_jac, fdisc_motion;
   RobotC rb;
 };
 
+// Accumulates candidate j into the LDS tile at its CSR slot (slot table transposed per tile: one
+// coalesced load per wave per candidate); the candidate's column is not needed on the device.
+template <int STRIDE>
 struct LdsEmit {
   const int32_t* slot;
   int j;
@@ -54,19 +57,30 @@ struct LdsEmit {
   double* gt;
   int r0;
   __device__ __forceinline__ void g(int row, double v) { gt[row - r0] = v; }
-  __device__ __forceinline__ void operator()(int row, int col, double v, bool) {
-    if (col >= 0) {
-      const int s = slot[j];
-      if (s >= 0) vt[s - v0] += v;
-    }
+  __device__ __forceinline__ void operator()(int, int, double v, bool) {
+    const int s = slot[j * STRIDE];
+    if (s >= 0) vt[s - v0] += v;
     ++j;
   }
 };
 
+template <int TYPE, class Emit>
+__device__ __forceinline__ void eval_typed(const Ctx& c, const ItemDesc& it, Emit& em) {
+  if constexpr (TYPE == IT_DYN) eval_dyn(c, it, em);
+  else if constexpr (TYPE == IT_ROM) eval_rom(c, it, em);
+  else if constexpr (TYPE == IT_FDISC) eval_fdisc(c, it, em);
+  else if constexpr (TYPE == IT_FNODE) eval_fnode(c, it, em);
+  else if constexpr (TYPE == IT_TERR) eval_height(c, it, sp_motion(it.ee), 0.0, em);
+  else if constexpr (TYPE == IT_BMOT) eval_bmot(c, it, em);
+  else if constexpr (TYPE == IT_SACC) eval_sacc(c, it, em);
+  else if constexpr (TYPE == IT_BHGT) eval_height(c, it, SP_BASE_LIN, it.p0, em);
+  else if constexpr (TYPE == IT_SWING) eval_swing(c, it, em);
+}
+
 // LDS -> HBM, 16-byte stores where the destination allows it
 __device__ __forceinline__ void copy_out(const double* __restrict__ src, double* __restrict__ dst, int n) {
-  const int head = (reinterpret_cast<uintptr_t>(dst) & 15) ? 1 : 0;
   if (n <= 0) return;
+  const int head = (reinterpret_cast<uintptr_t>(dst) & 15) ? 1 : 0;
   if (head && threadIdx.x == 0) dst[0] = src[0];
   const int m = (n - head) >> 1;
   double2* d2 = reinterpret_cast<double2*>(dst + head);
@@ -79,54 +93,56 @@ __device__ __forceinline__ void copy_out(const double* __restrict__ src, double*
   if (((n - head) & 1) && threadIdx.x == 0) dst[n - 1] = src[n - 1];
 }
 
-__global__ void __launch_bounds__(kBlock) towr_eval_kernel(KParams P) {
+// One block = one LDS tile (consecutive instances of one constraint set) of one problem; one item
+// per thread, laid out so every wave runs a single code path. x is read through L1/L2 (each
+// problem's x is ~9 KB and shared by all its tiles, which the mapping below keeps on one XCD).
+template <int TYPE, int BLOCK>
+__global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_kernel(KParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int total = P.B * P.n_groups;
+  const int total = P.B * P.ntiles;
   const int per = (total + 7) / 8;
-  // XCD-aware mapping: consecutive work ids (the groups of one problem) share blockIdx % 8
+  // XCD-aware mapping: work ids w and w+1 (tiles of one problem) share blockIdx % 8
   const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
   if (w >= total) return;
-  const int b = w / P.n_groups, grp = w % P.n_groups;
-  double* xs = smem;
-  double* vt = smem + P.n_pad;
-  double* gt = vt + kTileValueCap;
-
-  // stage x (NodesVariables / PhaseDurations of this problem) in LDS
-  const double* xb = P.X + (int64_t)b * P.ldx;
-  if ((reinterpret_cast<uintptr_t>(xb) & 15) == 0) {
-    const double2* x2 = reinterpret_cast<const double2*>(xb);
-    for (int i = threadIdx.x; i < (P.n >> 1); i += blockDim.x) {
-      const double2 v = x2[i];
-      xs[2 * i] = v.x; xs[2 * i + 1] = v.y;
-    }
-    if ((P.n & 1) && threadIdx.x == 0) xs[P.n - 1] = xb[P.n - 1];
-  } else {
-    for (int i = threadIdx.x; i < P.n; i += blockDim.x) xs[i] = xb[i];
+  const int b = w / P.ntiles;
+  const TileDesc T = P.tiles[P.tile0 + w % P.ntiles];
+  const int nv = T.v1 - T.v0, nr = T.r1 - T.r0;
+  double* vt = smem;
+  double* gt = smem + P.lds_rows_off;
+  for (int i = threadIdx.x; i < nv; i += BLOCK) vt[i] = 0.0;
+  __syncthreads();
+  const ItemDesc it = P.items[T.i0 + threadIdx.x];
+  if (it.type == TYPE) {
+    Ctx c;
+    c.seg = it.seg >= 0 ? P.segs + (int64_t)it.seg * P.n_spl : nullptr;
+    c.x = P.X + (int64_t)b * P.ldx; c.nodecol = P.nodecol; c.spl = P.spl; c.dur = P.dur;
+    c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
+    c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
+    LdsEmit<BLOCK> em{P.slots + it.slot, 0, vt, T.v0, gt, T.r0};
+    eval_typed<TYPE>(c, it, em);
   }
   __syncthreads();
-
-  Ctx c;
-  c.x = xs; c.nodecol = P.nodecol; c.spl = P.spl; c.dur = P.dur;
-  c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
-  c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
-
-  double* Vb = P.V + (int64_t)b * P.ldv;
-  double* Gb = P.G + (int64_t)b * P.ldg;
-  for (int ti = P.gtile[grp]; ti < P.gtile[grp + 1]; ++ti) {
-    const TileDesc T = P.tiles[ti];
-    const int nv = T.v1 - T.v0, nr = T.r1 - T.r0;
-    for (int i = threadIdx.x; i < nv; i += blockDim.x) vt[i] = 0.0;
-    __syncthreads();
-    for (int i = T.i0 + (int)threadIdx.x; i < T.i1; i += blockDim.x) {
-      const ItemDesc it = P.items[i];
-      LdsEmit em{P.slots + it.slot, 0, vt, T.v0, gt, T.r0};
-      eval_item(c, it, em);
-    }
-    __syncthreads();
-    if (P.want_jac) copy_out(vt, Vb + T.v0, nv);
-    if (P.want_g) for (int i = threadIdx.x; i < nr; i += blockDim.x) Gb[T.r0 + i] = gt[i];
-    __syncthreads();
+  if (P.want_jac) copy_out(vt, P.V + (int64_t)b * P.ldv + T.v0, nv);
+  if (P.want_g) {
+    double* Gb = P.G + (int64_t)b * P.ldg;
+    for (int i = threadIdx.x; i < nr; i += BLOCK) Gb[T.r0 + i] = gt[i];
   }
+}
+
+typedef void (*KernelFn)(KParams);
+const void* kernel_for(int type) {
+  switch (type) {
+    case IT_DYN: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_DYN, 256>);
+    case IT_ROM: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_ROM, 192>);
+    case IT_FDISC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_FDISC, 64>);
+    case IT_FNODE: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_FNODE, 64>);
+    case IT_TERR: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_TERR, 64>);
+    case IT_BMOT: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_BMOT, 64>);
+    case IT_SACC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_SACC, 64>);
+    case IT_BHGT: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_BHGT, 64>);
+    case IT_SWING: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_SWING, 64>);
+  }
+  return nullptr;
 }
 
 }  // namespace
@@ -146,12 +162,10 @@ struct towr_gpu_handle_s {
   int32_t* d_nodecol = nullptr;
   SplineMeta* d_spl = nullptr;
   double* d_dur = nullptr;
+  SegRec* d_segs = nullptr;
   towr_terrain_t* d_terrain = nullptr;      // base terrain (1 entry)
   towr_terrain_t* d_bterrain = nullptr;     // per-problem batch terrains
   int32_t bterrain_n = 0;
-  int32_t* d_gtile = nullptr;
-  int32_t gtile_groups = 0;
-  int32_t tiles_per_block = 0;              // 0 = automatic
   // staging for host-pointer entry points
   double *d_x = nullptr, *d_g = nullptr, *d_v = nullptr;
   double *h_x = nullptr, *h_g = nullptr, *h_v = nullptr;
@@ -183,47 +197,31 @@ int upload(towr_gpu_handle h, T** dst, const std::vector<T>& src) {
   return TOWR_OK;
 }
 
-int ensure_groups(towr_gpu_handle h, int n_groups) {
-  if (n_groups == h->gtile_groups && h->d_gtile) return TOWR_OK;
-  std::vector<int32_t> gt;
-  group_tiles(h->L, n_groups, gt);
-  if (h->d_gtile) { (void)hipFree(h->d_gtile); h->d_gtile = nullptr; }
-  if (int rc = upload(h, &h->d_gtile, gt)) return rc;
-  h->gtile_groups = (int32_t)gt.size() - 1;
-  return TOWR_OK;
-}
-
-int auto_groups(towr_gpu_handle h, int B) {
-  const int nt = (int)h->L.tiles.size();
-  if (h->tiles_per_block > 0) return std::max(1, (nt + h->tiles_per_block - 1) / h->tiles_per_block);
-  // enough blocks to fill 256 CUs several times over; one group per problem at large batches
-  int g = (4096 + B - 1) / B;
-  if (g < 1) g = 1;
-  if (g > nt) g = nt;
-  return g;
-}
-
 int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, int64_t ldg, double* V, int64_t ldv,
-           int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem) {
+           int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem, int only_type = -1) {
   if (B <= 0) return TOWR_OK;
-  int ng = auto_groups(h, B);
-  if (int rc = ensure_groups(h, ng)) return rc;
-  ng = h->gtile_groups;
   const Layout& L = h->L;
-  KParams P{};
-  P.X = X; P.ldx = ldx; P.G = G; P.ldg = ldg; P.V = V; P.ldv = ldv;
-  P.items = h->d_items; P.slots = h->d_slots; P.tiles = h->d_tiles; P.gtile = h->d_gtile;
-  P.nodecol = h->d_nodecol; P.spl = h->d_spl; P.dur = h->d_dur;
-  P.terrains = terrains; P.terrain_per_problem = per_problem;
-  P.n = L.n; P.n_pad = (L.n + 1) & ~1; P.B = B; P.n_groups = ng;
-  P.want_g = want_g; P.want_jac = want_jac; P.fdisc_motion = L.fdisc_motion;
-  P.rb = L.rb;
-  const size_t lds = sizeof(double) * ((size_t)P.n_pad + kTileValueCap + kTileRowCap);
-  const int64_t total = (int64_t)B * ng;
-  const int64_t grid = ((total + 7) / 8) * 8;
-  if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
-  hipLaunchKernelGGL(towr_eval_kernel, dim3((unsigned)grid), dim3(kBlock), lds, s, P);
-  HIPCHK(h, hipGetLastError());
+  for (int t = 0; t < IT_COUNT; ++t) {
+    if (only_type >= 0 && t != only_type) continue;
+    const int nt = L.type_tile0[t + 1] - L.type_tile0[t];
+    if (nt == 0) continue;
+    KParams P{};
+    P.X = X; P.ldx = ldx; P.G = G; P.ldg = ldg; P.V = V; P.ldv = ldv;
+    P.items = h->d_items; P.slots = h->d_slots; P.tiles = h->d_tiles;
+    P.nodecol = h->d_nodecol; P.spl = h->d_spl; P.dur = h->d_dur;
+    P.segs = h->d_segs; P.n_spl = (int32_t)L.spl.size();
+    P.terrains = terrains; P.terrain_per_problem = per_problem;
+    P.B = B; P.tile0 = L.type_tile0[t]; P.ntiles = nt;
+    P.lds_rows_off = L.type_lds_rows_off[t];
+    P.want_g = want_g; P.want_jac = want_jac; P.fdisc_motion = L.fdisc_motion;
+    P.rb = L.rb;
+    const int64_t total = (int64_t)B * nt;
+    const int64_t grid = ((total + 7) / 8) * 8;
+    if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
+    void* args[] = {&P};
+    HIPCHK(h, hipLaunchKernel(kernel_for(t), dim3((unsigned)grid), dim3((unsigned)L.type_block[t]), args,
+                              sizeof(double) * (size_t)L.type_lds[t], s));
+  }
   return TOWR_OK;
 }
 
@@ -271,6 +269,7 @@ int host_eval(towr_gpu_handle h, int B, const double* X, double* G, double* V) {
 extern "C" {
 
 int towr_gpu_abi_version(void) { return TOWR_GPU_ABI_VERSION; }
+int towr_gpu_num_kernels(void) { return IT_COUNT; }
 
 const char* towr_gpu_last_error(towr_gpu_handle h) {
   if (h) return h->err.c_str();
@@ -310,13 +309,14 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
   int r;
   if ((r = upload(h, &h->d_items, L.items)) || (r = upload(h, &h->d_slots, L.slots)) ||
       (r = upload(h, &h->d_tiles, L.tiles)) || (r = upload(h, &h->d_nodecol, L.nodecol)) ||
-      (r = upload(h, &h->d_spl, L.spl)) || (r = upload(h, &h->d_dur, L.dur)) || (r = upload(h, &h->d_terrain, ter)))
+      (r = upload(h, &h->d_spl, L.spl)) || (r = upload(h, &h->d_dur, L.dur)) || (r = upload(h, &h->d_segs, L.segs)) || (r = upload(h, &h->d_terrain, ter)))
     return bail(r);
-  const size_t lds = sizeof(double) * ((size_t)((L.n + 1) & ~1) + kTileValueCap + kTileRowCap);
-  if (lds > 160 * 1024) { h->err = "problem too large for the LDS layout"; return bail(TOWR_ERR_UNSUPPORTED); }
-  if (lds > 64 * 1024 &&
-      hipFuncSetAttribute(reinterpret_cast<const void*>(towr_eval_kernel), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
-    h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
+  for (int t = 0; t < IT_COUNT; ++t) {
+    const size_t lds = sizeof(double) * (size_t)L.type_lds[t];
+    if (lds > 160 * 1024) { h->err = "tile too large for LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
+    if (lds > 64 * 1024 && hipFuncSetAttribute(kernel_for(t), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+      h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
+    }
   }
   *out = h;
   return TOWR_OK;
@@ -324,8 +324,8 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
 
 int towr_gpu_destroy(towr_gpu_handle h) {
   if (!h) return TOWR_OK;
-  void* dev[] = {h->d_items, h->d_slots, h->d_tiles, h->d_nodecol, h->d_spl, h->d_dur, h->d_terrain,
-                 h->d_bterrain, h->d_gtile, h->d_x, h->d_g, h->d_v};
+  void* dev[] = {h->d_items, h->d_slots, h->d_tiles, h->d_nodecol, h->d_spl, h->d_dur, h->d_segs, h->d_terrain,
+                 h->d_bterrain, h->d_x, h->d_g, h->d_v};
   if (h->device >= 0) for (void* p : dev) if (p) (void)hipFree(p);
   void* host[] = {h->h_x, h->h_g, h->h_v};
   for (void* p : host) if (p) (void)hipHostFree(p);
@@ -429,8 +429,30 @@ int towr_gpu_eval_batch_device(towr_gpu_handle h, int32_t B, const double* X, in
   if (h->device < 0) return fail(h, TOWR_ERR_NO_DEVICE, "layout-only handle (created with device < 0) cannot evaluate");
   if (hipSetDevice(h->device) != hipSuccess) return fail(h, TOWR_ERR_HIP, "hipSetDevice");
   const bool per = h->d_bterrain && h->bterrain_n >= B;
-  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : h->stream;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);   // NULL = HIP's default stream
   return launch(h, B, X, ldx, G, ldg, V, ldv, want_g, want_jac, s, per ? h->d_bterrain : h->d_terrain, per ? 1 : 0);
+}
+
+int towr_gpu_kernel_info(towr_gpu_handle h, int32_t kernel, const char** name, int32_t* n_tiles, int64_t* bytes_per_problem) {
+  static const char* names[IT_COUNT] = {"dynamic", "range_of_motion", "force_discretized", "force_node", "terrain",
+                                        "base_motion", "spline_acc", "base_height", "swing"};
+  if (!h || kernel < 0 || kernel >= IT_COUNT) return fail(h, TOWR_ERR_INVALID, "bad kernel index");
+  if (name) *name = names[kernel];
+  if (n_tiles) *n_tiles = h->L.type_tile0[kernel + 1] - h->L.type_tile0[kernel];
+  if (bytes_per_problem) *bytes_per_problem = h->L.type_bytes[kernel];
+  return TOWR_OK;
+}
+
+int towr_gpu_eval_batch_device_kernel(towr_gpu_handle h, int32_t kernel, int32_t B, const double* X, int64_t ldx,
+                                      double* G, int64_t ldg, double* V, int64_t ldv, void* stream) {
+  if (!h || B < 0 || !X || !G || !V || kernel < 0 || kernel >= IT_COUNT) return fail(h, TOWR_ERR_INVALID, "bad argument");
+  const Layout& L = h->L;
+  if (ldx < L.n || ldg < L.m || ldv < L.nnz) return fail(h, TOWR_ERR_INVALID, "leading dimension too small");
+  if (h->device < 0) return fail(h, TOWR_ERR_NO_DEVICE, "layout-only handle (created with device < 0) cannot evaluate");
+  if (hipSetDevice(h->device) != hipSuccess) return fail(h, TOWR_ERR_HIP, "hipSetDevice");
+  const bool per = h->d_bterrain && h->bterrain_n >= B;
+  return launch(h, B, X, ldx, G, ldg, V, ldv, 1, 1, reinterpret_cast<hipStream_t>(stream),
+                per ? h->d_bterrain : h->d_terrain, per ? 1 : 0, kernel);
 }
 
 int towr_gpu_eval_batch(towr_gpu_handle h, int32_t B, const double* X, double* G, double* V) {
@@ -441,7 +463,7 @@ int towr_gpu_eval_batch(towr_gpu_handle h, int32_t B, const double* X, double* G
 
 int towr_gpu_set_tiles_per_block(towr_gpu_handle h, int32_t tiles_per_block) {
   if (!h || tiles_per_block < 0) return fail(h, TOWR_ERR_INVALID, "bad argument");
-  h->tiles_per_block = tiles_per_block;
+  (void)tiles_per_block;   // one block per (problem, tile) since the per-type kernels; kept for ABI stability
   return TOWR_OK;
 }
 

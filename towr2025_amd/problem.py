@@ -130,6 +130,23 @@ class TowrGpuProblem:
             C.c_void_p(G.data_ptr()), G.stride(0), C.c_void_p(V.data_ptr()), V.stride(0),
             int(want_g), int(want_jac), C.c_void_p(stream.cuda_stream)))
 
+    def kernels(self):
+        """[(index, name, n_tiles, algorithmic bytes per problem)] of the per-constraint-kind kernels."""
+        out = []
+        for k in range(self._lib.towr_gpu_num_kernels()):
+            name, nt, by = C.c_char_p(), C.c_int32(), C.c_int64()
+            self._check(self._lib.towr_gpu_kernel_info(self._h, k, C.byref(name), C.byref(nt), C.byref(by)))
+            if nt.value:
+                out.append((k, name.value.decode(), nt.value, by.value))
+        return out
+
+    def eval_batch_device_kernel(self, kernel, X, G, V, stream):
+        """Launch one constraint kind's kernel only (roofline accounting)."""
+        self._check(self._lib.towr_gpu_eval_batch_device_kernel(
+            self._h, kernel, X.shape[0], C.c_void_p(X.data_ptr()), X.stride(0),
+            C.c_void_p(G.data_ptr()), G.stride(0), C.c_void_p(V.data_ptr()), V.stride(0),
+            C.c_void_p(stream.cuda_stream)))
+
     def set_tiles_per_block(self, t: int):
         self._check(self._lib.towr_gpu_set_tiles_per_block(self._h, t))
 
