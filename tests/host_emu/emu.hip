@@ -13,7 +13,8 @@ struct AccEmit {
   const int32_t* slot; int stride; int j; double* v; double* gout;
   void g(int row, double val) { gout[row] = val; }
   void operator()(int, int, double val, bool) {
-    int s = slot[j * stride]; if (s >= 0) v[s] += val;
+    int s = slot[j * stride];
+    if (s >= 0) { if (s & kSlotAccumulate) v[s & kSlotMask] += val; else v[s] = val; }
     ++j;
   }
 };

@@ -1,0 +1,56 @@
+"""The C-ABI boundary: the built library loads, exports every symbol include/towr_gpu.h declares,
+and the ctypes mirror has the C layout (checked against gcc's sizeof/offsetof)."""
+import os
+import re
+import subprocess
+import tempfile
+
+from towr2025_amd import _capi as capi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "towr_gpu.h")
+
+
+def test_every_declared_symbol_is_exported():
+    lib = capi.load_library()
+    src = open(HDR).read()
+    declared = set(re.findall(r"\b(towr_gpu_\w+)\s*\(", src))
+    assert declared, "no declarations parsed"
+    for name in sorted(declared):
+        assert hasattr(lib, name), f"{name} declared in towr_gpu.h but not exported"
+        assert name in capi.SYMBOLS, f"{name} missing from the ctypes mirror"
+    assert lib.towr_gpu_abi_version() == capi.ABI_VERSION
+
+
+def test_struct_layout_matches_c():
+    import ctypes as C
+    prog = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "towr_gpu.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(towr_terrain_t), sizeof(towr_robot_t), sizeof(towr_constraint_t),
+         sizeof(towr_init_t), sizeof(towr_problem_desc_t), offsetof(towr_problem_desc_t, init));
+  return 0;
+}'''
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "s.c")
+        open(c, "w").write(prog)
+        exe = os.path.join(d, "s")
+        subprocess.check_call(["gcc", "-I", os.path.dirname(HDR), c, "-o", exe])
+        got = [int(v) for v in subprocess.check_output([exe]).split()]
+    want = [C.sizeof(capi.Terrain), C.sizeof(capi.Robot), C.sizeof(capi.ConstraintDesc),
+            C.sizeof(capi.InitDesc), C.sizeof(capi.ProblemDesc), capi.ProblemDesc.init.offset]
+    assert got == want
+
+
+def test_no_cpu_fallback_without_extension(tmp_path):
+    """The product refuses to run without its HIP extension (no CPU path to fall back to)."""
+    import pytest
+    saved = capi._lib
+    capi._lib = None
+    try:
+        with pytest.raises(RuntimeError, match="not built"):
+            capi.load_library(str(tmp_path / "missing.so"))
+    finally:
+        capi._lib = saved

@@ -1,0 +1,76 @@
+"""Central finite differences of the oracle's g against the oracle's J (pattern and values), on every
+configuration at seeded perturbations of x0 — the self-consistency pin of the CPU restatement.
+Terrains with height kinks are checked away from the kinks (Gap is pinned by its KAT instead:
+its parabola meets the flat ground at a slope discontinuity, where central differences do not
+apply). Whitelisted reference quirk: DynamicConstraint omits the torque term of d/d(phase durations)
+(dynamic_constraint.cc:116-122, SURVEY A22 ii) — checked by zeroing the torque variables."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from oracle.oracle import Oracle
+from tests.configs import config_descs
+from towr2025_amd import _capi as capi
+from towr2025_amd import formulation as F
+
+CONFIGS = config_descs()
+
+
+def _fd_check(desc, x, h_rel=1e-6, tol=2e-5, skip_cols=None):
+    o = Oracle(desc)
+    r, c, v = o.eval_jac(x)
+    J = sp.csr_matrix((v, (r, c)), shape=(o.m, o.n)).toarray()
+    mask = np.zeros_like(J, dtype=bool)
+    mask[r, c] = True
+    cols = range(o.n) if skip_cols is None else [j for j in range(o.n) if j not in skip_cols]
+    for j in cols:
+        h = h_rel * max(1.0, abs(x[j]))
+        xp, xm = x.copy(), x.copy()
+        xp[j] += h
+        xm[j] -= h
+        fd = (o.eval_g(xp) - o.eval_g(xm)) / (2 * h)
+        err = np.abs(fd - J[:, j]) / np.maximum(1.0, np.abs(J[:, j]))
+        assert err.max() < tol, f"col {j}: FD mismatch {err.max():.3g} at row {err.argmax()}"
+        # nothing outside the pattern moves (no missing entries)
+        assert np.all(np.abs(fd[~mask[:, j]]) < 1e-4), f"col {j}: FD nonzero outside the pattern"
+
+
+@pytest.mark.parametrize("name", ["monoped_procedural", "biped_walk_2s", "anymal_trot_2p4s",
+                                  "hopper_five_steps", "hyq_chimney", "anymal_slope_yaw", "anymal_block_baserom"])
+def test_fd_consistency(name):
+    desc = CONFIGS[name]
+    o = Oracle(desc)
+    x = o.initial_x() + 0.05 * np.random.default_rng(11).standard_normal(o.n)
+    _fd_check(desc, x)
+
+
+def test_fd_gait_optimisation_with_quirk():
+    """Phase-duration Jacobians (PhaseSpline / PhaseDurations::GetJacobianOfPos): FD-consistent
+    once torques are zero, because the reference drops the torque term (quirk A22 ii)."""
+    desc = F.anymal_trot(optimize_timings=True, terrain=F.HeightMap.MakeTerrain(F.HeightMap.StairsID)).to_desc()
+    o = Oracle(desc)
+    x = o.initial_x() + 0.01 * np.random.default_rng(3).standard_normal(o.n)
+    for i, (c0, n) in enumerate(o.varset_cols()):
+        if desc.varsets[i].kind == capi.VAR_EE_TORQUE:
+            x[c0:c0 + n] = 0.0
+    _fd_check(desc, x, tol=5e-5)
+
+
+def test_gait_opt_quirk_is_present():
+    """With nonzero torques the d/d(schedule) rows of the dynamic constraint disagree with FD:
+    the reference's omission is reproduced, not fixed."""
+    desc = F.anymal_trot(optimize_timings=True).to_desc()
+    o = Oracle(desc)
+    x = o.initial_x() + 0.01 * np.random.default_rng(4).standard_normal(o.n)
+    r, c, v = o.eval_jac(x)
+    J = sp.csr_matrix((v, (r, c)), shape=(o.m, o.n)).toarray()
+    c0, n = o.varset_cols()[-1]            # last schedule set
+    j = c0
+    h = 1e-6
+    xp, xm = x.copy(), x.copy()
+    xp[j] += h
+    xm[j] -= h
+    fd = (o.eval_g(xp) - o.eval_g(xm)) / (2 * h)
+    dyn_row0, dyn_rows = o.constraint_rows()[[d.kind for d in desc.constraints[:desc.n_constraints]].index(capi.C_DYNAMIC)]
+    err = np.abs(fd - J[:, j])[dyn_row0:dyn_row0 + dyn_rows]
+    assert err.max() > 1e-3

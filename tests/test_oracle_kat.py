@@ -150,5 +150,33 @@ def test_terrain_gap_kat():
         sub = {xs: x, ys: 0.2}
         np.testing.assert_allclose(out_h, [float(H.subs(sub)), float(sp.diff(H, xs).subs(sub)), 0.0], rtol=1e-12, atol=1e-12)
         np.testing.assert_allclose(bs, np.array([[float(c.subs(sub)) for c in b] for b in basis]).ravel(), rtol=1e-12, atol=1e-13)
-        ref_d = np.array([[[float(sp.diff(c, v).subs(sub)) for c in b] for b in basis] for v in (xs, ys)]).ravel()
-        np.testing.assert_allclose(dbs, ref_d, rtol=1e-10, atol=1e-12)
+        # the reference's formula (height_map.cc:80-91, 141-148): an element-wise product of the
+        # "derivative of the normalized vector w.r.t. its dim-th component" with d(basis)/d(dim)
+        raw = (n, t1, t2)
+        ref_d = []
+        for d, v in enumerate((xs, ys)):
+            for b in raw:
+                bv = np.array([float(cmp.subs(sub)) for cmp in b])
+                dv = np.array([float(sp.diff(cmp, v).subs(sub)) for cmp in b])
+                nrm = np.linalg.norm(bv)
+                ref_d.append(1 / nrm**2 * (nrm * np.eye(3)[d] - bv[d] * bv / nrm) * dv)
+        np.testing.assert_allclose(dbs, np.array(ref_d).ravel(), rtol=1e-10, atol=1e-12)
+
+
+def test_normalized_basis_derivative_quirk_is_reproduced():
+    """On curved terrain the reference's d(normalized basis)/dx is not the exact derivative (it is
+    an element-wise product, height_map.cc:80-91). The oracle reproduces it, so it must differ from
+    sympy's exact derivative somewhere inside the Gap."""
+    L = _lib()
+    t = capi.Terrain()
+    t.id, t.friction_coeff = capi.TERRAIN_GAP, 0.5
+    t.p[0], t.p[1], t.p[2] = 1.0, 0.5, 1.5
+    xs = sp.symbols("xs")
+    xc = 1.25
+    H = (4 * 1.5) / 0.25 * xs**2 - (8 * 1.5 * xc) / 0.25 * xs - (1.5 * (0.5 - 2 * xc) * (0.5 + 2 * xc)) / 0.25
+    nvec = sp.Matrix([-sp.diff(H, xs), 0, 1])
+    exact = sp.diff(nvec / sp.sqrt(nvec.dot(nvec)), xs)
+    out_h, bs, dbs = np.zeros(3), np.zeros(9), np.zeros(18)
+    L.oracle_kat_terrain(C.byref(t), 1.1, 0.0, _p(out_h), _p(bs), _p(dbs))
+    exact_n = np.array([float(v.subs(xs, 1.1)) for v in exact])
+    assert np.abs(dbs[0:3] - exact_n).max() > 1e-3

@@ -473,6 +473,14 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
   for (size_t i = 0; i < L.items.size(); ++i) {
     L.items[i].slot = item_cand_begin[i];
     L.items[i].ncand = item_cand_begin[i + 1] - item_cand_begin[i];
+    // the first contribution to a slot is a plain store, later ones (duplicate columns, e.g. the two
+    // nodes of a stance polynomial sharing one variable) accumulate: kSlotAccumulate marks them
+    std::vector<int32_t> seen;
+    for (int32_t q = item_cand_begin[i]; q < item_cand_begin[i + 1]; ++q) {
+      if (L.slots[q] < 0) continue;
+      if (std::find(seen.begin(), seen.end(), L.slots[q]) != seen.end()) L.slots[q] |= kSlotAccumulate;
+      else seen.push_back(L.slots[q]);
+    }
   }
 
   // ---- tiles: consecutive instances of one constraint set, bounded by the LDS caps, one block

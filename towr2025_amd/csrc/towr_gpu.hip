@@ -42,6 +42,8 @@ struct KParams {
   int32_t terrain_per_problem;
   int32_t B, tile0, ntiles;
   int32_t lds_rows_off;          // start of the g buffer in the dynamic LDS (doubles)
+  int32_t lds_x_off;             // start of the staged x / node-column table (stages_x kernels)
+  int32_t n, n_pad, n_nodecol;
   int32_t want_g, want_jac, fdisc_motion;
   RobotC rb;
 };
@@ -59,7 +61,10 @@ struct LdsEmit {
   __device__ __forceinline__ void g(int row, double v) { gt[row - r0] = v; }
   __device__ __forceinline__ void operator()(int, int, double v, bool) {
     const int s = slot[j * STRIDE];
-    if (s >= 0) vt[s - v0] += v;
+    if (s >= 0) {
+      if (s & kSlotAccumulate) vt[(s & kSlotMask) - v0] += v;   // rare: duplicate column
+      else vt[s - v0] = v;                                      // plain store, no read-modify-write
+    }
     ++j;
   }
 };
@@ -96,6 +101,9 @@ __device__ __forceinline__ void copy_out(const double* __restrict__ src, double*
 // One block = one LDS tile (consecutive instances of one constraint set) of one problem; one item
 // per thread, laid out so every wave runs a single code path. x is read through L1/L2 (each
 // problem's x is ~9 KB and shared by all its tiles, which the mapping below keeps on one XCD).
+// kernels whose items gather many spline nodes stage x and the node->column table in LDS
+constexpr bool stages_x(int type) { return type == IT_DYN || type == IT_ROM; }
+
 template <int TYPE, int BLOCK>
 __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_kernel(KParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -107,15 +115,24 @@ __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_ker
   const int b = w / P.ntiles;
   const TileDesc T = P.tiles[P.tile0 + w % P.ntiles];
   const int nv = T.v1 - T.v0, nr = T.r1 - T.r0;
-  double* vt = smem;
+  double* vt = smem;                       // every slot of [v0, v1) is stored by some candidate
   double* gt = smem + P.lds_rows_off;
-  for (int i = threadIdx.x; i < nv; i += BLOCK) vt[i] = 0.0;
-  __syncthreads();
+  const double* xg = P.X + (int64_t)b * P.ldx;
+  const double* xsrc = xg;
+  const int32_t* ncsrc = P.nodecol;
+  if constexpr (stages_x(TYPE)) {
+    double* xs = smem + P.lds_x_off;
+    int32_t* ns = reinterpret_cast<int32_t*>(smem + P.lds_x_off + P.n_pad);
+    for (int i = threadIdx.x; i < P.n; i += BLOCK) xs[i] = xg[i];
+    for (int i = threadIdx.x; i < P.n_nodecol; i += BLOCK) ns[i] = P.nodecol[i];
+    __syncthreads();
+    xsrc = xs; ncsrc = ns;
+  }
   const ItemDesc it = P.items[T.i0 + threadIdx.x];
   if (it.type == TYPE) {
     Ctx c;
     c.seg = it.seg >= 0 ? P.segs + (int64_t)it.seg * P.n_spl : nullptr;
-    c.x = P.X + (int64_t)b * P.ldx; c.nodecol = P.nodecol; c.spl = P.spl; c.dur = P.dur;
+    c.x = xsrc; c.nodecol = ncsrc; c.spl = P.spl; c.dur = P.dur;
     c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
     c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
     LdsEmit<BLOCK> em{P.slots + it.slot, 0, vt, T.v0, gt, T.r0};
@@ -197,6 +214,19 @@ int upload(towr_gpu_handle h, T** dst, const std::vector<T>& src) {
   return TOWR_OK;
 }
 
+// every evaluation entry point: refuse layout-only handles, make the handle's device current
+int bind(towr_gpu_handle h) {
+  if (h->device < 0) return fail(h, TOWR_ERR_NO_DEVICE, "layout-only handle (created with device < 0) cannot evaluate");
+  if (hipSetDevice(h->device) != hipSuccess) return fail(h, TOWR_ERR_HIP, "hipSetDevice failed");
+  return TOWR_OK;
+}
+
+size_t lds_bytes(const Layout& L, int t) {
+  size_t d = (size_t)L.type_lds[t];
+  if (stages_x(t)) d += (size_t)((L.n + 1) & ~1) + (L.nodecol.size() + 1) / 2;
+  return sizeof(double) * d;
+}
+
 int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, int64_t ldg, double* V, int64_t ldv,
            int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem, int only_type = -1) {
   if (B <= 0) return TOWR_OK;
@@ -213,6 +243,8 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
     P.terrains = terrains; P.terrain_per_problem = per_problem;
     P.B = B; P.tile0 = L.type_tile0[t]; P.ntiles = nt;
     P.lds_rows_off = L.type_lds_rows_off[t];
+    P.n = L.n; P.n_pad = (L.n + 1) & ~1; P.n_nodecol = (int32_t)L.nodecol.size();
+    P.lds_x_off = L.type_lds[t];
     P.want_g = want_g; P.want_jac = want_jac; P.fdisc_motion = L.fdisc_motion;
     P.rb = L.rb;
     const int64_t total = (int64_t)B * nt;
@@ -220,7 +252,7 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
     if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
     void* args[] = {&P};
     HIPCHK(h, hipLaunchKernel(kernel_for(t), dim3((unsigned)grid), dim3((unsigned)L.type_block[t]), args,
-                              sizeof(double) * (size_t)L.type_lds[t], s));
+                              lds_bytes(L, t), s));
   }
   return TOWR_OK;
 }
@@ -242,7 +274,6 @@ int ensure_stage(towr_gpu_handle h, int B) {
 }
 
 int host_eval(towr_gpu_handle h, int B, const double* X, double* G, double* V) {
-  if (h->device < 0) return fail(h, TOWR_ERR_NO_DEVICE, "layout-only handle (created with device < 0) cannot evaluate");
   if (int rc = ensure_stage(h, B)) return rc;
   const Layout& L = h->L;
   const size_t xb = sizeof(double) * (size_t)B * L.n, gb = sizeof(double) * (size_t)B * L.m,
@@ -312,7 +343,7 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
       (r = upload(h, &h->d_spl, L.spl)) || (r = upload(h, &h->d_dur, L.dur)) || (r = upload(h, &h->d_segs, L.segs)) || (r = upload(h, &h->d_terrain, ter)))
     return bail(r);
   for (int t = 0; t < IT_COUNT; ++t) {
-    const size_t lds = sizeof(double) * (size_t)L.type_lds[t];
+    const size_t lds = lds_bytes(L, t);
     if (lds > 160 * 1024) { h->err = "tile too large for LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
     if (lds > 64 * 1024 && hipFuncSetAttribute(kernel_for(t), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
       h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
@@ -384,19 +415,19 @@ int towr_gpu_varset_info(towr_gpu_handle h, int32_t i, int32_t* kind, int32_t* e
 
 int towr_gpu_eval_g(towr_gpu_handle h, const double* x, double* g) {
   if (!h || !x || !g) return fail(h, TOWR_ERR_INVALID, "null argument");
-  if (hipSetDevice(h->device) != hipSuccess) return fail(h, TOWR_ERR_HIP, "hipSetDevice");
+  if (int rc = bind(h)) return rc;
   return host_eval(h, 1, x, g, nullptr);
 }
 
 int towr_gpu_eval_jac_values(towr_gpu_handle h, const double* x, double* values) {
   if (!h || !x || !values) return fail(h, TOWR_ERR_INVALID, "null argument");
-  if (hipSetDevice(h->device) != hipSuccess) return fail(h, TOWR_ERR_HIP, "hipSetDevice");
+  if (int rc = bind(h)) return rc;
   return host_eval(h, 1, x, nullptr, values);
 }
 
 int towr_gpu_eval_g_jac(towr_gpu_handle h, const double* x, double* g, double* values) {
   if (!h || !x || !g || !values) return fail(h, TOWR_ERR_INVALID, "null argument");
-  if (hipSetDevice(h->device) != hipSuccess) return fail(h, TOWR_ERR_HIP, "hipSetDevice");
+  if (int rc = bind(h)) return rc;
   return host_eval(h, 1, x, g, values);
 }
 
@@ -410,8 +441,7 @@ int towr_gpu_set_batch_terrain(towr_gpu_handle h, int32_t B, const towr_terrain_
     if (ter_has_curvature(terrains[i].id) && B > 1)
       return fail(h, TOWR_ERR_UNSUPPORTED, "Gap terrain has an x-dependent pattern; batch it one problem per handle");
   }
-  if (h->device < 0) return fail(h, TOWR_ERR_NO_DEVICE, "layout-only handle (created with device < 0) cannot evaluate");
-  if (hipSetDevice(h->device) != hipSuccess) return fail(h, TOWR_ERR_HIP, "hipSetDevice");
+  if (int rc = bind(h)) return rc;
   if (h->d_bterrain) { (void)hipFree(h->d_bterrain); h->d_bterrain = nullptr; h->bterrain_n = 0; }
   if (B == 0) return TOWR_OK;
   std::vector<towr_terrain_t> v(terrains, terrains + B);
@@ -426,8 +456,7 @@ int towr_gpu_eval_batch_device(towr_gpu_handle h, int32_t B, const double* X, in
   const Layout& L = h->L;
   if (ldx < L.n || (want_g && (!G || ldg < L.m)) || (want_jac && (!V || ldv < L.nnz)))
     return fail(h, TOWR_ERR_INVALID, "leading dimension smaller than n / m / nnz, or missing output");
-  if (h->device < 0) return fail(h, TOWR_ERR_NO_DEVICE, "layout-only handle (created with device < 0) cannot evaluate");
-  if (hipSetDevice(h->device) != hipSuccess) return fail(h, TOWR_ERR_HIP, "hipSetDevice");
+  if (int rc = bind(h)) return rc;
   const bool per = h->d_bterrain && h->bterrain_n >= B;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);   // NULL = HIP's default stream
   return launch(h, B, X, ldx, G, ldg, V, ldv, want_g, want_jac, s, per ? h->d_bterrain : h->d_terrain, per ? 1 : 0);
@@ -448,8 +477,7 @@ int towr_gpu_eval_batch_device_kernel(towr_gpu_handle h, int32_t kernel, int32_t
   if (!h || B < 0 || !X || !G || !V || kernel < 0 || kernel >= IT_COUNT) return fail(h, TOWR_ERR_INVALID, "bad argument");
   const Layout& L = h->L;
   if (ldx < L.n || ldg < L.m || ldv < L.nnz) return fail(h, TOWR_ERR_INVALID, "leading dimension too small");
-  if (h->device < 0) return fail(h, TOWR_ERR_NO_DEVICE, "layout-only handle (created with device < 0) cannot evaluate");
-  if (hipSetDevice(h->device) != hipSuccess) return fail(h, TOWR_ERR_HIP, "hipSetDevice");
+  if (int rc = bind(h)) return rc;
   const bool per = h->d_bterrain && h->bterrain_n >= B;
   return launch(h, B, X, ldx, G, ldg, V, ldv, 1, 1, reinterpret_cast<hipStream_t>(stream),
                 per ? h->d_bterrain : h->d_terrain, per ? 1 : 0, kernel);
@@ -457,7 +485,7 @@ int towr_gpu_eval_batch_device_kernel(towr_gpu_handle h, int32_t kernel, int32_t
 
 int towr_gpu_eval_batch(towr_gpu_handle h, int32_t B, const double* X, double* G, double* V) {
   if (!h || B < 0 || !X) return fail(h, TOWR_ERR_INVALID, "bad argument");
-  if (hipSetDevice(h->device) != hipSuccess) return fail(h, TOWR_ERR_HIP, "hipSetDevice");
+  if (int rc = bind(h)) return rc;
   return host_eval(h, B, X, G, V);
 }
 
