@@ -80,7 +80,12 @@ struct ItemDesc {
 struct SegRec {
   double tl, T;
   int32_t poly, reserved;
+  double H[3][4];   // d{pos,vel,acc}(tl)/d{n0.p, n0.v, n1.p, n1.v}: batch-invariant Hermite basis
 };
+
+// item kinds whose emission can contain duplicate columns (stance polynomials whose two nodes share
+// one variable, junction nodes of SplineAcc); the others never do (checked at build time)
+TG_HD constexpr bool type_merges(int type) { return type <= 2 /* DYN, ROM, FDISC */ || type == 6 /* SACC */; }
 
 struct Ctx {
   const SegRec* seg;            // this item's segment row (one SegRec per spline), or nullptr
@@ -99,6 +104,7 @@ struct Ctx {
 struct SplinePt {
   int poly;
   double T, tl;
+  const double* H;   // SegRec::H of this instant on the device (basis precomputed), else nullptr
   double p[3], v[3], a[3];
 };
 
@@ -124,6 +130,29 @@ TG_HD int node_col(const Ctx& c, int s, int node, int deriv, int dim) {
 // column of Hermite basis function b (0 n0.p, 1 n0.v, 2 n1.p, 3 n1.v) of polynomial `poly`, dim e
 TG_HD int basis_col(const Ctx& c, int s, int poly, int b, int e) {
   return node_col(c, s, poly + (b >> 1), b & 1, e);
+}
+
+// GetDerivativeOf{Pos,Vel,Acc}Wrt{Start,End}Node (polynomial.cc:135-234); b = 0 n0.p, 1 n0.v, 2 n1.p, 3 n1.v
+TG_HD void hermite_dpos(double T, double t, double H[4]) {
+  const double T2 = T * T, T3 = T2 * T, t2 = t * t, t3 = t2 * t;
+  H[0] = (2 * t3) / T3 - (3 * t2) / T2 + 1;
+  H[1] = t - (2 * t2) / T + t3 / T2;
+  H[2] = (3 * t2) / T2 - (2 * t3) / T3;
+  H[3] = t3 / T2 - t2 / T;
+}
+TG_HD void hermite_dvel(double T, double t, double H[4]) {
+  const double T2 = T * T, T3 = T2 * T, t2 = t * t;
+  H[0] = (6 * t2) / T3 - (6 * t) / T2;
+  H[1] = (3 * t2) / T2 - (4 * t) / T + 1;
+  H[2] = (6 * t) / T2 - (6 * t2) / T3;
+  H[3] = (3 * t2) / T2 - (2 * t) / T;
+}
+TG_HD void hermite_dacc(double T, double t, double H[4]) {
+  const double T2 = T * T, T3 = T2 * T;
+  H[0] = (12 * t) / T3 - 6 / T2;
+  H[1] = (6 * t) / T2 - 4 / T;
+  H[2] = 6 / T2 - (12 * t) / T3;
+  H[3] = (6 * t) / T2 - 2 / T;
 }
 
 // CubicHermitePolynomial::UpdateCoeff (:97-104) + Polynomial::GetPoint (:47-58)
@@ -159,9 +188,26 @@ TG_HD void poly_state(const Ctx& c, int s, int poly, double T, double tl, Spline
 }
 
 // Spline::GetPoint(t_global) (spline.cc:80-93)
+// Device: every timed item carries its SegRec row (layout.hip's segment table), so the state is the
+// basis form H . (p0, v0, p1, v1) with the host-precomputed Hermite basis of this (instant,
+// polynomial) — the same polynomial as UpdateCoeff + GetPoint, with no divisions. Host: the
+// reference's own scan and coefficient form (the structure pass must reproduce its ties exactly).
 TG_HD void spline_eval(const Ctx& c, int s, double t, SplinePt& o) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const SegRec& r = c.seg[s];
+  o.poly = r.poly; o.tl = r.tl; o.T = r.T;
+  o.H = &r.H[0][0];
+  for (int e = 0; e < 3; ++e) {
+    const double u0 = xval(c, node_col(c, s, o.poly, kPos, e)), u1 = xval(c, node_col(c, s, o.poly, kVel, e));
+    const double u2 = xval(c, node_col(c, s, o.poly + 1, kPos, e)), u3 = xval(c, node_col(c, s, o.poly + 1, kVel, e));
+    o.p[e] = r.H[0][0] * u0 + r.H[0][1] * u1 + r.H[0][2] * u2 + r.H[0][3] * u3;
+    o.v[e] = r.H[1][0] * u0 + r.H[1][1] * u1 + r.H[1][2] * u2 + r.H[1][3] * u3;
+    o.a[e] = r.H[2][0] * u0 + r.H[2][1] * u1 + r.H[2][2] * u2 + r.H[2][3] * u3;
+  }
+#else
+  o.H = nullptr;
   if (c.seg) {
-    const SegRec r = c.seg[s];
+    const SegRec& r = c.seg[s];
     o.poly = r.poly; o.tl = r.tl; o.T = r.T;
   } else {
     const SplineMeta m = c.spl[s];
@@ -169,29 +215,18 @@ TG_HD void spline_eval(const Ctx& c, int s, double t, SplinePt& o) {
     o.T = c.dur[m.dur_off + o.poly];
   }
   poly_state(c, s, o.poly, o.T, o.tl, o);
+#endif
 }
 
-// GetDerivativeOf{Pos,Vel,Acc}Wrt{Start,End}Node (polynomial.cc:135-234); b = 0 n0.p, 1 n0.v, 2 n1.p, 3 n1.v
-TG_HD void hermite_dpos(double T, double t, double H[4]) {
-  const double T2 = T * T, T3 = T2 * T, t2 = t * t, t3 = t2 * t;
-  H[0] = (2 * t3) / T3 - (3 * t2) / T2 + 1;
-  H[1] = t - (2 * t2) / T + t3 / T2;
-  H[2] = (3 * t2) / T2 - (2 * t3) / T3;
-  H[3] = t3 / T2 - t2 / T;
-}
-TG_HD void hermite_dvel(double T, double t, double H[4]) {
-  const double T2 = T * T, T3 = T2 * T, t2 = t * t;
-  H[0] = (6 * t2) / T3 - (6 * t) / T2;
-  H[1] = (3 * t2) / T2 - (4 * t) / T + 1;
-  H[2] = (6 * t) / T2 - (6 * t2) / T3;
-  H[3] = (3 * t2) / T2 - (2 * t) / T;
-}
-TG_HD void hermite_dacc(double T, double t, double H[4]) {
-  const double T2 = T * T, T3 = T2 * T;
-  H[0] = (12 * t) / T3 - 6 / T2;
-  H[1] = (6 * t) / T2 - 4 / T;
-  H[2] = 6 / T2 - (12 * t) / T3;
-  H[3] = (6 * t) / T2 - 2 / T;
+// Hermite basis of a spline point for derivative d (precomputed on the device, evaluated on the host)
+TG_HD void spline_basis(const SplinePt& o, int d, double H[4]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  for (int b = 0; b < 4; ++b) H[b] = o.H[4 * d + b];
+#else
+  if (d == kPos) hermite_dpos(o.T, o.tl, H);
+  else if (d == kVel) hermite_dvel(o.T, o.tl, H);
+  else hermite_dacc(o.T, o.tl, H);
+#endif
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -359,10 +394,16 @@ TG_HD void ter_basis(const towr_terrain_t& T, int basis, double x, double y, int
     v[2] = req ? ter_dh(T, Y, x, y) : ter_d2h(T, Y, deriv, x, y);
   }
 }
+// Eigen normalized(): v / sqrt(|v|^2) if |v|^2 > 0
 TG_HD void normalize3(const double v[3], double o[3]) {
   const double z = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double s = z > 0 ? 1.0 / sqrt(z) : 1.0;   // one division instead of three
+  o[0] = v[0] * s; o[1] = v[1] * s; o[2] = v[2] * s;
+#else
   if (z > 0) { const double s = sqrt(z); o[0] = v[0] / s; o[1] = v[1] / s; o[2] = v[2] / s; }
   else { o[0] = v[0]; o[1] = v[1]; o[2] = v[2]; }
+#endif
 }
 // GetNormalizedBasis (:62-66)
 TG_HD void ter_nbasis(const towr_terrain_t& T, int basis, double x, double y, double o[3]) {
@@ -427,7 +468,7 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
     const double grav[3] = {0.0, 0.0, -c.rb.m * c.rb.g};
     for (int e = 0; e < 3; ++e) em.g(r0 + LX + e, c.rb.m * L.a[e] - fs[e] - grav[e]);
     double Hp[4], Ha[4];
-    hermite_dpos(L.T, L.tl, Hp); hermite_dacc(L.T, L.tl, Ha);
+    spline_basis(L, kPos, Hp); spline_basis(L, kAcc, Ha);
     for (int r = 0; r < 3; ++r)
       for (int d = 1; d <= 2; ++d) {
         const int e = (r + d) % 3;
@@ -464,7 +505,7 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
       for (int j = 0; j < 3; ++j) Iw[i][j] = RI[i][0] * R[j][0] + RI[i][1] * R[j][1] + RI[i][2] * R[j][2];
     double Iww[3]; mat3_vec(Iw, w, Iww);
     double Hp[4], Hv[4], Ha[4];
-    hermite_dpos(A.T, A.tl, Hp); hermite_dvel(A.T, A.tl, Hv); hermite_dacc(A.T, A.tl, Ha);
+    spline_basis(A, kPos, Hp); spline_basis(A, kVel, Hv); spline_basis(A, kAcc, Ha);
 #pragma unroll 1
     for (int e = 0; e < 3; ++e) {
       double dR[3][3]; euler_dR_axis(q, e, dR);
@@ -521,7 +562,7 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
   spline_eval(c, sp_motion(ee), t, P);
   const double rv[3] = {L.p[0] - P.p[0], L.p[1] - P.p[1], L.p[2] - P.p[2]};
   double H[4];
-  hermite_dpos(F.T, F.tl, H);
+  spline_basis(F, kPos, H);
   for (int r = 0; r < 3; ++r)
     for (int d = 1; d <= 2; ++d) {
       const int e = (r + d) % 3;
@@ -536,13 +577,13 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
       const int col = basis_col(c, sp_force(ee), F.poly, bb, e);
       em(r0 + LX + e, col, -H[bb], col >= 0);
     }
-  hermite_dpos(Tq.T, Tq.tl, H);
+  spline_basis(Tq, kPos, H);
   for (int e = 0; e < 3; ++e)
     for (int bb = 0; bb < 4; ++bb) {
       const int col = basis_col(c, sp_torque(ee), Tq.poly, bb, e);
       em(r0 + AX + e, col, -H[bb], col >= 0);
     }
-  hermite_dpos(P.T, P.tl, H);
+  spline_basis(P, kPos, H);
   for (int r = 0; r < 3; ++r)
     for (int d = 1; d <= 2; ++d) {
       const int e = (r + d) % 3;
@@ -569,13 +610,13 @@ TG_HD void eval_rom(const Ctx& c, const ItemDesc& it, Emit& em) {
   double H[4];
   if (it.group == 0) {
     for (int i = 0; i < 3; ++i) em.g(r0 + i, R[0][i] * rW[0] + R[1][i] * rW[1] + R[2][i] * rW[2]);
-    hermite_dpos(L.T, L.tl, H);
+    spline_basis(L, kPos, H);
     for (int r = 0; r < 3; ++r)
       for (int e = 0; e < 3; ++e)
         for (int bb = 0; bb < 4; ++bb) em(r0 + r, basis_col(c, SP_BASE_LIN, L.poly, bb, e), -R[e][r] * H[bb], true);
   } else if (it.group == 1) {
     // DerivOfRotVecMult(t, r_W, inverse=true): row r = sum_c rW[c] dR[c][r]; row X has no roll terms
-    hermite_dpos(A.T, A.tl, H);
+    spline_basis(A, kPos, H);
     for (int e = 0; e < 3; ++e) {
       double dR[3][3]; euler_dR_axis(q, e, dR);
       for (int r = (e == 0 ? 1 : 0); r < 3; ++r) {
@@ -584,7 +625,7 @@ TG_HD void eval_rom(const Ctx& c, const ItemDesc& it, Emit& em) {
       }
     }
   } else {
-    hermite_dpos(P.T, P.tl, H);
+    spline_basis(P, kPos, H);
     for (int r = 0; r < 3; ++r)
       for (int e = 0; e < 3; ++e)
         for (int bb = 0; bb < 4; ++bb) {
@@ -609,7 +650,7 @@ TG_HD void eval_fdisc(const Ctx& c, const ItemDesc& it, Emit& em) {
   pyramid(n, t1, t2, mu, b);
   for (int i = 0; i < 5; ++i) em.g(r0 + i, dot3(F.p, b[i]));
   double H[4];
-  hermite_dpos(F.T, F.tl, H);
+  spline_basis(F, kPos, H);
   for (int i = 0; i < 5; ++i)
     for (int e = 0; e < 3; ++e)
       for (int bb = 0; bb < 4; ++bb) {
@@ -617,7 +658,7 @@ TG_HD void eval_fdisc(const Ctx& c, const ItemDesc& it, Emit& em) {
         em(r0 + i, col, b[i][e] * H[bb], col >= 0);
       }
   if (c.fdisc_motion) {   // AccumulateScaledRowJacobian: skipped when scale == 0.0 (:58)
-    hermite_dpos(P.T, P.tl, H);
+    spline_basis(P, kPos, H);
     for (int dim = 0; dim < 2; ++dim) {
       double dn[3], dt1[3], dt2[3], db[5][3];
       ter_d_nbasis(*c.ter, 0, dim, P.p[0], P.p[1], dn);
@@ -682,10 +723,10 @@ TG_HD void eval_bmot(const Ctx& c, const ItemDesc& it, Emit& em) {
   spline_eval(c, SP_BASE_ANG, it.t, A);
   for (int e = 0; e < 3; ++e) { em.g(it.row0 + LX + e, L.p[e]); em.g(it.row0 + AX + e, A.p[e]); }
   double H[4];
-  hermite_dpos(A.T, A.tl, H);
+  spline_basis(A, kPos, H);
   for (int e = 0; e < 3; ++e)
     for (int bb = 0; bb < 4; ++bb) em(it.row0 + AX + e, basis_col(c, SP_BASE_ANG, A.poly, bb, e), H[bb], true);
-  hermite_dpos(L.T, L.tl, H);
+  spline_basis(L, kPos, H);
   for (int e = 0; e < 3; ++e)
     for (int bb = 0; bb < 4; ++bb) em(it.row0 + LX + e, basis_col(c, SP_BASE_LIN, L.poly, bb, e), H[bb], true);
 }
@@ -702,9 +743,17 @@ TG_HD void eval_sacc(const Ctx& c, const ItemDesc& it, Emit& em) {
   for (int e = 0; e < 3; ++e) em.g(it.row0 + e, a.a[e] - b.a[e]);
   double Hp[4], Hn[4];
   hermite_dacc(Tp, Tp, Hp); hermite_dacc(Tn, 0.0, Hn);
+  // acc_prev - acc_next; node j+1 belongs to both polynomials: its two contributions are emitted
+  // back to back so the emitter can merge them (emit order: n_j.p, n_j.v, n_j+1.p x2, n_j+1.v x2, n_j+2.p, n_j+2.v)
   for (int e = 0; e < 3; ++e) {
-    for (int bb = 0; bb < 4; ++bb) em(it.row0 + e, basis_col(c, s, j, bb, e), Hp[bb], true);
-    for (int bb = 0; bb < 4; ++bb) em(it.row0 + e, basis_col(c, s, j + 1, bb, e), -Hn[bb], true);
+    em(it.row0 + e, basis_col(c, s, j, 0, e), Hp[0], true);
+    em(it.row0 + e, basis_col(c, s, j, 1, e), Hp[1], true);
+    em(it.row0 + e, basis_col(c, s, j, 2, e), Hp[2], true);
+    em(it.row0 + e, basis_col(c, s, j + 1, 0, e), -Hn[0], true);
+    em(it.row0 + e, basis_col(c, s, j, 3, e), Hp[3], true);
+    em(it.row0 + e, basis_col(c, s, j + 1, 1, e), -Hn[1], true);
+    em(it.row0 + e, basis_col(c, s, j + 1, 2, e), -Hn[2], true);
+    em(it.row0 + e, basis_col(c, s, j + 1, 3, e), -Hn[3], true);
   }
 }
 

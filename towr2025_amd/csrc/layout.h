@@ -58,10 +58,6 @@ struct Layout {
   int64_t type_bytes[IT_COUNT] = {};
 };
 
-// slot-table flag: this candidate adds to a slot an earlier candidate of the same item stored to
-constexpr int32_t kSlotAccumulate = 1 << 30;
-constexpr int32_t kSlotMask = kSlotAccumulate - 1;
-
 // LDS tile caps (doubles of CSR values / rows per tile)
 constexpr int kTileValueCap = 8192;
 constexpr int kTileRowCap = 512;

@@ -417,6 +417,9 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
           SegRec r{};
           r.poly = seg_lookup(L.dur.data() + L.spl[sp].dur_off, L.spl[sp].n_polys, it.t, &r.tl);
           r.T = L.dur[L.spl[sp].dur_off + r.poly];
+          hermite_dpos(r.T, r.tl, r.H[kPos]);   // polynomial.cc:135-234, batch-invariant
+          hermite_dvel(r.T, r.tl, r.H[kVel]);
+          hermite_dacc(r.T, r.tl, r.H[kAcc]);
           L.segs.push_back(r);
         }
       }
@@ -473,13 +476,20 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
   for (size_t i = 0; i < L.items.size(); ++i) {
     L.items[i].slot = item_cand_begin[i];
     L.items[i].ncand = item_cand_begin[i + 1] - item_cand_begin[i];
-    // the first contribution to a slot is a plain store, later ones (duplicate columns, e.g. the two
-    // nodes of a stance polynomial sharing one variable) accumulate: kSlotAccumulate marks them
+    // The device merges contributions to one slot (duplicate columns, e.g. the two nodes of a
+    // stance polynomial sharing one variable) only when they are adjacent among the item's present
+    // candidates; every item's emission order is written so that they are — verified here.
     std::vector<int32_t> seen;
+    int32_t prev = -1;
+    const bool merges = type_merges(L.items[i].type);
     for (int32_t q = item_cand_begin[i]; q < item_cand_begin[i + 1]; ++q) {
       if (L.slots[q] < 0) continue;
-      if (std::find(seen.begin(), seen.end(), L.slots[q]) != seen.end()) L.slots[q] |= kSlotAccumulate;
-      else seen.push_back(L.slots[q]);
+      if ((L.slots[q] != prev || !merges) && std::find(seen.begin(), seen.end(), L.slots[q]) != seen.end()) {
+        err = "internal: non-adjacent duplicate candidate in item type " + std::to_string(L.items[i].type);
+        return TOWR_ERR_INVALID;
+      }
+      seen.push_back(L.slots[q]);
+      prev = L.slots[q];
     }
   }
 

@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -48,25 +49,34 @@ struct KParams {
   RobotC rb;
 };
 
-// Accumulates candidate j into the LDS tile at its CSR slot (slot table transposed per tile: one
-// coalesced load per wave per candidate); the candidate's column is not needed on the device.
-template <int STRIDE>
-struct LdsEmit {
+// Stores candidate j at its CSR slot (slot table transposed per tile: one coalesced load per wave
+// per candidate; the candidate's column is never needed on the device). Contributions of duplicate
+// columns are adjacent among an item's present candidates (checked at build time) and are summed
+// in registers, so every slot receives exactly one plain store: no read-modify-write.
+// `out` / `gout` are either the LDS tile (rebased so that out[slot] works) or the problem's rows
+// of V / G in HBM; nullptr disables the output.
+template <int STRIDE, bool MERGE>
+struct MergeEmit {
   const int32_t* slot;
+  double* out;
+  double* gout;
   int j;
-  double* vt;
-  int v0;
-  double* gt;
-  int r0;
-  __device__ __forceinline__ void g(int row, double v) { gt[row - r0] = v; }
+  int ps;
+  double pv;
+  __device__ __forceinline__ void g(int row, double v) { if (gout) gout[row] = v; }
   __device__ __forceinline__ void operator()(int, int, double v, bool) {
     const int s = slot[j * STRIDE];
-    if (s >= 0) {
-      if (s & kSlotAccumulate) vt[(s & kSlotMask) - v0] += v;   // rare: duplicate column
-      else vt[s - v0] = v;                                      // plain store, no read-modify-write
-    }
     ++j;
+    if (s < 0) return;
+    if constexpr (!MERGE) {
+      if (out) out[s] = v;
+    } else {
+      if (s == ps) { pv += v; return; }
+      if (ps >= 0 && out) out[ps] = pv;
+      ps = s; pv = v;
+    }
   }
+  __device__ __forceinline__ void flush() { if (MERGE && ps >= 0 && out) out[ps] = pv; }
 };
 
 template <int TYPE, class Emit>
@@ -98,13 +108,17 @@ __device__ __forceinline__ void copy_out(const double* __restrict__ src, double*
   if (((n - head) & 1) && threadIdx.x == 0) dst[n - 1] = src[n - 1];
 }
 
-// One block = one LDS tile (consecutive instances of one constraint set) of one problem; one item
-// per thread, laid out so every wave runs a single code path. x is read through L1/L2 (each
-// problem's x is ~9 KB and shared by all its tiles, which the mapping below keeps on one XCD).
-// kernels whose items gather many spline nodes stage x and the node->column table in LDS
+// One block = one tile (consecutive instances of one constraint set) of one problem; one item per
+// thread, laid out so every wave runs a single code path. Blocks of one problem share an XCD (the
+// mapping below), so its ~9 KB x is fetched from HBM once and then served by that XCD's L2.
+//   LDS_TILE = false: every lane stores its values straight to HBM. A wave's lanes hold consecutive
+//     instances, whose CSR rows form one contiguous range, so the XCD's L2 merges the partial lines
+//     before they leave; no LDS tile limits occupancy.
+//   LDS_TILE = true: values are staged in an LDS tile and written with 16-byte coalesced stores.
+// Kernels whose items gather many spline nodes stage x and the node->column table in LDS.
 constexpr bool stages_x(int type) { return type == IT_DYN || type == IT_ROM; }
 
-template <int TYPE, int BLOCK>
+template <int TYPE, int BLOCK, bool LDS_TILE>
 __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_kernel(KParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int total = P.B * P.ntiles;
@@ -114,9 +128,8 @@ __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_ker
   if (w >= total) return;
   const int b = w / P.ntiles;
   const TileDesc T = P.tiles[P.tile0 + w % P.ntiles];
-  const int nv = T.v1 - T.v0, nr = T.r1 - T.r0;
-  double* vt = smem;                       // every slot of [v0, v1) is stored by some candidate
-  double* gt = smem + P.lds_rows_off;
+  double* Vb = P.V + (int64_t)b * P.ldv;
+  double* Gb = P.G + (int64_t)b * P.ldg;
   const double* xg = P.X + (int64_t)b * P.ldx;
   const double* xsrc = xg;
   const int32_t* ncsrc = P.nodecol;
@@ -135,32 +148,37 @@ __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_ker
     c.x = xsrc; c.nodecol = ncsrc; c.spl = P.spl; c.dur = P.dur;
     c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
     c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
-    LdsEmit<BLOCK> em{P.slots + it.slot, 0, vt, T.v0, gt, T.r0};
+    double *out, *gout;
+    if constexpr (LDS_TILE) { out = smem - T.v0; gout = smem + P.lds_rows_off - T.r0; }
+    else { out = P.want_jac ? Vb : nullptr; gout = P.want_g ? Gb : nullptr; }
+    MergeEmit<BLOCK, type_merges(TYPE)> em{P.slots + it.slot, out, gout, 0, -1, 0.0};
     eval_typed<TYPE>(c, it, em);
+    em.flush();
   }
-  __syncthreads();
-  if (P.want_jac) copy_out(vt, P.V + (int64_t)b * P.ldv + T.v0, nv);
-  if (P.want_g) {
-    double* Gb = P.G + (int64_t)b * P.ldg;
-    for (int i = threadIdx.x; i < nr; i += BLOCK) Gb[T.r0 + i] = gt[i];
+  if constexpr (LDS_TILE) {
+    __syncthreads();
+    if (P.want_jac) copy_out(smem, Vb + T.v0, T.v1 - T.v0);
+    if (P.want_g)
+      for (int i = threadIdx.x; i < T.r1 - T.r0; i += BLOCK) Gb[T.r0 + i] = smem[P.lds_rows_off + i];
   }
 }
 
-typedef void (*KernelFn)(KParams);
-const void* kernel_for(int type) {
+template <bool LDS_TILE>
+const void* kernel_for_mode(int type) {
   switch (type) {
-    case IT_DYN: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_DYN, 256>);
-    case IT_ROM: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_ROM, 192>);
-    case IT_FDISC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_FDISC, 64>);
-    case IT_FNODE: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_FNODE, 64>);
-    case IT_TERR: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_TERR, 64>);
-    case IT_BMOT: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_BMOT, 64>);
-    case IT_SACC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_SACC, 64>);
-    case IT_BHGT: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_BHGT, 64>);
-    case IT_SWING: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_SWING, 64>);
+    case IT_DYN: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_DYN, 256, LDS_TILE>);
+    case IT_ROM: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_ROM, 192, LDS_TILE>);
+    case IT_FDISC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_FDISC, 64, LDS_TILE>);
+    case IT_FNODE: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_FNODE, 64, LDS_TILE>);
+    case IT_TERR: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_TERR, 64, LDS_TILE>);
+    case IT_BMOT: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_BMOT, 64, LDS_TILE>);
+    case IT_SACC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_SACC, 64, LDS_TILE>);
+    case IT_BHGT: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_BHGT, 64, LDS_TILE>);
+    case IT_SWING: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_SWING, 64, LDS_TILE>);
   }
   return nullptr;
 }
+const void* kernel_for(int type, bool lds_tile) { return lds_tile ? kernel_for_mode<true>(type) : kernel_for_mode<false>(type); }
 
 }  // namespace
 
@@ -183,6 +201,7 @@ struct towr_gpu_handle_s {
   towr_terrain_t* d_terrain = nullptr;      // base terrain (1 entry)
   towr_terrain_t* d_bterrain = nullptr;     // per-problem batch terrains
   int32_t bterrain_n = 0;
+  bool lds_tile = false;                    // output path (TOWR_GPU_OUTPUT=lds|direct), see the kernel
   // staging for host-pointer entry points
   double *d_x = nullptr, *d_g = nullptr, *d_v = nullptr;
   double *h_x = nullptr, *h_g = nullptr, *h_v = nullptr;
@@ -221,8 +240,8 @@ int bind(towr_gpu_handle h) {
   return TOWR_OK;
 }
 
-size_t lds_bytes(const Layout& L, int t) {
-  size_t d = (size_t)L.type_lds[t];
+size_t lds_bytes(const Layout& L, int t, bool lds_tile) {
+  size_t d = lds_tile ? (size_t)L.type_lds[t] : 0;
   if (stages_x(t)) d += (size_t)((L.n + 1) & ~1) + (L.nodecol.size() + 1) / 2;
   return sizeof(double) * d;
 }
@@ -244,15 +263,15 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
     P.B = B; P.tile0 = L.type_tile0[t]; P.ntiles = nt;
     P.lds_rows_off = L.type_lds_rows_off[t];
     P.n = L.n; P.n_pad = (L.n + 1) & ~1; P.n_nodecol = (int32_t)L.nodecol.size();
-    P.lds_x_off = L.type_lds[t];
+    P.lds_x_off = h->lds_tile ? L.type_lds[t] : 0;
     P.want_g = want_g; P.want_jac = want_jac; P.fdisc_motion = L.fdisc_motion;
     P.rb = L.rb;
     const int64_t total = (int64_t)B * nt;
     const int64_t grid = ((total + 7) / 8) * 8;
     if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
     void* args[] = {&P};
-    HIPCHK(h, hipLaunchKernel(kernel_for(t), dim3((unsigned)grid), dim3((unsigned)L.type_block[t]), args,
-                              lds_bytes(L, t), s));
+    HIPCHK(h, hipLaunchKernel(kernel_for(t, h->lds_tile), dim3((unsigned)grid), dim3((unsigned)L.type_block[t]), args,
+                              lds_bytes(L, t, h->lds_tile), s));
   }
   return TOWR_OK;
 }
@@ -342,10 +361,14 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
       (r = upload(h, &h->d_tiles, L.tiles)) || (r = upload(h, &h->d_nodecol, L.nodecol)) ||
       (r = upload(h, &h->d_spl, L.spl)) || (r = upload(h, &h->d_dur, L.dur)) || (r = upload(h, &h->d_segs, L.segs)) || (r = upload(h, &h->d_terrain, ter)))
     return bail(r);
+  {
+    const char* mode = std::getenv("TOWR_GPU_OUTPUT");
+    h->lds_tile = mode && std::strcmp(mode, "lds") == 0;
+  }
   for (int t = 0; t < IT_COUNT; ++t) {
-    const size_t lds = lds_bytes(L, t);
+    const size_t lds = lds_bytes(L, t, h->lds_tile);
     if (lds > 160 * 1024) { h->err = "tile too large for LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
-    if (lds > 64 * 1024 && hipFuncSetAttribute(kernel_for(t), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+    if (lds > 64 * 1024 && hipFuncSetAttribute(kernel_for(t, h->lds_tile), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
       h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
     }
   }
