@@ -4,20 +4,22 @@
 #include "../../towr2025_amd/csrc/layout.h"
 
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <string>
 
 using namespace tg;
 
 namespace {
-// same semantics as the kernel's MergeEmit: adjacent duplicates summed, one plain store per slot
+// same semantics as the kernel's TileEmit: 8 tile-relative positions per SlotGroup, adjacent
+// duplicates summed, one plain store per position
 struct AccEmit {
-  const int32_t* slot; int stride; int j; double* v; double* gout; int ps = -1; double pv = 0.0;
+  const SlotGroup* slot; int stride; double* v; double* gout; int j = 0; int ps = -1; double pv = 0.0;
   void g(int row, double val) { gout[row] = val; }
   void operator()(int, int, double val, bool) {
-    int s = slot[j * stride];
+    const int s = slot_pick(slot[(j / 8) * stride], j % 8);
     ++j;
-    if (s < 0) return;
+    if (s == kSlotAbsent) return;
     if (s == ps) { pv += val; return; }
     if (ps >= 0) v[ps] = pv;
     ps = s; pv = val;
@@ -35,12 +37,41 @@ extern "C" int emu_eval(const towr_problem_desc_t* d, const double* x, double* g
   Ctx c{};
   c.x = x; c.nodecol = L.nodecol.data(); c.spl = L.spl.data(); c.dur = L.dur.data();
   c.ter = &L.terrain; c.rb = L.rb; c.fdisc_motion = L.fdisc_motion;
-  for (const ItemDesc& it : L.items) {
-    if (it.type == IT_NONE) continue;
-    AccEmit em{L.slots.data() + it.slot, L.type_block[it.type], 0, v, g};
-    c.seg = it.seg >= 0 ? L.segs.data() + (size_t)it.seg * L.spl.size() : nullptr;
-    eval_item(c, it, em);
-    em.flush();
+  for (const TileDesc& td : L.tiles)
+    for (int l = td.i0; l < td.i1; ++l) {
+      const ItemDesc& it = L.items[l];
+      if (it.type == IT_NONE) continue;
+      AccEmit em{L.slot_groups.data() + it.slot, td.i1 - td.i0, v + td.v0, g};
+      c.seg = it.seg >= 0 ? L.segs.data() + (size_t)it.seg * L.spl.size() : nullptr;
+      eval_item(c, it, em);
+      em.flush();
+    }
+  return 0;
+}
+
+// layout statistics per item type (tiles, lanes used, candidates per wave, values per tile)
+extern "C" int emu_stats(const towr_problem_desc_t* d) {
+  Layout L; std::string e;
+  if (build_layout(*d, L, e)) return -1;
+  std::printf("n %d m %d nnz %lld\n", L.n, L.m, (long long)L.nnz);
+  for (int t = 0; t < IT_COUNT; ++t) {
+    int nt = L.type_tile0[t + 1] - L.type_tile0[t];
+    if (!nt) continue;
+    long used = 0, lanes = 0, candw = 0, cand = 0; int maxv = 0;
+    for (int ti = L.type_tile0[t]; ti < L.type_tile0[t + 1]; ++ti) {
+      const TileDesc& td = L.tiles[ti];
+      maxv = std::max(maxv, td.v1 - td.v0);
+      for (int w = td.i0; w < td.i1; w += 64) {
+        int mc = 0;
+        for (int l = w; l < std::min(w + 64, td.i1); ++l) {
+          ++lanes;
+          if (L.items[l].type != IT_NONE) { ++used; mc = std::max(mc, L.items[l].ncand); cand += L.items[l].ncand; }
+        }
+        candw += mc;
+      }
+    }
+    std::printf("type %d: tiles %d block %d lanes %ld used %ld maxvals %d cand %ld sum_wave_maxcand %ld lds %d\n", t, nt,
+                L.type_block[t], lanes, used, maxv, cand, candw, L.type_lds[t]);
   }
   return 0;
 }

@@ -81,7 +81,19 @@ struct SegRec {
   double tl, T;
   int32_t poly, reserved;
   double H[3][4];   // d{pos,vel,acc}(tl)/d{n0.p, n0.v, n1.p, n1.v}: batch-invariant Hermite basis
+  int32_t col[4][3];   // x column of basis value b, dim e (device numbering: a constant node -> n, x[n] = 0)
 };
+
+// Slot table entry: 8 tile-relative CSR positions (uint16, 0xFFFF = candidate absent) of one lane's
+// candidates 8g..8g+7, one 16-byte load per lane; group g of lane l of a tile sits at
+// tile_base + g * block + l (a wave's load is one coalesced 1 KiB access)
+struct alignas(16) SlotGroup { uint32_t w[4]; };
+constexpr int kSlotAbsent = 0xFFFF;
+TG_HD int slot_pick(const SlotGroup& q, int k) {   // select chain: k may be a runtime value
+  const uint32_t lo = (k & 2) ? q.w[1] : q.w[0], hi = (k & 2) ? q.w[3] : q.w[2];
+  const uint32_t w = (k & 4) ? hi : lo;
+  return (k & 1) ? (int)(w >> 16) : (int)(w & 0xFFFFu);
+}
 
 // item kinds whose emission can contain duplicate columns (stance polynomials whose two nodes share
 // one variable, junction nodes of SplineAcc); the others never do (checked at build time)
@@ -123,7 +135,15 @@ TG_HD int seg_lookup(const double* d, int n, double tg, double* tl) {
   return id;
 }
 
-TG_HD double xval(const Ctx& c, int col) { return col >= 0 ? c.x[col] : 0.0; }
+// x value of a node-value column; -1 = a constant node value (0). The device's staged x carries a
+// zero at index n and its node tables point constant values there, so its loads need no branch.
+TG_HD double xval(const Ctx& c, int col) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return c.x[col];
+#else
+  return col >= 0 ? c.x[col] : 0.0;
+#endif
+}
 TG_HD int node_col(const Ctx& c, int s, int node, int deriv, int dim) {
   return c.nodecol[(c.spl[s].node_off + node) * 6 + deriv * 3 + dim];
 }
@@ -198,8 +218,7 @@ TG_HD void spline_eval(const Ctx& c, int s, double t, SplinePt& o) {
   o.poly = r.poly; o.tl = r.tl; o.T = r.T;
   o.H = &r.H[0][0];
   for (int e = 0; e < 3; ++e) {
-    const double u0 = xval(c, node_col(c, s, o.poly, kPos, e)), u1 = xval(c, node_col(c, s, o.poly, kVel, e));
-    const double u2 = xval(c, node_col(c, s, o.poly + 1, kPos, e)), u3 = xval(c, node_col(c, s, o.poly + 1, kVel, e));
+    const double u0 = c.x[r.col[0][e]], u1 = c.x[r.col[1][e]], u2 = c.x[r.col[2][e]], u3 = c.x[r.col[3][e]];
     o.p[e] = r.H[0][0] * u0 + r.H[0][1] * u1 + r.H[0][2] * u2 + r.H[0][3] * u3;
     o.v[e] = r.H[1][0] * u0 + r.H[1][1] * u1 + r.H[1][2] * u2 + r.H[1][3] * u3;
     o.a[e] = r.H[2][0] * u0 + r.H[2][1] * u1 + r.H[2][2] * u2 + r.H[2][3] * u3;
@@ -437,10 +456,9 @@ template <class Emit>
 TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
   const double t = it.t;
   const int r0 = it.row0, E = c.rb.n_ee;
-  SplinePt L;
-  spline_eval(c, SP_BASE_LIN, t, L);
   if (it.group == 0) {
     // g (GetDynamicViolation :76-102) + d/d base-lin (GetJacobianWrtBaseLin :104-122)
+    SplinePt L; spline_eval(c, SP_BASE_LIN, t, L);
     SplinePt A; spline_eval(c, SP_BASE_ANG, t, A);
     const Trig q = trig(A.p);
     double R[3][3]; euler_R(q, R);
@@ -556,7 +574,8 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
   }
   // group 2 + ee: force (GetJacobianWrtForce :168-180), torque (:182-191), motion (:193-204)
   const int ee = it.group - 2;
-  SplinePt F, Tq, P;
+  SplinePt L, F, Tq, P;
+  spline_eval(c, SP_BASE_LIN, t, L);
   spline_eval(c, sp_force(ee), t, F);
   spline_eval(c, sp_torque(ee), t, Tq);
   spline_eval(c, sp_motion(ee), t, P);

@@ -38,7 +38,8 @@ struct Layout {
   std::vector<double> dur;
   std::vector<SegRec> segs;     // (2 + 4 n_ee) records per time instant
   std::vector<ItemDesc> items;
-  std::vector<int32_t> slots;
+  std::vector<int32_t> slots;     // build-time: candidate -> global CSR position (or -1)
+  std::vector<SlotGroup> slot_groups;   // device slot table (see SlotGroup); item.slot indexes it
   std::vector<int64_t> row_ptr;
   std::vector<int32_t> col;
   std::vector<TileDesc> tiles;
@@ -60,7 +61,7 @@ struct Layout {
 
 // LDS tile caps (doubles of CSR values / rows per tile)
 constexpr int kTileValueCap = 8192;
-constexpr int kTileRowCap = 512;
+constexpr int kTileRowCap = 2048;
 
 // Launch geometry of each item type (wave-uniform: each wave of a block runs one code path)
 struct TypeSpec { int block; int max_inst; };

@@ -420,6 +420,11 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
           hermite_dpos(r.T, r.tl, r.H[kPos]);   // polynomial.cc:135-234, batch-invariant
           hermite_dvel(r.T, r.tl, r.H[kVel]);
           hermite_dacc(r.T, r.tl, r.H[kAcc]);
+          for (int bb = 0; bb < 4; ++bb)
+            for (int e = 0; e < 3; ++e) {
+              const int32_t col = L.nodecol[(size_t)(L.spl[sp].node_off + r.poly + (bb >> 1)) * 6 + (bb & 1) * 3 + e];
+              r.col[bb][e] = col >= 0 ? col : L.n;
+            }
           L.segs.push_back(r);
         }
       }
@@ -501,16 +506,12 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
     std::vector<std::vector<ItemDesc>> per_type_items(IT_COUNT);
     size_t i = 0;
     while (i < L.items.size()) {
-      // one constraint set = maximal run of items with the same constraint row block
+      // maximal run of items of one type (adjacent constraint sets of one kind, e.g. the
+      // RangeOfMotion sets of all feet, share tiles: their rows are contiguous)
       const int type = L.items[i].type;
-      int ci = -1;
-      for (int q = 0; q < (int)L.cons.size(); ++q)
-        if (L.items[i].row0 >= L.cons[q].row0 && L.items[i].row0 < L.cons[q].row0 + L.cons[q].rows) { ci = q; break; }
-      if (ci < 0) { err = "internal: item outside every constraint set"; return TOWR_ERR_INVALID; }
-      const int set_end_row = L.cons[ci].row0 + L.cons[ci].rows;
       std::vector<Inst> insts;
       size_t j = i;
-      while (j < L.items.size() && L.items[j].type == type && L.items[j].row0 < set_end_row && L.items[j].row0 >= L.cons[ci].row0) {
+      while (j < L.items.size() && L.items[j].type == type) {
         size_t k = j;
         while (k < L.items.size() && item_inst[k] == item_inst[j]) ++k;
         insts.push_back({(int32_t)j, (int32_t)(k - j)});
@@ -576,24 +577,33 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
       L.type_lds[t] = L.type_lds_rows_off[t] + ((maxr + 1) & ~1);
     }
     L.type_tile0[IT_COUNT] = (int32_t)L.tiles.size();
-    // slot table per tile, transposed: candidate j of lane l at base + j * block + l, so that one
-    // wave's j-th slot load is a single coalesced 256-byte access
-    std::vector<int32_t> slots;
+    // slot table per tile: lane l's candidates 8g..8g+7 in group g at base + g * block + l, as
+    // tile-relative uint16 positions; two spare groups per lane absorb the kernel's prefetch
+    std::vector<SlotGroup> groups;
     for (const TileDesc& td : L.tiles) {
       const int block = td.i1 - td.i0;
       int maxc = 0;
       for (int l = 0; l < block; ++l) maxc = std::max(maxc, items[td.i0 + l].type == IT_NONE ? 0 : items[td.i0 + l].ncand);
-      const size_t base = slots.size();
-      slots.resize(base + (size_t)maxc * block, -1);
+      const int ng = (maxc + 7) / 8 + 2;
+      const size_t base = groups.size();
+      SlotGroup none; for (uint32_t& w : none.w) w = 0xFFFFFFFFu;
+      groups.resize(base + (size_t)ng * block, none);
       for (int l = 0; l < block; ++l) {
         ItemDesc& it = items[td.i0 + l];
-        if (it.type == IT_NONE) { it.slot = (int32_t)base + l; continue; }
-        for (int j = 0; j < it.ncand; ++j) slots[base + (size_t)j * block + l] = L.slots[it.slot + j];
+        if (it.type != IT_NONE)
+          for (int j = 0; j < it.ncand; ++j) {
+            const int32_t g = L.slots[it.slot + j];
+            const uint32_t rel = g < 0 ? (uint32_t)kSlotAbsent : (uint32_t)(g - td.v0);
+            if (g >= 0 && (g < td.v0 || g >= td.v1 || rel >= (uint32_t)kSlotAbsent)) { err = "internal: slot outside its tile"; return TOWR_ERR_INVALID; }
+            uint32_t& w = groups[base + (size_t)(j / 8) * block + l].w[(j % 8) / 2];
+            const int sh = (j & 1) ? 16 : 0;
+            w = (w & ~(0xFFFFu << sh)) | (rel << sh);
+          }
         it.slot = (int32_t)(base + l);
       }
     }
-    if (slots.size() >= (size_t)INT32_MAX) { err = "slot table too large"; return TOWR_ERR_UNSUPPORTED; }
-    L.slots.swap(slots);
+    if (groups.size() >= (size_t)INT32_MAX) { err = "slot table too large"; return TOWR_ERR_UNSUPPORTED; }
+    L.slot_groups.swap(groups);
     L.items.swap(items);
     for (int t = 0; t < IT_COUNT; ++t) {
       int64_t nv = 0, nr = 0;
@@ -615,6 +625,7 @@ TypeSpec type_spec(int type, int n_ee) {
   switch (type) {
     case IT_DYN: return {256, std::max(1, std::min(64, 128 / std::max(1, n_ee)))};  // waves: g0 | g1 | ee, ee
     case IT_ROM: return {192, 64};                                                      // waves: g0 | g1 | g2
+    case IT_FDISC: return {256, 256};
     default: return {64, 64};
   }
 }

@@ -32,7 +32,7 @@ struct KParams {
   double* G; int64_t ldg;
   double* V; int64_t ldv;
   const ItemDesc* items;
-  const int32_t* slots;
+  const SlotGroup* slots;
   const TileDesc* tiles;
   const int32_t* nodecol;
   const SplineMeta* spl;
@@ -43,40 +43,47 @@ struct KParams {
   int32_t terrain_per_problem;
   int32_t B, tile0, ntiles;
   int32_t lds_rows_off;          // start of the g buffer in the dynamic LDS (doubles)
-  int32_t lds_x_off;             // start of the staged x / node-column table (stages_x kernels)
+  int32_t lds_x_off;             // start of the staged x (+ zero slot) and node-column table
   int32_t n, n_pad, n_nodecol;
   int32_t want_g, want_jac, fdisc_motion;
   RobotC rb;
 };
 
-// Stores candidate j at its CSR slot (slot table transposed per tile: one coalesced load per wave
-// per candidate; the candidate's column is never needed on the device). Contributions of duplicate
-// columns are adjacent among an item's present candidates (checked at build time) and are summed
-// in registers, so every slot receives exactly one plain store: no read-modify-write.
-// `out` / `gout` are either the LDS tile (rebased so that out[slot] works) or the problem's rows
-// of V / G in HBM; nullptr disables the output.
-template <int STRIDE, bool MERGE>
-struct MergeEmit {
-  const int32_t* slot;
-  double* out;
-  double* gout;
-  int j;
-  int ps;
-  double pv;
-  __device__ __forceinline__ void g(int row, double v) { if (gout) gout[row] = v; }
+// Stores candidate j of this lane into the LDS tile at its tile-relative CSR position. Positions
+// come 8 per 16-byte SlotGroup; the next group is prefetched while the current one is consumed, so
+// the slot-table latency (L2: the table is shared by every problem of the batch) hides behind 8
+// candidates of arithmetic. The candidate's column is never needed on the device. Contributions to
+// one position (duplicate columns, e.g. the two nodes of a stance polynomial sharing one variable)
+// are adjacent among an item's present candidates (checked at build time) and summed in registers
+// (MERGE kinds), so every position receives exactly one plain LDS store.
+template <int BLOCK, bool MERGE>
+struct TileEmit {
+  const SlotGroup* slot;   // this lane's group 0; group g at slot[g * BLOCK]
+  double* out;             // LDS tile, tile-relative
+  double* gout;            // LDS g rows, tile-relative
+  SlotGroup cur, nxt;      // groups g, g+1
+  int j = 0;
+  int ps = -1;
+  double pv = 0.0;
+  __device__ __forceinline__ TileEmit(const SlotGroup* s, double* o, double* go) : slot(s), out(o), gout(go) {
+    cur = s[0];
+    nxt = s[BLOCK];
+  }
+  __device__ __forceinline__ void g(int row, double v) { gout[row] = v; }
   __device__ __forceinline__ void operator()(int, int, double v, bool) {
-    const int s = slot[j * STRIDE];
+    const int s = slot_pick(cur, j & 7);
     ++j;
-    if (s < 0) return;
+    if ((j & 7) == 0) { cur = nxt; nxt = slot[((j >> 3) + 1) * BLOCK]; }
+    if (s == kSlotAbsent) return;
     if constexpr (!MERGE) {
-      if (out) out[s] = v;
+      out[s] = v;
     } else {
       if (s == ps) { pv += v; return; }
-      if (ps >= 0 && out) out[ps] = pv;
+      if (ps >= 0) out[ps] = pv;
       ps = s; pv = v;
     }
   }
-  __device__ __forceinline__ void flush() { if (MERGE && ps >= 0 && out) out[ps] = pv; }
+  __device__ __forceinline__ void flush() { if (MERGE && ps >= 0) out[ps] = pv; }
 };
 
 template <int TYPE, class Emit>
@@ -90,6 +97,24 @@ __device__ __forceinline__ void eval_typed(const Ctx& c, const ItemDesc& it, Emi
   else if constexpr (TYPE == IT_SACC) eval_sacc(c, it, em);
   else if constexpr (TYPE == IT_BHGT) eval_height(c, it, SP_BASE_LIN, it.p0, em);
   else if constexpr (TYPE == IT_SWING) eval_swing(c, it, em);
+}
+
+// global -> LDS copy of n16 16-byte units: each thread issues up to K independent loads before its
+// first LDS write, so the staging costs one memory latency rather than one per loop trip
+template <int BLOCK>
+__device__ __forceinline__ void stage16(uint4* __restrict__ dst, const uint4* __restrict__ src, int n16) {
+  for (int i = threadIdx.x; i < n16; i += 4 * BLOCK) {   // 4 loads in flight per thread
+    const int i1 = i + BLOCK, i2 = i + 2 * BLOCK, i3 = i + 3 * BLOCK;
+    const uint4 r0 = src[i];
+    uint4 r1{}, r2{}, r3{};
+    if (i1 < n16) r1 = src[i1];
+    if (i2 < n16) r2 = src[i2];
+    if (i3 < n16) r3 = src[i3];
+    dst[i] = r0;
+    if (i1 < n16) dst[i1] = r1;
+    if (i2 < n16) dst[i2] = r2;
+    if (i3 < n16) dst[i3] = r3;
+  }
 }
 
 // LDS -> HBM, 16-byte stores where the destination allows it
@@ -108,17 +133,16 @@ __device__ __forceinline__ void copy_out(const double* __restrict__ src, double*
   if (((n - head) & 1) && threadIdx.x == 0) dst[n - 1] = src[n - 1];
 }
 
-// One block = one tile (consecutive instances of one constraint set) of one problem; one item per
+// One block = one tile (consecutive instances of one constraint kind) of one problem; one item per
 // thread, laid out so every wave runs a single code path. Blocks of one problem share an XCD (the
 // mapping below), so its ~9 KB x is fetched from HBM once and then served by that XCD's L2.
-//   LDS_TILE = false: every lane stores its values straight to HBM. A wave's lanes hold consecutive
-//     instances, whose CSR rows form one contiguous range, so the XCD's L2 merges the partial lines
-//     before they leave; no LDS tile limits occupancy.
-//   LDS_TILE = true: values are staged in an LDS tile and written with 16-byte coalesced stores.
-// Kernels whose items gather many spline nodes stage x and the node->column table in LDS.
-constexpr bool stages_x(int type) { return type == IT_DYN || type == IT_ROM; }
+// Candidates land in an LDS tile (no global store before the end, so no load ever waits behind a
+// store: gfx950's vmcnt counts both); the tile's contiguous CSR range and g rows then leave with
+// 16-byte coalesced stores. Every kernel stages the problem's x in LDS (spline items gather their
+// nodes through the segment record's columns); node-value kinds also stage the node->column table.
+constexpr bool stages_nodes(int type) { return type == IT_FNODE || type == IT_TERR || type == IT_SACC || type == IT_BHGT || type == IT_SWING; }
 
-template <int TYPE, int BLOCK, bool LDS_TILE>
+template <int TYPE, int BLOCK>
 __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_kernel(KParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int total = P.B * P.ntiles;
@@ -131,54 +155,53 @@ __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_ker
   double* Vb = P.V + (int64_t)b * P.ldv;
   double* Gb = P.G + (int64_t)b * P.ldg;
   const double* xg = P.X + (int64_t)b * P.ldx;
-  const double* xsrc = xg;
-  const int32_t* ncsrc = P.nodecol;
-  if constexpr (stages_x(TYPE)) {
-    double* xs = smem + P.lds_x_off;
-    int32_t* ns = reinterpret_cast<int32_t*>(smem + P.lds_x_off + P.n_pad);
-    for (int i = threadIdx.x; i < P.n; i += BLOCK) xs[i] = xg[i];
-    for (int i = threadIdx.x; i < P.n_nodecol; i += BLOCK) ns[i] = P.nodecol[i];
-    __syncthreads();
-    xsrc = xs; ncsrc = ns;
-  }
+  // issue the lane's item, first slot groups and (below) the x / node-table staging loads together
   const ItemDesc it = P.items[T.i0 + threadIdx.x];
+  TileEmit<BLOCK, type_merges(TYPE)> em(P.slots + it.slot, smem, smem + P.lds_rows_off - T.r0);
+  // x (+ a zero at index n for constant node values) and, for node-value kinds, the node table
+  double* xs = smem + P.lds_x_off;
+  int32_t* ns = reinterpret_cast<int32_t*>(smem + P.lds_x_off + P.n_pad);
+  if ((reinterpret_cast<uintptr_t>(xg) & 15) == 0) {
+    stage16<BLOCK>(reinterpret_cast<uint4*>(xs), reinterpret_cast<const uint4*>(xg), P.n >> 1);
+    if ((P.n & 1) && threadIdx.x == 0) xs[P.n - 1] = xg[P.n - 1];
+  } else {
+    for (int i = threadIdx.x; i < P.n; i += BLOCK) xs[i] = xg[i];
+  }
+  if (threadIdx.x == 0) xs[P.n] = 0.0;
+  if constexpr (stages_nodes(TYPE))
+    stage16<BLOCK>(reinterpret_cast<uint4*>(ns), reinterpret_cast<const uint4*>(P.nodecol), (P.n_nodecol + 3) >> 2);
+  __syncthreads();
+  const double* xsrc = xs;
+  const int32_t* ncsrc = ns;
   if (it.type == TYPE) {
     Ctx c;
     c.seg = it.seg >= 0 ? P.segs + (int64_t)it.seg * P.n_spl : nullptr;
     c.x = xsrc; c.nodecol = ncsrc; c.spl = P.spl; c.dur = P.dur;
     c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
     c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
-    double *out, *gout;
-    if constexpr (LDS_TILE) { out = smem - T.v0; gout = smem + P.lds_rows_off - T.r0; }
-    else { out = P.want_jac ? Vb : nullptr; gout = P.want_g ? Gb : nullptr; }
-    MergeEmit<BLOCK, type_merges(TYPE)> em{P.slots + it.slot, out, gout, 0, -1, 0.0};
     eval_typed<TYPE>(c, it, em);
     em.flush();
   }
-  if constexpr (LDS_TILE) {
-    __syncthreads();
-    if (P.want_jac) copy_out(smem, Vb + T.v0, T.v1 - T.v0);
-    if (P.want_g)
-      for (int i = threadIdx.x; i < T.r1 - T.r0; i += BLOCK) Gb[T.r0 + i] = smem[P.lds_rows_off + i];
-  }
+  __syncthreads();
+  if (P.want_jac) copy_out(smem, Vb + T.v0, T.v1 - T.v0);
+  if (P.want_g)
+    for (int i = threadIdx.x; i < T.r1 - T.r0; i += BLOCK) Gb[T.r0 + i] = smem[P.lds_rows_off + i];
 }
 
-template <bool LDS_TILE>
-const void* kernel_for_mode(int type) {
+const void* kernel_for(int type) {
   switch (type) {
-    case IT_DYN: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_DYN, 256, LDS_TILE>);
-    case IT_ROM: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_ROM, 192, LDS_TILE>);
-    case IT_FDISC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_FDISC, 64, LDS_TILE>);
-    case IT_FNODE: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_FNODE, 64, LDS_TILE>);
-    case IT_TERR: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_TERR, 64, LDS_TILE>);
-    case IT_BMOT: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_BMOT, 64, LDS_TILE>);
-    case IT_SACC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_SACC, 64, LDS_TILE>);
-    case IT_BHGT: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_BHGT, 64, LDS_TILE>);
-    case IT_SWING: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_SWING, 64, LDS_TILE>);
+    case IT_DYN: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_DYN, 256>);
+    case IT_ROM: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_ROM, 192>);
+    case IT_FDISC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_FDISC, 256>);
+    case IT_FNODE: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_FNODE, 64>);
+    case IT_TERR: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_TERR, 64>);
+    case IT_BMOT: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_BMOT, 64>);
+    case IT_SACC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_SACC, 64>);
+    case IT_BHGT: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_BHGT, 64>);
+    case IT_SWING: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_SWING, 64>);
   }
   return nullptr;
 }
-const void* kernel_for(int type, bool lds_tile) { return lds_tile ? kernel_for_mode<true>(type) : kernel_for_mode<false>(type); }
 
 }  // namespace
 
@@ -192,7 +215,7 @@ struct towr_gpu_handle_s {
   std::string err;
   // device tables
   ItemDesc* d_items = nullptr;
-  int32_t* d_slots = nullptr;
+  SlotGroup* d_slots = nullptr;
   TileDesc* d_tiles = nullptr;
   int32_t* d_nodecol = nullptr;
   SplineMeta* d_spl = nullptr;
@@ -201,7 +224,6 @@ struct towr_gpu_handle_s {
   towr_terrain_t* d_terrain = nullptr;      // base terrain (1 entry)
   towr_terrain_t* d_bterrain = nullptr;     // per-problem batch terrains
   int32_t bterrain_n = 0;
-  bool lds_tile = false;                    // output path (TOWR_GPU_OUTPUT=lds|direct), see the kernel
   // staging for host-pointer entry points
   double *d_x = nullptr, *d_g = nullptr, *d_v = nullptr;
   double *h_x = nullptr, *h_g = nullptr, *h_v = nullptr;
@@ -240,9 +262,10 @@ int bind(towr_gpu_handle h) {
   return TOWR_OK;
 }
 
-size_t lds_bytes(const Layout& L, int t, bool lds_tile) {
-  size_t d = lds_tile ? (size_t)L.type_lds[t] : 0;
-  if (stages_x(t)) d += (size_t)((L.n + 1) & ~1) + (L.nodecol.size() + 1) / 2;
+size_t lds_bytes(const Layout& L, int t) {
+  size_t d = (size_t)L.type_lds[t];
+  d += (size_t)((L.n + 2) & ~1);                                          // x + zero slot
+  if (stages_nodes(t)) d += (L.nodecol.size() + 3) / 4 * 2;                // node table (16-B units)
   return sizeof(double) * d;
 }
 
@@ -262,16 +285,16 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
     P.terrains = terrains; P.terrain_per_problem = per_problem;
     P.B = B; P.tile0 = L.type_tile0[t]; P.ntiles = nt;
     P.lds_rows_off = L.type_lds_rows_off[t];
-    P.n = L.n; P.n_pad = (L.n + 1) & ~1; P.n_nodecol = (int32_t)L.nodecol.size();
-    P.lds_x_off = h->lds_tile ? L.type_lds[t] : 0;
+    P.n = L.n; P.n_pad = (L.n + 2) & ~1; P.n_nodecol = (int32_t)L.nodecol.size();
+    P.lds_x_off = L.type_lds[t];
     P.want_g = want_g; P.want_jac = want_jac; P.fdisc_motion = L.fdisc_motion;
     P.rb = L.rb;
     const int64_t total = (int64_t)B * nt;
     const int64_t grid = ((total + 7) / 8) * 8;
     if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
     void* args[] = {&P};
-    HIPCHK(h, hipLaunchKernel(kernel_for(t, h->lds_tile), dim3((unsigned)grid), dim3((unsigned)L.type_block[t]), args,
-                              lds_bytes(L, t, h->lds_tile), s));
+    HIPCHK(h, hipLaunchKernel(kernel_for(t), dim3((unsigned)grid), dim3((unsigned)L.type_block[t]), args,
+                              lds_bytes(L, t), s));
   }
   return TOWR_OK;
 }
@@ -356,19 +379,18 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) { h->err = "hipStreamCreate failed"; return bail(TOWR_ERR_HIP); }
   const Layout& L = h->L;
   std::vector<towr_terrain_t> ter(1, L.terrain);
+  std::vector<int32_t> nodecol16(L.nodecol);   // constant node values -> x[n] = 0; whole 16-B units
+  for (int32_t& c : nodecol16) if (c < 0) c = L.n;
+  nodecol16.resize((nodecol16.size() + 3) / 4 * 4, L.n);
   int r;
-  if ((r = upload(h, &h->d_items, L.items)) || (r = upload(h, &h->d_slots, L.slots)) ||
-      (r = upload(h, &h->d_tiles, L.tiles)) || (r = upload(h, &h->d_nodecol, L.nodecol)) ||
+  if ((r = upload(h, &h->d_items, L.items)) || (r = upload(h, &h->d_slots, L.slot_groups)) ||
+      (r = upload(h, &h->d_tiles, L.tiles)) || (r = upload(h, &h->d_nodecol, nodecol16)) ||
       (r = upload(h, &h->d_spl, L.spl)) || (r = upload(h, &h->d_dur, L.dur)) || (r = upload(h, &h->d_segs, L.segs)) || (r = upload(h, &h->d_terrain, ter)))
     return bail(r);
-  {
-    const char* mode = std::getenv("TOWR_GPU_OUTPUT");
-    h->lds_tile = mode && std::strcmp(mode, "lds") == 0;
-  }
   for (int t = 0; t < IT_COUNT; ++t) {
-    const size_t lds = lds_bytes(L, t, h->lds_tile);
+    const size_t lds = lds_bytes(L, t);
     if (lds > 160 * 1024) { h->err = "tile too large for LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
-    if (lds > 64 * 1024 && hipFuncSetAttribute(kernel_for(t, h->lds_tile), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+    if (lds > 64 * 1024 && hipFuncSetAttribute(kernel_for(t), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
       h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
     }
   }
