@@ -61,6 +61,22 @@ def make_batch(prob, B, first_id):
     return X, terrains
 
 
+def shard_first_id(rank, B):
+    """Rank r owns problems [r*B, (r+1)*B) of the global batch (weak scaling, no collective)."""
+    return rank * B
+
+
+def max_over_ranks(wall, kern_ms, dev, world):
+    """Timing reduction: the slowest rank defines the job time."""
+    if world <= 1:
+        return wall, kern_ms
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0]), float(t[1])
+
+
 def cpu_baseline(desc, X, seconds):
     """The oracle timed on this host's cores, one independent problem per thread."""
     from oracle import oracle as O
@@ -105,7 +121,7 @@ def main():
     if args.tiles_per_block:
         prob.set_tiles_per_block(args.tiles_per_block)
     B = args.batch
-    Xh, terrains = make_batch(prob, B, first_id=rank * B)
+    Xh, terrains = make_batch(prob, B, first_id=shard_first_id(rank, B))
     prob.set_batch_terrain(terrains)
     ldv = (prob.nnz + 15) // 16 * 16
     ldg = (prob.m + 15) // 16 * 16
@@ -136,10 +152,7 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     kern_ms = e0.elapsed_time(e1) / args.steps
-    if world > 1:
-        t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall, kern_ms = float(t[0]), float(t[1])
+    wall, kern_ms = max_over_ranks(wall, kern_ms, dev, world)
 
     calls = B * world * args.steps
     value = calls / wall
@@ -183,8 +196,9 @@ def main():
         try:
             with open(pmc) as fh:
                 rec = json.load(fh)
-            if rec.get("problems_per_launch") == B:
-                out["roofline"]["traffic"] = rec["hbm_bytes_per_launch"]
+            k = rec.get("kernels", {}).get(dom)
+            if rec.get("problems_per_launch") == B and k:
+                out["roofline"]["traffic"] = k["hbm_bytes_per_launch"]
                 out["roofline"]["traffic_source"] = rec.get("source")
         except Exception:
             pass

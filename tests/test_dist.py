@@ -1,0 +1,55 @@
+"""Multi-process (N>1) path of bench.py on CPU with the gloo backend, world_size 2.
+
+The batch of independent problems is the only parallel axis: rank r owns problems
+[r*B, (r+1)*B) with no data-path collective; the only collectives are the timing barrier and the
+max-over-ranks reduction. Checked here: the shards partition exactly the single-process batch
+(same seeded instances, same x sets, same terrains), and the timing reduction takes the max."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+B = 3
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch
+    import bench
+    from towr2025_amd import TowrGpuProblem
+    from towr2025_amd import formulation as F
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    prob = TowrGpuProblem(F.anymal_trot().to_desc(), device=-1)   # layout only: no GPU here
+    first = bench.shard_first_id(rank, B)
+    X, terrains = bench.make_batch(prob, B, first_id=first)
+    np.save(os.path.join(outdir, f"x{rank}.npy"), X)
+    np.save(os.path.join(outdir, f"t{rank}.npy"), np.array([[t.id, *list(t.p)] for t in terrains]))
+    wall, kern = bench.max_over_ranks(float(rank + 1), 10.0 * (rank + 1), torch.device("cpu"), world)
+    np.save(os.path.join(outdir, f"r{rank}.npy"), np.array([wall, kern]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_shards_partition_the_batch(tmp_path):
+    world = 2
+    mp.spawn(_worker, args=(world, _port(), str(tmp_path)), nprocs=world, join=True)
+    import bench
+    from towr2025_amd import TowrGpuProblem
+    from towr2025_amd import formulation as F
+    prob = TowrGpuProblem(F.anymal_trot().to_desc(), device=-1)
+    X, terrains = bench.make_batch(prob, world * B, first_id=0)
+    Xs = np.concatenate([np.load(tmp_path / f"x{r}.npy") for r in range(world)], axis=1)
+    np.testing.assert_array_equal(Xs, X)
+    T = np.concatenate([np.load(tmp_path / f"t{r}.npy") for r in range(world)])
+    np.testing.assert_array_equal(T, np.array([[t.id, *list(t.p)] for t in terrains]))
+    for r in range(world):
+        np.testing.assert_array_equal(np.load(tmp_path / f"r{r}.npy"), [2.0, 20.0])

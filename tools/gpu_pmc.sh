@@ -1,19 +1,23 @@
 #!/bin/bash
-# GPU-box PMC passes (kernel-trace only, never combined with sys/runtime traces):
-#   pass 1: SQ instruction/wait counters; pass 2: FETCH_SIZE; pass 3: WRITE_SIZE.
-# Usage: tools/gpu_pmc.sh TAG [steps]
+# GPU-box PMC passes (kernel-trace only, never combined with sys/runtime traces), one counter group
+# per pass: sq = SQ instruction/wait counters, fetch = FETCH_SIZE, write = WRITE_SIZE.
+# Usage: tools/gpu_pmc.sh TAG [steps] [passes]
 TAG=${1:-pmc}
 STEPS=${2:-5}
+PASSES=${3:-"sq fetch write"}
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-run() {
-  local name=$1; shift
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc "$@" --output-format csv -d gpurun_out/${TAG}_$name -o run -- \
-      python3 bench.py --steps $STEPS --warmup 2 --no-cpu > gpurun_out/${TAG}_$name.log 2>&1
-  local rc=$?; echo "$name rc=$rc"; tail -2 gpurun_out/${TAG}_$name.log
-  return $rc
-}
-run sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY && \
-run fetch FETCH_SIZE && \
-run write WRITE_SIZE
+for p in $PASSES; do
+  case $p in
+    sq) C="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" ;;
+    fetch) C="FETCH_SIZE" ;;
+    write) C="WRITE_SIZE" ;;
+    *) echo "unknown pass $p"; exit 2 ;;
+  esac
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $C --output-format csv -d gpurun_out/${TAG}_$p -o run -- \
+      python3 bench.py --steps $STEPS --warmup 2 --no-cpu > gpurun_out/${TAG}_$p.log 2>&1
+  rc=$?; echo "$p rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+done
+exit 0

@@ -1,0 +1,48 @@
+"""Per-launch HBM traffic of every tile kernel from rocprofv3 FETCH_SIZE / WRITE_SIZE passes
+(tools/gpu_pmc.sh), written to profiles/pmc_traffic.json for bench.py's roofline.traffic.
+
+FETCH_SIZE and WRITE_SIZE are in KiB. Per /opt/skills/guides/MI355X_MICROARCH.md (HBM section), on
+gfx950 FETCH_SIZE counts half the bytes of wide (16 B/lane) coalesced reads — the kernels' only
+HBM reads are the 16 B/lane x staging loads — so FETCH_SIZE is doubled; WRITE_SIZE is exact for
+the 16 B/lane stores of the tile copy-out and is used as is.
+usage: python tools/pmc_traffic.py gpurun_out/TAG_fetch gpurun_out/TAG_write B [out.json]"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+NAMES = ["dynamic", "range_of_motion", "force_discretized", "force_node", "terrain", "base_motion",
+         "spline_acc", "base_height", "swing"]
+
+
+def per_kernel(d, counter):
+    acc = defaultdict(list)
+    for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
+        k = r["Kernel_Name"]
+        if "towr_tile_kernel<" not in k or r["Counter_Name"] != counter:
+            continue
+        t = int(k.split("towr_tile_kernel<")[1].split(",")[0])
+        acc[NAMES[t]].append(float(r["Counter_Value"]) * 1024.0)
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def main():
+    fdir, wdir, B = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    out = sys.argv[4] if len(sys.argv) > 4 else "profiles/pmc_traffic.json"
+    f, w = per_kernel(fdir, "FETCH_SIZE"), per_kernel(wdir, "WRITE_SIZE")
+    rec = {"problems_per_launch": B,
+           "source": f"rocprofv3 --kernel-trace --pmc FETCH_SIZE / WRITE_SIZE (separate passes), {fdir} {wdir}; "
+                     "FETCH_SIZE x2 (gfx950 16 B/lane read correction), WRITE_SIZE as is",
+           "kernels": {}}
+    for k in sorted(set(f) | set(w)):
+        fb, wb = 2.0 * f.get(k, 0.0), w.get(k, 0.0)
+        rec["kernels"][k] = {"fetch_bytes_raw": f.get(k), "fetch_bytes": fb, "write_bytes": wb,
+                             "hbm_bytes_per_launch": fb + wb}
+    with open(out, "w") as fh:
+        json.dump(rec, fh, indent=1)
+    for k, v in rec["kernels"].items():
+        print(f"{k:18s} fetch {v['fetch_bytes'] / 1e6:9.2f} MB  write {v['write_bytes'] / 1e6:9.2f} MB")
+
+
+if __name__ == "__main__":
+    main()
