@@ -100,6 +100,7 @@ def main():
     ap.add_argument("--batch", type=int, default=4096, help="problems per GPU (weak scaling)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-host", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
     ap.add_argument("--tiles-per-block", type=int, default=0)
     args = ap.parse_args()
 
@@ -202,6 +203,17 @@ def main():
                 out["roofline"]["traffic_source"] = rec.get("source")
         except Exception:
             pass
+    if rank == 0 and not args.no_host:
+        # PCIe-inclusive rate through the host-buffer entry point (towr_gpu_eval_batch: H2D of X,
+        # launch, D2H of G and V via pinned staging) — reported beside, never as `value`
+        prob.eval_batch(Xh[0])
+        reps = 3
+        t0 = time.perf_counter()
+        for i in range(reps):
+            prob.eval_batch(Xh[i % N_X])
+        th = (time.perf_counter() - t0) / reps
+        out["host_batch"] = {"value": B / th, "unit": "calls/s", "ms_per_batch": th * 1e3,
+                             "note": "host X/G/V buffers, PCIe transfers included (per GPU)"}
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(desc, Xh[0, :8], args.cpu_seconds)
     if rank == 0:

@@ -16,7 +16,7 @@ for p in $PASSES; do
     *) echo "unknown pass $p"; exit 2 ;;
   esac
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $C --output-format csv -d gpurun_out/${TAG}_$p -o run -- \
-      python3 bench.py --steps $STEPS --warmup 2 --no-cpu > gpurun_out/${TAG}_$p.log 2>&1
+      python3 bench.py --steps $STEPS --warmup 2 --no-cpu --no-host > gpurun_out/${TAG}_$p.log 2>&1
   rc=$?; echo "$p rc=$rc"
   [ $rc -eq 0 ] || exit $rc
 done

@@ -19,7 +19,7 @@ rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/${TAG}_bench.log
 [ $rc -eq 0 ] || exit $rc
 
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- \
-    python bench.py --steps $STEPS --warmup 3 --no-cpu > gpurun_out/${TAG}_prof.log 2>&1
+    python bench.py --steps $STEPS --warmup 3 --no-cpu --no-host > gpurun_out/${TAG}_prof.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; tail -2 gpurun_out/${TAG}_prof.log
 find gpurun_out/${TAG}_prof -name "*stats*" | head
 exit $rc

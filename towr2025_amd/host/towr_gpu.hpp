@@ -1,0 +1,119 @@
+// towr_gpu.hpp — C++ host side over the C-ABI (include/towr_gpu.h): what a towr/ifopt user calls.
+//
+// Engine     RAII owner of one towr_gpu handle. The names follow ifopt::Problem, which is what
+//            IpoptAdapter reaches for this path (ifopt ≥ 2.0.1, external to the reference):
+//              GetNumberOfOptimizationVariables / GetNumberOfConstraints / GetVariableValues,
+//              EvalConstraints(x) -> g, EvalNonzerosOfJacobian(x) -> values, the Jacobian
+//              structure in RowMajor (iRow, jCol) order.
+// NlpCallbacks  the IPOPT TNLP callback subset of ifopt's IpoptAdapter for the hot path
+//            (get_nlp_info / eval_g / eval_jac_g) with Ipopt's argument meaning: eval_jac_g with
+//            values == nullptr fills the structure, otherwise the values. Unlike ifopt (which
+//            ignores new_x and re-evaluates every set), g and J are produced by one fused launch per
+//            new x and J is served from that launch when IPOPT asks for it at the same x.
+//
+// Error behaviour: construction failures throw std::runtime_error (the reference's
+// NlpFormulation throws at setup, nlp_formulation.cc:396, 477-481); the callbacks return false on
+// a runtime failure, which makes IPOPT stop with an evaluation error (ifopt's callbacks always
+// return true, but it has no failure mode to report). There is no CPU path.
+#pragma once
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "towr_gpu.h"
+
+namespace towr_gpu {
+
+class Engine {
+ public:
+  // device < 0: layout-only (sizes, structure, x0; evaluation throws)
+  Engine(const towr_problem_desc_t& desc, int device = 0) {
+    const int rc = towr_gpu_create(&desc, device, &h_);
+    if (rc != TOWR_OK) throw std::runtime_error("towr_gpu_create failed (" + std::to_string(rc) + "): " + towr_gpu_last_error(nullptr));
+    int32_t n = 0, m = 0;
+    int64_t nnz = 0;
+    Check(towr_gpu_sizes(h_, &n, &m, &nnz));
+    n_ = n; m_ = m; nnz_ = nnz;
+  }
+  ~Engine() { if (h_) towr_gpu_destroy(h_); }
+  Engine(const Engine&) = delete;
+  Engine& operator=(const Engine&) = delete;
+
+  int GetNumberOfOptimizationVariables() const { return n_; }
+  int GetNumberOfConstraints() const { return m_; }
+  int64_t GetNumberOfJacobianNonzeros() const { return nnz_; }
+
+  std::vector<double> GetVariableValues() const {   // starting point x0
+    std::vector<double> x(n_);
+    Check(towr_gpu_initial_x(h_, x.data()));
+    return x;
+  }
+  void GetJacobianStructure(int32_t* iRow, int32_t* jCol) const { Check(towr_gpu_jac_structure(h_, iRow, jCol)); }
+  void EvalConstraints(const double* x, double* g) const { Check(towr_gpu_eval_g(h_, x, g)); }
+  void EvalNonzerosOfJacobian(const double* x, double* values) const { Check(towr_gpu_eval_jac_values(h_, x, values)); }
+  void EvalConstraintsAndJacobian(const double* x, double* g, double* values) const { Check(towr_gpu_eval_g_jac(h_, x, g, values)); }
+  // B independent problems sharing this layout (host buffers, row-major B x n / m / nnz)
+  void SetBatchTerrain(const std::vector<towr_terrain_t>& t) { Check(towr_gpu_set_batch_terrain(h_, (int32_t)t.size(), t.data())); }
+  void EvalBatch(int B, const double* X, double* G, double* V) const { Check(towr_gpu_eval_batch(h_, B, X, G, V)); }
+  // device-resident batch (HBM pointers), asynchronous on `stream` (hipStream_t, nullptr = default)
+  int EvalBatchDevice(int B, const double* X, int64_t ldx, double* G, int64_t ldg, double* V, int64_t ldv, void* stream) const {
+    return towr_gpu_eval_batch_device(h_, B, X, ldx, G, ldg, V, ldv, 1, 1, stream);
+  }
+  towr_gpu_handle handle() const { return h_; }
+
+ private:
+  void Check(int rc) const {
+    if (rc != TOWR_OK) throw std::runtime_error("towr_gpu error " + std::to_string(rc) + ": " + towr_gpu_last_error(h_));
+  }
+  towr_gpu_handle h_ = nullptr;
+  int n_ = 0, m_ = 0;
+  int64_t nnz_ = 0;
+};
+
+// The eval_g / eval_jac_g pair of an IPOPT TNLP (Index = int, Number = double), as ifopt's
+// IpoptAdapter implements it for towr, served by the engine.
+class NlpCallbacks {
+ public:
+  explicit NlpCallbacks(Engine& e) : e_(e), g_(e.GetNumberOfConstraints()), v_(e.GetNumberOfJacobianNonzeros()) {}
+
+  bool get_nlp_info(int& n, int& m, int& nnz_jac_g) const {
+    n = e_.GetNumberOfOptimizationVariables();
+    m = e_.GetNumberOfConstraints();
+    nnz_jac_g = (int)e_.GetNumberOfJacobianNonzeros();
+    return true;
+  }
+  bool eval_g(int n, const double* x, bool new_x, int m, double* g) {
+    if (n != e_.GetNumberOfOptimizationVariables() || m != e_.GetNumberOfConstraints()) return false;
+    if (!Update(x, new_x)) return false;
+    for (int i = 0; i < m; ++i) g[i] = g_[i];
+    return true;
+  }
+  bool eval_jac_g(int n, const double* x, bool new_x, int m, int nele_jac, int* iRow, int* jCol, double* values) {
+    if (n != e_.GetNumberOfOptimizationVariables() || m != e_.GetNumberOfConstraints() ||
+        nele_jac != (int)e_.GetNumberOfJacobianNonzeros())
+      return false;
+    if (values == nullptr) {   // structure (IPOPT asks once)
+      try { e_.GetJacobianStructure(iRow, jCol); } catch (const std::exception&) { return false; }
+      return true;
+    }
+    if (!Update(x, new_x)) return false;
+    for (int k = 0; k < nele_jac; ++k) values[k] = v_[k];
+    return true;
+  }
+
+ private:
+  // one fused launch per new x; IPOPT's new_x == false promises the x of the previous call
+  bool Update(const double* x, bool new_x) {
+    if (!new_x && valid_) return true;
+    try { e_.EvalConstraintsAndJacobian(x, g_.data(), v_.data()); } catch (const std::exception&) { valid_ = false; return false; }
+    valid_ = true;
+    return true;
+  }
+  Engine& e_;
+  std::vector<double> g_, v_;
+  bool valid_ = false;
+};
+
+}  // namespace towr_gpu
