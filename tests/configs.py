@@ -3,7 +3,7 @@ from towr2025_amd import formulation as F
 
 
 def config_descs():
-    """name -> ProblemDesc. configs[0..3] of BASELINE.json (gait optimisation excluded: next tier)."""
+    """name -> ProblemDesc: BASELINE.json configs[0..3] plus cases covering every kind and terrain."""
     return {
         "monoped_hopper_flat": F.monoped_hopper().to_desc(),                       # configs[0]
         "monoped_procedural": F.procedural_desc(),                                 # procedural_example.cc
@@ -16,7 +16,28 @@ def config_descs():
         "hyq_chimney": _hyq(F.HeightMap.ChimneyID),
         "hyq_gap": _hyq(F.HeightMap.GapID),
         "anymal_block_baserom": _anymal_baserom(),
+        # configs[3]: ANYmal on stairs with phase-duration (gait) optimisation
+        "anymal_stairs_gaitopt": F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.StairsID),
+                                               optimize_timings=True).to_desc(),
+        "biped_walk_gaitopt": _gaitopt(F.biped_walk()),
+        "hyq_gap_gaitopt": _gaitopt_hyq_gap(),
     }
+
+
+def _gaitopt(f):
+    f.params_.OptimizePhaseDurations()
+    return f.to_desc()
+
+
+def _gaitopt_hyq_gap():
+    d = _hyq(F.HeightMap.GapID)
+    f = F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.GapID), optimize_timings=True)
+    f.model_ = F.RobotModel(F.RobotModel.Hyq)
+    nominal = f.model_.kinematic_model.nominal_stance
+    f.initial_ee_W_ = [(p[0], p[1], 0.0) for p in nominal]
+    f.initial_base_ = F.BaseState(lin_p=(0.0, 0.0, -nominal[0][2]))
+    del d
+    return f.to_desc()
 
 
 def _hopper_steps():

@@ -1,9 +1,13 @@
 """Shared parity helpers: the tolerance of BASELINE.md / SURVEY §8(d), written once.
 
-values:  |a - b| <= 1e-9 * max(|a|, |b|) + 1e-12 * max(1, rowscale)
-where rowscale = max |J| over the reference row. The unit floor covers rows whose reference
-entries are all structural zeros (e.g. Hermite basis functions that vanish at a polynomial end,
-where the reference happens to round to exactly 0.0 and fused multiply-adds give ~4e-16).
+values:  |a - b| <= 1e-9 * max(|a|, |b|) + 1e-12 * max(1, rowscale, colscale)
+where rowscale / colscale = max |J| over the reference row / column. The floor covers entries that
+are exact zeros in exact arithmetic and come out as rounding residue of much larger terms:
+Hermite basis functions that vanish at a polynomial end (the reference rounds to exactly 0.0,
+fused multiply-adds give ~4e-16), and, with phase-duration optimisation, d pos / d duration of a
+PhaseSpline at an instant where the spline is analytically flat (a zero force in swing: its
+velocity is the ~1e-11 residue of ~1e5-sized Hermite terms). Such residue differs with any change
+of operation order, the reference's own build included; the column scale bounds its size.
 g:       |a - b| <= 1e-9 * max(|a|, |b|) + 1e-12 * max(1, |J row| scale)
 Pattern: bit-exact (same (row, col) list in the same order).
 """
@@ -13,24 +17,31 @@ REL = 1e-9
 ABS = 1e-12
 
 
-def check_values(g_ref, g, rows_ref, v_ref, v, m):
+def check_values(g_ref, g, rows_ref, v_ref, v, m, cols_ref=None):
     rs = np.zeros(m)
     np.maximum.at(rs, rows_ref, np.abs(v_ref))
     floor = ABS * np.maximum(1.0, rs)
-    tol_v = REL * np.maximum(np.abs(v_ref), np.abs(v)) + floor[rows_ref]
+    floor_v = floor[rows_ref]
+    if cols_ref is not None:
+        cs = np.zeros(int(cols_ref.max()) + 1 if len(cols_ref) else 1)
+        np.maximum.at(cs, cols_ref, np.abs(v_ref))
+        floor_v = np.maximum(floor_v, ABS * cs[cols_ref])
+    tol_v = REL * np.maximum(np.abs(v_ref), np.abs(v)) + floor_v
     bad_v = np.flatnonzero(np.abs(v_ref - v) > tol_v)
     tol_g = REL * np.maximum(np.abs(g_ref), np.abs(g)) + floor
     bad_g = np.flatnonzero(np.abs(g_ref - g) > tol_g)
     return bad_g, bad_v
 
 
-def assert_close(g_ref, g, rows_ref, v_ref, v, m, what=""):
-    bad_g, bad_v = check_values(g_ref, g, rows_ref, v_ref, v, m)
+def assert_close(g_ref, g, rows_ref, v_ref, v, m, what="", cols_ref=None):
+    bad_g, bad_v = check_values(g_ref, g, rows_ref, v_ref, v, m, cols_ref)
     msg = []
     if len(bad_g):
         i = bad_g[0]
         msg.append(f"{len(bad_g)} g mismatches, first row {i}: ref {g_ref[i]!r} got {g[i]!r}")
     if len(bad_v):
         i = bad_v[0]
-        msg.append(f"{len(bad_v)} J mismatches, first nz {i} (row {rows_ref[i]}): ref {v_ref[i]!r} got {v[i]!r}")
+        j = bad_v[np.argmax(np.abs(v_ref[bad_v] - v[bad_v]))]
+        msg.append(f"{len(bad_v)} J mismatches, first nz {i} (row {rows_ref[i]}): ref {v_ref[i]!r} got {v[i]!r}; "
+                   f"largest at nz {j} (row {rows_ref[j]}): ref {v_ref[j]!r} got {v[j]!r}")
     assert not msg, what + ": " + "; ".join(msg)

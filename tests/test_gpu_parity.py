@@ -36,7 +36,7 @@ def test_pattern_and_values(name):
             continue   # reference pattern moved at this x (only Gap terrain): out of contract
         g = p.eval_g(x)
         v = p.eval_jac_values(x)
-        assert_close(g_ref, g, r, v_ref, v, o.m, f"{name} seed {seed} (separate calls)")
+        assert_close(g_ref, g, r, v_ref, v, o.m, f"{name} seed {seed} (separate calls)", cols_ref=c)
         g2, v2 = p.eval_g_jac(x)
         np.testing.assert_array_equal(g2, g)
         np.testing.assert_array_equal(v2, v)

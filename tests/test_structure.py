@@ -48,8 +48,13 @@ def test_initial_x_for_matches_fresh_layout():
 
 
 def test_unsupported_and_invalid():
-    d = F.anymal_trot(optimize_timings=True).to_desc()
+    d = F.anymal_trot().to_desc()
+    d.angular_rep = 1                      # RotVec: next tier
     with pytest.raises(TowrGpuError, match="-2"):
+        TowrGpuProblem(d, device=-1)
+    d = F.anymal_trot(optimize_timings=True).to_desc()
+    d.n_varsets -= 1                       # drop a schedule set while optimising timings
+    with pytest.raises(TowrGpuError, match="-1"):
         TowrGpuProblem(d, device=-1)
     d = F.anymal_trot().to_desc()
     d.abi_version = 99

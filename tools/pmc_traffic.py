@@ -12,7 +12,7 @@ import sys
 from collections import defaultdict
 
 NAMES = ["dynamic", "range_of_motion", "force_discretized", "force_node", "terrain", "base_motion",
-         "spline_acc", "base_height", "swing"]
+         "spline_acc", "base_height", "swing", "total_duration"]
 
 
 def per_kernel(d, counter):

@@ -46,15 +46,37 @@ enum ItemType {
   IT_SACC = 6,   // SplineAccConstraint junction
   IT_BHGT = 7,   // BaseHeightConstraint node
   IT_SWING = 8,  // SwingConstraint node
-  IT_COUNT = 9
+  IT_TDUR = 9,   // TotalDurationConstraint (phase-duration optimisation)
+  IT_COUNT = 10
 };
 
 struct SplineMeta {
   int32_t node_off;  // first node's index into nodecol (6 ints per node: [deriv][dim])
   int32_t n_polys;
   int32_t dur_off;   // first polynomial duration in the durations table
+  // PhaseSpline (phase-duration optimisation, phase_spline.cc:35-93): durations come from the
+  // ee's schedule variables and the Jacobian keeps the full pattern of every polynomial
+  int32_t ee;        // endeffector of a PhaseSpline, else -1
+  int32_t pinfo_off; // first PolyPhase of this spline
+  int32_t pcol_off[3], pcol_n[3];   // PhaseCol entries of each dimension (the full pattern)
   int32_t reserved;
 };
+
+// phase of a polynomial (NodesVariablesPhaseBased::PolyInfo, nodes_variables_phase_based.cc:39-59)
+struct PolyPhase { int16_t phase, poly_in_phase, n_in_phase, reserved; };
+
+// one column of a PhaseSpline's full Jacobian pattern in one dimension: the optimisation variable
+// and the (1 or 2) node values it sets (a stance variable sets two nodes)
+struct PhaseCol {
+  int32_t col;
+  int16_t id[2];
+  int8_t deriv[2];
+  int8_t n, reserved;
+};
+
+// PhaseDurations of one endeffector (phase_durations.cc:41-100): the first n_phases - 1 durations
+// are the variables at col0.., the last is t_total minus their sum
+struct SchedInfo { int32_t col0, n_phases; double t_total; };
 
 struct RobotC {
   double m, g;
@@ -108,6 +130,10 @@ struct Ctx {
   const towr_terrain_t* ter;    // this problem's terrain
   RobotC rb;
   int32_t fdisc_motion;         // ForceConstraintDiscretized motion block enabled (terrain has d2h)
+  bool gait;                    // phase-duration optimisation (a compile-time constant in kernels)
+  const PolyPhase* pinfo;
+  const PhaseCol* pcols;
+  const SchedInfo* sched;       // per endeffector
 };
 
 // ----------------------------------------------------------------------------------------------
@@ -117,6 +143,7 @@ struct SplinePt {
   int poly;
   double T, tl;
   const double* H;   // SegRec::H of this instant on the device (basis precomputed), else nullptr
+  bool dyn;          // PhaseSpline: durations (hence polynomial, local time, basis) depend on x
   double p[3], v[3], a[3];
 };
 
@@ -152,6 +179,26 @@ TG_HD int basis_col(const Ctx& c, int s, int poly, int b, int e) {
   return node_col(c, s, poly + (b >> 1), b & 1, e);
 }
 
+// x^k for small k, correctly rounded like the std::pow of the reference's host build: a double-double
+// product on the device (the device pow is not correctly rounded). Used where the reference's
+// formulas cancel (polynomial state, d pos / d duration), so that the engine reproduces them.
+TG_HD double cpow(double x, int k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (k == 0) return 1.0;
+  double hi = x, lo = 0.0;
+  for (int i = 1; i < k; ++i) {
+    const double p = hi * x;
+    double e = fma(hi, x, -p);
+    e = fma(lo, x, e);
+    hi = p + e;
+    lo = e - (hi - p);
+  }
+  return hi;
+#else
+  return pow(x, k);
+#endif
+}
+
 // GetDerivativeOf{Pos,Vel,Acc}Wrt{Start,End}Node (polynomial.cc:135-234); b = 0 n0.p, 1 n0.v, 2 n1.p, 3 n1.v
 TG_HD void hermite_dpos(double T, double t, double H[4]) {
   const double T2 = T * T, T3 = T2 * T, t2 = t * t, t3 = t2 * t;
@@ -177,42 +224,66 @@ TG_HD void hermite_dacc(double T, double t, double H[4]) {
 
 // CubicHermitePolynomial::UpdateCoeff (:97-104) + Polynomial::GetPoint (:47-58)
 TG_HD void poly_state(const Ctx& c, int s, int poly, double T, double tl, SplinePt& o) {
-#if !defined(__HIP_DEVICE_COMPILE__)
-  // Host structure pass: the reference's own operation order (std::pow, sum over coefficients),
-  // so that data-dependent structure predicates (ForceConstraintDiscretized's `scale == 0.0`,
-  // force_constraint_discretized.cc:58) resolve floating-point ties exactly as the source does.
+  // The reference's own operation order (std::pow, sum over coefficients), on the host and the
+  // device alike: data-dependent structure predicates (ForceConstraintDiscretized's `scale == 0.0`,
+  // force_constraint_discretized.cc:58) must resolve floating-point ties as the source does, and
+  // near-zero velocities of PhaseSplines enter the duration derivatives.
+#pragma clang fp contract(off)
   for (int e = 0; e < 3; ++e) {
     const double p0 = xval(c, node_col(c, s, poly, kPos, e)), v0 = xval(c, node_col(c, s, poly, kVel, e));
     const double p1 = xval(c, node_col(c, s, poly + 1, kPos, e)), v1 = xval(c, node_col(c, s, poly + 1, kVel, e));
-    const double cf[4] = {p0, v0, -(3 * (p0 - p1) + T * (2 * v0 + v1)) / pow(T, 2),
-                          (2 * (p0 - p1) + T * (v0 + v1)) / pow(T, 3)};
+    const double cf[4] = {p0, v0, -(3 * (p0 - p1) + T * (2 * v0 + v1)) / cpow(T, 2),
+                          (2 * (p0 - p1) + T * (v0 + v1)) / cpow(T, 3)};
     double pp = 0.0, vv = 0.0, aa = 0.0;
-    for (int k = 0; k < 4; ++k) pp += pow(tl, k) * cf[k];
-    for (int k = 0; k < 4; ++k) vv += (k >= 1 ? k * pow(tl, k - 1) : 0.0) * cf[k];
-    for (int k = 0; k < 4; ++k) aa += (k >= 2 ? k * (k - 1) * pow(tl, k - 2) : 0.0) * cf[k];
+    for (int k = 0; k < 4; ++k) pp += cpow(tl, k) * cf[k];
+    for (int k = 0; k < 4; ++k) vv += (k >= 1 ? k * cpow(tl, k - 1) : 0.0) * cf[k];
+    for (int k = 0; k < 4; ++k) aa += (k >= 2 ? k * (k - 1) * cpow(tl, k - 2) : 0.0) * cf[k];
     o.p[e] = pp; o.v[e] = vv; o.a[e] = aa;
-  }
-  return;
-#endif
-  const double T2 = T * T, T3 = T2 * T, t2 = tl * tl, t3 = t2 * tl;
-  for (int e = 0; e < 3; ++e) {
-    const double p0 = xval(c, node_col(c, s, poly, kPos, e)), v0 = xval(c, node_col(c, s, poly, kVel, e));
-    const double p1 = xval(c, node_col(c, s, poly + 1, kPos, e)), v1 = xval(c, node_col(c, s, poly + 1, kVel, e));
-    const double ca = p0, cb = v0;
-    const double cc = -(3 * (p0 - p1) + T * (2 * v0 + v1)) / T2;
-    const double cd = (2 * (p0 - p1) + T * (v0 + v1)) / T3;
-    o.p[e] = ca + tl * cb + t2 * cc + t3 * cd;
-    o.v[e] = cb + 2 * tl * cc + 3 * t2 * cd;
-    o.a[e] = 2 * cc + 6 * tl * cd;
   }
 }
 
-// Spline::GetPoint(t_global) (spline.cc:80-93)
-// Device: every timed item carries its SegRec row (layout.hip's segment table), so the state is the
-// basis form H . (p0, v0, p1, v1) with the host-precomputed Hermite basis of this (instant,
-// polynomial) — the same polynomial as UpdateCoeff + GetPoint, with no divisions. Host: the
-// reference's own scan and coefficient form (the structure pass must reproduce its ties exactly).
+// PhaseDurations::GetPhaseDurations after SetVariables (phase_durations.cc:79-100)
+TG_HD double phase_duration(const Ctx& c, const SchedInfo& si, double last, int ph) {
+  return ph < si.n_phases - 1 ? c.x[si.col0 + ph] : last;
+}
+TG_HD double last_phase_duration(const Ctx& c, const SchedInfo& si) {
+  double sum = 0.0;
+  for (int i = 0; i < si.n_phases - 1; ++i) sum += c.x[si.col0 + i];   // x.sum()
+  return si.t_total - sum;
+}
+// polynomial duration of a PhaseSpline: phase duration / polynomials in the phase
+// (ConvertPhaseToPolyDurations, nodes_variables_phase_based.cc:75-86)
+TG_HD double phase_poly_duration(const Ctx& c, const SplineMeta& m, const SchedInfo& si, double last, int i) {
+  const PolyPhase pp = c.pinfo[m.pinfo_off + i];
+  return phase_duration(c, si, last, pp.phase) / pp.n_in_phase;
+}
+// Spline::GetLocalTime (spline.cc:48-78) over the x-dependent durations of a PhaseSpline
+TG_HD void phase_spline_locate(const Ctx& c, int s, double tg, SplinePt& o) {
+  const SplineMeta m = c.spl[s];
+  const SchedInfo si = c.sched[m.ee];
+  const double last = last_phase_duration(c, si), eps = 1e-10;
+  double t = 0.0;
+  int id = m.n_polys - 1;
+  for (int i = 0; i < m.n_polys; ++i) {
+    t += phase_poly_duration(c, m, si, last, i);
+    if (t >= tg - eps) { id = i; break; }
+  }
+  double l = tg;
+  for (int i = 0; i < id; ++i) l -= phase_poly_duration(c, m, si, last, i);
+  o.poly = id;
+  o.tl = l;
+  o.T = phase_poly_duration(c, m, si, last, id);
+}
+
 TG_HD void spline_eval(const Ctx& c, int s, double t, SplinePt& o) {
+  o.dyn = false;
+  if (c.gait && c.spl[s].ee >= 0) {
+    o.dyn = true;
+    o.H = nullptr;
+    phase_spline_locate(c, s, t, o);
+    poly_state(c, s, o.poly, o.T, o.tl, o);
+    return;
+  }
 #if defined(__HIP_DEVICE_COMPILE__)
   const SegRec& r = c.seg[s];
   o.poly = r.poly; o.tl = r.tl; o.T = r.T;
@@ -240,12 +311,79 @@ TG_HD void spline_eval(const Ctx& c, int s, double t, SplinePt& o) {
 // Hermite basis of a spline point for derivative d (precomputed on the device, evaluated on the host)
 TG_HD void spline_basis(const SplinePt& o, int d, double H[4]) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  for (int b = 0; b < 4; ++b) H[b] = o.H[4 * d + b];
-#else
+  if (!o.dyn) {
+    for (int b = 0; b < 4; ++b) H[b] = o.H[4 * d + b];
+    return;
+  }
+#endif
   if (d == kPos) hermite_dpos(o.T, o.tl, H);
   else if (d == kVel) hermite_dvel(o.T, o.tl, H);
   else hermite_dacc(o.T, o.tl, H);
-#endif
+}
+
+// scale * d{P's derivative}(spline s)/dx restricted to dimension e, into `row`, given the basis H:
+//   NodeSpline: the 4 basis columns of the active polynomial (node_spline.cc:62-112);
+//   PhaseSpline: every column of the set in dimension e (the full pattern, phase_spline.cc:45-51,
+//   kept through Eigen's products), non-zero only at the active polynomial's two nodes.
+template <class Emit>
+TG_HD void emit_dim(const Ctx& c, Emit& em, int row, int s, const SplinePt& P, const double H[4], int e, double scale,
+                    bool pres = true) {
+  if (!P.dyn) {
+    for (int bb = 0; bb < 4; ++bb) {
+      const int col = basis_col(c, s, P.poly, bb, e);
+      em(row, col, scale * H[bb], pres && col >= 0);
+    }
+    return;
+  }
+  const SplineMeta m = c.spl[s];
+  const PhaseCol* pc = c.pcols + m.pcol_off[e];
+  const int n = m.pcol_n[e];
+  for (int q = 0; q < n; ++q) {
+    const PhaseCol pq = pc[q];
+    double v = 0.0;
+    for (int k = 0; k < pq.n; ++k) {   // coeffRef += per node value the variable sets
+      if (pq.id[k] == P.poly) v += H[pq.deriv[k]];
+      else if (pq.id[k] == P.poly + 1) v += H[2 + pq.deriv[k]];
+    }
+    em(row, pq.col, scale * v, pres);
+  }
+}
+
+// d pos(t) / d schedule of a PhaseSpline: PhaseSpline::GetJacobianOfPosWrtDurations
+// (phase_spline.cc:67-93) with PhaseDurations::GetJacobianOfPos (phase_durations.cc:126-154).
+// J[k][col] over the endeffector's n_phases - 1 schedule variables is dense (sparseView(1, -1)).
+struct SchedJac { int cur, n, col0; double dx[3], v[3]; };
+TG_HD void sched_jac(const Ctx& c, int s, double t, const SplinePt& P, SchedJac& J) {
+#pragma clang fp contract(off)
+  const SplineMeta m = c.spl[s];
+  const SchedInfo si = c.sched[m.ee];
+  const PolyPhase pp = c.pinfo[m.pinfo_off + P.poly];
+  const double inner = 1. / pp.n_in_phase, prev = pp.poly_in_phase;
+  const double T = P.T, tl = P.tl, t2 = cpow(tl, 2), t3 = cpow(tl, 3), T2 = cpow(T, 2), T3 = cpow(T, 3), T4 = cpow(T, 4);
+  for (int k = 0; k < 3; ++k) {
+    // CubicHermitePolynomial::GetDerivativeOfPosWrtDuration (polynomial.cc:236-257)
+    const double x0 = xval(c, node_col(c, s, P.poly, kPos, k)), v0 = xval(c, node_col(c, s, P.poly, kVel, k));
+    const double x1 = xval(c, node_col(c, s, P.poly + 1, kPos, k)), v1 = xval(c, node_col(c, s, P.poly + 1, kVel, k));
+    const double dxdT = (t3 * (v0 + v1)) / T3 - (t2 * (2 * v0 + v1)) / T2 - (3 * t3 * (2 * x0 - 2 * x1 + T * v0 + T * v1)) / T4 +
+                        (2 * t2 * (3 * x0 - 3 * x1 + 2 * T * v0 + T * v1)) / T3;
+    J.dx[k] = inner * (dxdT - prev * P.v[k]);
+    J.v[k] = P.v[k];
+  }
+  const double last = last_phase_duration(c, si), eps = 1e-10;   // GetSegmentID over the phases
+  double acc = 0.0;
+  J.cur = si.n_phases - 1;
+  for (int ph = 0; ph < si.n_phases; ++ph) {
+    acc += phase_duration(c, si, last, ph);
+    if (acc >= t - eps) { J.cur = ph; break; }
+  }
+  J.n = si.n_phases;
+  J.col0 = si.col0;
+}
+TG_HD double sched_val(const SchedJac& J, int k, int col) {
+  const bool last = J.cur == J.n - 1;
+  if (col == J.cur && !last) return J.dx[k];
+  if (col < J.cur) return last ? -J.v[k] - J.dx[k] : -J.v[k];
+  return 0.0;
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -585,33 +723,34 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
   for (int r = 0; r < 3; ++r)
     for (int d = 1; d <= 2; ++d) {
       const int e = (r + d) % 3;
-      const double s = cross_el(rv, r, e);
-      for (int bb = 0; bb < 4; ++bb) {
-        const int col = basis_col(c, sp_force(ee), F.poly, bb, e);
-        em(r0 + AX + r, col, s * H[bb], col >= 0);
-      }
+      emit_dim(c, em, r0 + AX + r, sp_force(ee), F, H, e, cross_el(rv, r, e));
     }
-  for (int e = 0; e < 3; ++e)
-    for (int bb = 0; bb < 4; ++bb) {
-      const int col = basis_col(c, sp_force(ee), F.poly, bb, e);
-      em(r0 + LX + e, col, -H[bb], col >= 0);
-    }
+  for (int e = 0; e < 3; ++e) emit_dim(c, em, r0 + LX + e, sp_force(ee), F, H, e, -1.0);
   spline_basis(Tq, kPos, H);
-  for (int e = 0; e < 3; ++e)
-    for (int bb = 0; bb < 4; ++bb) {
-      const int col = basis_col(c, sp_torque(ee), Tq.poly, bb, e);
-      em(r0 + AX + e, col, -H[bb], col >= 0);
-    }
+  for (int e = 0; e < 3; ++e) emit_dim(c, em, r0 + AX + e, sp_torque(ee), Tq, H, e, -1.0);
   spline_basis(P, kPos, H);
   for (int r = 0; r < 3; ++r)
     for (int d = 1; d <= 2; ++d) {
       const int e = (r + d) % 3;
-      const double s = cross_el(F.p, r, e);
-      for (int bb = 0; bb < 4; ++bb) {
-        const int col = basis_col(c, sp_motion(ee), P.poly, bb, e);
-        em(r0 + AX + r, col, s * H[bb], col >= 0);
+      emit_dim(c, em, r0 + AX + r, sp_motion(ee), P, H, e, cross_el(F.p, r, e));
+    }
+  if (c.gait) {
+    // d/d ee schedule (dynamic_constraint.cc:116-122): force and ee-position terms; the reference
+    // omits the torque term here and so does this engine
+    SchedJac Jf, Jx;
+    sched_jac(c, sp_force(ee), t, F, Jf);
+    sched_jac(c, sp_motion(ee), t, P, Jx);
+    for (int r = 0; r < 3; ++r) {
+      const int e1 = (r + 1) % 3, e2 = (r + 2) % 3;
+      for (int col = 0; col < Jf.n - 1; ++col) {
+        const double a = cross_el(rv, r, e1) * sched_val(Jf, e1, col) + cross_el(rv, r, e2) * sched_val(Jf, e2, col);
+        const double b = cross_el(F.p, r, e1) * sched_val(Jx, e1, col) + cross_el(F.p, r, e2) * sched_val(Jx, e2, col);
+        em(r0 + AX + r, Jf.col0 + col, a + b, true);
       }
     }
+    for (int e = 0; e < 3; ++e)
+      for (int col = 0; col < Jf.n - 1; ++col) em(r0 + LX + e, Jf.col0 + col, -sched_val(Jf, e, col), true);
+  }
 }
 
 // RangeOfMotionConstraint instant (range_of_motion_constraint.cc:72-131)
@@ -646,11 +785,14 @@ TG_HD void eval_rom(const Ctx& c, const ItemDesc& it, Emit& em) {
   } else {
     spline_basis(P, kPos, H);
     for (int r = 0; r < 3; ++r)
-      for (int e = 0; e < 3; ++e)
-        for (int bb = 0; bb < 4; ++bb) {
-          const int col = basis_col(c, sp_motion(ee), P.poly, bb, e);
-          em(r0 + r, col, R[e][r] * H[bb], col >= 0);
-        }
+      for (int e = 0; e < 3; ++e) emit_dim(c, em, r0 + r, sp_motion(ee), P, H, e, R[e][r]);
+    if (c.gait) {   // b_R_w * d pos / d schedule (range_of_motion_constraint.cc:123-130)
+      SchedJac Jx;
+      sched_jac(c, sp_motion(ee), t, P, Jx);
+      for (int r = 0; r < 3; ++r)
+        for (int col = 0; col < Jx.n - 1; ++col)
+          em(r0 + r, Jx.col0 + col, R[0][r] * sched_val(Jx, 0, col) + R[1][r] * sched_val(Jx, 1, col) + R[2][r] * sched_val(Jx, 2, col), true);
+    }
   }
 }
 
@@ -671,11 +813,8 @@ TG_HD void eval_fdisc(const Ctx& c, const ItemDesc& it, Emit& em) {
   double H[4];
   spline_basis(F, kPos, H);
   for (int i = 0; i < 5; ++i)
-    for (int e = 0; e < 3; ++e)
-      for (int bb = 0; bb < 4; ++bb) {
-        const int col = basis_col(c, sp_force(ee), F.poly, bb, e);
-        em(r0 + i, col, b[i][e] * H[bb], col >= 0);
-      }
+    for (int e = 0; e < 3; ++e) emit_dim(c, em, r0 + i, sp_force(ee), F, H, e, b[i][e]);
+  double sc[2][5] = {{0, 0, 0, 0, 0}, {0, 0, 0, 0, 0}};   // F . d(pyramid)/d p_dim
   if (c.fdisc_motion) {   // AccumulateScaledRowJacobian: skipped when scale == 0.0 (:58)
     spline_basis(P, kPos, H);
     for (int dim = 0; dim < 2; ++dim) {
@@ -685,13 +824,22 @@ TG_HD void eval_fdisc(const Ctx& c, const ItemDesc& it, Emit& em) {
       ter_d_nbasis(*c.ter, 2, dim, P.p[0], P.p[1], dt2);
       pyramid(dn, dt1, dt2, mu, db);
       for (int i = 0; i < 5; ++i) {
-        const double s = dot3(F.p, db[i]);
-        for (int bb = 0; bb < 4; ++bb) {
-          const int col = basis_col(c, sp_motion(ee), P.poly, bb, dim);
-          em(r0 + i, col, s * H[bb], col >= 0 && s != 0.0);
-        }
+        sc[dim][i] = dot3(F.p, db[i]);
+        emit_dim(c, em, r0 + i, sp_motion(ee), P, H, dim, sc[dim][i], sc[dim][i] != 0.0);
       }
     }
+  }
+  if (c.gait) {   // schedule (force_constraint_discretized.cc:158-190): force linear form + motion scaled rows
+    SchedJac Jf, Jx;
+    sched_jac(c, sp_force(ee), t, F, Jf);
+    sched_jac(c, sp_motion(ee), t, P, Jx);
+    for (int i = 0; i < 5; ++i)
+      for (int col = 0; col < Jf.n - 1; ++col) {
+        double v = b[i][0] * sched_val(Jf, 0, col) + b[i][1] * sched_val(Jf, 1, col) + b[i][2] * sched_val(Jf, 2, col);
+        if (sc[0][i] != 0.0) v += sc[0][i] * sched_val(Jx, 0, col);
+        if (sc[1][i] != 0.0) v += sc[1][i] * sched_val(Jx, 1, col);
+        em(r0 + i, Jf.col0 + col, v, true);
+      }
   }
 }
 
@@ -798,6 +946,16 @@ TG_HD void eval_swing(const Ctx& c, const ItemDesc& it, Emit& em) {
   }
 }
 
+// TotalDurationConstraint (total_duration_constraint.cc:49-72): sum of the ee's optimised durations
+template <class Emit>
+TG_HD void eval_tdur(const Ctx& c, const ItemDesc& it, Emit& em) {
+  const SchedInfo si = c.sched[it.ee];
+  double sum = 0.0;
+  for (int i = 0; i < si.n_phases - 1; ++i) sum += c.x[si.col0 + i];
+  em.g(it.row0, sum);
+  for (int i = 0; i < si.n_phases - 1; ++i) em(it.row0, si.col0 + i, 1.0, true);
+}
+
 template <class Emit>
 TG_HD void eval_item(const Ctx& c, const ItemDesc& it, Emit& em) {
   switch (it.type) {
@@ -811,6 +969,7 @@ TG_HD void eval_item(const Ctx& c, const ItemDesc& it, Emit& em) {
     case IT_SACC: eval_sacc(c, it, em); break;
     case IT_BHGT: eval_height(c, it, SP_BASE_LIN, it.p0, em); break;
     case IT_SWING: eval_swing(c, it, em); break;
+    case IT_TDUR: eval_tdur(c, it, em); break;
   }
 }
 

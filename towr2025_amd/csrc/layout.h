@@ -37,6 +37,10 @@ struct Layout {
   std::vector<int32_t> nodecol;
   std::vector<double> dur;
   std::vector<SegRec> segs;     // (2 + 4 n_ee) records per time instant
+  bool gait = false;            // phase-duration optimisation (PhaseSplines, schedule variables)
+  std::vector<PolyPhase> pinfo; // PhaseSpline polynomial phases
+  std::vector<PhaseCol> pcols;  // PhaseSpline full-pattern columns
+  std::vector<SchedInfo> sched; // per endeffector (col0 = -1 without schedule variables)
   std::vector<ItemDesc> items;
   std::vector<int32_t> slots;     // build-time: candidate -> global CSR position (or -1)
   std::vector<SlotGroup> slot_groups;   // device slot table (see SlotGroup); item.slot indexes it

@@ -211,12 +211,66 @@ int init_values(const towr_problem_desc_t& d, const towr_init_t& in, const towr_
   return TOWR_OK;
 }
 
+// columns of every variable set in AddVariableSet order: node sets get NodeSet::col0, schedule
+// sets (PhaseDurations, n_phases - 1 variables, phase_durations.cc:41-77) fill sched[ee]
+int assign_columns(const towr_problem_desc_t& d, std::vector<NodeSet>& sets, std::vector<VarSetInfo>& vs,
+                   std::vector<SchedInfo>& sched, std::string& err) {
+  const int E = d.robot.n_ee;
+  sched.assign((size_t)E, SchedInfo{-1, 0, 0.0});
+  vs.clear();
+  int col = 0;
+  for (int i = 0; i < d.n_varsets; ++i) {
+    const int kind = d.varsets[i].kind, ee = d.varsets[i].ee;
+    if (kind != TOWR_VAR_BASE_LIN && kind != TOWR_VAR_BASE_ANG && (ee < 0 || ee >= E)) { err = "variable set endeffector out of range"; return TOWR_ERR_INVALID; }
+    int n = 0;
+    if (kind == TOWR_VAR_EE_SCHEDULE) {
+      if (!d.optimize_timings) { err = "ee-schedule variables require optimize_timings"; return TOWR_ERR_INVALID; }
+      if (sched[ee].col0 >= 0) { err = "variable set listed twice"; return TOWR_ERR_INVALID; }
+      double tt = 0.0;
+      for (int ph = 0; ph < d.n_phases[ee]; ++ph) tt += d.phase_durations[ee][ph];   // t_total_ (:47-50)
+      sched[ee] = SchedInfo{col, d.n_phases[ee], tt};
+      n = d.n_phases[ee] - 1;
+    } else {
+      int si = -1;
+      switch (kind) {
+        case TOWR_VAR_BASE_LIN: si = 0; break;
+        case TOWR_VAR_BASE_ANG: si = 1; break;
+        case TOWR_VAR_EE_MOTION: si = 2 + 4 * ee; break;
+        case TOWR_VAR_EE_ANG: si = 3 + 4 * ee; break;
+        case TOWR_VAR_EE_FORCE: si = 4 + 4 * ee; break;
+        case TOWR_VAR_EE_TORQUE: si = 5 + 4 * ee; break;
+        default: err = "unknown variable set kind " + std::to_string(kind); return TOWR_ERR_INVALID;
+      }
+      if (sets[si].col0 >= 0) { err = "variable set listed twice"; return TOWR_ERR_INVALID; }
+      sets[si].col0 = col;
+      n = sets[si].n_rows;
+    }
+    vs.push_back({kind, ee, col, n});
+    col += n;
+  }
+  for (auto& st : sets)
+    if (st.col0 < 0) { err = "every node variable set (base-lin, base-ang, ee motion/ang/force/torque) must be in the problem"; return TOWR_ERR_INVALID; }
+  if (d.optimize_timings)
+    for (int ee = 0; ee < E; ++ee)
+      if (sched[ee].col0 < 0) { err = "optimize_timings needs the ee-schedule variable set of every endeffector"; return TOWR_ERR_INVALID; }
+  return col;
+}
+
+// x0 of every set (node values; schedule = the first n_phases - 1 durations, phase_durations.cc:68-77)
+void fill_x0(const towr_problem_desc_t& d, std::vector<NodeSet>& sets, const std::vector<SchedInfo>& sched, int n, std::vector<double>& x0) {
+  x0.assign((size_t)n, 0.0);
+  for (auto& st : sets) { auto v = get_values(st); std::copy(v.begin(), v.end(), x0.begin() + st.col0); }
+  for (int ee = 0; ee < (int)sched.size(); ++ee)
+    if (sched[ee].col0 >= 0)
+      for (int ph = 0; ph < sched[ee].n_phases - 1; ++ph) x0[(size_t)sched[ee].col0 + ph] = d.phase_durations[ee][ph];
+}
+
 int item_rows(int type) {
   switch (type) {
     case IT_DYN: case IT_BMOT: return 6;
     case IT_ROM: case IT_SACC: return 3;
     case IT_FDISC: case IT_FNODE: return 5;
-    case IT_TERR: case IT_BHGT: return 1;
+    case IT_TERR: case IT_BHGT: case IT_TDUR: return 1;
     case IT_SWING: return 4;
   }
   return 0;
@@ -229,39 +283,18 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
   if (d.angular_rep != 0) { err = "only EulerZYX angular representation is supported (RotVec is next-tier)"; return TOWR_ERR_UNSUPPORTED; }
   const int E = d.robot.n_ee;
   if (E < 1 || E > TOWR_MAX_EE) { err = "robot.n_ee out of range"; return TOWR_ERR_INVALID; }
-  if (d.optimize_timings) { err = "phase-duration optimisation (gait optimisation) is not supported yet"; return TOWR_ERR_UNSUPPORTED; }
   if (!(d.total_time > 0) || !(d.duration_base_polynomial > 0)) { err = "bad total_time / duration_base_polynomial"; return TOWR_ERR_INVALID; }
 
   std::vector<double> base_d;
   std::vector<NodeSet> sets;
   if (int rc = make_sets(d, base_d, sets, err)) return rc;
-  auto set_index = [&](int kind, int ee) -> int {
-    if (kind == TOWR_VAR_BASE_LIN) return 0;
-    if (kind == TOWR_VAR_BASE_ANG) return 1;
-    if (ee < 0 || ee >= E) return -1;
-    switch (kind) {
-      case TOWR_VAR_EE_MOTION: return 2 + 4 * ee;
-      case TOWR_VAR_EE_ANG: return 3 + 4 * ee;
-      case TOWR_VAR_EE_FORCE: return 4 + 4 * ee;
-      case TOWR_VAR_EE_TORQUE: return 5 + 4 * ee;
-    }
-    return -1;
-  };
-
   // ---- variable sets in AddVariableSet order
-  int col = 0;
-  L.varsets.clear();
-  for (int i = 0; i < d.n_varsets; ++i) {
-    const int si = set_index(d.varsets[i].kind, d.varsets[i].ee);
-    if (si < 0) { err = "unsupported or malformed variable set " + std::to_string(i); return si == -1 ? TOWR_ERR_INVALID : TOWR_ERR_UNSUPPORTED; }
-    if (sets[si].col0 >= 0) { err = "variable set listed twice"; return TOWR_ERR_INVALID; }
-    sets[si].col0 = col;
-    L.varsets.push_back({d.varsets[i].kind, d.varsets[i].ee, col, sets[si].n_rows});
-    col += sets[si].n_rows;
+  {
+    const int n = assign_columns(d, sets, L.varsets, L.sched, err);
+    if (n < 0) return n;
+    L.n = n;
+    L.gait = d.optimize_timings != 0;
   }
-  for (auto& s : sets)
-    if (s.col0 < 0) { err = "every node variable set (base-lin, base-ang, ee motion/ang/force/torque) must be in the problem"; return TOWR_ERR_INVALID; }
-  L.n = col;
 
   // ---- node -> column table, spline metadata, polynomial durations
   L.spl.clear(); L.nodecol.clear(); L.dur.clear();
@@ -275,17 +308,36 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
     for (int idx = 0; idx < s.n_rows; ++idx)
       for (const Nvi& q : s.info(idx)) nc[(q.id * 2 + q.deriv) * 3 + q.dim] = s.col0 + idx;
     L.nodecol.insert(L.nodecol.end(), nc.begin(), nc.end());
+    m.ee = -1;
     if (si < 2) L.dur.insert(L.dur.end(), base_d.begin(), base_d.end());
     else {
       const int ee = (int)(si - 2) / 4;
       for (const PolyInfo& p : s.pinfo) L.dur.push_back(d.phase_durations[ee][p.phase] / p.n_polys_in_phase);  // :75-86
+      if (L.gait) {   // PhaseSpline (spline_holder.cc:50-66): polynomial phases + full-pattern columns
+        m.ee = ee;
+        m.pinfo_off = (int32_t)L.pinfo.size();
+        for (const PolyInfo& p : s.pinfo)
+          L.pinfo.push_back(PolyPhase{(int16_t)p.phase, (int16_t)p.poly_in_phase, (int16_t)p.n_polys_in_phase, 0});
+        for (int e = 0; e < 3; ++e) {
+          m.pcol_off[e] = (int32_t)L.pcols.size();
+          for (int idx = 0; idx < s.n_rows; ++idx) {
+            const std::vector<Nvi> q = s.info(idx);
+            if (q.empty() || q[0].dim != e) continue;
+            PhaseCol pc{};
+            pc.col = s.col0 + idx;
+            pc.n = (int8_t)std::min<size_t>(2, q.size());
+            for (int k = 0; k < pc.n; ++k) { pc.id[k] = (int16_t)q[k].id; pc.deriv[k] = (int8_t)q[k].deriv; }
+            L.pcols.push_back(pc);
+          }
+          m.pcol_n[e] = (int32_t)L.pcols.size() - m.pcol_off[e];
+        }
+      }
     }
     L.spl.push_back(m);
   }
 
   if (int rc = init_values(d, d.init, d.terrain, sets, err)) return rc;
-  L.x0.assign((size_t)L.n, 0.0);
-  for (auto& s : sets) { auto v = get_values(s); std::copy(v.begin(), v.end(), L.x0.begin() + s.col0); }
+  fill_x0(d, sets, L.sched, L.n, L.x0);
   L.desc = d;
 
   // ---- robot & terrain
@@ -392,8 +444,11 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
         info.rows = 3 * (nj > 0 ? nj : 0);
         break;
       }
-      case TOWR_C_TOTAL_DURATION:
-        err = "TotalDurationConstraint requires phase-duration optimisation (not supported yet)"; return TOWR_ERR_UNSUPPORTED;
+      case TOWR_C_TOTAL_DURATION:  // total_duration_constraint.cc:36-47
+        if (c.ee < 0 || c.ee >= E || L.sched[c.ee].col0 < 0) { err = "TotalDurationConstraint needs the ee's schedule variables"; return TOWR_ERR_INVALID; }
+        add(IT_TDUR, 0, c.ee, 0, row, 0.0, 0, 0, 0.0); ++inst;
+        info.rows = 1;
+        break;
       default: err = "unknown constraint kind"; return TOWR_ERR_INVALID;
     }
     row += info.rows;
@@ -439,6 +494,7 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
     Ctx cx{};
     cx.x = L.x0.data(); cx.nodecol = L.nodecol.data(); cx.spl = L.spl.data(); cx.dur = L.dur.data();
     cx.ter = &L.terrain; cx.rb = L.rb; cx.fdisc_motion = L.fdisc_motion;
+    cx.gait = L.gait; cx.pinfo = L.pinfo.data(); cx.pcols = L.pcols.data(); cx.sched = L.sched.data();
     for (size_t i = 0; i < L.items.size(); ++i) {
       item_cand_begin[i] = (int32_t)crow.size();
       RecordEmit em{&crow, &ccol, &cpres};
@@ -641,16 +697,12 @@ int initial_x_for(const towr_problem_desc_t& d, const towr_init_t& init, const t
   std::vector<double> base_d;
   std::vector<NodeSet> sets;
   if (int rc = make_sets(d, base_d, sets, err)) return rc;
-  int col = 0;
-  for (int i = 0; i < d.n_varsets; ++i) {   // same column layout as build_layout
-    const int k = d.varsets[i].kind, ee = d.varsets[i].ee;
-    int si = k == TOWR_VAR_BASE_LIN ? 0 : k == TOWR_VAR_BASE_ANG ? 1 : k == TOWR_VAR_EE_MOTION ? 2 + 4 * ee :
-             k == TOWR_VAR_EE_ANG ? 3 + 4 * ee : k == TOWR_VAR_EE_FORCE ? 4 + 4 * ee : 5 + 4 * ee;
-    sets[si].col0 = col; col += sets[si].n_rows;
-  }
+  std::vector<VarSetInfo> vs;
+  std::vector<SchedInfo> sched;
+  const int n = assign_columns(d, sets, vs, sched, err);   // same column layout as build_layout
+  if (n < 0) return n;
   if (int rc = init_values(d, init, ter, sets, err)) return rc;
-  x0.assign((size_t)col, 0.0);
-  for (auto& s : sets) { auto v = get_values(s); std::copy(v.begin(), v.end(), x0.begin() + s.col0); }
+  fill_x0(d, sets, sched, n, x0);
   return TOWR_OK;
 }
 

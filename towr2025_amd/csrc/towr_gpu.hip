@@ -38,6 +38,9 @@ struct KParams {
   const SplineMeta* spl;
   const double* dur;
   const SegRec* segs;
+  const PolyPhase* pinfo;        // phase-duration optimisation tables (see engine_math.h)
+  const PhaseCol* pcols;
+  const SchedInfo* sched;
   int32_t n_spl;
   const towr_terrain_t* terrains;
   int32_t terrain_per_problem;
@@ -97,6 +100,7 @@ __device__ __forceinline__ void eval_typed(const Ctx& c, const ItemDesc& it, Emi
   else if constexpr (TYPE == IT_SACC) eval_sacc(c, it, em);
   else if constexpr (TYPE == IT_BHGT) eval_height(c, it, SP_BASE_LIN, it.p0, em);
   else if constexpr (TYPE == IT_SWING) eval_swing(c, it, em);
+  else if constexpr (TYPE == IT_TDUR) eval_tdur(c, it, em);
 }
 
 // global -> LDS copy of n16 16-byte units: each thread issues up to K independent loads before its
@@ -140,9 +144,12 @@ __device__ __forceinline__ void copy_out(const double* __restrict__ src, double*
 // store: gfx950's vmcnt counts both); the tile's contiguous CSR range and g rows then leave with
 // 16-byte coalesced stores. Every kernel stages the problem's x in LDS (spline items gather their
 // nodes through the segment record's columns); node-value kinds also stage the node->column table.
-constexpr bool stages_nodes(int type) { return type == IT_FNODE || type == IT_TERR || type == IT_SACC || type == IT_BHGT || type == IT_SWING; }
+// GAIT: phase-duration optimisation (PhaseSplines evaluate polynomials from the node table).
+constexpr bool stages_nodes(int type, bool gait) {
+  return gait || type == IT_FNODE || type == IT_TERR || type == IT_SACC || type == IT_BHGT || type == IT_SWING;
+}
 
-template <int TYPE, int BLOCK>
+template <int TYPE, int BLOCK, bool GAIT>
 __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_kernel(KParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int total = P.B * P.ntiles;
@@ -168,7 +175,7 @@ __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_ker
     for (int i = threadIdx.x; i < P.n; i += BLOCK) xs[i] = xg[i];
   }
   if (threadIdx.x == 0) xs[P.n] = 0.0;
-  if constexpr (stages_nodes(TYPE))
+  if constexpr (stages_nodes(TYPE, GAIT))
     stage16<BLOCK>(reinterpret_cast<uint4*>(ns), reinterpret_cast<const uint4*>(P.nodecol), (P.n_nodecol + 3) >> 2);
   __syncthreads();
   const double* xsrc = xs;
@@ -179,6 +186,7 @@ __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_ker
     c.x = xsrc; c.nodecol = ncsrc; c.spl = P.spl; c.dur = P.dur;
     c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
     c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
+    c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.sched = P.sched;
     eval_typed<TYPE>(c, it, em);
     em.flush();
   }
@@ -188,20 +196,23 @@ __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_ker
     for (int i = threadIdx.x; i < T.r1 - T.r0; i += BLOCK) Gb[T.r0 + i] = smem[P.lds_rows_off + i];
 }
 
-const void* kernel_for(int type) {
+template <bool GAIT>
+const void* kernel_for_mode(int type) {
   switch (type) {
-    case IT_DYN: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_DYN, 256>);
-    case IT_ROM: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_ROM, 192>);
-    case IT_FDISC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_FDISC, 256>);
-    case IT_FNODE: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_FNODE, 64>);
-    case IT_TERR: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_TERR, 64>);
-    case IT_BMOT: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_BMOT, 64>);
-    case IT_SACC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_SACC, 64>);
-    case IT_BHGT: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_BHGT, 64>);
-    case IT_SWING: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_SWING, 64>);
+    case IT_DYN: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_DYN, 256, GAIT>);
+    case IT_ROM: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_ROM, 192, GAIT>);
+    case IT_FDISC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_FDISC, 256, GAIT>);
+    case IT_FNODE: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_FNODE, 64, GAIT>);
+    case IT_TERR: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_TERR, 64, GAIT>);
+    case IT_BMOT: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_BMOT, 64, GAIT>);
+    case IT_SACC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_SACC, 64, GAIT>);
+    case IT_BHGT: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_BHGT, 64, GAIT>);
+    case IT_SWING: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_SWING, 64, GAIT>);
+    case IT_TDUR: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_TDUR, 64, GAIT>);
   }
   return nullptr;
 }
+const void* kernel_for(int type, bool gait) { return gait ? kernel_for_mode<true>(type) : kernel_for_mode<false>(type); }
 
 }  // namespace
 
@@ -221,6 +232,9 @@ struct towr_gpu_handle_s {
   SplineMeta* d_spl = nullptr;
   double* d_dur = nullptr;
   SegRec* d_segs = nullptr;
+  PolyPhase* d_pinfo = nullptr;
+  PhaseCol* d_pcols = nullptr;
+  SchedInfo* d_sched = nullptr;
   towr_terrain_t* d_terrain = nullptr;      // base terrain (1 entry)
   towr_terrain_t* d_bterrain = nullptr;     // per-problem batch terrains
   int32_t bterrain_n = 0;
@@ -265,7 +279,7 @@ int bind(towr_gpu_handle h) {
 size_t lds_bytes(const Layout& L, int t) {
   size_t d = (size_t)L.type_lds[t];
   d += (size_t)((L.n + 2) & ~1);                                          // x + zero slot
-  if (stages_nodes(t)) d += (L.nodecol.size() + 3) / 4 * 2;                // node table (16-B units)
+  if (stages_nodes(t, L.gait)) d += (L.nodecol.size() + 3) / 4 * 2;        // node table (16-B units)
   return sizeof(double) * d;
 }
 
@@ -282,6 +296,7 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
     P.items = h->d_items; P.slots = h->d_slots; P.tiles = h->d_tiles;
     P.nodecol = h->d_nodecol; P.spl = h->d_spl; P.dur = h->d_dur;
     P.segs = h->d_segs; P.n_spl = (int32_t)L.spl.size();
+    P.pinfo = h->d_pinfo; P.pcols = h->d_pcols; P.sched = h->d_sched;
     P.terrains = terrains; P.terrain_per_problem = per_problem;
     P.B = B; P.tile0 = L.type_tile0[t]; P.ntiles = nt;
     P.lds_rows_off = L.type_lds_rows_off[t];
@@ -293,7 +308,7 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
     const int64_t grid = ((total + 7) / 8) * 8;
     if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
     void* args[] = {&P};
-    HIPCHK(h, hipLaunchKernel(kernel_for(t), dim3((unsigned)grid), dim3((unsigned)L.type_block[t]), args,
+    HIPCHK(h, hipLaunchKernel(kernel_for(t, L.gait), dim3((unsigned)grid), dim3((unsigned)L.type_block[t]), args,
                               lds_bytes(L, t), s));
   }
   return TOWR_OK;
@@ -385,12 +400,13 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
   int r;
   if ((r = upload(h, &h->d_items, L.items)) || (r = upload(h, &h->d_slots, L.slot_groups)) ||
       (r = upload(h, &h->d_tiles, L.tiles)) || (r = upload(h, &h->d_nodecol, nodecol16)) ||
-      (r = upload(h, &h->d_spl, L.spl)) || (r = upload(h, &h->d_dur, L.dur)) || (r = upload(h, &h->d_segs, L.segs)) || (r = upload(h, &h->d_terrain, ter)))
+      (r = upload(h, &h->d_spl, L.spl)) || (r = upload(h, &h->d_dur, L.dur)) || (r = upload(h, &h->d_segs, L.segs)) || (r = upload(h, &h->d_terrain, ter)) ||
+      (r = upload(h, &h->d_pinfo, L.pinfo)) || (r = upload(h, &h->d_pcols, L.pcols)) || (r = upload(h, &h->d_sched, L.sched)))
     return bail(r);
   for (int t = 0; t < IT_COUNT; ++t) {
     const size_t lds = lds_bytes(L, t);
     if (lds > 160 * 1024) { h->err = "tile too large for LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
-    if (lds > 64 * 1024 && hipFuncSetAttribute(kernel_for(t), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+    if (lds > 64 * 1024 && hipFuncSetAttribute(kernel_for(t, L.gait), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
       h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
     }
   }
@@ -401,6 +417,7 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
 int towr_gpu_destroy(towr_gpu_handle h) {
   if (!h) return TOWR_OK;
   void* dev[] = {h->d_items, h->d_slots, h->d_tiles, h->d_nodecol, h->d_spl, h->d_dur, h->d_segs, h->d_terrain,
+                 h->d_pinfo, h->d_pcols, h->d_sched,
                  h->d_bterrain, h->d_x, h->d_g, h->d_v};
   if (h->device >= 0) for (void* p : dev) if (p) (void)hipFree(p);
   void* host[] = {h->h_x, h->h_g, h->h_v};
@@ -509,7 +526,7 @@ int towr_gpu_eval_batch_device(towr_gpu_handle h, int32_t B, const double* X, in
 
 int towr_gpu_kernel_info(towr_gpu_handle h, int32_t kernel, const char** name, int32_t* n_tiles, int64_t* bytes_per_problem) {
   static const char* names[IT_COUNT] = {"dynamic", "range_of_motion", "force_discretized", "force_node", "terrain",
-                                        "base_motion", "spline_acc", "base_height", "swing"};
+                                        "base_motion", "spline_acc", "base_height", "swing", "total_duration"};
   if (!h || kernel < 0 || kernel >= IT_COUNT) return fail(h, TOWR_ERR_INVALID, "bad kernel index");
   if (name) *name = names[kernel];
   if (n_tiles) *n_tiles = h->L.type_tile0[kernel + 1] - h->L.type_tile0[kernel];
