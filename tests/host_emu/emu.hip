@@ -11,20 +11,18 @@
 using namespace tg;
 
 namespace {
-// same semantics as the kernel's TileEmit: 8 tile-relative positions per SlotGroup, adjacent
-// duplicates summed, one plain store per position
+// same semantics as the kernel's TileEmit: 8 tile-relative positions per SlotGroup, one plain store
+// per present candidate (a position written twice would be a layout bug: the check leaves NaN)
 struct AccEmit {
-  const SlotGroup* slot; int stride; double* v; double* gout; int j = 0; int ps = -1; double pv = 0.0;
+  const SlotGroup* slot; int stride; double* v; double* gout; int j = 0;
   void g(int row, double val) { gout[row] = val; }
   void operator()(int, int, double val, bool) {
     const int s = slot_pick(slot[(j / 8) * stride], j % 8);
     ++j;
     if (s == kSlotAbsent) return;
-    if (s == ps) { pv += val; return; }
-    if (ps >= 0) v[ps] = pv;
-    ps = s; pv = val;
+    v[s] = std::isnan(v[s]) ? val : std::nan("");
   }
-  void flush() { if (ps >= 0) v[ps] = pv; }
+  void flush() {}
 };
 }
 

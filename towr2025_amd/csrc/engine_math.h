@@ -117,9 +117,10 @@ TG_HD int slot_pick(const SlotGroup& q, int k) {   // select chain: k may be a r
   return (k & 1) ? (int)(w >> 16) : (int)(w & 0xFFFFu);
 }
 
-// item kinds whose emission can contain duplicate columns (stance polynomials whose two nodes share
-// one variable, junction nodes of SplineAcc); the others never do (checked at build time)
-TG_HD constexpr bool type_merges(int type) { return type <= 2 /* DYN, ROM, FDISC */ || type == 6 /* SACC */; }
+// No item emits the same column twice: contributions to one variable (the two nodes of a stance
+// polynomial sharing one variable, the junction node of SplineAcc) are summed into one candidate
+// before emission and the other candidate is marked absent (checked at build time), so every CSR
+// position receives exactly one plain store.
 
 struct Ctx {
   const SegRec* seg;            // this item's segment row (one SegRec per spline), or nullptr
@@ -143,6 +144,7 @@ struct SplinePt {
   int poly;
   double T, tl;
   const double* H;   // SegRec::H of this instant on the device (basis precomputed), else nullptr
+  const int32_t* C;  // SegRec::col of this instant on the device, else nullptr
   bool dyn;          // PhaseSpline: durations (hence polynomial, local time, basis) depend on x
   double p[3], v[3], a[3];
 };
@@ -288,6 +290,7 @@ TG_HD void spline_eval(const Ctx& c, int s, double t, SplinePt& o) {
   const SegRec& r = c.seg[s];
   o.poly = r.poly; o.tl = r.tl; o.T = r.T;
   o.H = &r.H[0][0];
+  o.C = &r.col[0][0];
   for (int e = 0; e < 3; ++e) {
     const double u0 = c.x[r.col[0][e]], u1 = c.x[r.col[1][e]], u2 = c.x[r.col[2][e]], u3 = c.x[r.col[3][e]];
     o.p[e] = r.H[0][0] * u0 + r.H[0][1] * u1 + r.H[0][2] * u2 + r.H[0][3] * u3;
@@ -329,10 +332,19 @@ template <class Emit>
 TG_HD void emit_dim(const Ctx& c, Emit& em, int row, int s, const SplinePt& P, const double H[4], int e, double scale,
                     bool pres = true) {
   if (!P.dyn) {
-    for (int bb = 0; bb < 4; ++bb) {
-      const int col = basis_col(c, s, P.poly, bb, e);
-      em(row, col, scale * H[bb], pres && col >= 0);
-    }
+    int col[4];
+    for (int bb = 0; bb < 4; ++bb) col[bb] = basis_col(c, s, P.poly, bb, e);
+    // a stance polynomial whose two nodes share one position variable (NodesVariablesPhaseBased,
+    // nodes_variables_phase_based.cc:215-258): coeffRef sums both contributions into one entry
+#if defined(__HIP_DEVICE_COMPILE__)
+    const bool shared = P.C[e] == P.C[2 * 3 + e];   // both constant -> both absent anyway
+#else
+    const bool shared = col[0] >= 0 && col[0] == col[2];
+#endif
+    em(row, col[0], scale * (shared ? H[0] + H[2] : H[0]), pres && col[0] >= 0);
+    em(row, col[1], scale * H[1], pres && col[1] >= 0);
+    em(row, col[2], scale * H[2], pres && col[2] >= 0 && !shared);
+    em(row, col[3], scale * H[3], pres && col[3] >= 0);
     return;
   }
   const SplineMeta m = c.spl[s];
@@ -910,15 +922,13 @@ TG_HD void eval_sacc(const Ctx& c, const ItemDesc& it, Emit& em) {
   for (int e = 0; e < 3; ++e) em.g(it.row0 + e, a.a[e] - b.a[e]);
   double Hp[4], Hn[4];
   hermite_dacc(Tp, Tp, Hp); hermite_dacc(Tn, 0.0, Hn);
-  // acc_prev - acc_next; node j+1 belongs to both polynomials: its two contributions are emitted
-  // back to back so the emitter can merge them (emit order: n_j.p, n_j.v, n_j+1.p x2, n_j+1.v x2, n_j+2.p, n_j+2.v)
+  // acc_prev - acc_next; node j+1 belongs to both polynomials (a base spline: its values are their
+  // own variables), so its two contributions are summed into one candidate each for p and v
   for (int e = 0; e < 3; ++e) {
     em(it.row0 + e, basis_col(c, s, j, 0, e), Hp[0], true);
     em(it.row0 + e, basis_col(c, s, j, 1, e), Hp[1], true);
-    em(it.row0 + e, basis_col(c, s, j, 2, e), Hp[2], true);
-    em(it.row0 + e, basis_col(c, s, j + 1, 0, e), -Hn[0], true);
-    em(it.row0 + e, basis_col(c, s, j, 3, e), Hp[3], true);
-    em(it.row0 + e, basis_col(c, s, j + 1, 1, e), -Hn[1], true);
+    em(it.row0 + e, basis_col(c, s, j, 2, e), Hp[2] - Hn[0], true);
+    em(it.row0 + e, basis_col(c, s, j, 3, e), Hp[3] - Hn[1], true);
     em(it.row0 + e, basis_col(c, s, j + 1, 2, e), -Hn[2], true);
     em(it.row0 + e, basis_col(c, s, j + 1, 3, e), -Hn[3], true);
   }

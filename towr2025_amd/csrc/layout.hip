@@ -537,20 +537,15 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
   for (size_t i = 0; i < L.items.size(); ++i) {
     L.items[i].slot = item_cand_begin[i];
     L.items[i].ncand = item_cand_begin[i + 1] - item_cand_begin[i];
-    // The device merges contributions to one slot (duplicate columns, e.g. the two nodes of a
-    // stance polynomial sharing one variable) only when they are adjacent among the item's present
-    // candidates; every item's emission order is written so that they are — verified here.
+    // every present candidate of an item has its own CSR position (see engine_math.h)
     std::vector<int32_t> seen;
-    int32_t prev = -1;
-    const bool merges = type_merges(L.items[i].type);
     for (int32_t q = item_cand_begin[i]; q < item_cand_begin[i + 1]; ++q) {
       if (L.slots[q] < 0) continue;
-      if ((L.slots[q] != prev || !merges) && std::find(seen.begin(), seen.end(), L.slots[q]) != seen.end()) {
-        err = "internal: non-adjacent duplicate candidate in item type " + std::to_string(L.items[i].type);
+      if (std::find(seen.begin(), seen.end(), L.slots[q]) != seen.end()) {
+        err = "internal: duplicate candidate in item type " + std::to_string(L.items[i].type);
         return TOWR_ERR_INVALID;
       }
       seen.push_back(L.slots[q]);
-      prev = L.slots[q];
     }
   }
 

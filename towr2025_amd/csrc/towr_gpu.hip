@@ -56,19 +56,15 @@ struct KParams {
 // Stores candidate j of this lane into the LDS tile at its tile-relative CSR position. Positions
 // come 8 per 16-byte SlotGroup; the next group is prefetched while the current one is consumed, so
 // the slot-table latency (L2: the table is shared by every problem of the batch) hides behind 8
-// candidates of arithmetic. The candidate's column is never needed on the device. Contributions to
-// one position (duplicate columns, e.g. the two nodes of a stance polynomial sharing one variable)
-// are adjacent among an item's present candidates (checked at build time) and summed in registers
-// (MERGE kinds), so every position receives exactly one plain LDS store.
-template <int BLOCK, bool MERGE>
+// candidates of arithmetic. The candidate's column is never needed on the device, and no item emits
+// a column twice (engine_math.h), so every position receives exactly one plain LDS store.
+template <int BLOCK>
 struct TileEmit {
   const SlotGroup* slot;   // this lane's group 0; group g at slot[g * BLOCK]
   double* out;             // LDS tile, tile-relative
   double* gout;            // LDS g rows, tile-relative
   SlotGroup cur, nxt;      // groups g, g+1
   int j = 0;
-  int ps = -1;
-  double pv = 0.0;
   __device__ __forceinline__ TileEmit(const SlotGroup* s, double* o, double* go) : slot(s), out(o), gout(go) {
     cur = s[0];
     nxt = s[BLOCK];
@@ -78,16 +74,9 @@ struct TileEmit {
     const int s = slot_pick(cur, j & 7);
     ++j;
     if ((j & 7) == 0) { cur = nxt; nxt = slot[((j >> 3) + 1) * BLOCK]; }
-    if (s == kSlotAbsent) return;
-    if constexpr (!MERGE) {
-      out[s] = v;
-    } else {
-      if (s == ps) { pv += v; return; }
-      if (ps >= 0) out[ps] = pv;
-      ps = s; pv = v;
-    }
+    if (s != kSlotAbsent) out[s] = v;
   }
-  __device__ __forceinline__ void flush() { if (MERGE && ps >= 0) out[ps] = pv; }
+  __device__ __forceinline__ void flush() {}
 };
 
 template <int TYPE, class Emit>
@@ -168,7 +157,7 @@ __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_ker
   const double* xg = P.X + (int64_t)b * P.ldx;
   // issue the lane's item, first slot groups and (below) the x / node-table staging loads together
   const ItemDesc it = P.items[T.i0 + threadIdx.x];
-  TileEmit<BLOCK, type_merges(TYPE)> em(P.slots + it.slot, smem, smem + P.lds_rows_off - T.r0);
+  TileEmit<BLOCK> em(P.slots + it.slot, smem, smem + P.lds_rows_off - T.r0);
   // x (+ a zero at index n for constant node values) and, for node-value kinds, the node table
   double* xs = smem + P.lds_x_off;
   int32_t* ns = reinterpret_cast<int32_t*>(smem + P.lds_x_off + P.n_pad);
