@@ -14,12 +14,12 @@ namespace {
 // same semantics as the kernel's TileEmit: 8 tile-relative positions per SlotGroup, one plain store
 // per present candidate (a position written twice would be a layout bug: the check leaves NaN)
 struct AccEmit {
-  const SlotGroup* slot; int stride; double* v; double* gout; int j = 0;
+  const SlotGroup* slot; int stride; double* v; double* gout; int nvals; int j = 0;
   void g(int row, double val) { gout[row] = val; }
   void operator()(int, int, double val, bool) {
     const int s = slot_pick(slot[(j / 8) * stride], j % 8);
     ++j;
-    if (s == kSlotAbsent) return;
+    if (s >= nvals) return;   // the lane's dummy slot (absent candidate)
     v[s] = std::isnan(v[s]) ? val : std::nan("");
   }
   void flush() {}
@@ -40,7 +40,7 @@ extern "C" int emu_eval(const towr_problem_desc_t* d, const double* x, double* g
     for (int l = td.i0; l < td.i1; ++l) {
       const ItemDesc& it = L.items[l];
       if (it.type == IT_NONE) continue;
-      AccEmit em{L.slot_groups.data() + it.slot, td.i1 - td.i0, v + td.v0, g};
+      AccEmit em{L.slot_groups.data() + it.slot, td.i1 - td.i0, v + td.v0, g, td.v1 - td.v0};
       c.seg = it.seg >= 0 ? L.segs.data() + (size_t)it.seg * L.spl.size() : nullptr;
       eval_item(c, it, em);
       em.flush();

@@ -106,9 +106,10 @@ struct SegRec {
   int32_t col[4][3];   // x column of basis value b, dim e (device numbering: a constant node -> n, x[n] = 0)
 };
 
-// Slot table entry: 8 tile-relative CSR positions (uint16, 0xFFFF = candidate absent) of one lane's
-// candidates 8g..8g+7, one 16-byte load per lane; group g of lane l of a tile sits at
-// tile_base + g * block + l (a wave's load is one coalesced 1 KiB access)
+// Slot table entry: 8 tile-relative LDS positions (uint16) of one lane's candidates 8g..8g+7, one
+// 16-byte load per lane; group g of lane l of a tile sits at tile_base + g * block + l (a wave's
+// load is one coalesced 1 KiB access). A present candidate's position is its CSR position minus
+// the tile's first; an absent one's is the lane's dummy slot past the tile's values.
 struct alignas(16) SlotGroup { uint32_t w[4]; };
 constexpr int kSlotAbsent = 0xFFFF;
 TG_HD int slot_pick(const SlotGroup& q, int k) {   // select chain: k may be a runtime value

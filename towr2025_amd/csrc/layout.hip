@@ -624,7 +624,9 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
       }
       items.insert(items.end(), per_type_items[t].begin(), per_type_items[t].end());
       L.type_block[t] = type_spec(t, E).block;
-      L.type_lds_rows_off[t] = (maxv + 1) & ~1;
+      // LDS: [tile values | 64 dummy slots (absent candidates, by wave lane) | g rows]
+      L.type_lds_dummy_off[t] = (maxv + 1) & ~1;
+      L.type_lds_rows_off[t] = L.type_lds_dummy_off[t] + 64;   // one per wave lane: waves never collide within an instruction
       L.type_lds[t] = L.type_lds_rows_off[t] + ((maxr + 1) & ~1);
     }
     L.type_tile0[IT_COUNT] = (int32_t)L.tiles.size();
@@ -644,8 +646,9 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
         if (it.type != IT_NONE)
           for (int j = 0; j < it.ncand; ++j) {
             const int32_t g = L.slots[it.slot + j];
-            const uint32_t rel = g < 0 ? (uint32_t)kSlotAbsent : (uint32_t)(g - td.v0);
-            if (g >= 0 && (g < td.v0 || g >= td.v1 || rel >= (uint32_t)kSlotAbsent)) { err = "internal: slot outside its tile"; return TOWR_ERR_INVALID; }
+            // an absent candidate is stored into the lane's own dummy slot (no branch, no LDS conflict)
+            const uint32_t rel = g < 0 ? (uint32_t)(L.type_lds_dummy_off[td.type] + (l & 63)) : (uint32_t)(g - td.v0);
+            if (rel >= (uint32_t)kSlotAbsent || (g >= 0 && (g < td.v0 || g >= td.v1))) { err = "internal: slot outside its tile"; return TOWR_ERR_INVALID; }
             uint32_t& w = groups[base + (size_t)(j / 8) * block + l].w[(j % 8) / 2];
             const int sh = (j & 1) ? 16 : 0;
             w = (w & ~(0xFFFFu << sh)) | (rel << sh);

@@ -57,7 +57,8 @@ struct KParams {
 // come 8 per 16-byte SlotGroup; the next group is prefetched while the current one is consumed, so
 // the slot-table latency (L2: the table is shared by every problem of the batch) hides behind 8
 // candidates of arithmetic. The candidate's column is never needed on the device, and no item emits
-// a column twice (engine_math.h), so every position receives exactly one plain LDS store.
+// a column twice (engine_math.h), so every position receives exactly one plain LDS store; absent
+// candidates (constant node values) go to a per-lane dummy slot, so the store needs no branch.
 template <int BLOCK>
 struct TileEmit {
   const SlotGroup* slot;   // this lane's group 0; group g at slot[g * BLOCK]
@@ -74,7 +75,7 @@ struct TileEmit {
     const int s = slot_pick(cur, j & 7);
     ++j;
     if ((j & 7) == 0) { cur = nxt; nxt = slot[((j >> 3) + 1) * BLOCK]; }
-    if (s != kSlotAbsent) out[s] = v;
+    out[s] = v;   // absent candidates land in the lane's dummy slot
   }
   __device__ __forceinline__ void flush() {}
 };
