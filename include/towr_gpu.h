@@ -209,9 +209,11 @@ int towr_gpu_eval_batch_device(towr_gpu_handle h, int32_t B,
 /* Host batch (H2D of X, D2H of G and V through pinned staging; contiguous lds = n, m, nnz).      */
 int towr_gpu_eval_batch(towr_gpu_handle h, int32_t B, const double* X, double* G, double* V);
 
-/* The engine launches one kernel per constraint kind ("kernel" 0..towr_gpu_num_kernels()-1).
- * For roofline accounting: its name, tile count, and algorithmic bytes per problem (CSR values
- * and g rows written + distinct x entries read), and a launch of that kernel alone.             */
+/* The engine launches one kernel per launch class ("kernel" 0..towr_gpu_num_kernels()-1): the
+ * Dynamic, RangeOfMotion and ForceConstraintDiscretized kinds each have their own, the small kinds
+ * (node-value constraints, SplineAcc, BaseMotion, TotalDuration) share one. For roofline
+ * accounting: its name, tiles (or tile groups) per problem, and algorithmic bytes per problem (CSR
+ * values and g rows written + distinct x entries read), and a launch of that kernel alone.      */
 int towr_gpu_kernel_info(towr_gpu_handle h, int32_t kernel, const char** name, int32_t* n_tiles,
                          int64_t* bytes_per_problem);
 int towr_gpu_eval_batch_device_kernel(towr_gpu_handle h, int32_t kernel, int32_t B,

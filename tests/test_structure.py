@@ -75,8 +75,7 @@ def test_layout_only_handle_cannot_evaluate():
 def test_kernel_bytes_cover_the_call():
     p = TowrGpuProblem(CONFIGS["anymal_trot_2p4s"], device=-1)
     ks = p.kernels()
-    assert {k[1] for k in ks} == {"dynamic", "range_of_motion", "force_discretized", "terrain", "spline_acc",
-                                  "base_height", "swing"}
+    assert {k[1] for k in ks} == {"dynamic", "range_of_motion", "force_discretized", "small_kinds"}
     # every value and row is written by exactly one kernel
     written = sum(b for *_, b in ks)
     assert written >= 8 * (p.m + p.nnz)

@@ -11,18 +11,20 @@ import json
 import sys
 from collections import defaultdict
 
-NAMES = ["dynamic", "range_of_motion", "force_discretized", "force_node", "terrain", "base_motion",
-         "spline_acc", "base_height", "swing", "total_duration"]
+NAMES = ["dynamic", "range_of_motion", "force_discretized"]
 
 
 def per_kernel(d, counter):
     acc = defaultdict(list)
     for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
         k = r["Kernel_Name"]
-        if "towr_tile_kernel<" not in k or r["Counter_Name"] != counter:
+        if r["Counter_Name"] != counter:
             continue
-        t = int(k.split("towr_tile_kernel<")[1].split(",")[0])
-        acc[NAMES[t]].append(float(r["Counter_Value"]) * 1024.0)
+        if "towr_misc_kernel" in k:
+            acc["small_kinds"].append(float(r["Counter_Value"]) * 1024.0)
+        elif "towr_tile_kernel<" in k:
+            t = int(k.split("towr_tile_kernel<")[1].split(",")[0])
+            acc[NAMES[t]].append(float(r["Counter_Value"]) * 1024.0)
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
 

@@ -62,7 +62,17 @@ struct Layout {
   // algorithmic bytes per problem of each type's launch: CSR values + g rows written, distinct
   // x columns read (= the columns of its Jacobian rows)
   int64_t type_bytes[IT_COUNT] = {};
+  // small kinds (is_misc_kind) run in one launch: kMiscWaves tiles per block, one per wave
+  std::vector<int32_t> misc_tiles;   // groups of kMiscWaves tile indices (-1 = empty wave)
+  int32_t misc_dummy_off = 0, misc_rows_off = 0, misc_stride = 0;   // per-wave LDS layout (doubles)
+  int64_t misc_bytes = 0;
 };
+
+constexpr int kMiscWaves = 4;
+constexpr bool is_misc_kind(int t) { return t != IT_DYN && t != IT_ROM && t != IT_FDISC; }
+
+// launch classes: the three heavy kinds have their own kernels, the small kinds share one
+enum LaunchClass { LC_DYN = 0, LC_ROM = 1, LC_FDISC = 2, LC_MISC = 3, LC_COUNT = 4 };
 
 // LDS tile caps (doubles of CSR values / rows per tile)
 constexpr int kTileValueCap = 8192;

@@ -630,6 +630,29 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
       L.type_lds[t] = L.type_lds_rows_off[t] + ((maxr + 1) & ~1);
     }
     L.type_tile0[IT_COUNT] = (int32_t)L.tiles.size();
+    // the small kinds (one-wave tiles) share one launch: up to 4 tiles per block, one per wave, with
+    // a common per-wave LDS layout [values | 64 dummy slots | g rows]
+    {
+      std::vector<int32_t> mt;
+      int mv = 0, mr = 0;
+      for (int t = 0; t < IT_COUNT; ++t) {
+        if (!is_misc_kind(t)) continue;
+        if (type_spec(t, E).block != 64) { err = "internal: small kinds must use one-wave tiles"; return TOWR_ERR_INVALID; }
+        for (int ti = L.type_tile0[t]; ti < L.type_tile0[t + 1]; ++ti) {
+          mt.push_back(ti);
+          mv = std::max(mv, L.tiles[ti].v1 - L.tiles[ti].v0);
+          mr = std::max(mr, L.tiles[ti].r1 - L.tiles[ti].r0);
+        }
+      }
+      L.misc_dummy_off = (mv + 1) & ~1;
+      L.misc_rows_off = L.misc_dummy_off + 64;
+      L.misc_stride = L.misc_rows_off + ((mr + 1) & ~1);
+      for (int t = 0; t < IT_COUNT; ++t)
+        if (is_misc_kind(t)) L.type_lds_dummy_off[t] = L.misc_dummy_off;
+      L.misc_tiles.clear();
+      for (size_t q = 0; q < mt.size(); q += kMiscWaves)
+        for (int w = 0; w < kMiscWaves; ++w) L.misc_tiles.push_back(q + w < mt.size() ? mt[q + w] : -1);
+    }
     // slot table per tile: lane l's candidates 8g..8g+7 in group g at base + g * block + l, as
     // tile-relative uint16 positions; two spare groups per lane absorb the kernel's prefetch
     std::vector<SlotGroup> groups;
@@ -670,6 +693,18 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
       int64_t nx = 0;
       for (uint8_t u : used) nx += u;
       L.type_bytes[t] = 8 * (nv + nr + nx);
+    }
+    {   // the merged small-kind launch: union of their x columns
+      int64_t nv = 0, nr = 0, nx = 0;
+      std::vector<uint8_t> used((size_t)L.n, 0);
+      for (int32_t ti : L.misc_tiles) {
+        if (ti < 0) continue;
+        const TileDesc& td = L.tiles[ti];
+        nv += td.v1 - td.v0; nr += td.r1 - td.r0;
+        for (int32_t k = td.v0; k < td.v1; ++k) used[L.col[k]] = 1;
+      }
+      for (uint8_t u : used) nx += u;
+      L.misc_bytes = 8 * (nv + nr + nx);
     }
   }
   return TOWR_OK;

@@ -50,6 +50,8 @@ struct KParams {
   int32_t lds_x_off;             // start of the staged x (+ zero slot) and node-column table
   int32_t n, n_pad, n_nodecol;
   int32_t want_g, want_jac, fdisc_motion;
+  const int32_t* misc_tiles;      // merged small-kind launch: kMiscWaves tile ids per group
+  int32_t misc_stride, misc_rows_off;
   RobotC rb;
 };
 
@@ -116,19 +118,34 @@ __device__ __forceinline__ void stage16(uint4* __restrict__ dst, const uint4* __
 // streamed (never re-read by the kernel); plain stores cost ~25 % more kernel time on MI355X
 // (ANYmal, B = 4096: 0.532 -> 0.444 ms per step with non-temporal stores).
 typedef double dbl2_t __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void copy_out(const double* __restrict__ src, double* __restrict__ dst, int n) {
+__device__ __forceinline__ void copy_out(const double* __restrict__ src, double* __restrict__ dst, int n,
+                                         int tid, int nthr) {
   if (n <= 0) return;
   const int head = (reinterpret_cast<uintptr_t>(dst) & 15) ? 1 : 0;
-  if (head && threadIdx.x == 0) __builtin_nontemporal_store(src[0], dst);
+  if (head && tid == 0) __builtin_nontemporal_store(src[0], dst);
   const int m = (n - head) >> 1;
   dbl2_t* d2 = reinterpret_cast<dbl2_t*>(dst + head);
-  for (int i = threadIdx.x; i < m; i += blockDim.x) {
+  for (int i = tid; i < m; i += nthr) {
     dbl2_t v;
     v.x = src[head + 2 * i];
     v.y = src[head + 2 * i + 1];
     __builtin_nontemporal_store(v, d2 + i);
   }
-  if (((n - head) & 1) && threadIdx.x == 0) __builtin_nontemporal_store(src[n - 1], dst + n - 1);
+  if (((n - head) & 1) && tid == 0) __builtin_nontemporal_store(src[n - 1], dst + n - 1);
+}
+
+// global -> LDS staging of the problem's x (+ zero slot at n) and optionally the node table
+template <int BLOCK, bool NODES>
+__device__ __forceinline__ void stage_x(const KParams& P, const double* xg, double* xs, int32_t* ns) {
+  if ((reinterpret_cast<uintptr_t>(xg) & 15) == 0) {
+    stage16<BLOCK>(reinterpret_cast<uint4*>(xs), reinterpret_cast<const uint4*>(xg), P.n >> 1);
+    if ((P.n & 1) && threadIdx.x == 0) xs[P.n - 1] = xg[P.n - 1];
+  } else {
+    for (int i = threadIdx.x; i < P.n; i += BLOCK) xs[i] = xg[i];
+  }
+  if (threadIdx.x == 0) xs[P.n] = 0.0;
+  if constexpr (NODES)
+    stage16<BLOCK>(reinterpret_cast<uint4*>(ns), reinterpret_cast<const uint4*>(P.nodecol), (P.n_nodecol + 3) >> 2);
 }
 
 // One block = one tile (consecutive instances of one constraint kind) of one problem; one item per
@@ -138,10 +155,9 @@ __device__ __forceinline__ void copy_out(const double* __restrict__ src, double*
 // store: gfx950's vmcnt counts both); the tile's contiguous CSR range and g rows then leave with
 // 16-byte coalesced stores. Every kernel stages the problem's x in LDS (spline items gather their
 // nodes through the segment record's columns); node-value kinds also stage the node->column table.
-// GAIT: phase-duration optimisation (PhaseSplines evaluate polynomials from the node table).
-constexpr bool stages_nodes(int type, bool gait) {
-  return gait || type == IT_FNODE || type == IT_TERR || type == IT_SACC || type == IT_BHGT || type == IT_SWING;
-}
+// The heavy kinds read spline nodes through the segment records; with phase-duration optimisation
+// (GAIT) their PhaseSplines evaluate polynomials from the node table, which is then staged too.
+constexpr bool stages_nodes(int type, bool gait) { return gait || is_misc_kind(type); }
 
 template <int TYPE, int BLOCK, bool GAIT>
 __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_kernel(KParams P) {
@@ -162,15 +178,7 @@ __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_ker
   // x (+ a zero at index n for constant node values) and, for node-value kinds, the node table
   double* xs = smem + P.lds_x_off;
   int32_t* ns = reinterpret_cast<int32_t*>(smem + P.lds_x_off + P.n_pad);
-  if ((reinterpret_cast<uintptr_t>(xg) & 15) == 0) {
-    stage16<BLOCK>(reinterpret_cast<uint4*>(xs), reinterpret_cast<const uint4*>(xg), P.n >> 1);
-    if ((P.n & 1) && threadIdx.x == 0) xs[P.n - 1] = xg[P.n - 1];
-  } else {
-    for (int i = threadIdx.x; i < P.n; i += BLOCK) xs[i] = xg[i];
-  }
-  if (threadIdx.x == 0) xs[P.n] = 0.0;
-  if constexpr (stages_nodes(TYPE, GAIT))
-    stage16<BLOCK>(reinterpret_cast<uint4*>(ns), reinterpret_cast<const uint4*>(P.nodecol), (P.n_nodecol + 3) >> 2);
+  stage_x<BLOCK, stages_nodes(TYPE, GAIT)>(P, xg, xs, ns);
   __syncthreads();
   const double* xsrc = xs;
   const int32_t* ncsrc = ns;
@@ -185,9 +193,64 @@ __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_ker
     em.flush();
   }
   __syncthreads();
-  if (P.want_jac) copy_out(smem, Vb + T.v0, T.v1 - T.v0);
+  if (P.want_jac) copy_out(smem, Vb + T.v0, T.v1 - T.v0, threadIdx.x, BLOCK);
   if (P.want_g)
     for (int i = threadIdx.x; i < T.r1 - T.r0; i += BLOCK) __builtin_nontemporal_store(smem[P.lds_rows_off + i], Gb + T.r0 + i);
+}
+
+// The small kinds (node-value constraints, SplineAcc, BaseMotion, TotalDuration: a few kB of output
+// per problem each) in one launch: a block = kMiscWaves one-wave tiles of one problem, sharing the
+// staged x and node table; each wave evaluates and writes out its own tile.
+template <bool GAIT>
+__global__ void __launch_bounds__(64 * kMiscWaves, 1) towr_misc_kernel(KParams P) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  constexpr int BLOCK = 64 * kMiscWaves;
+  const int total = P.B * P.ntiles;   // ntiles = groups per problem
+  const int per = (total + 7) / 8;
+  const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+  if (w >= total) return;
+  const int b = w / P.ntiles;
+  const int wave = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+  const int ti = P.misc_tiles[(w % P.ntiles) * kMiscWaves + wave];
+  TileDesc T{};
+  ItemDesc it{};
+  it.type = IT_NONE;
+  it.slot = 0;
+  if (ti >= 0) {
+    T = P.tiles[ti];
+    it = P.items[T.i0 + lane];
+  }
+  double* wl = smem + wave * P.misc_stride;
+  TileEmit<64> em(P.slots + it.slot, wl, wl + P.misc_rows_off - T.r0);
+  double* xs = smem + P.lds_x_off;
+  int32_t* ns = reinterpret_cast<int32_t*>(smem + P.lds_x_off + P.n_pad);
+  stage_x<BLOCK, true>(P, P.X + (int64_t)b * P.ldx, xs, ns);
+  __syncthreads();
+  if (it.type != IT_NONE) {
+    Ctx c;
+    c.seg = it.seg >= 0 ? P.segs + (int64_t)it.seg * P.n_spl : nullptr;
+    c.x = xs; c.nodecol = ns; c.spl = P.spl; c.dur = P.dur;
+    c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
+    c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
+    c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.sched = P.sched;
+    switch (it.type) {   // wave-uniform: a wave holds one tile of one kind
+      case IT_FNODE: eval_fnode(c, it, em); break;
+      case IT_TERR: eval_height(c, it, sp_motion(it.ee), 0.0, em); break;
+      case IT_BMOT: eval_bmot(c, it, em); break;
+      case IT_SACC: eval_sacc(c, it, em); break;
+      case IT_BHGT: eval_height(c, it, SP_BASE_LIN, it.p0, em); break;
+      case IT_SWING: eval_swing(c, it, em); break;
+      case IT_TDUR: eval_tdur(c, it, em); break;
+      default: break;
+    }
+  }
+  __syncthreads();
+  if (ti < 0) return;
+  double* Vb = P.V + (int64_t)b * P.ldv;
+  double* Gb = P.G + (int64_t)b * P.ldg;
+  if (P.want_jac) copy_out(wl, Vb + T.v0, T.v1 - T.v0, lane, 64);
+  if (P.want_g)
+    for (int i = lane; i < T.r1 - T.r0; i += 64) __builtin_nontemporal_store(wl[P.misc_rows_off + i], Gb + T.r0 + i);
 }
 
 template <bool GAIT>
@@ -196,17 +259,14 @@ const void* kernel_for_mode(int type) {
     case IT_DYN: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_DYN, 256, GAIT>);
     case IT_ROM: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_ROM, 192, GAIT>);
     case IT_FDISC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_FDISC, 256, GAIT>);
-    case IT_FNODE: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_FNODE, 64, GAIT>);
-    case IT_TERR: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_TERR, 64, GAIT>);
-    case IT_BMOT: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_BMOT, 64, GAIT>);
-    case IT_SACC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_SACC, 64, GAIT>);
-    case IT_BHGT: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_BHGT, 64, GAIT>);
-    case IT_SWING: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_SWING, 64, GAIT>);
-    case IT_TDUR: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_TDUR, 64, GAIT>);
   }
   return nullptr;
 }
 const void* kernel_for(int type, bool gait) { return gait ? kernel_for_mode<true>(type) : kernel_for_mode<false>(type); }
+const void* kernel_for_class(int lc, bool gait) {
+  if (lc == LC_MISC) return gait ? reinterpret_cast<const void*>(&towr_misc_kernel<true>) : reinterpret_cast<const void*>(&towr_misc_kernel<false>);
+  return kernel_for(lc, gait);   // LC_DYN/ROM/FDISC == IT_DYN/ROM/FDISC
+}
 
 }  // namespace
 
@@ -229,6 +289,7 @@ struct towr_gpu_handle_s {
   PolyPhase* d_pinfo = nullptr;
   PhaseCol* d_pcols = nullptr;
   SchedInfo* d_sched = nullptr;
+  int32_t* d_misc = nullptr;
   // fork-join of the per-kind launches (TOWR_GPU_STREAMS = total streams incl. the caller's, 1..4)
   static constexpr int kMaxSide = 3;
   int n_side = 0;
@@ -275,32 +336,37 @@ int bind(towr_gpu_handle h) {
   return TOWR_OK;
 }
 
-size_t lds_bytes(const Layout& L, int t) {
-  size_t d = (size_t)L.type_lds[t];
-  d += (size_t)((L.n + 2) & ~1);                                          // x + zero slot
-  if (stages_nodes(t, L.gait)) d += (L.nodecol.size() + 3) / 4 * 2;        // node table (16-B units)
+// LDS of a launch class: [tile region(s) | x + zero slot | node table]
+size_t lds_region(const Layout& L, int lc) { return lc == LC_MISC ? (size_t)kMiscWaves * L.misc_stride : (size_t)L.type_lds[lc]; }
+size_t lds_bytes(const Layout& L, int lc) {
+  size_t d = lds_region(L, lc);
+  d += (size_t)((L.n + 2) & ~1);                                                          // x + zero slot
+  if (lc == LC_MISC || stages_nodes(lc, L.gait)) d += (L.nodecol.size() + 3) / 4 * 2;     // node table (16-B units)
   return sizeof(double) * d;
 }
+int class_units(const Layout& L, int lc) {   // tiles (or misc groups) per problem
+  return lc == LC_MISC ? (int)(L.misc_tiles.size() / kMiscWaves) : L.type_tile0[lc + 1] - L.type_tile0[lc];
+}
+int64_t class_bytes(const Layout& L, int lc) { return lc == LC_MISC ? L.misc_bytes : L.type_bytes[lc]; }
 
 int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, int64_t ldg, double* V, int64_t ldv,
-           int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem, int only_type = -1) {
+           int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem, int only_class = -1) {
   if (B <= 0) return TOWR_OK;
   const Layout& L = h->L;
-  // The per-kind launches are independent (disjoint rows and CSR ranges): fork them onto the
-  // handle's side streams so that kinds with different register / LDS footprints share the CUs,
-  // and join back into the caller's stream. Heaviest kinds first.
-  int order[IT_COUNT], nk = 0;
-  for (int t = 0; t < IT_COUNT; ++t)
-    if (L.type_tile0[t + 1] > L.type_tile0[t] && (only_type < 0 || t == only_type)) order[nk++] = t;
-  std::sort(order, order + nk, [&](int a, int b) { return L.type_bytes[a] > L.type_bytes[b]; });
-  const int nside = (only_type < 0 && nk > 1) ? std::min(h->n_side, nk - 1) : 0;
+  // The launch classes are independent (disjoint rows and CSR ranges): optionally fork them onto the
+  // handle's side streams (TOWR_GPU_STREAMS) and join back into the caller's stream. Heaviest first.
+  int order[LC_COUNT], nk = 0;
+  for (int lc = 0; lc < LC_COUNT; ++lc)
+    if (class_units(L, lc) > 0 && (only_class < 0 || lc == only_class)) order[nk++] = lc;
+  std::sort(order, order + nk, [&](int a, int b) { return class_bytes(L, a) > class_bytes(L, b); });
+  const int nside = (only_class < 0 && nk > 1) ? std::min(h->n_side, nk - 1) : 0;
   if (nside > 0) {
     HIPCHK(h, hipEventRecord(h->fork, s));
     for (int i = 0; i < nside; ++i) HIPCHK(h, hipStreamWaitEvent(h->side[i], h->fork, 0));
   }
   for (int q = 0; q < nk; ++q) {
-    const int t = order[q];
-    const int nt = L.type_tile0[t + 1] - L.type_tile0[t];
+    const int lc = order[q];
+    const int nt = class_units(L, lc);
     const hipStream_t st = (nside > 0 && q % (nside + 1) != 0) ? h->side[q % (nside + 1) - 1] : s;
     KParams P{};
     P.X = X; P.ldx = ldx; P.G = G; P.ldg = ldg; P.V = V; P.ldv = ldv;
@@ -309,18 +375,25 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
     P.segs = h->d_segs; P.n_spl = (int32_t)L.spl.size();
     P.pinfo = h->d_pinfo; P.pcols = h->d_pcols; P.sched = h->d_sched;
     P.terrains = terrains; P.terrain_per_problem = per_problem;
-    P.B = B; P.tile0 = L.type_tile0[t]; P.ntiles = nt;
-    P.lds_rows_off = L.type_lds_rows_off[t];
+    P.B = B; P.ntiles = nt;
+    if (lc == LC_MISC) {
+      P.tile0 = 0;
+      P.misc_tiles = h->d_misc; P.misc_stride = L.misc_stride; P.misc_rows_off = L.misc_rows_off;
+    } else {
+      P.tile0 = L.type_tile0[lc];
+      P.lds_rows_off = L.type_lds_rows_off[lc];
+    }
     P.n = L.n; P.n_pad = (L.n + 2) & ~1; P.n_nodecol = (int32_t)L.nodecol.size();
-    P.lds_x_off = L.type_lds[t];
+    P.lds_x_off = (int32_t)lds_region(L, lc);
     P.want_g = want_g; P.want_jac = want_jac; P.fdisc_motion = L.fdisc_motion;
     P.rb = L.rb;
     const int64_t total = (int64_t)B * nt;
     const int64_t grid = ((total + 7) / 8) * 8;
     if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
+    const int block = lc == LC_MISC ? 64 * kMiscWaves : L.type_block[lc];
     void* args[] = {&P};
-    HIPCHK(h, hipLaunchKernel(kernel_for(t, L.gait), dim3((unsigned)grid), dim3((unsigned)L.type_block[t]), args,
-                              lds_bytes(L, t), st));
+    HIPCHK(h, hipLaunchKernel(kernel_for_class(lc, L.gait), dim3((unsigned)grid), dim3((unsigned)block), args,
+                              lds_bytes(L, lc), st));
   }
   for (int i = 0; i < nside; ++i) {
     HIPCHK(h, hipEventRecord(h->join[i], h->side[i]));
@@ -372,7 +445,7 @@ int host_eval(towr_gpu_handle h, int B, const double* X, double* G, double* V) {
 extern "C" {
 
 int towr_gpu_abi_version(void) { return TOWR_GPU_ABI_VERSION; }
-int towr_gpu_num_kernels(void) { return IT_COUNT; }
+int towr_gpu_num_kernels(void) { return LC_COUNT; }
 
 const char* towr_gpu_last_error(towr_gpu_handle h) {
   if (h) return h->err.c_str();
@@ -416,7 +489,8 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
   if ((r = upload(h, &h->d_items, L.items)) || (r = upload(h, &h->d_slots, L.slot_groups)) ||
       (r = upload(h, &h->d_tiles, L.tiles)) || (r = upload(h, &h->d_nodecol, nodecol16)) ||
       (r = upload(h, &h->d_spl, L.spl)) || (r = upload(h, &h->d_dur, L.dur)) || (r = upload(h, &h->d_segs, L.segs)) || (r = upload(h, &h->d_terrain, ter)) ||
-      (r = upload(h, &h->d_pinfo, L.pinfo)) || (r = upload(h, &h->d_pcols, L.pcols)) || (r = upload(h, &h->d_sched, L.sched)))
+      (r = upload(h, &h->d_pinfo, L.pinfo)) || (r = upload(h, &h->d_pcols, L.pcols)) || (r = upload(h, &h->d_sched, L.sched)) ||
+      (r = upload(h, &h->d_misc, L.misc_tiles)))
     return bail(r);
   {
     const char* ns = std::getenv("TOWR_GPU_STREAMS");
@@ -431,10 +505,11 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
         h->err = "side stream creation failed"; return bail(TOWR_ERR_HIP);
       }
   }
-  for (int t = 0; t < IT_COUNT; ++t) {
-    const size_t lds = lds_bytes(L, t);
+  for (int lc = 0; lc < LC_COUNT; ++lc) {
+    if (class_units(L, lc) == 0) continue;
+    const size_t lds = lds_bytes(L, lc);
     if (lds > 160 * 1024) { h->err = "tile too large for LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
-    if (lds > 64 * 1024 && hipFuncSetAttribute(kernel_for(t, L.gait), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+    if (lds > 64 * 1024 && hipFuncSetAttribute(kernel_for_class(lc, L.gait), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
       h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
     }
   }
@@ -445,7 +520,7 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
 int towr_gpu_destroy(towr_gpu_handle h) {
   if (!h) return TOWR_OK;
   void* dev[] = {h->d_items, h->d_slots, h->d_tiles, h->d_nodecol, h->d_spl, h->d_dur, h->d_segs, h->d_terrain,
-                 h->d_pinfo, h->d_pcols, h->d_sched,
+                 h->d_pinfo, h->d_pcols, h->d_sched, h->d_misc,
                  h->d_bterrain, h->d_x, h->d_g, h->d_v};
   if (h->device >= 0) for (void* p : dev) if (p) (void)hipFree(p);
   void* host[] = {h->h_x, h->h_g, h->h_v};
@@ -558,18 +633,16 @@ int towr_gpu_eval_batch_device(towr_gpu_handle h, int32_t B, const double* X, in
 }
 
 int towr_gpu_kernel_info(towr_gpu_handle h, int32_t kernel, const char** name, int32_t* n_tiles, int64_t* bytes_per_problem) {
-  static const char* names[IT_COUNT] = {"dynamic", "range_of_motion", "force_discretized", "force_node", "terrain",
-                                        "base_motion", "spline_acc", "base_height", "swing", "total_duration"};
-  if (!h || kernel < 0 || kernel >= IT_COUNT) return fail(h, TOWR_ERR_INVALID, "bad kernel index");
+  static const char* names[LC_COUNT] = {"dynamic", "range_of_motion", "force_discretized", "small_kinds"};
+  if (!h || kernel < 0 || kernel >= LC_COUNT) return fail(h, TOWR_ERR_INVALID, "bad kernel index");
   if (name) *name = names[kernel];
-  if (n_tiles) *n_tiles = h->L.type_tile0[kernel + 1] - h->L.type_tile0[kernel];
-  if (bytes_per_problem) *bytes_per_problem = h->L.type_bytes[kernel];
+  if (n_tiles) *n_tiles = class_units(h->L, kernel);
+  if (bytes_per_problem) *bytes_per_problem = class_bytes(h->L, kernel);
   return TOWR_OK;
 }
-
 int towr_gpu_eval_batch_device_kernel(towr_gpu_handle h, int32_t kernel, int32_t B, const double* X, int64_t ldx,
                                       double* G, int64_t ldg, double* V, int64_t ldv, void* stream) {
-  if (!h || B < 0 || !X || !G || !V || kernel < 0 || kernel >= IT_COUNT) return fail(h, TOWR_ERR_INVALID, "bad argument");
+  if (!h || B < 0 || !X || !G || !V || kernel < 0 || kernel >= LC_COUNT) return fail(h, TOWR_ERR_INVALID, "bad argument");
   const Layout& L = h->L;
   if (ldx < L.n || ldg < L.m || ldv < L.nnz) return fail(h, TOWR_ERR_INVALID, "leading dimension too small");
   if (int rc = bind(h)) return rc;
