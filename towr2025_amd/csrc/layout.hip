@@ -714,7 +714,7 @@ TypeSpec type_spec(int type, int n_ee) {
   switch (type) {
     case IT_DYN: return {256, std::max(1, std::min(64, 128 / std::max(1, n_ee)))};  // waves: g0 | g1 | ee, ee
     case IT_ROM: return {192, 64};                                                      // waves: g0 | g1 | g2
-    case IT_FDISC: return {256, 256};
+    case IT_FDISC: return {192, 192};
     default: return {64, 64};
   }
 }

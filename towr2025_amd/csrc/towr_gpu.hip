@@ -258,7 +258,7 @@ const void* kernel_for_mode(int type) {
   switch (type) {
     case IT_DYN: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_DYN, 256, GAIT>);
     case IT_ROM: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_ROM, 192, GAIT>);
-    case IT_FDISC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_FDISC, 256, GAIT>);
+    case IT_FDISC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_FDISC, 192, GAIT>);
   }
   return nullptr;
 }
