@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TOWR_GPU_ABI_VERSION 1
+#define TOWR_GPU_ABI_VERSION 2
 
 #define TOWR_MAX_EE          4
 #define TOWR_MAX_PHASES      48
@@ -103,7 +103,14 @@ enum towr_constraint_kind {
   TOWR_C_SPLINE_ACC       = 6, /* SplineAccConstraint          ee=0 base-lin, ee=1 base-ang (spline_acc_constraint.cc:34-86)     */
   TOWR_C_BASE_HEIGHT      = 7, /* BaseHeightConstraint         p[0]=safety distance   (base_height_constraint.cc:35-110)         */
   TOWR_C_SWING            = 8, /* SwingConstraint              ee; p[0]=t_swing_avg (0.3, swing_constraint.h:68)                  */
-  TOWR_C_TOTAL_DURATION   = 9  /* TotalDurationConstraint      ee; T                  (total_duration_constraint.cc:36-72)       */
+  TOWR_C_TOTAL_DURATION   = 9, /* TotalDurationConstraint      ee; T                  (total_duration_constraint.cc:36-72)       */
+  TOWR_C_TORQUE_DISCRETIZED = 10, /* TorqueConstraintDiscretized ee; T; dt; p[0..3] = tx_min, tx_max, ty_min, ty_max;
+                                     p[4] = k_friction                     (torque_constraint_discretized.cc:69-235) */
+  TOWR_C_TORQUE           = 11, /* TorqueConstraint (node-based) ee; p[0..4] as above      (torque_constraint.cc:36-194)  */
+  TOWR_C_TERRAIN_HARD     = 12, /* TerrainConstraintHard       ee; T; dt              (terrain_constraint_hard.cc:35-132)       */
+  TOWR_C_EE_LINEAR        = 13  /* EELinearConstraint          T; dt; ip[0] = target (0 motion, 1 ang), ip[1] = deriv (0 pos,
+                                     1 vel), ip[2] = n_terms (<= 6), ip[3 + i] = ee_i * 3 + dim_i; p[i] = coeff_i;
+                                     (ee_linear_constraint.cc:5-48; the bound tolerance is setup data, not used here)  */
 };
 
 typedef struct {
@@ -112,6 +119,8 @@ typedef struct {
   double  T;      /* total horizon the constraint was constructed with                         */
   double  dt;     /* discretisation step of TimeDiscretizationConstraint subclasses            */
   double  p[6];   /* per-kind parameters (see enum)                                            */
+  int32_t ip[9];  /* per-kind integer parameters (EELinear)                                    */
+  int32_t reserved;
 } towr_constraint_t;
 
 /* ---- initial guess (NlpFormulation::MakeBaseVariables etc., nlp_formulation.cc:121-346) ---- */

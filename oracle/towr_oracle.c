@@ -488,6 +488,7 @@ static spmat spline_jac_pos_wrt_durations(const Spline* s, double t) {
  * HeightMap (src/terrain/height_map.cc, height_map_examples.cc, height_map_examples.h)
  * ===========================================================================================*/
 typedef towr_terrain_t Terrain;
+static double dot3(const double a[3], const double b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 
 static double ter_h(const Terrain* T, double x, double y) {
   const double* p = T->p;
@@ -981,6 +982,7 @@ typedef struct {
 typedef struct {
   int kind, ee, rows, row0;
   double T, dt, p[6];
+  int ip[9];                       /* EELinearConstraint: target, deriv, n_terms, ee*3+dim    */
   int n_dts; double* dts;          /* TimeDiscretizationConstraint::dts_                    */
   int n_ids; int* ids;             /* node ids (force/terrain/swing/base-height)           */
   /* SplineAccConstraint (spline_acc_constraint.cc:34-46) */
@@ -1120,6 +1122,54 @@ static void cons_values(oracle_t* o, const Cons* c, double* g) {
       }
       break;
     }
+    case TOWR_C_TORQUE_DISCRETIZED: { /* torque_constraint_discretized.cc:101-122 */
+      double mu = T->friction_coeff, kf = c->p[4];
+      for (int k = 0; k < c->n_dts; ++k) {
+        double t = c->dts[k], p[3][3], f[3][3], tq[3][3], n[3], t1[3], t2[3];
+        spline_point(o->s_motion[c->ee], t, p); spline_point(o->s_force[c->ee], t, f); spline_point(o->s_torque[c->ee], t, tq);
+        ter_nbasis(T, NORMAL, p[kPos][X], p[kPos][Y], n);
+        ter_nbasis(T, TANGENT1, p[kPos][X], p[kPos][Y], t1);
+        ter_nbasis(T, TANGENT2, p[kPos][X], p[kPos][Y], t2);
+        double tau_t1 = dot3(tq[kPos], t1), tau_t2 = dot3(tq[kPos], t2), tau_n = dot3(tq[kPos], n), f_n = dot3(f[kPos], n);
+        double tz_lim = kf * mu * f_n;
+        g[4 * k + 0] = tau_t1; g[4 * k + 1] = tau_t2; g[4 * k + 2] = tau_n - tz_lim; g[4 * k + 3] = -tau_n - tz_lim;
+      }
+      break;
+    }
+    case TOWR_C_TORQUE: {         /* torque_constraint.cc:68-103 */
+      const NodesVar* tv = o->torque[c->ee]; const NodesVar* mv = o->motion[c->ee];
+      for (int i = 0; i < c->n_ids; ++i) {
+        int tid = c->ids[i], phase = nv_get_phase(tv, tid);
+        const double* p = mv->nodes[nv_node_at_start_of_phase(mv, phase)][kPos];
+        const double* tau = tv->nodes[tid][kPos];
+        double n[3], t1[3], t2[3];
+        ter_nbasis(T, NORMAL, p[X], p[Y], n); ter_nbasis(T, TANGENT1, p[X], p[Y], t1); ter_nbasis(T, TANGENT2, p[X], p[Y], t2);
+        g[3 * i + 0] = dot3(tau, t1); g[3 * i + 1] = dot3(tau, t2); g[3 * i + 2] = dot3(tau, n);
+      }
+      break;
+    }
+    case TOWR_C_TERRAIN_HARD:     /* terrain_constraint_hard.cc:50-72 */
+      for (int k = 0; k < c->n_dts; ++k) {
+        double st[3][3], n[3], t1[3], t2[3];
+        spline_point(o->s_motion[c->ee], c->dts[k], st);
+        const double* p = st[kPos]; const double* v = st[kVel];
+        ter_nbasis(T, NORMAL, p[X], p[Y], n); ter_nbasis(T, TANGENT1, p[X], p[Y], t1); ter_nbasis(T, TANGENT2, p[X], p[Y], t2);
+        double vt1 = dot3(v, t1), vt2 = dot3(v, t2), vtm = sqrt(vt1 * vt1 + vt2 * vt2);
+        double dz = p[Z] - ter_h(T, p[X], p[Y]), kc = 0.02, a = kc * vtm;
+        g[k] = dz - (a < kc ? a : kc);   /* std::min(k*|v_t|, k_coeff_) */
+      }
+      break;
+    case TOWR_C_EE_LINEAR:        /* ee_linear_constraint.cc:19-28 */
+      for (int k = 0; k < c->n_dts; ++k) {
+        double val = 0.0;
+        for (int q = 0; q < c->ip[2]; ++q) {
+          int ee = c->ip[3 + q] / 3, dim = c->ip[3 + q] % 3; double st[3][3];
+          spline_point(c->ip[0] == 0 ? o->s_motion[ee] : o->s_ang_ee[ee], c->dts[k], st);
+          val += c->p[q] * (c->ip[1] == 0 ? st[kPos][dim] : st[kVel][dim]);
+        }
+        g[k] = val;
+      }
+      break;
     case TOWR_C_TOTAL_DURATION: { /* total_duration_constraint.cc:49-55 */
       const PhaseDur* p = o->pd[c->ee]; double s = 0.0;
       for (int i = 0; i < p->n - 1; ++i) s += p->d[i];
@@ -1206,7 +1256,6 @@ static void acc_scaled_row(const spmat* J, int src, double s, int dst, spmat* ou
       if (r == src) *sp_coeffref(out, dst, J->r[r].e[q].col) += s * J->r[r].e[q].val;
 }
 
-static double dot3(const double a[3], const double b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 /* F . (a + s*b) */
 static double fdot(const double F[3], const double a[3], double s, const double b[3]) {
   double t[3] = {a[0] + s * b[0], a[1] + s * b[1], a[2] + s * b[2]};
@@ -1303,6 +1352,94 @@ static void force_node_jac(oracle_t* o, const Cons* c, const VarSet* v, spmat* j
   }
 }
 
+/* TorqueConstraintDiscretized::UpdateJacobianAtInstance, torque_constraint_discretized.cc:135-235 */
+static void tqdisc_jac_instance(oracle_t* o, const Cons* c, double t, int k, const VarSet* v, spmat* jac) {
+  const Terrain* T = &o->terrain; double mu = T->friction_coeff, kf = c->p[4];
+  double p[3][3], f[3][3], tq[3][3], n[3], t1[3], t2[3], mn[3], b[3];
+  spline_point(o->s_motion[c->ee], t, p); spline_point(o->s_force[c->ee], t, f); spline_point(o->s_torque[c->ee], t, tq);
+  ter_nbasis(T, NORMAL, p[kPos][X], p[kPos][Y], n);
+  ter_nbasis(T, TANGENT1, p[kPos][X], p[kPos][Y], t1);
+  ter_nbasis(T, TANGENT2, p[kPos][X], p[kPos][Y], t2);
+  for (int q = 0; q < 3; ++q) { mn[q] = -n[q]; b[q] = -kf * mu * n[q]; }
+  int r0 = 4 * k, r1 = r0 + 1, r2 = r0 + 2, r3 = r0 + 3;
+  int is_t = vs_is(v, TOWR_VAR_EE_TORQUE, c->ee), is_f = vs_is(v, TOWR_VAR_EE_FORCE, c->ee);
+  int is_m = vs_is(v, TOWR_VAR_EE_MOTION, c->ee), is_s = vs_is(v, TOWR_VAR_EE_SCHEDULE, c->ee);
+  if (is_t || is_s) {
+    spmat J = is_t ? spline_jac(o->s_torque[c->ee], t, kPos) : spline_jac_pos_wrt_durations(o->s_torque[c->ee], t);
+    acc_linear_form(&J, t1, r0, jac); acc_linear_form(&J, t2, r1, jac);
+    acc_linear_form(&J, n, r2, jac); acc_linear_form(&J, mn, r3, jac);
+    sp_free(&J);
+  }
+  if (is_f || is_s) {
+    spmat J = is_f ? spline_jac(o->s_force[c->ee], t, kPos) : spline_jac_pos_wrt_durations(o->s_force[c->ee], t);
+    acc_linear_form(&J, b, r2, jac); acc_linear_form(&J, b, r3, jac);
+    sp_free(&J);
+  }
+  if (is_m || is_s) {
+    spmat Jp = is_m ? spline_jac(o->s_motion[c->ee], t, kPos) : spline_jac_pos_wrt_durations(o->s_motion[c->ee], t);
+    for (int dim = X; dim <= Y; ++dim) {
+      double dn[3], dt1[3], dt2[3];
+      ter_d_nbasis(T, NORMAL, dim, p[kPos][X], p[kPos][Y], dn);
+      ter_d_nbasis(T, TANGENT1, dim, p[kPos][X], p[kPos][Y], dt1);
+      ter_d_nbasis(T, TANGENT2, dim, p[kPos][X], p[kPos][Y], dt2);
+      double s_tx = dot3(tq[kPos], dt1), s_ty = dot3(tq[kPos], dt2), s_tau_n = dot3(tq[kPos], dn);
+      double s_lim = kf * mu * dot3(f[kPos], dn);
+      acc_scaled_row(&Jp, dim, s_tx, r0, jac);
+      acc_scaled_row(&Jp, dim, s_ty, r1, jac);
+      acc_scaled_row(&Jp, dim, s_tau_n - s_lim, r2, jac);
+      acc_scaled_row(&Jp, dim, -s_tau_n - s_lim, r3, jac);
+    }
+    sp_free(&Jp);
+  }
+}
+
+/* TerrainConstraintHard::UpdateJacobianAtInstance, terrain_constraint_hard.cc:84-132 */
+static void thard_jac_instance(oracle_t* o, const Cons* c, double t, int k, const VarSet* v, spmat* jac) {
+  if (!vs_is(v, TOWR_VAR_EE_MOTION, c->ee)) return;
+  const Terrain* T = &o->terrain;
+  double st[3][3], n[3], t1[3], t2[3];
+  spline_point(o->s_motion[c->ee], t, st);
+  const double* p = st[kPos]; const double* vel = st[kVel];
+  ter_nbasis(T, NORMAL, p[X], p[Y], n); ter_nbasis(T, TANGENT1, p[X], p[Y], t1); ter_nbasis(T, TANGENT2, p[X], p[Y], t2);
+  double vt1 = dot3(vel, t1), vt2 = dot3(vel, t2), vtm = sqrt(vt1 * vt1 + vt2 * vt2), kc = 0.02;
+  spmat jp = spline_jac(o->s_motion[c->ee], t, kPos), jv = spline_jac(o->s_motion[c->ee], t, kVel);
+  spmat row = sp_row_of(&jp, Z);
+  for (int dim = X; dim <= Y; ++dim) {
+    spmat r = sp_row_of(&jp, dim);
+    sp_add_inplace(&row, &r, -ter_dh(T, dim, p[X], p[Y]));   /* -= terrain_deriv * jac_pos.row(dim) */
+    sp_free(&r);
+  }
+  if (vtm > 1e-6 && kc * vtm < 0.05 - 1e-6) {
+    double td[3];
+    for (int q = 0; q < 3; ++q) td[q] = (vt1 * t1[q] + vt2 * t2[q]) / vtm;
+    for (int dim = X; dim <= Z; ++dim) {
+      spmat r = sp_row_of(&jv, dim);
+      sp_add_inplace(&row, &r, -(kc * td[dim]));
+      sp_free(&r);
+    }
+  }
+  sp_set_rows(jac, k, &row);
+  sp_free(&row); sp_free(&jp); sp_free(&jv);
+}
+
+/* EELinearConstraint::UpdateJacobianAtInstance, ee_linear_constraint.cc:37-48 */
+static void eelin_jac_instance(oracle_t* o, const Cons* c, double t, int k, const VarSet* v, spmat* jac) {
+  const int kind = c->ip[0] == 0 ? TOWR_VAR_EE_MOTION : TOWR_VAR_EE_ANG;
+  spmat row = sp_zero(1, jac->cols);
+  int any = 0;
+  for (int q = 0; q < c->ip[2]; ++q) {
+    int ee = c->ip[3 + q] / 3, dim = c->ip[3 + q] % 3;
+    if (!vs_is(v, kind, ee)) continue;
+    spmat J = spline_jac(kind == TOWR_VAR_EE_MOTION ? o->s_motion[ee] : o->s_ang_ee[ee], t, c->ip[1] == 0 ? kPos : kVel);
+    spmat r = sp_row_of(&J, dim);
+    sp_add_inplace(&row, &r, c->p[q]);
+    sp_free(&J); sp_free(&r);
+    any = 1;
+  }
+  if (any) sp_set_rows(jac, k, &row);
+  sp_free(&row);
+}
+
 static void cons_fill_jac(oracle_t* o, const Cons* c, const VarSet* v, spmat* jac) {
   const Terrain* T = &o->terrain;
   switch (c->kind) {
@@ -1374,6 +1511,49 @@ static void cons_fill_jac(oracle_t* o, const Cons* c, const VarSet* v, spmat* ja
         }
       }
       break;
+    case TOWR_C_TORQUE_DISCRETIZED:
+      for (int k = 0; k < c->n_dts; ++k) tqdisc_jac_instance(o, c, c->dts[k], k, v, jac);
+      break;
+    case TOWR_C_TERRAIN_HARD:
+      for (int k = 0; k < c->n_dts; ++k) thard_jac_instance(o, c, c->dts[k], k, v, jac);
+      break;
+    case TOWR_C_EE_LINEAR:
+      for (int k = 0; k < c->n_dts; ++k) eelin_jac_instance(o, c, c->dts[k], k, v, jac);
+      break;
+    case TOWR_C_TORQUE: {          /* torque_constraint.cc:129-193 */
+      const NodesVar* tv = o->torque[c->ee]; const NodesVar* mv = o->motion[c->ee];
+      if (vs_is(v, TOWR_VAR_EE_TORQUE, c->ee))
+        for (int i = 0; i < c->n_ids; ++i) {
+          int tid = c->ids[i], phase = nv_get_phase(tv, tid);
+          const double* p = mv->nodes[nv_node_at_start_of_phase(mv, phase)][kPos];
+          double n[3], t1[3], t2[3];
+          ter_nbasis(T, NORMAL, p[X], p[Y], n); ter_nbasis(T, TANGENT1, p[X], p[Y], t1); ter_nbasis(T, TANGENT2, p[X], p[Y], t2);
+          for (int dim = X; dim <= Z; ++dim) {
+            int idx = nv_opt_index(tv, tid, kPos, dim);
+            *sp_coeffref(jac, 3 * i + 0, idx) = t1[dim];
+            *sp_coeffref(jac, 3 * i + 1, idx) = t2[dim];
+            *sp_coeffref(jac, 3 * i + 2, idx) = n[dim];
+          }
+        }
+      if (vs_is(v, TOWR_VAR_EE_MOTION, c->ee))
+        for (int i = 0; i < c->n_ids; ++i) {
+          int tid = c->ids[i], phase = nv_get_phase(tv, tid);
+          int ee_node = nv_node_at_start_of_phase(mv, phase);
+          const double* p = mv->nodes[ee_node][kPos];
+          const double* tau = tv->nodes[nv_node_at_start_of_phase(tv, phase)][kPos];   /* GetValueAtStartOfPhase (:166) */
+          for (int dim = X; dim <= Y; ++dim) {
+            double dn[3], dt1[3], dt2[3];
+            ter_d_nbasis(T, TANGENT1, dim, p[X], p[Y], dt1);
+            ter_d_nbasis(T, TANGENT2, dim, p[X], p[Y], dt2);
+            ter_d_nbasis(T, NORMAL, dim, p[X], p[Y], dn);
+            int idx = nv_opt_index(mv, ee_node, kPos, dim);
+            *sp_coeffref(jac, 3 * i + 0, idx) = dot3(tau, dt1);
+            *sp_coeffref(jac, 3 * i + 1, idx) = dot3(tau, dt2);
+            *sp_coeffref(jac, 3 * i + 2, idx) = dot3(tau, dn);
+          }
+        }
+      break;
+    }
     case TOWR_C_TOTAL_DURATION:    /* total_duration_constraint.cc:66-72 */
       if (vs_is(v, TOWR_VAR_EE_SCHEDULE, c->ee))
         for (int col = 0; col < o->pd[c->ee]->n - 1; ++col) *sp_coeffref(jac, 0, col) = 1.0;
@@ -1557,7 +1737,22 @@ oracle_t* oracle_create(const towr_problem_desc_t* d, char* err, int errlen) {
     const towr_constraint_t* s = &d->constraints[i];
     c->kind = s->kind; c->ee = s->ee; c->T = s->T; c->dt = s->dt;
     memcpy(c->p, s->p, sizeof(c->p));
+    memcpy(c->ip, s->ip, sizeof(c->ip));
     switch (c->kind) {
+      case TOWR_C_TORQUE_DISCRETIZED: make_dts(c); c->rows = 4 * c->n_dts; break;      /* torque_constraint_discretized.cc:92-93 */
+      case TOWR_C_TERRAIN_HARD: make_dts(c); c->rows = c->n_dts; break;                /* terrain_constraint_hard.cc:47 */
+      case TOWR_C_EE_LINEAR:      /* ee_linear_constraint.cc:15-16 */
+        if (c->ip[2] < 1 || c->ip[2] > 6 || c->ip[0] < 0 || c->ip[0] > 1 || c->ip[1] < 0 || c->ip[1] > 1) { set_err(err, errlen, "bad EELinear definition"); oracle_destroy(o); return NULL; }
+        for (int q = 0; q < c->ip[2]; ++q)
+          if (c->ip[3 + q] < 0 || c->ip[3 + q] >= 3 * E) { set_err(err, errlen, "bad EELinear term"); oracle_destroy(o); return NULL; }
+        make_dts(c); c->rows = c->n_dts; break;
+      case TOWR_C_TORQUE: {       /* TorqueConstraint::InitVariableDependedQuantities, torque_constraint.cc:56-66 */
+        NodesVar* tv = o->torque[c->ee];
+        c->ids = (int*)malloc(sizeof(int) * (size_t)tv->n_nodes);
+        for (int id = 0; id < tv->n_nodes; ++id) if (!nv_is_constant_node(tv, id)) c->ids[c->n_ids++] = id;
+        c->rows = 3 * c->n_ids;
+        break;
+      }
       case TOWR_C_DYNAMIC: make_dts(c); c->rows = 6 * c->n_dts; break;                 /* :54 */
       case TOWR_C_RANGE_OF_MOTION: make_dts(c); c->rows = 3 * c->n_dts; break;         /* :55 */
       case TOWR_C_FORCE_DISCRETIZED: make_dts(c); c->rows = 5 * c->n_dts; break;       /* :88 */

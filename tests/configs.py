@@ -21,7 +21,37 @@ def config_descs():
                                                optimize_timings=True).to_desc(),
         "biped_walk_gaitopt": _gaitopt(F.biped_walk()),
         "hyq_gap_gaitopt": _gaitopt_hyq_gap(),
+        # Torque (discretized and node-based), TerrainHard, EELinear
+        "biped_torque_hard_eelin": _with_next_tier(F.biped_walk()),
+        "hopper_torque_node": _with_next_tier(F.monoped_hopper(), node_torque=True, eelin=False),
+        "anymal_gait_torque": _with_next_tier(F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.StairsID),
+                                                            optimize_timings=True), hard=False),
+        "hyq_gap_torque": _with_next_tier(_hyq_formulation(F.HeightMap.GapID)),
     }
+
+
+def _hyq_formulation(tid):
+    f = F.anymal_trot(terrain=F.HeightMap.MakeTerrain(tid))
+    f.model_ = F.RobotModel(F.RobotModel.Hyq)
+    nominal = f.model_.kinematic_model.nominal_stance
+    f.initial_ee_W_ = [(p[0], p[1], 0.0) for p in nominal]
+    f.initial_base_ = F.BaseState(lin_p=(0.0, 0.0, -nominal[0][2]))
+    return f
+
+
+def _with_next_tier(f, node_torque=False, hard=True, eelin=True):
+    P = f.params_
+    P.constraints_.append(F.Parameters.Torque)
+    if node_torque:
+        P.dt_constraint_torque_ = 0.0
+    if hard:
+        P.constraints_.append(F.Parameters.TerrainHard)
+    E = P.GetEECount()
+    if eelin and E >= 2:   # symmetric lateral foot positions; yaw-rate of the first foot's angle
+        P.ee_linear_constraints_.append(F.EELinearConstraintDef(terms=[(0, 1, 1.0), (1, 1, 1.0)], tolerance=0.5))
+        P.ee_linear_constraints_.append(F.EELinearConstraintDef(terms=[(0, 2, 0.5), (E - 1, 0, -1.0), (0, 2, 0.5)],
+                                                                target=1, deriv=1, tolerance=1.0, dt=0.05))
+    return f.to_desc()
 
 
 def _gaitopt(f):

@@ -36,6 +36,7 @@ extern "C" int emu_eval(const towr_problem_desc_t* d, const double* x, double* g
   c.x = x; c.nodecol = L.nodecol.data(); c.spl = L.spl.data(); c.dur = L.dur.data();
   c.ter = &L.terrain; c.rb = L.rb; c.fdisc_motion = L.fdisc_motion;
   c.gait = L.gait; c.pinfo = L.pinfo.data(); c.pcols = L.pcols.data(); c.sched = L.sched.data();
+  c.eelin = L.eelin.data();
   for (const TileDesc& td : L.tiles)
     for (int l = td.i0; l < td.i1; ++l) {
       const ItemDesc& it = L.items[l];

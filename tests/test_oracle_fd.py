@@ -16,7 +16,7 @@ from towr2025_amd import formulation as F
 CONFIGS = config_descs()
 
 
-def _fd_check(desc, x, h_rel=1e-6, tol=2e-5, skip_cols=None):
+def _fd_check(desc, x, h_rel=1e-6, tol=2e-5, skip_cols=None, skip_rows=None):
     o = Oracle(desc)
     r, c, v = o.eval_jac(x)
     J = sp.csr_matrix((v, (r, c)), shape=(o.m, o.n)).toarray()
@@ -29,6 +29,8 @@ def _fd_check(desc, x, h_rel=1e-6, tol=2e-5, skip_cols=None):
         xp[j] += h
         xm[j] -= h
         fd = (o.eval_g(xp) - o.eval_g(xm)) / (2 * h)
+        if skip_rows is not None:
+            fd[skip_rows] = J[skip_rows, j]
         err = np.abs(fd - J[:, j]) / np.maximum(1.0, np.abs(J[:, j]))
         assert err.max() < tol, f"col {j}: FD mismatch {err.max():.3g} at row {err.argmax()}"
         # nothing outside the pattern moves (no missing entries)
@@ -74,3 +76,90 @@ def test_gait_opt_quirk_is_present():
     dyn_row0, dyn_rows = o.constraint_rows()[[d.kind for d in desc.constraints[:desc.n_constraints]].index(capi.C_DYNAMIC)]
     err = np.abs(fd - J[:, j])[dyn_row0:dyn_row0 + dyn_rows]
     assert err.max() > 1e-3
+
+
+def _rows_of(desc, o, kind):
+    out = []
+    for i, (r0, n) in enumerate(o.constraint_rows()):
+        if desc.constraints[i].kind == kind:
+            out += list(range(r0, r0 + n))
+    return np.array(out, dtype=int)
+
+
+def test_fd_torque_ee_linear():
+    """TorqueConstraintDiscretized and EELinearConstraint (positions, angular velocities). The
+    TerrainConstraintHard rows are checked on slow feet below (fast swing feet sit in its quirk)."""
+    desc = CONFIGS["biped_torque_hard_eelin"]
+    o = Oracle(desc)
+    x = o.initial_x() + 0.01 * np.random.default_rng(12).standard_normal(o.n)
+    _fd_check(desc, x, skip_rows=_rows_of(desc, o, capi.C_TERRAIN_HARD))
+
+
+def test_fd_terrain_hard_slow_feet():
+    """TerrainConstraintHard with swing feet below 1 m/s (under the value cap of its quirk)."""
+    f = F.biped_walk(total_duration=8.0, goal=(0.6, 0.0, 0.0))
+    f.params_.constraints_.append(F.Parameters.TerrainHard)
+    f.terrain_ = F.HeightMap.MakeTerrain(F.HeightMap.ChimneyID)
+    desc = f.to_desc()
+    o = Oracle(desc)
+    x = o.initial_x() + 0.01 * np.random.default_rng(16).standard_normal(o.n)
+    _fd_check(desc, x)
+
+
+def test_fd_torque_node_with_quirk():
+    """TorqueConstraint's motion Jacobian uses the torque at the start of the phase
+    (torque_constraint.cc:166): FD-consistent once every torque node of a phase holds the same
+    torque, which a constant torque everywhere guarantees."""
+    desc = CONFIGS["hopper_torque_node"]
+    o = Oracle(desc)
+    x = o.initial_x() + 0.01 * np.random.default_rng(13).standard_normal(o.n)
+    for i, (c0, n) in enumerate(o.varset_cols()):
+        if desc.varsets[i].kind == capi.VAR_EE_TORQUE:
+            x[c0:c0 + n] = 0.7
+    _fd_check(desc, x)
+
+
+def test_fd_gait_optimisation_torque_discretized():
+    """d/d schedule of TorqueConstraintDiscretized (torque, force and motion PhaseSplines). The
+    dynamic rows are skipped: their torque term is the reference's quirk (A22 ii)."""
+    desc = CONFIGS["anymal_gait_torque"]
+    o = Oracle(desc)
+    x = o.initial_x() + 0.01 * np.random.default_rng(14).standard_normal(o.n)
+    skip = np.concatenate([_rows_of(desc, o, capi.C_DYNAMIC), _rows_of(desc, o, capi.C_EE_LINEAR)])
+    _fd_check(desc, x, tol=5e-5, skip_rows=skip)
+
+
+def test_ee_linear_has_no_schedule_derivative():
+    """EELinearConstraint only fills the blocks of its ee-motion / ee-angle sets
+    (ee_linear_constraint.cc:37-48): with phase-duration optimisation its rows move with the
+    schedule but carry no schedule entries — reproduced as in the reference."""
+    desc = CONFIGS["anymal_gait_torque"]
+    o = Oracle(desc)
+    r, c, _ = o.eval_jac(o.initial_x())
+    rows = set(_rows_of(desc, o, capi.C_EE_LINEAR).tolist())
+    sched0 = min(c0 for i, (c0, n) in enumerate(o.varset_cols()) if desc.varsets[i].kind == capi.VAR_EE_SCHEDULE)
+    assert not any(ri in rows and ci >= sched0 for ri, ci in zip(r, c))
+
+
+def test_terrain_hard_cap_quirk_is_present():
+    """TerrainConstraintHard caps the value at k_coeff = 0.02 (|v_t| >= 1 m/s) but keeps the velocity
+    Jacobian up to 0.05 (terrain_constraint_hard.cc:71,120; SURVEY A22 iii): with fast feet the
+    velocity columns disagree with finite differences, as in the reference."""
+    desc = CONFIGS["biped_torque_hard_eelin"]
+    o = Oracle(desc)
+    x = o.initial_x() + 0.01 * np.random.default_rng(15).standard_normal(o.n)   # swing feet at 1.3-2.7 m/s
+    r, c, v = o.eval_jac(x)
+    J = sp.csr_matrix((v, (r, c)), shape=(o.m, o.n)).toarray()
+    rows = _rows_of(desc, o, capi.C_TERRAIN_HARD)
+    worst = 0.0
+    for i, (c0, n) in enumerate(o.varset_cols()):
+        if desc.varsets[i].kind != capi.VAR_EE_MOTION:
+            continue
+        for j in range(c0, c0 + n):
+            h = 1e-6
+            xp, xm = x.copy(), x.copy()
+            xp[j] += h
+            xm[j] -= h
+            fd = (o.eval_g(xp) - o.eval_g(xm)) / (2 * h)
+            worst = max(worst, np.abs(fd - J[:, j])[rows].max())
+    assert worst > 1e-3

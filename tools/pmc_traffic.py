@@ -11,7 +11,7 @@ import json
 import sys
 from collections import defaultdict
 
-NAMES = ["dynamic", "range_of_motion", "force_discretized"]
+NAMES = {0: "dynamic", 1: "range_of_motion", 2: "force_discretized", 10: "torque_discretized"}
 
 
 def per_kernel(d, counter):

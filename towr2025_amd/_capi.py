@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_EE = 4
 MAX_PHASES = 48
 MAX_VARSETS = 2 + 5 * MAX_EE
@@ -30,7 +30,8 @@ VAR_BASE_LIN, VAR_BASE_ANG, VAR_EE_MOTION, VAR_EE_ANG, VAR_EE_FORCE, VAR_EE_TORQ
 
 # towr_constraint_kind
 C_DYNAMIC, C_RANGE_OF_MOTION, C_FORCE, C_FORCE_DISCRETIZED, C_TERRAIN, C_BASE_MOTION, \
-    C_SPLINE_ACC, C_BASE_HEIGHT, C_SWING, C_TOTAL_DURATION = range(10)
+    C_SPLINE_ACC, C_BASE_HEIGHT, C_SWING, C_TOTAL_DURATION, C_TORQUE_DISCRETIZED, C_TORQUE, C_TERRAIN_HARD, \
+    C_EE_LINEAR = range(14)
 
 INIT_FORMULATION, INIT_PROCEDURAL = 0, 1
 
@@ -54,7 +55,7 @@ class VarSetDesc(C.Structure):
 
 class ConstraintDesc(C.Structure):
     _fields_ = [("kind", C.c_int32), ("ee", C.c_int32), ("T", C.c_double), ("dt", C.c_double),
-                ("p", C.c_double * 6)]
+                ("p", C.c_double * 6), ("ip", C.c_int32 * 9), ("reserved", C.c_int32)]
 
 
 class InitDesc(C.Structure):

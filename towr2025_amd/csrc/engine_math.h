@@ -33,6 +33,7 @@ enum { SP_BASE_LIN = 0, SP_BASE_ANG = 1 };
 TG_HD int sp_motion(int ee) { return 2 + 4 * ee + 0; }
 TG_HD int sp_force(int ee)  { return 2 + 4 * ee + 2; }
 TG_HD int sp_torque(int ee) { return 2 + 4 * ee + 3; }
+TG_HD int sp_ang(int ee)    { return 2 + 4 * ee + 1; }
 
 // work item types
 enum ItemType {
@@ -47,7 +48,11 @@ enum ItemType {
   IT_BHGT = 7,   // BaseHeightConstraint node
   IT_SWING = 8,  // SwingConstraint node
   IT_TDUR = 9,   // TotalDurationConstraint (phase-duration optimisation)
-  IT_COUNT = 10
+  IT_TQDISC = 10,  // TorqueConstraintDiscretized instant
+  IT_TQNODE = 11,  // TorqueConstraint node (a0 torque node, a1 motion node / a2 torque node at phase start)
+  IT_THARD = 12,   // TerrainConstraintHard instant
+  IT_EELIN = 13,   // EELinearConstraint instant (a0 = definition index)
+  IT_COUNT = 14
 };
 
 struct SplineMeta {
@@ -78,6 +83,14 @@ struct PhaseCol {
 // are the variables at col0.., the last is t_total minus their sum
 struct SchedInfo { int32_t col0, n_phases; double t_total; };
 
+// EELinearConstraint definition (ee_linear_constraint.cc:5-48): sum of coeff * (pos|vel)[dim] of the
+// ee motion (target 0) or ee angle (target 1) splines; terms on one (ee, dim) are merged
+struct EELinDef {
+  int32_t target, deriv, n, reserved;
+  int32_t code[6];   // ee * 3 + dim
+  double coeff[6];
+};
+
 struct RobotC {
   double m, g;
   double Ib[9];      // BuildInertiaTensor (single_rigid_body_dynamics.cc:36-44), row-major
@@ -92,7 +105,7 @@ struct ItemDesc {
   int32_t slot;                 // candidate j of this item is slot_table[slot + j * stride]
   int32_t seg;                  // row of the segment table (time-discretised items), else -1
   int32_t ncand;                // number of candidates the item emits
-  int32_t reserved[2];
+  int32_t a2, reserved;         // third node id (TorqueConstraint: torque node at phase start)
   double t;                     // time of the instant (time-discretised sets)
   double p0;                    // scalar parameter (safety distance, t_swing_avg, ...)
 };
@@ -136,6 +149,7 @@ struct Ctx {
   const PolyPhase* pinfo;
   const PhaseCol* pcols;
   const SchedInfo* sched;       // per endeffector
+  const EELinDef* eelin;        // EELinearConstraint definitions
 };
 
 // ----------------------------------------------------------------------------------------------
@@ -957,6 +971,148 @@ TG_HD void eval_swing(const Ctx& c, const ItemDesc& it, Emit& em) {
   }
 }
 
+// TorqueConstraintDiscretized instant (torque_constraint_discretized.cc:101-235); it.p0 = k_friction
+template <class Emit>
+TG_HD void eval_tqdisc(const Ctx& c, const ItemDesc& it, Emit& em) {
+  const double t = it.t, mu = c.ter->friction_coeff, kf = it.p0;
+  const int r0 = it.row0, ee = it.ee;
+  SplinePt P, F, Tq;
+  spline_eval(c, sp_motion(ee), t, P);
+  spline_eval(c, sp_force(ee), t, F);
+  spline_eval(c, sp_torque(ee), t, Tq);
+  double n[3], t1[3], t2[3];
+  ter_nbasis(*c.ter, 0, P.p[0], P.p[1], n);
+  ter_nbasis(*c.ter, 1, P.p[0], P.p[1], t1);
+  ter_nbasis(*c.ter, 2, P.p[0], P.p[1], t2);
+  const double tau_n = dot3(Tq.p, n), tz_lim = kf * mu * dot3(F.p, n);
+  em.g(r0 + 0, dot3(Tq.p, t1));
+  em.g(r0 + 1, dot3(Tq.p, t2));
+  em.g(r0 + 2, tau_n - tz_lim);
+  em.g(r0 + 3, -tau_n - tz_lim);
+  const double mn[3] = {-n[0], -n[1], -n[2]}, b[3] = {-kf * mu * n[0], -kf * mu * n[1], -kf * mu * n[2]};
+  const double* tb[4] = {t1, t2, n, mn};
+  double H[4];
+  spline_basis(Tq, kPos, H);   // AccumulateLinearFormJacobian of the torque spline
+  for (int r = 0; r < 4; ++r)
+    for (int e = 0; e < 3; ++e) emit_dim(c, em, r0 + r, sp_torque(ee), Tq, H, e, tb[r][e]);
+  spline_basis(F, kPos, H);    // ... of the force spline into the two normal-torque rows
+  for (int r = 2; r < 4; ++r)
+    for (int e = 0; e < 3; ++e) emit_dim(c, em, r0 + r, sp_force(ee), F, H, e, b[e]);
+  double sc[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};   // d rows / d p_dim through the terrain basis
+  if (c.fdisc_motion) {   // AccumulateScaledRowJacobian: skipped when scale == 0.0 (:58)
+    spline_basis(P, kPos, H);
+    for (int dim = 0; dim < 2; ++dim) {
+      double dn[3], dt1[3], dt2[3];
+      ter_d_nbasis(*c.ter, 0, dim, P.p[0], P.p[1], dn);
+      ter_d_nbasis(*c.ter, 1, dim, P.p[0], P.p[1], dt1);
+      ter_d_nbasis(*c.ter, 2, dim, P.p[0], P.p[1], dt2);
+      const double s_tau_n = dot3(Tq.p, dn), s_lim = kf * mu * dot3(F.p, dn);
+      sc[dim][0] = dot3(Tq.p, dt1);
+      sc[dim][1] = dot3(Tq.p, dt2);
+      sc[dim][2] = s_tau_n - s_lim;
+      sc[dim][3] = -s_tau_n - s_lim;
+      for (int r = 0; r < 4; ++r) emit_dim(c, em, r0 + r, sp_motion(ee), P, H, dim, sc[dim][r], sc[dim][r] != 0.0);
+    }
+  }
+  if (c.gait) {   // schedule (:210-234): torque and force linear forms, motion scaled rows
+    SchedJac Jt, Jf, Jx;
+    sched_jac(c, sp_torque(ee), t, Tq, Jt);
+    sched_jac(c, sp_force(ee), t, F, Jf);
+    sched_jac(c, sp_motion(ee), t, P, Jx);
+    for (int r = 0; r < 4; ++r)
+      for (int col = 0; col < Jt.n - 1; ++col) {
+        double v = tb[r][0] * sched_val(Jt, 0, col) + tb[r][1] * sched_val(Jt, 1, col) + tb[r][2] * sched_val(Jt, 2, col);
+        if (r >= 2) v += b[0] * sched_val(Jf, 0, col) + b[1] * sched_val(Jf, 1, col) + b[2] * sched_val(Jf, 2, col);
+        if (sc[0][r] != 0.0) v += sc[0][r] * sched_val(Jx, 0, col);
+        if (sc[1][r] != 0.0) v += sc[1][r] * sched_val(Jx, 1, col);
+        em(r0 + r, Jt.col0 + col, v, true);
+      }
+  }
+}
+
+// TorqueConstraint node (torque_constraint.cc:68-193): a0 = torque node, a1 = motion node and
+// a2 = torque node at the start of its phase. The motion Jacobian uses the torque at the start of
+// the phase, not the node's own torque (torque_constraint.cc:166), as the reference does.
+template <class Emit>
+TG_HD void eval_tqnode(const Ctx& c, const ItemDesc& it, Emit& em) {
+  const int r0 = it.row0, ee = it.ee, ts = sp_torque(ee), ms = sp_motion(ee);
+  double p[3], tau[3], tau0[3];
+  for (int e = 0; e < 3; ++e) {
+    p[e] = xval(c, node_col(c, ms, it.a1, kPos, e));
+    tau[e] = xval(c, node_col(c, ts, it.a0, kPos, e));
+    tau0[e] = xval(c, node_col(c, ts, it.a2, kPos, e));
+  }
+  double n[3], t1[3], t2[3];
+  ter_nbasis(*c.ter, 0, p[0], p[1], n);
+  ter_nbasis(*c.ter, 1, p[0], p[1], t1);
+  ter_nbasis(*c.ter, 2, p[0], p[1], t2);
+  em.g(r0 + 0, dot3(tau, t1));
+  em.g(r0 + 1, dot3(tau, t2));
+  em.g(r0 + 2, dot3(tau, n));
+  for (int dim = 0; dim < 3; ++dim) {
+    const int col = node_col(c, ts, it.a0, kPos, dim);
+    em(r0 + 0, col, t1[dim], true);
+    em(r0 + 1, col, t2[dim], true);
+    em(r0 + 2, col, n[dim], true);
+  }
+  for (int dim = 0; dim < 2; ++dim) {
+    double dn[3], dt1[3], dt2[3];
+    ter_d_nbasis(*c.ter, 1, dim, p[0], p[1], dt1);
+    ter_d_nbasis(*c.ter, 2, dim, p[0], p[1], dt2);
+    ter_d_nbasis(*c.ter, 0, dim, p[0], p[1], dn);
+    const int col = node_col(c, ms, it.a1, kPos, dim);
+    em(r0 + 0, col, dot3(tau0, dt1), true);
+    em(r0 + 1, col, dot3(tau0, dt2), true);
+    em(r0 + 2, col, dot3(tau0, dn), true);
+  }
+}
+
+// TerrainConstraintHard instant (terrain_constraint_hard.cc:50-132). The value caps the clearance
+// term at k_coeff_ = 0.02 while the Jacobian's velocity term switches off at 0.05 (SURVEY A22 iii),
+// as in the reference. Position and velocity rows of one dimension share their columns.
+template <class Emit>
+TG_HD void eval_thard(const Ctx& c, const ItemDesc& it, Emit& em) {
+  const int ms = sp_motion(it.ee);
+  SplinePt P;
+  spline_eval(c, ms, it.t, P);
+  double n[3], t1[3], t2[3];
+  ter_nbasis(*c.ter, 0, P.p[0], P.p[1], n);
+  ter_nbasis(*c.ter, 1, P.p[0], P.p[1], t1);
+  ter_nbasis(*c.ter, 2, P.p[0], P.p[1], t2);
+  const double vt1 = dot3(P.v, t1), vt2 = dot3(P.v, t2), vtm = sqrt(vt1 * vt1 + vt2 * vt2), kc = 0.02;
+  const double a = kc * vtm;
+  em.g(it.row0, (P.p[2] - ter_h(*c.ter, P.p[0], P.p[1])) - (kc < a ? kc : a));
+  const bool vel = vtm > 1e-6 && a < 0.05 - 1e-6;
+  double Hp[4], Hv[4];
+  spline_basis(P, kPos, Hp);
+  spline_basis(P, kVel, Hv);
+  for (int k = 0; k < 3; ++k) {
+    const int dim = k == 0 ? Z : k - 1;   // jac_pos.row(Z), then -= dh/d(x|y) * jac_pos.row(x|y)
+    const double cp = dim == Z ? 1.0 : -ter_dh(*c.ter, dim, P.p[0], P.p[1]);
+    const double cv = vel ? -(kc * ((vt1 * t1[dim] + vt2 * t2[dim]) / vtm)) : 0.0;
+    double Heff[4];
+    for (int bb = 0; bb < 4; ++bb) Heff[bb] = cp * Hp[bb] + cv * Hv[bb];
+    emit_dim(c, em, it.row0, ms, P, Heff, dim, 1.0);
+  }
+}
+
+// EELinearConstraint instant (ee_linear_constraint.cc:19-48); it.a0 = definition
+template <class Emit>
+TG_HD void eval_eelin(const Ctx& c, const ItemDesc& it, Emit& em) {
+  const EELinDef& d = c.eelin[it.a0];
+  double val = 0.0;
+  for (int q = 0; q < d.n; ++q) {
+    const int ee = d.code[q] / 3, dim = d.code[q] % 3, s = d.target == 0 ? sp_motion(ee) : sp_ang(ee);
+    SplinePt P;
+    spline_eval(c, s, it.t, P);
+    val += d.coeff[q] * (d.deriv == 0 ? P.p[dim] : P.v[dim]);
+    double H[4];
+    spline_basis(P, d.deriv == 0 ? kPos : kVel, H);
+    emit_dim(c, em, it.row0, s, P, H, dim, d.coeff[q]);
+  }
+  em.g(it.row0, val);
+}
+
 // TotalDurationConstraint (total_duration_constraint.cc:49-72): sum of the ee's optimised durations
 template <class Emit>
 TG_HD void eval_tdur(const Ctx& c, const ItemDesc& it, Emit& em) {
@@ -981,6 +1137,10 @@ TG_HD void eval_item(const Ctx& c, const ItemDesc& it, Emit& em) {
     case IT_BHGT: eval_height(c, it, SP_BASE_LIN, it.p0, em); break;
     case IT_SWING: eval_swing(c, it, em); break;
     case IT_TDUR: eval_tdur(c, it, em); break;
+    case IT_TQDISC: eval_tqdisc(c, it, em); break;
+    case IT_TQNODE: eval_tqnode(c, it, em); break;
+    case IT_THARD: eval_thard(c, it, em); break;
+    case IT_EELIN: eval_eelin(c, it, em); break;
   }
 }
 

@@ -41,6 +41,7 @@ struct Layout {
   std::vector<PolyPhase> pinfo; // PhaseSpline polynomial phases
   std::vector<PhaseCol> pcols;  // PhaseSpline full-pattern columns
   std::vector<SchedInfo> sched; // per endeffector (col0 = -1 without schedule variables)
+  std::vector<EELinDef> eelin;  // EELinearConstraint definitions (ItemDesc::a0 indexes them)
   std::vector<ItemDesc> items;
   std::vector<int32_t> slots;     // build-time: candidate -> global CSR position (or -1)
   std::vector<SlotGroup> slot_groups;   // device slot table (see SlotGroup); item.slot indexes it
@@ -69,14 +70,17 @@ struct Layout {
 };
 
 constexpr int kMiscWaves = 4;
-constexpr bool is_misc_kind(int t) { return t != IT_DYN && t != IT_ROM && t != IT_FDISC; }
+constexpr bool is_misc_kind(int t) { return t != IT_DYN && t != IT_ROM && t != IT_FDISC && t != IT_TQDISC; }
 
-// launch classes: the three heavy kinds have their own kernels, the small kinds share one
-enum LaunchClass { LC_DYN = 0, LC_ROM = 1, LC_FDISC = 2, LC_MISC = 3, LC_COUNT = 4 };
+// launch classes: the heavy kinds have their own kernels, the small kinds share one
+enum LaunchClass { LC_DYN = 0, LC_ROM = 1, LC_FDISC = 2, LC_TQDISC = 3, LC_MISC = 4, LC_COUNT = 5 };
+constexpr int class_type(int lc) { return lc == LC_TQDISC ? IT_TQDISC : lc; }   // tile classes
 
 // LDS tile caps (doubles of CSR values / rows per tile)
 constexpr int kTileValueCap = 8192;
 constexpr int kTileRowCap = 2048;
+constexpr int kMiscValueCap = 3072;   // small-kind tiles: 4 share one block's LDS
+constexpr int kMiscRowCap = 512;
 
 // Launch geometry of each item type (wave-uniform: each wave of a block runs one code path)
 struct TypeSpec { int block; int max_inst; };

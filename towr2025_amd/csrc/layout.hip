@@ -270,7 +270,9 @@ int item_rows(int type) {
     case IT_DYN: case IT_BMOT: return 6;
     case IT_ROM: case IT_SACC: return 3;
     case IT_FDISC: case IT_FNODE: return 5;
-    case IT_TERR: case IT_BHGT: case IT_TDUR: return 1;
+    case IT_TERR: case IT_BHGT: case IT_TDUR: case IT_THARD: case IT_EELIN: return 1;
+    case IT_TQDISC: return 4;
+    case IT_TQNODE: return 3;
     case IT_SWING: return 4;
   }
   return 0;
@@ -351,7 +353,7 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
   }
 
   // ---- constraint sets and work items (AddConstraintSet order)
-  L.cons.clear(); L.items.clear();
+  L.cons.clear(); L.items.clear(); L.eelin.clear();
   std::vector<int> item_inst;   // instance id (items of one instance share rows)
   int row = 0, inst = 0;
   auto dts_of = [](double Tc, double dt) {   // time_discretization_constraint.cc:37-50
@@ -369,10 +371,12 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
       L.items.push_back(it); item_inst.push_back(inst);
     };
     const bool timed = c.kind == TOWR_C_DYNAMIC || c.kind == TOWR_C_RANGE_OF_MOTION ||
-                       c.kind == TOWR_C_FORCE_DISCRETIZED || c.kind == TOWR_C_BASE_MOTION;
+                       c.kind == TOWR_C_FORCE_DISCRETIZED || c.kind == TOWR_C_BASE_MOTION ||
+                       c.kind == TOWR_C_TORQUE_DISCRETIZED || c.kind == TOWR_C_TERRAIN_HARD || c.kind == TOWR_C_EE_LINEAR;
     if (timed && !(c.dt > 0 && c.T > 0)) { err = "time-discretised constraint needs T > 0 and dt > 0"; return TOWR_ERR_INVALID; }
     const bool ee_c = c.kind == TOWR_C_RANGE_OF_MOTION || c.kind == TOWR_C_FORCE || c.kind == TOWR_C_FORCE_DISCRETIZED ||
-                      c.kind == TOWR_C_TERRAIN || c.kind == TOWR_C_SWING;
+                      c.kind == TOWR_C_TERRAIN || c.kind == TOWR_C_SWING || c.kind == TOWR_C_TORQUE_DISCRETIZED ||
+                      c.kind == TOWR_C_TORQUE || c.kind == TOWR_C_TERRAIN_HARD;
     if (ee_c && (c.ee < 0 || c.ee >= E)) { err = "constraint endeffector out of range"; return TOWR_ERR_INVALID; }
     switch (c.kind) {
       case TOWR_C_DYNAMIC: {
@@ -444,6 +448,53 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
         info.rows = 3 * (nj > 0 ? nj : 0);
         break;
       }
+      case TOWR_C_TORQUE_DISCRETIZED: {   // torque_constraint_discretized.cc:69-93
+        auto ts = dts_of(c.T, c.dt);
+        for (int k = 0; k < (int)ts.size(); ++k, ++inst) add(IT_TQDISC, 0, c.ee, k, row + 4 * k, ts[k], 0, 0, c.p[4]);
+        info.rows = 4 * (int)ts.size();
+        break;
+      }
+      case TOWR_C_TORQUE: {        // torque_constraint.cc:56-66: non-constant torque nodes
+        const NodeSet& tv = sets[5 + 4 * c.ee];
+        const NodeSet& mv = sets[2 + 4 * c.ee];
+        int k = 0;
+        for (int id = 0; id < tv.n_nodes; ++id)
+          if (!tv.is_constant_node(id)) {
+            const int ph = tv.phase_of(id);
+            const int mn = mv.node_at_start_of_phase(ph), tn = tv.node_at_start_of_phase(ph);
+            if (mn < 0 || tn < 0) { err = "torque node phase has no start node"; return TOWR_ERR_INVALID; }
+            add(IT_TQNODE, 0, c.ee, k, row + 3 * k, 0.0, id, mn, c.p[4]);
+            L.items.back().a2 = tn;
+            ++k; ++inst;
+          }
+        info.rows = 3 * k;
+        break;
+      }
+      case TOWR_C_TERRAIN_HARD: {  // terrain_constraint_hard.cc:35-48
+        auto ts = dts_of(c.T, c.dt);
+        for (int k = 0; k < (int)ts.size(); ++k, ++inst) add(IT_THARD, 0, c.ee, k, row + k, ts[k], 0, 0, 0.0);
+        info.rows = (int)ts.size();
+        break;
+      }
+      case TOWR_C_EE_LINEAR: {     // ee_linear_constraint.cc:5-17
+        if (c.ip[2] < 1 || c.ip[2] > 6 || c.ip[0] < 0 || c.ip[0] > 1 || c.ip[1] < 0 || c.ip[1] > 1) { err = "bad EELinear definition"; return TOWR_ERR_INVALID; }
+        EELinDef def{};
+        def.target = c.ip[0]; def.deriv = c.ip[1];
+        for (int q = 0; q < c.ip[2]; ++q) {   // one term per (ee, dim): coefficients of repeats are summed
+          const int code = c.ip[3 + q];
+          if (code < 0 || code >= 3 * E) { err = "bad EELinear term"; return TOWR_ERR_INVALID; }
+          int w = 0;
+          while (w < def.n && def.code[w] != code) ++w;
+          if (w == def.n) { def.code[def.n] = code; def.coeff[def.n] = 0.0; ++def.n; }
+          def.coeff[w] += c.p[q];
+        }
+        const int di = (int)L.eelin.size();
+        L.eelin.push_back(def);
+        auto ts = dts_of(c.T, c.dt);
+        for (int k = 0; k < (int)ts.size(); ++k, ++inst) add(IT_EELIN, 0, 0, k, row + k, ts[k], di, 0, 0.0);
+        info.rows = (int)ts.size();
+        break;
+      }
       case TOWR_C_TOTAL_DURATION:  // total_duration_constraint.cc:36-47
         if (c.ee < 0 || c.ee >= E || L.sched[c.ee].col0 < 0) { err = "TotalDurationConstraint needs the ee's schedule variables"; return TOWR_ERR_INVALID; }
         add(IT_TDUR, 0, c.ee, 0, row, 0.0, 0, 0, 0.0); ++inst;
@@ -463,7 +514,8 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
     int last_inst = -1, last_row = -1;
     for (size_t q = 0; q < L.items.size(); ++q) {
       ItemDesc& it = L.items[q];
-      const bool timed = it.type == IT_DYN || it.type == IT_ROM || it.type == IT_FDISC || it.type == IT_BMOT;
+      const bool timed = it.type == IT_DYN || it.type == IT_ROM || it.type == IT_FDISC || it.type == IT_BMOT ||
+                         it.type == IT_TQDISC || it.type == IT_THARD || it.type == IT_EELIN;
       if (!timed) { it.seg = -1; continue; }
       if (item_inst[q] != last_inst) {
         last_inst = item_inst[q];
@@ -495,6 +547,7 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
     cx.x = L.x0.data(); cx.nodecol = L.nodecol.data(); cx.spl = L.spl.data(); cx.dur = L.dur.data();
     cx.ter = &L.terrain; cx.rb = L.rb; cx.fdisc_motion = L.fdisc_motion;
     cx.gait = L.gait; cx.pinfo = L.pinfo.data(); cx.pcols = L.pcols.data(); cx.sched = L.sched.data();
+    cx.eelin = L.eelin.data();
     for (size_t i = 0; i < L.items.size(); ++i) {
       item_cand_begin[i] = (int32_t)crow.size();
       RecordEmit em{&crow, &ccol, &cpres};
@@ -582,7 +635,8 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
           const int a = (int)((int64_t)t * n_inst / n_tiles), b = (int)((int64_t)(t + 1) * n_inst / n_tiles);
           if (b <= a) continue;
           auto rr = inst_rows(a, b);
-          if (L.row_ptr[rr.second] - L.row_ptr[rr.first] > kTileValueCap || rr.second - rr.first > kTileRowCap) ok = false;
+          const int vcap = is_misc_kind(type) ? kMiscValueCap : kTileValueCap, rcap = is_misc_kind(type) ? kMiscRowCap : kTileRowCap;
+          if (L.row_ptr[rr.second] - L.row_ptr[rr.first] > vcap || rr.second - rr.first > rcap) ok = false;
         }
         if (ok) break;
         if (n_tiles >= n_inst) { err = "internal: one instance exceeds the LDS tile"; return TOWR_ERR_UNSUPPORTED; }
@@ -715,6 +769,7 @@ TypeSpec type_spec(int type, int n_ee) {
     case IT_DYN: return {256, std::max(1, std::min(64, 128 / std::max(1, n_ee)))};  // waves: g0 | g1 | ee, ee
     case IT_ROM: return {192, 64};                                                      // waves: g0 | g1 | g2
     case IT_FDISC: return {192, 192};
+    case IT_TQDISC: return {192, 192};
     default: return {64, 64};
   }
 }

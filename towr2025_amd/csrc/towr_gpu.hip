@@ -42,6 +42,7 @@ struct KParams {
   const PolyPhase* pinfo;        // phase-duration optimisation tables (see engine_math.h)
   const PhaseCol* pcols;
   const SchedInfo* sched;
+  const EELinDef* eelin;
   int32_t n_spl;
   const towr_terrain_t* terrains;
   int32_t terrain_per_problem;
@@ -94,6 +95,7 @@ __device__ __forceinline__ void eval_typed(const Ctx& c, const ItemDesc& it, Emi
   else if constexpr (TYPE == IT_BHGT) eval_height(c, it, SP_BASE_LIN, it.p0, em);
   else if constexpr (TYPE == IT_SWING) eval_swing(c, it, em);
   else if constexpr (TYPE == IT_TDUR) eval_tdur(c, it, em);
+  else if constexpr (TYPE == IT_TQDISC) eval_tqdisc(c, it, em);
 }
 
 // global -> LDS copy of n16 16-byte units: each thread issues up to K independent loads before its
@@ -188,7 +190,7 @@ __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_ker
     c.x = xsrc; c.nodecol = ncsrc; c.spl = P.spl; c.dur = P.dur;
     c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
     c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
-    c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.sched = P.sched;
+    c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.sched = P.sched; c.eelin = P.eelin;
     eval_typed<TYPE>(c, it, em);
     em.flush();
   }
@@ -232,7 +234,7 @@ __global__ void __launch_bounds__(64 * kMiscWaves, 1) towr_misc_kernel(KParams P
     c.x = xs; c.nodecol = ns; c.spl = P.spl; c.dur = P.dur;
     c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
     c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
-    c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.sched = P.sched;
+    c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.sched = P.sched; c.eelin = P.eelin;
     switch (it.type) {   // wave-uniform: a wave holds one tile of one kind
       case IT_FNODE: eval_fnode(c, it, em); break;
       case IT_TERR: eval_height(c, it, sp_motion(it.ee), 0.0, em); break;
@@ -241,6 +243,9 @@ __global__ void __launch_bounds__(64 * kMiscWaves, 1) towr_misc_kernel(KParams P
       case IT_BHGT: eval_height(c, it, SP_BASE_LIN, it.p0, em); break;
       case IT_SWING: eval_swing(c, it, em); break;
       case IT_TDUR: eval_tdur(c, it, em); break;
+      case IT_TQNODE: eval_tqnode(c, it, em); break;
+      case IT_THARD: eval_thard(c, it, em); break;
+      case IT_EELIN: eval_eelin(c, it, em); break;
       default: break;
     }
   }
@@ -259,13 +264,14 @@ const void* kernel_for_mode(int type) {
     case IT_DYN: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_DYN, 256, GAIT>);
     case IT_ROM: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_ROM, 192, GAIT>);
     case IT_FDISC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_FDISC, 192, GAIT>);
+    case IT_TQDISC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_TQDISC, 192, GAIT>);
   }
   return nullptr;
 }
 const void* kernel_for(int type, bool gait) { return gait ? kernel_for_mode<true>(type) : kernel_for_mode<false>(type); }
 const void* kernel_for_class(int lc, bool gait) {
   if (lc == LC_MISC) return gait ? reinterpret_cast<const void*>(&towr_misc_kernel<true>) : reinterpret_cast<const void*>(&towr_misc_kernel<false>);
-  return kernel_for(lc, gait);   // LC_DYN/ROM/FDISC == IT_DYN/ROM/FDISC
+  return kernel_for(class_type(lc), gait);
 }
 
 }  // namespace
@@ -290,6 +296,7 @@ struct towr_gpu_handle_s {
   PhaseCol* d_pcols = nullptr;
   SchedInfo* d_sched = nullptr;
   int32_t* d_misc = nullptr;
+  EELinDef* d_eelin = nullptr;
   // fork-join of the per-kind launches (TOWR_GPU_STREAMS = total streams incl. the caller's, 1..4)
   static constexpr int kMaxSide = 3;
   int n_side = 0;
@@ -337,17 +344,19 @@ int bind(towr_gpu_handle h) {
 }
 
 // LDS of a launch class: [tile region(s) | x + zero slot | node table]
-size_t lds_region(const Layout& L, int lc) { return lc == LC_MISC ? (size_t)kMiscWaves * L.misc_stride : (size_t)L.type_lds[lc]; }
+size_t lds_region(const Layout& L, int lc) { return lc == LC_MISC ? (size_t)kMiscWaves * L.misc_stride : (size_t)L.type_lds[class_type(lc)]; }
 size_t lds_bytes(const Layout& L, int lc) {
   size_t d = lds_region(L, lc);
-  d += (size_t)((L.n + 2) & ~1);                                                          // x + zero slot
-  if (lc == LC_MISC || stages_nodes(lc, L.gait)) d += (L.nodecol.size() + 3) / 4 * 2;     // node table (16-B units)
+  d += (size_t)((L.n + 2) & ~1);                                                                  // x + zero slot
+  if (lc == LC_MISC || stages_nodes(class_type(lc), L.gait)) d += (L.nodecol.size() + 3) / 4 * 2;  // node table (16-B units)
   return sizeof(double) * d;
 }
 int class_units(const Layout& L, int lc) {   // tiles (or misc groups) per problem
-  return lc == LC_MISC ? (int)(L.misc_tiles.size() / kMiscWaves) : L.type_tile0[lc + 1] - L.type_tile0[lc];
+  if (lc == LC_MISC) return (int)(L.misc_tiles.size() / kMiscWaves);
+  const int t = class_type(lc);
+  return L.type_tile0[t + 1] - L.type_tile0[t];
 }
-int64_t class_bytes(const Layout& L, int lc) { return lc == LC_MISC ? L.misc_bytes : L.type_bytes[lc]; }
+int64_t class_bytes(const Layout& L, int lc) { return lc == LC_MISC ? L.misc_bytes : L.type_bytes[class_type(lc)]; }
 
 int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, int64_t ldg, double* V, int64_t ldv,
            int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem, int only_class = -1) {
@@ -373,15 +382,15 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
     P.items = h->d_items; P.slots = h->d_slots; P.tiles = h->d_tiles;
     P.nodecol = h->d_nodecol; P.spl = h->d_spl; P.dur = h->d_dur;
     P.segs = h->d_segs; P.n_spl = (int32_t)L.spl.size();
-    P.pinfo = h->d_pinfo; P.pcols = h->d_pcols; P.sched = h->d_sched;
+    P.pinfo = h->d_pinfo; P.pcols = h->d_pcols; P.sched = h->d_sched; P.eelin = h->d_eelin;
     P.terrains = terrains; P.terrain_per_problem = per_problem;
     P.B = B; P.ntiles = nt;
     if (lc == LC_MISC) {
       P.tile0 = 0;
       P.misc_tiles = h->d_misc; P.misc_stride = L.misc_stride; P.misc_rows_off = L.misc_rows_off;
     } else {
-      P.tile0 = L.type_tile0[lc];
-      P.lds_rows_off = L.type_lds_rows_off[lc];
+      P.tile0 = L.type_tile0[class_type(lc)];
+      P.lds_rows_off = L.type_lds_rows_off[class_type(lc)];
     }
     P.n = L.n; P.n_pad = (L.n + 2) & ~1; P.n_nodecol = (int32_t)L.nodecol.size();
     P.lds_x_off = (int32_t)lds_region(L, lc);
@@ -390,7 +399,7 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
     const int64_t total = (int64_t)B * nt;
     const int64_t grid = ((total + 7) / 8) * 8;
     if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
-    const int block = lc == LC_MISC ? 64 * kMiscWaves : L.type_block[lc];
+    const int block = lc == LC_MISC ? 64 * kMiscWaves : L.type_block[class_type(lc)];
     void* args[] = {&P};
     HIPCHK(h, hipLaunchKernel(kernel_for_class(lc, L.gait), dim3((unsigned)grid), dim3((unsigned)block), args,
                               lds_bytes(L, lc), st));
@@ -490,7 +499,7 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
       (r = upload(h, &h->d_tiles, L.tiles)) || (r = upload(h, &h->d_nodecol, nodecol16)) ||
       (r = upload(h, &h->d_spl, L.spl)) || (r = upload(h, &h->d_dur, L.dur)) || (r = upload(h, &h->d_segs, L.segs)) || (r = upload(h, &h->d_terrain, ter)) ||
       (r = upload(h, &h->d_pinfo, L.pinfo)) || (r = upload(h, &h->d_pcols, L.pcols)) || (r = upload(h, &h->d_sched, L.sched)) ||
-      (r = upload(h, &h->d_misc, L.misc_tiles)))
+      (r = upload(h, &h->d_misc, L.misc_tiles)) || (r = upload(h, &h->d_eelin, L.eelin)))
     return bail(r);
   {
     const char* ns = std::getenv("TOWR_GPU_STREAMS");
@@ -520,7 +529,7 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
 int towr_gpu_destroy(towr_gpu_handle h) {
   if (!h) return TOWR_OK;
   void* dev[] = {h->d_items, h->d_slots, h->d_tiles, h->d_nodecol, h->d_spl, h->d_dur, h->d_segs, h->d_terrain,
-                 h->d_pinfo, h->d_pcols, h->d_sched, h->d_misc,
+                 h->d_pinfo, h->d_pcols, h->d_sched, h->d_misc, h->d_eelin,
                  h->d_bterrain, h->d_x, h->d_g, h->d_v};
   if (h->device >= 0) for (void* p : dev) if (p) (void)hipFree(p);
   void* host[] = {h->h_x, h->h_g, h->h_v};
@@ -633,7 +642,7 @@ int towr_gpu_eval_batch_device(towr_gpu_handle h, int32_t B, const double* X, in
 }
 
 int towr_gpu_kernel_info(towr_gpu_handle h, int32_t kernel, const char** name, int32_t* n_tiles, int64_t* bytes_per_problem) {
-  static const char* names[LC_COUNT] = {"dynamic", "range_of_motion", "force_discretized", "small_kinds"};
+  static const char* names[LC_COUNT] = {"dynamic", "range_of_motion", "force_discretized", "torque_discretized", "small_kinds"};
   if (!h || kernel < 0 || kernel >= LC_COUNT) return fail(h, TOWR_ERR_INVALID, "bad kernel index");
   if (name) *name = names[kernel];
   if (n_tiles) *n_tiles = class_units(h->L, kernel);

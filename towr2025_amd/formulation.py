@@ -375,6 +375,11 @@ class Parameters:
         self.dt_constraint_dynamic_ = 0.1
         self.dt_constraint_base_motion_ = self.duration_base_polynomial_ / 4.
         self.dt_constraint_force_ = 0.02
+        self.dt_constraint_torque_ = 0.02           # 0 => node-based TorqueConstraint
+        self.torque_tx_min_, self.torque_tx_max_ = -100.0, 100.0
+        self.torque_ty_min_, self.torque_ty_max_ = -100.0, 100.0
+        self.torque_k_friction_ = 2.0 / 3.0
+        self.ee_linear_constraints_: List["EELinearConstraintDef"] = []
         self.dt_constraint_torque_ = 0.02
         self.bound_phase_duration_ = (0.2, 1.0)
         self.constraints_ = [Parameters.Terrain, Parameters.Dynamic, Parameters.BaseAcc,
@@ -417,6 +422,18 @@ class Parameters:
             out.append(dt if t_left > dt else t_left)
             t_left -= dt
         return out
+
+
+@dataclass
+class EELinearConstraintDef:
+    """Parameters::EELinearConstraintDef (parameters.h:317-325): |sum_i coeff_i * ee_i[dim_i]| <= tolerance
+    at discretised times, on the ee motion (target 0) or ee angle (target 1) splines, position
+    (deriv 0) or velocity (deriv 1). terms: (ee, dim, coeff) triples (at most 6)."""
+    terms: List[Tuple[int, int, float]]
+    target: int = 0
+    deriv: int = 0
+    tolerance: float = 0.0
+    dt: float = 0.1
 
 
 @dataclass
@@ -488,10 +505,23 @@ class NlpFormulation:
                 out += [dict(kind=capi.C_SPLINE_ACC, ee=0), dict(kind=capi.C_SPLINE_ACC, ee=1)]
             elif name == Parameters.BaseHeight:
                 out.append(dict(kind=capi.C_BASE_HEIGHT, ee=0, p=[0.4]))  # nlp_formulation.cc:597
-            elif name in (Parameters.TerrainHard, Parameters.Torque):
-                raise NotImplementedError("TerrainHard/Torque constraints are next-tier (SURVEY §8f)")
+            elif name == Parameters.TerrainHard:     # nlp_formulation.cc:492-506
+                out += [dict(kind=capi.C_TERRAIN_HARD, ee=ee, T=T, dt=P.dt_constraint_range_of_motion_)
+                        for ee in range(E)]
+            elif name == Parameters.Torque:          # nlp_formulation.cc:533-558
+                tp = [P.torque_tx_min_, P.torque_tx_max_, P.torque_ty_min_, P.torque_ty_max_, P.torque_k_friction_]
+                for ee in range(E):
+                    if P.dt_constraint_torque_ > 0.0:
+                        out.append(dict(kind=capi.C_TORQUE_DISCRETIZED, ee=ee, T=T, dt=P.dt_constraint_torque_, p=tp))
+                    else:
+                        out.append(dict(kind=capi.C_TORQUE, ee=ee, p=tp))
             else:
                 raise ValueError("constraint not defined!")
+        for dfn in P.ee_linear_constraints_:        # GetConstraints, nlp_formulation.cc:373-375
+            if not 1 <= len(dfn.terms) <= 6:
+                raise ValueError("EELinear: 1..6 terms supported")
+            out.append(dict(kind=capi.C_EE_LINEAR, ee=0, T=T, dt=dfn.dt, p=[c for _, _, c in dfn.terms],
+                            ip=[dfn.target, dfn.deriv, len(dfn.terms)] + [e * 3 + d for e, d, _ in dfn.terms]))
         return out
 
     def to_desc(self, varsets=None, constraints=None, init_mode=capi.INIT_FORMULATION,
@@ -542,6 +572,8 @@ class NlpFormulation:
             d.constraints[i].dt = c.get("dt", 0.0)
             for j, v in enumerate(c.get("p", [])):
                 d.constraints[i].p[j] = v
+            for j, v in enumerate(c.get("ip", [])):
+                d.constraints[i].ip[j] = v
         it = d.init
         it.mode = init_mode
         b0, b1 = self.initial_base_, self.final_base_

@@ -302,10 +302,30 @@ std::vector<ConstraintSpec> NlpFormulation::GetConstraints() const {
         out.push_back({TOWR_C_SPLINE_ACC, 1, T, 0.0});
         break;
       case Parameters::BaseHeight: { ConstraintSpec c{TOWR_C_BASE_HEIGHT, 0, T, 0.0}; c.p[0] = 0.4; out.push_back(c); break; }   // nlp_formulation.cc:597
-      case Parameters::TerrainHard:
-      case Parameters::Torque: throw std::runtime_error("TerrainHard/Torque constraints are next-tier (SURVEY §8f)");
+      case Parameters::TerrainHard:   // nlp_formulation.cc:492-506
+        for (int ee = 0; ee < E; ++ee) out.push_back({TOWR_C_TERRAIN_HARD, ee, T, P.dt_constraint_range_of_motion_});
+        break;
+      case Parameters::Torque:        // nlp_formulation.cc:533-558
+        for (int ee = 0; ee < E; ++ee) {
+          ConstraintSpec c = P.dt_constraint_torque_ > 0.0 ? ConstraintSpec{TOWR_C_TORQUE_DISCRETIZED, ee, T, P.dt_constraint_torque_}
+                                                           : ConstraintSpec{TOWR_C_TORQUE, ee, T, 0.0};
+          c.p[0] = P.torque_tx_min_; c.p[1] = P.torque_tx_max_; c.p[2] = P.torque_ty_min_; c.p[3] = P.torque_ty_max_;
+          c.p[4] = P.torque_k_friction_;
+          out.push_back(c);
+        }
+        break;
       default: throw std::runtime_error("constraint not defined!");
     }
+  }
+  for (const auto& def : P.ee_linear_constraints_) {   // GetConstraints, nlp_formulation.cc:373-375
+    if (def.terms.empty() || def.terms.size() > 6) throw std::invalid_argument("EELinear: 1..6 terms supported");
+    ConstraintSpec c{TOWR_C_EE_LINEAR, 0, T, def.dt};
+    c.ip[0] = def.target; c.ip[1] = def.deriv; c.ip[2] = (int32_t)def.terms.size();
+    for (size_t q = 0; q < def.terms.size(); ++q) {
+      c.p[q] = def.terms[q].coeff;
+      c.ip[3 + q] = def.terms[q].ee * 3 + def.terms[q].dim;
+    }
+    out.push_back(c);
   }
   return out;
 }
@@ -362,6 +382,7 @@ towr_problem_desc_t NlpFormulation::MakeDesc(const std::vector<VarSet>& vs, cons
     d.constraints[i].T = cs[i].T;
     d.constraints[i].dt = cs[i].dt;
     for (int j = 0; j < 6; ++j) d.constraints[i].p[j] = cs[i].p[j];
+    for (int j = 0; j < 9; ++j) d.constraints[i].ip[j] = cs[i].ip[j];
   }
   towr_init_t& it = d.init;
   it.mode = init_mode;

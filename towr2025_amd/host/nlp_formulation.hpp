@@ -83,6 +83,19 @@ struct Parameters {
   double dt_constraint_dynamic_ = 0.1;
   double dt_constraint_base_motion_ = 0.1 / 4.;
   double dt_constraint_force_ = 0.02;
+  double dt_constraint_torque_ = 0.02;   // 0 => node-based TorqueConstraint
+  double torque_tx_min_ = -100.0, torque_tx_max_ = 100.0, torque_ty_min_ = -100.0, torque_ty_max_ = 100.0;
+  double torque_k_friction_ = 2.0 / 3.0;
+  // Parameters::EELinearConstraintDef (parameters.h:317-325)
+  struct EELinearConstraintDef {
+    struct Term { int ee, dim; double coeff; };
+    std::vector<Term> terms;
+    int target = 0;   // 0 motion, 1 angle
+    int deriv = 0;    // 0 pos, 1 vel
+    double tolerance = 0.0;
+    double dt = 0.1;
+  };
+  std::vector<EELinearConstraintDef> ee_linear_constraints_;
   std::array<double, 2> bound_phase_duration_{0.2, 1.0};
   std::vector<ConstraintName> constraints_{Terrain, Dynamic, BaseAcc, EndeffectorRom, Force, Swing, BaseHeight};
   std::vector<std::vector<double>> ee_phase_durations_;
@@ -100,7 +113,7 @@ struct BaseState {
 };
 
 struct VarSet { int kind, ee; };
-struct ConstraintSpec { int kind, ee; double T, dt; std::array<double, 6> p{}; };
+struct ConstraintSpec { int kind, ee; double T, dt; std::array<double, 6> p{}; std::array<int32_t, 9> ip{}; };
 
 class NlpFormulation {
  public:

@@ -4,7 +4,7 @@
 //   get_nlp_info -> eval_jac_g(structure) -> eval_g(x, new_x = true) -> eval_jac_g(x, new_x = false)
 // and dumps everything to a binary file:
 //   desc bytes | n m (int32) nnz (int64) | x0[n] | iRow[nnz] jCol[nnz] | (device >= 0) g[m] values[nnz]
-// usage: towr_host_check <anymal|biped|hopper> <out.bin> [device (default -1: layout only)]
+// usage: towr_host_check <anymal|biped|biped_next|hopper> <out.bin> [device (default -1: layout only)]
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -19,7 +19,17 @@ int main(int argc, char** argv) {
   if (argc < 3) { std::fprintf(stderr, "usage: %s <anymal|biped|hopper> <out.bin> [device]\n", argv[0]); return 2; }
   const std::string cfg = argv[1];
   const int device = argc > 3 ? std::atoi(argv[3]) : -1;
-  NlpFormulation f = cfg == "anymal" ? AnymalTrot() : cfg == "biped" ? BipedWalk() : MonopedHopper();
+  NlpFormulation f = cfg == "anymal" ? AnymalTrot() : (cfg == "biped" || cfg == "biped_next") ? BipedWalk() : MonopedHopper();
+  if (cfg == "biped_next") {   // SURVEY §8(f) kinds: Torque, TerrainHard, EELinear (tests/configs.py)
+    f.params_.constraints_.push_back(Parameters::Torque);
+    f.params_.constraints_.push_back(Parameters::TerrainHard);
+    Parameters::EELinearConstraintDef a, b;
+    a.terms = {{0, 1, 1.0}, {1, 1, 1.0}};
+    a.tolerance = 0.5;
+    b.terms = {{0, 2, 0.5}, {1, 0, -1.0}, {0, 2, 0.5}};
+    b.target = 1; b.deriv = 1; b.tolerance = 1.0; b.dt = 0.05;
+    f.params_.ee_linear_constraints_ = {a, b};
+  }
   try {
     const towr_problem_desc_t d = f.MakeDesc();
     Engine e(d, device);
