@@ -28,12 +28,13 @@
 extern "C" {
 #endif
 
-#define TOWR_GPU_ABI_VERSION 2
+#define TOWR_GPU_ABI_VERSION 3
 
 #define TOWR_MAX_EE          4
 #define TOWR_MAX_PHASES      48
 #define TOWR_MAX_VARSETS     (2 + 5 * TOWR_MAX_EE)
 #define TOWR_MAX_CONSTRAINTS 64
+#define TOWR_MAX_COSTS       128
 
 /* ---- status codes ---------------------------------------------------------------------- */
 #define TOWR_OK                  0
@@ -123,6 +124,23 @@ typedef struct {
   int32_t reserved;
 } towr_constraint_t;
 
+/* ---- cost terms: NlpFormulation::GetCosts (nlp_formulation.cc:604-680) ------------------------ */
+enum towr_cost_kind {
+  TOWR_COST_NODE        = 0, /* NodeCost: ip[0] = variable set kind (towr_varset_kind), ee, ip[1] = deriv
+                                (0 pos, 1 vel), ip[2] = dim; weight             (node_cost.cc:36-79)       */
+  TOWR_COST_ENERGY      = 1, /* EnergyCost: weight, dt, p[0] = torque weight   (energy_cost.cc:36-152)    */
+  TOWR_COST_ANG_MOMENTUM= 2, /* AngularMomentumCost: weight, dt                 (angular_momentum_cost.cc:39-208) */
+  TOWR_COST_EE_BASE_POS = 3  /* EEBasePosCost: ee, weight, dt, p[0..2] = p_ref_B  (ee_base_pos_cost.cc:38-162) */
+};
+typedef struct {
+  int32_t kind;    /* towr_cost_kind                                                             */
+  int32_t ee;
+  double  weight;
+  double  dt;
+  double  p[4];
+  int32_t ip[4];
+} towr_cost_t;
+
 /* ---- initial guess (NlpFormulation::MakeBaseVariables etc., nlp_formulation.cc:121-346) ---- */
 enum towr_init_mode {
   TOWR_INIT_FORMULATION = 0,  /* NlpFormulation::GetVariableSets initialisation                  */
@@ -160,6 +178,9 @@ typedef struct {
   towr_varset_t     varsets[TOWR_MAX_VARSETS];
   towr_constraint_t constraints[TOWR_MAX_CONSTRAINTS];
   towr_init_t       init;
+  int32_t           n_costs;                /* order = ifopt AddCostSet order (cost terms)          */
+  int32_t           reserved_costs;
+  towr_cost_t       costs[TOWR_MAX_COSTS];
 } towr_problem_desc_t;
 
 typedef struct towr_gpu_handle_s* towr_gpu_handle;
@@ -199,6 +220,14 @@ int towr_gpu_eval_g(towr_gpu_handle h, const double* x, double* g);
 int towr_gpu_eval_jac_values(towr_gpu_handle h, const double* x, double* values);
 /* both at once (one fused launch)                                                                */
 int towr_gpu_eval_g_jac(towr_gpu_handle h, const double* x, double* g, double* values);
+/* Objective (IpoptAdapter::eval_f = Problem::EvaluateCostFunction, the sum of every cost term's
+ * GetCost) and its dense gradient (eval_grad_f = Problem::EvaluateCostFunctionGradient). A problem
+ * without cost terms has f = 0 and a zero gradient.                                               */
+int towr_gpu_eval_f(towr_gpu_handle h, const double* x, double* f);
+int towr_gpu_eval_grad_f(towr_gpu_handle h, const double* x, double* grad);
+/* Batched objective on the device: F[b], GRAD[b*ldgrad + j]; stream as for eval_batch_device.    */
+int towr_gpu_eval_cost_batch_device(towr_gpu_handle h, int32_t B, const double* X, int64_t ldx,
+                                    double* F, double* GRAD, int64_t ldgrad, void* stream);
 
 /* ---- batched evaluation over independent problems that share the layout ---------------------- */
 /* Per-problem terrain parameters (the only per-instance input to g/J besides x). `terrains` is a

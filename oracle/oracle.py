@@ -39,6 +39,8 @@ def lib():
         L.oracle_eval_jac.argtypes = [C.c_void_p, D, C.c_long, I, I, D]
         L.oracle_eval_jac_values.restype = C.c_long
         L.oracle_eval_jac_values.argtypes = [C.c_void_p, D, D]
+        L.oracle_eval_f.argtypes = [C.c_void_p, D, D]
+        L.oracle_eval_grad_f.argtypes = [C.c_void_p, D, D]
         L.oracle_constraint_rows.argtypes = [C.c_void_p, C.c_int, I, I]
         L.oracle_varset_cols.argtypes = [C.c_void_p, C.c_int, I, I]
         L.oracle_bench.restype = C.c_double
@@ -82,6 +84,20 @@ class Oracle:
         x = np.ascontiguousarray(x, dtype=np.float64)
         g = np.zeros(self.m)
         lib().oracle_eval_g(self.h, _d(x), _d(g))
+        return g
+
+    def eval_f(self, x):
+        """Problem::EvaluateCostFunction (IpoptAdapter::eval_f)."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        f = np.zeros(1)
+        lib().oracle_eval_f(self.h, _d(x), _d(f))
+        return float(f[0])
+
+    def eval_grad_f(self, x):
+        """Problem::EvaluateCostFunctionGradient (IpoptAdapter::eval_grad_f), dense."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        g = np.zeros(self.n)
+        lib().oracle_eval_grad_f(self.h, _d(x), _d(g))
         return g
 
     def eval_jac(self, x):

@@ -1729,6 +1729,18 @@ oracle_t* oracle_create(const towr_problem_desc_t* d, char* err, int errlen) {
   }
   o->n = col;
 
+  /* ---- cost terms ---- */
+  if (d->n_costs < 0 || d->n_costs > TOWR_MAX_COSTS) { set_err(err, errlen, "bad n_costs"); oracle_destroy(o); return NULL; }
+  for (int i = 0; i < d->n_costs; ++i) {
+    const towr_cost_t* c = &d->costs[i];
+    int ok = c->kind >= TOWR_COST_NODE && c->kind <= TOWR_COST_EE_BASE_POS;
+    if (c->kind == TOWR_COST_NODE)
+      ok = ok && c->ip[0] >= TOWR_VAR_BASE_LIN && c->ip[0] <= TOWR_VAR_EE_TORQUE && c->ip[1] >= 0 && c->ip[1] <= 1 &&
+           c->ip[2] >= 0 && c->ip[2] <= 2 && (c->ip[0] <= TOWR_VAR_BASE_ANG || (c->ee >= 0 && c->ee < E));
+    if (c->kind == TOWR_COST_EE_BASE_POS) ok = ok && c->ee >= 0 && c->ee < E;
+    if (!ok) { set_err(err, errlen, "bad cost term"); oracle_destroy(o); return NULL; }
+  }
+
   /* ---- constraint sets in AddConstraintSet order ---- */
   int row = 0;
   o->n_cons = d->n_constraints;
@@ -1818,6 +1830,190 @@ void oracle_destroy(oracle_t* o) {
   nv_free(o->base_lin); nv_free(o->base_ang);
   sp_free(&o->euler.jac_struct); sp_free(&o->model.I_b);
   free(o);
+}
+
+
+/* =============================================================================================
+ * Cost terms (NlpFormulation::GetCosts, nlp_formulation.cc:604-680; towr/src/costs/):
+ * IpoptAdapter::eval_f = sum of every term's GetCost, eval_grad_f = the dense sum of their
+ * FillJacobianBlock rows.
+ * ===========================================================================================*/
+/* GetSampleTimes (energy_cost.cc:41-55 and identical copies): t = 0, dt, ... while t <= T + 1e-9,
+ * accumulated; T = base_linear_->GetTotalTime() (the sum of the base polynomial durations) */
+static int cost_times(const oracle_t* o, double dt, double** out) {
+  double T = 0.0;
+  for (int i = 0; i < o->s_lin->n_polys; ++i) T += o->s_lin->polys[i].T;
+  int cap = dt > 0.0 ? (int)(T / dt) + 4 : 2, n = 0;
+  double* ts = (double*)malloc(sizeof(double) * (size_t)cap);
+  if (dt <= 0.0) { ts[n++] = 0.0; ts[n++] = T; }
+  else for (double t = 0.0; t <= T + 1e-9; t += dt) ts[n++] = t;
+  *out = ts;
+  return n;
+}
+
+/* PhaseDurations::IsContactPhase, phase_durations.cc:120-124 */
+static int pd_is_contact(const PhaseDur* p, double t) {
+  int id = get_segment_id(t, p->d, p->n);
+  return id % 2 == 0 ? p->initial_contact : !p->initial_contact;
+}
+
+static const NodesVar* cost_nodes(const oracle_t* o, int kind, int ee) {
+  switch (kind) {
+    case TOWR_VAR_BASE_LIN: return o->base_lin;
+    case TOWR_VAR_BASE_ANG: return o->base_ang;
+    case TOWR_VAR_EE_MOTION: return o->motion[ee];
+    case TOWR_VAR_EE_ANG: return o->ang[ee];
+    case TOWR_VAR_EE_FORCE: return o->force[ee];
+    case TOWR_VAR_EE_TORQUE: return o->torque[ee];
+  }
+  return NULL;
+}
+
+static int varset_col0(const oracle_t* o, int kind, int ee) {
+  for (int i = 0; i < o->n_vs; ++i) if (vs_is(&o->vs[i], kind, ee)) return o->vs[i].col0;
+  return -1;
+}
+
+/* grad[col0 + col] += s * J[r][col] for every entry of row r of a 3 x n Jacobian */
+static void grad_add_rows(double* grad, int col0, const spmat* J, const double m[3]) {
+  if (col0 < 0) return;
+  for (int r = 0; r < J->rows; ++r)
+    for (int q = 0; q < J->r[r].n; ++q) grad[col0 + J->r[r].e[q].col] += m[r] * J->r[r].e[q].val;
+}
+
+/* value of one term, and (grad != NULL) its gradient added into grad */
+static double cost_term(oracle_t* o, const towr_cost_t* c, double* grad) {
+  double cost = 0.0;   /* NodeCost::GetCost leaves its accumulator uninitialised (node_cost.cc:58): 0 here */
+  switch (c->kind) {
+    case TOWR_COST_NODE: {          /* node_cost.cc:55-79 */
+      const NodesVar* v = cost_nodes(o, c->ip[0], c->ee);
+      int deriv = c->ip[1], dim = c->ip[2];
+      for (int id = 0; id < v->n_nodes; ++id) cost += c->weight * pow(v->nodes[id][deriv][dim], 2);
+      int col0 = varset_col0(o, c->ip[0], c->ee);
+      if (grad && col0 >= 0) {
+        Nvi l[2];
+        for (int i = 0; i < v->n_rows; ++i) {
+          int nl = nv_info(v, i, l);
+          for (int q = 0; q < nl; ++q)
+            if (l[q].deriv == deriv && l[q].dim == dim) grad[col0 + i] += c->weight * 2.0 * v->nodes[l[q].id][deriv][dim];
+        }
+      }
+      break;
+    }
+    case TOWR_COST_ENERGY: {        /* energy_cost.cc:57-152 */
+      if (c->weight <= 0.0) break;
+      double* ts; int nt = cost_times(o, c->dt, &ts);
+      double tw = c->p[0], wdt = c->weight * (c->dt > 0.0 ? c->dt : 1.0);
+      for (int k = 0; k < nt; ++k) {
+        double inst = 0.0, t = ts[k];
+        for (int ee = 0; ee < o->n_ee; ++ee) {
+          double f[3][3], tq[3][3];
+          spline_point(o->s_force[ee], t, f); spline_point(o->s_torque[ee], t, tq);
+          inst += dot3(f[kPos], f[kPos]) + tw * dot3(tq[kPos], tq[kPos]);
+          if (!grad) continue;
+          double mf[3], mt[3];
+          for (int r = 0; r < 3; ++r) { mf[r] = (2.0 * wdt) * f[kPos][r]; mt[r] = (2.0 * wdt * tw) * tq[kPos][r]; }
+          spmat J = spline_jac(o->s_force[ee], t, kPos);
+          grad_add_rows(grad, varset_col0(o, TOWR_VAR_EE_FORCE, ee), &J, mf); sp_free(&J);
+          if (tw != 0.0) { J = spline_jac(o->s_torque[ee], t, kPos); grad_add_rows(grad, varset_col0(o, TOWR_VAR_EE_TORQUE, ee), &J, mt); sp_free(&J); }
+          int cs = varset_col0(o, TOWR_VAR_EE_SCHEDULE, ee);
+          if (cs >= 0) {
+            J = spline_jac_pos_wrt_durations(o->s_force[ee], t); grad_add_rows(grad, cs, &J, mf); sp_free(&J);
+            if (tw != 0.0) { J = spline_jac_pos_wrt_durations(o->s_torque[ee], t); grad_add_rows(grad, cs, &J, mt); sp_free(&J); }
+          }
+        }
+        cost += c->weight * inst * (c->dt > 0.0 ? c->dt : 1.0);
+      }
+      free(ts);
+      break;
+    }
+    case TOWR_COST_ANG_MOMENTUM: {  /* angular_momentum_cost.cc:67-208 (SingleRigidBodyDynamics: true L) */
+      if (c->weight <= 0.0) break;
+      double* ts; int nt = cost_times(o, c->dt, &ts);
+      double wdt = c->weight * (c->dt > 0.0 ? c->dt : 1.0);
+      double Ib[3][3];
+      { const double* I = o->d.robot.inertia;
+        double m9[9] = {I[0], -I[3], -I[4], -I[3], I[1], -I[5], -I[4], -I[5], I[2]};
+        memcpy(Ib, m9, sizeof Ib); }
+      int col0 = varset_col0(o, TOWR_VAR_BASE_ANG, 0);
+      for (int k = 0; k < nt; ++k) {
+        double t = ts[k], R[3][3], w[3], RI[3][3], Iw[3][3], v[3];
+        eu_R_t(&o->euler, t, R); eu_omega(&o->euler, t, w);
+        for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) RI[i][j] = R[i][0] * Ib[0][j] + R[i][1] * Ib[1][j] + R[i][2] * Ib[2][j];
+        for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) Iw[i][j] = RI[i][0] * R[j][0] + RI[i][1] * R[j][1] + RI[i][2] * R[j][2];
+        for (int i = 0; i < 3; ++i) v[i] = Iw[i][0] * w[0] + Iw[i][1] * w[1] + Iw[i][2] * w[2];
+        cost += wdt * dot3(v, v);
+        if (!grad || col0 < 0) continue;
+        double m[3], u[3], v2[3];
+        for (int r = 0; r < 3; ++r) m[r] = (2.0 * wdt) * v[r];
+        for (int i = 0; i < 3; ++i) u[i] = R[0][i] * w[0] + R[1][i] * w[1] + R[2][i] * w[2];   /* R^T omega */
+        for (int i = 0; i < 3; ++i) v2[i] = Ib[i][0] * u[0] + Ib[i][1] * u[1] + Ib[i][2] * u[2];
+        spmat Jrv2 = eu_d_rotvec(&o->euler, t, v2, 0), Jrtw = eu_d_rotvec(&o->euler, t, w, 1), Jw = eu_d_angvel(&o->euler, t);
+        int n = Jw.cols;
+        double* ta = (double*)calloc((size_t)(3 * n), sizeof(double));
+        double* tb = (double*)calloc((size_t)(3 * n), sizeof(double));
+        for (int r = 0; r < 3; ++r) {
+          for (int q = 0; q < Jrtw.r[r].n; ++q) ta[r * n + Jrtw.r[r].e[q].col] += Jrtw.r[r].e[q].val;
+          for (int q = 0; q < Jw.r[r].n; ++q) tb[r * n + Jw.r[r].e[q].col] += Jw.r[r].e[q].val;
+        }
+        grad_add_rows(grad, col0, &Jrv2, m);
+        for (int col = 0; col < n; ++col) {
+          double tbc[3], tu[3], it[3], j2[3];
+          for (int i = 0; i < 3; ++i) tbc[i] = R[0][i] * tb[0 * n + col] + R[1][i] * tb[1 * n + col] + R[2][i] * tb[2 * n + col];
+          for (int i = 0; i < 3; ++i) tu[i] = ta[i * n + col] + tbc[i];
+          for (int i = 0; i < 3; ++i) it[i] = Ib[i][0] * tu[0] + Ib[i][1] * tu[1] + Ib[i][2] * tu[2];
+          for (int i = 0; i < 3; ++i) j2[i] = R[i][0] * it[0] + R[i][1] * it[1] + R[i][2] * it[2];
+          double g2 = m[0] * j2[0] + m[1] * j2[1] + m[2] * j2[2];
+          if (g2 != 0.0) grad[col0 + col] += g2;
+        }
+        free(ta); free(tb); sp_free(&Jrv2); sp_free(&Jrtw); sp_free(&Jw);
+      }
+      free(ts);
+      break;
+    }
+    case TOWR_COST_EE_BASE_POS: {   /* ee_base_pos_cost.cc:57-162 */
+      if (c->weight <= 0.0) break;
+      double* ts; int nt = cost_times(o, c->dt, &ts);
+      int ee = c->ee;
+      for (int k = 0; k < nt; ++k) {
+        double t = ts[k];
+        if (pd_is_contact(o->pd[ee], t)) continue;   /* only during swing */
+        double b[3][3], pe[3][3], R[3][3], rW[3], pB[3], e[3], m[3];
+        spline_point(o->s_lin, t, b); spline_point(o->s_motion[ee], t, pe); eu_R_t(&o->euler, t, R);
+        for (int q = 0; q < 3; ++q) rW[q] = pe[kPos][q] - b[kPos][q];
+        for (int i = 0; i < 3; ++i) pB[i] = R[0][i] * rW[0] + R[1][i] * rW[1] + R[2][i] * rW[2];
+        for (int i = 0; i < 3; ++i) e[i] = pB[i] - c->p[i];
+        cost += c->weight * dot3(e, e);
+        if (!grad) continue;
+        for (int i = 0; i < 3; ++i) m[i] = (2.0 * c->weight) * e[i];
+        double mW[3], mWn[3];
+        for (int j = 0; j < 3; ++j) { mW[j] = m[0] * R[j][0] + m[1] * R[j][1] + m[2] * R[j][2]; }   /* m * b_R_w */
+        for (int j = 0; j < 3; ++j) { double nm0 = -m[0], nm1 = -m[1], nm2 = -m[2]; mWn[j] = nm0 * R[j][0] + nm1 * R[j][1] + nm2 * R[j][2]; }
+        spmat J = spline_jac(o->s_motion[ee], t, kPos); grad_add_rows(grad, varset_col0(o, TOWR_VAR_EE_MOTION, ee), &J, mW); sp_free(&J);
+        J = spline_jac(o->s_lin, t, kPos); grad_add_rows(grad, varset_col0(o, TOWR_VAR_BASE_LIN, 0), &J, mWn); sp_free(&J);
+        J = eu_d_rotvec(&o->euler, t, rW, 1); grad_add_rows(grad, varset_col0(o, TOWR_VAR_BASE_ANG, 0), &J, m); sp_free(&J);
+        /* the schedule block is omitted by the reference (:150-154) */
+      }
+      free(ts);
+      break;
+    }
+  }
+  return cost;
+}
+
+int oracle_eval_f(oracle_t* o, const double* x, double* f) {
+  set_variables(o, x);
+  double s = 0.0;
+  for (int i = 0; i < o->d.n_costs; ++i) s += cost_term(o, &o->d.costs[i], NULL);
+  *f = s;
+  return 0;
+}
+
+int oracle_eval_grad_f(oracle_t* o, const double* x, double* grad) {
+  set_variables(o, x);
+  for (int j = 0; j < o->n; ++j) grad[j] = 0.0;
+  for (int i = 0; i < o->d.n_costs; ++i) cost_term(o, &o->d.costs[i], grad);
+  return 0;
 }
 
 int oracle_sizes(oracle_t* o, int* n, int* m) { *n = o->n; *m = o->m; return 0; }

@@ -37,6 +37,9 @@ int       oracle_eval_g(oracle_t* o, const double* x, double* g);
 long      oracle_eval_jac(oracle_t* o, const double* x, long cap, int* rows, int* cols, double* vals);
 /* ifopt Problem::EvalNonzerosOfJacobian: values in the pattern order at x (nnz returned).      */
 long      oracle_eval_jac_values(oracle_t* o, const double* x, double* values);
+/* objective (sum of the cost terms) and its dense gradient */
+int       oracle_eval_f(oracle_t* o, const double* x, double* f);
+int       oracle_eval_grad_f(oracle_t* o, const double* x, double* grad);
 /* constraint-set row ranges: row0 / n_rows of constraint i                                      */
 int       oracle_constraint_rows(oracle_t* o, int i, int* row0, int* n_rows);
 int       oracle_varset_cols(oracle_t* o, int i, int* col0, int* n_cols);

@@ -90,3 +90,36 @@ def _anymal_baserom():
     f.params_.constraints_.append(F.Parameters.BaseRom)
     f.params_.dt_constraint_force_ = 0.0   # node-based ForceConstraint instead of the discretised one
     return f.to_desc()
+
+
+def _with_costs(f, costs=None, ee_base_pos=True, torque_weight=None):
+    """Cost terms of NlpFormulation::GetCosts (nlp_formulation.cc:604-680) on a formulation."""
+    P = f.params_
+    P.costs_ = costs if costs is not None else [(F.Parameters.ForcesCostID, 1e-3), (F.Parameters.EEMotionCostID, 0.5),
+                                                 (F.Parameters.EnergyCostID, 1e-4), (F.Parameters.AngMomCostID, 0.1)]
+    P.enable_swing_ee_base_pos_tracking = ee_base_pos
+    if torque_weight is not None:
+        P.energy_cost_torque_weight_ = torque_weight
+    return f
+
+
+def cost_descs():
+    """name -> ProblemDesc with cost terms (eval_f / eval_grad_f)."""
+    C = F.Parameters
+    return {
+        "anymal_all_costs": _with_costs(F.anymal_trot()).to_desc(),
+        "anymal_stairs_gaitopt_costs": _with_costs(F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.StairsID),
+                                                                 optimize_timings=True)).to_desc(),
+        "biped_energy_angmom": _with_costs(F.biped_walk(), costs=[(C.EnergyCostID, 1e-3), (C.AngMomCostID, 1.0)],
+                                           ee_base_pos=True, torque_weight=0.0).to_desc(),
+        "biped_gaitopt_costs": _with_costs(_gaitopt_f(F.biped_walk()), torque_weight=2.0).to_desc(),
+        "hopper_forces_motion": _with_costs(F.monoped_hopper(), costs=[(C.ForcesCostID, 1.0), (C.EEMotionCostID, 1.0)],
+                                            ee_base_pos=False).to_desc(),
+        "anymal_slope_yaw_costs": _with_costs(F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.SlopeID),
+                                                            goal=(1.8, 0.3, 0.0), goal_yaw=0.3)).to_desc(),
+    }
+
+
+def _gaitopt_f(f):
+    f.params_.OptimizePhaseDurations()
+    return f

@@ -49,6 +49,32 @@ extern "C" int emu_eval(const towr_problem_desc_t* d, const double* x, double* g
   return 0;
 }
 
+// objective and dense gradient through engine_math.h's cost items (host instantiation)
+namespace {
+struct GradEmit {
+  double* grad; double f = 0.0;
+  void operator()(int, int col, double v, bool pres) { if (pres && col >= 0) grad[col] += v; }
+};
+}
+extern "C" int emu_cost(const towr_problem_desc_t* d, const double* x, double* f, double* grad, char* err, int errlen) {
+  Layout L; std::string e;
+  int rc = build_layout(*d, L, e);
+  if (rc) { if (err) std::snprintf(err, errlen, "%s", e.c_str()); return rc; }
+  std::memset(grad, 0, sizeof(double) * L.n);
+  Ctx c{};
+  c.x = x; c.nodecol = L.nodecol.data(); c.spl = L.spl.data(); c.dur = L.dur.data();
+  c.ter = &L.terrain; c.rb = L.rb; c.fdisc_motion = L.fdisc_motion;
+  c.gait = L.gait; c.pinfo = L.pinfo.data(); c.pcols = L.pcols.data(); c.sched = L.sched.data();
+  c.eelin = L.eelin.data();
+  GradEmit em{grad};
+  for (const CostItem& it : L.cost_items) {
+    c.seg = it.seg >= 0 ? L.segs.data() + (size_t)it.seg * L.spl.size() : nullptr;
+    eval_cost_item(c, it, em);
+  }
+  *f = em.f;
+  return 0;
+}
+
 // layout statistics per item type (tiles, lanes used, candidates per wave, values per tile)
 extern "C" int emu_stats(const towr_problem_desc_t* d) {
   Layout L; std::string e;

@@ -45,3 +45,17 @@ def assert_close(g_ref, g, rows_ref, v_ref, v, m, what="", cols_ref=None):
         msg.append(f"{len(bad_v)} J mismatches, first nz {i} (row {rows_ref[i]}): ref {v_ref[i]!r} got {v[i]!r}; "
                    f"largest at nz {j} (row {rows_ref[j]}): ref {v_ref[j]!r} got {v[j]!r}")
     assert not msg, what + ": " + "; ".join(msg)
+
+
+def assert_cost_close(f_ref, f, g_ref, g, what=""):
+    """Objective and dense gradient: the value tolerance above with the floor 1e-12 * max(1, |f|) for f
+    and 1e-12 * max(1, max |grad|) for the gradient (its entries are sums over many samples whose
+    order differs: the device accumulates them with atomics)."""
+    assert abs(f - f_ref) <= REL * max(abs(f), abs(f_ref)) + ABS * max(1.0, abs(f_ref)), \
+        f"{what}: f ref {f_ref!r} got {f!r}"
+    scale = max(1.0, float(np.max(np.abs(g_ref))) if len(g_ref) else 1.0)
+    tol = REL * np.maximum(np.abs(g_ref), np.abs(g)) + ABS * scale
+    bad = np.flatnonzero(np.abs(g_ref - g) > tol)
+    if len(bad):
+        j = bad[np.argmax(np.abs(g_ref[bad] - g[bad]))]
+        raise AssertionError(f"{what}: {len(bad)} gradient mismatches, largest at {j}: ref {g_ref[j]!r} got {g[j]!r}")

@@ -1,0 +1,140 @@
+"""Cost terms (IpoptAdapter::eval_f / eval_grad_f) on the CPU:
+  * the oracle's gradient against central differences of its objective (self-consistency pin);
+  * the reference quirk EEBasePosCost adds no schedule block (ee_base_pos_cost.cc:150-154);
+  * engine_math.h's cost items through the test-only host emulation against the oracle;
+  * description validation of cost terms at handle creation (layout-only handle, no GPU).
+Parity of the objective is "pinned by FD and the oracle only": the reference's own tests hold no
+cost fixtures."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle.oracle import Oracle
+from tests.configs import cost_descs, _with_costs
+from tests.parity import assert_cost_close
+from towr2025_amd import _capi as capi
+from towr2025_amd import formulation as F
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+COSTS = cost_descs()
+D = C.POINTER(C.c_double)
+
+
+def _fd_grad(o, x, cols, h_rel=1e-4):
+    out = np.zeros(len(cols))
+    for k, j in enumerate(cols):
+        h = h_rel * max(1.0, abs(x[j]))
+        xp, xm = x.copy(), x.copy()
+        xp[j] += h
+        xm[j] -= h
+        out[k] = (o.eval_f(xp) - o.eval_f(xm)) / (2 * h)
+    return out
+
+
+def _sched_cols(o, desc):
+    cols = []
+    for i, (c0, n) in enumerate(o.varset_cols()):
+        if desc.varsets[i].kind == capi.VAR_EE_SCHEDULE:
+            cols += list(range(c0, c0 + n))
+    return cols
+
+
+@pytest.mark.parametrize("name", sorted(COSTS))
+def test_oracle_gradient_matches_fd(name):
+    desc = COSTS[name]
+    o = Oracle(desc)
+    x = o.initial_x() + 0.02 * np.random.default_rng(5).standard_normal(o.n)
+    g = o.eval_grad_f(x)
+    skip = set(_sched_cols(o, desc)) if desc.optimize_timings else set()   # EEBasePos quirk: below
+    cols = [j for j in range(0, o.n, 2) if j not in skip]
+    fd = _fd_grad(o, x, cols)
+    # central differences with h = 1e-4: truncation O(h^2), cancellation ~ eps |f| / h
+    noise = 8 * np.finfo(float).eps * abs(o.eval_f(x)) / 1e-4
+    err = np.abs(fd - g[cols]) / (np.maximum(1.0, np.abs(g[cols])) + noise)
+    assert err.max() < 2e-5, f"col {cols[err.argmax()]}: FD {fd[err.argmax()]} grad {g[cols][err.argmax()]}"
+
+
+def test_gait_schedule_gradient_and_eebase_quirk():
+    """With phase-duration optimisation: the schedule gradient of Energy/AngularMomentum/Node costs is
+    FD-consistent; EEBasePosCost's is missing exactly as in the reference (no schedule block)."""
+    f = _with_costs(F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.StairsID), optimize_timings=True),
+                    ee_base_pos=False)
+    desc = f.to_desc()
+    o = Oracle(desc)
+    x = o.initial_x() + 0.01 * np.random.default_rng(3).standard_normal(o.n)
+    sc = _sched_cols(o, desc)
+    assert sc
+    g = o.eval_grad_f(x)
+    fd = _fd_grad(o, x, sc, h_rel=1e-6)   # durations enter nonlinearly; f is O(100) here
+    assert np.max(np.abs(fd - g[sc]) / np.maximum(1.0, np.abs(g[sc]))) < 5e-5
+    # EEBasePos only: its true schedule derivative is not zero, its reported one is
+    f2 = _with_costs(F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.StairsID), optimize_timings=True),
+                     costs=[], ee_base_pos=True)
+    f2.params_.swing_ee_base_pos_tracking_weight_ = 10.0
+    d2 = f2.to_desc()
+    o2 = Oracle(d2)
+    g2 = o2.eval_grad_f(x)
+    assert np.all(g2[sc] == 0.0)
+    assert np.max(np.abs(_fd_grad(o2, x, sc, h_rel=1e-6))) > 1e-6
+
+
+def test_no_costs_is_zero():
+    desc = F.anymal_trot().to_desc()
+    o = Oracle(desc)
+    x = o.initial_x()
+    assert o.eval_f(x) == 0.0
+    assert not np.any(o.eval_grad_f(x))
+
+
+@pytest.fixture(scope="module")
+def emu():
+    lib = os.path.join(HERE, "host_emu", "build", "libemu.so")
+    if not os.path.exists(lib):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "host_emu")])
+    L = C.CDLL(lib)
+    L.emu_cost.argtypes = [C.POINTER(capi.ProblemDesc), D, D, D, C.c_char_p, C.c_int]
+    return L
+
+
+@pytest.mark.parametrize("name", sorted(COSTS))
+def test_emulated_costs_match_oracle(emu, name):
+    desc = COSTS[name]
+    o = Oracle(desc)
+    for seed in (0, 1, 2):
+        x = o.initial_x()
+        if seed:
+            x = x + 0.05 * np.random.default_rng(seed).standard_normal(o.n)
+        f, g = C.c_double(), np.zeros(o.n)
+        err = C.create_string_buffer(256)
+        assert emu.emu_cost(C.byref(desc), x.ctypes.data_as(D), C.byref(f), g.ctypes.data_as(D), err, 256) == 0, err.value
+        assert_cost_close(o.eval_f(x), f.value, o.eval_grad_f(x), g, f"{name} seed {seed}")
+
+
+def _create_layout(desc):
+    lib = capi.load_library()
+    h = C.c_void_p()
+    rc = lib.towr_gpu_create(C.byref(desc), -1, C.byref(h))
+    if rc == 0:
+        lib.towr_gpu_destroy(h)
+    return rc, lib.towr_gpu_last_error(None).decode()
+
+
+@pytest.mark.parametrize("field,value", [("kind", 9), ("ip0", 6), ("ip1", 2), ("ip2", 3), ("ee", 7)])
+def test_bad_cost_terms_rejected(field, value):
+    desc = COSTS["anymal_all_costs"]
+    d = capi.ProblemDesc.from_buffer_copy(desc)
+    c = d.costs[0]   # a NodeCost (forces)
+    assert c.kind == capi.COST_NODE
+    if field == "kind":
+        c.kind = value
+    elif field == "ee":
+        c.ee = value
+    else:
+        c.ip[int(field[2])] = value
+    rc, msg = _create_layout(d)
+    assert rc == capi.TOWR_ERR_INVALID, msg
+    rc, _ = _create_layout(desc)
+    assert rc == 0

@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 MAX_EE = 4
 MAX_PHASES = 48
 MAX_VARSETS = 2 + 5 * MAX_EE
@@ -67,6 +67,16 @@ class InitDesc(C.Structure):
                 ("ee_p0", (C.c_double * 3) * MAX_EE), ("ee_p1", (C.c_double * 3) * MAX_EE)]
 
 
+# towr_cost_kind
+COST_NODE, COST_ENERGY, COST_ANG_MOMENTUM, COST_EE_BASE_POS = range(4)
+MAX_COSTS = 128
+
+
+class CostDesc(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("ee", C.c_int32), ("weight", C.c_double), ("dt", C.c_double),
+                ("p", C.c_double * 4), ("ip", C.c_int32 * 4)]
+
+
 class ProblemDesc(C.Structure):
     _fields_ = [("abi_version", C.c_int32), ("angular_rep", C.c_int32),
                 ("robot", Robot), ("terrain", Terrain),
@@ -81,7 +91,9 @@ class ProblemDesc(C.Structure):
                 ("n_varsets", C.c_int32), ("n_constraints", C.c_int32),
                 ("varsets", VarSetDesc * MAX_VARSETS),
                 ("constraints", ConstraintDesc * MAX_CONSTRAINTS),
-                ("init", InitDesc)]
+                ("init", InitDesc),
+                ("n_costs", C.c_int32), ("reserved_costs", C.c_int32),
+                ("costs", CostDesc * MAX_COSTS)]
 
 
 # symbol table of include/towr_gpu.h: name -> (restype, argtypes)
@@ -103,6 +115,10 @@ SYMBOLS = {
     "towr_gpu_eval_g": (C.c_int, [_HANDLE, _DP, _DP]),
     "towr_gpu_eval_jac_values": (C.c_int, [_HANDLE, _DP, _DP]),
     "towr_gpu_eval_g_jac": (C.c_int, [_HANDLE, _DP, _DP, _DP]),
+    "towr_gpu_eval_f": (C.c_int, [_HANDLE, _DP, _DP]),
+    "towr_gpu_eval_grad_f": (C.c_int, [_HANDLE, _DP, _DP]),
+    "towr_gpu_eval_cost_batch_device": (C.c_int, [_HANDLE, C.c_int32, C.c_void_p, C.c_int64, C.c_void_p,
+                                                   C.c_void_p, C.c_int64, C.c_void_p]),
     "towr_gpu_set_batch_terrain": (C.c_int, [_HANDLE, C.c_int32, C.POINTER(Terrain)]),
     "towr_gpu_eval_batch_device": (C.c_int, [_HANDLE, C.c_int32, C.c_void_p, C.c_int64,
                                               C.c_void_p, C.c_int64, C.c_void_p, C.c_int64,

@@ -1123,6 +1123,168 @@ TG_HD void eval_tdur(const Ctx& c, const ItemDesc& it, Emit& em) {
   for (int i = 0; i < si.n_phases - 1; ++i) em(it.row0, si.col0 + i, 1.0, true);
 }
 
+// ----------------------------------------------------------------------------------------------
+// cost terms (NlpFormulation::GetCosts, nlp_formulation.cc:604-680; towr/src/costs/)
+//   eval_f = sum of every term's GetCost; eval_grad_f = the dense sum of their gradients.
+// A cost work item is one (term, sample time[, endeffector]) of a time-sampled cost, or one whole
+// NodeCost. It adds its value to em.f and its gradient entries with em(0, col, value, present):
+// the same emitter interface as the constraint items, so the spline chain rules (emit_dim, the
+// PhaseSpline full pattern, sched_jac) are shared with the constraints.
+// ----------------------------------------------------------------------------------------------
+enum CostType { CT_NODE = 0, CT_ENERGY = 1, CT_ANGMOM = 2, CT_EEBP = 3, CT_COUNT = 4 };
+
+struct CostItem {
+  int32_t type, ee, seg, s;        // seg: segment-table row of the sample time; s: spline (CT_NODE)
+  int32_t deriv, dim;              // CT_NODE: node value penalised
+  int32_t contact0, reserved;      // CT_EEBP: ee in contact at start (swing test under gait optimisation)
+  double t, w, wdt, tw;            // sample time, weight, weight * dt, EnergyCost torque weight
+  double p[3], pad;                // CT_EEBP: reference ee position in base frame
+};
+
+// NodeCost (node_cost.cc:55-79): sum over nodes of w * value^2; d/dx_i = sum over the node values
+// variable i sets of 2 w value (a stance position variable sets two nodes: counted twice)
+template <class Emit>
+TG_HD void cost_node(const Ctx& c, const CostItem& it, Emit& em) {
+  const int nn = c.spl[it.s].n_polys + 1;
+  for (int id = 0; id < nn; ++id) {
+    const int col = node_col(c, it.s, id, it.deriv, it.dim);
+    const double v = xval(c, col);
+    em.f += it.w * (v * v);
+    em(0, col, it.w * 2.0 * v, col >= 0);
+  }
+}
+
+// EnergyCost sample (energy_cost.cc:57-152) of one endeffector: w dt (|f|^2 + tw |tau|^2)
+template <class Emit>
+TG_HD void cost_energy(const Ctx& c, const CostItem& it, Emit& em) {
+  const int ee = it.ee;
+  SplinePt F, Tq;
+  spline_eval(c, sp_force(ee), it.t, F);
+  spline_eval(c, sp_torque(ee), it.t, Tq);
+  em.f += it.wdt * (dot3(F.p, F.p) + it.tw * dot3(Tq.p, Tq.p));
+  double mf[3], mt[3], H[4];
+  for (int r = 0; r < 3; ++r) { mf[r] = (2.0 * it.wdt) * F.p[r]; mt[r] = (2.0 * it.wdt * it.tw) * Tq.p[r]; }
+  spline_basis(F, kPos, H);
+  for (int e = 0; e < 3; ++e) emit_dim(c, em, 0, sp_force(ee), F, H, e, mf[e]);
+  if (it.tw != 0.0) {
+    spline_basis(Tq, kPos, H);
+    for (int e = 0; e < 3; ++e) emit_dim(c, em, 0, sp_torque(ee), Tq, H, e, mt[e]);
+  }
+  if (c.gait) {   // d pos / d schedule of both splines (energy_cost.cc:131-150)
+    SchedJac Jf, Jt;
+    sched_jac(c, sp_force(ee), it.t, F, Jf);
+    if (it.tw != 0.0) sched_jac(c, sp_torque(ee), it.t, Tq, Jt);
+    for (int col = 0; col < Jf.n - 1; ++col) {
+      double v = mf[0] * sched_val(Jf, 0, col) + mf[1] * sched_val(Jf, 1, col) + mf[2] * sched_val(Jf, 2, col);
+      if (it.tw != 0.0) v += mt[0] * sched_val(Jt, 0, col) + mt[1] * sched_val(Jt, 1, col) + mt[2] * sched_val(Jt, 2, col);
+      em(0, Jf.col0 + col, v, true);
+    }
+  }
+}
+
+// AngularMomentumCost sample (angular_momentum_cost.cc:67-208): w dt |L|^2, L = R I_b R^T omega,
+// omega = M(theta) theta_dot. d L / d theta_e = dR I_b R^T w + R I_b dR^T w + I_w dM_e theta_dot;
+// d L / d theta_dot_e = I_w M[:, e]; chained through the Euler spline's position / velocity basis.
+template <class Emit>
+TG_HD void cost_angmom(const Ctx& c, const CostItem& it, Emit& em) {
+  SplinePt A;
+  spline_eval(c, SP_BASE_ANG, it.t, A);
+  const Trig q = trig(A.p);
+  const double sy = q.sy, cy = q.cy, sz = q.sz, cz = q.cz, xd = A.v[0], yd = A.v[1];
+  double R[3][3]; euler_R(q, R);
+  const double M0[3] = {cy * cz, cy * sz, -sy}, M1[3] = {-sz, cz, 0.0};
+  double w[3];
+  for (int i = 0; i < 3; ++i) w[i] = M0[i] * xd + M1[i] * yd + (i == 2 ? A.v[2] : 0.0);
+  double RI[3][3], Iw[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) RI[i][j] = R[i][0] * c.rb.Ib[0 * 3 + j] + R[i][1] * c.rb.Ib[1 * 3 + j] + R[i][2] * c.rb.Ib[2 * 3 + j];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) Iw[i][j] = RI[i][0] * R[j][0] + RI[i][1] * R[j][1] + RI[i][2] * R[j][2];
+  double L[3]; mat3_vec(Iw, w, L);
+  em.f += it.wdt * dot3(L, L);
+  double m[3], u[3];
+  for (int r = 0; r < 3; ++r) m[r] = (2.0 * it.wdt) * L[r];
+  for (int j = 0; j < 3; ++j) u[j] = R[0][j] * w[0] + R[1][j] * w[1] + R[2][j] * w[2];   // R^T w
+  double Hp[4], Hv[4];
+  spline_basis(A, kPos, Hp);
+  spline_basis(A, kVel, Hv);
+#pragma unroll 1
+  for (int e = 0; e < 3; ++e) {
+    double dR[3][3]; euler_dR_axis(q, e, dR);
+    double dw[3] = {0.0, 0.0, 0.0};   // dM_e theta_dot (GetDerivMwrtNodes, euler_converter.cc:168-198)
+    if (e == 1) { dw[0] = -sy * cz * xd; dw[1] = -sy * sz * xd; dw[2] = -cy * xd; }
+    else if (e == 2) { dw[0] = -cy * sz * xd - cz * yd; dw[1] = cy * cz * xd - sz * yd; }
+    double v[3], dRI[3][3], t1[3], t2[3];
+    for (int j = 0; j < 3; ++j) v[j] = dR[0][j] * w[0] + dR[1][j] * w[1] + dR[2][j] * w[2];   // dR^T w
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) dRI[i][j] = dR[i][0] * c.rb.Ib[0 * 3 + j] + dR[i][1] * c.rb.Ib[1 * 3 + j] + dR[i][2] * c.rb.Ib[2 * 3 + j];
+    mat3_vec(Iw, dw, t1);
+    double sp = 0.0;
+    for (int i = 0; i < 3; ++i)
+      sp += m[i] * ((dRI[i][0] * u[0] + dRI[i][1] * u[1] + dRI[i][2] * u[2]) + (RI[i][0] * v[0] + RI[i][1] * v[1] + RI[i][2] * v[2]) + t1[i]);
+    const double Me[3] = {e == 0 ? M0[0] : e == 1 ? M1[0] : 0.0, e == 0 ? M0[1] : e == 1 ? M1[1] : 0.0, e == 0 ? M0[2] : e == 1 ? M1[2] : 1.0};
+    mat3_vec(Iw, Me, t2);
+    const double sv = dot3(m, t2);
+    for (int bb = 0; bb < 4; ++bb) em(0, basis_col(c, SP_BASE_ANG, A.poly, bb, e), sp * Hp[bb] + sv * Hv[bb], true);
+  }
+}
+
+// PhaseDurations::IsContactPhase (phase_durations.cc:120-124) over the optimised durations
+TG_HD bool sched_is_contact(const Ctx& c, int ee, bool contact0, double t) {
+  const SchedInfo si = c.sched[ee];
+  const double last = last_phase_duration(c, si), eps = 1e-10;
+  double acc = 0.0;
+  int id = si.n_phases - 1;
+  for (int ph = 0; ph < si.n_phases; ++ph) {
+    acc += phase_duration(c, si, last, ph);
+    if (acc >= t - eps) { id = ph; break; }
+  }
+  return (id % 2 == 0) ? contact0 : !contact0;
+}
+
+// EEBasePosCost sample (ee_base_pos_cost.cc:57-162), only while the foot swings: w |R^T (p_ee - p_b) - p_ref|^2.
+// The reference adds no schedule block (:150-154); neither does this engine.
+template <class Emit>
+TG_HD void cost_eebp(const Ctx& c, const CostItem& it, Emit& em) {
+  const int ee = it.ee;
+  if (c.gait && sched_is_contact(c, ee, it.contact0 != 0, it.t)) return;   // fixed gait: filtered at build
+  SplinePt L, A, P;
+  spline_eval(c, SP_BASE_LIN, it.t, L);
+  spline_eval(c, SP_BASE_ANG, it.t, A);
+  spline_eval(c, sp_motion(ee), it.t, P);
+  const Trig q = trig(A.p);
+  double R[3][3]; euler_R(q, R);
+  const double rW[3] = {P.p[0] - L.p[0], P.p[1] - L.p[1], P.p[2] - L.p[2]};
+  double e3[3], m[3], mW[3];
+  for (int i = 0; i < 3; ++i) e3[i] = (R[0][i] * rW[0] + R[1][i] * rW[1] + R[2][i] * rW[2]) - it.p[i];
+  em.f += it.w * dot3(e3, e3);
+  for (int i = 0; i < 3; ++i) m[i] = (2.0 * it.w) * e3[i];
+  for (int j = 0; j < 3; ++j) mW[j] = m[0] * R[j][0] + m[1] * R[j][1] + m[2] * R[j][2];   // m b_R_w
+  double H[4];
+  spline_basis(P, kPos, H);
+  for (int j = 0; j < 3; ++j) emit_dim(c, em, 0, sp_motion(ee), P, H, j, mW[j]);
+  spline_basis(L, kPos, H);
+  for (int j = 0; j < 3; ++j)
+    for (int bb = 0; bb < 4; ++bb) em(0, basis_col(c, SP_BASE_LIN, L.poly, bb, j), -mW[j] * H[bb], true);
+  spline_basis(A, kPos, H);   // DerivOfRotVecMult(t, r_W, inverse = true)
+  for (int e = 0; e < 3; ++e) {
+    double dR[3][3]; euler_dR_axis(q, e, dR);
+    double s = 0.0;
+    for (int r = 0; r < 3; ++r) s += m[r] * (rW[0] * dR[0][r] + rW[1] * dR[1][r] + rW[2] * dR[2][r]);
+    for (int bb = 0; bb < 4; ++bb) em(0, basis_col(c, SP_BASE_ANG, A.poly, bb, e), s * H[bb], true);
+  }
+}
+
+template <class Emit>
+TG_HD void eval_cost_item(const Ctx& c, const CostItem& it, Emit& em) {
+  switch (it.type) {
+    case CT_NODE: cost_node(c, it, em); break;
+    case CT_ENERGY: cost_energy(c, it, em); break;
+    case CT_ANGMOM: cost_angmom(c, it, em); break;
+    case CT_EEBP: cost_eebp(c, it, em); break;
+  }
+}
+
 template <class Emit>
 TG_HD void eval_item(const Ctx& c, const ItemDesc& it, Emit& em) {
   switch (it.type) {

@@ -67,6 +67,9 @@ struct Layout {
   std::vector<int32_t> misc_tiles;   // groups of kMiscWaves tile indices (-1 = empty wave)
   int32_t misc_dummy_off = 0, misc_rows_off = 0, misc_stride = 0;   // per-wave LDS layout (doubles)
   int64_t misc_bytes = 0;
+  // cost terms (eval_f / eval_grad_f): work items sorted by CostType, one block per problem
+  std::vector<CostItem> cost_items;
+  int32_t cost_type0[CT_COUNT + 1] = {};
 };
 
 constexpr int kMiscWaves = 4;

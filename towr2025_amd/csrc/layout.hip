@@ -278,6 +278,106 @@ int item_rows(int type) {
   return 0;
 }
 
+// one segment-table row: the reference's GetLocalTime scan of every spline at time t
+int push_seg_row(Layout& L, double t) {
+  const int nspl = (int)L.spl.size();
+  const int row = (int)(L.segs.size() / nspl);
+  for (int sp = 0; sp < nspl; ++sp) {
+    SegRec r{};
+    r.poly = seg_lookup(L.dur.data() + L.spl[sp].dur_off, L.spl[sp].n_polys, t, &r.tl);
+    r.T = L.dur[L.spl[sp].dur_off + r.poly];
+    hermite_dpos(r.T, r.tl, r.H[kPos]);   // polynomial.cc:135-234, batch-invariant
+    hermite_dvel(r.T, r.tl, r.H[kVel]);
+    hermite_dacc(r.T, r.tl, r.H[kAcc]);
+    for (int bb = 0; bb < 4; ++bb)
+      for (int e = 0; e < 3; ++e) {
+        const int32_t col = L.nodecol[(size_t)(L.spl[sp].node_off + r.poly + (bb >> 1)) * 6 + (bb & 1) * 3 + e];
+        r.col[bb][e] = col >= 0 ? col : L.n;
+      }
+    L.segs.push_back(r);
+  }
+  return row;
+}
+
+// cost work items (NlpFormulation::GetCosts, nlp_formulation.cc:604-680), grouped by type
+int build_costs(const towr_problem_desc_t& d, const std::vector<double>& base_d, Layout& L, std::string& err) {
+  const int E = d.robot.n_ee;
+  if (d.n_costs < 0 || d.n_costs > TOWR_MAX_COSTS) { err = "n_costs out of range"; return TOWR_ERR_INVALID; }
+  // GetSampleTimes (energy_cost.cc:41-55 and its copies): 0, dt, ... while t <= T + 1e-9, accumulated,
+  // T = base_linear_->GetTotalTime() (the sum of the base polynomial durations)
+  double Tb = 0.0;
+  for (double v : base_d) Tb += v;
+  auto sample_times = [&](double dt) {
+    std::vector<double> ts;
+    if (dt <= 0.0) { ts.push_back(0.0); ts.push_back(Tb); }
+    else for (double t = 0.0; t <= Tb + 1e-9; t += dt) ts.push_back(t);
+    return ts;
+  };
+  std::map<double, int> rows;   // one segment row per distinct sample time
+  auto seg_of = [&](double t) {
+    auto f = rows.find(t);
+    if (f != rows.end()) return f->second;
+    const int r = push_seg_row(L, t);
+    rows[t] = r;
+    return r;
+  };
+  std::vector<CostItem> items;
+  for (int i = 0; i < d.n_costs; ++i) {
+    const towr_cost_t& c = d.costs[i];
+    CostItem it{};
+    it.type = -1; it.seg = -1; it.w = c.weight;
+    it.wdt = c.weight * (c.dt > 0.0 ? c.dt : 1.0);
+    switch (c.kind) {
+      case TOWR_COST_NODE: {   // node_cost.cc:36-79
+        const int vk = c.ip[0];
+        const bool base = vk == TOWR_VAR_BASE_LIN || vk == TOWR_VAR_BASE_ANG;
+        if (vk < TOWR_VAR_BASE_LIN || vk > TOWR_VAR_EE_TORQUE || c.ip[1] < 0 || c.ip[1] > 1 || c.ip[2] < 0 || c.ip[2] > 2 ||
+            (!base && (c.ee < 0 || c.ee >= E))) { err = "bad NodeCost term"; return TOWR_ERR_INVALID; }
+        it.type = CT_NODE; it.ee = base ? 0 : c.ee;
+        it.s = vk == TOWR_VAR_BASE_LIN ? 0 : vk == TOWR_VAR_BASE_ANG ? 1 : 2 + 4 * c.ee + (vk - TOWR_VAR_EE_MOTION);
+        it.deriv = c.ip[1]; it.dim = c.ip[2];
+        items.push_back(it);
+        break;
+      }
+      case TOWR_COST_ENERGY:   // energy_cost.cc:57-152: one item per (sample, ee)
+        if (c.weight <= 0.0) break;
+        it.type = CT_ENERGY; it.tw = c.p[0];
+        for (double t : sample_times(c.dt))
+          for (int ee = 0; ee < E; ++ee) { it.t = t; it.seg = seg_of(t); it.ee = ee; items.push_back(it); }
+        break;
+      case TOWR_COST_ANG_MOMENTUM:   // angular_momentum_cost.cc:67-208
+        if (c.weight <= 0.0) break;
+        it.type = CT_ANGMOM;
+        for (double t : sample_times(c.dt)) { it.t = t; it.seg = seg_of(t); items.push_back(it); }
+        break;
+      case TOWR_COST_EE_BASE_POS: {   // ee_base_pos_cost.cc:57-162: swing samples only
+        if (c.ee < 0 || c.ee >= E) { err = "bad EEBasePosCost endeffector"; return TOWR_ERR_INVALID; }
+        if (c.weight <= 0.0) break;
+        it.type = CT_EEBP; it.ee = c.ee; it.contact0 = d.contact_at_start[c.ee] != 0;
+        for (int k = 0; k < 3; ++k) it.p[k] = c.p[k];
+        for (double t : sample_times(c.dt)) {
+          if (!L.gait) {   // fixed phase durations: IsContactPhase once, here
+            double tl;
+            const int ph = seg_lookup(d.phase_durations[c.ee], d.n_phases[c.ee], t, &tl);
+            if ((ph % 2 == 0) == (it.contact0 != 0)) continue;
+          }
+          it.t = t; it.seg = seg_of(t); items.push_back(it);
+        }
+        break;
+      }
+      default: err = "unknown cost kind"; return TOWR_ERR_INVALID;
+    }
+  }
+  std::stable_sort(items.begin(), items.end(), [](const CostItem& a, const CostItem& b) { return a.type < b.type; });
+  L.cost_items.swap(items);
+  for (int t = 0; t <= CT_COUNT; ++t) {
+    int k = 0;
+    while (k < (int)L.cost_items.size() && L.cost_items[k].type < t) ++k;
+    L.cost_type0[t] = k;
+  }
+  return TOWR_OK;
+}
+
 }  // namespace
 
 int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
@@ -509,7 +609,6 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
 
   // ---- segment table: the reference's GetLocalTime scan for every (timed instance, spline)
   {
-    const int nspl = (int)L.spl.size();
     L.segs.clear();
     int last_inst = -1, last_row = -1;
     for (size_t q = 0; q < L.items.size(); ++q) {
@@ -519,25 +618,14 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
       if (!timed) { it.seg = -1; continue; }
       if (item_inst[q] != last_inst) {
         last_inst = item_inst[q];
-        last_row = (int)(L.segs.size() / nspl);
-        for (int sp = 0; sp < nspl; ++sp) {
-          SegRec r{};
-          r.poly = seg_lookup(L.dur.data() + L.spl[sp].dur_off, L.spl[sp].n_polys, it.t, &r.tl);
-          r.T = L.dur[L.spl[sp].dur_off + r.poly];
-          hermite_dpos(r.T, r.tl, r.H[kPos]);   // polynomial.cc:135-234, batch-invariant
-          hermite_dvel(r.T, r.tl, r.H[kVel]);
-          hermite_dacc(r.T, r.tl, r.H[kAcc]);
-          for (int bb = 0; bb < 4; ++bb)
-            for (int e = 0; e < 3; ++e) {
-              const int32_t col = L.nodecol[(size_t)(L.spl[sp].node_off + r.poly + (bb >> 1)) * 6 + (bb & 1) * 3 + e];
-              r.col[bb][e] = col >= 0 ? col : L.n;
-            }
-          L.segs.push_back(r);
-        }
+        last_row = push_seg_row(L, it.t);
       }
       it.seg = last_row;
     }
   }
+
+  // ---- cost terms (their sample times append rows to the segment table)
+  if (int rc = build_costs(d, base_d, L, err)) return rc;
 
   // ---- structure pass at x0: candidate (row, col) of every item
   std::vector<int32_t> crow, ccol; std::vector<uint8_t> cpres;

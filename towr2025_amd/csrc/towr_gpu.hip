@@ -54,6 +54,10 @@ struct KParams {
   const int32_t* misc_tiles;      // merged small-kind launch: kMiscWaves tile ids per group
   int32_t misc_stride, misc_rows_off;
   RobotC rb;
+  const CostItem* citems;         // cost launch: work items, objective and gradient outputs
+  int32_t n_citems, lds_red_off;
+  double* F;
+  double* GR; int64_t ldgr;
 };
 
 // Stores candidate j of this lane into the LDS tile at its tile-relative CSR position. Positions
@@ -258,6 +262,63 @@ __global__ void __launch_bounds__(64 * kMiscWaves, 1) towr_misc_kernel(KParams P
     for (int i = lane; i < T.r1 - T.r0; i += 64) __builtin_nontemporal_store(wl[P.misc_rows_off + i], Gb + T.r0 + i);
 }
 
+// Objective and gradient (IpoptAdapter::eval_f / eval_grad_f): one block per problem. The block
+// stages x and the node table in LDS and keeps the problem's dense gradient there; lanes take the
+// cost work items round-robin (grouped by kind, so waves mostly run one path) and add their
+// gradient entries with LDS atomics (ds_add_f64); f is reduced over the block. The gradient then
+// leaves with 16-byte non-temporal stores. The gradient's summation order is not fixed (atomics),
+// so it is reproducible to rounding only; f's order is fixed.
+template <bool GRAD>
+struct CostEmit {
+  double* grad;   // LDS; the dump slot at index n absorbs constant node values
+  double f = 0.0;
+  __device__ __forceinline__ void operator()(int, int col, double v, bool pres) {
+    if constexpr (GRAD)
+      if (pres && v != 0.0) atomicAdd(grad + col, v);
+  }
+};
+
+constexpr int kCostBlock = 256;
+template <bool GAIT, bool GRAD>
+__global__ void __launch_bounds__(kCostBlock, 1) towr_cost_kernel(KParams P) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int b = blockIdx.x;
+  double* gs = smem;                       // [n_pad] gradient (+ dump slot at n)
+  double* xs = smem + P.n_pad;             // [n_pad] x (+ zero slot at n)
+  int32_t* ns = reinterpret_cast<int32_t*>(smem + 2 * P.n_pad);
+  double* red = smem + P.lds_red_off;     // [kCostBlock / 64] per-wave partial objectives
+  stage_x<kCostBlock, true>(P, P.X + (int64_t)b * P.ldx, xs, ns);
+  if constexpr (GRAD)
+    for (int i = threadIdx.x; i < P.n_pad; i += kCostBlock) gs[i] = 0.0;
+  __syncthreads();
+  CostEmit<GRAD> em{gs};
+  Ctx c;
+  c.x = xs; c.nodecol = ns; c.spl = P.spl; c.dur = P.dur;
+  c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
+  c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
+  c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.sched = P.sched; c.eelin = P.eelin;
+  for (int i = threadIdx.x; i < P.n_citems; i += kCostBlock) {
+    const CostItem it = P.citems[i];
+    c.seg = it.seg >= 0 ? P.segs + (int64_t)it.seg * P.n_spl : nullptr;
+    eval_cost_item(c, it, em);
+  }
+  // f: wave butterfly, then the waves' partials in order
+  double f = em.f;
+  for (int o = 32; o > 0; o >>= 1) f += __shfl_xor(f, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = f;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int w = 0; w < kCostBlock / 64; ++w) s += red[w];
+    P.F[b] = s;
+  }
+  if constexpr (GRAD) copy_out(gs, P.GR + (int64_t)b * P.ldgr, P.n, threadIdx.x, kCostBlock);
+}
+const void* cost_kernel_for(bool gait, bool grad) {
+  if (gait) return grad ? reinterpret_cast<const void*>(&towr_cost_kernel<true, true>) : reinterpret_cast<const void*>(&towr_cost_kernel<true, false>);
+  return grad ? reinterpret_cast<const void*>(&towr_cost_kernel<false, true>) : reinterpret_cast<const void*>(&towr_cost_kernel<false, false>);
+}
+
 template <bool GAIT>
 const void* kernel_for_mode(int type) {
   switch (type) {
@@ -297,6 +358,7 @@ struct towr_gpu_handle_s {
   SchedInfo* d_sched = nullptr;
   int32_t* d_misc = nullptr;
   EELinDef* d_eelin = nullptr;
+  CostItem* d_citems = nullptr;
   // fork-join of the per-kind launches (TOWR_GPU_STREAMS = total streams incl. the caller's, 1..4)
   static constexpr int kMaxSide = 3;
   int n_side = 0;
@@ -309,6 +371,7 @@ struct towr_gpu_handle_s {
   double *d_x = nullptr, *d_g = nullptr, *d_v = nullptr;
   double *h_x = nullptr, *h_g = nullptr, *h_v = nullptr;
   int32_t stage_B = 0;
+  double *d_f = nullptr, *d_grad = nullptr;   // host-pointer objective entry points (one problem)
 };
 
 namespace {
@@ -411,6 +474,32 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
   return TOWR_OK;
 }
 
+// LDS of the cost launch: [gradient + dump slot | x + zero slot | node table | wave partials]
+size_t cost_red_off(const Layout& L) { return 2 * (size_t)((L.n + 2) & ~1) + (L.nodecol.size() + 3) / 4 * 2; }
+size_t cost_lds_bytes(const Layout& L) { return sizeof(double) * (cost_red_off(L) + kCostBlock / 64); }
+
+int launch_cost(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* F, double* GR, int64_t ldgr,
+                hipStream_t s, const towr_terrain_t* terrains, int per_problem) {
+  if (B <= 0) return TOWR_OK;
+  const Layout& L = h->L;
+  KParams P{};
+  P.X = X; P.ldx = ldx;
+  P.nodecol = h->d_nodecol; P.spl = h->d_spl; P.dur = h->d_dur;
+  P.segs = h->d_segs; P.n_spl = (int32_t)L.spl.size();
+  P.pinfo = h->d_pinfo; P.pcols = h->d_pcols; P.sched = h->d_sched; P.eelin = h->d_eelin;
+  P.terrains = terrains; P.terrain_per_problem = per_problem;
+  P.B = B;
+  P.n = L.n; P.n_pad = (L.n + 2) & ~1; P.n_nodecol = (int32_t)L.nodecol.size();
+  P.fdisc_motion = L.fdisc_motion; P.rb = L.rb;
+  P.citems = h->d_citems; P.n_citems = (int32_t)L.cost_items.size();
+  P.lds_red_off = (int32_t)cost_red_off(L);
+  P.F = F; P.GR = GR; P.ldgr = ldgr;
+  void* args[] = {&P};
+  HIPCHK(h, hipLaunchKernel(cost_kernel_for(L.gait, GR != nullptr), dim3((unsigned)B), dim3(kCostBlock), args,
+                            cost_lds_bytes(L), s));
+  return TOWR_OK;
+}
+
 int ensure_stage(towr_gpu_handle h, int B) {
   if (B <= h->stage_B) return TOWR_OK;
   const Layout& L = h->L;
@@ -420,6 +509,10 @@ int ensure_stage(towr_gpu_handle h, int B) {
   HIPCHK(h, hipMalloc(&h->d_x, sizeof(double) * (size_t)B * L.n));
   HIPCHK(h, hipMalloc(&h->d_g, sizeof(double) * (size_t)B * std::max(1, L.m)));
   HIPCHK(h, hipMalloc(&h->d_v, sizeof(double) * (size_t)B * std::max<int64_t>(1, L.nnz)));
+  if (!h->d_f) {
+    HIPCHK(h, hipMalloc(&h->d_f, sizeof(double)));
+    HIPCHK(h, hipMalloc(&h->d_grad, sizeof(double) * (size_t)std::max(1, L.n)));
+  }
   HIPCHK(h, hipHostMalloc(&h->h_x, sizeof(double) * (size_t)B * L.n, hipHostMallocDefault));
   HIPCHK(h, hipHostMalloc(&h->h_g, sizeof(double) * (size_t)B * std::max(1, L.m), hipHostMallocDefault));
   HIPCHK(h, hipHostMalloc(&h->h_v, sizeof(double) * (size_t)B * std::max<int64_t>(1, L.nnz), hipHostMallocDefault));
@@ -499,7 +592,8 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
       (r = upload(h, &h->d_tiles, L.tiles)) || (r = upload(h, &h->d_nodecol, nodecol16)) ||
       (r = upload(h, &h->d_spl, L.spl)) || (r = upload(h, &h->d_dur, L.dur)) || (r = upload(h, &h->d_segs, L.segs)) || (r = upload(h, &h->d_terrain, ter)) ||
       (r = upload(h, &h->d_pinfo, L.pinfo)) || (r = upload(h, &h->d_pcols, L.pcols)) || (r = upload(h, &h->d_sched, L.sched)) ||
-      (r = upload(h, &h->d_misc, L.misc_tiles)) || (r = upload(h, &h->d_eelin, L.eelin)))
+      (r = upload(h, &h->d_misc, L.misc_tiles)) || (r = upload(h, &h->d_eelin, L.eelin)) ||
+      (r = upload(h, &h->d_citems, L.cost_items)))
     return bail(r);
   {
     const char* ns = std::getenv("TOWR_GPU_STREAMS");
@@ -522,6 +616,15 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
       h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
     }
   }
+  {
+    const size_t lds = cost_lds_bytes(L);
+    if (lds > 160 * 1024) { h->err = "problem too large for the cost kernel's LDS gradient"; return bail(TOWR_ERR_UNSUPPORTED); }
+    if (lds > 64 * 1024)
+      for (int g = 0; g < 2; ++g)
+        if (hipFuncSetAttribute(cost_kernel_for(L.gait, g != 0), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+          h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
+        }
+  }
   *out = h;
   return TOWR_OK;
 }
@@ -529,8 +632,8 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
 int towr_gpu_destroy(towr_gpu_handle h) {
   if (!h) return TOWR_OK;
   void* dev[] = {h->d_items, h->d_slots, h->d_tiles, h->d_nodecol, h->d_spl, h->d_dur, h->d_segs, h->d_terrain,
-                 h->d_pinfo, h->d_pcols, h->d_sched, h->d_misc, h->d_eelin,
-                 h->d_bterrain, h->d_x, h->d_g, h->d_v};
+                 h->d_pinfo, h->d_pcols, h->d_sched, h->d_misc, h->d_eelin, h->d_citems,
+                 h->d_bterrain, h->d_x, h->d_g, h->d_v, h->d_f, h->d_grad};
   if (h->device >= 0) for (void* p : dev) if (p) (void)hipFree(p);
   void* host[] = {h->h_x, h->h_g, h->h_v};
   for (void* p : host) if (p) (void)hipHostFree(p);
@@ -608,6 +711,47 @@ int towr_gpu_eval_g_jac(towr_gpu_handle h, const double* x, double* g, double* v
   if (!h || !x || !g || !values) return fail(h, TOWR_ERR_INVALID, "null argument");
   if (int rc = bind(h)) return rc;
   return host_eval(h, 1, x, g, values);
+}
+
+// one problem through the staging buffers: x -> HBM, cost launch, f (and gradient) -> host
+static int host_cost(towr_gpu_handle h, const double* x, double* f, double* grad) {
+  if (int rc = ensure_stage(h, 1)) return rc;
+  const Layout& L = h->L;
+  const size_t xb = sizeof(double) * (size_t)L.n;
+  std::memcpy(h->h_x, x, xb);
+  HIPCHK(h, hipMemcpyAsync(h->d_x, h->h_x, xb, hipMemcpyHostToDevice, h->stream));
+  if (int rc = launch_cost(h, 1, h->d_x, L.n, h->d_f, grad ? h->d_grad : nullptr, L.n, h->stream, h->d_terrain, 0)) return rc;
+  double fv = 0.0;
+  HIPCHK(h, hipMemcpyAsync(h->h_g, h->d_f, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  if (grad) HIPCHK(h, hipMemcpyAsync(h->h_x, h->d_grad, xb, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  std::memcpy(&fv, h->h_g, sizeof(double));
+  if (f) *f = fv;
+  if (grad) std::memcpy(grad, h->h_x, xb);
+  return TOWR_OK;
+}
+
+int towr_gpu_eval_f(towr_gpu_handle h, const double* x, double* f) {
+  if (!h || !x || !f) return fail(h, TOWR_ERR_INVALID, "null argument");
+  if (int rc = bind(h)) return rc;
+  return host_cost(h, x, f, nullptr);
+}
+
+int towr_gpu_eval_grad_f(towr_gpu_handle h, const double* x, double* grad) {
+  if (!h || !x || !grad) return fail(h, TOWR_ERR_INVALID, "null argument");
+  if (int rc = bind(h)) return rc;
+  return host_cost(h, x, nullptr, grad);
+}
+
+int towr_gpu_eval_cost_batch_device(towr_gpu_handle h, int32_t B, const double* X, int64_t ldx, double* F,
+                                    double* GRAD, int64_t ldgrad, void* stream) {
+  if (!h || B < 0 || !X || !F) return fail(h, TOWR_ERR_INVALID, "bad argument");
+  const Layout& L = h->L;
+  if (ldx < L.n || (GRAD && ldgrad < L.n)) return fail(h, TOWR_ERR_INVALID, "leading dimension smaller than n");
+  if (int rc = bind(h)) return rc;
+  const bool per = h->d_bterrain && h->bterrain_n >= B;
+  return launch_cost(h, B, X, ldx, F, GRAD, ldgrad, reinterpret_cast<hipStream_t>(stream),
+                     per ? h->d_bterrain : h->d_terrain, per ? 1 : 0);
 }
 
 int towr_gpu_set_batch_terrain(towr_gpu_handle h, int32_t B, const towr_terrain_t* terrains) {

@@ -364,6 +364,7 @@ class Parameters:
     """Parameters, parameters.cc:40-167 (defaults) and parameters.h:141-152 (constraint names)."""
     (Dynamic, EndeffectorRom, TotalTime, Terrain, TerrainHard, Force, Torque, Swing, BaseRom,
      BaseAcc, BaseHeight) = range(11)
+    ForcesCostID, EEMotionCostID, EnergyCostID, AngMomCostID = range(4)   # parameters.h:157-161
 
     def __init__(self):
         self.duration_base_polynomial_ = 0.1
@@ -380,6 +381,14 @@ class Parameters:
         self.torque_ty_min_, self.torque_ty_max_ = -100.0, 100.0
         self.torque_k_friction_ = 2.0 / 3.0
         self.ee_linear_constraints_: List["EELinearConstraintDef"] = []
+        # costs (parameters.h:157-247): (CostName, weight) pairs; none by default (parameters.cc:90)
+        self.costs_: List[Tuple[int, float]] = []
+        self.energy_cost_torque_weight_ = 1.0
+        self.dt_cost_energy_ = 0.02
+        self.dt_cost_ang_mom_ = 0.02
+        self.enable_swing_ee_base_pos_tracking = False
+        self.swing_ee_base_pos_tracking_weight_ = 1e-2
+        self.dt_cost_swing_ee_base_pos_tracking_ = 0.05
         self.dt_constraint_torque_ = 0.02
         self.bound_phase_duration_ = (0.2, 1.0)
         self.constraints_ = [Parameters.Terrain, Parameters.Dynamic, Parameters.BaseAcc,
@@ -422,6 +431,14 @@ class Parameters:
             out.append(dt if t_left > dt else t_left)
             t_left -= dt
         return out
+
+
+def _euler_zyx(a):
+    """EulerConverter::GetRotationMatrixBaseToWorld (euler_converter.cc:207-221)."""
+    sx, cx, sy, cy, sz, cz = math.sin(a[0]), math.cos(a[0]), math.sin(a[1]), math.cos(a[1]), math.sin(a[2]), math.cos(a[2])
+    return [[cy * cz, cz * sx * sy - cx * sz, sx * sz + cx * cz * sy],
+            [cy * sz, cx * cz + sx * sy * sz, cx * sy * sz - cz * sx],
+            [-sy, cy * sx, cx * cy]]
 
 
 @dataclass
@@ -524,6 +541,39 @@ class NlpFormulation:
                             ip=[dfn.target, dfn.deriv, len(dfn.terms)] + [e * 3 + d for e, d, _ in dfn.terms]))
         return out
 
+    # cost terms in NlpFormulation::GetCosts order (nlp_formulation.cc:604-680)
+    def cost_terms(self) -> List[dict]:
+        P, E = self.params_, self.params_.GetEECount()
+        out = []
+        for name, w in P.costs_:
+            if name == Parameters.ForcesCostID:      # MakeForcesCost (:646-664)
+                for ee in range(E):
+                    for dim in range(3):
+                        out.append(dict(kind=capi.COST_NODE, ee=ee, weight=w, ip=[capi.VAR_EE_FORCE, 0, dim]))
+                        out.append(dict(kind=capi.COST_NODE, ee=ee, weight=w, ip=[capi.VAR_EE_TORQUE, 0, dim]))
+                        out.append(dict(kind=capi.COST_NODE, ee=ee, weight=0.1 * w, ip=[capi.VAR_EE_FORCE, 1, dim]))
+                        out.append(dict(kind=capi.COST_NODE, ee=ee, weight=0.1 * w, ip=[capi.VAR_EE_TORQUE, 1, dim]))
+            elif name == Parameters.EEMotionCostID:  # MakeEEMotionCost (:666-678)
+                for ee in range(E):
+                    out.append(dict(kind=capi.COST_NODE, ee=ee, weight=w, ip=[capi.VAR_EE_MOTION, 1, 0]))
+                    out.append(dict(kind=capi.COST_NODE, ee=ee, weight=w, ip=[capi.VAR_EE_MOTION, 1, 1]))
+                    out.append(dict(kind=capi.COST_NODE, ee=ee, weight=0.5 * w, ip=[capi.VAR_EE_MOTION, 1, 2]))
+            elif name == Parameters.EnergyCostID:
+                out.append(dict(kind=capi.COST_ENERGY, weight=w, dt=P.dt_cost_energy_, p=[P.energy_cost_torque_weight_]))
+            elif name == Parameters.AngMomCostID:
+                out.append(dict(kind=capi.COST_ANG_MOMENTUM, weight=w, dt=P.dt_cost_ang_mom_))
+            else:
+                raise ValueError("cost not defined!")
+        if P.enable_swing_ee_base_pos_tracking and P.swing_ee_base_pos_tracking_weight_ > 0.0:   # :613-626
+            b0 = self.initial_base_
+            R = _euler_zyx(b0.ang_p)
+            for ee in range(E):
+                rW = [self.initial_ee_W_[ee][k] - b0.lin_p[k] for k in range(3)]
+                rB = [R[0][i] * rW[0] + R[1][i] * rW[1] + R[2][i] * rW[2] for i in range(3)]
+                out.append(dict(kind=capi.COST_EE_BASE_POS, ee=ee, weight=P.swing_ee_base_pos_tracking_weight_,
+                                dt=P.dt_cost_swing_ee_base_pos_tracking_, p=rB))
+        return out
+
     def to_desc(self, varsets=None, constraints=None, init_mode=capi.INIT_FORMULATION,
                 ee_goal=None, total_time=None) -> capi.ProblemDesc:
         P = self.params_
@@ -574,6 +624,17 @@ class NlpFormulation:
                 d.constraints[i].p[j] = v
             for j, v in enumerate(c.get("ip", [])):
                 d.constraints[i].ip[j] = v
+        cts = self.cost_terms()
+        if len(cts) > capi.MAX_COSTS:
+            raise ValueError("too many cost terms")
+        d.n_costs = len(cts)
+        for i, c in enumerate(cts):
+            d.costs[i].kind, d.costs[i].ee = c["kind"], c.get("ee", 0)
+            d.costs[i].weight, d.costs[i].dt = c["weight"], c.get("dt", 0.0)
+            for j, v in enumerate(c.get("p", [])):
+                d.costs[i].p[j] = v
+            for j, v in enumerate(c.get("ip", [])):
+                d.costs[i].ip[j] = v
         it = d.init
         it.mode = init_mode
         b0, b1 = self.initial_base_, self.final_base_

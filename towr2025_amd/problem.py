@@ -106,6 +106,31 @@ class TowrGpuProblem:
         self._check(self._lib.towr_gpu_eval_g_jac(self._h, capi.dptr(x), capi.dptr(g), capi.dptr(v)))
         return g, v
 
+    def eval_f(self, x) -> float:
+        """Objective (IpoptAdapter::eval_f): the sum of every cost term."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        f = C.c_double()
+        self._check(self._lib.towr_gpu_eval_f(self._h, capi.dptr(x), C.byref(f)))
+        return f.value
+
+    def eval_grad_f(self, x) -> np.ndarray:
+        """Dense objective gradient (IpoptAdapter::eval_grad_f)."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        grad = np.zeros(self.n)
+        self._check(self._lib.towr_gpu_eval_grad_f(self._h, capi.dptr(x), capi.dptr(grad)))
+        return grad
+
+    def eval_cost_batch_device(self, X, F, GRAD=None, stream=None):
+        """Device batch objective on torch HIP tensors: X (B, ldx) -> F (B,), GRAD (B, ldgrad) or None."""
+        import torch
+        B = X.shape[0]
+        if stream is None:
+            stream = torch.cuda.current_stream(X.device)
+        self._check(self._lib.towr_gpu_eval_cost_batch_device(
+            self._h, B, C.c_void_p(X.data_ptr()), X.stride(0), C.c_void_p(F.data_ptr()),
+            C.c_void_p(GRAD.data_ptr() if GRAD is not None else 0), GRAD.stride(0) if GRAD is not None else 0,
+            C.c_void_p(stream.cuda_stream)))
+
     def set_batch_terrain(self, terrains):
         arr = (capi.Terrain * len(terrains))(*terrains)
         self._check(self._lib.towr_gpu_set_batch_terrain(self._h, len(terrains), arr))
