@@ -203,6 +203,29 @@ def main():
                 out["roofline"]["traffic_source"] = rec.get("source")
         except Exception:
             pass
+    if rank == 0:
+        # the objective callbacks on the same batch: every cost kind of
+        # NlpFormulation::GetCosts on this formulation; one eval_f + eval_grad_f per problem
+        cdesc = F.with_costs(F.anymal_trot()).to_desc()
+        cprob = TowrGpuProblem(cdesc, device=local)
+        cprob.set_batch_terrain(terrains)
+        Fo = torch.empty(B, dtype=torch.float64, device=dev)
+        Go = torch.empty((B, (prob.n + 15) // 16 * 16), dtype=torch.float64, device=dev)
+        for i in range(2):
+            cprob.eval_cost_batch_device(X[i % N_X], Fo, Go, stream)
+        a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for i in range(reps):
+            cprob.eval_cost_batch_device(X[i % N_X], Fo, Go, stream)
+        z.record(stream)
+        torch.cuda.synchronize()
+        ms = a.elapsed_time(z) / reps
+        cbytes = 8 * (2 * prob.n + 1)
+        out["objective"] = {"value": B / (ms * 1e-3), "unit": "eval_f+eval_grad_f calls/s", "ms_per_batch": ms,
+                            "cost_terms": cdesc.n_costs, "bytes_per_call": cbytes,
+                            "GB/s": B * cbytes / (ms * 1e-3) / 1e9,
+                            "note": "ANYmal trot + Forces/EEMotion/Energy/AngularMomentum/EEBasePos costs, same batch"}
+        cprob.close()
     if rank == 0 and not args.no_host:
         # PCIe-inclusive rate through the host-buffer entry point (towr_gpu_eval_batch: H2D of X,
         # launch, D2H of G and V via pinned staging) — reported beside, never as `value`

@@ -92,15 +92,7 @@ def _anymal_baserom():
     return f.to_desc()
 
 
-def _with_costs(f, costs=None, ee_base_pos=True, torque_weight=None):
-    """Cost terms of NlpFormulation::GetCosts (nlp_formulation.cc:604-680) on a formulation."""
-    P = f.params_
-    P.costs_ = costs if costs is not None else [(F.Parameters.ForcesCostID, 1e-3), (F.Parameters.EEMotionCostID, 0.5),
-                                                 (F.Parameters.EnergyCostID, 1e-4), (F.Parameters.AngMomCostID, 0.1)]
-    P.enable_swing_ee_base_pos_tracking = ee_base_pos
-    if torque_weight is not None:
-        P.energy_cost_torque_weight_ = torque_weight
-    return f
+_with_costs = F.with_costs
 
 
 def cost_descs():

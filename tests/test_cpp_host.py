@@ -1,6 +1,6 @@
 """C++ host side (towr2025_amd/host): the NlpFormulation mirror builds byte-identical problem
-descriptions to the Python mirror, and the Engine / NlpCallbacks (IPOPT TNLP-shaped eval_g /
-eval_jac_g) driver reproduces the oracle's sizes, x0 and pattern (CPU, layout-only handle) and its
+descriptions to the Python mirror, and the Engine / NlpCallbacks (IPOPT TNLP-shaped eval_f /
+eval_grad_f / eval_g / eval_jac_g) driver reproduces the oracle's sizes, x0 and pattern (CPU, layout-only handle) and its
 values on the GPU. The driver runs as a child process (tests/.. towr_host_check)."""
 import ctypes as C
 import os
@@ -20,8 +20,13 @@ def _biped_next():
     return _with_next_tier(F.biped_walk())
 
 
+def _anymal_costs():
+    from tests.configs import _with_costs
+    return _with_costs(F.anymal_trot()).to_desc()
+
+
 CFGS = {"anymal": lambda: F.anymal_trot().to_desc(), "biped": lambda: F.biped_walk().to_desc(),
-        "hopper": lambda: F.monoped_hopper().to_desc(), "biped_next": _biped_next}
+        "hopper": lambda: F.monoped_hopper().to_desc(), "biped_next": _biped_next, "anymal_costs": _anymal_costs}
 
 
 @pytest.fixture(scope="module")
@@ -46,7 +51,9 @@ def _run(exe, cfg, out, device):
     out = dict(desc=desc, n=int(n), m=int(m), nnz=nnz, x0=x0, iRow=r, jCol=c)
     if device >= 0:
         out["g"] = np.frombuffer(raw, np.float64, m, off); off += 8 * m
-        out["values"] = np.frombuffer(raw, np.float64, nnz, off)
+        out["values"] = np.frombuffer(raw, np.float64, nnz, off); off += 8 * nnz
+        out["f"] = float(np.frombuffer(raw, np.float64, 1, off)[0]); off += 8
+        out["grad"] = np.frombuffer(raw, np.float64, n, off)
     return out
 
 
@@ -68,9 +75,10 @@ def test_cpp_layout_matches_python_and_oracle(exe, tmp_path, cfg):
 @pytest.mark.parametrize("cfg", sorted(CFGS))
 def test_cpp_callbacks_on_gpu_match_oracle(exe, tmp_path, cfg):
     from oracle.oracle import Oracle
-    from tests.parity import assert_close
+    from tests.parity import assert_close, assert_cost_close
     res = _run(exe, cfg, tmp_path / "o.bin", 0)
     o = Oracle(CFGS[cfg]())
     x0 = o.initial_x()
     r, _, v = o.eval_jac(x0)
     assert_close(o.eval_g(x0), res["g"], r, v, res["values"], o.m, f"C++ host {cfg}")
+    assert_cost_close(o.eval_f(x0), res["f"], o.eval_grad_f(x0), res["grad"], f"C++ host {cfg} costs")

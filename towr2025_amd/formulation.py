@@ -738,3 +738,15 @@ def procedural_desc() -> capi.ProblemDesc:
     f, vs, cs, goal, T = procedural_monoped()
     return f.to_desc(varsets=vs, constraints=cs, init_mode=capi.INIT_PROCEDURAL, ee_goal=goal,
                      total_time=T)
+
+
+def with_costs(f: "NlpFormulation", costs=None, ee_base_pos=True, torque_weight=None) -> "NlpFormulation":
+    """Enables cost terms (Parameters::costs_, parameters.h:157-247) on a formulation; by default every
+    kind: Forces 1e-3, EEMotion 0.5, Energy 1e-4, AngularMomentum 0.1 and the swing ee-base tracking."""
+    P = f.params_
+    P.costs_ = costs if costs is not None else [(Parameters.ForcesCostID, 1e-3), (Parameters.EEMotionCostID, 0.5),
+                                                 (Parameters.EnergyCostID, 1e-4), (Parameters.AngMomCostID, 0.1)]
+    P.enable_swing_ee_base_pos_tracking = ee_base_pos
+    if torque_weight is not None:
+        P.energy_cost_torque_weight_ = torque_weight
+    return f

@@ -330,6 +330,67 @@ std::vector<ConstraintSpec> NlpFormulation::GetConstraints() const {
   return out;
 }
 
+// NlpFormulation::GetCosts (nlp_formulation.cc:604-680): MakeForcesCost (:646-664) and
+// MakeEEMotionCost (:666-678) expand into NodeCosts; the swing ee-base tracking terms (:613-626) follow
+std::vector<CostSpec> NlpFormulation::GetCosts() const {
+  const Parameters& P = params_;
+  const int E = P.GetEECount();
+  std::vector<CostSpec> out;
+  auto node = [&](int ee, double w, int kind, int deriv, int dim) {
+    CostSpec c{TOWR_COST_NODE, ee, w, 0.0};
+    c.ip[0] = kind; c.ip[1] = deriv; c.ip[2] = dim;
+    out.push_back(c);
+  };
+  for (const auto& [name, w] : P.costs_) {
+    switch (name) {
+      case Parameters::ForcesCostID:
+        for (int ee = 0; ee < E; ++ee)
+          for (int dim = 0; dim < 3; ++dim) {
+            node(ee, w, TOWR_VAR_EE_FORCE, 0, dim);
+            node(ee, w, TOWR_VAR_EE_TORQUE, 0, dim);
+            node(ee, 0.1 * w, TOWR_VAR_EE_FORCE, 1, dim);
+            node(ee, 0.1 * w, TOWR_VAR_EE_TORQUE, 1, dim);
+          }
+        break;
+      case Parameters::EEMotionCostID:
+        for (int ee = 0; ee < E; ++ee) {
+          node(ee, w, TOWR_VAR_EE_MOTION, 1, 0);
+          node(ee, w, TOWR_VAR_EE_MOTION, 1, 1);
+          node(ee, 0.5 * w, TOWR_VAR_EE_MOTION, 1, 2);
+        }
+        break;
+      case Parameters::EnergyCostID: {
+        CostSpec c{TOWR_COST_ENERGY, 0, w, P.dt_cost_energy_};
+        c.p[0] = P.energy_cost_torque_weight_;
+        out.push_back(c);
+        break;
+      }
+      case Parameters::AngMomCostID: out.push_back(CostSpec{TOWR_COST_ANG_MOMENTUM, 0, w, P.dt_cost_ang_mom_}); break;
+      default: throw std::runtime_error("cost not defined!");
+    }
+  }
+  if (P.enable_swing_ee_base_pos_tracking && P.swing_ee_base_pos_tracking_weight_ > 0.0) {
+    // reference ee positions in the base frame at the initial state
+    double R[3][3];
+    {
+      const auto& a = initial_base_.ang_p;
+      const double sx = std::sin(a[0]), cx = std::cos(a[0]), sy = std::sin(a[1]), cy = std::cos(a[1]), sz = std::sin(a[2]), cz = std::cos(a[2]);
+      const double m[3][3] = {{cy * cz, cz * sx * sy - cx * sz, sx * sz + cx * cz * sy},
+                              {cy * sz, cx * cz + sx * sy * sz, cx * sy * sz - cz * sx},
+                              {-sy, cy * sx, cx * cy}};
+      std::memcpy(R, m, sizeof R);
+    }
+    for (int ee = 0; ee < E; ++ee) {
+      double rW[3];
+      for (int k = 0; k < 3; ++k) rW[k] = initial_ee_W_.at(ee)[k] - initial_base_.lin_p[k];
+      CostSpec c{TOWR_COST_EE_BASE_POS, ee, P.swing_ee_base_pos_tracking_weight_, P.dt_cost_swing_ee_base_pos_tracking_};
+      for (int i = 0; i < 3; ++i) c.p[i] = R[0][i] * rW[0] + R[1][i] * rW[1] + R[2][i] * rW[2];
+      out.push_back(c);
+    }
+  }
+  return out;
+}
+
 towr_problem_desc_t NlpFormulation::MakeDesc() const {
   return MakeDesc(GetVariableSets(), GetConstraints(), TOWR_INIT_FORMULATION, {}, params_.GetTotalTime());
 }
@@ -383,6 +444,14 @@ towr_problem_desc_t NlpFormulation::MakeDesc(const std::vector<VarSet>& vs, cons
     d.constraints[i].dt = cs[i].dt;
     for (int j = 0; j < 6; ++j) d.constraints[i].p[j] = cs[i].p[j];
     for (int j = 0; j < 9; ++j) d.constraints[i].ip[j] = cs[i].ip[j];
+  }
+  const std::vector<CostSpec> costs = GetCosts();
+  if ((int)costs.size() > TOWR_MAX_COSTS) throw std::invalid_argument("too many cost terms");
+  d.n_costs = (int)costs.size();
+  for (size_t i = 0; i < costs.size(); ++i) {
+    towr_cost_t& c = d.costs[i];
+    c.kind = costs[i].kind; c.ee = costs[i].ee; c.weight = costs[i].weight; c.dt = costs[i].dt;
+    for (int j = 0; j < 4; ++j) { c.p[j] = costs[i].p[j]; c.ip[j] = costs[i].ip[j]; }
   }
   towr_init_t& it = d.init;
   it.mode = init_mode;

@@ -96,6 +96,14 @@ struct Parameters {
     double dt = 0.1;
   };
   std::vector<EELinearConstraintDef> ee_linear_constraints_;
+  // costs (parameters.h:157-247): (CostName, weight) pairs, none by default (parameters.cc:90)
+  enum CostName { ForcesCostID, EEMotionCostID, EnergyCostID, AngMomCostID };
+  std::vector<std::pair<CostName, double>> costs_;
+  double energy_cost_torque_weight_ = 1.0;
+  double dt_cost_energy_ = 0.02, dt_cost_ang_mom_ = 0.02;
+  bool enable_swing_ee_base_pos_tracking = false;
+  double swing_ee_base_pos_tracking_weight_ = 1e-2;
+  double dt_cost_swing_ee_base_pos_tracking_ = 0.05;
   std::array<double, 2> bound_phase_duration_{0.2, 1.0};
   std::vector<ConstraintName> constraints_{Terrain, Dynamic, BaseAcc, EndeffectorRom, Force, Swing, BaseHeight};
   std::vector<std::vector<double>> ee_phase_durations_;
@@ -113,6 +121,7 @@ struct BaseState {
 };
 
 struct VarSet { int kind, ee; };
+struct CostSpec { int kind, ee; double weight, dt; std::array<double, 4> p{}; std::array<int32_t, 4> ip{}; };
 struct ConstraintSpec { int kind, ee; double T, dt; std::array<double, 6> p{}; std::array<int32_t, 9> ip{}; };
 
 class NlpFormulation {
@@ -125,6 +134,7 @@ class NlpFormulation {
 
   std::vector<VarSet> GetVariableSets() const;          // nlp_formulation.cc:76-119 order
   std::vector<ConstraintSpec> GetConstraints() const;   // nlp_formulation.cc:365-398 expansion
+  std::vector<CostSpec> GetCosts() const;               // nlp_formulation.cc:604-680 expansion
   // the engine's problem description (optionally with an explicit variable / constraint list as
   // towr/test/procedural_example.cc builds, a procedural initial guess and goal footholds)
   towr_problem_desc_t MakeDesc() const;

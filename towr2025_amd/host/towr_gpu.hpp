@@ -6,7 +6,8 @@
 //              EvalConstraints(x) -> g, EvalNonzerosOfJacobian(x) -> values, the Jacobian
 //              structure in RowMajor (iRow, jCol) order.
 // NlpCallbacks  the IPOPT TNLP callback subset of ifopt's IpoptAdapter for the hot path
-//            (get_nlp_info / eval_g / eval_jac_g) with Ipopt's argument meaning: eval_jac_g with
+//            (get_nlp_info / eval_f / eval_grad_f / eval_g / eval_jac_g) with Ipopt's argument
+//            meaning: eval_jac_g with
 //            values == nullptr fills the structure, otherwise the values. Unlike ifopt (which
 //            ignores new_x and re-evaluates every set), g and J are produced by one fused launch per
 //            new x and J is served from that launch when IPOPT asks for it at the same x.
@@ -54,6 +55,9 @@ class Engine {
   void EvalConstraints(const double* x, double* g) const { Check(towr_gpu_eval_g(h_, x, g)); }
   void EvalNonzerosOfJacobian(const double* x, double* values) const { Check(towr_gpu_eval_jac_values(h_, x, values)); }
   void EvalConstraintsAndJacobian(const double* x, double* g, double* values) const { Check(towr_gpu_eval_g_jac(h_, x, g, values)); }
+  // objective (ifopt Problem::EvaluateCostFunction) and its dense gradient
+  double EvalCostFunction(const double* x) const { double f = 0.0; Check(towr_gpu_eval_f(h_, x, &f)); return f; }
+  void EvalCostFunctionGradient(const double* x, double* grad) const { Check(towr_gpu_eval_grad_f(h_, x, grad)); }
   // B independent problems sharing this layout (host buffers, row-major B x n / m / nnz)
   void SetBatchTerrain(const std::vector<towr_terrain_t>& t) { Check(towr_gpu_set_batch_terrain(h_, (int32_t)t.size(), t.data())); }
   void EvalBatch(int B, const double* X, double* G, double* V) const { Check(towr_gpu_eval_batch(h_, B, X, G, V)); }
@@ -72,11 +76,24 @@ class Engine {
   int64_t nnz_ = 0;
 };
 
-// The eval_g / eval_jac_g pair of an IPOPT TNLP (Index = int, Number = double), as ifopt's
-// IpoptAdapter implements it for towr, served by the engine.
+// The eval_f / eval_grad_f / eval_g / eval_jac_g callbacks of an IPOPT TNLP (Index = int,
+// Number = double), as ifopt's IpoptAdapter implements them for towr, served by the engine.
 class NlpCallbacks {
  public:
   explicit NlpCallbacks(Engine& e) : e_(e), g_(e.GetNumberOfConstraints()), v_(e.GetNumberOfJacobianNonzeros()) {}
+
+  bool eval_f(int n, const double* x, bool new_x, double& obj_value) {
+    if (n != e_.GetNumberOfOptimizationVariables()) return false;
+    NewX(new_x);
+    try { obj_value = e_.EvalCostFunction(x); } catch (const std::exception&) { return false; }
+    return true;
+  }
+  bool eval_grad_f(int n, const double* x, bool new_x, double* grad_f) {
+    if (n != e_.GetNumberOfOptimizationVariables()) return false;
+    NewX(new_x);
+    try { e_.EvalCostFunctionGradient(x, grad_f); } catch (const std::exception&) { return false; }
+    return true;
+  }
 
   bool get_nlp_info(int& n, int& m, int& nnz_jac_g) const {
     n = e_.GetNumberOfOptimizationVariables();
@@ -104,9 +121,12 @@ class NlpCallbacks {
   }
 
  private:
+  // IPOPT's new_x == true on the first callback at a new x (whichever it is) invalidates the cache
+  void NewX(bool new_x) { if (new_x) valid_ = false; }
   // one fused launch per new x; IPOPT's new_x == false promises the x of the previous call
   bool Update(const double* x, bool new_x) {
-    if (!new_x && valid_) return true;
+    NewX(new_x);
+    if (valid_) return true;
     try { e_.EvalConstraintsAndJacobian(x, g_.data(), v_.data()); } catch (const std::exception&) { valid_ = false; return false; }
     valid_ = true;
     return true;
