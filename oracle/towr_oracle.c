@@ -644,7 +644,307 @@ static void ter_d_nbasis(const Terrain* T, int basis, int dim, double x, double 
 /* =============================================================================================
  * EulerConverter (src/helpers/euler_converter.cc)
  * ===========================================================================================*/
-typedef struct { const Spline* euler; spmat jac_struct; } Euler;
+typedef struct { const Spline* euler; spmat jac_struct; int rotvec; } Euler;   /* rotvec: RotVecConverter */
+
+/* ---------------------------------------------------------------------------------------------
+ * RotVecConverter (src/helpers/rotvec_converter.cc; Parameters::RotationVector, parameters.h:334):
+ * the base angular spline holds a rotation vector theta; R = exp([theta]x) (Rodrigues),
+ * omega = J_L(theta) theta_dot, omega_dot = J_L_dot theta_dot + J_L theta_ddot. The Jacobians keep
+ * the reference's structure: DenseTimesSparse (every row for each active column) followed by
+ * EnsureFullPattern (all 3 rows of every column active in d pos / d vel).
+ * -------------------------------------------------------------------------------------------*/
+#define RV_EPS 1e-10   /* kEps, :10 */
+typedef struct { double alpha, beta, gamma, dalpha, dbeta, dgamma; } RvCoeffs;
+
+static double rv_norm(const double v[3]) { return sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); }
+
+/* ComputeCoeffs, :30-59 */
+static RvCoeffs rv_coeffs(double theta) {
+  RvCoeffs c;
+  double t2 = theta * theta;
+  if (theta < RV_EPS) {
+    c.alpha = 1.0 - t2 / 6.0; c.beta = 1.0 / 6.0 - t2 / 120.0; c.gamma = 0.5 - t2 / 24.0;
+    c.dalpha = -theta / 3.0; c.dbeta = -theta / 60.0; c.dgamma = -theta / 12.0;
+  } else {
+    double st = sin(theta), ct = cos(theta), t3 = t2 * theta, t4 = t3 * theta;
+    c.alpha = st / theta; c.beta = (theta - st) / t3; c.gamma = (1.0 - ct) / t2;
+    c.dalpha = (theta * ct - st) / t2;
+    c.dbeta = (-2.0 * theta - theta * ct + 3.0 * st) / t4;
+    c.dgamma = (theta * st - 2.0 + 2.0 * ct) / t3;
+  }
+  return c;
+}
+/* Skew, :20-28 */
+static void rv_skew(const double v[3], double S[3][3]) {
+  S[0][0] = 0;     S[0][1] = -v[2]; S[0][2] = v[1];
+  S[1][0] = v[2];  S[1][1] = 0;     S[1][2] = -v[0];
+  S[2][0] = -v[1]; S[2][1] = v[0];  S[2][2] = 0;
+}
+static void m3_mul(const double A[3][3], const double B[3][3], double C[3][3]) {
+  double T[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) T[i][j] = A[i][0] * B[0][j] + A[i][1] * B[1][j] + A[i][2] * B[2][j];
+  memcpy(C, T, sizeof T);
+}
+static void m3_vec(const double A[3][3], const double v[3], double o[3]) {
+  for (int i = 0; i < 3; ++i) o[i] = A[i][0] * v[0] + A[i][1] * v[1] + A[i][2] * v[2];
+}
+/* Rodrigues, :61-72 */
+static void rv_rodrigues(const double rv[3], double R[3][3]) {
+  double theta = rv_norm(rv), K[3][3];
+  rv_skew(rv, K);
+  if (theta < RV_EPS) {
+    for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) R[i][j] = (i == j ? 1.0 : 0.0) + K[i][j];
+    return;
+  }
+  double s = sin(theta) / theta, h = (1.0 - cos(theta)) / (theta * theta), KK[3][3];
+  m3_mul(K, K, KK);
+  for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) R[i][j] = ((i == j ? 1.0 : 0.0) + s * K[i][j]) + h * KK[i][j];
+}
+/* LeftJacobian, :74-85 */
+static void rv_left_jac(const double rv[3], double J[3][3]) {
+  double theta = rv_norm(rv), S[3][3];
+  rv_skew(rv, S);
+  if (theta < RV_EPS) {
+    for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) J[i][j] = (i == j ? 1.0 : 0.0) + 0.5 * S[i][j];
+    return;
+  }
+  RvCoeffs c = rv_coeffs(theta);
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) J[i][j] = (c.alpha * (i == j ? 1.0 : 0.0) + c.beta * (rv[i] * rv[j])) + c.gamma * S[i][j];
+}
+/* LeftJacobianDot, :87-107 */
+static void rv_left_jac_dot(const double rv[3], const double rvd[3], double J[3][3]) {
+  double theta = rv_norm(rv), S[3][3], Sd[3][3];
+  rv_skew(rv, S); rv_skew(rvd, Sd);
+  if (theta < RV_EPS) {
+    for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) J[i][j] = 0.5 * Sd[i][j];
+    return;
+  }
+  RvCoeffs c = rv_coeffs(theta);
+  double theta_dot = (rv[0] * rvd[0] + rv[1] * rvd[1] + rv[2] * rvd[2]) / theta;
+  double ad = c.dalpha * theta_dot, bd = c.dbeta * theta_dot, gd = c.dgamma * theta_dot;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      J[i][j] = (((ad * (i == j ? 1.0 : 0.0) + bd * (rv[i] * rv[j])) + c.beta * (rvd[i] * rv[j] + rv[i] * rvd[j])) + gd * S[i][j]) + c.gamma * Sd[i][j];
+}
+static void rv_R_t(const Euler* e, double t, double R[3][3]) {   /* GetRotationMatrixBaseToWorld, :118-123 */
+  double st[3][3]; spline_point(e->euler, t, st);
+  rv_rodrigues(st[kPos], R);
+}
+static void rv_omega(const Euler* e, double t, double w[3]) {   /* GetAngularVelocityInWorld, :125-130 */
+  double st[3][3], J[3][3]; spline_point(e->euler, t, st);
+  rv_left_jac(st[kPos], J); m3_vec(J, st[kVel], w);
+}
+static void rv_omega_dot(const Euler* e, double t, double wd[3]) {   /* GetAngularAccelerationInWorld, :132-138 */
+  double st[3][3], J[3][3], Jd[3][3], a[3], b[3]; spline_point(e->euler, t, st);
+  rv_left_jac_dot(st[kPos], st[kVel], Jd); rv_left_jac(st[kPos], J);
+  m3_vec(Jd, st[kVel], a); m3_vec(J, st[kAcc], b);
+  for (int k = 0; k < 3; ++k) wd[k] = a[k] + b[k];
+}
+/* DenseTimesSparse, :148-174: all 3 rows for every column active in B */
+static spmat rv_dense_times_sparse(const double A[3][3], const spmat* B) {
+  int n = B->cols;
+  char* act = (char*)calloc((size_t)n + 1, 1);
+  for (int r = 0; r < B->rows; ++r) for (int q = 0; q < B->r[r].n; ++q) act[B->r[r].e[q].col] = 1;
+  spmat out = sp_zero(3, n);
+  for (int col = 0; col < n; ++col) {
+    if (!act[col]) continue;
+    double bc[3] = {0, 0, 0};
+    for (int r = 0; r < 3; ++r)
+      for (int q = 0; q < B->r[r].n; ++q) if (B->r[r].e[q].col == col) bc[r] = B->r[r].e[q].val;
+    double rc[3]; m3_vec(A, bc, rc);
+    for (int r = 0; r < 3; ++r) *sp_coeffref(&out, r, col) = rc[r];
+  }
+  free(act);
+  return out;
+}
+/* EnsureFullPattern, :176-208 */
+static void rv_full_pattern(const Euler* e, double t, spmat* J) {
+  spmat jp = spline_jac(e->euler, t, kPos), jv = spline_jac(e->euler, t, kVel);
+  int n = J->cols;
+  char* act = (char*)calloc((size_t)n + 1, 1);
+  for (int r = 0; r < 3; ++r) {
+    for (int q = 0; q < jp.r[r].n; ++q) act[jp.r[r].e[q].col] = 1;
+    for (int q = 0; q < jv.r[r].n; ++q) act[jv.r[r].e[q].col] = 1;
+  }
+  for (int r = 0; r < J->rows; ++r) for (int q = 0; q < J->r[r].n; ++q) act[J->r[r].e[q].col] = 1;
+  for (int c = 0; c < n; ++c)
+    if (act[c]) for (int r = 0; r < 3; ++r) (void)sp_coeffref(J, r, c);   /* existing value or 0 */
+  free(act); sp_free(&jp); sp_free(&jv);
+}
+/* DerivOfRotVecMult, :210-233: d(R v)/dtheta = -[R v]x J_L, d(R^T v)/dtheta = R^T [v]x J_L */
+static spmat rv_d_rotvec(const Euler* e, double t, const double v[3], int inverse) {
+  double st[3][3], R[3][3], JL[3][3], A[3][3], S[3][3];
+  spline_point(e->euler, t, st);
+  rv_rodrigues(st[kPos], R); rv_left_jac(st[kPos], JL);
+  spmat jac_pos = spline_jac(e->euler, t, kPos);
+  if (inverse) {
+    double Rt[3][3];
+    for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) Rt[i][j] = R[j][i];
+    rv_skew(v, S); m3_mul(Rt, S, A); m3_mul(A, JL, A);
+  } else {
+    double Rv[3]; m3_vec(R, v, Rv);
+    rv_skew(Rv, S);
+    for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) S[i][j] = -S[i][j];
+    m3_mul(S, JL, A);
+  }
+  spmat res = rv_dense_times_sparse(A, &jac_pos);
+  rv_full_pattern(e, t, &res);
+  sp_free(&jac_pos);
+  return res;
+}
+static void rv_row_add(spmat* res, int j, const spmat* row1xn, double s) {   /* result.row(j) += s * row */
+  spmat cur = sp_row_of(res, j);
+  sp_add_inplace(&cur, row1xn, s);
+  sp_set_row_from(res, j, &cur);
+  sp_free(&cur);
+}
+/* Levi-Civita sign of the skew entry (dim, j): [theta]x_{dim,j} = sign * theta_k, k = 3 - dim - j */
+static double rv_sign(int dim, int j) { return ((j - dim + 3) % 3 == 1) ? -1.0 : 1.0; }
+
+/* GetDerivJLwrtNodes, :235-325: result.row(j) = d(J_L[dim][j]) / d nodes */
+static spmat rv_dJL(const Euler* e, double t, int dim) {
+  double st[3][3]; spline_point(e->euler, t, st);
+  const double* rv = st[kPos];
+  double theta = rv_norm(rv);
+  RvCoeffs c = rv_coeffs(theta);
+  spmat jac_pos = spline_jac(e->euler, t, kPos);
+  int n = jac_pos.cols;
+  spmat result = sp_copy(&e->jac_struct);
+  spmat pr[3];
+  for (int l = 0; l < 3; ++l) pr[l] = sp_row_of(&jac_pos, l);
+  spmat da = sp_zero(1, n), db = sp_zero(1, n), dg = sp_zero(1, n);
+  if (theta >= RV_EPS) {
+    double inv = 1.0 / theta;
+    spmat tj = sp_zero(1, n);
+    for (int l = 0; l < 3; ++l) if (fabs(rv[l]) > 1e-15) sp_add_inplace(&tj, &pr[l], rv[l] * inv);
+    sp_free(&da); sp_free(&db); sp_free(&dg);
+    da = sp_scale(&tj, c.dalpha); db = sp_scale(&tj, c.dbeta); dg = sp_scale(&tj, c.dgamma);
+    sp_free(&tj);
+  }
+  double Sk[3][3]; rv_skew(rv, Sk);
+  for (int j = 0; j < 3; ++j) {
+    if (dim == j) rv_row_add(&result, j, &da, 1.0);
+    double rvdj = rv[dim] * rv[j];
+    if (fabs(rvdj) > 1e-15) rv_row_add(&result, j, &db, rvdj);
+    if (fabs(c.beta) > 1e-15) {
+      if (fabs(rv[j]) > 1e-15) rv_row_add(&result, j, &pr[dim], c.beta * rv[j]);
+      if (fabs(rv[dim]) > 1e-15) rv_row_add(&result, j, &pr[j], c.beta * rv[dim]);
+    }
+    double sk = Sk[dim][j];
+    if (fabs(sk) > 1e-15) rv_row_add(&result, j, &dg, sk);
+    if (fabs(c.gamma) > 1e-15 && dim != j) rv_row_add(&result, j, &pr[3 - dim - j], c.gamma * rv_sign(dim, j));
+  }
+  for (int l = 0; l < 3; ++l) sp_free(&pr[l]);
+  sp_free(&da); sp_free(&db); sp_free(&dg); sp_free(&jac_pos);
+  return result;
+}
+
+/* GetDerivJLdotwrtNodes, :327-506: result.row(j) = d(J_L_dot[dim][j]) / d nodes */
+static spmat rv_dJLdot(const Euler* e, double t, int dim) {
+  double st[3][3]; spline_point(e->euler, t, st);
+  const double *rv = st[kPos], *rvd = st[kVel];
+  double theta = rv_norm(rv);
+  RvCoeffs c = rv_coeffs(theta);
+  spmat jac_pos = spline_jac(e->euler, t, kPos), jac_vel = spline_jac(e->euler, t, kVel);
+  int n = jac_pos.cols;
+  spmat result = sp_copy(&e->jac_struct);
+  spmat pr[3], vr[3];
+  for (int l = 0; l < 3; ++l) { pr[l] = sp_row_of(&jac_pos, l); vr[l] = sp_row_of(&jac_vel, l); }
+  double theta_dot = 0.0;
+  if (theta > RV_EPS) theta_dot = (rv[0] * rvd[0] + rv[1] * rvd[1] + rv[2] * rvd[2]) / theta;
+  double beta_dot = c.dbeta * theta_dot, gamma_dot = c.dgamma * theta_dot;
+  spmat dad = sp_zero(1, n), dbd = sp_zero(1, n), dgd = sp_zero(1, n);
+  spmat nhat = sp_zero(1, n);   /* n_hat^T jac_pos (theta > eps only) */
+  if (theta > RV_EPS) {
+    double inv = 1.0 / theta, t2 = theta * theta;
+    spmat dtd = sp_zero(1, n);
+    for (int l = 0; l < 3; ++l) { sp_add_inplace(&dtd, &pr[l], rvd[l] * inv); sp_add_inplace(&dtd, &vr[l], rv[l] * inv); }
+    for (int l = 0; l < 3; ++l) sp_add_inplace(&nhat, &pr[l], rv[l] * inv);
+    sp_add_inplace(&dtd, &nhat, -(theta_dot * inv));
+    double st_ = sin(theta), ct = cos(theta);
+    double alpha_pp = (-theta * st_ - 2.0 * (theta * ct - st_) / theta) / t2;
+    double beta_pp, gamma_pp;
+    { double num = -2.0 * theta - theta * ct + 3.0 * st_, dnum = -2.0 - ct + theta * st_ + 3.0 * ct, t4 = t2 * t2;
+      beta_pp = (dnum - 4.0 * num / theta) / t4; }
+    { double num = theta * st_ - 2.0 + 2.0 * ct, dnum = st_ + theta * ct - 2.0 * st_, t3 = t2 * theta;
+      gamma_pp = (dnum - 3.0 * num / theta) / t3; }
+    sp_free(&dad); sp_free(&dbd); sp_free(&dgd);
+    dad = sp_lincomb(&nhat, alpha_pp * theta_dot, &dtd, c.dalpha);
+    dbd = sp_lincomb(&nhat, beta_pp * theta_dot, &dtd, c.dbeta);
+    dgd = sp_lincomb(&nhat, gamma_pp * theta_dot, &dtd, c.dgamma);
+    sp_free(&dtd);
+  }
+  double Sk[3][3], Skd[3][3]; rv_skew(rv, Sk); rv_skew(rvd, Skd);
+  for (int j = 0; j < 3; ++j) {
+    if (dim == j) rv_row_add(&result, j, &dad, 1.0);
+    double rv_dj = rv[dim] * rv[j];
+    if (fabs(rv_dj) > 1e-15) rv_row_add(&result, j, &dbd, rv_dj);
+    if (fabs(beta_dot) > 1e-15) {
+      if (fabs(rv[j]) > 1e-15) rv_row_add(&result, j, &pr[dim], beta_dot * rv[j]);
+      if (fabs(rv[dim]) > 1e-15) rv_row_add(&result, j, &pr[j], beta_dot * rv[dim]);
+    }
+    double td_dj = rvd[dim] * rv[j] + rv[dim] * rvd[j];
+    if (fabs(td_dj) > 1e-15 && fabs(c.beta) > 1e-15 && theta > RV_EPS) rv_row_add(&result, j, &nhat, c.dbeta * td_dj);
+    if (fabs(c.beta) > 1e-15) {
+      if (fabs(rv[j]) > 1e-15) rv_row_add(&result, j, &vr[dim], c.beta * rv[j]);
+      if (fabs(rvd[dim]) > 1e-15) rv_row_add(&result, j, &pr[j], c.beta * rvd[dim]);
+      if (fabs(rvd[j]) > 1e-15) rv_row_add(&result, j, &pr[dim], c.beta * rvd[j]);
+      if (fabs(rv[dim]) > 1e-15) rv_row_add(&result, j, &vr[j], c.beta * rv[dim]);
+    }
+    double sk = Sk[dim][j];
+    if (fabs(sk) > 1e-15) rv_row_add(&result, j, &dgd, sk);
+    if (fabs(gamma_dot) > 1e-15 && dim != j) rv_row_add(&result, j, &pr[3 - dim - j], gamma_dot * rv_sign(dim, j));
+    double skd = Skd[dim][j];
+    if (fabs(skd) > 1e-15 && fabs(c.gamma) > 1e-15 && theta > RV_EPS) rv_row_add(&result, j, &nhat, c.dgamma * skd);
+    if (fabs(c.gamma) > 1e-15 && dim != j) rv_row_add(&result, j, &vr[3 - dim - j], c.gamma * rv_sign(dim, j));
+  }
+  for (int l = 0; l < 3; ++l) { sp_free(&pr[l]); sp_free(&vr[l]); }
+  sp_free(&dad); sp_free(&dbd); sp_free(&dgd); sp_free(&nhat); sp_free(&jac_pos); sp_free(&jac_vel);
+  return result;
+}
+
+/* GetDerivOfAngVelWrtNodes, :508-528 */
+static spmat rv_d_angvel(const Euler* e, double t) {
+  spmat jac = sp_copy(&e->jac_struct);
+  double st[3][3], JL[3][3]; spline_point(e->euler, t, st);
+  spmat vel = sp_from_dense(1, 3, st[kVel], 1);
+  spmat dVel = spline_jac(e->euler, t, kVel);
+  rv_left_jac(st[kPos], JL);
+  spmat JLdv = rv_dense_times_sparse(JL, &dVel);
+  for (int dim = X; dim <= Z; ++dim) {
+    spmat dJL = rv_dJL(e, t, dim);
+    spmat a = sp_mul(&vel, &dJL), b = sp_row_of(&JLdv, dim);
+    spmat s = sp_lincomb(&a, 1.0, &b, 1.0);
+    sp_set_row_from(&jac, dim, &s);
+    sp_free(&dJL); sp_free(&a); sp_free(&b); sp_free(&s);
+  }
+  rv_full_pattern(e, t, &jac);
+  sp_free(&vel); sp_free(&dVel); sp_free(&JLdv);
+  return jac;
+}
+
+/* GetDerivOfAngAccWrtNodes, :530-561 */
+static spmat rv_d_angacc(const Euler* e, double t) {
+  spmat jac = sp_copy(&e->jac_struct);
+  double st[3][3], JL[3][3], JLd[3][3]; spline_point(e->euler, t, st);
+  spmat vel = sp_from_dense(1, 3, st[kVel], 1), acc = sp_from_dense(1, 3, st[kAcc], 1);
+  spmat dVel = spline_jac(e->euler, t, kVel), dAcc = spline_jac(e->euler, t, kAcc);
+  rv_left_jac(st[kPos], JL); rv_left_jac_dot(st[kPos], st[kVel], JLd);
+  spmat JLd_dv = rv_dense_times_sparse(JLd, &dVel), JL_da = rv_dense_times_sparse(JL, &dAcc);
+  for (int dim = X; dim <= Z; ++dim) {
+    spmat dJLd = rv_dJLdot(e, t, dim), dJL = rv_dJL(e, t, dim);
+    spmat t1 = sp_mul(&vel, &dJLd), t2 = sp_row_of(&JLd_dv, dim), t3 = sp_mul(&acc, &dJL), t4 = sp_row_of(&JL_da, dim);
+    spmat s = sp_lincomb(&t1, 1.0, &t2, 1.0);
+    sp_add_inplace(&s, &t3, 1.0); sp_add_inplace(&s, &t4, 1.0);
+    sp_set_row_from(&jac, dim, &s);
+    sp_free(&dJLd); sp_free(&dJL); sp_free(&t1); sp_free(&t2); sp_free(&t3); sp_free(&t4); sp_free(&s);
+  }
+  rv_full_pattern(e, t, &jac);
+  sp_free(&vel); sp_free(&acc); sp_free(&dVel); sp_free(&dAcc); sp_free(&JLd_dv); sp_free(&JL_da);
+  return jac;
+}
 
 /* EulerConverter::GetM, euler_converter.cc:133-148 */
 static spmat eu_M(const double xyz[3]) {
@@ -666,6 +966,7 @@ static spmat eu_Mdot(const double xyz[3], const double xyzd[3]) {
 }
 /* GetRotationMatrixBaseToWorld(t), euler_converter.cc:200-205 -> dense + sparseView(1,-1) */
 static void eu_R_t(const Euler* e, double t, double R[3][3]) {
+  if (e->rotvec) { rv_R_t(e, t, R); return; }
   double st[3][3]; spline_point(e->euler, t, st);
   euler_R(st[kPos], R);
 }
@@ -673,10 +974,12 @@ static spmat eu_R_sparse(const double R[3][3]) { return sp_from_dense(3, 3, &R[0
 
 /* GetAngularVelocityInWorld, :58-70 ; GetAngularAccelerationInWorld, :72-83 */
 static void eu_omega(const Euler* e, double t, double w[3]) {
+  if (e->rotvec) { rv_omega(e, t, w); return; }
   double st[3][3]; spline_point(e->euler, t, st);
   spmat M = eu_M(st[kPos]); sp_mul_vec(&M, st[kVel], w); sp_free(&M);
 }
 static void eu_omega_dot(const Euler* e, double t, double wd[3]) {
+  if (e->rotvec) { rv_omega_dot(e, t, wd); return; }
   double st[3][3]; spline_point(e->euler, t, st);
   spmat Md = eu_Mdot(st[kPos], st[kVel]), M = eu_M(st[kPos]);
   double a[3], b[3];
@@ -754,6 +1057,7 @@ static spmat eu_dMdot(const Euler* e, double t, int dim) {
 
 /* EulerConverter::GetDerivOfAngVelWrtNodes, euler_converter.cc:85-102 */
 static spmat eu_d_angvel(const Euler* e, double t) {
+  if (e->rotvec) return rv_d_angvel(e, t);
   spmat jac = sp_copy(&e->jac_struct);
   double st[3][3]; spline_point(e->euler, t, st);
   spmat vel = sp_from_dense(1, 3, st[kVel], 1);
@@ -774,6 +1078,7 @@ static spmat eu_d_angvel(const Euler* e, double t) {
 
 /* EulerConverter::GetDerivOfAngAccWrtNodes, euler_converter.cc:104-131 */
 static spmat eu_d_angacc(const Euler* e, double t) {
+  if (e->rotvec) return rv_d_angacc(e, t);
   spmat jac = sp_copy(&e->jac_struct);
   double st[3][3]; spline_point(e->euler, t, st);
   spmat vel = sp_from_dense(1, 3, st[kVel], 1);
@@ -819,6 +1124,7 @@ static void eu_dR(const Euler* e, double t, spmat Rd[3][3]) {
 
 /* EulerConverter::DerivOfRotVecMult, euler_converter.cc:223-239 */
 static spmat eu_d_rotvec(const Euler* e, double t, const double v[3], int inverse) {
+  if (e->rotvec) return rv_d_rotvec(e, t, v, inverse);
   spmat Rd[3][3]; eu_dR(e, t, Rd);
   spmat jac = sp_copy(&e->jac_struct);
   for (int row = X; row <= Z; ++row)
@@ -1623,7 +1929,7 @@ static void set_err(char* err, int len, const char* msg) { if (err && len > 0) {
 
 oracle_t* oracle_create(const towr_problem_desc_t* d, char* err, int errlen) {
   if (!d || d->abi_version != TOWR_GPU_ABI_VERSION) { set_err(err, errlen, "bad abi version"); return NULL; }
-  if (d->angular_rep != 0) { set_err(err, errlen, "only EulerZYX supported"); return NULL; }
+  if (d->angular_rep != 0 && d->angular_rep != 1) { set_err(err, errlen, "angular_rep must be 0 (EulerZYX) or 1 (RotationVector)"); return NULL; }
   int E = d->robot.n_ee;
   if (E < 1 || E > MAXE) { set_err(err, errlen, "bad n_ee"); return NULL; }
   oracle_t* o = (oracle_t*)calloc(1, sizeof(oracle_t));
@@ -1699,7 +2005,8 @@ oracle_t* oracle_create(const towr_problem_desc_t* d, char* err, int errlen) {
     }
   }
   o->euler.euler = o->s_ang;
-  o->euler.jac_struct = sp_zero(3, o->base_ang->n_rows);   /* euler_converter.cc:38-42 */
+  o->euler.jac_struct = sp_zero(3, o->base_ang->n_rows);   /* euler_converter.cc:38-42, rotvec_converter.cc:12-16 */
+  o->euler.rotvec = d->angular_rep == 1;                     /* nlp_formulation.cc:113-116 */
 
   /* ---- model (SingleRigidBodyDynamics ctor + BuildInertiaTensor, :36-74) ---- */
   o->model.m = rb->mass; o->model.g = rb->gravity; o->model.n_ee = E;
@@ -2147,6 +2454,14 @@ void oracle_kat_euler(const double th[3], const double thd[3], const double thdd
   sp_mul_vec(&M, thd, w); sp_mul_vec(&Md, thd, a); sp_mul_vec(&M, thdd, b);
   for (int k = 0; k < 3; ++k) wd[k] = a[k] + b[k];
   sp_free(&M); sp_free(&Md);
+}
+/* RotVecConverter: R = Rodrigues(theta) (row-major), omega = J_L theta_dot, omega_dot = J_L_dot theta_dot + J_L theta_ddot */
+void oracle_kat_rotvec(const double th[3], const double thd[3], const double thdd[3], double R[9], double w[3], double wd[3]) {
+  double Rm[3][3], J[3][3], Jd[3][3], a[3], b[3];
+  rv_rodrigues(th, Rm); memcpy(R, Rm, sizeof Rm);
+  rv_left_jac(th, J); rv_left_jac_dot(th, thd, Jd);
+  m3_vec(J, thd, w); m3_vec(Jd, thd, a); m3_vec(J, thdd, b);
+  for (int k = 0; k < 3; ++k) wd[k] = a[k] + b[k];
 }
 /* SingleRigidBodyDynamics::GetDynamicViolation for n_ee contacts */
 void oracle_kat_srbd(double m, double g, const double inertia[6], int n_ee, const double com[3], const double com_acc[3],

@@ -27,7 +27,17 @@ def config_descs():
         "anymal_gait_torque": _with_next_tier(F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.StairsID),
                                                             optimize_timings=True), hard=False),
         "hyq_gap_torque": _with_next_tier(_hyq_formulation(F.HeightMap.GapID)),
+        # RotVecConverter base orientation
+        "anymal_trot_rotvec": _rotvec(F.anymal_trot()).to_desc(),
+        "biped_gaitopt_rotvec": _rotvec(_gaitopt_f(F.biped_walk())).to_desc(),
+        "hopper_next_rotvec": _with_next_tier(_rotvec(F.monoped_hopper()), eelin=False),
+        "monoped_backflip_rotvec": F.backflip_desc(),                            # backflip_example.cc
     }
+
+
+def _rotvec(f):
+    f.params_.angular_rep_ = 1
+    return f
 
 
 def _hyq_formulation(tid):
@@ -107,6 +117,9 @@ def cost_descs():
         "biped_gaitopt_costs": _with_costs(_gaitopt_f(F.biped_walk()), torque_weight=2.0).to_desc(),
         "hopper_forces_motion": _with_costs(F.monoped_hopper(), costs=[(C.ForcesCostID, 1.0), (C.EEMotionCostID, 1.0)],
                                             ee_base_pos=False).to_desc(),
+        "anymal_rotvec_costs": _with_costs(_rotvec(F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.StairsID),
+                                                                 optimize_timings=True))).to_desc(),
+        "monoped_backflip_rotvec": F.backflip_desc(),
         "anymal_slope_yaw_costs": _with_costs(F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.SlopeID),
                                                             goal=(1.8, 0.3, 0.0), goal_yaw=0.3)).to_desc(),
     }

@@ -25,7 +25,13 @@ def _anymal_costs():
     return _with_costs(F.anymal_trot()).to_desc()
 
 
-CFGS = {"anymal": lambda: F.anymal_trot().to_desc(), "biped": lambda: F.biped_walk().to_desc(),
+def _anymal_rotvec():
+    f = F.anymal_trot()
+    f.params_.angular_rep_ = 1
+    return f.to_desc()
+
+
+CFGS = {"anymal_rotvec": _anymal_rotvec, "anymal": lambda: F.anymal_trot().to_desc(), "biped": lambda: F.biped_walk().to_desc(),
         "hopper": lambda: F.monoped_hopper().to_desc(), "biped_next": _biped_next, "anymal_costs": _anymal_costs}
 
 

@@ -163,3 +163,43 @@ def test_terrain_hard_cap_quirk_is_present():
             fd = (o.eval_g(xp) - o.eval_g(xm)) / (2 * h)
             worst = max(worst, np.abs(fd - J[:, j])[rows].max())
     assert worst > 1e-3
+
+
+@pytest.mark.parametrize("name", ["anymal_trot_rotvec", "monoped_backflip_rotvec", "hopper_next_rotvec"])
+def test_fd_consistency_rotvec(name):
+    """RotVecConverter Jacobians (DerivOfRotVecMult, GetDerivOfAngVel/AccWrtNodes): FD-consistent at a
+    generic x (rotation vectors away from 0; the backflip's reach 2 pi). TerrainHard rows are left to
+    their own tests (quirk A22 iii)."""
+    desc = CONFIGS[name]
+    o = Oracle(desc)
+    x = o.initial_x() + 0.05 * np.random.default_rng(17).standard_normal(o.n)
+    _fd_check(desc, x, tol=5e-5, skip_rows=_rows_of(desc, o, capi.C_TERRAIN_HARD))
+
+
+def test_rotvec_zero_angle_quirk():
+    """At a rotation vector of exactly 0 (|theta| < kEps: every x0 that starts level) the reference's
+    GetDerivJLdotwrtNodes zeroes d(alpha_dot)/d nodes (rotvec_converter.cc:419-423), although
+    alpha_dot = -theta . theta_dot / 3 there: d omega_dot / d theta misses -theta_dot theta_dot^T / 3.
+    The oracle and the engine keep the reference's value; FD sees the true one."""
+    desc = CONFIGS["monoped_backflip_rotvec"]
+    o = Oracle(desc)
+    x = o.initial_x()
+    r, c, v = o.eval_jac(x)
+    J = sp.csr_matrix((v, (r, c)), shape=(o.m, o.n)).toarray()
+    a0 = [c0 for i, (c0, n) in enumerate(o.varset_cols()) if desc.varsets[i].kind == capi.VAR_BASE_ANG][0]
+    thd = x[a0 + 3:a0 + 6]          # node 0 velocity (NodesVariablesAll: p xyz, v xyz)
+    Ib = np.array(desc.robot.inertia[:])
+    I = np.array([[Ib[0], -Ib[3], -Ib[4]], [-Ib[3], Ib[1], -Ib[5]], [-Ib[4], -Ib[5], Ib[2]]])   # R = I at theta = 0
+    expect = -I @ np.outer(thd, thd) / 3.0
+    h = 1e-6
+    # the flip turns about y: the missing term sits in column theta_y. (FD across theta = 0 in x and z
+    # meets the reference's cancellation in beta = (theta - sin theta) / theta^3 at |theta| ~ h.)
+    for l in (1,):
+        j = a0 + l
+        xp, xm = x.copy(), x.copy()
+        xp[j] += h
+        xm[j] -= h
+        fd = (o.eval_g(xp) - o.eval_g(xm)) / (2 * h)
+        # Dynamic rows AX..AZ at t = 0 (constraint 0, instant 0): node 0 carries the whole basis there
+        np.testing.assert_allclose(fd[0:3] - J[0:3, j], expect[:, l], rtol=1e-5, atol=1e-6)
+    assert abs(expect[1, 1]) > 1.0

@@ -180,3 +180,35 @@ def test_normalized_basis_derivative_quirk_is_reproduced():
     L.oracle_kat_terrain(C.byref(t), 1.1, 0.0, _p(out_h), _p(bs), _p(dbs))
     exact_n = np.array([float(v.subs(xs, 1.1)) for v in exact])
     assert np.abs(dbs[0:3] - exact_n).max() > 1e-3
+
+
+# RotVecConverter (rotvec_converter.cc): R(t) = exp([theta(t)]x) by the Rodrigues series in sympy,
+# omega from dR/dt R^T = [omega]x and its time derivative: independent of J_L and J_L_dot
+_th = sp.symbols("a0:3")
+_thd = sp.symbols("b0:3")
+_thdd = sp.symbols("c0:3")
+_tt = sp.symbols("tt")
+_thet = [_th[i] + _thd[i] * _tt + _thdd[i] * _tt**2 / 2 for i in range(3)]
+_K = sp.Matrix([[0, -_thet[2], _thet[1]], [_thet[2], 0, -_thet[0]], [-_thet[1], _thet[0], 0]])
+_n = sp.sqrt(_thet[0]**2 + _thet[1]**2 + _thet[2]**2)
+_Rt = sp.eye(3) + sp.sin(_n) / _n * _K + (1 - sp.cos(_n)) / _n**2 * _K * _K
+_Om = sp.diff(_Rt, _tt) * _Rt.T
+_w = sp.Matrix([_Om[2, 1], _Om[0, 2], _Om[1, 0]])
+_F_RV = sp.lambdify((_th, _thd, _thdd), [_Rt.subs(_tt, 0), _w.subs(_tt, 0), sp.diff(_w, _tt).subs(_tt, 0)])
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_rotvec_kat(seed):
+    L = O.lib()
+    L.oracle_kat_rotvec.argtypes = [D, D, D, D, D, D]
+    rng = np.random.default_rng(100 + seed)
+    scale = [0.05, 0.5, 1.5, 3.0, 5.5, 2.0 * np.pi - 0.1][seed]   # up to a full flip
+    th = rng.standard_normal(3)
+    th = _a(*(th / np.linalg.norm(th) * scale))
+    thd, thdd = _a(*rng.normal(0, 2.0, 3)), _a(*rng.normal(0, 5.0, 3))
+    R, w, wd = np.zeros(9), np.zeros(3), np.zeros(3)
+    L.oracle_kat_rotvec(_p(th), _p(thd), _p(thdd), _p(R), _p(w), _p(wd))
+    Rr, wr, wdr = _F_RV(th, thd, thdd)
+    np.testing.assert_allclose(R.reshape(3, 3), np.array(Rr, dtype=float), rtol=0, atol=1e-13)
+    np.testing.assert_allclose(w, np.array(wr, dtype=float).ravel(), rtol=1e-11, atol=1e-12)
+    np.testing.assert_allclose(wd, np.array(wdr, dtype=float).ravel(), rtol=1e-10, atol=1e-10)

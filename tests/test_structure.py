@@ -49,8 +49,8 @@ def test_initial_x_for_matches_fresh_layout():
 
 def test_unsupported_and_invalid():
     d = F.anymal_trot().to_desc()
-    d.angular_rep = 1                      # RotVec: next tier
-    with pytest.raises(TowrGpuError, match="-2"):
+    d.angular_rep = 2                      # neither EulerZYX (0) nor RotationVector (1)
+    with pytest.raises(TowrGpuError, match="-1"):
         TowrGpuProblem(d, device=-1)
     d = F.anymal_trot(optimize_timings=True).to_desc()
     d.n_varsets -= 1                       # drop a schedule set while optimising timings

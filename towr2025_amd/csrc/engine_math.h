@@ -146,6 +146,7 @@ struct Ctx {
   RobotC rb;
   int32_t fdisc_motion;         // ForceConstraintDiscretized motion block enabled (terrain has d2h)
   bool gait;                    // phase-duration optimisation (a compile-time constant in kernels)
+  bool rotvec;                  // Parameters::RotationVector base orientation (compile-time in kernels)
   const PolyPhase* pinfo;
   const PhaseCol* pcols;
   const SchedInfo* sched;       // per endeffector
@@ -477,6 +478,218 @@ TG_HD void mat3_vec(const double A[3][3], const double v[3], double o[3]) {
 }
 
 // ----------------------------------------------------------------------------------------------
+// RotVecConverter (towr/src/helpers/rotvec_converter.cc): theta = rotation vector, R = exp([theta]x),
+// omega = J_L theta_dot, omega_dot = J_L_dot theta_dot + J_L theta_ddot.
+// Every Jacobian w.r.t. the base-angular nodes is returned in coefficient form: the entry at the
+// basis column (b, axis l) is P[r][l] Hp[b] + V[r][l] Hv[b] + A[r][l] Ha[b], because each spline
+// Jacobian row l of the reference (GetJacobianWrtNodes(t, kPos|kVel|kAcc).row(l)) is the basis of
+// axis l. The reference's skip rules (|.| > 1e-15) and its small-angle branches are kept.
+// ----------------------------------------------------------------------------------------------
+constexpr double kRvEps = 1e-10;   // kEps, rotvec_converter.cc:10
+struct RvCoeffs { double alpha, beta, gamma, dalpha, dbeta, dgamma; };
+TG_HD double rv_norm(const double v[3]) { return sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); }
+// ComputeCoeffs (:30-59)
+TG_HD RvCoeffs rv_coeffs(double theta) {
+  RvCoeffs c;
+  const double t2 = theta * theta;
+  if (theta < kRvEps) {
+    c.alpha = 1.0 - t2 / 6.0; c.beta = 1.0 / 6.0 - t2 / 120.0; c.gamma = 0.5 - t2 / 24.0;
+    c.dalpha = -theta / 3.0; c.dbeta = -theta / 60.0; c.dgamma = -theta / 12.0;
+  } else {
+    const double st = sin(theta), ct = cos(theta), t3 = t2 * theta, t4 = t3 * theta;
+    c.alpha = st / theta; c.beta = (theta - st) / t3; c.gamma = (1.0 - ct) / t2;
+    c.dalpha = (theta * ct - st) / t2;
+    c.dbeta = (-2.0 * theta - theta * ct + 3.0 * st) / t4;
+    c.dgamma = (theta * st - 2.0 + 2.0 * ct) / t3;
+  }
+  return c;
+}
+TG_HD void rv_skew(const double v[3], double S[3][3]) {   // Skew (:20-28)
+  S[0][0] = 0.0;   S[0][1] = -v[2]; S[0][2] = v[1];
+  S[1][0] = v[2];  S[1][1] = 0.0;   S[1][2] = -v[0];
+  S[2][0] = -v[1]; S[2][1] = v[0];  S[2][2] = 0.0;
+}
+TG_HD void m3_mul(const double A[3][3], const double B[3][3], double C[3][3]) {   // C may not alias
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) C[i][j] = A[i][0] * B[0][j] + A[i][1] * B[1][j] + A[i][2] * B[2][j];
+}
+// Rodrigues (:61-72)
+TG_HD void rv_rodrigues(const double rv[3], double R[3][3]) {
+  const double theta = rv_norm(rv);
+  double K[3][3]; rv_skew(rv, K);
+  if (theta < kRvEps) {
+    for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) R[i][j] = (i == j ? 1.0 : 0.0) + K[i][j];
+    return;
+  }
+  const double sn = sin(theta) / theta, h = (1.0 - cos(theta)) / (theta * theta);
+  double KK[3][3]; m3_mul(K, K, KK);
+  for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) R[i][j] = ((i == j ? 1.0 : 0.0) + sn * K[i][j]) + h * KK[i][j];
+}
+// LeftJacobian (:74-85)
+TG_HD void rv_left_jac(const double rv[3], double J[3][3]) {
+  const double theta = rv_norm(rv);
+  double S[3][3]; rv_skew(rv, S);
+  if (theta < kRvEps) {
+    for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) J[i][j] = (i == j ? 1.0 : 0.0) + 0.5 * S[i][j];
+    return;
+  }
+  const RvCoeffs c = rv_coeffs(theta);
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) J[i][j] = (c.alpha * (i == j ? 1.0 : 0.0) + c.beta * (rv[i] * rv[j])) + c.gamma * S[i][j];
+}
+// LeftJacobianDot (:87-107)
+TG_HD void rv_left_jac_dot(const double rv[3], const double rvd[3], double J[3][3]) {
+  const double theta = rv_norm(rv);
+  double S[3][3], Sd[3][3]; rv_skew(rv, S); rv_skew(rvd, Sd);
+  if (theta < kRvEps) {
+    for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) J[i][j] = 0.5 * Sd[i][j];
+    return;
+  }
+  const RvCoeffs c = rv_coeffs(theta);
+  const double td = (rv[0] * rvd[0] + rv[1] * rvd[1] + rv[2] * rvd[2]) / theta;
+  const double ad = c.dalpha * td, bd = c.dbeta * td, gd = c.dgamma * td;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      J[i][j] = (((ad * (i == j ? 1.0 : 0.0) + bd * (rv[i] * rv[j])) + c.beta * (rvd[i] * rv[j] + rv[i] * rvd[j])) + gd * S[i][j]) + c.gamma * Sd[i][j];
+}
+TG_HD double rv_sign(int dim, int j) { return ((j - dim + 3) % 3 == 1) ? -1.0 : 1.0; }   // [theta]x_{dim,j} = sign theta_k
+
+// GetDerivJLwrtNodes (:235-325) for all three rows dim: P[dim][j][l] = d J_L[dim][j] / d theta_l
+TG_HD void rv_dJL(const double rv[3], double P[3][3][3]) {
+  const double theta = rv_norm(rv);
+  const RvCoeffs c = rv_coeffs(theta);
+  double nh[3] = {0.0, 0.0, 0.0};   // theta^T jac_pos / theta, components with |theta_l| > 1e-15
+  if (theta >= kRvEps) {
+    const double inv = 1.0 / theta;
+    for (int l = 0; l < 3; ++l) nh[l] = fabs(rv[l]) > 1e-15 ? rv[l] * inv : 0.0;
+  }
+  double Sk[3][3]; rv_skew(rv, Sk);
+  for (int dim = 0; dim < 3; ++dim)
+    for (int j = 0; j < 3; ++j) {
+      double* p = P[dim][j];
+      p[0] = p[1] = p[2] = 0.0;
+      if (dim == j) for (int l = 0; l < 3; ++l) p[l] += c.dalpha * nh[l];
+      const double rvdj = rv[dim] * rv[j];
+      if (fabs(rvdj) > 1e-15) for (int l = 0; l < 3; ++l) p[l] += rvdj * (c.dbeta * nh[l]);
+      if (fabs(c.beta) > 1e-15) {
+        if (fabs(rv[j]) > 1e-15) p[dim] += c.beta * rv[j];
+        if (fabs(rv[dim]) > 1e-15) p[j] += c.beta * rv[dim];
+      }
+      const double sk = Sk[dim][j];
+      if (fabs(sk) > 1e-15) for (int l = 0; l < 3; ++l) p[l] += sk * (c.dgamma * nh[l]);
+      if (fabs(c.gamma) > 1e-15 && dim != j) p[3 - dim - j] += c.gamma * rv_sign(dim, j);
+    }
+}
+
+// d omega / d nodes (GetDerivOfAngVelWrtNodes, :508-528): Pw (theta), Vw (theta_dot)
+TG_HD void rv_angvel_jac(const double rv[3], const double rvd[3], double Pw[3][3], double Vw[3][3]) {
+  double P[3][3][3]; rv_dJL(rv, P);
+  rv_left_jac(rv, Vw);
+  for (int dim = 0; dim < 3; ++dim)
+    for (int l = 0; l < 3; ++l) Pw[dim][l] = rvd[0] * P[dim][0][l] + rvd[1] * P[dim][1][l] + rvd[2] * P[dim][2][l];
+}
+
+// d omega_dot / d nodes (GetDerivOfAngAccWrtNodes :530-561 with GetDerivJLdotwrtNodes :327-506):
+// Pa (theta), Va (theta_dot), Aa (theta_ddot)
+TG_HD void rv_angacc_jac(const double rv[3], const double rvd[3], const double rva[3], double Pa[3][3], double Va[3][3],
+                         double Aa[3][3]) {
+  const double theta = rv_norm(rv);
+  const RvCoeffs c = rv_coeffs(theta);
+  double td = 0.0;
+  if (theta > kRvEps) td = (rv[0] * rvd[0] + rv[1] * rvd[1] + rv[2] * rvd[2]) / theta;
+  const double beta_dot = c.dbeta * td, gamma_dot = c.dgamma * td;
+  // d(alpha_dot), d(beta_dot), d(gamma_dot) / d nodes: (theta part, theta_dot part); n_hat
+  double nh[3] = {0.0, 0.0, 0.0}, dap[3] = {0, 0, 0}, dav[3] = {0, 0, 0}, dbp[3] = {0, 0, 0}, dbv[3] = {0, 0, 0},
+         dgp[3] = {0, 0, 0}, dgv[3] = {0, 0, 0};
+  if (theta > kRvEps) {
+    const double inv = 1.0 / theta, t2 = theta * theta, st = sin(theta), ct = cos(theta);
+    double dtp[3], dtv[3];   // d theta_dot_angle / d (theta, theta_dot)
+    for (int l = 0; l < 3; ++l) { nh[l] = rv[l] * inv; dtp[l] = rvd[l] * inv - (td * inv) * nh[l]; dtv[l] = rv[l] * inv; }
+    const double alpha_pp = (-theta * st - 2.0 * (theta * ct - st) / theta) / t2;
+    double beta_pp, gamma_pp;
+    { const double num = -2.0 * theta - theta * ct + 3.0 * st, dnum = -2.0 - ct + theta * st + 3.0 * ct;
+      beta_pp = (dnum - 4.0 * num / theta) / (t2 * t2); }
+    { const double num = theta * st - 2.0 + 2.0 * ct, dnum = st + theta * ct - 2.0 * st;
+      gamma_pp = (dnum - 3.0 * num / theta) / (t2 * theta); }
+    for (int l = 0; l < 3; ++l) {
+      dap[l] = (alpha_pp * td) * nh[l] + c.dalpha * dtp[l]; dav[l] = c.dalpha * dtv[l];
+      dbp[l] = (beta_pp * td) * nh[l] + c.dbeta * dtp[l];   dbv[l] = c.dbeta * dtv[l];
+      dgp[l] = (gamma_pp * td) * nh[l] + c.dgamma * dtp[l]; dgv[l] = c.dgamma * dtv[l];
+    }
+  }
+  double Sk[3][3], Skd[3][3]; rv_skew(rv, Sk); rv_skew(rvd, Skd);
+  double JLd[3][3]; rv_left_jac_dot(rv, rvd, JLd);
+  double P1[3][3][3]; rv_dJL(rv, P1);   // acc * dJL_du
+  rv_left_jac(rv, Aa);
+  for (int dim = 0; dim < 3; ++dim) {
+    double pa[3] = {0, 0, 0}, va[3] = {0, 0, 0};
+    for (int j = 0; j < 3; ++j) {
+      double p[3] = {0, 0, 0}, v[3] = {0, 0, 0};   // d J_L_dot[dim][j] / d (theta, theta_dot)
+      if (dim == j) for (int l = 0; l < 3; ++l) { p[l] += dap[l]; v[l] += dav[l]; }
+      const double rv_dj = rv[dim] * rv[j];
+      if (fabs(rv_dj) > 1e-15) for (int l = 0; l < 3; ++l) { p[l] += rv_dj * dbp[l]; v[l] += rv_dj * dbv[l]; }
+      if (fabs(beta_dot) > 1e-15) {
+        if (fabs(rv[j]) > 1e-15) p[dim] += beta_dot * rv[j];
+        if (fabs(rv[dim]) > 1e-15) p[j] += beta_dot * rv[dim];
+      }
+      const double td_dj = rvd[dim] * rv[j] + rv[dim] * rvd[j];
+      if (fabs(td_dj) > 1e-15 && fabs(c.beta) > 1e-15 && theta > kRvEps) for (int l = 0; l < 3; ++l) p[l] += (c.dbeta * td_dj) * nh[l];
+      if (fabs(c.beta) > 1e-15) {
+        if (fabs(rv[j]) > 1e-15) v[dim] += c.beta * rv[j];
+        if (fabs(rvd[dim]) > 1e-15) p[j] += c.beta * rvd[dim];
+        if (fabs(rvd[j]) > 1e-15) p[dim] += c.beta * rvd[j];
+        if (fabs(rv[dim]) > 1e-15) v[j] += c.beta * rv[dim];
+      }
+      const double sk = Sk[dim][j];
+      if (fabs(sk) > 1e-15) for (int l = 0; l < 3; ++l) { p[l] += sk * dgp[l]; v[l] += sk * dgv[l]; }
+      if (fabs(gamma_dot) > 1e-15 && dim != j) p[3 - dim - j] += gamma_dot * rv_sign(dim, j);
+      const double skd = Skd[dim][j];
+      if (fabs(skd) > 1e-15 && fabs(c.gamma) > 1e-15 && theta > kRvEps) for (int l = 0; l < 3; ++l) p[l] += (c.dgamma * skd) * nh[l];
+      if (fabs(c.gamma) > 1e-15 && dim != j) v[3 - dim - j] += c.gamma * rv_sign(dim, j);
+      for (int l = 0; l < 3; ++l) { pa[l] += rvd[j] * p[l]; va[l] += rvd[j] * v[l]; }
+    }
+    for (int l = 0; l < 3; ++l) {
+      Pa[dim][l] = pa[l] + (rva[0] * P1[dim][0][l] + rva[1] * P1[dim][1][l] + rva[2] * P1[dim][2][l]);
+      Va[dim][l] = va[l] + JLd[dim][l];
+    }
+  }
+}
+
+// DerivOfRotVecMult (:210-233) coefficient matrix: d(R v)/dtheta = -[R v]x J_L (forward),
+// d(R^T v)/dtheta = R^T [v]x J_L (inverse)
+TG_HD void rv_rotvec_mult(const double R[3][3], const double JL[3][3], const double v[3], bool inverse, double A[3][3]) {
+  double S[3][3], T[3][3];
+  if (inverse) {
+    double Rt[3][3];
+    for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) Rt[i][j] = R[j][i];
+    rv_skew(v, S); m3_mul(Rt, S, T); m3_mul(T, JL, A);
+  } else {
+    double Rv[3]; mat3_vec(R, v, Rv);
+    rv_skew(Rv, S);
+    for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) S[i][j] = -S[i][j];
+    m3_mul(S, JL, A);
+  }
+}
+
+// RotVec R, omega, omega_dot (GetRotationMatrixBaseToWorld / GetAngularVelocityInWorld /
+// GetAngularAccelerationInWorld, :118-138)
+TG_HD void rv_state(const SplinePt& A, double R[3][3], double w[3], double wd[3]) {
+  double JL[3][3], JLd[3][3], a[3], b[3];
+  rv_rodrigues(A.p, R);
+  rv_left_jac(A.p, JL);
+  rv_left_jac_dot(A.p, A.v, JLd);
+  mat3_vec(JL, A.v, w);
+  mat3_vec(JLd, A.v, a); mat3_vec(JL, A.a, b);
+  for (int k = 0; k < 3; ++k) wd[k] = a[k] + b[k];
+}
+
+// base orientation at a spline point: R (base to world)
+TG_HD void base_rot(const Ctx& c, const SplinePt& A, double R[3][3]) {
+  if (c.rotvec) rv_rodrigues(A.p, R);
+  else euler_R(trig(A.p), R);
+}
+
+// ----------------------------------------------------------------------------------------------
 // terrain (towr/src/terrain/height_map.cc, height_map_examples.cc)
 // ----------------------------------------------------------------------------------------------
 TG_HD double ter_h(const towr_terrain_t& T, double x, double y) {
@@ -625,9 +838,13 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
     // g (GetDynamicViolation :76-102) + d/d base-lin (GetJacobianWrtBaseLin :104-122)
     SplinePt L; spline_eval(c, SP_BASE_LIN, t, L);
     SplinePt A; spline_eval(c, SP_BASE_ANG, t, A);
-    const Trig q = trig(A.p);
-    double R[3][3]; euler_R(q, R);
-    double w[3], wd[3]; euler_w_wd(q, A.v, A.a, w, wd);
+    double R[3][3], w[3], wd[3];
+    if (c.rotvec) rv_state(A, R, w, wd);
+    else {
+      const Trig q = trig(A.p);
+      euler_R(q, R);
+      euler_w_wd(q, A.v, A.a, w, wd);
+    }
     double fs[3] = {0, 0, 0}, ts[3] = {0, 0, 0};
 #pragma unroll 1
     for (int ee = 0; ee < E; ++ee) {
@@ -660,6 +877,65 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
       }
     for (int e = 0; e < 3; ++e)
       for (int bb = 0; bb < 4; ++bb) em(r0 + LX + e, basis_col(c, SP_BASE_LIN, L.poly, bb, e), c.rb.m * Ha[bb], true);
+    return;
+  }
+  if (it.group == 1 && c.rotvec) {
+    // d/d base-ang, RotVecConverter (GetJacobianWrtBaseAng :124-166 with the converter's
+    // DerivOfRotVecMult / GetDerivOfAngVelWrtNodes / GetDerivOfAngAccWrtNodes), coefficient form:
+    //   jac1 = d(R v11)/. + R I_b d(R^T wd)/. + I_w d wd/.
+    //   jac2 = [w]x (d(R v21)/. + R I_b d(R^T w)/. + I_w d w/.) - [I_w w]x d w/.
+    SplinePt A; spline_eval(c, SP_BASE_ANG, t, A);
+    double R[3][3], w[3], wd[3];
+    rv_state(A, R, w, wd);
+    double JL[3][3]; rv_left_jac(A.p, JL);
+    double RI[3][3], Iw[3][3];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) RI[i][j] = R[i][0] * c.rb.Ib[0 * 3 + j] + R[i][1] * c.rb.Ib[1 * 3 + j] + R[i][2] * c.rb.Ib[2 * 3 + j];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) Iw[i][j] = RI[i][0] * R[j][0] + RI[i][1] * R[j][1] + RI[i][2] * R[j][2];
+    double Mp[3][3], Mv[3][3], Ma[3][3];
+    {
+      double Pw[3][3], Vw[3][3], Pa[3][3], Va[3][3], Aa[3][3], T1[3][3], T2[3][3], T3[3][3];
+      rv_angvel_jac(A.p, A.v, Pw, Vw);
+      rv_angacc_jac(A.p, A.v, A.a, Pa, Va, Aa);
+      double u[3], v11[3], v21[3];
+      for (int j = 0; j < 3; ++j) u[j] = R[0][j] * wd[0] + R[1][j] * wd[1] + R[2][j] * wd[2];
+      for (int i = 0; i < 3; ++i) v11[i] = c.rb.Ib[i * 3 + 0] * u[0] + c.rb.Ib[i * 3 + 1] * u[1] + c.rb.Ib[i * 3 + 2] * u[2];
+      for (int j = 0; j < 3; ++j) u[j] = R[0][j] * w[0] + R[1][j] * w[1] + R[2][j] * w[2];
+      for (int i = 0; i < 3; ++i) v21[i] = c.rb.Ib[i * 3 + 0] * u[0] + c.rb.Ib[i * 3 + 1] * u[1] + c.rb.Ib[i * 3 + 2] * u[2];
+      // jac1, theta part
+      rv_rotvec_mult(R, JL, v11, false, Mp);
+      rv_rotvec_mult(R, JL, wd, true, T1); m3_mul(RI, T1, T2);
+      m3_mul(Iw, Pa, T3);
+      for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) Mp[i][j] = (Mp[i][j] + T2[i][j]) + T3[i][j];
+      // jac2 inner sum, theta part
+      double S[3][3];
+      rv_rotvec_mult(R, JL, v21, false, S);
+      rv_rotvec_mult(R, JL, w, true, T1); m3_mul(RI, T1, T2);
+      m3_mul(Iw, Pw, T3);
+      for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) S[i][j] = (S[i][j] + T2[i][j]) + T3[i][j];
+      double Iww[3]; mat3_vec(Iw, w, Iww);
+      for (int r = 0; r < 3; ++r)
+        for (int e = 0; e < 3; ++e) {
+          double a = 0.0, b = 0.0, av = 0.0, bv = 0.0;
+          for (int k = 0; k < 3; ++k) {
+            const double cw = cross_el(w, r, k), ci = cross_el(Iww, r, k);
+            a += cw * S[k][e]; b += ci * Pw[k][e];
+            double iv = Iw[k][0] * Vw[0][e] + Iw[k][1] * Vw[1][e] + Iw[k][2] * Vw[2][e];
+            av += cw * iv; bv += ci * Vw[k][e];
+          }
+          Mp[r][e] += a - b;
+          Mv[r][e] = (Iw[r][0] * Va[0][e] + Iw[r][1] * Va[1][e] + Iw[r][2] * Va[2][e]) + (av - bv);
+          Ma[r][e] = Iw[r][0] * Aa[0][e] + Iw[r][1] * Aa[1][e] + Iw[r][2] * Aa[2][e];
+        }
+    }
+    double Hp[4], Hv[4], Ha[4];
+    spline_basis(A, kPos, Hp); spline_basis(A, kVel, Hv); spline_basis(A, kAcc, Ha);
+#pragma unroll 1
+    for (int e = 0; e < 3; ++e)
+      for (int r = 0; r < 3; ++r)
+        for (int bb = 0; bb < 4; ++bb)
+          em(r0 + AX + r, basis_col(c, SP_BASE_ANG, A.poly, bb, e), Mp[r][e] * Hp[bb] + Mv[r][e] * Hv[bb] + Ma[r][e] * Ha[bb], true);
     return;
   }
   if (it.group == 1) {
@@ -789,10 +1065,20 @@ TG_HD void eval_rom(const Ctx& c, const ItemDesc& it, Emit& em) {
   spline_eval(c, SP_BASE_LIN, t, L);
   spline_eval(c, SP_BASE_ANG, t, A);
   spline_eval(c, sp_motion(ee), t, P);
-  const Trig q = trig(A.p);
-  double R[3][3]; euler_R(q, R);
+  double R[3][3]; base_rot(c, A, R);
   const double rW[3] = {P.p[0] - L.p[0], P.p[1] - L.p[1], P.p[2] - L.p[2]};
   double H[4];
+  if (it.group == 1 && c.rotvec) {
+    // DerivOfRotVecMult(t, r_W, inverse = true) of the RotVecConverter: R^T [r_W]x J_L, full pattern
+    double JL[3][3], Am[3][3];
+    rv_left_jac(A.p, JL);
+    rv_rotvec_mult(R, JL, rW, true, Am);
+    spline_basis(A, kPos, H);
+    for (int e = 0; e < 3; ++e)
+      for (int r = 0; r < 3; ++r)
+        for (int bb = 0; bb < 4; ++bb) em(r0 + r, basis_col(c, SP_BASE_ANG, A.poly, bb, e), Am[r][e] * H[bb], true);
+    return;
+  }
   if (it.group == 0) {
     for (int i = 0; i < 3; ++i) em.g(r0 + i, R[0][i] * rW[0] + R[1][i] * rW[1] + R[2][i] * rW[2]);
     spline_basis(L, kPos, H);
@@ -801,6 +1087,7 @@ TG_HD void eval_rom(const Ctx& c, const ItemDesc& it, Emit& em) {
         for (int bb = 0; bb < 4; ++bb) em(r0 + r, basis_col(c, SP_BASE_LIN, L.poly, bb, e), -R[e][r] * H[bb], true);
   } else if (it.group == 1) {
     // DerivOfRotVecMult(t, r_W, inverse=true): row r = sum_c rW[c] dR[c][r]; row X has no roll terms
+    const Trig q = trig(A.p);
     spline_basis(A, kPos, H);
     for (int e = 0; e < 3; ++e) {
       double dR[3][3]; euler_dR_axis(q, e, dR);
@@ -1182,6 +1469,49 @@ TG_HD void cost_energy(const Ctx& c, const CostItem& it, Emit& em) {
   }
 }
 
+// AngularMomentumCost sample with the RotVecConverter: dL = d(R v2)/. + R I_b (d(R^T w)/. + R^T dw/.)
+// (angular_momentum_cost.cc:150-200), v2 = I_b R^T w
+template <class Emit>
+TG_HD void cost_angmom_rotvec(const Ctx& c, const CostItem& it, const SplinePt& A, Emit& em) {
+  double R[3][3], JL[3][3], w[3];
+  rv_rodrigues(A.p, R);
+  rv_left_jac(A.p, JL);
+  mat3_vec(JL, A.v, w);
+  double RI[3][3], Iw[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) RI[i][j] = R[i][0] * c.rb.Ib[0 * 3 + j] + R[i][1] * c.rb.Ib[1 * 3 + j] + R[i][2] * c.rb.Ib[2 * 3 + j];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) Iw[i][j] = RI[i][0] * R[j][0] + RI[i][1] * R[j][1] + RI[i][2] * R[j][2];
+  double L[3]; mat3_vec(Iw, w, L);
+  em.f += it.wdt * dot3(L, L);
+  double m[3];
+  for (int r = 0; r < 3; ++r) m[r] = (2.0 * it.wdt) * L[r];
+  double u[3], v2[3];
+  for (int j = 0; j < 3; ++j) u[j] = R[0][j] * w[0] + R[1][j] * w[1] + R[2][j] * w[2];
+  for (int i = 0; i < 3; ++i) v2[i] = c.rb.Ib[i * 3 + 0] * u[0] + c.rb.Ib[i * 3 + 1] * u[1] + c.rb.Ib[i * 3 + 2] * u[2];
+  double Pw[3][3], Vw[3][3], A1[3][3], A2[3][3];
+  rv_angvel_jac(A.p, A.v, Pw, Vw);
+  rv_rotvec_mult(R, JL, v2, false, A1);
+  rv_rotvec_mult(R, JL, w, true, A2);
+  double Hp[4], Hv[4];
+  spline_basis(A, kPos, Hp);
+  spline_basis(A, kVel, Hv);
+  for (int e = 0; e < 3; ++e) {
+    // m . (A1 + R I_b (A2 + R^T Pw)) [:, e] and m . (R I_b R^T Vw) [:, e]
+    double sp = 0.0, sv = 0.0;
+    for (int i = 0; i < 3; ++i) {
+      double tu[3], tv[3];
+      for (int k = 0; k < 3; ++k) {
+        tu[k] = A2[k][e] + (R[0][k] * Pw[0][e] + R[1][k] * Pw[1][e] + R[2][k] * Pw[2][e]);
+        tv[k] = R[0][k] * Vw[0][e] + R[1][k] * Vw[1][e] + R[2][k] * Vw[2][e];
+      }
+      sp += m[i] * (A1[i][e] + (RI[i][0] * tu[0] + RI[i][1] * tu[1] + RI[i][2] * tu[2]));
+      sv += m[i] * (RI[i][0] * tv[0] + RI[i][1] * tv[1] + RI[i][2] * tv[2]);
+    }
+    for (int bb = 0; bb < 4; ++bb) em(0, basis_col(c, SP_BASE_ANG, A.poly, bb, e), sp * Hp[bb] + sv * Hv[bb], true);
+  }
+}
+
 // AngularMomentumCost sample (angular_momentum_cost.cc:67-208): w dt |L|^2, L = R I_b R^T omega,
 // omega = M(theta) theta_dot. d L / d theta_e = dR I_b R^T w + R I_b dR^T w + I_w dM_e theta_dot;
 // d L / d theta_dot_e = I_w M[:, e]; chained through the Euler spline's position / velocity basis.
@@ -1189,6 +1519,7 @@ template <class Emit>
 TG_HD void cost_angmom(const Ctx& c, const CostItem& it, Emit& em) {
   SplinePt A;
   spline_eval(c, SP_BASE_ANG, it.t, A);
+  if (c.rotvec) { cost_angmom_rotvec(c, it, A, em); return; }
   const Trig q = trig(A.p);
   const double sy = q.sy, cy = q.cy, sz = q.sz, cz = q.cz, xd = A.v[0], yd = A.v[1];
   double R[3][3]; euler_R(q, R);
@@ -1252,8 +1583,7 @@ TG_HD void cost_eebp(const Ctx& c, const CostItem& it, Emit& em) {
   spline_eval(c, SP_BASE_LIN, it.t, L);
   spline_eval(c, SP_BASE_ANG, it.t, A);
   spline_eval(c, sp_motion(ee), it.t, P);
-  const Trig q = trig(A.p);
-  double R[3][3]; euler_R(q, R);
+  double R[3][3]; base_rot(c, A, R);
   const double rW[3] = {P.p[0] - L.p[0], P.p[1] - L.p[1], P.p[2] - L.p[2]};
   double e3[3], m[3], mW[3];
   for (int i = 0; i < 3; ++i) e3[i] = (R[0][i] * rW[0] + R[1][i] * rW[1] + R[2][i] * rW[2]) - it.p[i];
@@ -1267,6 +1597,17 @@ TG_HD void cost_eebp(const Ctx& c, const CostItem& it, Emit& em) {
   for (int j = 0; j < 3; ++j)
     for (int bb = 0; bb < 4; ++bb) em(0, basis_col(c, SP_BASE_LIN, L.poly, bb, j), -mW[j] * H[bb], true);
   spline_basis(A, kPos, H);   // DerivOfRotVecMult(t, r_W, inverse = true)
+  if (c.rotvec) {
+    double JL[3][3], Am[3][3];
+    rv_left_jac(A.p, JL);
+    rv_rotvec_mult(R, JL, rW, true, Am);
+    for (int e = 0; e < 3; ++e) {
+      const double s = m[0] * Am[0][e] + m[1] * Am[1][e] + m[2] * Am[2][e];
+      for (int bb = 0; bb < 4; ++bb) em(0, basis_col(c, SP_BASE_ANG, A.poly, bb, e), s * H[bb], true);
+    }
+    return;
+  }
+  const Trig q = trig(A.p);
   for (int e = 0; e < 3; ++e) {
     double dR[3][3]; euler_dR_axis(q, e, dR);
     double s = 0.0;

@@ -38,6 +38,7 @@ struct Layout {
   std::vector<double> dur;
   std::vector<SegRec> segs;     // (2 + 4 n_ee) records per time instant
   bool gait = false;            // phase-duration optimisation (PhaseSplines, schedule variables)
+  bool rotvec = false;          // Parameters::RotationVector base orientation (RotVecConverter)
   std::vector<PolyPhase> pinfo; // PhaseSpline polynomial phases
   std::vector<PhaseCol> pcols;  // PhaseSpline full-pattern columns
   std::vector<SchedInfo> sched; // per endeffector (col0 = -1 without schedule variables)

@@ -382,7 +382,7 @@ int build_costs(const towr_problem_desc_t& d, const std::vector<double>& base_d,
 
 int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
   if (d.abi_version != TOWR_GPU_ABI_VERSION) { err = "abi version mismatch"; return TOWR_ERR_INVALID; }
-  if (d.angular_rep != 0) { err = "only EulerZYX angular representation is supported (RotVec is next-tier)"; return TOWR_ERR_UNSUPPORTED; }
+  if (d.angular_rep != 0 && d.angular_rep != 1) { err = "angular_rep must be 0 (EulerZYX) or 1 (RotationVector)"; return TOWR_ERR_INVALID; }
   const int E = d.robot.n_ee;
   if (E < 1 || E > TOWR_MAX_EE) { err = "robot.n_ee out of range"; return TOWR_ERR_INVALID; }
   if (!(d.total_time > 0) || !(d.duration_base_polynomial > 0)) { err = "bad total_time / duration_base_polynomial"; return TOWR_ERR_INVALID; }
@@ -396,6 +396,7 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
     if (n < 0) return n;
     L.n = n;
     L.gait = d.optimize_timings != 0;
+    L.rotvec = d.angular_rep == 1;   // nlp_formulation.cc:113-116
   }
 
   // ---- node -> column table, spline metadata, polynomial durations
@@ -635,7 +636,7 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
     cx.x = L.x0.data(); cx.nodecol = L.nodecol.data(); cx.spl = L.spl.data(); cx.dur = L.dur.data();
     cx.ter = &L.terrain; cx.rb = L.rb; cx.fdisc_motion = L.fdisc_motion;
     cx.gait = L.gait; cx.pinfo = L.pinfo.data(); cx.pcols = L.pcols.data(); cx.sched = L.sched.data();
-    cx.eelin = L.eelin.data();
+    cx.eelin = L.eelin.data(); cx.rotvec = L.rotvec;
     for (size_t i = 0; i < L.items.size(); ++i) {
       item_cand_begin[i] = (int32_t)crow.size();
       RecordEmit em{&crow, &ccol, &cpres};

@@ -165,7 +165,7 @@ __device__ __forceinline__ void stage_x(const KParams& P, const double* xg, doub
 // (GAIT) their PhaseSplines evaluate polynomials from the node table, which is then staged too.
 constexpr bool stages_nodes(int type, bool gait) { return gait || is_misc_kind(type); }
 
-template <int TYPE, int BLOCK, bool GAIT>
+template <int TYPE, int BLOCK, bool GAIT, bool ROTVEC>
 __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_kernel(KParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int total = P.B * P.ntiles;
@@ -195,6 +195,7 @@ __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_ker
     c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
     c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
     c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.sched = P.sched; c.eelin = P.eelin;
+    c.rotvec = ROTVEC;
     eval_typed<TYPE>(c, it, em);
     em.flush();
   }
@@ -239,6 +240,7 @@ __global__ void __launch_bounds__(64 * kMiscWaves, 1) towr_misc_kernel(KParams P
     c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
     c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
     c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.sched = P.sched; c.eelin = P.eelin;
+    c.rotvec = false;   // no small kind uses the base orientation
     switch (it.type) {   // wave-uniform: a wave holds one tile of one kind
       case IT_FNODE: eval_fnode(c, it, em); break;
       case IT_TERR: eval_height(c, it, sp_motion(it.ee), 0.0, em); break;
@@ -279,7 +281,7 @@ struct CostEmit {
 };
 
 constexpr int kCostBlock = 256;
-template <bool GAIT, bool GRAD>
+template <bool GAIT, bool GRAD, bool ROTVEC>
 __global__ void __launch_bounds__(kCostBlock, 1) towr_cost_kernel(KParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int b = blockIdx.x;
@@ -297,6 +299,7 @@ __global__ void __launch_bounds__(kCostBlock, 1) towr_cost_kernel(KParams P) {
   c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
   c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
   c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.sched = P.sched; c.eelin = P.eelin;
+  c.rotvec = ROTVEC;
   for (int i = threadIdx.x; i < P.n_citems; i += kCostBlock) {
     const CostItem it = P.citems[i];
     c.seg = it.seg >= 0 ? P.segs + (int64_t)it.seg * P.n_spl : nullptr;
@@ -314,25 +317,34 @@ __global__ void __launch_bounds__(kCostBlock, 1) towr_cost_kernel(KParams P) {
   }
   if constexpr (GRAD) copy_out(gs, P.GR + (int64_t)b * P.ldgr, P.n, threadIdx.x, kCostBlock);
 }
-const void* cost_kernel_for(bool gait, bool grad) {
-  if (gait) return grad ? reinterpret_cast<const void*>(&towr_cost_kernel<true, true>) : reinterpret_cast<const void*>(&towr_cost_kernel<true, false>);
-  return grad ? reinterpret_cast<const void*>(&towr_cost_kernel<false, true>) : reinterpret_cast<const void*>(&towr_cost_kernel<false, false>);
+template <bool GAIT, bool GRAD>
+const void* cost_kernel_rv(bool rotvec) {
+  return rotvec ? reinterpret_cast<const void*>(&towr_cost_kernel<GAIT, GRAD, true>)
+                : reinterpret_cast<const void*>(&towr_cost_kernel<GAIT, GRAD, false>);
+}
+const void* cost_kernel_for(bool gait, bool grad, bool rotvec) {
+  if (gait) return grad ? cost_kernel_rv<true, true>(rotvec) : cost_kernel_rv<true, false>(rotvec);
+  return grad ? cost_kernel_rv<false, true>(rotvec) : cost_kernel_rv<false, false>(rotvec);
 }
 
-template <bool GAIT>
+// DYN and ROM read the base orientation and come in Euler / RotVec variants; the others do not
+template <bool GAIT, bool ROTVEC>
 const void* kernel_for_mode(int type) {
   switch (type) {
-    case IT_DYN: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_DYN, 256, GAIT>);
-    case IT_ROM: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_ROM, 192, GAIT>);
-    case IT_FDISC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_FDISC, 192, GAIT>);
-    case IT_TQDISC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_TQDISC, 192, GAIT>);
+    case IT_DYN: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_DYN, 256, GAIT, ROTVEC>);
+    case IT_ROM: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_ROM, 192, GAIT, ROTVEC>);
+    case IT_FDISC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_FDISC, 192, GAIT, false>);
+    case IT_TQDISC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_TQDISC, 192, GAIT, false>);
   }
   return nullptr;
 }
-const void* kernel_for(int type, bool gait) { return gait ? kernel_for_mode<true>(type) : kernel_for_mode<false>(type); }
-const void* kernel_for_class(int lc, bool gait) {
+const void* kernel_for(int type, bool gait, bool rotvec) {
+  if (gait) return rotvec ? kernel_for_mode<true, true>(type) : kernel_for_mode<true, false>(type);
+  return rotvec ? kernel_for_mode<false, true>(type) : kernel_for_mode<false, false>(type);
+}
+const void* kernel_for_class(int lc, bool gait, bool rotvec) {
   if (lc == LC_MISC) return gait ? reinterpret_cast<const void*>(&towr_misc_kernel<true>) : reinterpret_cast<const void*>(&towr_misc_kernel<false>);
-  return kernel_for(class_type(lc), gait);
+  return kernel_for(class_type(lc), gait, rotvec);
 }
 
 }  // namespace
@@ -464,7 +476,7 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
     if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
     const int block = lc == LC_MISC ? 64 * kMiscWaves : L.type_block[class_type(lc)];
     void* args[] = {&P};
-    HIPCHK(h, hipLaunchKernel(kernel_for_class(lc, L.gait), dim3((unsigned)grid), dim3((unsigned)block), args,
+    HIPCHK(h, hipLaunchKernel(kernel_for_class(lc, L.gait, L.rotvec), dim3((unsigned)grid), dim3((unsigned)block), args,
                               lds_bytes(L, lc), st));
   }
   for (int i = 0; i < nside; ++i) {
@@ -495,7 +507,7 @@ int launch_cost(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* 
   P.lds_red_off = (int32_t)cost_red_off(L);
   P.F = F; P.GR = GR; P.ldgr = ldgr;
   void* args[] = {&P};
-  HIPCHK(h, hipLaunchKernel(cost_kernel_for(L.gait, GR != nullptr), dim3((unsigned)B), dim3(kCostBlock), args,
+  HIPCHK(h, hipLaunchKernel(cost_kernel_for(L.gait, GR != nullptr, L.rotvec), dim3((unsigned)B), dim3(kCostBlock), args,
                             cost_lds_bytes(L), s));
   return TOWR_OK;
 }
@@ -612,7 +624,7 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
     if (class_units(L, lc) == 0) continue;
     const size_t lds = lds_bytes(L, lc);
     if (lds > 160 * 1024) { h->err = "tile too large for LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
-    if (lds > 64 * 1024 && hipFuncSetAttribute(kernel_for_class(lc, L.gait), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+    if (lds > 64 * 1024 && hipFuncSetAttribute(kernel_for_class(lc, L.gait, L.rotvec), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
       h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
     }
   }
@@ -621,7 +633,7 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
     if (lds > 160 * 1024) { h->err = "problem too large for the cost kernel's LDS gradient"; return bail(TOWR_ERR_UNSUPPORTED); }
     if (lds > 64 * 1024)
       for (int g = 0; g < 2; ++g)
-        if (hipFuncSetAttribute(cost_kernel_for(L.gait, g != 0), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+        if (hipFuncSetAttribute(cost_kernel_for(L.gait, g != 0, L.rotvec), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
           h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
         }
   }

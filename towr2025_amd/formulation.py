@@ -575,7 +575,10 @@ class NlpFormulation:
         return out
 
     def to_desc(self, varsets=None, constraints=None, init_mode=capi.INIT_FORMULATION,
-                ee_goal=None, total_time=None) -> capi.ProblemDesc:
+                ee_goal=None, total_time=None, costs=None) -> capi.ProblemDesc:
+        """The engine's problem description. varsets / constraints / costs override the lists
+        GetVariableSets / GetConstraints / GetCosts would build (a hand-assembled ifopt::Problem,
+        as towr/test/procedural_example.cc and backflip_example.cc do)."""
         P = self.params_
         d = capi.ProblemDesc()
         d.abi_version = capi.ABI_VERSION
@@ -624,7 +627,7 @@ class NlpFormulation:
                 d.constraints[i].p[j] = v
             for j, v in enumerate(c.get("ip", [])):
                 d.constraints[i].ip[j] = v
-        cts = self.cost_terms()
+        cts = self.cost_terms() if costs is None else costs
         if len(cts) > capi.MAX_COSTS:
             raise ValueError("too many cost terms")
         d.n_costs = len(cts)
@@ -738,6 +741,48 @@ def procedural_desc() -> capi.ProblemDesc:
     f, vs, cs, goal, T = procedural_monoped()
     return f.to_desc(varsets=vs, constraints=cs, init_mode=capi.INIT_PROCEDURAL, ee_goal=goal,
                      total_time=T)
+
+
+def backflip_monoped():
+    """towr/test/backflip_example.cc:43-192: monoped backflip with the RotVecConverter (rotation vector
+    0 -> (0, -2 pi, 0)), phases 0.5 / 0.8 / 0.6 s, 3 swing / 4 force and torque polynomials, manual
+    constraint list and NodeCosts on force and torque. Returns (formulation, varsets, constraints,
+    goal, T, costs). The procedural initialisation interpolates the ee angle like the base angle
+    (the example sets it to zero); x0 is only the starting point."""
+    f = NlpFormulation()
+    f.model_ = RobotModel(RobotModel.Monoped)
+    f.terrain_ = HeightMap.Flat(0.0)
+    P = f.params_
+    P.angular_rep_ = 1
+    P.ee_phase_durations_.append([0.5, 0.8, 0.6])
+    P.ee_in_contact_at_start_.append(True)
+    P.ee_polynomials_per_swing_phase_ = 3
+    P.force_polynomials_per_stance_phase_ = 4
+    P.torque_polynomials_per_stance_phase_ = 4
+    f.initial_base_ = BaseState(lin_p=(0.0, 0.0, 0.58))
+    f.final_base_ = BaseState(lin_p=(0.0, 0.0, 0.58), ang_p=(0.0, -2.0 * math.pi, 0.0))
+    f.initial_ee_W_ = [(0.0, 0.0, 0.0)]
+    T = 1.9
+    vs = [(capi.VAR_BASE_LIN, 0), (capi.VAR_BASE_ANG, 0), (capi.VAR_EE_MOTION, 0),
+          (capi.VAR_EE_ANG, 0), (capi.VAR_EE_FORCE, 0), (capi.VAR_EE_TORQUE, 0)]
+    cs = [dict(kind=capi.C_DYNAMIC, ee=0, T=T, dt=0.1),
+          dict(kind=capi.C_RANGE_OF_MOTION, ee=0, T=T, dt=0.08),
+          dict(kind=capi.C_TERRAIN, ee=0, p=[0.02, 1e20]),
+          dict(kind=capi.C_FORCE, ee=0, p=[2000.0]),
+          dict(kind=capi.C_SWING, ee=0, p=[0.3]),
+          dict(kind=capi.C_SPLINE_ACC, ee=0),
+          dict(kind=capi.C_SPLINE_ACC, ee=1)]
+    costs = []
+    for d in range(3):
+        costs.append(dict(kind=capi.COST_NODE, ee=0, weight=1e-5, ip=[capi.VAR_EE_FORCE, 0, d]))
+        costs.append(dict(kind=capi.COST_NODE, ee=0, weight=1e-5, ip=[capi.VAR_EE_TORQUE, 0, d]))
+    return f, vs, cs, [(0.0, 0.0, 0.0)], T, costs
+
+
+def backflip_desc() -> capi.ProblemDesc:
+    f, vs, cs, goal, T, costs = backflip_monoped()
+    return f.to_desc(varsets=vs, constraints=cs, init_mode=capi.INIT_PROCEDURAL, ee_goal=goal, total_time=T,
+                     costs=costs)
 
 
 def with_costs(f: "NlpFormulation", costs=None, ee_base_pos=True, torque_weight=None) -> "NlpFormulation":

@@ -407,7 +407,7 @@ towr_problem_desc_t NlpFormulation::MakeDesc(const std::vector<VarSet>& vs, cons
   towr_problem_desc_t d;
   std::memset(&d, 0, sizeof(d));
   d.abi_version = TOWR_GPU_ABI_VERSION;
-  d.angular_rep = 0;
+  d.angular_rep = P.angular_rep_ == Parameters::RotationVector ? 1 : 0;   // nlp_formulation.cc:113-116
   d.robot.mass = dm.m;
   d.robot.gravity = dm.g;
   for (int i = 0; i < 6; ++i) d.robot.inertia[i] = dm.inertia[i];

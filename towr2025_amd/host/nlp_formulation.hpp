@@ -105,6 +105,8 @@ struct Parameters {
   double swing_ee_base_pos_tracking_weight_ = 1e-2;
   double dt_cost_swing_ee_base_pos_tracking_ = 0.05;
   std::array<double, 2> bound_phase_duration_{0.2, 1.0};
+  enum AngularRepresentation { EulerZYX, RotationVector };   // parameters.h:334-335
+  AngularRepresentation angular_rep_ = EulerZYX;
   std::vector<ConstraintName> constraints_{Terrain, Dynamic, BaseAcc, EndeffectorRom, Force, Swing, BaseHeight};
   std::vector<std::vector<double>> ee_phase_durations_;
   std::vector<bool> ee_in_contact_at_start_;

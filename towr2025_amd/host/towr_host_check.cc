@@ -5,7 +5,7 @@
 //   -> eval_g(x, false) -> eval_jac_g(x, false)
 // and dumps everything to a binary file:
 //   desc bytes | n m (int32) nnz (int64) | x0[n] | iRow[nnz] jCol[nnz] | (device >= 0) g[m] values[nnz] f grad[n]
-// usage: towr_host_check <anymal|anymal_costs|biped|biped_next|hopper> <out.bin> [device (default -1: layout only)]
+// usage: towr_host_check <anymal|anymal_costs|anymal_rotvec|biped|biped_next|hopper> <out.bin> [device (default -1: layout only)]
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -20,7 +20,7 @@ int main(int argc, char** argv) {
   if (argc < 3) { std::fprintf(stderr, "usage: %s <anymal|biped|hopper> <out.bin> [device]\n", argv[0]); return 2; }
   const std::string cfg = argv[1];
   const int device = argc > 3 ? std::atoi(argv[3]) : -1;
-  NlpFormulation f = (cfg == "anymal" || cfg == "anymal_costs") ? AnymalTrot() : (cfg == "biped" || cfg == "biped_next") ? BipedWalk() : MonopedHopper();
+  NlpFormulation f = (cfg == "anymal" || cfg == "anymal_costs" || cfg == "anymal_rotvec") ? AnymalTrot() : (cfg == "biped" || cfg == "biped_next") ? BipedWalk() : MonopedHopper();
   if (cfg == "biped_next") {   // SURVEY §8(f) kinds: Torque, TerrainHard, EELinear (tests/configs.py)
     f.params_.constraints_.push_back(Parameters::Torque);
     f.params_.constraints_.push_back(Parameters::TerrainHard);
@@ -31,6 +31,7 @@ int main(int argc, char** argv) {
     b.target = 1; b.deriv = 1; b.tolerance = 1.0; b.dt = 0.05;
     f.params_.ee_linear_constraints_ = {a, b};
   }
+  if (cfg == "anymal_rotvec") f.params_.angular_rep_ = Parameters::RotationVector;
   if (cfg == "anymal_costs") {   // every cost kind (tests/configs.py _with_costs)
     f.params_.costs_ = {{Parameters::ForcesCostID, 1e-3}, {Parameters::EEMotionCostID, 0.5},
                         {Parameters::EnergyCostID, 1e-4}, {Parameters::AngMomCostID, 0.1}};
