@@ -1,0 +1,73 @@
+// bw_probe — practical HBM ceilings on this MI355X for the engine's access pattern: streaming
+// 16-byte writes (plain and non-temporal), streaming reads, and a copy, over 460 MB (the
+// force_discretized launch's output at B = 4096). Prints GB/s per pattern. Tool, not product.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <vector>
+
+typedef double dbl2_t __attribute__((ext_vector_type(2)));
+
+__global__ void w_nt(dbl2_t* p, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    dbl2_t v; v.x = (double)i; v.y = 1.0;
+    __builtin_nontemporal_store(v, p + i);
+  }
+}
+__global__ void w_plain(dbl2_t* p, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    dbl2_t v; v.x = (double)i; v.y = 1.0;
+    p[i] = v;
+  }
+}
+// block-contiguous chunks (like one tile per block): each block writes `chunk` consecutive units
+__global__ void w_nt_chunk(dbl2_t* p, size_t n, int chunk) {
+  const size_t base = (size_t)blockIdx.x * chunk;
+  for (int i = threadIdx.x; i < chunk; i += blockDim.x) {
+    if (base + i >= n) return;
+    dbl2_t v; v.x = (double)i; v.y = 1.0;
+    __builtin_nontemporal_store(v, p + base + i);
+  }
+}
+__global__ void r_sum(const dbl2_t* p, size_t n, double* out) {
+  double s = 0.0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    dbl2_t v = p[i]; s += v.x + v.y;
+  }
+  if (s == 12345.678) out[0] = s;
+}
+__global__ void copy_nt(const dbl2_t* a, dbl2_t* b, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    __builtin_nontemporal_store(a[i], b + i);
+}
+
+int main() {
+  const size_t bytes = 460ull << 20, n = bytes / 16;
+  dbl2_t *a, *b; double* o;
+  if (hipMalloc(&a, bytes) != hipSuccess || hipMalloc(&b, bytes) != hipSuccess || hipMalloc(&o, 8) != hipSuccess) return 1;
+  hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+  auto run = [&](const char* name, auto launch, double traffic) {
+    for (int i = 0; i < 3; ++i) launch();
+    hipEventRecord(e0);
+    const int reps = 20;
+    for (int i = 0; i < reps; ++i) launch();
+    hipEventRecord(e1); hipEventSynchronize(e1);
+    float ms; hipEventElapsedTime(&ms, e0, e1);
+    std::printf("%-28s %8.4f ms  %7.1f GB/s\n", name, ms / reps, traffic / (ms / reps * 1e-3) / 1e9);
+  };
+  for (int blocks : {1024, 2048, 4096, 16384}) {
+    char nm[64];
+    std::snprintf(nm, sizeof nm, "write_nt grid %d", blocks);
+    run(nm, [&] { w_nt<<<blocks, 256>>>(a, n); }, (double)bytes);
+    std::snprintf(nm, sizeof nm, "write_plain grid %d", blocks);
+    run(nm, [&] { w_plain<<<blocks, 256>>>(a, n); }, (double)bytes);
+  }
+  for (int chunk : {2300, 4600}) {   // ~37 KB / ~74 KB tiles
+    char nm[64];
+    std::snprintf(nm, sizeof nm, "write_nt tiles %d B", chunk * 16);
+    run(nm, [&] { w_nt_chunk<<<(unsigned)((n + chunk - 1) / chunk), 192>>>(a, n, chunk); }, (double)bytes);
+  }
+  run("read grid 4096", [&] { r_sum<<<4096, 256>>>(a, n, o); }, (double)bytes);
+  run("copy_nt grid 4096", [&] { copy_nt<<<4096, 256>>>(a, b, n); }, 2.0 * bytes);
+  run("hipMemsetAsync", [&] { hipMemsetAsync(a, 0, bytes); }, (double)bytes);
+  return 0;
+}

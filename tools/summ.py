@@ -7,3 +7,6 @@ for f in sys.argv[1:]:
             print(f"{f}: value {d['value']:.4g} calls/s  step {d['roofline']['step']['ms']:.3f} ms ({d['roofline']['step']['GB/s']:.0f} GB/s)" + (f"  cpu {cpu:.0f}" if cpu else ""))
             for k, v in d['roofline']['kernels'].items():
                 print(f"   {k:18s} {v['ms']:.4f} ms {v['GB/s']:7.0f} GB/s")
+            if 'objective' in d:
+                o = d['objective']
+                print(f"   objective          {o['ms_per_batch']:.4f} ms {o['value']:.4g} calls/s")

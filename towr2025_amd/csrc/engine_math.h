@@ -136,8 +136,24 @@ TG_HD int slot_pick(const SlotGroup& q, int k) {   // select chain: k may be a r
 // before emission and the other candidate is marked absent (checked at build time), so every CSR
 // position receives exactly one plain store.
 
+// Device copy of the segment table in blocks of 32 rows (array of structures of arrays): for
+// spline s and rows 32G..32G+31, one block of doubles [tl | T | H(d, b) x 12] and one block of
+// ints [poly | col(b, e) x 12], each field 32 entries long. The lanes of a wave (consecutive
+// instants) then read one field with one coalesced access, and every field of a row is an
+// immediate offset (< 4 KiB) from the row's two base addresses.
+constexpr int kSegGroup = 32;
+constexpr int kSegDoubles = 14;   // tl, T, H[12]
+constexpr int kSegInts = 13;      // poly, col[12]
+struct SegSoA {
+  const double* d;       // [(s * ng + G) * 14 * 32]
+  const int32_t* i;      // [(s * ng + G) * 13 * 32]
+  int32_t ng, reserved;  // 32-row groups
+};
+
 struct Ctx {
-  const SegRec* seg;            // this item's segment row (one SegRec per spline), or nullptr
+  const SegRec* seg;            // host: this item's segment row (one SegRec per spline), or nullptr
+  SegSoA sg;                    // device: the segment table
+  int32_t row;                  // device: this item's segment row, or -1
   const double* x;              // this problem's decision vector
   const int32_t* nodecol;       // node value -> global column of x, or -1 (constant 0)
   const SplineMeta* spl;
@@ -159,8 +175,8 @@ struct Ctx {
 struct SplinePt {
   int poly;
   double T, tl;
-  const double* H;   // SegRec::H of this instant on the device (basis precomputed), else nullptr
-  const int32_t* C;  // SegRec::col of this instant on the device, else nullptr
+  const double* H;   // device: basis of this instant, entry (d, b) at H[(4 * d + b) * hs]; else nullptr
+  const int32_t* C;  // device: x columns of this instant, entry (b, e) at C[(3 * b + e) * kSegGroup]
   bool dyn;          // PhaseSpline: durations (hence polynomial, local time, basis) depend on x
   double p[3], v[3], a[3];
 };
@@ -303,15 +319,20 @@ TG_HD void spline_eval(const Ctx& c, int s, double t, SplinePt& o) {
     return;
   }
 #if defined(__HIP_DEVICE_COMPILE__)
-  const SegRec& r = c.seg[s];
-  o.poly = r.poly; o.tl = r.tl; o.T = r.T;
-  o.H = &r.H[0][0];
-  o.C = &r.col[0][0];
+  const size_t blk = (size_t)s * c.sg.ng + (c.row >> 5);
+  const double* D = c.sg.d + blk * (kSegDoubles * kSegGroup) + (c.row & 31);
+  const int32_t* I = c.sg.i + blk * (kSegInts * kSegGroup) + (c.row & 31);
+  o.poly = I[0]; o.tl = D[0]; o.T = D[kSegGroup];
+  o.H = D + 2 * kSegGroup;
+  o.C = I + kSegGroup;
+  const double* H = o.H;
+  const int32_t* C = o.C;
+  constexpr int G = kSegGroup;
   for (int e = 0; e < 3; ++e) {
-    const double u0 = c.x[r.col[0][e]], u1 = c.x[r.col[1][e]], u2 = c.x[r.col[2][e]], u3 = c.x[r.col[3][e]];
-    o.p[e] = r.H[0][0] * u0 + r.H[0][1] * u1 + r.H[0][2] * u2 + r.H[0][3] * u3;
-    o.v[e] = r.H[1][0] * u0 + r.H[1][1] * u1 + r.H[1][2] * u2 + r.H[1][3] * u3;
-    o.a[e] = r.H[2][0] * u0 + r.H[2][1] * u1 + r.H[2][2] * u2 + r.H[2][3] * u3;
+    const double u0 = c.x[C[(0 + e) * G]], u1 = c.x[C[(3 + e) * G]], u2 = c.x[C[(6 + e) * G]], u3 = c.x[C[(9 + e) * G]];
+    o.p[e] = H[0 * G] * u0 + H[1 * G] * u1 + H[2 * G] * u2 + H[3 * G] * u3;
+    o.v[e] = H[4 * G] * u0 + H[5 * G] * u1 + H[6 * G] * u2 + H[7 * G] * u3;
+    o.a[e] = H[8 * G] * u0 + H[9 * G] * u1 + H[10 * G] * u2 + H[11 * G] * u3;
   }
 #else
   o.H = nullptr;
@@ -331,7 +352,7 @@ TG_HD void spline_eval(const Ctx& c, int s, double t, SplinePt& o) {
 TG_HD void spline_basis(const SplinePt& o, int d, double H[4]) {
 #if defined(__HIP_DEVICE_COMPILE__)
   if (!o.dyn) {
-    for (int b = 0; b < 4; ++b) H[b] = o.H[4 * d + b];
+    for (int b = 0; b < 4; ++b) H[b] = o.H[(4 * d + b) * kSegGroup];
     return;
   }
 #endif
@@ -353,7 +374,7 @@ TG_HD void emit_dim(const Ctx& c, Emit& em, int row, int s, const SplinePt& P, c
     // a stance polynomial whose two nodes share one position variable (NodesVariablesPhaseBased,
     // nodes_variables_phase_based.cc:215-258): coeffRef sums both contributions into one entry
 #if defined(__HIP_DEVICE_COMPILE__)
-    const bool shared = P.C[e] == P.C[2 * 3 + e];   // both constant -> both absent anyway
+    const bool shared = P.C[e * kSegGroup] == P.C[(2 * 3 + e) * kSegGroup];   // both constant -> both absent anyway
 #else
     const bool shared = col[0] >= 0 && col[0] == col[2];
 #endif
@@ -420,9 +441,15 @@ TG_HD double sched_val(const SchedJac& J, int k, int col) {
 struct Trig { double sx, cx, sy, cy, sz, cz; };
 TG_HD Trig trig(const double a[3]) {
   Trig r;
+#if defined(__HIP_DEVICE_COMPILE__)
+  sincos(a[0], &r.sx, &r.cx);   // one shared argument reduction per angle
+  sincos(a[1], &r.sy, &r.cy);
+  sincos(a[2], &r.sz, &r.cz);
+#else
   r.sx = sin(a[0]); r.cx = cos(a[0]);
   r.sy = sin(a[1]); r.cy = cos(a[1]);
   r.sz = sin(a[2]); r.cz = cos(a[2]);
+#endif
   return r;
 }
 // GetRotationMatrixBaseToWorld (:207-221)
@@ -1065,7 +1092,10 @@ TG_HD void eval_rom(const Ctx& c, const ItemDesc& it, Emit& em) {
   spline_eval(c, SP_BASE_LIN, t, L);
   spline_eval(c, SP_BASE_ANG, t, A);
   spline_eval(c, sp_motion(ee), t, P);
-  double R[3][3]; base_rot(c, A, R);
+  double R[3][3];
+  Trig q{};
+  if (c.rotvec) rv_rodrigues(A.p, R);
+  else { q = trig(A.p); euler_R(q, R); }
   const double rW[3] = {P.p[0] - L.p[0], P.p[1] - L.p[1], P.p[2] - L.p[2]};
   double H[4];
   if (it.group == 1 && c.rotvec) {
@@ -1087,7 +1117,6 @@ TG_HD void eval_rom(const Ctx& c, const ItemDesc& it, Emit& em) {
         for (int bb = 0; bb < 4; ++bb) em(r0 + r, basis_col(c, SP_BASE_LIN, L.poly, bb, e), -R[e][r] * H[bb], true);
   } else if (it.group == 1) {
     // DerivOfRotVecMult(t, r_W, inverse=true): row r = sum_c rW[c] dR[c][r]; row X has no roll terms
-    const Trig q = trig(A.p);
     spline_basis(A, kPos, H);
     for (int e = 0; e < 3; ++e) {
       double dR[3][3]; euler_dR_axis(q, e, dR);

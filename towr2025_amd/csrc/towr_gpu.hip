@@ -38,7 +38,7 @@ struct KParams {
   const int32_t* nodecol;
   const SplineMeta* spl;
   const double* dur;
-  const SegRec* segs;
+  SegSoA sg;                     // segment table (structure of arrays)
   const PolyPhase* pinfo;        // phase-duration optimisation tables (see engine_math.h)
   const PhaseCol* pcols;
   const SchedInfo* sched;
@@ -165,6 +165,19 @@ __device__ __forceinline__ void stage_x(const KParams& P, const double* xg, doub
 // (GAIT) their PhaseSplines evaluate polynomials from the node table, which is then staged too.
 constexpr bool stages_nodes(int type, bool gait) { return gait || is_misc_kind(type); }
 
+// Phase timing (tools/phase_timing.py; only in the -DTOWR_PHASE_TIMING build, never in the product):
+// per block, 16 timestamps: [0] realtime start, [1] memtime start, [2] after staging, [3..6] each
+// wave's end of evaluation, [7] after the evaluation barrier, [8] end of wave 0's copy-out,
+// [9] realtime end.
+#ifdef TOWR_PHASE_TIMING
+__device__ unsigned long long* g_tbuf;
+#define TSTAMP(slot, v) do { if (g_tbuf && (threadIdx.x & 63) == 0) g_tbuf[(size_t)blockIdx.x * 16 + (slot)] = (v); } while (0)
+#define TS_MEM() ((unsigned long long)__builtin_amdgcn_s_memtime())
+#define TS_REAL() ((unsigned long long)__builtin_amdgcn_s_memrealtime())
+#else
+#define TSTAMP(slot, v) do { } while (0)
+#endif
+
 template <int TYPE, int BLOCK, bool GAIT, bool ROTVEC>
 __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_kernel(KParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -179,6 +192,9 @@ __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_ker
   double* Gb = P.G + (int64_t)b * P.ldg;
   const double* xg = P.X + (int64_t)b * P.ldx;
   // issue the lane's item, first slot groups and (below) the x / node-table staging loads together
+#ifdef TOWR_PHASE_TIMING
+  if (threadIdx.x < 64) { TSTAMP(0, TS_REAL()); TSTAMP(1, TS_MEM()); }
+#endif
   const ItemDesc it = P.items[T.i0 + threadIdx.x];
   TileEmit<BLOCK> em(P.slots + it.slot, smem, smem + P.lds_rows_off - T.r0);
   // x (+ a zero at index n for constant node values) and, for node-value kinds, the node table
@@ -186,11 +202,14 @@ __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_ker
   int32_t* ns = reinterpret_cast<int32_t*>(smem + P.lds_x_off + P.n_pad);
   stage_x<BLOCK, stages_nodes(TYPE, GAIT)>(P, xg, xs, ns);
   __syncthreads();
+#ifdef TOWR_PHASE_TIMING
+  if (threadIdx.x < 64) TSTAMP(2, TS_MEM());
+#endif
   const double* xsrc = xs;
   const int32_t* ncsrc = ns;
   if (it.type == TYPE) {
     Ctx c;
-    c.seg = it.seg >= 0 ? P.segs + (int64_t)it.seg * P.n_spl : nullptr;
+    c.seg = nullptr; c.sg = P.sg; c.row = it.seg;
     c.x = xsrc; c.nodecol = ncsrc; c.spl = P.spl; c.dur = P.dur;
     c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
     c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
@@ -199,10 +218,19 @@ __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_ker
     eval_typed<TYPE>(c, it, em);
     em.flush();
   }
+#ifdef TOWR_PHASE_TIMING
+  if ((threadIdx.x >> 6) < 4) TSTAMP(3 + (threadIdx.x >> 6), TS_MEM());
+#endif
   __syncthreads();
+#ifdef TOWR_PHASE_TIMING
+  if (threadIdx.x < 64) TSTAMP(7, TS_MEM());
+#endif
   if (P.want_jac) copy_out(smem, Vb + T.v0, T.v1 - T.v0, threadIdx.x, BLOCK);
   if (P.want_g)
     for (int i = threadIdx.x; i < T.r1 - T.r0; i += BLOCK) __builtin_nontemporal_store(smem[P.lds_rows_off + i], Gb + T.r0 + i);
+#ifdef TOWR_PHASE_TIMING
+  if (threadIdx.x < 64) { TSTAMP(8, TS_MEM()); TSTAMP(9, TS_REAL()); }
+#endif
 }
 
 // The small kinds (node-value constraints, SplineAcc, BaseMotion, TotalDuration: a few kB of output
@@ -231,11 +259,17 @@ __global__ void __launch_bounds__(64 * kMiscWaves, 1) towr_misc_kernel(KParams P
   TileEmit<64> em(P.slots + it.slot, wl, wl + P.misc_rows_off - T.r0);
   double* xs = smem + P.lds_x_off;
   int32_t* ns = reinterpret_cast<int32_t*>(smem + P.lds_x_off + P.n_pad);
+#ifdef TOWR_PHASE_TIMING
+  if (threadIdx.x < 64) { TSTAMP(0, TS_REAL()); TSTAMP(1, TS_MEM()); }
+#endif
   stage_x<BLOCK, true>(P, P.X + (int64_t)b * P.ldx, xs, ns);
   __syncthreads();
+#ifdef TOWR_PHASE_TIMING
+  if (threadIdx.x < 64) TSTAMP(2, TS_MEM());
+#endif
   if (it.type != IT_NONE) {
     Ctx c;
-    c.seg = it.seg >= 0 ? P.segs + (int64_t)it.seg * P.n_spl : nullptr;
+    c.seg = nullptr; c.sg = P.sg; c.row = it.seg;
     c.x = xs; c.nodecol = ns; c.spl = P.spl; c.dur = P.dur;
     c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
     c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
@@ -255,13 +289,22 @@ __global__ void __launch_bounds__(64 * kMiscWaves, 1) towr_misc_kernel(KParams P
       default: break;
     }
   }
+#ifdef TOWR_PHASE_TIMING
+  TSTAMP(3 + wave, TS_MEM());
+#endif
   __syncthreads();
+#ifdef TOWR_PHASE_TIMING
+  if (threadIdx.x < 64) TSTAMP(7, TS_MEM());
+#endif
   if (ti < 0) return;
   double* Vb = P.V + (int64_t)b * P.ldv;
   double* Gb = P.G + (int64_t)b * P.ldg;
   if (P.want_jac) copy_out(wl, Vb + T.v0, T.v1 - T.v0, lane, 64);
   if (P.want_g)
     for (int i = lane; i < T.r1 - T.r0; i += 64) __builtin_nontemporal_store(wl[P.misc_rows_off + i], Gb + T.r0 + i);
+#ifdef TOWR_PHASE_TIMING
+  if (threadIdx.x < 64) { TSTAMP(8, TS_MEM()); TSTAMP(9, TS_REAL()); }
+#endif
 }
 
 // Objective and gradient (IpoptAdapter::eval_f / eval_grad_f): one block per problem. The block
@@ -302,7 +345,7 @@ __global__ void __launch_bounds__(kCostBlock, 1) towr_cost_kernel(KParams P) {
   c.rotvec = ROTVEC;
   for (int i = threadIdx.x; i < P.n_citems; i += kCostBlock) {
     const CostItem it = P.citems[i];
-    c.seg = it.seg >= 0 ? P.segs + (int64_t)it.seg * P.n_spl : nullptr;
+    c.seg = nullptr; c.sg = P.sg; c.row = it.seg;
     eval_cost_item(c, it, em);
   }
   // f: wave butterfly, then the waves' partials in order
@@ -364,7 +407,8 @@ struct towr_gpu_handle_s {
   int32_t* d_nodecol = nullptr;
   SplineMeta* d_spl = nullptr;
   double* d_dur = nullptr;
-  SegRec* d_segs = nullptr;
+  void* d_segs = nullptr;      // SegSoA storage
+  SegSoA sg{};
   PolyPhase* d_pinfo = nullptr;
   PhaseCol* d_pcols = nullptr;
   SchedInfo* d_sched = nullptr;
@@ -456,7 +500,7 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
     P.X = X; P.ldx = ldx; P.G = G; P.ldg = ldg; P.V = V; P.ldv = ldv;
     P.items = h->d_items; P.slots = h->d_slots; P.tiles = h->d_tiles;
     P.nodecol = h->d_nodecol; P.spl = h->d_spl; P.dur = h->d_dur;
-    P.segs = h->d_segs; P.n_spl = (int32_t)L.spl.size();
+    P.sg = h->sg; P.n_spl = (int32_t)L.spl.size();
     P.pinfo = h->d_pinfo; P.pcols = h->d_pcols; P.sched = h->d_sched; P.eelin = h->d_eelin;
     P.terrains = terrains; P.terrain_per_problem = per_problem;
     P.B = B; P.ntiles = nt;
@@ -497,7 +541,7 @@ int launch_cost(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* 
   KParams P{};
   P.X = X; P.ldx = ldx;
   P.nodecol = h->d_nodecol; P.spl = h->d_spl; P.dur = h->d_dur;
-  P.segs = h->d_segs; P.n_spl = (int32_t)L.spl.size();
+  P.sg = h->sg; P.n_spl = (int32_t)L.spl.size();
   P.pinfo = h->d_pinfo; P.pcols = h->d_pcols; P.sched = h->d_sched; P.eelin = h->d_eelin;
   P.terrains = terrains; P.terrain_per_problem = per_problem;
   P.B = B;
@@ -559,6 +603,14 @@ int host_eval(towr_gpu_handle h, int B, const double* X, double* G, double* V) {
 extern "C" {
 
 int towr_gpu_abi_version(void) { return TOWR_GPU_ABI_VERSION; }
+
+#ifdef TOWR_PHASE_TIMING
+// timing build only (tools/phase_timing.py): device buffer of 16 u64 per block, or NULL
+int towr_gpu_debug_set_timing_buffer(void* p) {
+  unsigned long long* v = reinterpret_cast<unsigned long long*>(p);
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_tbuf), &v, sizeof(v)) == hipSuccess ? 0 : TOWR_ERR_HIP;
+}
+#endif
 int towr_gpu_num_kernels(void) { return LC_COUNT; }
 
 const char* towr_gpu_last_error(towr_gpu_handle h) {
@@ -602,11 +654,39 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
   int r;
   if ((r = upload(h, &h->d_items, L.items)) || (r = upload(h, &h->d_slots, L.slot_groups)) ||
       (r = upload(h, &h->d_tiles, L.tiles)) || (r = upload(h, &h->d_nodecol, nodecol16)) ||
-      (r = upload(h, &h->d_spl, L.spl)) || (r = upload(h, &h->d_dur, L.dur)) || (r = upload(h, &h->d_segs, L.segs)) || (r = upload(h, &h->d_terrain, ter)) ||
+      (r = upload(h, &h->d_spl, L.spl)) || (r = upload(h, &h->d_dur, L.dur)) || (r = upload(h, &h->d_terrain, ter)) ||
       (r = upload(h, &h->d_pinfo, L.pinfo)) || (r = upload(h, &h->d_pcols, L.pcols)) || (r = upload(h, &h->d_sched, L.sched)) ||
       (r = upload(h, &h->d_misc, L.misc_tiles)) || (r = upload(h, &h->d_eelin, L.eelin)) ||
       (r = upload(h, &h->d_citems, L.cost_items)))
     return bail(r);
+  {   // segment table in 32-row blocks (see SegSoA)
+    const int nspl = (int)L.spl.size();
+    const int nr = L.segs.empty() ? 0 : (int)(L.segs.size() / nspl);
+    const int ng = std::max(1, (nr + kSegGroup - 1) / kSegGroup);
+    std::vector<double> dv((size_t)nspl * ng * kSegDoubles * kSegGroup, 0.0);
+    std::vector<int32_t> iv((size_t)nspl * ng * kSegInts * kSegGroup, L.n);
+    for (int sp = 0; sp < nspl; ++sp)
+      for (int k = 0; k < ng * kSegGroup; ++k) {
+        const size_t blk = (size_t)sp * ng + k / kSegGroup;
+        double* D = dv.data() + blk * kSegDoubles * kSegGroup + k % kSegGroup;
+        int32_t* I = iv.data() + blk * kSegInts * kSegGroup + k % kSegGroup;
+        if (k >= nr) { D[kSegGroup] = 1.0; I[0] = 0; continue; }   // padding rows: a harmless polynomial
+        const SegRec& rr = L.segs[(size_t)k * nspl + sp];
+        D[0] = rr.tl; D[kSegGroup] = rr.T; I[0] = rr.poly;
+        for (int f = 0; f < 12; ++f) {
+          D[(2 + f) * kSegGroup] = rr.H[f / 4][f % 4];
+          I[(1 + f) * kSegGroup] = rr.col[f / 3][f % 3];
+        }
+      }
+    const size_t db = sizeof(double) * dv.size(), ib = sizeof(int32_t) * iv.size();
+    if (hipMalloc(&h->d_segs, db + ib) != hipSuccess || hipMemcpy(h->d_segs, dv.data(), db, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(static_cast<char*>(h->d_segs) + db, iv.data(), ib, hipMemcpyHostToDevice) != hipSuccess) {
+      h->err = "segment table upload failed"; return bail(TOWR_ERR_HIP);
+    }
+    h->sg.d = static_cast<const double*>(h->d_segs);
+    h->sg.i = reinterpret_cast<const int32_t*>(static_cast<const char*>(h->d_segs) + db);
+    h->sg.ng = ng;
+  }
   {
     const char* ns = std::getenv("TOWR_GPU_STREAMS");
     // default: serial launches. Measured on MI355X (ANYmal, B = 4096): 1, 2, 4 streams gave 0.524,
