@@ -101,3 +101,43 @@ extern "C" int emu_stats(const towr_problem_desc_t* d) {
   }
   return 0;
 }
+
+// LDS bank-conflict degree of the tile emission (ds_write_b64: 4 groups of 16 lanes, bank pair =
+// double position mod 16): per item type, LDS cycles spent / conflict-free cycles, with the
+// position map `swz` applied (0 = identity, 1 = the kernel's XOR swizzle)
+extern "C" int emu_conflicts(const towr_problem_desc_t* d, int swz) {
+  Layout L; std::string e;
+  if (build_layout(*d, L, e)) return -1;
+  for (int t = 0; t < IT_COUNT; ++t) {
+    long cyc = 0, ideal = 0, wc[4] = {0, 0, 0, 0}, wi[4] = {0, 0, 0, 0};
+    for (int ti = L.type_tile0[t]; ti < L.type_tile0[t + 1]; ++ti) {
+      const TileDesc& td = L.tiles[ti];
+      const int block = td.i1 - td.i0;
+      for (int w = 0; w < block; w += 64) {
+        int maxc = 0;
+        for (int l = w; l < w + 64 && l < block; ++l)
+          if (L.items[td.i0 + l].type != IT_NONE) maxc = std::max(maxc, L.items[td.i0 + l].ncand);
+        for (int j = 0; j < maxc; ++j)
+          for (int g = 0; g < 4; ++g) {
+            int cnt[16] = {0}; bool any = false;
+            for (int l = w + 16 * g; l < w + 16 * g + 16 && l < block; ++l) {
+              const ItemDesc& it = L.items[td.i0 + l];
+              if (it.type == IT_NONE || j >= it.ncand) continue;
+              int pos = slot_pick(L.slot_groups[it.slot + (size_t)(j / 8) * block], j % 8);
+              if (swz == 1 && pos < td.v1 - td.v0) { const int q = pos + (td.v0 & 1); pos = q ^ (((q >> 5) & 15) << 1); }
+              if (swz == 2 && pos < td.v1 - td.v0) { const int q = pos + (td.v0 & 1); pos = q ^ (((q >> 4) & 7) << 1); }
+              if (swz == 3 && pos < td.v1 - td.v0) { const int q = pos + (td.v0 & 1); pos = q ^ ((((q >> 4) ^ (q >> 7)) & 7) << 1); }
+              cnt[pos & 15]++; any = true;
+            }
+            if (!any) continue;
+            int m = 0; for (int q = 0; q < 16; ++q) m = std::max(m, cnt[q]);
+            cyc += m; ideal += 1;
+            if (w / 64 < 4) { wc[w / 64] += m; wi[w / 64] += 1; }
+          }
+      }
+    }
+    if (ideal) std::printf("type %d: lds write cycles %ld conflict-free %ld (x%.2f)  per wave %ld/%ld %ld/%ld %ld/%ld %ld/%ld\n", t, cyc, ideal,
+                           (double)cyc / ideal, wc[0], wi[0], wc[1], wi[1], wc[2], wi[2], wc[3], wi[3]);
+  }
+  return 0;
+}

@@ -20,10 +20,11 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--gait", action="store_true")
     ap.add_argument("--rotvec", action="store_true")
+    ap.add_argument("--lib", default="libtowr_gpu_timing.so", help="library under tools/build")
     args = ap.parse_args()
     import torch
     from towr2025_amd import _capi as capi
-    lib = capi.load_library(os.path.join(ROOT, "tools", "build", "libtowr_gpu_timing.so"))
+    lib = capi.load_library(os.path.join(ROOT, "tools", "build", args.lib))
     lib.towr_gpu_debug_set_timing_buffer.argtypes = [C.c_void_p]
     from towr2025_amd import TowrGpuProblem
     from towr2025_amd import formulation as F

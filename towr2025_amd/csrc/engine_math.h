@@ -1116,10 +1116,14 @@ TG_HD void eval_rom(const Ctx& c, const ItemDesc& it, Emit& em) {
       for (int e = 0; e < 3; ++e)
         for (int bb = 0; bb < 4; ++bb) em(r0 + r, basis_col(c, SP_BASE_LIN, L.poly, bb, e), -R[e][r] * H[bb], true);
   } else if (it.group == 1) {
-    // DerivOfRotVecMult(t, r_W, inverse=true): row r = sum_c rW[c] dR[c][r]; row X has no roll terms
+    // DerivOfRotVecMult(t, r_W, inverse=true): row r = sum_c rW[c] dR[c][r]; row X has no roll terms.
+    // Fully unrolled: the 33 candidates then have compile-time emission indices, so the slot-group
+    // loads are hoisted instead of waited for one group at a time.
     spline_basis(A, kPos, H);
+#pragma unroll
     for (int e = 0; e < 3; ++e) {
       double dR[3][3]; euler_dR_axis(q, e, dR);
+#pragma unroll
       for (int r = (e == 0 ? 1 : 0); r < 3; ++r) {
         const double s = rW[0] * dR[0][r] + rW[1] * dR[1][r] + rW[2] * dR[2][r];
         for (int bb = 0; bb < 4; ++bb) em(r0 + r, basis_col(c, SP_BASE_ANG, A.poly, bb, e), s * H[bb], true);

@@ -74,6 +74,7 @@ struct Layout {
 };
 
 constexpr int kMiscWaves = 4;
+constexpr int kSlotSpare = 4;   // spare slot groups per lane: the kernels prefetch up to this many ahead
 constexpr bool is_misc_kind(int t) { return t != IT_DYN && t != IT_ROM && t != IT_FDISC && t != IT_TQDISC; }
 
 // launch classes: the heavy kinds have their own kernels, the small kinds share one

@@ -797,13 +797,13 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
         for (int w = 0; w < kMiscWaves; ++w) L.misc_tiles.push_back(q + w < mt.size() ? mt[q + w] : -1);
     }
     // slot table per tile: lane l's candidates 8g..8g+7 in group g at base + g * block + l, as
-    // tile-relative uint16 positions; two spare groups per lane absorb the kernel's prefetch
+    // tile-relative uint16 positions; four spare groups per lane absorb the kernel's prefetch
     std::vector<SlotGroup> groups;
     for (const TileDesc& td : L.tiles) {
       const int block = td.i1 - td.i0;
       int maxc = 0;
       for (int l = 0; l < block; ++l) maxc = std::max(maxc, items[td.i0 + l].type == IT_NONE ? 0 : items[td.i0 + l].ncand);
-      const int ng = (maxc + 7) / 8 + 2;
+      const int ng = (maxc + 7) / 8 + kSlotSpare;   // + spare groups for the kernels' slot prefetch
       const size_t base = groups.size();
       SlotGroup none; for (uint32_t& w : none.w) w = 0xFFFFFFFFu;
       groups.resize(base + (size_t)ng * block, none);

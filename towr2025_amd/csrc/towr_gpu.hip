@@ -66,26 +66,39 @@ struct KParams {
 // candidates of arithmetic. The candidate's column is never needed on the device, and no item emits
 // a column twice (engine_math.h), so every position receives exactly one plain LDS store; absent
 // candidates (constant node values) go to a per-lane dummy slot, so the store needs no branch.
-template <int BLOCK>
+template <int BLOCK, int DEPTH>
 struct TileEmit {
   const SlotGroup* slot;   // this lane's group 0; group g at slot[g * BLOCK]
   double* out;             // LDS tile, tile-relative
   double* gout;            // LDS g rows, tile-relative
-  SlotGroup cur, nxt;      // groups g, g+1
+  SlotGroup q[DEPTH];      // groups g .. g + DEPTH - 1 in flight (q[0] = current)
   int j = 0;
   __device__ __forceinline__ TileEmit(const SlotGroup* s, double* o, double* go) : slot(s), out(o), gout(go) {
-    cur = s[0];
-    nxt = s[BLOCK];
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) q[d] = s[d * BLOCK];
   }
   __device__ __forceinline__ void g(int row, double v) { gout[row] = v; }
   __device__ __forceinline__ void operator()(int, int, double v, bool) {
-    const int s = slot_pick(cur, j & 7);
+#ifdef TOWR_EXPERIMENT_NOSLOT   // timing experiment only: wrong positions, no slot-table traffic
+    out[(threadIdx.x * 7 + j++) & 1023] = v;
+#else
+    const int s = slot_pick(q[0], j & 7);
     ++j;
-    if ((j & 7) == 0) { cur = nxt; nxt = slot[((j >> 3) + 1) * BLOCK]; }
+    if ((j & 7) == 0) {
+#pragma unroll
+      for (int d = 0; d + 1 < DEPTH; ++d) q[d] = q[d + 1];
+      q[DEPTH - 1] = slot[((j >> 3) + DEPTH - 1) * BLOCK];
+    }
     out[s] = v;   // absent candidates land in the lane's dummy slot
+#endif
   }
   __device__ __forceinline__ void flush() {}
 };
+// Slot-group prefetch depth. Deeper rings only pay off where the emission index is a compile-time
+// constant: in a runtime loop, rotating the ring copies registers whose loads are still in flight
+// and waits for the newest one (measured: depth 4 made RangeOfMotion's base-angular wave slower).
+constexpr int slot_depth(int) { return 2; }
+static_assert(slot_depth(IT_ROM) <= kSlotSpare, "slot prefetch past the spare groups");
 
 template <int TYPE, class Emit>
 __device__ __forceinline__ void eval_typed(const Ctx& c, const ItemDesc& it, Emit& em) {
@@ -196,7 +209,7 @@ __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_ker
   if (threadIdx.x < 64) { TSTAMP(0, TS_REAL()); TSTAMP(1, TS_MEM()); }
 #endif
   const ItemDesc it = P.items[T.i0 + threadIdx.x];
-  TileEmit<BLOCK> em(P.slots + it.slot, smem, smem + P.lds_rows_off - T.r0);
+  TileEmit<BLOCK, slot_depth(TYPE)> em(P.slots + it.slot, smem, smem + P.lds_rows_off - T.r0);
   // x (+ a zero at index n for constant node values) and, for node-value kinds, the node table
   double* xs = smem + P.lds_x_off;
   int32_t* ns = reinterpret_cast<int32_t*>(smem + P.lds_x_off + P.n_pad);
@@ -256,7 +269,7 @@ __global__ void __launch_bounds__(64 * kMiscWaves, 1) towr_misc_kernel(KParams P
     it = P.items[T.i0 + lane];
   }
   double* wl = smem + wave * P.misc_stride;
-  TileEmit<64> em(P.slots + it.slot, wl, wl + P.misc_rows_off - T.r0);
+  TileEmit<64, 3> em(P.slots + it.slot, wl, wl + P.misc_rows_off - T.r0);
   double* xs = smem + P.lds_x_off;
   int32_t* ns = reinterpret_cast<int32_t*>(smem + P.lds_x_off + P.n_pad);
 #ifdef TOWR_PHASE_TIMING
