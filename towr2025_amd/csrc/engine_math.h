@@ -992,7 +992,7 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
     double Iww[3]; mat3_vec(Iw, w, Iww);
     double Hp[4], Hv[4], Ha[4];
     spline_basis(A, kPos, Hp); spline_basis(A, kVel, Hv); spline_basis(A, kAcc, Ha);
-#pragma unroll 1
+#pragma unroll
     for (int e = 0; e < 3; ++e) {
       double dR[3][3]; euler_dR_axis(q, e, dR);
       // dw = dM_e thd; dwd = dMdot_e thd + dM_e thdd (GetDerivMwrtNodes :168-198, GetDerivMdotwrtNodes :270-304)
