@@ -163,6 +163,7 @@ struct Ctx {
   int32_t fdisc_motion;         // ForceConstraintDiscretized motion block enabled (terrain has d2h)
   bool gait;                    // phase-duration optimisation (a compile-time constant in kernels)
   bool rotvec;                  // Parameters::RotationVector base orientation (compile-time in kernels)
+  double* dyn_scratch;          // device DYN tiles: per-instant endeffector terms (see dyn_g0_a), else nullptr
   const PolyPhase* pinfo;
   const PhaseCol* pcols;
   const SchedInfo* sched;       // per endeffector
@@ -857,53 +858,78 @@ TG_HD double dot3(const double a[3], const double b[3]) { return a[0] * b[0] + a
 // ----------------------------------------------------------------------------------------------
 
 // DynamicConstraint instant (dynamic_constraint.cc:63-148, single_rigid_body_dynamics.cc:76-204)
+// Group 0 of a DynamicConstraint instant (g: GetDynamicViolation :76-102; d/d base-lin:
+// GetJacobianWrtBaseLin :104-122) in two phases. Phase A needs no endeffector sum; phase B takes
+// sum_ee (f x (c - p) + tau) and sum_ee f. On the device the endeffector lanes of the same instant
+// deposit their terms in LDS (Ctx::dyn_scratch) and phase B runs after a block barrier, so the
+// group-0 lane no longer evaluates 3 E splines in a latency-bound loop; the host sums inline in the
+// same order.
+struct DynG0 { double ab[3], La[3], Lp[3], Hp[4]; int poly; };
+template <class Emit>
+TG_HD void dyn_g0_a(const Ctx& c, const ItemDesc& it, Emit& em, DynG0& st) {
+  const double t = it.t;
+  const int r0 = it.row0;
+  SplinePt L; spline_eval(c, SP_BASE_LIN, t, L);
+  SplinePt A; spline_eval(c, SP_BASE_ANG, t, A);
+  double R[3][3], w[3], wd[3];
+  if (c.rotvec) rv_state(A, R, w, wd);
+  else {
+    const Trig q = trig(A.p);
+    euler_R(q, R);
+    euler_w_wd(q, A.v, A.a, w, wd);
+  }
+  // I_w = R I_b R^T
+  double RI[3][3], Iw[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) RI[i][j] = R[i][0] * c.rb.Ib[0 * 3 + j] + R[i][1] * c.rb.Ib[1 * 3 + j] + R[i][2] * c.rb.Ib[2 * 3 + j];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) Iw[i][j] = RI[i][0] * R[j][0] + RI[i][1] * R[j][1] + RI[i][2] * R[j][2];
+  double a[3], Iww[3], b[3];
+  mat3_vec(Iw, wd, a); mat3_vec(Iw, w, Iww); cross3(w, Iww, b);
+  for (int e = 0; e < 3; ++e) { st.ab[e] = a[e] + b[e]; st.La[e] = L.a[e]; st.Lp[e] = L.p[e]; }
+  st.poly = L.poly;
+  double Ha[4];
+  spline_basis(L, kPos, st.Hp); spline_basis(L, kAcc, Ha);
+  for (int e = 0; e < 3; ++e)
+    for (int bb = 0; bb < 4; ++bb) em(r0 + LX + e, basis_col(c, SP_BASE_LIN, L.poly, bb, e), c.rb.m * Ha[bb], true);
+}
+// one endeffector's terms of the sums at an instant: ts = f x (c - p) + tau, fs = f
+TG_HD void dyn_ee_terms(const double Lp[3], const SplinePt& F, const SplinePt& Tq, const SplinePt& P, double out[6]) {
+  const double rr[3] = {Lp[0] - P.p[0], Lp[1] - P.p[1], Lp[2] - P.p[2]};
+  double cr[3]; cross3(F.p, rr, cr);
+  for (int e = 0; e < 3; ++e) { out[e] = cr[e] + Tq.p[e]; out[3 + e] = F.p[e]; }
+}
+template <class Emit>
+TG_HD void dyn_g0_b(const Ctx& c, const ItemDesc& it, Emit& em, const DynG0& st, const double fs[3], const double ts[3]) {
+  const int r0 = it.row0;
+  for (int e = 0; e < 3; ++e) em.g(r0 + AX + e, st.ab[e] - ts[e]);
+  const double grav[3] = {0.0, 0.0, -c.rb.m * c.rb.g};
+  for (int e = 0; e < 3; ++e) em.g(r0 + LX + e, c.rb.m * st.La[e] - fs[e] - grav[e]);
+  for (int r = 0; r < 3; ++r)
+    for (int d = 1; d <= 2; ++d) {
+      const int e = (r + d) % 3;
+      const double sc = -cross_el(fs, r, e);  // -(sum_ee Cross(f_ee))[r][e]
+      for (int bb = 0; bb < 4; ++bb) em(r0 + AX + r, basis_col(c, SP_BASE_LIN, st.poly, bb, e), sc * st.Hp[bb], true);
+    }
+}
+
 template <class Emit>
 TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
   const double t = it.t;
   const int r0 = it.row0, E = c.rb.n_ee;
-  if (it.group == 0) {
-    // g (GetDynamicViolation :76-102) + d/d base-lin (GetJacobianWrtBaseLin :104-122)
-    SplinePt L; spline_eval(c, SP_BASE_LIN, t, L);
-    SplinePt A; spline_eval(c, SP_BASE_ANG, t, A);
-    double R[3][3], w[3], wd[3];
-    if (c.rotvec) rv_state(A, R, w, wd);
-    else {
-      const Trig q = trig(A.p);
-      euler_R(q, R);
-      euler_w_wd(q, A.v, A.a, w, wd);
-    }
+  if (it.group == 0) {   // both phases inline (host structure pass; see dyn_g0_a)
+    DynG0 st;
+    dyn_g0_a(c, it, em, st);
     double fs[3] = {0, 0, 0}, ts[3] = {0, 0, 0};
-#pragma unroll 1
     for (int ee = 0; ee < E; ++ee) {
       SplinePt F, Tq, P;
       spline_eval(c, sp_force(ee), t, F);
       spline_eval(c, sp_torque(ee), t, Tq);
       spline_eval(c, sp_motion(ee), t, P);
-      double rr[3] = {L.p[0] - P.p[0], L.p[1] - P.p[1], L.p[2] - P.p[2]}, cr[3];
-      cross3(F.p, rr, cr);
-      for (int e = 0; e < 3; ++e) { ts[e] += cr[e] + Tq.p[e]; fs[e] += F.p[e]; }
+      double v[6]; dyn_ee_terms(st.Lp, F, Tq, P, v);
+      for (int e = 0; e < 3; ++e) { ts[e] += v[e]; fs[e] += v[3 + e]; }
     }
-    // I_w = R I_b R^T
-    double RI[3][3], Iw[3][3];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) RI[i][j] = R[i][0] * c.rb.Ib[0 * 3 + j] + R[i][1] * c.rb.Ib[1 * 3 + j] + R[i][2] * c.rb.Ib[2 * 3 + j];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) Iw[i][j] = RI[i][0] * R[j][0] + RI[i][1] * R[j][1] + RI[i][2] * R[j][2];
-    double a[3], Iww[3], b[3];
-    mat3_vec(Iw, wd, a); mat3_vec(Iw, w, Iww); cross3(w, Iww, b);
-    for (int e = 0; e < 3; ++e) em.g(r0 + AX + e, a[e] + b[e] - ts[e]);
-    const double grav[3] = {0.0, 0.0, -c.rb.m * c.rb.g};
-    for (int e = 0; e < 3; ++e) em.g(r0 + LX + e, c.rb.m * L.a[e] - fs[e] - grav[e]);
-    double Hp[4], Ha[4];
-    spline_basis(L, kPos, Hp); spline_basis(L, kAcc, Ha);
-    for (int r = 0; r < 3; ++r)
-      for (int d = 1; d <= 2; ++d) {
-        const int e = (r + d) % 3;
-        const double s = -cross_el(fs, r, e);  // -(sum_ee Cross(f_ee))[r][e]
-        for (int bb = 0; bb < 4; ++bb) em(r0 + AX + r, basis_col(c, SP_BASE_LIN, L.poly, bb, e), s * Hp[bb], true);
-      }
-    for (int e = 0; e < 3; ++e)
-      for (int bb = 0; bb < 4; ++bb) em(r0 + LX + e, basis_col(c, SP_BASE_LIN, L.poly, bb, e), c.rb.m * Ha[bb], true);
+    dyn_g0_b(c, it, em, st, fs, ts);
     return;
   }
   if (it.group == 1 && c.rotvec) {
@@ -1047,6 +1073,11 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
   spline_eval(c, sp_force(ee), t, F);
   spline_eval(c, sp_torque(ee), t, Tq);
   spline_eval(c, sp_motion(ee), t, P);
+  if (c.dyn_scratch) {   // this endeffector's terms of the group-0 sums (it.a2 = instant within the tile)
+    double v[6]; dyn_ee_terms(L.p, F, Tq, P, v);
+    double* d = c.dyn_scratch + (it.a2 * E + ee) * 6;
+    for (int q = 0; q < 6; ++q) d[q] = v[q];
+  }
   const double rv[3] = {L.p[0] - P.p[0], L.p[1] - P.p[1], L.p[2] - P.p[2]};
   double H[4];
   spline_basis(F, kPos, H);

@@ -746,6 +746,7 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
             const int lane = type_lane(type, it.group, k - a, b - a, E);
             if (lane < 0 || lane >= sp.block || lanes[lane].type != IT_NONE) { err = "internal: lane assignment"; return TOWR_ERR_INVALID; }
             lanes[lane] = it;
+            if (type == IT_DYN) lanes[lane].a2 = k - a;   // instant within the tile (LDS sum terms)
           }
         td.i0 = (int32_t)per_type_items[type].size();   // relative; rebased below
         per_type_items[type].insert(per_type_items[type].end(), lanes.begin(), lanes.end());
@@ -771,6 +772,10 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
       L.type_lds_dummy_off[t] = (maxv + 1) & ~1;
       L.type_lds_rows_off[t] = L.type_lds_dummy_off[t] + 64;   // one per wave lane: waves never collide within an instruction
       L.type_lds[t] = L.type_lds_rows_off[t] + ((maxr + 1) & ~1);
+      if (t == IT_DYN) {   // + per-instant endeffector sum terms (dyn_g0_a)
+        L.dyn_scr_off = L.type_lds[t];
+        L.type_lds[t] += type_spec(IT_DYN, E).max_inst * E * 6;
+      }
     }
     L.type_tile0[IT_COUNT] = (int32_t)L.tiles.size();
     // the small kinds (one-wave tiles) share one launch: up to 4 tiles per block, one per wave, with

@@ -49,6 +49,7 @@ struct KParams {
   int32_t B, tile0, ntiles;
   int32_t lds_rows_off;          // start of the g buffer in the dynamic LDS (doubles)
   int32_t lds_x_off;             // start of the staged x (+ zero slot) and node-column table
+  int32_t lds_scr_off;           // DYN: per-instant endeffector sum terms (instants x n_ee x 6)
   int32_t n, n_pad, n_nodecol;
   int32_t want_g, want_jac, fdisc_motion;
   const int32_t* misc_tiles;      // merged small-kind launch: kMiscWaves tile ids per group
@@ -218,18 +219,32 @@ __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_ker
 #ifdef TOWR_PHASE_TIMING
   if (threadIdx.x < 64) TSTAMP(2, TS_MEM());
 #endif
-  const double* xsrc = xs;
-  const int32_t* ncsrc = ns;
+  Ctx c;
+  c.seg = nullptr; c.sg = P.sg; c.row = it.seg;
+  c.x = xs; c.nodecol = ns; c.spl = P.spl; c.dur = P.dur;
+  c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
+  c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
+  c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.sched = P.sched; c.eelin = P.eelin;
+  c.rotvec = ROTVEC;
+  c.dyn_scratch = TYPE == IT_DYN ? smem + P.lds_scr_off : nullptr;
+  DynG0 g0;   // DYN group 0 between its two phases
   if (it.type == TYPE) {
-    Ctx c;
-    c.seg = nullptr; c.sg = P.sg; c.row = it.seg;
-    c.x = xsrc; c.nodecol = ncsrc; c.spl = P.spl; c.dur = P.dur;
-    c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
-    c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
-    c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.sched = P.sched; c.eelin = P.eelin;
-    c.rotvec = ROTVEC;
-    eval_typed<TYPE>(c, it, em);
-    em.flush();
+    if constexpr (TYPE == IT_DYN) {
+      if (it.group == 0) dyn_g0_a(c, it, em, g0);
+      else eval_dyn(c, it, em);   // group 1 and the endeffector groups (these deposit their sum terms)
+    } else {
+      eval_typed<TYPE>(c, it, em);
+    }
+  }
+  if constexpr (TYPE == IT_DYN) {   // phase B of group 0: the endeffector sums from LDS
+    __syncthreads();
+    if (it.type == TYPE && it.group == 0) {
+      double fs[3] = {0, 0, 0}, ts[3] = {0, 0, 0};
+      const double* d = c.dyn_scratch + it.a2 * P.rb.n_ee * 6;
+      for (int ee = 0; ee < P.rb.n_ee; ++ee)
+        for (int e = 0; e < 3; ++e) { ts[e] += d[ee * 6 + e]; fs[e] += d[ee * 6 + 3 + e]; }
+      dyn_g0_b(c, it, em, g0, fs, ts);
+    }
   }
 #ifdef TOWR_PHASE_TIMING
   if ((threadIdx.x >> 6) < 4) TSTAMP(3 + (threadIdx.x >> 6), TS_MEM());
@@ -288,6 +303,7 @@ __global__ void __launch_bounds__(64 * kMiscWaves, 1) towr_misc_kernel(KParams P
     c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
     c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.sched = P.sched; c.eelin = P.eelin;
     c.rotvec = false;   // no small kind uses the base orientation
+    c.dyn_scratch = nullptr;
     switch (it.type) {   // wave-uniform: a wave holds one tile of one kind
       case IT_FNODE: eval_fnode(c, it, em); break;
       case IT_TERR: eval_height(c, it, sp_motion(it.ee), 0.0, em); break;
@@ -356,6 +372,7 @@ __global__ void __launch_bounds__(kCostBlock, 1) towr_cost_kernel(KParams P) {
   c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
   c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.sched = P.sched; c.eelin = P.eelin;
   c.rotvec = ROTVEC;
+  c.dyn_scratch = nullptr;
   for (int i = threadIdx.x; i < P.n_citems; i += kCostBlock) {
     const CostItem it = P.citems[i];
     c.seg = nullptr; c.sg = P.sg; c.row = it.seg;
@@ -523,6 +540,7 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
     } else {
       P.tile0 = L.type_tile0[class_type(lc)];
       P.lds_rows_off = L.type_lds_rows_off[class_type(lc)];
+      P.lds_scr_off = L.dyn_scr_off;
     }
     P.n = L.n; P.n_pad = (L.n + 2) & ~1; P.n_nodecol = (int32_t)L.nodecol.size();
     P.lds_x_off = (int32_t)lds_region(L, lc);
