@@ -28,6 +28,25 @@ __global__ void w_nt_chunk(dbl2_t* p, size_t n, int chunk) {
     __builtin_nontemporal_store(v, p + base + i);
   }
 }
+// each lane stores U consecutive 16-B units (a wave covers 64*U*16 B contiguous)
+template <int U>
+__global__ void w_nt_u(dbl2_t* p, size_t n) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x * U;
+  for (size_t i = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * U; i + U <= n; i += stride) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) { dbl2_t v; v.x = (double)(i + u); v.y = 1.0; __builtin_nontemporal_store(v, p + i + u); }
+  }
+}
+// wave-contiguous: lane l of a wave stores units base + u*64 + l (U stores of 1 KiB each)
+template <int U>
+__global__ void w_nt_wu(dbl2_t* p, size_t n) {
+  const size_t waves = (size_t)gridDim.x * blockDim.x / 64, wid = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / 64;
+  const int l = threadIdx.x & 63;
+  for (size_t base = wid * 64 * U; base + 64 * U <= n; base += waves * 64 * U) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) { dbl2_t v; v.x = (double)u; v.y = 1.0; __builtin_nontemporal_store(v, p + base + u * 64 + l); }
+  }
+}
 __global__ void r_sum(const dbl2_t* p, size_t n, double* out) {
   double s = 0.0;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
@@ -65,6 +84,17 @@ int main() {
     char nm[64];
     std::snprintf(nm, sizeof nm, "write_nt tiles %d B", chunk * 16);
     run(nm, [&] { w_nt_chunk<<<(unsigned)((n + chunk - 1) / chunk), 192>>>(a, n, chunk); }, (double)bytes);
+  }
+  for (int blocks : {2048, 8192}) {
+    char nm[64];
+    std::snprintf(nm, sizeof nm, "write_nt_u4 grid %d", blocks);
+    run(nm, [&] { w_nt_u<4><<<blocks, 256>>>(a, n); }, (double)bytes);
+    std::snprintf(nm, sizeof nm, "write_nt_wu4 grid %d", blocks);
+    run(nm, [&] { w_nt_wu<4><<<blocks, 256>>>(a, n); }, (double)bytes);
+    std::snprintf(nm, sizeof nm, "write_nt_wu8 grid %d", blocks);
+    run(nm, [&] { w_nt_wu<8><<<blocks, 256>>>(a, n); }, (double)bytes);
+    std::snprintf(nm, sizeof nm, "write_nt 1024thr grid %d", blocks / 4);
+    run(nm, [&] { w_nt<<<blocks / 4, 1024>>>(a, n); }, (double)bytes);
   }
   run("read grid 4096", [&] { r_sum<<<4096, 256>>>(a, n, o); }, (double)bytes);
   run("copy_nt grid 4096", [&] { copy_nt<<<4096, 256>>>(a, b, n); }, 2.0 * bytes);
