@@ -229,6 +229,19 @@ int towr_gpu_eval_grad_f(towr_gpu_handle h, const double* x, double* grad);
 int towr_gpu_eval_cost_batch_device(towr_gpu_handle h, int32_t B, const double* X, int64_t ldx,
                                     double* F, double* GRAD, int64_t ldgrad, void* stream);
 
+/* ---- trajectory export: SaveTrajectoryToCSV (towr/src/utils/save_data.cpp:9-130) ------------ */
+/* Samples at t = 0, dt, 2dt, ... (accumulated) while t <= T + 1e-9, T = the base-linear spline's total
+ * time. Row layout, n_cols = 19 + 25 * n_ee doubles:
+ *   t | base-lin pos vel acc | base-ang pos vel acc (the raw angular spline: Euler angles or rotation
+ *   vector and its derivatives) | per ee: motion pos vel acc | ee-ang pos vel acc | force | torque |
+ *   is_contact (1.0 / 0.0)                                                                        */
+int towr_gpu_trajectory_size(towr_gpu_handle h, double dt, int32_t* n_samples, int32_t* n_cols);
+/* one problem, host buffers: out = n_samples x n_cols row-major                                   */
+int towr_gpu_sample_trajectory(towr_gpu_handle h, const double* x, double dt, double* out);
+/* B problems on the device: OUT[b * ldo + k * n_cols + c], ldo >= n_samples * n_cols              */
+int towr_gpu_sample_trajectory_batch_device(towr_gpu_handle h, int32_t B, const double* X, int64_t ldx, double dt,
+                                            double* OUT, int64_t ldo, void* stream);
+
 /* ---- batched evaluation over independent problems that share the layout ---------------------- */
 /* Per-problem terrain parameters (the only per-instance input to g/J besides x). `terrains` is a
  * host array of B entries; all entries must keep the Jacobian pattern identical. */

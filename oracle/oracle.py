@@ -41,6 +41,7 @@ def lib():
         L.oracle_eval_jac_values.argtypes = [C.c_void_p, D, D]
         L.oracle_eval_f.argtypes = [C.c_void_p, D, D]
         L.oracle_eval_grad_f.argtypes = [C.c_void_p, D, D]
+        L.oracle_sample_trajectory.argtypes = [C.c_void_p, D, C.c_double, D]
         L.oracle_constraint_rows.argtypes = [C.c_void_p, C.c_int, I, I]
         L.oracle_varset_cols.argtypes = [C.c_void_p, C.c_int, I, I]
         L.oracle_bench.restype = C.c_double
@@ -99,6 +100,14 @@ class Oracle:
         g = np.zeros(self.n)
         lib().oracle_eval_grad_f(self.h, _d(x), _d(g))
         return g
+
+    def sample_trajectory(self, x, dt):
+        """SaveTrajectoryToCSV's sample rows (save_data.cpp:9-130): (n_samples, 19 + 25 E)."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        ns = lib().oracle_sample_trajectory(self.h, _d(x), dt, None)
+        out = np.zeros((ns, 19 + 25 * self.desc.robot.n_ee))
+        lib().oracle_sample_trajectory(self.h, _d(x), dt, _d(out))
+        return out
 
     def eval_jac(self, x):
         """(rows, cols, vals) of GetJacobianOfConstraints at x — pattern at x, sorted row-major."""

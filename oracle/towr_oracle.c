@@ -2323,6 +2323,40 @@ int oracle_eval_grad_f(oracle_t* o, const double* x, double* grad) {
   return 0;
 }
 
+/* SaveTrajectoryToCSV (save_data.cpp:9-130): rows at t = 0, dt, ... (accumulated) while t <= T + 1e-9,
+ * 19 + 25 E columns (include/towr_gpu.h). Returns the sample count; out = NULL only counts. */
+int oracle_sample_trajectory(oracle_t* o, const double* x, double dt, double* out) {
+  if (!(dt > 0.0)) return -1;
+  if (x) set_variables(o, x);
+  double T = 0.0;
+  for (int i = 0; i < o->s_lin->n_polys; ++i) T += o->s_lin->polys[i].T;
+  const int E = o->n_ee, cols = 19 + 25 * E;
+  int k = 0;
+  for (double t = 0.0; t <= T + 1e-9; t += dt, ++k) {
+    if (!out) continue;
+    double* row = out + (size_t)k * cols, st[3][3];
+    row[0] = t;
+    const Spline* base[2] = {o->s_lin, o->s_ang};
+    for (int s = 0; s < 2; ++s) {
+      spline_point(base[s], t, st);
+      for (int d = 0; d < 3; ++d) for (int e = 0; e < 3; ++e) row[1 + 9 * s + 3 * d + e] = st[d][e];
+    }
+    for (int ee = 0; ee < E; ++ee) {
+      double* r = row + 19 + 25 * ee;
+      spline_point(o->s_motion[ee], t, st);
+      for (int d = 0; d < 3; ++d) for (int e = 0; e < 3; ++e) r[3 * d + e] = st[d][e];
+      spline_point(o->s_ang_ee[ee], t, st);
+      for (int d = 0; d < 3; ++d) for (int e = 0; e < 3; ++e) r[9 + 3 * d + e] = st[d][e];
+      spline_point(o->s_force[ee], t, st);
+      for (int e = 0; e < 3; ++e) r[18 + e] = st[kPos][e];
+      spline_point(o->s_torque[ee], t, st);
+      for (int e = 0; e < 3; ++e) r[21 + e] = st[kPos][e];
+      r[24] = pd_is_contact(o->pd[ee], t) ? 1.0 : 0.0;
+    }
+  }
+  return k;
+}
+
 int oracle_sizes(oracle_t* o, int* n, int* m) { *n = o->n; *m = o->m; return 0; }
 
 /* ifopt Composite::GetValues over the variable sets */

@@ -40,6 +40,7 @@ long      oracle_eval_jac_values(oracle_t* o, const double* x, double* values);
 /* objective (sum of the cost terms) and its dense gradient */
 int       oracle_eval_f(oracle_t* o, const double* x, double* f);
 int       oracle_eval_grad_f(oracle_t* o, const double* x, double* grad);
+int       oracle_sample_trajectory(oracle_t* o, const double* x, double dt, double* out);  /* rows, or -1 */
 /* constraint-set row ranges: row0 / n_rows of constraint i                                      */
 int       oracle_constraint_rows(oracle_t* o, int i, int* row0, int* n_rows);
 int       oracle_varset_cols(oracle_t* o, int i, int* col0, int* n_cols);

@@ -141,3 +141,28 @@ extern "C" int emu_conflicts(const towr_problem_desc_t* d, int swz) {
   }
   return 0;
 }
+
+// trajectory rows through engine_math.h's traj_row (host instantiation)
+extern "C" int emu_traj(const towr_problem_desc_t* d, const double* x, double dt, double* out, int max_rows) {
+  Layout L; std::string e;
+  if (build_layout(*d, L, e)) return -1;
+  std::vector<double> pd((size_t)TOWR_MAX_EE * TOWR_MAX_PHASES, 0.0);
+  std::vector<int32_t> pn(TOWR_MAX_EE, 0), pc(TOWR_MAX_EE, 0);
+  for (int ee = 0; ee < d->robot.n_ee; ++ee) {
+    pn[ee] = d->n_phases[ee]; pc[ee] = d->contact_at_start[ee] != 0;
+    for (int q = 0; q < d->n_phases[ee]; ++q) pd[(size_t)ee * TOWR_MAX_PHASES + q] = d->phase_durations[ee][q];
+  }
+  TrajPhases ph{pd.data(), pn.data(), pc.data()};
+  Ctx c{};
+  c.x = x; c.nodecol = L.nodecol.data(); c.spl = L.spl.data(); c.dur = L.dur.data();
+  c.ter = &L.terrain; c.rb = L.rb; c.fdisc_motion = L.fdisc_motion;
+  c.gait = L.gait; c.pinfo = L.pinfo.data(); c.pcols = L.pcols.data(); c.sched = L.sched.data();
+  c.eelin = L.eelin.data(); c.rotvec = L.rotvec;
+  double T = 0.0;
+  for (int i = 0; i < L.spl[0].n_polys; ++i) T += L.dur[L.spl[0].dur_off + i];
+  const int cols = traj_cols(L.rb.n_ee);
+  int k = 0;
+  for (double t = 0.0; t <= T + 1e-9; t += dt, ++k)
+    if (k < max_rows) traj_row(c, ph, t, out + (size_t)k * cols, 1);
+  return k;
+}

@@ -88,3 +88,12 @@ def test_cpp_callbacks_on_gpu_match_oracle(exe, tmp_path, cfg):
     r, _, v = o.eval_jac(x0)
     assert_close(o.eval_g(x0), res["g"], r, v, res["values"], o.m, f"C++ host {cfg}")
     assert_cost_close(o.eval_f(x0), res["f"], o.eval_grad_f(x0), res["grad"], f"C++ host {cfg} costs")
+    # SaveTrajectoryToCSV text from the C++ host (6 decimals) against the oracle's samples
+    from towr2025_amd import trajectory as T
+    text = open(str(tmp_path / "o.bin") + ".csv").read().splitlines()
+    n_ee = CFGS[cfg]().robot.n_ee
+    assert text[0] == ",".join(T.csv_header(n_ee))
+    got = np.array([[float(v) for v in line.split(",")] for line in text[1:]])
+    ref = o.sample_trajectory(x0, 0.01)
+    assert got.shape == ref.shape
+    np.testing.assert_allclose(got, ref, rtol=0, atol=5e-7 + 1e-12 * np.abs(ref).max())

@@ -119,6 +119,10 @@ SYMBOLS = {
     "towr_gpu_eval_grad_f": (C.c_int, [_HANDLE, _DP, _DP]),
     "towr_gpu_eval_cost_batch_device": (C.c_int, [_HANDLE, C.c_int32, C.c_void_p, C.c_int64, C.c_void_p,
                                                    C.c_void_p, C.c_int64, C.c_void_p]),
+    "towr_gpu_trajectory_size": (C.c_int, [_HANDLE, C.c_double, _IP, _IP]),
+    "towr_gpu_sample_trajectory": (C.c_int, [_HANDLE, _DP, C.c_double, _DP]),
+    "towr_gpu_sample_trajectory_batch_device": (C.c_int, [_HANDLE, C.c_int32, C.c_void_p, C.c_int64, C.c_double,
+                                                          C.c_void_p, C.c_int64, C.c_void_p]),
     "towr_gpu_set_batch_terrain": (C.c_int, [_HANDLE, C.c_int32, C.POINTER(Terrain)]),
     "towr_gpu_eval_batch_device": (C.c_int, [_HANDLE, C.c_int32, C.c_void_p, C.c_int64,
                                               C.c_void_p, C.c_int64, C.c_void_p, C.c_int64,

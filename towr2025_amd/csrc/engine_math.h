@@ -1690,6 +1690,66 @@ TG_HD void eval_cost_item(const Ctx& c, const CostItem& it, Emit& em) {
   }
 }
 
+// ----------------------------------------------------------------------------------------------
+// Trajectory export (SaveTrajectoryToCSV, towr/src/utils/save_data.cpp:9-130): one row per sample
+// time, columns (traj_cols = 19 + 25 E):
+//   time | base-lin p v a | base-ang p v a (the raw spline: Euler angles or rotation vector and their
+//   time derivatives, as the reference writes them) | per ee: motion p v a | ee-ang p v a |
+//   force p | torque p | is_contact (PhaseDurations::IsContactPhase, phase_durations.cc:120-124)
+// ----------------------------------------------------------------------------------------------
+TG_HD int traj_cols(int E) { return 19 + 25 * E; }
+// fixed phase durations (no phase-duration optimisation): [ee * TOWR_MAX_PHASES + phase], counts,
+// contact at start
+struct TrajPhases { const double* d; const int32_t* n; const int32_t* c0; };
+
+// Spline::GetPoint at an arbitrary time (spline.cc:80-93): the segment scan, then the polynomial
+TG_HD void spline_eval_at(const Ctx& c, int s, double t, SplinePt& o) {
+  o.H = nullptr;
+  if (c.gait && c.spl[s].ee >= 0) {
+    o.dyn = true;
+    phase_spline_locate(c, s, t, o);
+  } else {
+    o.dyn = false;
+    const SplineMeta m = c.spl[s];
+    o.poly = seg_lookup(c.dur + m.dur_off, m.n_polys, t, &o.tl);
+    o.T = c.dur[m.dur_off + o.poly];
+  }
+  poly_state(c, s, o.poly, o.T, o.tl, o);
+}
+
+TG_HD void traj_row(const Ctx& c, const TrajPhases& ph, double t, double* row, int stride) {
+  const int E = c.rb.n_ee;
+  row[0] = t;
+  SplinePt P;
+  for (int s = 0; s < 2; ++s) {   // base-lin, base-ang
+    spline_eval_at(c, s, t, P);
+    for (int e = 0; e < 3; ++e) {
+      row[(1 + 9 * s + e) * stride] = P.p[e];
+      row[(4 + 9 * s + e) * stride] = P.v[e];
+      row[(7 + 9 * s + e) * stride] = P.a[e];
+    }
+  }
+  for (int ee = 0; ee < E; ++ee) {
+    const int b = 19 + 25 * ee;
+    spline_eval_at(c, sp_motion(ee), t, P);
+    for (int e = 0; e < 3; ++e) { row[(b + e) * stride] = P.p[e]; row[(b + 3 + e) * stride] = P.v[e]; row[(b + 6 + e) * stride] = P.a[e]; }
+    spline_eval_at(c, sp_ang(ee), t, P);
+    for (int e = 0; e < 3; ++e) { row[(b + 9 + e) * stride] = P.p[e]; row[(b + 12 + e) * stride] = P.v[e]; row[(b + 15 + e) * stride] = P.a[e]; }
+    spline_eval_at(c, sp_force(ee), t, P);
+    for (int e = 0; e < 3; ++e) row[(b + 18 + e) * stride] = P.p[e];
+    spline_eval_at(c, sp_torque(ee), t, P);
+    for (int e = 0; e < 3; ++e) row[(b + 21 + e) * stride] = P.p[e];
+    bool contact;
+    if (c.gait) contact = sched_is_contact(c, ee, ph.c0[ee] != 0, t);
+    else {
+      double tl;
+      const int id = seg_lookup(ph.d + ee * TOWR_MAX_PHASES, ph.n[ee], t, &tl);
+      contact = (id % 2 == 0) ? (ph.c0[ee] != 0) : (ph.c0[ee] == 0);
+    }
+    row[(b + 24) * stride] = contact ? 1.0 : 0.0;
+  }
+}
+
 template <class Emit>
 TG_HD void eval_item(const Ctx& c, const ItemDesc& it, Emit& em) {
   switch (it.type) {

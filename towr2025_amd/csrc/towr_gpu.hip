@@ -400,6 +400,44 @@ const void* cost_kernel_for(bool gait, bool grad, bool rotvec) {
   return grad ? cost_kernel_rv<false, true>(rotvec) : cost_kernel_rv<false, false>(rotvec);
 }
 
+// Trajectory export (SaveTrajectoryToCSV): one 64-lane block per (problem, 64 sample times). Each
+// lane evaluates its sample's row into an LDS buffer kept column-major with an odd stride (writes and
+// reads both conflict-free); the block's rows are one contiguous output range, copied out coalesced.
+constexpr int kTrajBlock = 64;
+template <bool GAIT>
+__global__ void __launch_bounds__(kTrajBlock, 1) towr_traj_kernel(KParams P, const double* times, int ns, TrajPhases ph,
+                                                                   double* OUT, int64_t ldo, int32_t lds_x_off) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int nb = (ns + kTrajBlock - 1) / kTrajBlock;
+  const int b = blockIdx.x / nb, k0 = (blockIdx.x % nb) * kTrajBlock;
+  const int cols = traj_cols(P.rb.n_ee), stride = kTrajBlock + 1;
+  double* rows = smem;
+  double* xs = smem + lds_x_off;
+  int32_t* nsp = reinterpret_cast<int32_t*>(xs + P.n_pad);
+  stage_x<kTrajBlock, true>(P, P.X + (int64_t)b * P.ldx, xs, nsp);
+  __syncthreads();
+  const int k = k0 + (int)threadIdx.x;
+  if (k < ns) {
+    Ctx c;
+    c.seg = nullptr; c.row = -1;
+    c.x = xs; c.nodecol = nsp; c.spl = P.spl; c.dur = P.dur;
+    c.ter = P.terrains; c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
+    c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.sched = P.sched; c.eelin = P.eelin;
+    c.rotvec = false; c.dyn_scratch = nullptr;
+    traj_row(c, ph, times[k], rows + threadIdx.x, stride);
+  }
+  __syncthreads();
+  const int cnt = min(kTrajBlock, ns - k0);
+  double* out = OUT + (int64_t)b * ldo + (int64_t)k0 * cols;
+  for (int i = threadIdx.x; i < cnt * cols; i += kTrajBlock) {
+    const int r = i / cols, col = i - r * cols;
+    __builtin_nontemporal_store(rows[col * stride + r], out + i);
+  }
+}
+const void* traj_kernel_for(bool gait) {
+  return gait ? reinterpret_cast<const void*>(&towr_traj_kernel<true>) : reinterpret_cast<const void*>(&towr_traj_kernel<false>);
+}
+
 // DYN and ROM read the base orientation and come in Euler / RotVec variants; the others do not
 template <bool GAIT, bool ROTVEC>
 const void* kernel_for_mode(int type) {
@@ -458,6 +496,13 @@ struct towr_gpu_handle_s {
   double *h_x = nullptr, *h_g = nullptr, *h_v = nullptr;
   int32_t stage_B = 0;
   double *d_f = nullptr, *d_grad = nullptr;   // host-pointer objective entry points (one problem)
+  // trajectory export: fixed phase table and the sample times of the last dt
+  double* d_traj_pd = nullptr;
+  int32_t* d_traj_n = nullptr;
+  int32_t* d_traj_c0 = nullptr;
+  double* d_traj_t = nullptr;
+  double traj_dt = 0.0;
+  int32_t traj_ns = 0;
 };
 
 namespace {
@@ -587,6 +632,51 @@ int launch_cost(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* 
   return TOWR_OK;
 }
 
+// SaveTrajectoryToCSV's sample times: t = 0, dt, ... accumulated while t <= T + 1e-9, with
+// T = base_linear_->GetTotalTime() (save_data.cpp:14, 55-58)
+std::vector<double> traj_times(const Layout& L, double dt) {
+  double T = 0.0;
+  for (int i = 0; i < L.spl[0].n_polys; ++i) T += L.dur[L.spl[0].dur_off + i];
+  std::vector<double> ts;
+  for (double t = 0.0; t <= T + 1e-9; t += dt) ts.push_back(t);
+  return ts;
+}
+constexpr int64_t kTrajMaxSamples = 1 << 22;
+
+int launch_traj(towr_gpu_handle h, int B, const double* X, int64_t ldx, double dt, double* OUT, int64_t ldo, hipStream_t s) {
+  const Layout& L = h->L;
+  if (!(dt > 0.0)) return fail(h, TOWR_ERR_INVALID, "sample period must be > 0");
+  if (dt != h->traj_dt || !h->d_traj_t) {
+    const std::vector<double> ts = traj_times(L, dt);
+    if ((int64_t)ts.size() > kTrajMaxSamples) return fail(h, TOWR_ERR_INVALID, "too many trajectory samples");
+    if (h->d_traj_t) { (void)hipFree(h->d_traj_t); h->d_traj_t = nullptr; }
+    HIPCHK(h, hipMalloc(&h->d_traj_t, sizeof(double) * ts.size()));
+    HIPCHK(h, hipMemcpy(h->d_traj_t, ts.data(), sizeof(double) * ts.size(), hipMemcpyHostToDevice));
+    h->traj_dt = dt; h->traj_ns = (int32_t)ts.size();
+  }
+  const int ns = h->traj_ns, cols = traj_cols(L.rb.n_ee);
+  if (ldo < (int64_t)ns * cols) return fail(h, TOWR_ERR_INVALID, "leading dimension smaller than n_samples * n_cols");
+  if (B <= 0) return TOWR_OK;
+  KParams P{};
+  P.X = X; P.ldx = ldx;
+  P.nodecol = h->d_nodecol; P.spl = h->d_spl; P.dur = h->d_dur;
+  P.pinfo = h->d_pinfo; P.pcols = h->d_pcols; P.sched = h->d_sched; P.eelin = h->d_eelin;
+  P.terrains = h->d_terrain;
+  P.n = L.n; P.n_pad = (L.n + 2) & ~1; P.n_nodecol = (int32_t)L.nodecol.size();
+  P.rb = L.rb;
+  TrajPhases ph{h->d_traj_pd, h->d_traj_n, h->d_traj_c0};
+  const int32_t xoff = ((cols * (kTrajBlock + 1)) + 1) & ~1;
+  const size_t lds = sizeof(double) * ((size_t)xoff + P.n_pad + (L.nodecol.size() + 3) / 4 * 2);
+  if (lds > 160 * 1024) return fail(h, TOWR_ERR_UNSUPPORTED, "trajectory rows exceed the LDS");
+  if (lds > 64 * 1024) HIPCHK(h, hipFuncSetAttribute(traj_kernel_for(L.gait), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  const int64_t grid = (int64_t)B * ((ns + kTrajBlock - 1) / kTrajBlock);
+  if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
+  const double* tp = h->d_traj_t;
+  void* args[] = {&P, &tp, const_cast<int*>(&ns), &ph, &OUT, &ldo, const_cast<int32_t*>(&xoff)};
+  HIPCHK(h, hipLaunchKernel(traj_kernel_for(L.gait), dim3((unsigned)grid), dim3(kTrajBlock), args, lds, s));
+  return TOWR_OK;
+}
+
 int ensure_stage(towr_gpu_handle h, int B) {
   if (B <= h->stage_B) return TOWR_OK;
   const Layout& L = h->L;
@@ -690,6 +780,16 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
       (r = upload(h, &h->d_misc, L.misc_tiles)) || (r = upload(h, &h->d_eelin, L.eelin)) ||
       (r = upload(h, &h->d_citems, L.cost_items)))
     return bail(r);
+  {   // trajectory export: phase durations of the description (fixed gait), counts, contact at start
+    const towr_problem_desc_t& d = L.desc;
+    std::vector<double> pd((size_t)TOWR_MAX_EE * TOWR_MAX_PHASES, 0.0);
+    std::vector<int32_t> pn(TOWR_MAX_EE, 0), pc(TOWR_MAX_EE, 0);
+    for (int ee = 0; ee < d.robot.n_ee; ++ee) {
+      pn[ee] = d.n_phases[ee]; pc[ee] = d.contact_at_start[ee] != 0;
+      for (int q = 0; q < d.n_phases[ee]; ++q) pd[(size_t)ee * TOWR_MAX_PHASES + q] = d.phase_durations[ee][q];
+    }
+    if ((r = upload(h, &h->d_traj_pd, pd)) || (r = upload(h, &h->d_traj_n, pn)) || (r = upload(h, &h->d_traj_c0, pc))) return bail(r);
+  }
   {   // segment table in 32-row blocks (see SegSoA)
     const int nspl = (int)L.spl.size();
     const int nr = L.segs.empty() ? 0 : (int)(L.segs.size() / nspl);
@@ -756,7 +856,8 @@ int towr_gpu_destroy(towr_gpu_handle h) {
   if (!h) return TOWR_OK;
   void* dev[] = {h->d_items, h->d_slots, h->d_tiles, h->d_nodecol, h->d_spl, h->d_dur, h->d_segs, h->d_terrain,
                  h->d_pinfo, h->d_pcols, h->d_sched, h->d_misc, h->d_eelin, h->d_citems,
-                 h->d_bterrain, h->d_x, h->d_g, h->d_v, h->d_f, h->d_grad};
+                 h->d_bterrain, h->d_x, h->d_g, h->d_v, h->d_f, h->d_grad,
+                 h->d_traj_pd, h->d_traj_n, h->d_traj_c0, h->d_traj_t};
   if (h->device >= 0) for (void* p : dev) if (p) (void)hipFree(p);
   void* host[] = {h->h_x, h->h_g, h->h_v};
   for (void* p : host) if (p) (void)hipHostFree(p);
@@ -875,6 +976,42 @@ int towr_gpu_eval_cost_batch_device(towr_gpu_handle h, int32_t B, const double* 
   const bool per = h->d_bterrain && h->bterrain_n >= B;
   return launch_cost(h, B, X, ldx, F, GRAD, ldgrad, reinterpret_cast<hipStream_t>(stream),
                      per ? h->d_bterrain : h->d_terrain, per ? 1 : 0);
+}
+
+int towr_gpu_trajectory_size(towr_gpu_handle h, double dt, int32_t* n_samples, int32_t* n_cols) {
+  if (!h || !(dt > 0.0)) return fail(h, TOWR_ERR_INVALID, "bad argument");
+  const std::vector<double> ts = traj_times(h->L, dt);
+  if ((int64_t)ts.size() > kTrajMaxSamples) return fail(h, TOWR_ERR_INVALID, "too many trajectory samples");
+  if (n_samples) *n_samples = (int32_t)ts.size();
+  if (n_cols) *n_cols = traj_cols(h->L.rb.n_ee);
+  return TOWR_OK;
+}
+
+int towr_gpu_sample_trajectory(towr_gpu_handle h, const double* x, double dt, double* out) {
+  if (!h || !x || !out) return fail(h, TOWR_ERR_INVALID, "null argument");
+  if (int rc = bind(h)) return rc;
+  if (int rc = ensure_stage(h, 1)) return rc;
+  int32_t ns = 0, cols = 0;
+  if (int rc = towr_gpu_trajectory_size(h, dt, &ns, &cols)) return rc;
+  const Layout& L = h->L;
+  HIPCHK(h, hipMemcpyAsync(h->d_x, x, sizeof(double) * L.n, hipMemcpyHostToDevice, h->stream));
+  double* d_out = nullptr;
+  const size_t bytes = sizeof(double) * (size_t)ns * cols;
+  HIPCHK(h, hipMalloc(&d_out, bytes));
+  int rc = launch_traj(h, 1, h->d_x, L.n, dt, d_out, (int64_t)ns * cols, h->stream);
+  if (rc == TOWR_OK && (hipMemcpyAsync(out, d_out, bytes, hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+                        hipStreamSynchronize(h->stream) != hipSuccess))
+    rc = fail(h, TOWR_ERR_HIP, "trajectory copy failed");
+  (void)hipFree(d_out);
+  return rc;
+}
+
+int towr_gpu_sample_trajectory_batch_device(towr_gpu_handle h, int32_t B, const double* X, int64_t ldx, double dt,
+                                            double* OUT, int64_t ldo, void* stream) {
+  if (!h || B < 0 || !X || !OUT) return fail(h, TOWR_ERR_INVALID, "bad argument");
+  if (ldx < h->L.n) return fail(h, TOWR_ERR_INVALID, "leading dimension smaller than n");
+  if (int rc = bind(h)) return rc;
+  return launch_traj(h, B, X, ldx, dt, OUT, ldo, reinterpret_cast<hipStream_t>(stream));
 }
 
 int towr_gpu_set_batch_terrain(towr_gpu_handle h, int32_t B, const towr_terrain_t* terrains) {

@@ -19,6 +19,7 @@
 #pragma once
 
 #include <cstdint>
+#include <cstdio>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -58,6 +59,16 @@ class Engine {
   // objective (ifopt Problem::EvaluateCostFunction) and its dense gradient
   double EvalCostFunction(const double* x) const { double f = 0.0; Check(towr_gpu_eval_f(h_, x, &f)); return f; }
   void EvalCostFunctionGradient(const double* x, double* grad) const { Check(towr_gpu_eval_grad_f(h_, x, grad)); }
+  // trajectory samples (SaveTrajectoryToCSV's rows, include/towr_gpu.h), n_samples x n_cols
+  std::vector<double> SampleTrajectory(const double* x, double T_sample, int* n_samples, int* n_cols) const {
+    int32_t ns = 0, nc = 0;
+    Check(towr_gpu_trajectory_size(h_, T_sample, &ns, &nc));
+    std::vector<double> rows((size_t)ns * nc);
+    Check(towr_gpu_sample_trajectory(h_, x, T_sample, rows.data()));
+    if (n_samples) *n_samples = ns;
+    if (n_cols) *n_cols = nc;
+    return rows;
+  }
   // B independent problems sharing this layout (host buffers, row-major B x n / m / nnz)
   void SetBatchTerrain(const std::vector<towr_terrain_t>& t) { Check(towr_gpu_set_batch_terrain(h_, (int32_t)t.size(), t.data())); }
   void EvalBatch(int B, const double* X, double* G, double* V) const { Check(towr_gpu_eval_batch(h_, B, X, G, V)); }
@@ -135,5 +146,44 @@ class NlpCallbacks {
   std::vector<double> g_, v_;
   bool valid_ = false;
 };
+
+// The CSV text of SaveTrajectoryToCSV (towr/src/utils/save_data.cpp:9-130): the reference's header,
+// fixed notation with 6 decimals, is_contact_phase as 0/1.
+inline bool WriteTrajectoryCSV(std::FILE* fp, const double* rows, int n_samples, int n_ee) {
+  static const char* base[] = {"time", "base_pos_x", "base_pos_y", "base_pos_z", "base_vel_x", "base_vel_y", "base_vel_z",
+                               "base_acc_x", "base_acc_y", "base_acc_z", "base_euler_roll", "base_euler_pitch",
+                               "base_euler_yaw", "base_omega_x", "base_omega_y", "base_omega_z", "base_omegadot_x",
+                               "base_omegadot_y", "base_omegadot_z"};
+  static const char* ee[] = {"ee_pos_x_", "ee_pos_y_", "ee_pos_z_", "ee_vel_x_", "ee_vel_y_", "ee_vel_z_", "ee_acc_x_",
+                             "ee_acc_y_", "ee_acc_z_", "ee_euler_roll_", "ee_euler_pitch_", "ee_euler_yaw_", "ee_omega_x_",
+                             "ee_omega_y_", "ee_omega_z_", "ee_omegadot_x_", "ee_omegadot_y_", "ee_omegadot_z_",
+                             "contact_force_x_", "contact_force_y_", "contact_force_z_", "contact_torque_x_",
+                             "contact_torque_y_", "contact_torque_z_", "is_contact_phase_"};
+  for (int c = 0; c < 19; ++c) std::fprintf(fp, c ? ",%s" : "%s", base[c]);
+  for (int i = 0; i < n_ee; ++i)
+    for (int c = 0; c < 25; ++c) std::fprintf(fp, ",%s%d", ee[c], i);
+  std::fprintf(fp, "\n");
+  const int cols = 19 + 25 * n_ee;
+  for (int k = 0; k < n_samples; ++k) {
+    const double* r = rows + (size_t)k * cols;
+    for (int c = 0; c < cols; ++c) {
+      const bool contact = c >= 19 && (c - 19) % 25 == 24;
+      if (contact) std::fprintf(fp, ",%d", r[c] != 0.0 ? 1 : 0);
+      else std::fprintf(fp, c ? ",%.6f" : "%.6f", r[c]);
+    }
+    std::fprintf(fp, "\n");
+  }
+  return std::ferror(fp) == 0;
+}
+
+// SaveTrajectoryToCSV(solution, filename, T_sample) for a solution vector x of the engine's problem
+inline bool SaveTrajectoryToCSV(const Engine& e, const double* x, const std::string& filename, double T_sample = 0.001) {
+  int ns = 0, nc = 0;
+  const std::vector<double> rows = e.SampleTrajectory(x, T_sample, &ns, &nc);
+  std::FILE* fp = std::fopen(filename.c_str(), "w");
+  if (!fp) return false;
+  const bool ok = WriteTrajectoryCSV(fp, rows.data(), ns, (nc - 19) / 25);
+  return std::fclose(fp) == 0 && ok;
+}
 
 }  // namespace towr_gpu

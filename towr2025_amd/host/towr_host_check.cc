@@ -5,6 +5,7 @@
 //   -> eval_g(x, false) -> eval_jac_g(x, false)
 // and dumps everything to a binary file:
 //   desc bytes | n m (int32) nnz (int64) | x0[n] | iRow[nnz] jCol[nnz] | (device >= 0) g[m] values[nnz] f grad[n]
+// and (device >= 0) the trajectory of x0 sampled at 0.01 s as SaveTrajectoryToCSV writes it, to <out.bin>.csv
 // usage: towr_host_check <anymal|anymal_costs|anymal_rotvec|biped|biped_next|hopper> <out.bin> [device (default -1: layout only)]
 #include <cstdio>
 #include <cstring>
@@ -70,6 +71,8 @@ int main(int argc, char** argv) {
       std::fwrite(v.data(), sizeof(double), v.size(), fp);
       std::fwrite(&obj, sizeof(double), 1, fp);
       std::fwrite(grad.data(), sizeof(double), grad.size(), fp);
+      // the trajectory export of x (SaveTrajectoryToCSV), to <out>.csv
+      if (!SaveTrajectoryToCSV(e, x.data(), std::string(argv[2]) + ".csv", 0.01)) { std::fprintf(stderr, "csv export failed\n"); return 1; }
     }
     std::fclose(fp);
     std::printf("%s: n=%d m=%d nnz=%d%s\n", cfg.c_str(), n, m, nnz, device >= 0 ? " (evaluated on the GPU)" : " (layout only)");

@@ -6,7 +6,9 @@ Mirrors what IPOPT reaches through ifopt's IpoptAdapter for the hot path:
   EvalConstraints(x)                         (IpoptAdapter::eval_g)     -> eval_g(x)
   GetJacobianOfConstraints structure         (eval_jac_g, values=NULL)  -> jac_structure()
   EvalNonzerosOfJacobian(x)                  (eval_jac_g, values!=NULL) -> eval_jac_values(x)
-plus the batched, device-resident entry point used by bench.py.
+  EvaluateCostFunction / ...Gradient         (eval_f / eval_grad_f)     -> eval_f(x) / eval_grad_f(x)
+  SaveTrajectoryToCSV's samples              (save_data.cpp:9-130)      -> sample_trajectory(x, dt)
+plus the batched, device-resident entry points used by bench.py.
 
 Every evaluation runs on the GPU through libtowr_gpu.so; there is no CPU path. A missing or
 unloadable extension raises.
@@ -129,6 +131,29 @@ class TowrGpuProblem:
         self._check(self._lib.towr_gpu_eval_cost_batch_device(
             self._h, B, C.c_void_p(X.data_ptr()), X.stride(0), C.c_void_p(F.data_ptr()),
             C.c_void_p(GRAD.data_ptr() if GRAD is not None else 0), GRAD.stride(0) if GRAD is not None else 0,
+            C.c_void_p(stream.cuda_stream)))
+
+    def trajectory_size(self, dt: float):
+        """(n_samples, n_cols) of the trajectory export at sample period dt."""
+        ns, nc = C.c_int32(), C.c_int32()
+        self._check(self._lib.towr_gpu_trajectory_size(self._h, dt, C.byref(ns), C.byref(nc)))
+        return ns.value, nc.value
+
+    def sample_trajectory(self, x, dt: float = 0.001) -> np.ndarray:
+        """SaveTrajectoryToCSV's samples (save_data.cpp:9-130) on the device: (n_samples, 19 + 25 n_ee)."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        ns, nc = self.trajectory_size(dt)
+        out = np.zeros((ns, nc))
+        self._check(self._lib.towr_gpu_sample_trajectory(self._h, capi.dptr(x), dt, capi.dptr(out)))
+        return out
+
+    def sample_trajectory_batch_device(self, X, dt, OUT, stream=None):
+        """Device batch on torch HIP tensors: X (B, ldx) -> OUT (B, ldo >= n_samples * n_cols)."""
+        import torch
+        if stream is None:
+            stream = torch.cuda.current_stream(X.device)
+        self._check(self._lib.towr_gpu_sample_trajectory_batch_device(
+            self._h, X.shape[0], C.c_void_p(X.data_ptr()), X.stride(0), dt, C.c_void_p(OUT.data_ptr()), OUT.stride(0),
             C.c_void_p(stream.cuda_stream)))
 
     def set_batch_terrain(self, terrains):
