@@ -47,6 +47,22 @@ __global__ void w_nt_wu(dbl2_t* p, size_t n) {
     for (int u = 0; u < U; ++u) { dbl2_t v; v.x = (double)u; v.y = 1.0; __builtin_nontemporal_store(v, p + base + u * 64 + l); }
   }
 }
+// tile pattern with explicit cache-policy bits on global_store_dwordx4
+template <int POL>
+__global__ void w_tile_pol(dbl2_t* p, size_t n, int chunk) {
+  const size_t base = (size_t)blockIdx.x * chunk;
+  for (int i = threadIdx.x; i < chunk; i += blockDim.x) {
+    if (base + i >= n) return;
+    dbl2_t v; v.x = (double)i; v.y = 1.0;
+    dbl2_t* q = p + base + i;
+    if constexpr (POL == 0) asm volatile("global_store_dwordx4 %0, %1, off" :: "v"(q), "v"(v) : "memory");
+    if constexpr (POL == 1) asm volatile("global_store_dwordx4 %0, %1, off nt" :: "v"(q), "v"(v) : "memory");
+    if constexpr (POL == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" :: "v"(q), "v"(v) : "memory");
+    if constexpr (POL == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" :: "v"(q), "v"(v) : "memory");
+    if constexpr (POL == 4) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"(q), "v"(v) : "memory");
+    if constexpr (POL == 5) asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(q), "v"(v) : "memory");
+  }
+}
 __global__ void r_sum(const dbl2_t* p, size_t n, double* out) {
   double s = 0.0;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
@@ -95,6 +111,16 @@ int main() {
     run(nm, [&] { w_nt_wu<8><<<blocks, 256>>>(a, n); }, (double)bytes);
     std::snprintf(nm, sizeof nm, "write_nt 1024thr grid %d", blocks / 4);
     run(nm, [&] { w_nt<<<blocks / 4, 1024>>>(a, n); }, (double)bytes);
+  }
+  {
+    const int chunk = 2300;
+    const unsigned g = (unsigned)((n + chunk - 1) / chunk);
+    run("tile pol plain", [&] { w_tile_pol<0><<<g, 192>>>(a, n, chunk); }, (double)bytes);
+    run("tile pol nt", [&] { w_tile_pol<1><<<g, 192>>>(a, n, chunk); }, (double)bytes);
+    run("tile pol sc1 nt", [&] { w_tile_pol<2><<<g, 192>>>(a, n, chunk); }, (double)bytes);
+    run("tile pol sc0 sc1 nt", [&] { w_tile_pol<3><<<g, 192>>>(a, n, chunk); }, (double)bytes);
+    run("tile pol sc0 sc1", [&] { w_tile_pol<4><<<g, 192>>>(a, n, chunk); }, (double)bytes);
+    run("tile pol sc1", [&] { w_tile_pol<5><<<g, 192>>>(a, n, chunk); }, (double)bytes);
   }
   run("read grid 4096", [&] { r_sum<<<4096, 256>>>(a, n, o); }, (double)bytes);
   run("copy_nt grid 4096", [&] { copy_nt<<<4096, 256>>>(a, b, n); }, 2.0 * bytes);

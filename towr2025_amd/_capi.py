@@ -137,7 +137,7 @@ SYMBOLS = {
 }
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libtowr_gpu.so")
+LIB_PATH = os.environ.get("TOWR_GPU_LIB") or os.path.join(_HERE, "lib", "libtowr_gpu.so")   # override: A/B builds
 _lib = None
 
 
