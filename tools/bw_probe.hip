@@ -75,6 +75,51 @@ __global__ void copy_nt(const dbl2_t* a, dbl2_t* b, size_t n) {
     __builtin_nontemporal_store(a[i], b + i);
 }
 
+// wave-contiguous stores, U independent 1-KiB stores per wave in flight per iteration, grid-stride
+template <int U>
+__global__ void w_nt_wave_unroll(dbl2_t* p, size_t n) {
+  const size_t nthr = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i + (U - 1) * nthr < n; i += U * nthr) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) { dbl2_t v; v.x = (double)u; v.y = 1.0; __builtin_nontemporal_store(v, p + i + u * nthr); }
+  }
+}
+// block-contiguous chunk, U stores in flight per thread (stride blockDim)
+template <int U>
+__global__ void w_nt_chunk_u(dbl2_t* p, size_t n, int chunk) {
+  const size_t base = (size_t)blockIdx.x * chunk;
+  for (int i = threadIdx.x; i < chunk; i += U * blockDim.x) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = i + u * blockDim.x;
+      if (k < chunk && base + k < n) { dbl2_t v; v.x = (double)k; v.y = 1.0; __builtin_nontemporal_store(v, p + base + k); }
+    }
+  }
+}
+
+// tile pattern with the engine's XCD-chunked work order: tile w = (blockIdx % 8) * per + blockIdx / 8
+__global__ void w_nt_chunk_xcd(dbl2_t* p, size_t n, int chunk) {
+  const int per = (gridDim.x + 7) / 8;
+  const size_t w = (size_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+  const size_t base = w * chunk;
+  for (int i = threadIdx.x; i < chunk; i += blockDim.x) {
+    if (base + i >= n) return;
+    dbl2_t v; v.x = (double)i; v.y = 1.0;
+    __builtin_nontemporal_store(v, p + base + i);
+  }
+}
+// persistent tiles: gridDim blocks loop over tiles blockIdx, blockIdx + gridDim, ...
+__global__ void w_nt_chunk_persist(dbl2_t* p, size_t n, int chunk, int ntiles) {
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const size_t base = (size_t)t * chunk;
+    for (int i = threadIdx.x; i < chunk; i += blockDim.x) {
+      if (base + i >= n) break;
+      dbl2_t v; v.x = (double)i; v.y = 1.0;
+      __builtin_nontemporal_store(v, p + base + i);
+    }
+  }
+}
+
 int main() {
   const size_t bytes = 460ull << 20, n = bytes / 16;
   dbl2_t *a, *b; double* o;
@@ -122,8 +167,44 @@ int main() {
     run("tile pol sc0 sc1", [&] { w_tile_pol<4><<<g, 192>>>(a, n, chunk); }, (double)bytes);
     run("tile pol sc1", [&] { w_tile_pol<5><<<g, 192>>>(a, n, chunk); }, (double)bytes);
   }
+  for (int blocks : {1024, 2048, 4096}) {
+    char nm[64];
+    std::snprintf(nm, sizeof nm, "wave_unroll4 grid %d x256", blocks);
+    run(nm, [&] { w_nt_wave_unroll<4><<<blocks, 256>>>(a, n); }, (double)bytes);
+    std::snprintf(nm, sizeof nm, "wave_unroll4 grid %d x1024", blocks / 4);
+    run(nm, [&] { w_nt_wave_unroll<4><<<blocks / 4, 1024>>>(a, n); }, (double)bytes);
+  }
+  for (int chunk : {2300, 4600, 9200}) {
+    char nm[64];
+    const unsigned g = (unsigned)((n + chunk - 1) / chunk);
+    std::snprintf(nm, sizeof nm, "chunk_u4 %d B x192", chunk * 16);
+    run(nm, [&] { w_nt_chunk_u<4><<<g, 192>>>(a, n, chunk); }, (double)bytes);
+    std::snprintf(nm, sizeof nm, "chunk_u4 %d B x256", chunk * 16);
+    run(nm, [&] { w_nt_chunk_u<4><<<g, 256>>>(a, n, chunk); }, (double)bytes);
+    std::snprintf(nm, sizeof nm, "chunk_u1 %d B x512", chunk * 16);
+    run(nm, [&] { w_nt_chunk_u<1><<<g, 512>>>(a, n, chunk); }, (double)bytes);
+  }
+  for (int blocks : {256, 512}) {
+    char nm[64];
+    std::snprintf(nm, sizeof nm, "write_nt grid %d", blocks);
+    run(nm, [&] { w_nt<<<blocks, 256>>>(a, n); }, (double)bytes);
+  }
+  {
+    const int chunk = 2300;
+    const unsigned g = (unsigned)((n + chunk - 1) / chunk);
+    run("tiles 36800 B xcd order", [&] { w_nt_chunk_xcd<<<g, 192>>>(a, n, chunk); }, (double)bytes);
+    for (int pb : {256, 512, 768, 1024}) {
+      char nm[64];
+      std::snprintf(nm, sizeof nm, "tiles persistent %d x192", pb);
+      run(nm, [&] { w_nt_chunk_persist<<<pb, 192>>>(a, n, chunk, (int)g); }, (double)bytes);
+      std::snprintf(nm, sizeof nm, "tiles persistent %d x256", pb);
+      run(nm, [&] { w_nt_chunk_persist<<<pb, 256>>>(a, n, chunk, (int)g); }, (double)bytes);
+    }
+  }
   run("read grid 4096", [&] { r_sum<<<4096, 256>>>(a, n, o); }, (double)bytes);
   run("copy_nt grid 4096", [&] { copy_nt<<<4096, 256>>>(a, b, n); }, 2.0 * bytes);
   run("hipMemsetAsync", [&] { hipMemsetAsync(a, 0, bytes); }, (double)bytes);
+  run("hipMemsetD32Async", [&] { hipMemsetD32Async((hipDeviceptr_t)a, 0x3f800000, bytes / 4); }, (double)bytes);
+  run("hipMemcpyAsync DtoD", [&] { hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice); }, 2.0 * bytes);
   return 0;
 }

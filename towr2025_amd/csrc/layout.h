@@ -67,7 +67,8 @@ struct Layout {
   int64_t type_bytes[IT_COUNT] = {};
   // small kinds (is_misc_kind) run in one launch: kMiscWaves tiles per block, one per wave
   std::vector<int32_t> misc_tiles;   // groups of kMiscWaves tile indices (-1 = empty wave)
-  int32_t misc_dummy_off = 0, misc_rows_off = 0, misc_stride = 0;   // per-wave LDS layout (doubles)
+  std::vector<int32_t> misc_lds;     // per (group, wave): LDS offset of the wave's tile, its g-row offset (doubles)
+  int32_t misc_region = 0;           // LDS of the largest group (doubles)
   int64_t misc_bytes = 0;
   // cost terms (eval_f / eval_grad_f): work items sorted by CostType, one block per problem
   std::vector<CostItem> cost_items;

@@ -778,28 +778,41 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
       }
     }
     L.type_tile0[IT_COUNT] = (int32_t)L.tiles.size();
-    // the small kinds (one-wave tiles) share one launch: up to 4 tiles per block, one per wave, with
-    // a common per-wave LDS layout [values | 64 dummy slots | g rows]
+    // the small kinds (one-wave tiles) share one launch: up to 4 tiles per block, one per wave.
+    // Each kind has its own per-wave LDS layout [values | 64 dummy slots | g rows], sized for its
+    // largest tile; a block's waves are packed back to back (misc_lds), so the block's LDS is the
+    // sum of its tiles' kinds, not 4x the largest kind.
     {
       std::vector<int32_t> mt;
-      int mv = 0, mr = 0;
+      int stride[IT_COUNT] = {}, rows_off[IT_COUNT] = {};
       for (int t = 0; t < IT_COUNT; ++t) {
         if (!is_misc_kind(t)) continue;
         if (type_spec(t, E).block != 64) { err = "internal: small kinds must use one-wave tiles"; return TOWR_ERR_INVALID; }
+        int mv = 0, mr = 0;
         for (int ti = L.type_tile0[t]; ti < L.type_tile0[t + 1]; ++ti) {
           mt.push_back(ti);
           mv = std::max(mv, L.tiles[ti].v1 - L.tiles[ti].v0);
           mr = std::max(mr, L.tiles[ti].r1 - L.tiles[ti].r0);
         }
+        L.type_lds_dummy_off[t] = (mv + 1) & ~1;
+        rows_off[t] = L.type_lds_dummy_off[t] + 64;
+        stride[t] = rows_off[t] + ((mr + 1) & ~1);
       }
-      L.misc_dummy_off = (mv + 1) & ~1;
-      L.misc_rows_off = L.misc_dummy_off + 64;
-      L.misc_stride = L.misc_rows_off + ((mr + 1) & ~1);
-      for (int t = 0; t < IT_COUNT; ++t)
-        if (is_misc_kind(t)) L.type_lds_dummy_off[t] = L.misc_dummy_off;
       L.misc_tiles.clear();
-      for (size_t q = 0; q < mt.size(); q += kMiscWaves)
-        for (int w = 0; w < kMiscWaves; ++w) L.misc_tiles.push_back(q + w < mt.size() ? mt[q + w] : -1);
+      L.misc_lds.clear();
+      L.misc_region = 0;
+      for (size_t q = 0; q < mt.size(); q += kMiscWaves) {
+        int32_t off = 0;
+        for (int w = 0; w < kMiscWaves; ++w) {
+          const int32_t ti = q + w < mt.size() ? mt[q + w] : -1;
+          L.misc_tiles.push_back(ti);
+          const int t = ti >= 0 ? L.tiles[ti].type : -1;
+          L.misc_lds.push_back(off);
+          L.misc_lds.push_back(ti >= 0 ? rows_off[t] : 0);
+          if (ti >= 0) off += stride[t];
+        }
+        L.misc_region = std::max(L.misc_region, off);
+      }
     }
     // slot table per tile: lane l's candidates 8g..8g+7 in group g at base + g * block + l, as
     // tile-relative uint16 positions; four spare groups per lane absorb the kernel's prefetch

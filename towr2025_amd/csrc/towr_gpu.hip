@@ -28,6 +28,10 @@ using namespace tg;
 
 namespace {
 
+// one unit of the fused launch: a tile of a tile class, or a small-kind group (LC_MISC)
+struct UnitDesc { int32_t lc, tile, lds_x_off, lds_rows_off; };
+constexpr int kFusedBlock = 256;
+
 struct KParams {
   const double* X; int64_t ldx;
   double* G; int64_t ldg;
@@ -53,8 +57,10 @@ struct KParams {
   int32_t n, n_pad, n_nodecol;
   int32_t want_g, want_jac, fdisc_motion;
   const int32_t* misc_tiles;      // merged small-kind launch: kMiscWaves tile ids per group
-  int32_t misc_stride, misc_rows_off;
+  const int32_t* misc_lds;        // per (group, wave): LDS offset, g-row offset
   RobotC rb;
+  const UnitDesc* units;          // fused launch: a problem's units (UnitDesc), n_units per problem
+  int32_t n_units;
   const CostItem* citems;         // cost launch: work items, objective and gradient outputs
   int32_t n_citems, lds_red_off;
   double* F;
@@ -192,16 +198,12 @@ __device__ unsigned long long* g_tbuf;
 #define TSTAMP(slot, v) do { } while (0)
 #endif
 
-template <int TYPE, int BLOCK, bool GAIT, bool ROTVEC>
-__global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_kernel(KParams P) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int total = P.B * P.ntiles;
-  const int per = (total + 7) / 8;
-  // XCD-aware mapping: work ids w and w+1 (tiles of one problem) share blockIdx % 8
-  const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
-  if (w >= total) return;
-  const int b = w / P.ntiles;
-  const TileDesc T = P.tiles[P.tile0 + w % P.ntiles];
+// Body of one tile block. TBLOCK = the tile's lane count (its slot-table stride), KBLOCK = the
+// launch's block size (>= TBLOCK): in the fused launch a 192-lane tile runs in a 256-thread block,
+// whose extra wave only helps stage x and copy out.
+template <int TYPE, int TBLOCK, int KBLOCK, bool GAIT, bool ROTVEC>
+__device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b, int tile, int lds_x_off, int lds_rows_off) {
+  const TileDesc T = P.tiles[tile];
   double* Vb = P.V + (int64_t)b * P.ldv;
   double* Gb = P.G + (int64_t)b * P.ldg;
   const double* xg = P.X + (int64_t)b * P.ldx;
@@ -209,12 +211,17 @@ __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_ker
 #ifdef TOWR_PHASE_TIMING
   if (threadIdx.x < 64) { TSTAMP(0, TS_REAL()); TSTAMP(1, TS_MEM()); }
 #endif
-  const ItemDesc it = P.items[T.i0 + threadIdx.x];
-  TileEmit<BLOCK, slot_depth(TYPE)> em(P.slots + it.slot, smem, smem + P.lds_rows_off - T.r0);
+  ItemDesc it;
+  if (KBLOCK == TBLOCK || (int)threadIdx.x < TBLOCK) {
+    it = P.items[T.i0 + threadIdx.x];
+  } else {
+    it = ItemDesc{}; it.type = IT_NONE; it.slot = 0;
+  }
+  TileEmit<TBLOCK, slot_depth(TYPE)> em(P.slots + it.slot, smem, smem + lds_rows_off - T.r0);
   // x (+ a zero at index n for constant node values) and, for node-value kinds, the node table
-  double* xs = smem + P.lds_x_off;
-  int32_t* ns = reinterpret_cast<int32_t*>(smem + P.lds_x_off + P.n_pad);
-  stage_x<BLOCK, stages_nodes(TYPE, GAIT)>(P, xg, xs, ns);
+  double* xs = smem + lds_x_off;
+  int32_t* ns = reinterpret_cast<int32_t*>(smem + lds_x_off + P.n_pad);
+  stage_x<KBLOCK, stages_nodes(TYPE, GAIT)>(P, xg, xs, ns);
   __syncthreads();
 #ifdef TOWR_PHASE_TIMING
   if (threadIdx.x < 64) TSTAMP(2, TS_MEM());
@@ -253,28 +260,33 @@ __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_ker
 #ifdef TOWR_PHASE_TIMING
   if (threadIdx.x < 64) TSTAMP(7, TS_MEM());
 #endif
-  if (P.want_jac) copy_out(smem, Vb + T.v0, T.v1 - T.v0, threadIdx.x, BLOCK);
+  if (P.want_jac) copy_out(smem, Vb + T.v0, T.v1 - T.v0, threadIdx.x, KBLOCK);
   if (P.want_g)
-    for (int i = threadIdx.x; i < T.r1 - T.r0; i += BLOCK) __builtin_nontemporal_store(smem[P.lds_rows_off + i], Gb + T.r0 + i);
+    for (int i = threadIdx.x; i < T.r1 - T.r0; i += KBLOCK) __builtin_nontemporal_store(smem[lds_rows_off + i], Gb + T.r0 + i);
 #ifdef TOWR_PHASE_TIMING
   if (threadIdx.x < 64) { TSTAMP(8, TS_MEM()); TSTAMP(9, TS_REAL()); }
 #endif
+}
+
+template <int TYPE, int BLOCK, bool GAIT, bool ROTVEC>
+__global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_kernel(KParams P) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int total = P.B * P.ntiles;
+  const int per = (total + 7) / 8;
+  // XCD-aware mapping: work ids w and w+1 (tiles of one problem) share blockIdx % 8
+  const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+  if (w >= total) return;
+  tile_body<TYPE, BLOCK, BLOCK, GAIT, ROTVEC>(P, smem, w / P.ntiles, P.tile0 + w % P.ntiles, P.lds_x_off, P.lds_rows_off);
 }
 
 // The small kinds (node-value constraints, SplineAcc, BaseMotion, TotalDuration: a few kB of output
 // per problem each) in one launch: a block = kMiscWaves one-wave tiles of one problem, sharing the
 // staged x and node table; each wave evaluates and writes out its own tile.
 template <bool GAIT>
-__global__ void __launch_bounds__(64 * kMiscWaves, 1) towr_misc_kernel(KParams P) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
+__device__ __forceinline__ void misc_body(const KParams& P, double* smem, int b, int group, int lds_x_off) {
   constexpr int BLOCK = 64 * kMiscWaves;
-  const int total = P.B * P.ntiles;   // ntiles = groups per problem
-  const int per = (total + 7) / 8;
-  const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
-  if (w >= total) return;
-  const int b = w / P.ntiles;
   const int wave = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
-  const int ti = P.misc_tiles[(w % P.ntiles) * kMiscWaves + wave];
+  const int ti = P.misc_tiles[group * kMiscWaves + wave];
   TileDesc T{};
   ItemDesc it{};
   it.type = IT_NONE;
@@ -283,10 +295,12 @@ __global__ void __launch_bounds__(64 * kMiscWaves, 1) towr_misc_kernel(KParams P
     T = P.tiles[ti];
     it = P.items[T.i0 + lane];
   }
-  double* wl = smem + wave * P.misc_stride;
-  TileEmit<64, 3> em(P.slots + it.slot, wl, wl + P.misc_rows_off - T.r0);
-  double* xs = smem + P.lds_x_off;
-  int32_t* ns = reinterpret_cast<int32_t*>(smem + P.lds_x_off + P.n_pad);
+  const int32_t wl_off = P.misc_lds[2 * (group * kMiscWaves + wave)];
+  const int32_t rows_off = P.misc_lds[2 * (group * kMiscWaves + wave) + 1];
+  double* wl = smem + wl_off;
+  TileEmit<64, 3> em(P.slots + it.slot, wl, wl + rows_off - T.r0);
+  double* xs = smem + lds_x_off;
+  int32_t* ns = reinterpret_cast<int32_t*>(smem + lds_x_off + P.n_pad);
 #ifdef TOWR_PHASE_TIMING
   if (threadIdx.x < 64) { TSTAMP(0, TS_REAL()); TSTAMP(1, TS_MEM()); }
 #endif
@@ -330,10 +344,51 @@ __global__ void __launch_bounds__(64 * kMiscWaves, 1) towr_misc_kernel(KParams P
   double* Gb = P.G + (int64_t)b * P.ldg;
   if (P.want_jac) copy_out(wl, Vb + T.v0, T.v1 - T.v0, lane, 64);
   if (P.want_g)
-    for (int i = lane; i < T.r1 - T.r0; i += 64) __builtin_nontemporal_store(wl[P.misc_rows_off + i], Gb + T.r0 + i);
+    for (int i = lane; i < T.r1 - T.r0; i += 64) __builtin_nontemporal_store(wl[rows_off + i], Gb + T.r0 + i);
 #ifdef TOWR_PHASE_TIMING
   if (threadIdx.x < 64) { TSTAMP(8, TS_MEM()); TSTAMP(9, TS_REAL()); }
 #endif
+}
+
+// The small kinds (node-value constraints, SplineAcc, BaseMotion, TotalDuration: a few kB of output
+// per problem each) in one launch: a block = kMiscWaves one-wave tiles of one problem, sharing the
+// staged x and node table; each wave evaluates and writes out its own tile.
+template <bool GAIT>
+__global__ void __launch_bounds__(64 * kMiscWaves, 1) towr_misc_kernel(KParams P) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int total = P.B * P.ntiles;   // ntiles = groups per problem
+  const int per = (total + 7) / 8;
+  const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+  if (w >= total) return;
+  misc_body<GAIT>(P, smem, w / P.ntiles, w % P.ntiles, P.lds_x_off);
+}
+
+// The whole step in ONE launch: a problem's units (its tiles of every class and its small-kind
+// groups) are consecutive work ids, interleaved so that latency-bound units (Dynamic, small kinds)
+// share the CUs with write-bound ones (RangeOfMotion, ForceConstraintDiscretized) and no launch
+// boundary drains the machine between classes. Every unit runs the same code as its per-class
+// kernel (tile_body / misc_body); 192-lane tiles leave the block's fourth wave to staging and
+// copy-out. The unit table is uniform per block (scalar loads).
+template <bool GAIT, bool ROTVEC>
+__global__ void __launch_bounds__(kFusedBlock, 2) towr_step_kernel(KParams P) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int total = P.B * P.n_units;
+  const int per = (total + 7) / 8;
+  const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+  if (w >= total) return;
+  const int b = w / P.n_units;
+  const UnitDesc u = P.units[w % P.n_units];
+  switch (u.lc) {
+    case LC_DYN: tile_body<IT_DYN, 256, kFusedBlock, GAIT, ROTVEC>(P, smem, b, u.tile, u.lds_x_off, u.lds_rows_off); break;
+    case LC_ROM: tile_body<IT_ROM, 192, kFusedBlock, GAIT, ROTVEC>(P, smem, b, u.tile, u.lds_x_off, u.lds_rows_off); break;
+    case LC_FDISC: tile_body<IT_FDISC, 192, kFusedBlock, GAIT, false>(P, smem, b, u.tile, u.lds_x_off, u.lds_rows_off); break;
+    case LC_TQDISC: tile_body<IT_TQDISC, 192, kFusedBlock, GAIT, false>(P, smem, b, u.tile, u.lds_x_off, u.lds_rows_off); break;
+    default: misc_body<GAIT>(P, smem, b, u.tile, u.lds_x_off); break;
+  }
+}
+const void* step_kernel_for(bool gait, bool rotvec) {
+  if (gait) return rotvec ? reinterpret_cast<const void*>(&towr_step_kernel<true, true>) : reinterpret_cast<const void*>(&towr_step_kernel<true, false>);
+  return rotvec ? reinterpret_cast<const void*>(&towr_step_kernel<false, true>) : reinterpret_cast<const void*>(&towr_step_kernel<false, false>);
 }
 
 // Objective and gradient (IpoptAdapter::eval_f / eval_grad_f): one block per problem. The block
@@ -481,8 +536,13 @@ struct towr_gpu_handle_s {
   PhaseCol* d_pcols = nullptr;
   SchedInfo* d_sched = nullptr;
   int32_t* d_misc = nullptr;
+  int32_t* d_misc_lds = nullptr;
   EELinDef* d_eelin = nullptr;
   CostItem* d_citems = nullptr;
+  // fused single-launch step (TOWR_GPU_FUSED, see towr_step_kernel): the unit table of one problem
+  UnitDesc* d_units = nullptr;
+  int32_t n_units = 0;
+  bool fused = false;
   // fork-join of the per-kind launches (TOWR_GPU_STREAMS = total streams incl. the caller's, 1..4)
   static constexpr int kMaxSide = 3;
   int n_side = 0;
@@ -538,7 +598,7 @@ int bind(towr_gpu_handle h) {
 }
 
 // LDS of a launch class: [tile region(s) | x + zero slot | node table]
-size_t lds_region(const Layout& L, int lc) { return lc == LC_MISC ? (size_t)kMiscWaves * L.misc_stride : (size_t)L.type_lds[class_type(lc)]; }
+size_t lds_region(const Layout& L, int lc) { return lc == LC_MISC ? (size_t)((L.misc_region + 1) & ~1) : (size_t)L.type_lds[class_type(lc)]; }
 size_t lds_bytes(const Layout& L, int lc) {
   size_t d = lds_region(L, lc);
   d += (size_t)((L.n + 2) & ~1);                                                                  // x + zero slot
@@ -552,10 +612,75 @@ int class_units(const Layout& L, int lc) {   // tiles (or misc groups) per probl
 }
 int64_t class_bytes(const Layout& L, int lc) { return lc == LC_MISC ? L.misc_bytes : L.type_bytes[class_type(lc)]; }
 
+// LDS of the fused launch: the largest class's
+size_t fused_lds_bytes(const Layout& L) {
+  size_t m = 0;
+  for (int lc = 0; lc < LC_COUNT; ++lc)
+    if (class_units(L, lc) > 0) m = std::max(m, lds_bytes(L, lc));
+  return m;
+}
+
+// the fused launch's unit table: one round-robin pass over the classes at a time (heaviest writer
+// first), so consecutive blocks of a problem alternate latency-bound and write-bound units
+std::vector<UnitDesc> fused_units(const Layout& L) {
+  static const int order[] = {LC_FDISC, LC_DYN, LC_ROM, LC_TQDISC, LC_MISC};
+  std::vector<UnitDesc> u;
+  int left[LC_COUNT];
+  for (int lc = 0; lc < LC_COUNT; ++lc) left[lc] = class_units(L, lc);
+  for (bool any = true; any;) {
+    any = false;
+    for (int lc : order) {
+      if (left[lc] == 0) continue;
+      const int k = class_units(L, lc) - left[lc]--;
+      UnitDesc d{};
+      d.lc = lc;
+      d.tile = lc == LC_MISC ? k : L.type_tile0[class_type(lc)] + k;
+      d.lds_x_off = (int32_t)lds_region(L, lc);
+      d.lds_rows_off = lc == LC_MISC ? 0 : L.type_lds_rows_off[class_type(lc)];   // small kinds: misc_lds
+      u.push_back(d);
+      any = true;
+    }
+  }
+  return u;
+}
+
+void fill_common(towr_gpu_handle h, KParams& P, int B, const double* X, int64_t ldx, double* G, int64_t ldg, double* V,
+                 int64_t ldv, int want_g, int want_jac, const towr_terrain_t* terrains, int per_problem) {
+  const Layout& L = h->L;
+  P.X = X; P.ldx = ldx; P.G = G; P.ldg = ldg; P.V = V; P.ldv = ldv;
+  P.items = h->d_items; P.slots = h->d_slots; P.tiles = h->d_tiles;
+  P.nodecol = h->d_nodecol; P.spl = h->d_spl; P.dur = h->d_dur;
+  P.sg = h->sg; P.n_spl = (int32_t)L.spl.size();
+  P.pinfo = h->d_pinfo; P.pcols = h->d_pcols; P.sched = h->d_sched; P.eelin = h->d_eelin;
+  P.terrains = terrains; P.terrain_per_problem = per_problem;
+  P.B = B;
+  P.n = L.n; P.n_pad = (L.n + 2) & ~1; P.n_nodecol = (int32_t)L.nodecol.size();
+  P.want_g = want_g; P.want_jac = want_jac; P.fdisc_motion = L.fdisc_motion;
+  P.rb = L.rb;
+  P.misc_tiles = h->d_misc; P.misc_lds = h->d_misc_lds;
+  P.lds_scr_off = L.dyn_scr_off;
+}
+
+int launch_fused(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, int64_t ldg, double* V, int64_t ldv,
+                 int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem) {
+  const Layout& L = h->L;
+  KParams P{};
+  fill_common(h, P, B, X, ldx, G, ldg, V, ldv, want_g, want_jac, terrains, per_problem);
+  P.units = h->d_units; P.n_units = h->n_units;
+  const int64_t total = (int64_t)B * h->n_units;
+  const int64_t grid = ((total + 7) / 8) * 8;
+  if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
+  void* args[] = {&P};
+  HIPCHK(h, hipLaunchKernel(step_kernel_for(L.gait, L.rotvec), dim3((unsigned)grid), dim3(kFusedBlock), args,
+                            fused_lds_bytes(L), s));
+  return TOWR_OK;
+}
+
 int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, int64_t ldg, double* V, int64_t ldv,
            int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem, int only_class = -1) {
   if (B <= 0) return TOWR_OK;
   const Layout& L = h->L;
+  if (h->fused && only_class < 0) return launch_fused(h, B, X, ldx, G, ldg, V, ldv, want_g, want_jac, s, terrains, per_problem);
   // The launch classes are independent (disjoint rows and CSR ranges): optionally fork them onto the
   // handle's side streams (TOWR_GPU_STREAMS) and join back into the caller's stream. Heaviest first.
   int order[LC_COUNT], nk = 0;
@@ -581,7 +706,7 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
     P.B = B; P.ntiles = nt;
     if (lc == LC_MISC) {
       P.tile0 = 0;
-      P.misc_tiles = h->d_misc; P.misc_stride = L.misc_stride; P.misc_rows_off = L.misc_rows_off;
+      P.misc_tiles = h->d_misc; P.misc_lds = h->d_misc_lds;
     } else {
       P.tile0 = L.type_tile0[class_type(lc)];
       P.lds_rows_off = L.type_lds_rows_off[class_type(lc)];
@@ -777,7 +902,7 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
       (r = upload(h, &h->d_tiles, L.tiles)) || (r = upload(h, &h->d_nodecol, nodecol16)) ||
       (r = upload(h, &h->d_spl, L.spl)) || (r = upload(h, &h->d_dur, L.dur)) || (r = upload(h, &h->d_terrain, ter)) ||
       (r = upload(h, &h->d_pinfo, L.pinfo)) || (r = upload(h, &h->d_pcols, L.pcols)) || (r = upload(h, &h->d_sched, L.sched)) ||
-      (r = upload(h, &h->d_misc, L.misc_tiles)) || (r = upload(h, &h->d_eelin, L.eelin)) ||
+      (r = upload(h, &h->d_misc, L.misc_tiles)) || (r = upload(h, &h->d_misc_lds, L.misc_lds)) || (r = upload(h, &h->d_eelin, L.eelin)) ||
       (r = upload(h, &h->d_citems, L.cost_items)))
     return bail(r);
   {   // trajectory export: phase durations of the description (fixed gait), counts, contact at start
@@ -831,6 +956,25 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
         h->err = "side stream creation failed"; return bail(TOWR_ERR_HIP);
       }
   }
+  {   // fused single-launch step: TOWR_GPU_FUSED=1 (default off). Measured on MI355X (ANYmal,
+      // B = 4096): 0.317 ms per step fused vs 0.287 ms with the per-class launches — the fused
+      // kernel carries Dynamic's 242 VGPRs into every unit (2 waves per SIMD), so RangeOfMotion and
+      // ForceConstraintDiscretized lose a third of their resident waves.
+    const char* fz = std::getenv("TOWR_GPU_FUSED");
+    h->fused = fz && std::atoi(fz) != 0;
+    const std::vector<UnitDesc> units = fused_units(L);
+    for (const UnitDesc& u : units)
+      if (u.lc != LC_MISC && L.type_block[class_type(u.lc)] != (u.lc == LC_DYN ? 256 : 192)) {
+        h->err = "internal: fused launch expects 256-lane Dynamic and 192-lane tiles"; return bail(TOWR_ERR_INVALID);
+      }
+    h->n_units = (int32_t)units.size();
+    if ((r = upload(h, &h->d_units, units))) return bail(r);
+    const size_t lds = fused_lds_bytes(L);
+    if (lds > 160 * 1024) { h->err = "tile too large for LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
+    if (lds > 64 * 1024 && hipFuncSetAttribute(step_kernel_for(L.gait, L.rotvec), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+      h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
+    }
+  }
   for (int lc = 0; lc < LC_COUNT; ++lc) {
     if (class_units(L, lc) == 0) continue;
     const size_t lds = lds_bytes(L, lc);
@@ -855,7 +999,7 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
 int towr_gpu_destroy(towr_gpu_handle h) {
   if (!h) return TOWR_OK;
   void* dev[] = {h->d_items, h->d_slots, h->d_tiles, h->d_nodecol, h->d_spl, h->d_dur, h->d_segs, h->d_terrain,
-                 h->d_pinfo, h->d_pcols, h->d_sched, h->d_misc, h->d_eelin, h->d_citems,
+                 h->d_pinfo, h->d_pcols, h->d_sched, h->d_misc, h->d_misc_lds, h->d_eelin, h->d_citems, h->d_units,
                  h->d_bterrain, h->d_x, h->d_g, h->d_v, h->d_f, h->d_grad,
                  h->d_traj_pd, h->d_traj_n, h->d_traj_c0, h->d_traj_t};
   if (h->device >= 0) for (void* p : dev) if (p) (void)hipFree(p);
