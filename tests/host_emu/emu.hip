@@ -65,7 +65,7 @@ extern "C" int emu_cost(const towr_problem_desc_t* d, const double* x, double* f
   c.x = x; c.nodecol = L.nodecol.data(); c.spl = L.spl.data(); c.dur = L.dur.data();
   c.ter = &L.terrain; c.rb = L.rb; c.fdisc_motion = L.fdisc_motion;
   c.gait = L.gait; c.pinfo = L.pinfo.data(); c.pcols = L.pcols.data(); c.sched = L.sched.data();
-  c.eelin = L.eelin.data(); c.rotvec = L.rotvec;
+  c.eelin = L.eelin.data(); c.rotvec = L.rotvec; c.cq = L.cost_q.data();
   GradEmit em{grad};
   for (const CostItem& it : L.cost_items) {
     c.seg = it.seg >= 0 ? L.segs.data() + (size_t)it.seg * L.spl.size() : nullptr;

@@ -168,6 +168,7 @@ struct Ctx {
   const PhaseCol* pcols;
   const SchedInfo* sched;       // per endeffector
   const EELinDef* eelin;        // EELinearConstraint definitions
+  const double* cq;             // cost kernel: CT_ENERGYQ Gram matrices (16 doubles each)
 };
 
 // ----------------------------------------------------------------------------------------------
@@ -1482,12 +1483,15 @@ TG_HD void eval_tdur(const Ctx& c, const ItemDesc& it, Emit& em) {
 // the same emitter interface as the constraint items, so the spline chain rules (emit_dim, the
 // PhaseSpline full pattern, sched_jac) are shared with the constraints.
 // ----------------------------------------------------------------------------------------------
-enum CostType { CT_NODE = 0, CT_ENERGY = 1, CT_ANGMOM = 2, CT_EEBP = 3, CT_COUNT = 4 };
+// CT_ENERGYQ: EnergyCost of one polynomial of a force / torque spline with fixed durations (see
+// cost_energy_q); CT_ENERGY: one (sample, ee) of EnergyCost under phase-duration optimisation
+enum CostType { CT_NODE = 0, CT_ENERGY = 1, CT_ANGMOM = 2, CT_EEBP = 3, CT_ENERGYQ = 4, CT_COUNT = 5 };
 
 struct CostItem {
   int32_t type, ee, seg, s;        // seg: segment-table row of the sample time; s: spline (CT_NODE)
-  int32_t deriv, dim;              // CT_NODE: node value penalised
-  int32_t contact0, reserved;      // CT_EEBP: ee in contact at start (swing test under gait optimisation)
+  int32_t deriv, dim;              // CT_NODE: node value penalised; CT_ENERGYQ: deriv = polynomial of spline s
+  int32_t a0, a1;                  // CT_NODE: nodes [a0, a1); CT_EEBP: a0 = ee in contact at start (swing
+                                   // test under gait optimisation); CT_ENERGYQ: a0 = Gram matrix index (Ctx::cq)
   double t, w, wdt, tw;            // sample time, weight, weight * dt, EnergyCost torque weight
   double p[3], pad;                // CT_EEBP: reference ee position in base frame
 };
@@ -1496,8 +1500,7 @@ struct CostItem {
 // variable i sets of 2 w value (a stance position variable sets two nodes: counted twice)
 template <class Emit>
 TG_HD void cost_node(const Ctx& c, const CostItem& it, Emit& em) {
-  const int nn = c.spl[it.s].n_polys + 1;
-  for (int id = 0; id < nn; ++id) {
+  for (int id = it.a0; id < it.a1; ++id) {   // one chunk of the spline's nodes (layout.hip build_costs)
     const int col = node_col(c, it.s, id, it.deriv, it.dim);
     const double v = xval(c, col);
     em.f += it.w * (v * v);
@@ -1530,6 +1533,26 @@ TG_HD void cost_energy(const Ctx& c, const CostItem& it, Emit& em) {
       if (it.tw != 0.0) v += mt[0] * sched_val(Jt, 0, col) + mt[1] * sched_val(Jt, 1, col) + mt[2] * sched_val(Jt, 2, col);
       em(0, Jf.col0 + col, v, true);
     }
+  }
+}
+
+// EnergyCost (energy_cost.cc:57-152) over one polynomial of a force or torque spline whose durations
+// are fixed. The polynomial's samples contribute sum_t w dt |F(t)|^2 with F_e(t) = H(t) . u_e (the
+// Hermite position basis times the polynomial's four node values of dim e), i.e. sum_e u_e^T Q u_e
+// with the batch-invariant Gram matrix Q = sum_t w dt H(t) H(t)^T (times the torque weight for a
+// torque spline), built once on the host from the same sample times and basis (layout.hip
+// build_costs). d/du_e = 2 Q u_e: one gradient entry per node value and polynomial instead of one
+// per sample. Equal to the per-sample sums of the reference up to rounding (summation order).
+template <class Emit>
+TG_HD void cost_energy_q(const Ctx& c, const CostItem& it, Emit& em) {
+  const double* Q = c.cq + 16 * (size_t)it.a0;
+  for (int e = 0; e < 3; ++e) {
+    int col[4];
+    double u[4], Qu[4];
+    for (int b = 0; b < 4; ++b) { col[b] = basis_col(c, it.s, it.deriv, b, e); u[b] = xval(c, col[b]); }
+    for (int b = 0; b < 4; ++b) Qu[b] = Q[4 * b + 0] * u[0] + Q[4 * b + 1] * u[1] + Q[4 * b + 2] * u[2] + Q[4 * b + 3] * u[3];
+    em.f += u[0] * Qu[0] + u[1] * Qu[1] + u[2] * Qu[2] + u[3] * Qu[3];
+    for (int b = 0; b < 4; ++b) em(0, col[b], 2.0 * Qu[b], col[b] >= 0);   // a shared stance variable sums both
   }
 }
 
@@ -1642,7 +1665,7 @@ TG_HD bool sched_is_contact(const Ctx& c, int ee, bool contact0, double t) {
 template <class Emit>
 TG_HD void cost_eebp(const Ctx& c, const CostItem& it, Emit& em) {
   const int ee = it.ee;
-  if (c.gait && sched_is_contact(c, ee, it.contact0 != 0, it.t)) return;   // fixed gait: filtered at build
+  if (c.gait && sched_is_contact(c, ee, it.a0 != 0, it.t)) return;   // fixed gait: filtered at build
   SplinePt L, A, P;
   spline_eval(c, SP_BASE_LIN, it.t, L);
   spline_eval(c, SP_BASE_ANG, it.t, A);
@@ -1687,6 +1710,7 @@ TG_HD void eval_cost_item(const Ctx& c, const CostItem& it, Emit& em) {
     case CT_ENERGY: cost_energy(c, it, em); break;
     case CT_ANGMOM: cost_angmom(c, it, em); break;
     case CT_EEBP: cost_eebp(c, it, em); break;
+    case CT_ENERGYQ: cost_energy_q(c, it, em); break;
   }
 }
 

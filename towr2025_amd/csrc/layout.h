@@ -72,6 +72,7 @@ struct Layout {
   int64_t misc_bytes = 0;
   // cost terms (eval_f / eval_grad_f): work items sorted by CostType, one block per problem
   std::vector<CostItem> cost_items;
+  std::vector<double> cost_q;        // CT_ENERGYQ Gram matrices, 16 doubles per item (CostItem::q)
   int32_t cost_type0[CT_COUNT + 1] = {};
 };
 

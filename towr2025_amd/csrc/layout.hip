@@ -4,6 +4,7 @@
 #include "layout.h"
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -300,6 +301,7 @@ int push_seg_row(Layout& L, double t) {
 }
 
 // cost work items (NlpFormulation::GetCosts, nlp_formulation.cc:604-680), grouped by type
+constexpr int kNodeChunk = 4;   // NodeCost nodes per work item
 int build_costs(const towr_problem_desc_t& d, const std::vector<double>& base_d, Layout& L, std::string& err) {
   const int E = d.robot.n_ee;
   if (d.n_costs < 0 || d.n_costs > TOWR_MAX_COSTS) { err = "n_costs out of range"; return TOWR_ERR_INVALID; }
@@ -336,14 +338,47 @@ int build_costs(const towr_problem_desc_t& d, const std::vector<double>& base_d,
         it.type = CT_NODE; it.ee = base ? 0 : c.ee;
         it.s = vk == TOWR_VAR_BASE_LIN ? 0 : vk == TOWR_VAR_BASE_ANG ? 1 : 2 + 4 * c.ee + (vk - TOWR_VAR_EE_MOTION);
         it.deriv = c.ip[1]; it.dim = c.ip[2];
-        items.push_back(it);
+        {   // the term's nodes in chunks of kNodeChunk: lanes share a long spline's node loop
+          const int nn = L.spl[it.s].n_polys + 1;
+          for (int a = 0; a < nn; a += kNodeChunk) { it.a0 = a; it.a1 = std::min(nn, a + kNodeChunk); items.push_back(it); }
+        }
         break;
       }
-      case TOWR_COST_ENERGY:   // energy_cost.cc:57-152: one item per (sample, ee)
+      case TOWR_COST_ENERGY:   // energy_cost.cc:57-152
         if (c.weight <= 0.0) break;
         it.type = CT_ENERGY; it.tw = c.p[0];
-        for (double t : sample_times(c.dt))
-          for (int ee = 0; ee < E; ++ee) { it.t = t; it.seg = seg_of(t); it.ee = ee; items.push_back(it); }
+        if (L.gait) {   // x-dependent polynomial durations: one item per (sample, ee)
+          for (double t : sample_times(c.dt))
+            for (int ee = 0; ee < E; ++ee) { it.t = t; it.seg = seg_of(t); it.ee = ee; items.push_back(it); }
+        } else {        // fixed durations: one item per (spline, polynomial) with its Gram matrix
+          // (cost_energy_q): Q(s, poly) = sum over the samples t on the polynomial of
+          // w dt H(t) H(t)^T, times tw for the torque splines, in sample order
+          const int nspl = (int)L.spl.size();
+          std::map<std::pair<int, int>, std::array<double, 16>> gram;
+          std::vector<std::pair<int, int>> order;
+          for (double t : sample_times(c.dt)) {
+            const int r = seg_of(t);
+            for (int ee = 0; ee < E; ++ee)
+              for (int k = 0; k < (it.tw != 0.0 ? 2 : 1); ++k) {
+                const int sp = k == 0 ? sp_force(ee) : sp_torque(ee);
+                const SegRec& sr = L.segs[(size_t)r * nspl + sp];
+                const double wk = k == 0 ? it.wdt : it.wdt * it.tw;
+                auto key = std::make_pair(sp, sr.poly);
+                auto f = gram.find(key);
+                if (f == gram.end()) { f = gram.emplace(key, std::array<double, 16>{}).first; order.push_back(key); }
+                for (int a = 0; a < 4; ++a)
+                  for (int b = 0; b < 4; ++b) f->second[4 * a + b] += wk * sr.H[kPos][a] * sr.H[kPos][b];
+              }
+          }
+          for (const auto& key : order) {
+            CostItem q = it;
+            q.type = CT_ENERGYQ; q.seg = -1; q.s = key.first; q.deriv = key.second; q.ee = -1;
+            q.a0 = (int32_t)(L.cost_q.size() / 16);
+            const auto& Q = gram[key];
+            L.cost_q.insert(L.cost_q.end(), Q.begin(), Q.end());
+            items.push_back(q);
+          }
+        }
         break;
       case TOWR_COST_ANG_MOMENTUM:   // angular_momentum_cost.cc:67-208
         if (c.weight <= 0.0) break;
@@ -353,13 +388,13 @@ int build_costs(const towr_problem_desc_t& d, const std::vector<double>& base_d,
       case TOWR_COST_EE_BASE_POS: {   // ee_base_pos_cost.cc:57-162: swing samples only
         if (c.ee < 0 || c.ee >= E) { err = "bad EEBasePosCost endeffector"; return TOWR_ERR_INVALID; }
         if (c.weight <= 0.0) break;
-        it.type = CT_EEBP; it.ee = c.ee; it.contact0 = d.contact_at_start[c.ee] != 0;
+        it.type = CT_EEBP; it.ee = c.ee; it.a0 = d.contact_at_start[c.ee] != 0;
         for (int k = 0; k < 3; ++k) it.p[k] = c.p[k];
         for (double t : sample_times(c.dt)) {
           if (!L.gait) {   // fixed phase durations: IsContactPhase once, here
             double tl;
             const int ph = seg_lookup(d.phase_durations[c.ee], d.n_phases[c.ee], t, &tl);
-            if ((ph % 2 == 0) == (it.contact0 != 0)) continue;
+            if ((ph % 2 == 0) == (it.a0 != 0)) continue;
           }
           it.t = t; it.seg = seg_of(t); items.push_back(it);
         }

@@ -62,6 +62,7 @@ struct KParams {
   const UnitDesc* units;          // fused launch: a problem's units (UnitDesc), n_units per problem
   int32_t n_units;
   const CostItem* citems;         // cost launch: work items, objective and gradient outputs
+  const double* cq;               // cost launch: CT_ENERGYQ Gram matrices
   int32_t n_citems, lds_red_off;
   double* F;
   double* GR; int64_t ldgr;
@@ -428,6 +429,7 @@ __global__ void __launch_bounds__(kCostBlock, 1) towr_cost_kernel(KParams P) {
   c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.sched = P.sched; c.eelin = P.eelin;
   c.rotvec = ROTVEC;
   c.dyn_scratch = nullptr;
+  c.cq = P.cq;
   for (int i = threadIdx.x; i < P.n_citems; i += kCostBlock) {
     const CostItem it = P.citems[i];
     c.seg = nullptr; c.sg = P.sg; c.row = it.seg;
@@ -539,6 +541,7 @@ struct towr_gpu_handle_s {
   int32_t* d_misc_lds = nullptr;
   EELinDef* d_eelin = nullptr;
   CostItem* d_citems = nullptr;
+  double* d_cq = nullptr;
   // fused single-launch step (TOWR_GPU_FUSED, see towr_step_kernel): the unit table of one problem
   UnitDesc* d_units = nullptr;
   int32_t n_units = 0;
@@ -748,7 +751,7 @@ int launch_cost(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* 
   P.B = B;
   P.n = L.n; P.n_pad = (L.n + 2) & ~1; P.n_nodecol = (int32_t)L.nodecol.size();
   P.fdisc_motion = L.fdisc_motion; P.rb = L.rb;
-  P.citems = h->d_citems; P.n_citems = (int32_t)L.cost_items.size();
+  P.citems = h->d_citems; P.n_citems = (int32_t)L.cost_items.size(); P.cq = h->d_cq;
   P.lds_red_off = (int32_t)cost_red_off(L);
   P.F = F; P.GR = GR; P.ldgr = ldgr;
   void* args[] = {&P};
@@ -903,7 +906,7 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
       (r = upload(h, &h->d_spl, L.spl)) || (r = upload(h, &h->d_dur, L.dur)) || (r = upload(h, &h->d_terrain, ter)) ||
       (r = upload(h, &h->d_pinfo, L.pinfo)) || (r = upload(h, &h->d_pcols, L.pcols)) || (r = upload(h, &h->d_sched, L.sched)) ||
       (r = upload(h, &h->d_misc, L.misc_tiles)) || (r = upload(h, &h->d_misc_lds, L.misc_lds)) || (r = upload(h, &h->d_eelin, L.eelin)) ||
-      (r = upload(h, &h->d_citems, L.cost_items)))
+      (r = upload(h, &h->d_citems, L.cost_items)) || (r = upload(h, &h->d_cq, L.cost_q)))
     return bail(r);
   {   // trajectory export: phase durations of the description (fixed gait), counts, contact at start
     const towr_problem_desc_t& d = L.desc;
@@ -999,7 +1002,7 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
 int towr_gpu_destroy(towr_gpu_handle h) {
   if (!h) return TOWR_OK;
   void* dev[] = {h->d_items, h->d_slots, h->d_tiles, h->d_nodecol, h->d_spl, h->d_dur, h->d_segs, h->d_terrain,
-                 h->d_pinfo, h->d_pcols, h->d_sched, h->d_misc, h->d_misc_lds, h->d_eelin, h->d_citems, h->d_units,
+                 h->d_pinfo, h->d_pcols, h->d_sched, h->d_misc, h->d_misc_lds, h->d_eelin, h->d_citems, h->d_cq, h->d_units,
                  h->d_bterrain, h->d_x, h->d_g, h->d_v, h->d_f, h->d_grad,
                  h->d_traj_pd, h->d_traj_n, h->d_traj_c0, h->d_traj_t};
   if (h->device >= 0) for (void* p : dev) if (p) (void)hipFree(p);
