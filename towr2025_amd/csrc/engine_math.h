@@ -866,6 +866,8 @@ TG_HD double dot3(const double a[3], const double b[3]) { return a[0] * b[0] + a
 // group-0 lane no longer evaluates 3 E splines in a latency-bound loop; the host sums inline in the
 // same order.
 struct DynG0 { double ab[3], La[3], Lp[3], Hp[4]; int poly; };
+constexpr int kDynG0PhaseA = 12;   // candidates of dyn_g0_a (base-linear acceleration block)
+constexpr int kDynG0Cand = 36;     // + dyn_g0_b's 24 (the base-linear block of the angular rows)
 template <class Emit>
 TG_HD void dyn_g0_a(const Ctx& c, const ItemDesc& it, Emit& em, DynG0& st) {
   const double t = it.t;
@@ -906,10 +908,13 @@ TG_HD void dyn_g0_b(const Ctx& c, const ItemDesc& it, Emit& em, const DynG0& st,
   for (int e = 0; e < 3; ++e) em.g(r0 + AX + e, st.ab[e] - ts[e]);
   const double grav[3] = {0.0, 0.0, -c.rb.m * c.rb.g};
   for (int e = 0; e < 3; ++e) em.g(r0 + LX + e, c.rb.m * st.La[e] - fs[e] - grav[e]);
+#pragma unroll
   for (int r = 0; r < 3; ++r)
+#pragma unroll
     for (int d = 1; d <= 2; ++d) {
       const int e = (r + d) % 3;
       const double sc = -cross_el(fs, r, e);  // -(sum_ee Cross(f_ee))[r][e]
+#pragma unroll
       for (int bb = 0; bb < 4; ++bb) em(r0 + AX + r, basis_col(c, SP_BASE_LIN, st.poly, bb, e), sc * st.Hp[bb], true);
     }
 }

@@ -714,6 +714,10 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
   for (size_t i = 0; i < L.items.size(); ++i) {
     L.items[i].slot = item_cand_begin[i];
     L.items[i].ncand = item_cand_begin[i + 1] - item_cand_begin[i];
+    if (L.items[i].type == IT_DYN && L.items[i].group == 0 && L.items[i].ncand != kDynG0Cand) {
+      err = "internal: Dynamic group-0 candidate count (the kernel's phase-B slot preload assumes kDynG0Cand)";
+      return TOWR_ERR_INVALID;
+    }
     // every present candidate of an item has its own CSR position (see engine_math.h)
     std::vector<int32_t> seen;
     for (int32_t q = item_cand_begin[i]; q < item_cand_begin[i + 1]; ++q) {

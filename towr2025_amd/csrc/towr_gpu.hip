@@ -102,6 +102,36 @@ struct TileEmit {
   }
   __device__ __forceinline__ void flush() {}
 };
+// Emitter for a fixed stretch of a lane's candidates J0 .. J0 + 8 NG - 1 whose slot groups are all
+// loaded at construction: Dynamic group 0 builds it before the block barrier that separates its two
+// phases, so phase B's slot loads complete during the barrier wait instead of once per 8 candidates
+// after it. Candidate indices must be compile-time constants (fully unrolled emission).
+template <int BLOCK, int J0>
+struct TileEmitPre {   // four groups: candidates J0 - J0 % 8 .. + 31
+  double* out;
+  double* gout;
+  SlotGroup q0, q1, q2, q3;   // named registers (a runtime-indexed array would go to scratch)
+  int j = J0;
+  __device__ __forceinline__ TileEmitPre(const SlotGroup* s, double* o, double* go, bool load) : out(o), gout(go) {
+    if (load) {
+      q0 = s[(J0 >> 3) * BLOCK]; q1 = s[((J0 >> 3) + 1) * BLOCK];
+      q2 = s[((J0 >> 3) + 2) * BLOCK]; q3 = s[((J0 >> 3) + 3) * BLOCK];
+    }
+  }
+  __device__ __forceinline__ void g(int row, double v) { gout[row] = v; }
+  __device__ __forceinline__ void operator()(int, int, double v, bool) {
+    const int k = (j >> 3) - (J0 >> 3);
+    SlotGroup q;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) q.w[w] = k == 0 ? q0.w[w] : k == 1 ? q1.w[w] : k == 2 ? q2.w[w] : q3.w[w];
+    const int s = slot_pick(q, j & 7);
+    ++j;
+    out[s] = v;
+  }
+  __device__ __forceinline__ void flush() {}
+};
+static_assert(kDynG0Cand - (kDynG0PhaseA - kDynG0PhaseA % 8) <= 32, "phase B of Dynamic group 0 exceeds the preloaded groups");
+
 // Slot-group prefetch depth. Deeper rings only pay off where the emission index is a compile-time
 // constant: in a runtime loop, rotating the ring copies registers whose loads are still in flight
 // and waits for the newest one (measured: depth 4 made RangeOfMotion's base-angular wave slower).
@@ -161,6 +191,59 @@ __device__ __forceinline__ void copy_out(const double* __restrict__ src, double*
   if (((n - head) & 1) && tid == 0) __builtin_nontemporal_store(src[n - 1], dst + n - 1);
 }
 
+// Split staging: issue() puts the first K 16-byte units per thread of x (and the node table) in
+// flight before the block's item / slot-table loads, commit() stores them to LDS afterwards, so the
+// staging's memory latency overlaps the item loads instead of following them. Units beyond K per
+// thread (problems larger than the bench's) go through stage16 in commit().
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+template <int BLOCK, bool NODES>
+struct XStage {
+  static constexpr int K = 3;   // named native-vector registers (HIP's uint4 class or an array goes to scratch)
+  u32x4_t x0 = {}, x1 = {}, x2 = {}, n0 = {}, n1 = {}, n2 = {};
+  bool aligned;
+  __device__ __forceinline__ void issue(const KParams& P, const double* xg) {
+    aligned = (reinterpret_cast<uintptr_t>(xg) & 15) == 0;
+    const int nx = P.n >> 1, i = threadIdx.x;
+    const u32x4_t* sx = reinterpret_cast<const u32x4_t*>(xg);
+    if (aligned) {
+      if (i < nx) x0 = sx[i];
+      if (i + BLOCK < nx) x1 = sx[i + BLOCK];
+      if (i + 2 * BLOCK < nx) x2 = sx[i + 2 * BLOCK];
+    }
+    if constexpr (NODES) {
+      const int nn = (P.n_nodecol + 3) >> 2;
+      const u32x4_t* sn = reinterpret_cast<const u32x4_t*>(P.nodecol);
+      if (i < nn) n0 = sn[i];
+      if (i + BLOCK < nn) n1 = sn[i + BLOCK];
+      if (i + 2 * BLOCK < nn) n2 = sn[i + 2 * BLOCK];
+    }
+  }
+  __device__ __forceinline__ void commit(const KParams& P, const double* xg, double* xs, int32_t* ns) {
+    const int nx = P.n >> 1, i = threadIdx.x;
+    if (aligned) {
+      u32x4_t* dx = reinterpret_cast<u32x4_t*>(xs);
+      if (i < nx) dx[i] = x0;
+      if (i + BLOCK < nx) dx[i + BLOCK] = x1;
+      if (i + 2 * BLOCK < nx) dx[i + 2 * BLOCK] = x2;
+      if (nx > K * BLOCK)
+        stage16<BLOCK>(reinterpret_cast<uint4*>(xs) + K * BLOCK, reinterpret_cast<const uint4*>(xg) + K * BLOCK, nx - K * BLOCK);
+      if ((P.n & 1) && threadIdx.x == 0) xs[P.n - 1] = xg[P.n - 1];
+    } else {
+      for (int k = threadIdx.x; k < P.n; k += BLOCK) xs[k] = xg[k];
+    }
+    if (threadIdx.x == 0) xs[P.n] = 0.0;
+    if constexpr (NODES) {
+      const int nn = (P.n_nodecol + 3) >> 2;
+      u32x4_t* dn = reinterpret_cast<u32x4_t*>(ns);
+      if (i < nn) dn[i] = n0;
+      if (i + BLOCK < nn) dn[i + BLOCK] = n1;
+      if (i + 2 * BLOCK < nn) dn[i + 2 * BLOCK] = n2;
+      if (nn > K * BLOCK)
+        stage16<BLOCK>(reinterpret_cast<uint4*>(ns) + K * BLOCK, reinterpret_cast<const uint4*>(P.nodecol) + K * BLOCK, nn - K * BLOCK);
+    }
+  }
+};
+
 // global -> LDS staging of the problem's x (+ zero slot at n) and optionally the node table
 template <int BLOCK, bool NODES>
 __device__ __forceinline__ void stage_x(const KParams& P, const double* xg, double* xs, int32_t* ns) {
@@ -185,6 +268,11 @@ __device__ __forceinline__ void stage_x(const KParams& P, const double* xg, doub
 // The heavy kinds read spline nodes through the segment records; with phase-duration optimisation
 // (GAIT) their PhaseSplines evaluate polynomials from the node table, which is then staged too.
 constexpr bool stages_nodes(int type, bool gait) { return gait || is_misc_kind(type); }
+// Split staging (XStage: x loads issued before the item / slot loads) where it measured faster on
+// MI355X (ANYmal, B = 4096): Dynamic 0.0617 -> 0.0582 ms, ForceConstraintDiscretized 0.1018 ->
+// 0.098 ms; RangeOfMotion got slower (0.0838 -> 0.0878 ms) and the small kinds were unchanged, so
+// they stage after their item loads as before.
+constexpr bool early_stage(int type) { return type == IT_DYN || type == IT_FDISC; }
 
 // Phase timing (tools/phase_timing.py; only in the -DTOWR_PHASE_TIMING build, never in the product):
 // per block, 16 timestamps: [0] realtime start, [1] memtime start, [2] after staging, [3..6] each
@@ -212,6 +300,10 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
 #ifdef TOWR_PHASE_TIMING
   if (threadIdx.x < 64) { TSTAMP(0, TS_REAL()); TSTAMP(1, TS_MEM()); }
 #endif
+  // x (+ a zero at index n for constant node values) and, for node-value kinds, the node table:
+  // loads in flight first, then the lane's item and slot groups, then the LDS stores
+  XStage<KBLOCK, stages_nodes(TYPE, GAIT)> xst;
+  if constexpr (early_stage(TYPE)) xst.issue(P, xg);
   ItemDesc it;
   if (KBLOCK == TBLOCK || (int)threadIdx.x < TBLOCK) {
     it = P.items[T.i0 + threadIdx.x];
@@ -219,10 +311,10 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
     it = ItemDesc{}; it.type = IT_NONE; it.slot = 0;
   }
   TileEmit<TBLOCK, slot_depth(TYPE)> em(P.slots + it.slot, smem, smem + lds_rows_off - T.r0);
-  // x (+ a zero at index n for constant node values) and, for node-value kinds, the node table
   double* xs = smem + lds_x_off;
   int32_t* ns = reinterpret_cast<int32_t*>(smem + lds_x_off + P.n_pad);
-  stage_x<KBLOCK, stages_nodes(TYPE, GAIT)>(P, xg, xs, ns);
+  if constexpr (early_stage(TYPE)) xst.commit(P, xg, xs, ns);
+  else stage_x<KBLOCK, stages_nodes(TYPE, GAIT)>(P, xg, xs, ns);
   __syncthreads();
 #ifdef TOWR_PHASE_TIMING
   if (threadIdx.x < 64) TSTAMP(2, TS_MEM());
@@ -245,13 +337,16 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
     }
   }
   if constexpr (TYPE == IT_DYN) {   // phase B of group 0: the endeffector sums from LDS
+    const bool g0lane = it.type == TYPE && it.group == 0;
+    TileEmitPre<TBLOCK, kDynG0PhaseA> emb(P.slots + it.slot, smem,
+                                                                                     smem + lds_rows_off - T.r0, g0lane);
     __syncthreads();
-    if (it.type == TYPE && it.group == 0) {
+    if (g0lane) {
       double fs[3] = {0, 0, 0}, ts[3] = {0, 0, 0};
       const double* d = c.dyn_scratch + it.a2 * P.rb.n_ee * 6;
       for (int ee = 0; ee < P.rb.n_ee; ++ee)
         for (int e = 0; e < 3; ++e) { ts[e] += d[ee * 6 + e]; fs[e] += d[ee * 6 + 3 + e]; }
-      dyn_g0_b(c, it, em, g0, fs, ts);
+      dyn_g0_b(c, it, emb, g0, fs, ts);
     }
   }
 #ifdef TOWR_PHASE_TIMING
