@@ -260,17 +260,22 @@ int towr_gpu_eval_batch_device(towr_gpu_handle h, int32_t B,
 /* Host batch (H2D of X, D2H of G and V through pinned staging; contiguous lds = n, m, nnz).      */
 int towr_gpu_eval_batch(towr_gpu_handle h, int32_t B, const double* X, double* G, double* V);
 
-/* The engine launches one kernel per launch class ("kernel" 0..towr_gpu_num_kernels()-1): the
- * Dynamic, RangeOfMotion and ForceConstraintDiscretized kinds each have their own, the small kinds
- * (node-value constraints, SplineAcc, BaseMotion, TotalDuration) share one. For roofline
- * accounting: its name, tiles (or tile groups) per problem, and algorithmic bytes per problem (CSR
- * values and g rows written + distinct x entries read), and a launch of that kernel alone.      */
+/* Launch classes and launches, for roofline accounting. Kernel indices 0..4 are the launch
+ * classes: Dynamic, RangeOfMotion, ForceConstraintDiscretized, TorqueConstraintDiscretized and the
+ * small kinds (node-value constraints, SplineAcc, BaseMotion, TotalDuration, ...), one kernel each.
+ * Indices 5..towr_gpu_num_kernels()-1 are the handle's fusion groups: classes that a step launches
+ * together in one kernel (default RangeOfMotion + ForceConstraintDiscretized; environment variable
+ * TOWR_GPU_FUSE at handle creation). towr_gpu_kernel_info gives a kernel's name, tiles (or units)
+ * per problem (0 = not used by this handle) and algorithmic bytes per problem (CSR values and g rows
+ * written + distinct x entries read); towr_gpu_eval_batch_device_kernel launches that kernel alone.
+ * towr_gpu_step_launches lists the kernels one evaluation launches (returns their count).       */
 int towr_gpu_kernel_info(towr_gpu_handle h, int32_t kernel, const char** name, int32_t* n_tiles,
                          int64_t* bytes_per_problem);
 int towr_gpu_eval_batch_device_kernel(towr_gpu_handle h, int32_t kernel, int32_t B,
                                       const double* X, int64_t ldx, double* G, int64_t ldg,
                                       double* V, int64_t ldv, void* stream);
 int towr_gpu_num_kernels(void);
+int towr_gpu_step_launches(towr_gpu_handle h, int32_t* kernels, int32_t cap);
 
 /* Sets the launch geometry (tiles per workgroup); 0 = automatic. For benchmarking.              */
 int towr_gpu_set_tiles_per_block(towr_gpu_handle h, int32_t tiles_per_block);

@@ -129,3 +129,18 @@ def test_costs_batch_device_matches_single():
         assert_cost_close(o.eval_f(X[b]), Fh[b], o.eval_grad_f(X[b]), Gh[b, :o.n], f"batch {b}")
     np.testing.assert_array_equal(F0h, Fh)
     assert np.all(np.isnan(Gh[:, o.n:]))   # nothing written past n
+
+
+# every launch arrangement (TOWR_GPU_FUSE) on configurations covering all launch classes: the
+# default fusion group, per-class launches, and the fused groups measured slower (kept selectable)
+@pytest.mark.parametrize("spec", ["none", "rf,dm", "drftm", "rftm,d"])
+@pytest.mark.parametrize("name", ["anymal_trot_2p4s", "biped_torque_hard_eelin", "anymal_stairs_gaitopt", "anymal_trot_rotvec", "anymal_gait_torque"])
+def test_fusion_groups(monkeypatch, spec, name):
+    monkeypatch.setenv("TOWR_GPU_FUSE", spec)
+    desc = CONFIGS[name]
+    o = Oracle(desc)
+    p = TowrGpuProblem(desc, device=0)
+    x = _perturb(o.initial_x(), 77)
+    r, c, v_ref = o.eval_jac(x)
+    g, v = p.eval_g_jac(x)
+    assert_close(o.eval_g(x), g, r, v_ref, v, o.m, f"{name} fuse {spec}", cols_ref=c)

@@ -74,8 +74,26 @@ def test_layout_only_handle_cannot_evaluate():
 
 def test_kernel_bytes_cover_the_call():
     p = TowrGpuProblem(CONFIGS["anymal_trot_2p4s"], device=-1)
-    ks = p.kernels()
-    assert {k[1] for k in ks} == {"dynamic", "range_of_motion", "force_discretized", "small_kinds"}
-    # every value and row is written by exactly one kernel
-    written = sum(b for *_, b in ks)
-    assert written >= 8 * (p.m + p.nnz)
+    ks = {k[0]: k for k in p.kernels()}
+    assert {k[1] for k in ks.values() if k[0] < 5} == {"dynamic", "range_of_motion", "force_discretized", "small_kinds"}
+    # every value and row is written by exactly one launch class, and by exactly one launch of a step
+    assert sum(k[3] for k in ks.values() if k[0] < 5) >= 8 * (p.m + p.nnz)
+    steps = p.step_launches()
+    assert sum(ks[k][3] for k in steps) >= 8 * (p.m + p.nnz)
+    # default fusion: RangeOfMotion + ForceConstraintDiscretized in one launch, x columns counted once
+    assert [ks[k][1] for k in steps] == ["range_of_motion+force_discretized", "dynamic", "small_kinds"]
+    assert ks[steps[0]][3] <= ks[1][3] + ks[2][3]
+    assert ks[steps[0]][2] == ks[1][2] + ks[2][2]   # units = both classes' tiles
+
+
+@pytest.mark.parametrize("spec,launches", [
+    ("none", ["dynamic", "range_of_motion", "force_discretized", "small_kinds"]),
+    ("rf,dm", ["range_of_motion+force_discretized", "dynamic+small_kinds"]),
+    ("drftm", ["dynamic+range_of_motion+force_discretized+small_kinds"]),
+    ("rt", ["dynamic", "range_of_motion", "force_discretized", "small_kinds"]),   # no torque sets: no group
+])
+def test_fusion_groups_from_environment(monkeypatch, spec, launches):
+    monkeypatch.setenv("TOWR_GPU_FUSE", spec)
+    p = TowrGpuProblem(CONFIGS["anymal_trot_2p4s"], device=-1)
+    names = dict((k[0], k[1]) for k in p.kernels())
+    assert [names[k] for k in p.step_launches()] == launches

@@ -132,6 +132,7 @@ SYMBOLS = {
     "towr_gpu_eval_batch_device_kernel": (C.c_int, [_HANDLE, C.c_int32, C.c_int32, C.c_void_p, C.c_int64,
                                                      C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p]),
     "towr_gpu_num_kernels": (C.c_int, []),
+    "towr_gpu_step_launches": (C.c_int, [_HANDLE, _IP, C.c_int32]),
     "towr_gpu_set_tiles_per_block": (C.c_int, [_HANDLE, C.c_int32]),
     "towr_gpu_algorithmic_bytes_per_call": (C.c_int64, [_HANDLE]),
 }

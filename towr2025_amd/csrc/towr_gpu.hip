@@ -30,7 +30,6 @@ namespace {
 
 // one unit of the fused launch: a tile of a tile class, or a small-kind group (LC_MISC)
 struct UnitDesc { int32_t lc, tile, lds_x_off, lds_rows_off; };
-constexpr int kFusedBlock = 256;
 
 struct KParams {
   const double* X; int64_t ldx;
@@ -459,14 +458,16 @@ __global__ void __launch_bounds__(64 * kMiscWaves, 1) towr_misc_kernel(KParams P
   misc_body<GAIT>(P, smem, w / P.ntiles, w % P.ntiles, P.lds_x_off);
 }
 
-// The whole step in ONE launch: a problem's units (its tiles of every class and its small-kind
-// groups) are consecutive work ids, interleaved so that latency-bound units (Dynamic, small kinds)
-// share the CUs with write-bound ones (RangeOfMotion, ForceConstraintDiscretized) and no launch
-// boundary drains the machine between classes. Every unit runs the same code as its per-class
-// kernel (tile_body / misc_body); 192-lane tiles leave the block's fourth wave to staging and
-// copy-out. The unit table is uniform per block (scalar loads).
-template <bool GAIT, bool ROTVEC>
-__global__ void __launch_bounds__(kFusedBlock, 2) towr_step_kernel(KParams P) {
+// Fused launches: a fusion group's classes run in ONE launch. A problem's units (its tiles of the
+// group's classes and its small-kind groups) are consecutive work ids, interleaved round-robin over
+// the classes, so latency-bound units (Dynamic, small kinds) share the CUs with write-bound ones and
+// no launch boundary drains the machine between the group's classes. Every unit runs the same code
+// as its per-class kernel (tile_body / misc_body). KBLOCK = the group's block size: 256 when it holds
+// Dynamic or the small kinds (192-lane tiles then leave the fourth wave to staging and copy-out),
+// else 192. The unit table is uniform per block (scalar loads). The kernel's register allocation is
+// the largest of its classes' (Dynamic: 242 VGPRs), which is what decides whether a group pays off.
+template <bool GAIT, bool ROTVEC, int KBLOCK>
+__global__ void __launch_bounds__(KBLOCK, (KBLOCK == 256 ? 2 : 1)) towr_step_kernel(KParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int total = P.B * P.n_units;
   const int per = (total + 7) / 8;
@@ -475,16 +476,24 @@ __global__ void __launch_bounds__(kFusedBlock, 2) towr_step_kernel(KParams P) {
   const int b = w / P.n_units;
   const UnitDesc u = P.units[w % P.n_units];
   switch (u.lc) {
-    case LC_DYN: tile_body<IT_DYN, 256, kFusedBlock, GAIT, ROTVEC>(P, smem, b, u.tile, u.lds_x_off, u.lds_rows_off); break;
-    case LC_ROM: tile_body<IT_ROM, 192, kFusedBlock, GAIT, ROTVEC>(P, smem, b, u.tile, u.lds_x_off, u.lds_rows_off); break;
-    case LC_FDISC: tile_body<IT_FDISC, 192, kFusedBlock, GAIT, false>(P, smem, b, u.tile, u.lds_x_off, u.lds_rows_off); break;
-    case LC_TQDISC: tile_body<IT_TQDISC, 192, kFusedBlock, GAIT, false>(P, smem, b, u.tile, u.lds_x_off, u.lds_rows_off); break;
-    default: misc_body<GAIT>(P, smem, b, u.tile, u.lds_x_off); break;
+    case LC_ROM: tile_body<IT_ROM, 192, KBLOCK, GAIT, ROTVEC>(P, smem, b, u.tile, u.lds_x_off, u.lds_rows_off); break;
+    case LC_FDISC: tile_body<IT_FDISC, 192, KBLOCK, GAIT, false>(P, smem, b, u.tile, u.lds_x_off, u.lds_rows_off); break;
+    case LC_TQDISC: tile_body<IT_TQDISC, 192, KBLOCK, GAIT, false>(P, smem, b, u.tile, u.lds_x_off, u.lds_rows_off); break;
+    default:
+      if constexpr (KBLOCK == 256) {
+        if (u.lc == LC_DYN) tile_body<IT_DYN, 256, KBLOCK, GAIT, ROTVEC>(P, smem, b, u.tile, u.lds_x_off, u.lds_rows_off);
+        else misc_body<GAIT>(P, smem, b, u.tile, u.lds_x_off);
+      }
+      break;
   }
 }
-const void* step_kernel_for(bool gait, bool rotvec) {
-  if (gait) return rotvec ? reinterpret_cast<const void*>(&towr_step_kernel<true, true>) : reinterpret_cast<const void*>(&towr_step_kernel<true, false>);
-  return rotvec ? reinterpret_cast<const void*>(&towr_step_kernel<false, true>) : reinterpret_cast<const void*>(&towr_step_kernel<false, false>);
+template <int KBLOCK>
+const void* step_kernel_kb(bool gait, bool rotvec) {
+  if (gait) return rotvec ? reinterpret_cast<const void*>(&towr_step_kernel<true, true, KBLOCK>) : reinterpret_cast<const void*>(&towr_step_kernel<true, false, KBLOCK>);
+  return rotvec ? reinterpret_cast<const void*>(&towr_step_kernel<false, true, KBLOCK>) : reinterpret_cast<const void*>(&towr_step_kernel<false, false, KBLOCK>);
+}
+const void* step_kernel_for(bool gait, bool rotvec, int kblock) {
+  return kblock == 256 ? step_kernel_kb<256>(gait, rotvec) : step_kernel_kb<192>(gait, rotvec);
 }
 
 // Objective and gradient (IpoptAdapter::eval_f / eval_grad_f): one block per problem. The block
@@ -610,6 +619,7 @@ const void* kernel_for_class(int lc, bool gait, bool rotvec) {
   return kernel_for(class_type(lc), gait, rotvec);
 }
 
+
 }  // namespace
 
 // =================================================================================================
@@ -637,10 +647,18 @@ struct towr_gpu_handle_s {
   EELinDef* d_eelin = nullptr;
   CostItem* d_citems = nullptr;
   double* d_cq = nullptr;
-  // fused single-launch step (TOWR_GPU_FUSED, see towr_step_kernel): the unit table of one problem
-  UnitDesc* d_units = nullptr;
-  int32_t n_units = 0;
-  bool fused = false;
+  // fusion groups (TOWR_GPU_FUSE, see towr_step_kernel): classes that run in one launch
+  struct FuseGroup {
+    uint32_t mask = 0;        // bit lc: launch class lc belongs to the group
+    int kblock = 0;
+    UnitDesc* d_units = nullptr;
+    int32_t n_units = 0;
+    size_t lds = 0;
+  };
+  static constexpr int kMaxFuse = 2;
+  FuseGroup fuse[kMaxFuse];
+  int n_fuse = 0;
+  std::string fuse_name[kMaxFuse];   // towr_gpu_kernel_info
   // fork-join of the per-kind launches (TOWR_GPU_STREAMS = total streams incl. the caller's, 1..4)
   static constexpr int kMaxSide = 3;
   int n_side = 0;
@@ -710,21 +728,43 @@ int class_units(const Layout& L, int lc) {   // tiles (or misc groups) per probl
 }
 int64_t class_bytes(const Layout& L, int lc) { return lc == LC_MISC ? L.misc_bytes : L.type_bytes[class_type(lc)]; }
 
-// LDS of the fused launch: the largest class's
-size_t fused_lds_bytes(const Layout& L) {
-  size_t m = 0;
-  for (int lc = 0; lc < LC_COUNT; ++lc)
-    if (class_units(L, lc) > 0) m = std::max(m, lds_bytes(L, lc));
-  return m;
+// RangeOfMotion + ForceConstraintDiscretized in one launch (both 192-lane, their registers and LDS
+// allow 3 blocks per CU either way). Measured on MI355X (ANYmal, B = 4096, 3 alternating runs each):
+// per-class 0.269-0.275 ms per step, "rf" 0.263-0.268 ms; adding Dynamic + small kinds as a second
+// group ("rf,dm") 0.285 ms, the small kinds into the first ("rfm") 0.308 ms, everything ("drftm")
+// 0.317 ms: a group inherits its largest class's registers, and Dynamic's 242 VGPRs or a 256-lane
+// block cost the others their residency.
+constexpr const char* kDefaultFuse = "rf";
+
+// algorithmic bytes per problem of the classes in `mask` launched together: CSR values and g rows
+// written + the union of the x columns their Jacobian rows read
+int64_t mask_bytes(const Layout& L, uint32_t mask) {
+  std::vector<uint8_t> used((size_t)L.n, 0);
+  int64_t nv = 0, nr = 0;
+  auto add = [&](const TileDesc& td) {
+    nv += td.v1 - td.v0; nr += td.r1 - td.r0;
+    for (int32_t k = td.v0; k < td.v1; ++k) used[L.col[k]] = 1;
+  };
+  for (int lc = 0; lc < LC_COUNT; ++lc) {
+    if (!((mask >> lc) & 1)) continue;
+    if (lc == LC_MISC) {
+      for (int32_t ti : L.misc_tiles) if (ti >= 0) add(L.tiles[ti]);
+    } else {
+      for (int ti = L.type_tile0[class_type(lc)]; ti < L.type_tile0[class_type(lc) + 1]; ++ti) add(L.tiles[ti]);
+    }
+  }
+  int64_t nx = 0;
+  for (uint8_t u : used) nx += u;
+  return 8 * (nv + nr + nx);
 }
 
-// the fused launch's unit table: one round-robin pass over the classes at a time (heaviest writer
+// a fusion group's unit table: one round-robin pass over its classes at a time (heaviest writer
 // first), so consecutive blocks of a problem alternate latency-bound and write-bound units
-std::vector<UnitDesc> fused_units(const Layout& L) {
+std::vector<UnitDesc> fused_units(const Layout& L, uint32_t mask) {
   static const int order[] = {LC_FDISC, LC_DYN, LC_ROM, LC_TQDISC, LC_MISC};
   std::vector<UnitDesc> u;
   int left[LC_COUNT];
-  for (int lc = 0; lc < LC_COUNT; ++lc) left[lc] = class_units(L, lc);
+  for (int lc = 0; lc < LC_COUNT; ++lc) left[lc] = (mask >> lc) & 1 ? class_units(L, lc) : 0;
   for (bool any = true; any;) {
     any = false;
     for (int lc : order) {
@@ -759,18 +799,19 @@ void fill_common(towr_gpu_handle h, KParams& P, int B, const double* X, int64_t 
   P.lds_scr_off = L.dyn_scr_off;
 }
 
-int launch_fused(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, int64_t ldg, double* V, int64_t ldv,
-                 int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem) {
+int launch_fused(towr_gpu_handle h, const towr_gpu_handle_s::FuseGroup& fg, int B, const double* X, int64_t ldx, double* G,
+                 int64_t ldg, double* V, int64_t ldv, int want_g, int want_jac, hipStream_t s,
+                 const towr_terrain_t* terrains, int per_problem) {
   const Layout& L = h->L;
   KParams P{};
   fill_common(h, P, B, X, ldx, G, ldg, V, ldv, want_g, want_jac, terrains, per_problem);
-  P.units = h->d_units; P.n_units = h->n_units;
-  const int64_t total = (int64_t)B * h->n_units;
+  P.units = fg.d_units; P.n_units = fg.n_units;
+  const int64_t total = (int64_t)B * fg.n_units;
   const int64_t grid = ((total + 7) / 8) * 8;
   if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
   void* args[] = {&P};
-  HIPCHK(h, hipLaunchKernel(step_kernel_for(L.gait, L.rotvec), dim3((unsigned)grid), dim3(kFusedBlock), args,
-                            fused_lds_bytes(L), s));
+  HIPCHK(h, hipLaunchKernel(step_kernel_for(L.gait, L.rotvec, fg.kblock), dim3((unsigned)grid), dim3((unsigned)fg.kblock),
+                            args, fg.lds, s));
   return TOWR_OK;
 }
 
@@ -778,12 +819,17 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
            int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem, int only_class = -1) {
   if (B <= 0) return TOWR_OK;
   const Layout& L = h->L;
-  if (h->fused && only_class < 0) return launch_fused(h, B, X, ldx, G, ldg, V, ldv, want_g, want_jac, s, terrains, per_problem);
+  uint32_t fused_mask = 0;
+  if (only_class < 0)
+    for (int g = 0; g < h->n_fuse; ++g) {
+      if (int rc = launch_fused(h, h->fuse[g], B, X, ldx, G, ldg, V, ldv, want_g, want_jac, s, terrains, per_problem)) return rc;
+      fused_mask |= h->fuse[g].mask;
+    }
   // The launch classes are independent (disjoint rows and CSR ranges): optionally fork them onto the
   // handle's side streams (TOWR_GPU_STREAMS) and join back into the caller's stream. Heaviest first.
   int order[LC_COUNT], nk = 0;
   for (int lc = 0; lc < LC_COUNT; ++lc)
-    if (class_units(L, lc) > 0 && (only_class < 0 || lc == only_class)) order[nk++] = lc;
+    if (class_units(L, lc) > 0 && !((fused_mask >> lc) & 1) && (only_class < 0 || lc == only_class)) order[nk++] = lc;
   std::sort(order, order + nk, [&](int a, int b) { return class_bytes(L, a) > class_bytes(L, b); });
   const int nside = (only_class < 0 && nk > 1) ? std::min(h->n_side, nk - 1) : 0;
   if (nside > 0) {
@@ -939,6 +985,45 @@ int host_eval(towr_gpu_handle h, int B, const double* X, double* G, double* V) {
   return TOWR_OK;
 }
 
+// Fusion groups from TOWR_GPU_FUSE (or kDefaultFuse): comma-separated groups of class letters (d
+// Dynamic, r RangeOfMotion, f ForceConstraintDiscretized, t TorqueConstraintDiscretized, m small
+// kinds), e.g. "rf" or "rf,dm"; "none" = per-class launches. Classes this layout lacks are dropped; a
+// group needs two classes. Layout-only: the unit tables are uploaded by towr_gpu_create.
+int setup_fusion(towr_gpu_handle h, std::string& err) {
+  const Layout& L = h->L;
+  const char* fz = std::getenv("TOWR_GPU_FUSE");
+  const std::string spec = fz ? fz : kDefaultFuse;
+  size_t p0 = 0;
+  while (p0 <= spec.size() && h->n_fuse < towr_gpu_handle_s::kMaxFuse) {
+    const size_t p1 = std::min(spec.find(',', p0), spec.size());
+    uint32_t mask = 0;
+    for (size_t k = p0; k < p1; ++k) {
+      const char* letters = "drftm";
+      const char* f = std::strchr(letters, spec[k]);
+      if (f && *f) mask |= 1u << (f - letters);
+    }
+    for (int lc = 0; lc < LC_COUNT; ++lc)
+      if (((mask >> lc) & 1) && class_units(L, lc) == 0) mask &= ~(1u << lc);
+    for (int g = 0; g < h->n_fuse; ++g) mask &= ~h->fuse[g].mask;
+    if (__builtin_popcount(mask) >= 2) {
+      towr_gpu_handle_s::FuseGroup& fg = h->fuse[h->n_fuse++];
+      fg.mask = mask;
+      fg.kblock = (mask & ((1u << LC_DYN) | (1u << LC_MISC))) ? 256 : 192;
+      for (int lc = 0; lc < LC_COUNT; ++lc)
+        if ((mask >> lc) & 1) {
+          fg.lds = std::max(fg.lds, lds_bytes(L, lc));
+          if (lc != LC_MISC && L.type_block[class_type(lc)] != (lc == LC_DYN ? 256 : 192)) {
+            err = "internal: fused launch expects 256-lane Dynamic and 192-lane tiles"; return TOWR_ERR_INVALID;
+          }
+        }
+      fg.n_units = (int32_t)fused_units(L, mask).size();
+      if (fg.lds > 160 * 1024) { err = "tile too large for LDS"; return TOWR_ERR_UNSUPPORTED; }
+    }
+    p0 = p1 + 1;
+  }
+  return TOWR_OK;
+}
+
 }  // namespace
 
 // =================================================================================================
@@ -955,7 +1040,7 @@ int towr_gpu_debug_set_timing_buffer(void* p) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_tbuf), &v, sizeof(v)) == hipSuccess ? 0 : TOWR_ERR_HIP;
 }
 #endif
-int towr_gpu_num_kernels(void) { return LC_COUNT; }
+int towr_gpu_num_kernels(void) { return LC_COUNT + towr_gpu_handle_s::kMaxFuse; }
 
 const char* towr_gpu_last_error(towr_gpu_handle h) {
   if (h) return h->err.c_str();
@@ -970,6 +1055,7 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
   std::string err;
   const int rc = build_layout(*desc, h->L, err);
   if (rc != TOWR_OK) { fail(nullptr, rc, err); delete h; return rc; }
+  if (int rf = setup_fusion(h, err)) { fail(nullptr, rf, err); delete h; return rf; }
   if (device < 0) {   // layout-only handle: sizes / structure / x0, no evaluation (CPU-side tests)
     h->device = -1;
     *out = h;
@@ -1054,22 +1140,11 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
         h->err = "side stream creation failed"; return bail(TOWR_ERR_HIP);
       }
   }
-  {   // fused single-launch step: TOWR_GPU_FUSED=1 (default off). Measured on MI355X (ANYmal,
-      // B = 4096): 0.317 ms per step fused vs 0.287 ms with the per-class launches — the fused
-      // kernel carries Dynamic's 242 VGPRs into every unit (2 waves per SIMD), so RangeOfMotion and
-      // ForceConstraintDiscretized lose a third of their resident waves.
-    const char* fz = std::getenv("TOWR_GPU_FUSED");
-    h->fused = fz && std::atoi(fz) != 0;
-    const std::vector<UnitDesc> units = fused_units(L);
-    for (const UnitDesc& u : units)
-      if (u.lc != LC_MISC && L.type_block[class_type(u.lc)] != (u.lc == LC_DYN ? 256 : 192)) {
-        h->err = "internal: fused launch expects 256-lane Dynamic and 192-lane tiles"; return bail(TOWR_ERR_INVALID);
-      }
-    h->n_units = (int32_t)units.size();
-    if ((r = upload(h, &h->d_units, units))) return bail(r);
-    const size_t lds = fused_lds_bytes(L);
-    if (lds > 160 * 1024) { h->err = "tile too large for LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
-    if (lds > 64 * 1024 && hipFuncSetAttribute(step_kernel_for(L.gait, L.rotvec), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+  for (int g = 0; g < h->n_fuse; ++g) {   // fusion groups (set up with the layout): unit tables
+    towr_gpu_handle_s::FuseGroup& fg = h->fuse[g];
+    const std::vector<UnitDesc> units = fused_units(L, fg.mask);
+    if ((r = upload(h, &fg.d_units, units))) return bail(r);
+    if (fg.lds > 64 * 1024 && hipFuncSetAttribute(step_kernel_for(L.gait, L.rotvec, fg.kblock), hipFuncAttributeMaxDynamicSharedMemorySize, (int)fg.lds) != hipSuccess) {
       h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
     }
   }
@@ -1097,7 +1172,7 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
 int towr_gpu_destroy(towr_gpu_handle h) {
   if (!h) return TOWR_OK;
   void* dev[] = {h->d_items, h->d_slots, h->d_tiles, h->d_nodecol, h->d_spl, h->d_dur, h->d_segs, h->d_terrain,
-                 h->d_pinfo, h->d_pcols, h->d_sched, h->d_misc, h->d_misc_lds, h->d_eelin, h->d_citems, h->d_cq, h->d_units,
+                 h->d_pinfo, h->d_pcols, h->d_sched, h->d_misc, h->d_misc_lds, h->d_eelin, h->d_citems, h->d_cq, h->fuse[0].d_units, h->fuse[1].d_units,
                  h->d_bterrain, h->d_x, h->d_g, h->d_v, h->d_f, h->d_grad,
                  h->d_traj_pd, h->d_traj_n, h->d_traj_c0, h->d_traj_t};
   if (h->device >= 0) for (void* p : dev) if (p) (void)hipFree(p);
@@ -1289,19 +1364,54 @@ int towr_gpu_eval_batch_device(towr_gpu_handle h, int32_t B, const double* X, in
 
 int towr_gpu_kernel_info(towr_gpu_handle h, int32_t kernel, const char** name, int32_t* n_tiles, int64_t* bytes_per_problem) {
   static const char* names[LC_COUNT] = {"dynamic", "range_of_motion", "force_discretized", "torque_discretized", "small_kinds"};
-  if (!h || kernel < 0 || kernel >= LC_COUNT) return fail(h, TOWR_ERR_INVALID, "bad kernel index");
+  if (!h || kernel < 0 || kernel >= towr_gpu_num_kernels()) return fail(h, TOWR_ERR_INVALID, "bad kernel index");
+  if (kernel >= LC_COUNT) {   // fusion group slot
+    const int g = kernel - LC_COUNT;
+    const bool on = g < h->n_fuse;
+    if (name) {
+      h->fuse_name[g].clear();
+      for (int lc = 0; on && lc < LC_COUNT; ++lc)
+        if ((h->fuse[g].mask >> lc) & 1) h->fuse_name[g] += (h->fuse_name[g].empty() ? "" : "+") + std::string(names[lc]);
+      *name = h->fuse_name[g].c_str();
+    }
+    if (n_tiles) *n_tiles = on ? h->fuse[g].n_units : 0;
+    if (bytes_per_problem) *bytes_per_problem = on ? mask_bytes(h->L, h->fuse[g].mask) : 0;
+    return TOWR_OK;
+  }
   if (name) *name = names[kernel];
   if (n_tiles) *n_tiles = class_units(h->L, kernel);
   if (bytes_per_problem) *bytes_per_problem = class_bytes(h->L, kernel);
   return TOWR_OK;
 }
+int towr_gpu_step_launches(towr_gpu_handle h, int32_t* kernels, int32_t cap) {
+  if (!h || (cap > 0 && !kernels)) return fail(h, TOWR_ERR_INVALID, "bad argument");
+  int cnt = 0;
+  uint32_t fused = 0;
+  for (int g = 0; g < h->n_fuse; ++g) {
+    if (cnt < cap) kernels[cnt] = LC_COUNT + g;
+    ++cnt;
+    fused |= h->fuse[g].mask;
+  }
+  for (int lc = 0; lc < LC_COUNT; ++lc)
+    if (class_units(h->L, lc) > 0 && !((fused >> lc) & 1)) {
+      if (cnt < cap) kernels[cnt] = lc;
+      ++cnt;
+    }
+  return cnt;
+}
 int towr_gpu_eval_batch_device_kernel(towr_gpu_handle h, int32_t kernel, int32_t B, const double* X, int64_t ldx,
                                       double* G, int64_t ldg, double* V, int64_t ldv, void* stream) {
-  if (!h || B < 0 || !X || !G || !V || kernel < 0 || kernel >= LC_COUNT) return fail(h, TOWR_ERR_INVALID, "bad argument");
+  if (!h || B < 0 || !X || !G || !V || kernel < 0 || kernel >= towr_gpu_num_kernels()) return fail(h, TOWR_ERR_INVALID, "bad argument");
   const Layout& L = h->L;
   if (ldx < L.n || ldg < L.m || ldv < L.nnz) return fail(h, TOWR_ERR_INVALID, "leading dimension too small");
   if (int rc = bind(h)) return rc;
   const bool per = h->d_bterrain && h->bterrain_n >= B;
+  if (kernel >= LC_COUNT) {
+    const int g = kernel - LC_COUNT;
+    if (g >= h->n_fuse) return fail(h, TOWR_ERR_INVALID, "no fusion group at this kernel index");
+    return launch_fused(h, h->fuse[g], B, X, ldx, G, ldg, V, ldv, 1, 1, reinterpret_cast<hipStream_t>(stream),
+                        per ? h->d_bterrain : h->d_terrain, per ? 1 : 0);
+  }
   return launch(h, B, X, ldx, G, ldg, V, ldv, 1, 1, reinterpret_cast<hipStream_t>(stream),
                 per ? h->d_bterrain : h->d_terrain, per ? 1 : 0, kernel);
 }

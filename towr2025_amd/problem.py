@@ -180,8 +180,17 @@ class TowrGpuProblem:
             C.c_void_p(G.data_ptr()), G.stride(0), C.c_void_p(V.data_ptr()), V.stride(0),
             int(want_g), int(want_jac), C.c_void_p(stream.cuda_stream)))
 
+    def step_launches(self):
+        """Kernel indices (see kernels()) that one evaluation launches: fusion groups, then the unfused classes."""
+        buf = (C.c_int32 * 16)()
+        n = self._lib.towr_gpu_step_launches(self._h, buf, 16)
+        if n < 0:
+            self._check(n)
+        return list(buf[:n])
+
     def kernels(self):
-        """[(index, name, n_tiles, algorithmic bytes per problem)] of the per-constraint-kind kernels."""
+        """[(index, name, n_tiles, algorithmic bytes per problem)] of the launch classes' kernels and the
+        fusion groups (index >= 5) this handle uses."""
         out = []
         for k in range(self._lib.towr_gpu_num_kernels()):
             name, nt, by = C.c_char_p(), C.c_int32(), C.c_int64()
@@ -191,7 +200,7 @@ class TowrGpuProblem:
         return out
 
     def eval_batch_device_kernel(self, kernel, X, G, V, stream):
-        """Launch one constraint kind's kernel only (roofline accounting)."""
+        """Launch one kernel only: a launch class or a fusion group (roofline accounting)."""
         self._check(self._lib.towr_gpu_eval_batch_device_kernel(
             self._h, kernel, X.shape[0], C.c_void_p(X.data_ptr()), X.stride(0),
             C.c_void_p(G.data_ptr()), G.stride(0), C.c_void_p(V.data_ptr()), V.stride(0),
