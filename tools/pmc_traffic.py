@@ -23,7 +23,7 @@ def per_kernel(d, counter):
         if "towr_misc_kernel" in k:
             acc["small_kinds"].append(float(r["Counter_Value"]) * 1024.0)
         elif "towr_step_kernel<" in k:   # fusion group: the default 192-lane group is RangeOfMotion + FDISC
-            acc["range_of_motion+force_discretized" if k.rstrip(")").split("(")[0].endswith("192>") else "fused_256"].append(
+            acc["range_of_motion+force_discretized" if ", 192>(" in k else "fused_256"].append(
                 float(r["Counter_Value"]) * 1024.0)
         elif "towr_tile_kernel<" in k:
             t = int(k.split("towr_tile_kernel<")[1].split(",")[0])
