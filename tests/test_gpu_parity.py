@@ -144,3 +144,46 @@ def test_fusion_groups(monkeypatch, spec, name):
     r, c, v_ref = o.eval_jac(x)
     g, v = p.eval_g_jac(x)
     assert_close(o.eval_g(x), g, r, v_ref, v, o.m, f"{name} fuse {spec}", cols_ref=c)
+
+
+def test_bench_workload_full_size(monkeypatch):
+    """The bench's workload at its full size (B = 4096 randomised ANYmal problems, bench.make_batch):
+    a seeded sample of problems against the oracle; every problem bit-identical between the default
+    launch arrangement and per-class launches and between two evaluations (idempotence); no NaN, and
+    the padding of the leading dimensions untouched."""
+    import torch
+    import bench
+    from towr2025_amd import formulation as F
+    B = 4096
+    desc = F.anymal_trot().to_desc()
+    p = TowrGpuProblem(desc)
+    monkeypatch.setenv("TOWR_GPU_FUSE", "none")
+    q = TowrGpuProblem(desc)
+    Xh, terrains = bench.make_batch(p, B, first_id=0)
+    p.set_batch_terrain(terrains)
+    q.set_batch_terrain(terrains)
+    dev = torch.device("cuda:0")
+    ldg, ldv = (p.m + 15) // 16 * 16, (p.nnz + 15) // 16 * 16
+    X = torch.from_numpy(np.ascontiguousarray(Xh[1])).to(dev)
+    outs = []
+    for prob in (p, p, q):
+        G = torch.full((B, ldg), np.nan, dtype=torch.float64, device=dev)
+        V = torch.full((B, ldv), np.nan, dtype=torch.float64, device=dev)
+        prob.eval_batch_device(X, G, V)
+        torch.cuda.synchronize()
+        outs.append((G.cpu().numpy(), V.cpu().numpy()))
+    (G, V), (G2, V2), (G3, V3) = outs
+    assert np.isnan(G[:, p.m:]).all() and np.isnan(V[:, p.nnz:]).all()
+    G, V = G[:, :p.m], V[:, :p.nnz]
+    assert np.isfinite(G).all() and np.isfinite(V).all()
+    np.testing.assert_array_equal(G2[:, :p.m], G)
+    np.testing.assert_array_equal(V2[:, :p.nnz], V)
+    np.testing.assert_array_equal(G3[:, :p.m], G)
+    np.testing.assert_array_equal(V3[:, :p.nnz], V)
+    rng = np.random.default_rng(4096)
+    for b in sorted(rng.choice(B, 12, replace=False)):
+        d = F.anymal_trot().to_desc()
+        d.terrain = terrains[b]
+        o = Oracle(d)
+        r, _, v_ref = o.eval_jac(Xh[1, b])
+        assert_close(o.eval_g(Xh[1, b]), G[b], r, v_ref, V[b], o.m, f"bench problem {b}")
