@@ -31,17 +31,22 @@ SEED = 20261015
 N_X = 4          # pre-generated x sets cycled over (every step reads a different x)
 
 
-def make_batch(prob, B, first_id):
+def make_batch(prob, B, first_id, optimize_timings=False):
     """Randomised instances (SURVEY §8(d) config 5): start xy ~ U(-0.5,0.5), yaw ~ U(-0.3,0.3);
     goal = start + (U(1.5,2.5), U(-0.3,0.3)); terrain Flat(h~U(0,0.3)) or Stairs(start~U(0.8,1.4),
-    heights~U(0.1,0.25)); x = x0 + sigma * N(0,1) per variable-set kind."""
+    heights~U(0.1,0.25)); x = x0 + sigma * N(0,1) per variable-set kind. With optimize_timings (the
+    phase-duration variables of BASELINE configs[3]) the durations get +-3 % multiplicative noise."""
     from towr2025_amd import formulation as F
     from towr2025_amd import _capi as capi
     sig_kind = {capi.VAR_BASE_LIN: 0.05, capi.VAR_BASE_ANG: 0.1, capi.VAR_EE_MOTION: 0.05,
                 capi.VAR_EE_ANG: 0.1, capi.VAR_EE_FORCE: 20.0, capi.VAR_EE_TORQUE: 1.0}
     sigma = np.zeros(prob.n)
+    sched = np.zeros(prob.n, dtype=bool)
     for kind, _ee, c0, n in prob.varset_info():
-        sigma[c0:c0 + n] = sig_kind[kind]
+        if kind == capi.VAR_EE_SCHEDULE:
+            sched[c0:c0 + n] = True
+        else:
+            sigma[c0:c0 + n] = sig_kind[kind]
     X = np.zeros((N_X, B, prob.n))
     terrains = []
     for b in range(B):
@@ -54,11 +59,13 @@ def make_batch(prob, B, first_id):
         else:
             ter = F.HeightMap(F.HeightMap.StairsID, (rng.uniform(0.8, 1.4), 0.4, rng.uniform(0.1, 0.25),
                                                      rng.uniform(0.1, 0.25), 1.0))
-        f = F.anymal_trot(goal=(gx, gy, 0.0), terrain=ter, start_xy=(sx, sy), start_yaw=syaw, goal_yaw=syaw)
+        f = F.anymal_trot(goal=(gx, gy, 0.0), terrain=ter, start_xy=(sx, sy), start_yaw=syaw, goal_yaw=syaw,
+                          optimize_timings=optimize_timings)
         d = f.to_desc()
         x0 = prob.initial_x_for(d.init, d.terrain)
         for k in range(N_X):
             X[k, b] = x0 + sigma * rng.standard_normal(prob.n)
+            X[k, b, sched] = x0[sched] * (1.0 + 0.03 * rng.standard_normal(int(sched.sum())))
         terrains.append(d.terrain)
     return X, terrains
 
@@ -103,6 +110,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
+    ap.add_argument("--no-gait", action="store_true", help="skip the phase-duration optimisation figure")
     ap.add_argument("--tiles-per-block", type=int, default=0)
     args = ap.parse_args()
 
@@ -234,6 +242,31 @@ def main():
                             "GB/s": B * cbytes / (ms * 1e-3) / 1e9,
                             "note": "ANYmal trot + Forces/EEMotion/Energy/AngularMomentum/EEBasePos costs, same batch"}
         cprob.close()
+    if rank == 0 and not args.no_gait:
+        # BASELINE configs[3]'s formulation (phase-duration optimisation: PhaseSplines with x-dependent
+        # durations, schedule Jacobian columns) on a batch of the same randomised instances
+        gprob = TowrGpuProblem(F.anymal_trot(optimize_timings=True).to_desc(), device=local)
+        Bg = min(B, 1024)
+        Xg, gter = make_batch(gprob, Bg, first_id=shard_first_id(rank, Bg), optimize_timings=True)
+        gprob.set_batch_terrain(gter)
+        Xgd = [torch.from_numpy(Xg[k]).to(dev) for k in range(2)]
+        Gg = torch.empty((Bg, (gprob.m + 15) // 16 * 16), dtype=torch.float64, device=dev)
+        Vg = torch.empty((Bg, (gprob.nnz + 15) // 16 * 16), dtype=torch.float64, device=dev)
+        for i in range(2):
+            gprob.eval_batch_device(Xgd[i % 2], Gg, Vg, stream=stream)
+        a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for i in range(reps):
+            gprob.eval_batch_device(Xgd[i % 2], Gg, Vg, stream=stream)
+        z.record(stream)
+        torch.cuda.synchronize()
+        ms = a.elapsed_time(z) / reps
+        gb = gprob.algorithmic_bytes_per_call()
+        out["gait_optimization"] = {"value": Bg / (ms * 1e-3), "unit": "calls/s", "ms_per_batch": ms, "problems": Bg,
+                                    "n": gprob.n, "m": gprob.m, "nnz": gprob.nnz, "GB/s": Bg * gb / (ms * 1e-3) / 1e9,
+                                    "note": "BASELINE configs[3] formulation (ANYmal, phase-duration optimisation), "
+                                            "randomised Flat/Stairs instances, durations +-3 %"}
+        gprob.close()
     if rank == 0 and not args.no_host:
         # PCIe-inclusive rate through the host-buffer entry point (towr_gpu_eval_batch: H2D of X,
         # launch, D2H of G and V via pinned staging) — reported beside, never as `value`

@@ -10,3 +10,6 @@ for f in sys.argv[1:]:
             if 'objective' in d:
                 o = d['objective']
                 print(f"   objective          {o['ms_per_batch']:.4f} ms {o['value']:.4g} calls/s")
+            if 'gait_optimization' in d:
+                o = d['gait_optimization']
+                print(f"   gait_optimization  {o['ms_per_batch']:.4f} ms {o['value']:.4g} calls/s ({o['problems']} problems, nnz {o['nnz']}, {o['GB/s']:.0f} GB/s)")

@@ -393,8 +393,9 @@ TG_HD void emit_dim(const Ctx& c, Emit& em, int row, int s, const SplinePt& P, c
     const PhaseCol pq = pc[q];
     double v = 0.0;
     for (int k = 0; k < pq.n; ++k) {   // coeffRef += per node value the variable sets
-      if (pq.id[k] == P.poly) v += H[pq.deriv[k]];
-      else if (pq.id[k] == P.poly + 1) v += H[2 + pq.deriv[k]];
+      // selects, not H[runtime index] (which would keep H in scratch on the device)
+      if (pq.id[k] == P.poly) v += pq.deriv[k] ? H[1] : H[0];
+      else if (pq.id[k] == P.poly + 1) v += pq.deriv[k] ? H[3] : H[2];
     }
     em(row, pq.col, scale * v, pres);
   }
@@ -1462,7 +1463,10 @@ TG_HD void eval_eelin(const Ctx& c, const ItemDesc& it, Emit& em) {
     const int ee = d.code[q] / 3, dim = d.code[q] % 3, s = d.target == 0 ? sp_motion(ee) : sp_ang(ee);
     SplinePt P;
     spline_eval(c, s, it.t, P);
-    val += d.coeff[q] * (d.deriv == 0 ? P.p[dim] : P.v[dim]);
+    // select chains, not a runtime index or pointer (either keeps P in scratch on the device)
+    const double pd = dim == 0 ? P.p[0] : dim == 1 ? P.p[1] : P.p[2];
+    const double vd = dim == 0 ? P.v[0] : dim == 1 ? P.v[1] : P.v[2];
+    val += d.coeff[q] * (d.deriv == 0 ? pd : vd);
     double H[4];
     spline_basis(P, d.deriv == 0 ? kPos : kVel, H);
     emit_dim(c, em, it.row0, s, P, H, dim, d.coeff[q]);
