@@ -64,7 +64,7 @@ struct SplineMeta {
   int32_t ee;        // endeffector of a PhaseSpline, else -1
   int32_t pinfo_off; // first PolyPhase of this spline
   int32_t pcol_off[3], pcol_n[3];   // PhaseCol entries of each dimension (the full pattern)
-  int32_t reserved;
+  int32_t pact_off;  // PhaseSpline: active PhaseCol range of each (dim, polynomial), see Ctx::pact
 };
 
 // phase of a polynomial (NodesVariablesPhaseBased::PolyInfo, nodes_variables_phase_based.cc:39-59)
@@ -166,6 +166,8 @@ struct Ctx {
   double* dyn_scratch;          // device DYN tiles: per-instant endeffector terms (see dyn_g0_a), else nullptr
   const PolyPhase* pinfo;
   const PhaseCol* pcols;
+  const int32_t* pact;          // PhaseSpline: [qa, qb] PhaseCol index range (within the dim's list) whose
+                                // columns polynomial p touches, at pact[spl.pact_off + 2 (e n_polys + p)]
   const SchedInfo* sched;       // per endeffector
   const EELinDef* eelin;        // EELinearConstraint definitions
   const double* cq;             // cost kernel: CT_ENERGYQ Gram matrices (16 doubles each)
@@ -363,6 +365,12 @@ TG_HD void spline_basis(const SplinePt& o, int d, double H[4]) {
   else hermite_dacc(o.T, o.tl, H);
 }
 
+// Emitters that write into zero-filled outputs declare `static constexpr bool kSparse = true` and
+// `skip(k)` (advance past k candidates whose value is 0); emit_dim then emits only the nonzero window
+// of a PhaseSpline's full pattern. The structure pass and the test emulation emit every candidate.
+template <class E, class = void> struct emit_sparse { static constexpr bool value = false; };
+template <class E> struct emit_sparse<E, decltype((void)E::kSparse)> { static constexpr bool value = E::kSparse; };
+
 // scale * d{P's derivative}(spline s)/dx restricted to dimension e, into `row`, given the basis H:
 //   NodeSpline: the 4 basis columns of the active polynomial (node_spline.cc:62-112);
 //   PhaseSpline: every column of the set in dimension e (the full pattern, phase_spline.cc:45-51,
@@ -389,6 +397,24 @@ TG_HD void emit_dim(const Ctx& c, Emit& em, int row, int s, const SplinePt& P, c
   const SplineMeta m = c.spl[s];
   const PhaseCol* pc = c.pcols + m.pcol_off[e];
   const int n = m.pcol_n[e];
+  if constexpr (emit_sparse<Emit>::value) {
+    // An emitter over a zero-filled output (the device tiles, the gradient) only needs the columns
+    // the active polynomial touches: every other column of the full pattern is exactly 0.
+    const int32_t* r = c.pact + m.pact_off + 2 * (e * m.n_polys + P.poly);
+    const int qa = r[0], qb = r[1];
+    em.skip(qa);
+    for (int q = qa; q <= qb; ++q) {
+      const PhaseCol pq = pc[q];
+      double v = 0.0;
+      for (int k = 0; k < pq.n; ++k) {
+        if (pq.id[k] == P.poly) v += pq.deriv[k] ? H[1] : H[0];
+        else if (pq.id[k] == P.poly + 1) v += pq.deriv[k] ? H[3] : H[2];
+      }
+      em(row, pq.col, scale * v, pres);
+    }
+    em.skip(n - 1 - (qb >= qa ? qb : qa - 1));
+    return;
+  }
   for (int q = 0; q < n; ++q) {
     const PhaseCol pq = pc[q];
     double v = 0.0;

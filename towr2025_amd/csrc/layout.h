@@ -41,6 +41,7 @@ struct Layout {
   bool rotvec = false;          // Parameters::RotationVector base orientation (RotVecConverter)
   std::vector<PolyPhase> pinfo; // PhaseSpline polynomial phases
   std::vector<PhaseCol> pcols;  // PhaseSpline full-pattern columns
+  std::vector<int32_t> pact;    // PhaseSpline active PhaseCol ranges (SplineMeta::pact_off)
   std::vector<SchedInfo> sched; // per endeffector (col0 = -1 without schedule variables)
   std::vector<EELinDef> eelin;  // EELinearConstraint definitions (ItemDesc::a0 indexes them)
   std::vector<ItemDesc> items;

@@ -469,6 +469,27 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
           }
           m.pcol_n[e] = (int32_t)L.pcols.size() - m.pcol_off[e];
         }
+        // active window of each (dim, polynomial): the PhaseCol range whose columns the polynomial's
+        // two nodes set (node ids grow with the column, so the range is contiguous); empty: qa > qb
+        m.pact_off = (int32_t)L.pact.size();
+        for (int e = 0; e < 3; ++e)
+          for (int p = 0; p < m.n_polys; ++p) {
+            int qa = m.pcol_n[e], qb = m.pcol_n[e] - 1;
+            for (int q = 0; q < m.pcol_n[e]; ++q) {
+              const PhaseCol& pc = L.pcols[m.pcol_off[e] + q];
+              bool act = false;
+              for (int k = 0; k < pc.n; ++k) act = act || pc.id[k] == p || pc.id[k] == p + 1;
+              if (act) { qa = std::min(qa, q); qb = q; }
+            }
+            for (int q = qa; q <= qb; ++q) {   // contiguity (the kernels rely on it)
+              const PhaseCol& pc = L.pcols[m.pcol_off[e] + q];
+              bool act = false;
+              for (int k = 0; k < pc.n; ++k) act = act || pc.id[k] == p || pc.id[k] == p + 1;
+              if (!act) { err = "internal: PhaseSpline active columns not contiguous"; return TOWR_ERR_INVALID; }
+            }
+            L.pact.push_back(qa);
+            L.pact.push_back(qb);
+          }
       }
     }
     L.spl.push_back(m);
@@ -670,7 +691,7 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
     Ctx cx{};
     cx.x = L.x0.data(); cx.nodecol = L.nodecol.data(); cx.spl = L.spl.data(); cx.dur = L.dur.data();
     cx.ter = &L.terrain; cx.rb = L.rb; cx.fdisc_motion = L.fdisc_motion;
-    cx.gait = L.gait; cx.pinfo = L.pinfo.data(); cx.pcols = L.pcols.data(); cx.sched = L.sched.data();
+    cx.gait = L.gait; cx.pinfo = L.pinfo.data(); cx.pcols = L.pcols.data(); cx.sched = L.sched.data(); cx.pact = L.pact.data();
     cx.eelin = L.eelin.data(); cx.rotvec = L.rotvec;
     for (size_t i = 0; i < L.items.size(); ++i) {
       item_cand_begin[i] = (int32_t)crow.size();

@@ -44,6 +44,7 @@ struct KParams {
   SegSoA sg;                     // segment table (structure of arrays)
   const PolyPhase* pinfo;        // phase-duration optimisation tables (see engine_math.h)
   const PhaseCol* pcols;
+  const int32_t* pact;
   const SchedInfo* sched;
   const EELinDef* eelin;
   int32_t n_spl;
@@ -85,6 +86,19 @@ struct TileEmit {
     for (int d = 0; d < DEPTH; ++d) q[d] = s[d * BLOCK];
   }
   __device__ __forceinline__ void g(int row, double v) { gout[row] = v; }
+  // GAIT tiles are zero-filled before the evaluation (tile_body / misc_body), so candidates whose
+  // value is 0 can be skipped: move to candidate j + k, reloading the slot ring if the group changes
+  static constexpr bool kSparse = true;
+  __device__ __forceinline__ void skip(int k) {
+    if (k <= 0) return;
+    const int g0 = j >> 3;
+    j += k;
+    const int g1 = j >> 3;
+    if (g1 != g0) {
+#pragma unroll
+      for (int d = 0; d < DEPTH; ++d) q[d] = slot[(g1 + d) * BLOCK];
+    }
+  }
   __device__ __forceinline__ void operator()(int, int, double v, bool) {
 #ifdef TOWR_EXPERIMENT_NOSLOT   // timing experiment only: wrong positions, no slot-table traffic
     out[(threadIdx.x * 7 + j++) & 1023] = v;
@@ -243,6 +257,13 @@ struct XStage {
   }
 };
 
+// zero n doubles of LDS (16-byte stores; n rounded up to even, the tile regions are even-sized)
+__device__ __forceinline__ void zero_lds(double* d, int n, int tid, int nthr) {
+  dbl2_t* d2 = reinterpret_cast<dbl2_t*>(d);
+  const dbl2_t z = {0.0, 0.0};
+  for (int i = tid; i < (n + 1) >> 1; i += nthr) d2[i] = z;
+}
+
 // global -> LDS staging of the problem's x (+ zero slot at n) and optionally the node table
 template <int BLOCK, bool NODES>
 __device__ __forceinline__ void stage_x(const KParams& P, const double* xg, double* xs, int32_t* ns) {
@@ -312,6 +333,7 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
   TileEmit<TBLOCK, slot_depth(TYPE)> em(P.slots + it.slot, smem, smem + lds_rows_off - T.r0);
   double* xs = smem + lds_x_off;
   int32_t* ns = reinterpret_cast<int32_t*>(smem + lds_x_off + P.n_pad);
+  if constexpr (GAIT) zero_lds(smem, T.v1 - T.v0, threadIdx.x, KBLOCK);   // sparse PhaseSpline emission
   if constexpr (early_stage(TYPE)) xst.commit(P, xg, xs, ns);
   else stage_x<KBLOCK, stages_nodes(TYPE, GAIT)>(P, xg, xs, ns);
   __syncthreads();
@@ -323,7 +345,7 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
   c.x = xs; c.nodecol = ns; c.spl = P.spl; c.dur = P.dur;
   c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
   c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
-  c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.sched = P.sched; c.eelin = P.eelin;
+  c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.pact = P.pact; c.sched = P.sched; c.eelin = P.eelin;
   c.rotvec = ROTVEC;
   c.dyn_scratch = TYPE == IT_DYN ? smem + P.lds_scr_off : nullptr;
   DynG0 g0;   // DYN group 0 between its two phases
@@ -399,6 +421,8 @@ __device__ __forceinline__ void misc_body(const KParams& P, double* smem, int b,
 #ifdef TOWR_PHASE_TIMING
   if (threadIdx.x < 64) { TSTAMP(0, TS_REAL()); TSTAMP(1, TS_MEM()); }
 #endif
+  if constexpr (GAIT)   // sparse PhaseSpline emission: each wave zero-fills its own tile
+    if (ti >= 0) zero_lds(wl, T.v1 - T.v0, lane, 64);
   stage_x<BLOCK, true>(P, P.X + (int64_t)b * P.ldx, xs, ns);
   __syncthreads();
 #ifdef TOWR_PHASE_TIMING
@@ -410,7 +434,7 @@ __device__ __forceinline__ void misc_body(const KParams& P, double* smem, int b,
     c.x = xs; c.nodecol = ns; c.spl = P.spl; c.dur = P.dur;
     c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
     c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
-    c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.sched = P.sched; c.eelin = P.eelin;
+    c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.pact = P.pact; c.sched = P.sched; c.eelin = P.eelin;
     c.rotvec = false;   // no small kind uses the base orientation
     c.dyn_scratch = nullptr;
     switch (it.type) {   // wave-uniform: a wave holds one tile of one kind
@@ -506,6 +530,8 @@ template <bool GRAD>
 struct CostEmit {
   double* grad;   // LDS; the dump slot at index n absorbs constant node values
   double f = 0.0;
+  static constexpr bool kSparse = true;   // zero gradient contributions need no atomic
+  __device__ __forceinline__ void skip(int) {}
   __device__ __forceinline__ void operator()(int, int col, double v, bool pres) {
     if constexpr (GRAD)
       if (pres && v != 0.0) atomicAdd(grad + col, v);
@@ -530,7 +556,7 @@ __global__ void __launch_bounds__(kCostBlock, 1) towr_cost_kernel(KParams P) {
   c.x = xs; c.nodecol = ns; c.spl = P.spl; c.dur = P.dur;
   c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
   c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
-  c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.sched = P.sched; c.eelin = P.eelin;
+  c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.pact = P.pact; c.sched = P.sched; c.eelin = P.eelin;
   c.rotvec = ROTVEC;
   c.dyn_scratch = nullptr;
   c.cq = P.cq;
@@ -583,7 +609,7 @@ __global__ void __launch_bounds__(kTrajBlock, 1) towr_traj_kernel(KParams P, con
     c.seg = nullptr; c.row = -1;
     c.x = xs; c.nodecol = nsp; c.spl = P.spl; c.dur = P.dur;
     c.ter = P.terrains; c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
-    c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.sched = P.sched; c.eelin = P.eelin;
+    c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.pact = P.pact; c.sched = P.sched; c.eelin = P.eelin;
     c.rotvec = false; c.dyn_scratch = nullptr;
     traj_row(c, ph, times[k], rows + threadIdx.x, stride);
   }
@@ -641,6 +667,7 @@ struct towr_gpu_handle_s {
   SegSoA sg{};
   PolyPhase* d_pinfo = nullptr;
   PhaseCol* d_pcols = nullptr;
+  int32_t* d_pact = nullptr;
   SchedInfo* d_sched = nullptr;
   int32_t* d_misc = nullptr;
   int32_t* d_misc_lds = nullptr;
@@ -789,7 +816,7 @@ void fill_common(towr_gpu_handle h, KParams& P, int B, const double* X, int64_t 
   P.items = h->d_items; P.slots = h->d_slots; P.tiles = h->d_tiles;
   P.nodecol = h->d_nodecol; P.spl = h->d_spl; P.dur = h->d_dur;
   P.sg = h->sg; P.n_spl = (int32_t)L.spl.size();
-  P.pinfo = h->d_pinfo; P.pcols = h->d_pcols; P.sched = h->d_sched; P.eelin = h->d_eelin;
+  P.pinfo = h->d_pinfo; P.pcols = h->d_pcols; P.pact = h->d_pact; P.sched = h->d_sched; P.eelin = h->d_eelin;
   P.terrains = terrains; P.terrain_per_problem = per_problem;
   P.B = B;
   P.n = L.n; P.n_pad = (L.n + 2) & ~1; P.n_nodecol = (int32_t)L.nodecol.size();
@@ -845,7 +872,7 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
     P.items = h->d_items; P.slots = h->d_slots; P.tiles = h->d_tiles;
     P.nodecol = h->d_nodecol; P.spl = h->d_spl; P.dur = h->d_dur;
     P.sg = h->sg; P.n_spl = (int32_t)L.spl.size();
-    P.pinfo = h->d_pinfo; P.pcols = h->d_pcols; P.sched = h->d_sched; P.eelin = h->d_eelin;
+    P.pinfo = h->d_pinfo; P.pcols = h->d_pcols; P.pact = h->d_pact; P.sched = h->d_sched; P.eelin = h->d_eelin;
     P.terrains = terrains; P.terrain_per_problem = per_problem;
     P.B = B; P.ntiles = nt;
     if (lc == LC_MISC) {
@@ -887,7 +914,7 @@ int launch_cost(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* 
   P.X = X; P.ldx = ldx;
   P.nodecol = h->d_nodecol; P.spl = h->d_spl; P.dur = h->d_dur;
   P.sg = h->sg; P.n_spl = (int32_t)L.spl.size();
-  P.pinfo = h->d_pinfo; P.pcols = h->d_pcols; P.sched = h->d_sched; P.eelin = h->d_eelin;
+  P.pinfo = h->d_pinfo; P.pcols = h->d_pcols; P.pact = h->d_pact; P.sched = h->d_sched; P.eelin = h->d_eelin;
   P.terrains = terrains; P.terrain_per_problem = per_problem;
   P.B = B;
   P.n = L.n; P.n_pad = (L.n + 2) & ~1; P.n_nodecol = (int32_t)L.nodecol.size();
@@ -929,7 +956,7 @@ int launch_traj(towr_gpu_handle h, int B, const double* X, int64_t ldx, double d
   KParams P{};
   P.X = X; P.ldx = ldx;
   P.nodecol = h->d_nodecol; P.spl = h->d_spl; P.dur = h->d_dur;
-  P.pinfo = h->d_pinfo; P.pcols = h->d_pcols; P.sched = h->d_sched; P.eelin = h->d_eelin;
+  P.pinfo = h->d_pinfo; P.pcols = h->d_pcols; P.pact = h->d_pact; P.sched = h->d_sched; P.eelin = h->d_eelin;
   P.terrains = h->d_terrain;
   P.n = L.n; P.n_pad = (L.n + 2) & ~1; P.n_nodecol = (int32_t)L.nodecol.size();
   P.rb = L.rb;
@@ -1085,7 +1112,7 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
   if ((r = upload(h, &h->d_items, L.items)) || (r = upload(h, &h->d_slots, L.slot_groups)) ||
       (r = upload(h, &h->d_tiles, L.tiles)) || (r = upload(h, &h->d_nodecol, nodecol16)) ||
       (r = upload(h, &h->d_spl, L.spl)) || (r = upload(h, &h->d_dur, L.dur)) || (r = upload(h, &h->d_terrain, ter)) ||
-      (r = upload(h, &h->d_pinfo, L.pinfo)) || (r = upload(h, &h->d_pcols, L.pcols)) || (r = upload(h, &h->d_sched, L.sched)) ||
+      (r = upload(h, &h->d_pinfo, L.pinfo)) || (r = upload(h, &h->d_pcols, L.pcols)) || (r = upload(h, &h->d_pact, L.pact)) || (r = upload(h, &h->d_sched, L.sched)) ||
       (r = upload(h, &h->d_misc, L.misc_tiles)) || (r = upload(h, &h->d_misc_lds, L.misc_lds)) || (r = upload(h, &h->d_eelin, L.eelin)) ||
       (r = upload(h, &h->d_citems, L.cost_items)) || (r = upload(h, &h->d_cq, L.cost_q)))
     return bail(r);
@@ -1172,7 +1199,7 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
 int towr_gpu_destroy(towr_gpu_handle h) {
   if (!h) return TOWR_OK;
   void* dev[] = {h->d_items, h->d_slots, h->d_tiles, h->d_nodecol, h->d_spl, h->d_dur, h->d_segs, h->d_terrain,
-                 h->d_pinfo, h->d_pcols, h->d_sched, h->d_misc, h->d_misc_lds, h->d_eelin, h->d_citems, h->d_cq, h->fuse[0].d_units, h->fuse[1].d_units,
+                 h->d_pinfo, h->d_pcols, h->d_pact, h->d_sched, h->d_misc, h->d_misc_lds, h->d_eelin, h->d_citems, h->d_cq, h->fuse[0].d_units, h->fuse[1].d_units,
                  h->d_bterrain, h->d_x, h->d_g, h->d_v, h->d_f, h->d_grad,
                  h->d_traj_pd, h->d_traj_n, h->d_traj_c0, h->d_traj_t};
   if (h->device >= 0) for (void* p : dev) if (p) (void)hipFree(p);
