@@ -14,9 +14,12 @@ namespace {
 // same semantics as the kernel's TileEmit: 8 tile-relative positions per SlotGroup, one plain store
 // per present candidate (a position written twice would be a layout bug: the check leaves NaN)
 struct AccEmit {
-  const SlotGroup* slot; int stride; double* v; double* gout; int nvals; int j = 0;
+  const SlotGroup* slot; int stride; double* v; double* gout; int nvals; int frow = -1; int j = 0;
+  static constexpr bool kFilter = true;   // row-split items (ItemDesc::rsel), as the kernel's TileEmit
+  bool want(int row) const { return frow < 0 || row == frow; }
   void g(int row, double val) { gout[row] = val; }
-  void operator()(int, int, double val, bool) {
+  void operator()(int row, int, double val, bool) {
+    if (!want(row)) return;
     const int s = slot_pick(slot[(j / 8) * stride], j % 8);
     ++j;
     if (s >= nvals) return;   // the lane's dummy slot (absent candidate)
@@ -41,7 +44,8 @@ extern "C" int emu_eval(const towr_problem_desc_t* d, const double* x, double* g
     for (int l = td.i0; l < td.i1; ++l) {
       const ItemDesc& it = L.items[l];
       if (it.type == IT_NONE) continue;
-      AccEmit em{L.slot_groups.data() + it.slot, td.i1 - td.i0, v + td.v0, g, td.v1 - td.v0};
+      AccEmit em{L.slot_groups.data() + it.slot, td.i1 - td.i0, v + td.v0, g, td.v1 - td.v0,
+                 it.rsel > 0 ? it.row0 + it.rsel - 1 : -1};
       c.seg = it.seg >= 0 ? L.segs.data() + (size_t)it.seg * L.spl.size() : nullptr;
       eval_item(c, it, em);
       em.flush();
@@ -79,7 +83,8 @@ extern "C" int emu_cost(const towr_problem_desc_t* d, const double* x, double* f
 extern "C" int emu_stats(const towr_problem_desc_t* d) {
   Layout L; std::string e;
   if (build_layout(*d, L, e)) return -1;
-  std::printf("n %d m %d nnz %lld\n", L.n, L.m, (long long)L.nnz);
+  std::printf("n %d m %d nnz %lld nodecol %zu | gait tables: spl %zu pinfo %zu pcols %zu pact %zu sched %zu\n", L.n, L.m,
+              (long long)L.nnz, L.nodecol.size(), L.spl.size(), L.pinfo.size(), L.pcols.size(), L.pact.size(), L.sched.size());
   for (int t = 0; t < IT_COUNT; ++t) {
     int nt = L.type_tile0[t + 1] - L.type_tile0[t];
     if (!nt) continue;

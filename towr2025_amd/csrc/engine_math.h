@@ -105,7 +105,10 @@ struct ItemDesc {
   int32_t slot;                 // candidate j of this item is slot_table[slot + j * stride]
   int32_t seg;                  // row of the segment table (time-discretised items), else -1
   int32_t ncand;                // number of candidates the item emits
-  int32_t a2, reserved;         // third node id (TorqueConstraint: torque node at phase start)
+  int32_t a2;                   // third node id (TorqueConstraint: torque node at phase start)
+  int32_t rsel;                 // row select: 0 = the item emits all its rows' candidates, r > 0 = only
+                                // row row0 + r - 1 (phase-duration optimisation splits the heavy
+                                // PhaseSpline items one row per lane, see layout.h split_rows)
   double t;                     // time of the instant (time-discretised sets)
   double p0;                    // scalar parameter (safety distance, t_swing_avg, ...)
 };
@@ -171,6 +174,16 @@ struct Ctx {
   const SchedInfo* sched;       // per endeffector
   const EELinDef* eelin;        // EELinearConstraint definitions
   const double* cq;             // cost kernel: CT_ENERGYQ Gram matrices (16 doubles each)
+  // Device tile blocks under phase-duration optimisation: the x-dependent PhaseSpline timings,
+  // computed once per block (gait_timings in towr_gpu.hip) with the same operations in the same order
+  // as the per-call code below, so every lane reads bit-identical values: per PolyPhase entry the
+  // polynomial duration (pdur) and the running sum of durations up to its end (pend); per endeffector
+  // the running sum of phase durations up to each phase's end (phend, stride ph_stride).
+  // nullptr: computed per call.
+  const double* pdur = nullptr;
+  const double* pend = nullptr;
+  const double* phend = nullptr;
+  int32_t ph_stride = 0;
 };
 
 // ----------------------------------------------------------------------------------------------
@@ -295,8 +308,47 @@ TG_HD double phase_poly_duration(const Ctx& c, const SplineMeta& m, const SchedI
   const PolyPhase pp = c.pinfo[m.pinfo_off + i];
   return phase_duration(c, si, last, pp.phase) / pp.n_in_phase;
 }
+// The block-shared PhaseSpline timings of Ctx::pdur / pend / phend, by the per-call code's own
+// operations: spline s's polynomial durations and their running sums (phase_spline_locate's scan),
+// endeffector ee's running sums of phase durations (sched_jac's scan).
+TG_HD void phase_spline_timings(const Ctx& c, int s, double* pdur, double* pend) {
+  const SplineMeta m = c.spl[s];
+  const SchedInfo si = c.sched[m.ee];
+  const double last = last_phase_duration(c, si);
+  double t = 0.0;
+  for (int i = 0; i < m.n_polys; ++i) {
+    const double d = phase_poly_duration(c, m, si, last, i);
+    t += d;
+    pdur[m.pinfo_off + i] = d;
+    pend[m.pinfo_off + i] = t;
+  }
+}
+TG_HD void phase_end_timings(const Ctx& c, int ee, double* phend) {
+  const SchedInfo si = c.sched[ee];
+  const double last = last_phase_duration(c, si);
+  double acc = 0.0;
+  for (int ph = 0; ph < si.n_phases; ++ph) {
+    acc += phase_duration(c, si, last, ph);
+    phend[ph] = acc;
+  }
+}
 // Spline::GetLocalTime (spline.cc:48-78) over the x-dependent durations of a PhaseSpline
 TG_HD void phase_spline_locate(const Ctx& c, int s, double tg, SplinePt& o) {
+  if (c.pdur) {   // the block's precomputed durations and running sums (see Ctx::pdur)
+    const int off = c.spl[s].pinfo_off, np = c.spl[s].n_polys;
+    const double* d = c.pdur + off;
+    const double* e = c.pend + off;
+    const double eps = 1e-10;
+    int id = np - 1;
+    for (int i = 0; i < np; ++i)
+      if (e[i] >= tg - eps) { id = i; break; }
+    double l = tg;
+    for (int i = 0; i < id; ++i) l -= d[i];
+    o.poly = id;
+    o.tl = l;
+    o.T = d[id];
+    return;
+  }
   const SplineMeta m = c.spl[s];
   const SchedInfo si = c.sched[m.ee];
   const double last = last_phase_duration(c, si), eps = 1e-10;
@@ -371,6 +423,17 @@ TG_HD void spline_basis(const SplinePt& o, int d, double H[4]) {
 template <class E, class = void> struct emit_sparse { static constexpr bool value = false; };
 template <class E> struct emit_sparse<E, decltype((void)E::kSparse)> { static constexpr bool value = E::kSparse; };
 
+// Emitters that evaluate only some rows of an item (row-split items, ItemDesc::rsel) declare
+// `static constexpr bool kFilter = true` and `want(row)`; their operator() drops the other rows'
+// candidates itself, and emit_dim skips such rows' full-pattern work before it starts.
+template <class E, class = void> struct emit_filter { static constexpr bool value = false; };
+template <class E> struct emit_filter<E, decltype((void)E::kFilter)> { static constexpr bool value = E::kFilter; };
+
+template <class E> TG_HD bool em_wants(const E& em, int row) {
+  if constexpr (emit_filter<E>::value) return em.want(row);
+  else return true;
+}
+
 // scale * d{P's derivative}(spline s)/dx restricted to dimension e, into `row`, given the basis H:
 //   NodeSpline: the 4 basis columns of the active polynomial (node_spline.cc:62-112);
 //   PhaseSpline: every column of the set in dimension e (the full pattern, phase_spline.cc:45-51,
@@ -378,6 +441,8 @@ template <class E> struct emit_sparse<E, decltype((void)E::kSparse)> { static co
 template <class Emit>
 TG_HD void emit_dim(const Ctx& c, Emit& em, int row, int s, const SplinePt& P, const double H[4], int e, double scale,
                     bool pres = true) {
+  if constexpr (emit_filter<Emit>::value)
+    if (!em.want(row)) return;
   if (!P.dyn) {
     int col[4];
     for (int bb = 0; bb < 4; ++bb) col[bb] = basis_col(c, s, P.poly, bb, e);
@@ -397,6 +462,12 @@ TG_HD void emit_dim(const Ctx& c, Emit& em, int row, int s, const SplinePt& P, c
   const SplineMeta m = c.spl[s];
   const PhaseCol* pc = c.pcols + m.pcol_off[e];
   const int n = m.pcol_n[e];
+  // the basis as opaque registers: the compiler otherwise turns the selects below into a load
+  // H[runtime index], which keeps H in scratch memory on the device
+  double h0 = H[0], h1 = H[1], h2 = H[2], h3 = H[3];
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(h0), "+v"(h1), "+v"(h2), "+v"(h3));
+#endif
   if constexpr (emit_sparse<Emit>::value) {
     // An emitter over a zero-filled output (the device tiles, the gradient) only needs the columns
     // the active polynomial touches: every other column of the full pattern is exactly 0.
@@ -406,9 +477,11 @@ TG_HD void emit_dim(const Ctx& c, Emit& em, int row, int s, const SplinePt& P, c
     for (int q = qa; q <= qb; ++q) {
       const PhaseCol pq = pc[q];
       double v = 0.0;
-      for (int k = 0; k < pq.n; ++k) {
-        if (pq.id[k] == P.poly) v += pq.deriv[k] ? H[1] : H[0];
-        else if (pq.id[k] == P.poly + 1) v += pq.deriv[k] ? H[3] : H[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {   // constant indices: a runtime-indexed pq.id / deriv would go to scratch
+        if (k >= pq.n) break;
+        if (pq.id[k] == P.poly) v += pq.deriv[k] ? h1 : h0;
+        else if (pq.id[k] == P.poly + 1) v += pq.deriv[k] ? h3 : h2;
       }
       em(row, pq.col, scale * v, pres);
     }
@@ -418,10 +491,11 @@ TG_HD void emit_dim(const Ctx& c, Emit& em, int row, int s, const SplinePt& P, c
   for (int q = 0; q < n; ++q) {
     const PhaseCol pq = pc[q];
     double v = 0.0;
-    for (int k = 0; k < pq.n; ++k) {   // coeffRef += per node value the variable sets
-      // selects, not H[runtime index] (which would keep H in scratch on the device)
-      if (pq.id[k] == P.poly) v += pq.deriv[k] ? H[1] : H[0];
-      else if (pq.id[k] == P.poly + 1) v += pq.deriv[k] ? H[3] : H[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {   // coeffRef += per node value the variable sets
+      if (k >= pq.n) break;
+      if (pq.id[k] == P.poly) v += pq.deriv[k] ? h1 : h0;
+      else if (pq.id[k] == P.poly + 1) v += pq.deriv[k] ? h3 : h2;
     }
     em(row, pq.col, scale * v, pres);
   }
@@ -447,12 +521,19 @@ TG_HD void sched_jac(const Ctx& c, int s, double t, const SplinePt& P, SchedJac&
     J.dx[k] = inner * (dxdT - prev * P.v[k]);
     J.v[k] = P.v[k];
   }
-  const double last = last_phase_duration(c, si), eps = 1e-10;   // GetSegmentID over the phases
-  double acc = 0.0;
+  const double eps = 1e-10;   // GetSegmentID over the phases
   J.cur = si.n_phases - 1;
-  for (int ph = 0; ph < si.n_phases; ++ph) {
-    acc += phase_duration(c, si, last, ph);
-    if (acc >= t - eps) { J.cur = ph; break; }
+  if (c.phend) {
+    const double* pe = c.phend + m.ee * c.ph_stride;
+    for (int ph = 0; ph < si.n_phases; ++ph)
+      if (pe[ph] >= t - eps) { J.cur = ph; break; }
+  } else {
+    const double last = last_phase_duration(c, si);
+    double acc = 0.0;
+    for (int ph = 0; ph < si.n_phases; ++ph) {
+      acc += phase_duration(c, si, last, ph);
+      if (acc >= t - eps) { J.cur = ph; break; }
+    }
   }
   J.n = si.n_phases;
   J.col0 = si.col0;
@@ -1114,16 +1195,22 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
   const double rv[3] = {L.p[0] - P.p[0], L.p[1] - P.p[1], L.p[2] - P.p[2]};
   double H[4];
   spline_basis(F, kPos, H);
+  #pragma unroll
   for (int r = 0; r < 3; ++r)
+    #pragma unroll
     for (int d = 1; d <= 2; ++d) {
       const int e = (r + d) % 3;
       emit_dim(c, em, r0 + AX + r, sp_force(ee), F, H, e, cross_el(rv, r, e));
     }
+  #pragma unroll
   for (int e = 0; e < 3; ++e) emit_dim(c, em, r0 + LX + e, sp_force(ee), F, H, e, -1.0);
   spline_basis(Tq, kPos, H);
+  #pragma unroll
   for (int e = 0; e < 3; ++e) emit_dim(c, em, r0 + AX + e, sp_torque(ee), Tq, H, e, -1.0);
   spline_basis(P, kPos, H);
+  #pragma unroll
   for (int r = 0; r < 3; ++r)
+    #pragma unroll
     for (int d = 1; d <= 2; ++d) {
       const int e = (r + d) % 3;
       emit_dim(c, em, r0 + AX + r, sp_motion(ee), P, H, e, cross_el(F.p, r, e));
@@ -1134,7 +1221,9 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
     SchedJac Jf, Jx;
     sched_jac(c, sp_force(ee), t, F, Jf);
     sched_jac(c, sp_motion(ee), t, P, Jx);
+    #pragma unroll
     for (int r = 0; r < 3; ++r) {
+      if (!em_wants(em, r0 + AX + r)) continue;
       const int e1 = (r + 1) % 3, e2 = (r + 2) % 3;
       for (int col = 0; col < Jf.n - 1; ++col) {
         const double a = cross_el(rv, r, e1) * sched_val(Jf, e1, col) + cross_el(rv, r, e2) * sched_val(Jf, e2, col);
@@ -1142,8 +1231,10 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
         em(r0 + AX + r, Jf.col0 + col, a + b, true);
       }
     }
+    #pragma unroll
     for (int e = 0; e < 3; ++e)
-      for (int col = 0; col < Jf.n - 1; ++col) em(r0 + LX + e, Jf.col0 + col, -sched_val(Jf, e, col), true);
+      if (em_wants(em, r0 + LX + e))
+        for (int col = 0; col < Jf.n - 1; ++col) em(r0 + LX + e, Jf.col0 + col, -sched_val(Jf, e, col), true);
   }
 }
 
@@ -1195,14 +1286,18 @@ TG_HD void eval_rom(const Ctx& c, const ItemDesc& it, Emit& em) {
     }
   } else {
     spline_basis(P, kPos, H);
+    #pragma unroll
     for (int r = 0; r < 3; ++r)
+      #pragma unroll
       for (int e = 0; e < 3; ++e) emit_dim(c, em, r0 + r, sp_motion(ee), P, H, e, R[e][r]);
     if (c.gait) {   // b_R_w * d pos / d schedule (range_of_motion_constraint.cc:123-130)
       SchedJac Jx;
       sched_jac(c, sp_motion(ee), t, P, Jx);
+      #pragma unroll
       for (int r = 0; r < 3; ++r)
-        for (int col = 0; col < Jx.n - 1; ++col)
-          em(r0 + r, Jx.col0 + col, R[0][r] * sched_val(Jx, 0, col) + R[1][r] * sched_val(Jx, 1, col) + R[2][r] * sched_val(Jx, 2, col), true);
+        if (em_wants(em, r0 + r))
+          for (int col = 0; col < Jx.n - 1; ++col)
+            em(r0 + r, Jx.col0 + col, R[0][r] * sched_val(Jx, 0, col) + R[1][r] * sched_val(Jx, 1, col) + R[2][r] * sched_val(Jx, 2, col), true);
     }
   }
 }
@@ -1223,17 +1318,21 @@ TG_HD void eval_fdisc(const Ctx& c, const ItemDesc& it, Emit& em) {
   for (int i = 0; i < 5; ++i) em.g(r0 + i, dot3(F.p, b[i]));
   double H[4];
   spline_basis(F, kPos, H);
+  #pragma unroll
   for (int i = 0; i < 5; ++i)
+    #pragma unroll
     for (int e = 0; e < 3; ++e) emit_dim(c, em, r0 + i, sp_force(ee), F, H, e, b[i][e]);
   double sc[2][5] = {{0, 0, 0, 0, 0}, {0, 0, 0, 0, 0}};   // F . d(pyramid)/d p_dim
   if (c.fdisc_motion) {   // AccumulateScaledRowJacobian: skipped when scale == 0.0 (:58)
     spline_basis(P, kPos, H);
+    #pragma unroll
     for (int dim = 0; dim < 2; ++dim) {
       double dn[3], dt1[3], dt2[3], db[5][3];
       ter_d_nbasis(*c.ter, 0, dim, P.p[0], P.p[1], dn);
       ter_d_nbasis(*c.ter, 1, dim, P.p[0], P.p[1], dt1);
       ter_d_nbasis(*c.ter, 2, dim, P.p[0], P.p[1], dt2);
       pyramid(dn, dt1, dt2, mu, db);
+      #pragma unroll
       for (int i = 0; i < 5; ++i) {
         sc[dim][i] = dot3(F.p, db[i]);
         emit_dim(c, em, r0 + i, sp_motion(ee), P, H, dim, sc[dim][i], sc[dim][i] != 0.0);
@@ -1244,8 +1343,10 @@ TG_HD void eval_fdisc(const Ctx& c, const ItemDesc& it, Emit& em) {
     SchedJac Jf, Jx;
     sched_jac(c, sp_force(ee), t, F, Jf);
     sched_jac(c, sp_motion(ee), t, P, Jx);
+    #pragma unroll
     for (int i = 0; i < 5; ++i)
-      for (int col = 0; col < Jf.n - 1; ++col) {
+      if (em_wants(em, r0 + i))
+        for (int col = 0; col < Jf.n - 1; ++col) {
         double v = b[i][0] * sched_val(Jf, 0, col) + b[i][1] * sched_val(Jf, 1, col) + b[i][2] * sched_val(Jf, 2, col);
         if (sc[0][i] != 0.0) v += sc[0][i] * sched_val(Jx, 0, col);
         if (sc[1][i] != 0.0) v += sc[1][i] * sched_val(Jx, 1, col);
@@ -1377,14 +1478,19 @@ TG_HD void eval_tqdisc(const Ctx& c, const ItemDesc& it, Emit& em) {
   const double* tb[4] = {t1, t2, n, mn};
   double H[4];
   spline_basis(Tq, kPos, H);   // AccumulateLinearFormJacobian of the torque spline
+  #pragma unroll
   for (int r = 0; r < 4; ++r)
+    #pragma unroll
     for (int e = 0; e < 3; ++e) emit_dim(c, em, r0 + r, sp_torque(ee), Tq, H, e, tb[r][e]);
   spline_basis(F, kPos, H);    // ... of the force spline into the two normal-torque rows
+  #pragma unroll
   for (int r = 2; r < 4; ++r)
+    #pragma unroll
     for (int e = 0; e < 3; ++e) emit_dim(c, em, r0 + r, sp_force(ee), F, H, e, b[e]);
   double sc[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};   // d rows / d p_dim through the terrain basis
   if (c.fdisc_motion) {   // AccumulateScaledRowJacobian: skipped when scale == 0.0 (:58)
     spline_basis(P, kPos, H);
+    #pragma unroll
     for (int dim = 0; dim < 2; ++dim) {
       double dn[3], dt1[3], dt2[3];
       ter_d_nbasis(*c.ter, 0, dim, P.p[0], P.p[1], dn);
@@ -1395,6 +1501,7 @@ TG_HD void eval_tqdisc(const Ctx& c, const ItemDesc& it, Emit& em) {
       sc[dim][1] = dot3(Tq.p, dt2);
       sc[dim][2] = s_tau_n - s_lim;
       sc[dim][3] = -s_tau_n - s_lim;
+      #pragma unroll
       for (int r = 0; r < 4; ++r) emit_dim(c, em, r0 + r, sp_motion(ee), P, H, dim, sc[dim][r], sc[dim][r] != 0.0);
     }
   }
@@ -1403,8 +1510,10 @@ TG_HD void eval_tqdisc(const Ctx& c, const ItemDesc& it, Emit& em) {
     sched_jac(c, sp_torque(ee), t, Tq, Jt);
     sched_jac(c, sp_force(ee), t, F, Jf);
     sched_jac(c, sp_motion(ee), t, P, Jx);
+    #pragma unroll
     for (int r = 0; r < 4; ++r)
-      for (int col = 0; col < Jt.n - 1; ++col) {
+      if (em_wants(em, r0 + r))
+        for (int col = 0; col < Jt.n - 1; ++col) {
         double v = tb[r][0] * sched_val(Jt, 0, col) + tb[r][1] * sched_val(Jt, 1, col) + tb[r][2] * sched_val(Jt, 2, col);
         if (r >= 2) v += b[0] * sched_val(Jf, 0, col) + b[1] * sched_val(Jf, 1, col) + b[2] * sched_val(Jf, 2, col);
         if (sc[0][r] != 0.0) v += sc[0][r] * sched_val(Jx, 0, col);

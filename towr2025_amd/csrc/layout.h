@@ -91,11 +91,24 @@ constexpr int kTileRowCap = 2048;
 constexpr int kMiscValueCap = 3072;   // small-kind tiles: 4 share one block's LDS
 constexpr int kMiscRowCap = 512;
 
+// LDS tile value cap under phase-duration optimisation: the block also stages the PhaseSpline tables
+// and their timings (GaitTables), and the tile + x + node table + tables must stay within 80 KB
+// for 2 blocks per CU
+constexpr int kTileValueCapGait = 4864;
+
+// Row-split items (phase-duration optimisation only). A PhaseSpline item emits its full-pattern
+// windows and schedule columns one candidate at a time, a chain of dependent slot-table and
+// PhaseCol loads; one item per instant would leave a tile of ~20 instants on 20 lanes of a 192-lane
+// block. Such items are split into one lane per row (ItemDesc::rsel): every lane evaluates the
+// instant, only its row's candidates are emitted. Returns the rows per lane split (1 = not split).
+int split_rows(int type, int group, bool gait);
+
 // Launch geometry of each item type (wave-uniform: each wave of a block runs one code path)
 struct TypeSpec { int block; int max_inst; };
-TypeSpec type_spec(int type, int n_ee);
-// thread (lane) of the block that evaluates group `g` of the k-th of n instances in a tile
-int type_lane(int type, int group, int k, int n, int n_ee);
+TypeSpec type_spec(int type, int n_ee, bool gait);
+// thread (lane) of the block that evaluates row-part `sub` (0 .. split_rows - 1) of group `g` of
+// the k-th of n instances in a tile
+int type_lane(int type, int group, int k, int n, int n_ee, bool gait, int sub);
 
 // Returns TOWR_OK or an error code with a message in `err`.
 int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err);

@@ -146,7 +146,12 @@ struct RecordEmit {
   int g_rows_lo = 0, g_rows_hi = 0;
   bool bad_g = false;
   void g(int row, double) { if (row < g_rows_lo || row >= g_rows_hi) bad_g = true; }
+  // row-split items (ItemDesc::rsel): only the selected row's candidates, as the kernel's TileEmit
+  int frow = -1;
+  static constexpr bool kFilter = true;
+  bool want(int row) const { return frow < 0 || row == frow; }
   void operator()(int row, int col, double, bool pres) {
+    if (!want(row)) return;
     rows->push_back(row); cols->push_back(col); present->push_back(pres && col >= 0 ? 1 : 0);
   }
 };
@@ -525,7 +530,11 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
     auto add = [&](int type, int group, int ee, int k, int row0, double t, int a0, int a1, double p0) {
       ItemDesc it{}; it.type = type; it.group = group; it.ee = ee; it.k = k; it.row0 = row0; it.seg = -1;
       it.t = t; it.a0 = a0; it.a1 = a1; it.p0 = p0;
-      L.items.push_back(it); item_inst.push_back(inst);
+      const int S = split_rows(type, group, L.gait);   // one lane per row of a PhaseSpline item
+      for (int r = 0; r < S; ++r) {
+        it.rsel = S > 1 ? r + 1 : 0;
+        L.items.push_back(it); item_inst.push_back(inst);
+      }
     };
     const bool timed = c.kind == TOWR_C_DYNAMIC || c.kind == TOWR_C_RANGE_OF_MOTION ||
                        c.kind == TOWR_C_FORCE_DISCRETIZED || c.kind == TOWR_C_BASE_MOTION ||
@@ -697,6 +706,7 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
       item_cand_begin[i] = (int32_t)crow.size();
       RecordEmit em{&crow, &ccol, &cpres};
       em.g_rows_lo = L.items[i].row0; em.g_rows_hi = L.items[i].row0 + item_rows(L.items[i].type);
+      em.frow = L.items[i].rsel > 0 ? L.items[i].row0 + L.items[i].rsel - 1 : -1;
       cx.seg = L.items[i].seg >= 0 ? L.segs.data() + (size_t)L.items[i].seg * L.spl.size() : nullptr;
       eval_item(cx, L.items[i], em);
       if (em.bad_g) { err = "internal: item wrote g outside its rows"; return TOWR_ERR_INVALID; }
@@ -770,7 +780,7 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
         insts.push_back({(int32_t)j, (int32_t)(k - j)});
         j = k;
       }
-      const TypeSpec sp = type_spec(type, E);
+      const TypeSpec sp = type_spec(type, E, L.gait);
       const int n_inst = (int)insts.size();
       auto inst_rows = [&](int a, int b) {   // rows of instances [a, b)
         const int r0 = L.items[insts[a].first].row0;
@@ -784,7 +794,7 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
           const int a = (int)((int64_t)t * n_inst / n_tiles), b = (int)((int64_t)(t + 1) * n_inst / n_tiles);
           if (b <= a) continue;
           auto rr = inst_rows(a, b);
-          const int vcap = is_misc_kind(type) ? kMiscValueCap : kTileValueCap, rcap = is_misc_kind(type) ? kMiscRowCap : kTileRowCap;
+          const int vcap = is_misc_kind(type) ? kMiscValueCap : L.gait ? kTileValueCapGait : kTileValueCap, rcap = is_misc_kind(type) ? kMiscRowCap : kTileRowCap;
           if (L.row_ptr[rr.second] - L.row_ptr[rr.first] > vcap || rr.second - rr.first > rcap) ok = false;
         }
         if (ok) break;
@@ -803,7 +813,7 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
         for (int k = a; k < b; ++k)
           for (int q = 0; q < insts[k].count; ++q) {
             const ItemDesc& it = L.items[insts[k].first + q];
-            const int lane = type_lane(type, it.group, k - a, b - a, E);
+            const int lane = type_lane(type, it.group, k - a, b - a, E, L.gait, it.rsel > 0 ? it.rsel - 1 : 0);
             if (lane < 0 || lane >= sp.block || lanes[lane].type != IT_NONE) { err = "internal: lane assignment"; return TOWR_ERR_INVALID; }
             lanes[lane] = it;
             if (type == IT_DYN) lanes[lane].a2 = k - a;   // instant within the tile (LDS sum terms)
@@ -827,14 +837,14 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
         L.tiles.push_back(td);
       }
       items.insert(items.end(), per_type_items[t].begin(), per_type_items[t].end());
-      L.type_block[t] = type_spec(t, E).block;
+      L.type_block[t] = type_spec(t, E, L.gait).block;
       // LDS: [tile values | 64 dummy slots (absent candidates, by wave lane) | g rows]
       L.type_lds_dummy_off[t] = (maxv + 1) & ~1;
       L.type_lds_rows_off[t] = L.type_lds_dummy_off[t] + 64;   // one per wave lane: waves never collide within an instruction
       L.type_lds[t] = L.type_lds_rows_off[t] + ((maxr + 1) & ~1);
       if (t == IT_DYN) {   // + per-instant endeffector sum terms (dyn_g0_a)
         L.dyn_scr_off = L.type_lds[t];
-        L.type_lds[t] += type_spec(IT_DYN, E).max_inst * E * 6;
+        L.type_lds[t] += type_spec(IT_DYN, E, L.gait).max_inst * E * 6;
       }
     }
     L.type_tile0[IT_COUNT] = (int32_t)L.tiles.size();
@@ -847,7 +857,7 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
       int stride[IT_COUNT] = {}, rows_off[IT_COUNT] = {};
       for (int t = 0; t < IT_COUNT; ++t) {
         if (!is_misc_kind(t)) continue;
-        if (type_spec(t, E).block != 64) { err = "internal: small kinds must use one-wave tiles"; return TOWR_ERR_INVALID; }
+        if (type_spec(t, E, L.gait).block != 64) { err = "internal: small kinds must use one-wave tiles"; return TOWR_ERR_INVALID; }
         int mv = 0, mr = 0;
         for (int ti = L.type_tile0[t]; ti < L.type_tile0[t + 1]; ++ti) {
           mt.push_back(ti);
@@ -931,20 +941,34 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
   return TOWR_OK;
 }
 
-TypeSpec type_spec(int type, int n_ee) {
+int split_rows(int type, int group, bool gait) {
+  if (!gait) return 1;
   switch (type) {
-    case IT_DYN: return {256, std::max(1, std::min(64, 128 / std::max(1, n_ee)))};  // waves: g0 | g1 | ee, ee
-    case IT_ROM: return {192, 64};                                                      // waves: g0 | g1 | g2
-    case IT_FDISC: return {192, 192};
-    case IT_TQDISC: return {192, 192};
+    case IT_DYN: return group >= 2 ? 6 : 1;   // the endeffector groups (force / torque / motion PhaseSplines)
+    case IT_ROM: return group == 2 ? 3 : 1;   // the endeffector-motion group
+    case IT_FDISC: return 5;
+    case IT_TQDISC: return 4;
+    default: return 1;
+  }
+}
+
+TypeSpec type_spec(int type, int n_ee, bool gait) {
+  const int E = std::max(1, n_ee);
+  switch (type) {
+    case IT_DYN:   // waves: g0 | g1 | ee, ee (split: 6 lanes per ee instant)
+      return {256, std::max(1, std::min(64, 128 / (E * split_rows(IT_DYN, 2, gait))))};
+    case IT_ROM: return {192, 64 / split_rows(IT_ROM, 2, gait)};                         // waves: g0 | g1 | g2
+    case IT_FDISC: return {192, 192 / split_rows(IT_FDISC, 0, gait)};
+    case IT_TQDISC: return {192, 192 / split_rows(IT_TQDISC, 0, gait)};
     default: return {64, 64};
   }
 }
 
-int type_lane(int type, int group, int k, int n, int n_ee) {
-  if (type == IT_DYN) return group == 0 ? k : group == 1 ? 64 + k : 128 + (group - 2) * n + k;
-  if (type == IT_ROM) return 64 * group + k;
-  return k;
+int type_lane(int type, int group, int k, int n, int n_ee, bool gait, int sub) {
+  const int S = split_rows(type, group, gait);
+  if (type == IT_DYN) return group == 0 ? k : group == 1 ? 64 + k : 128 + ((group - 2) * n + k) * S + sub;
+  if (type == IT_ROM) return 64 * group + k * S + sub;
+  return k * S + sub;
 }
 
 int initial_x_for(const towr_problem_desc_t& d, const towr_init_t& init, const towr_terrain_t& ter,

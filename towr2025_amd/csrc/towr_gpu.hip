@@ -47,6 +47,9 @@ struct KParams {
   const int32_t* pact;
   const SchedInfo* sched;
   const EELinDef* eelin;
+  const uint4* gtab;             // GAIT: the PhaseSpline tables in one blob (GaitTables), staged per tile block
+  int32_t gt_off[5], gt_n16;
+  int32_t n_pinfo, ph_stride;    // GAIT: the block's PhaseSpline timings (Ctx::pdur / pend / phend)
   int32_t n_spl;
   const towr_terrain_t* terrains;
   int32_t terrain_per_problem;
@@ -74,13 +77,18 @@ struct KParams {
 // candidates of arithmetic. The candidate's column is never needed on the device, and no item emits
 // a column twice (engine_math.h), so every position receives exactly one plain LDS store; absent
 // candidates (constant node values) go to a per-lane dummy slot, so the store needs no branch.
-template <int BLOCK, int DEPTH>
+// FILTER (phase-duration optimisation): the lane's item may be row-split (ItemDesc::rsel); only row
+// frow's candidates are emitted (and counted), exactly as the structure pass recorded them.
+template <int BLOCK, int DEPTH, bool FILTER = false>
 struct TileEmit {
   const SlotGroup* slot;   // this lane's group 0; group g at slot[g * BLOCK]
   double* out;             // LDS tile, tile-relative
   double* gout;            // LDS g rows, tile-relative
   SlotGroup q[DEPTH];      // groups g .. g + DEPTH - 1 in flight (q[0] = current)
   int j = 0;
+  int frow = -1;           // FILTER: the selected row, or -1 = all rows
+  static constexpr bool kFilter = FILTER;
+  __device__ __forceinline__ bool want(int row) const { return !FILTER || frow < 0 || row == frow; }
   __device__ __forceinline__ TileEmit(const SlotGroup* s, double* o, double* go) : slot(s), out(o), gout(go) {
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d) q[d] = s[d * BLOCK];
@@ -99,7 +107,9 @@ struct TileEmit {
       for (int d = 0; d < DEPTH; ++d) q[d] = slot[(g1 + d) * BLOCK];
     }
   }
-  __device__ __forceinline__ void operator()(int, int, double v, bool) {
+  __device__ __forceinline__ void operator()(int row, int, double v, bool) {
+    if constexpr (FILTER)
+      if (!want(row)) return;
 #ifdef TOWR_EXPERIMENT_NOSLOT   // timing experiment only: wrong positions, no slot-table traffic
     out[(threadIdx.x * 7 + j++) & 1023] = v;
 #else
@@ -330,12 +340,15 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
   } else {
     it = ItemDesc{}; it.type = IT_NONE; it.slot = 0;
   }
-  TileEmit<TBLOCK, slot_depth(TYPE)> em(P.slots + it.slot, smem, smem + lds_rows_off - T.r0);
+  TileEmit<TBLOCK, slot_depth(TYPE), GAIT> em(P.slots + it.slot, smem, smem + lds_rows_off - T.r0);
+  if constexpr (GAIT) em.frow = it.rsel > 0 ? it.row0 + it.rsel - 1 : -1;
   double* xs = smem + lds_x_off;
   int32_t* ns = reinterpret_cast<int32_t*>(smem + lds_x_off + P.n_pad);
+  char* gt = reinterpret_cast<char*>(smem + lds_x_off + P.n_pad + ((P.n_nodecol + 3) >> 2) * 2);   // GAIT tables
   if constexpr (GAIT) zero_lds(smem, T.v1 - T.v0, threadIdx.x, KBLOCK);   // sparse PhaseSpline emission
   if constexpr (early_stage(TYPE)) xst.commit(P, xg, xs, ns);
   else stage_x<KBLOCK, stages_nodes(TYPE, GAIT)>(P, xg, xs, ns);
+  if constexpr (GAIT) stage16<KBLOCK>(reinterpret_cast<uint4*>(gt), P.gtab, P.gt_n16);
   __syncthreads();
 #ifdef TOWR_PHASE_TIMING
   if (threadIdx.x < 64) TSTAMP(2, TS_MEM());
@@ -346,8 +359,28 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
   c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
   c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
   c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.pact = P.pact; c.sched = P.sched; c.eelin = P.eelin;
+  if constexpr (GAIT) {   // the PhaseSpline searches and window emission read their tables from LDS
+    c.spl = reinterpret_cast<const SplineMeta*>(gt + P.gt_off[0]);
+    c.sched = reinterpret_cast<const SchedInfo*>(gt + P.gt_off[1]);
+    c.pinfo = reinterpret_cast<const PolyPhase*>(gt + P.gt_off[2]);
+    c.pact = reinterpret_cast<const int32_t*>(gt + P.gt_off[3]);
+    c.pcols = reinterpret_cast<const PhaseCol*>(gt + P.gt_off[4]);
+  }
   c.rotvec = ROTVEC;
   c.dyn_scratch = TYPE == IT_DYN ? smem + P.lds_scr_off : nullptr;
+  if constexpr (GAIT) {
+    // the x-dependent PhaseSpline timings once per block (one thread per spline / endeffector)
+    // instead of a division-carrying scan per lane and spline evaluation
+    double* tm = reinterpret_cast<double*>(gt + 16 * P.gt_n16);
+    const int tid = threadIdx.x, nspl = P.n_spl, nee = P.rb.n_ee;
+    if (tid < nspl) {
+      if (c.spl[tid].ee >= 0) phase_spline_timings(c, tid, tm, tm + P.n_pinfo);
+    } else if (tid < nspl + nee) {
+      if (c.sched[tid - nspl].col0 >= 0) phase_end_timings(c, tid - nspl, tm + 2 * P.n_pinfo + (tid - nspl) * P.ph_stride);
+    }
+    __syncthreads();
+    c.pdur = tm; c.pend = tm + P.n_pinfo; c.phend = tm + 2 * P.n_pinfo; c.ph_stride = P.ph_stride;
+  }
   DynG0 g0;   // DYN group 0 between its two phases
   if (it.type == TYPE) {
     if constexpr (TYPE == IT_DYN) {
@@ -672,6 +705,7 @@ struct towr_gpu_handle_s {
   int32_t* d_misc = nullptr;
   int32_t* d_misc_lds = nullptr;
   EELinDef* d_eelin = nullptr;
+  uint4* d_gtab = nullptr;     // GAIT: PhaseSpline tables blob (GaitTables)
   CostItem* d_citems = nullptr;
   double* d_cq = nullptr;
   // fusion groups (TOWR_GPU_FUSE, see towr_step_kernel): classes that run in one launch
@@ -740,12 +774,45 @@ int bind(towr_gpu_handle h) {
   return TOWR_OK;
 }
 
-// LDS of a launch class: [tile region(s) | x + zero slot | node table]
+// The PhaseSpline tables a tile block stages in LDS under phase-duration optimisation, as one blob of
+// 16-byte aligned sections [SplineMeta | SchedInfo | PolyPhase | pact | PhaseCol] (~18 KB for ANYmal):
+// the device-side duration searches (phase_spline_locate, sched_jac) and the full-pattern window
+// emission (emit_dim) walk them in dependent loads, ~10x cheaper from LDS than from L2.
+// Behind the tables, each block computes the x-dependent timings of Ctx::pdur / pend / phend
+// (n_time doubles: 2 per PolyPhase entry + ph_stride per endeffector).
+struct GaitTables { int32_t off[5]; int32_t n16; int32_t n_time, ph_stride; };
+GaitTables gait_tables(const Layout& L) {
+  GaitTables g{};
+  for (const SchedInfo& si : L.sched) g.ph_stride = std::max(g.ph_stride, (int32_t)si.n_phases);
+  g.n_time = L.gait ? (int32_t)(2 * L.pinfo.size() + L.sched.size() * g.ph_stride) : 0;
+  const size_t sz[5] = {sizeof(SplineMeta) * L.spl.size(), sizeof(SchedInfo) * L.sched.size(), sizeof(PolyPhase) * L.pinfo.size(),
+                        sizeof(int32_t) * L.pact.size(), sizeof(PhaseCol) * L.pcols.size()};
+  size_t o = 0;
+  for (int k = 0; k < 5; ++k) { g.off[k] = (int32_t)o; o += (sz[k] + 15) & ~(size_t)15; }
+  g.n16 = L.gait ? (int32_t)(o / 16) : 0;
+  return g;
+}
+std::vector<uint4> gait_blob(const Layout& L) {
+  const GaitTables g = gait_tables(L);
+  std::vector<uint4> b((size_t)std::max(1, g.n16));
+  std::memset(b.data(), 0, b.size() * sizeof(uint4));
+  char* p = reinterpret_cast<char*>(b.data());
+  if (g.n16 == 0) return b;
+  std::memcpy(p + g.off[0], L.spl.data(), sizeof(SplineMeta) * L.spl.size());
+  std::memcpy(p + g.off[1], L.sched.data(), sizeof(SchedInfo) * L.sched.size());
+  std::memcpy(p + g.off[2], L.pinfo.data(), sizeof(PolyPhase) * L.pinfo.size());
+  std::memcpy(p + g.off[3], L.pact.data(), sizeof(int32_t) * L.pact.size());
+  std::memcpy(p + g.off[4], L.pcols.data(), sizeof(PhaseCol) * L.pcols.size());
+  return b;
+}
+
+// LDS of a launch class: [tile region(s) | x + zero slot | node table | GAIT: PhaseSpline tables]
 size_t lds_region(const Layout& L, int lc) { return lc == LC_MISC ? (size_t)((L.misc_region + 1) & ~1) : (size_t)L.type_lds[class_type(lc)]; }
 size_t lds_bytes(const Layout& L, int lc) {
   size_t d = lds_region(L, lc);
   d += (size_t)((L.n + 2) & ~1);                                                                  // x + zero slot
   if (lc == LC_MISC || stages_nodes(class_type(lc), L.gait)) d += (L.nodecol.size() + 3) / 4 * 2;  // node table (16-B units)
+  if (lc != LC_MISC && L.gait) d += (size_t)gait_tables(L).n16 * 2 + gait_tables(L).n_time;         // PhaseSpline tables, timings
   return sizeof(double) * d;
 }
 int class_units(const Layout& L, int lc) {   // tiles (or misc groups) per problem
@@ -824,6 +891,12 @@ void fill_common(towr_gpu_handle h, KParams& P, int B, const double* X, int64_t 
   P.rb = L.rb;
   P.misc_tiles = h->d_misc; P.misc_lds = h->d_misc_lds;
   P.lds_scr_off = L.dyn_scr_off;
+  const GaitTables gt = gait_tables(L);
+  P.gtab = h->d_gtab;
+  for (int k = 0; k < 5; ++k) P.gt_off[k] = gt.off[k];
+  P.gt_n16 = gt.n16;
+  P.n_pinfo = (int32_t)L.pinfo.size();
+  P.ph_stride = gt.ph_stride;
 }
 
 int launch_fused(towr_gpu_handle h, const towr_gpu_handle_s::FuseGroup& fg, int B, const double* X, int64_t ldx, double* G,
@@ -868,13 +941,8 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
     const int nt = class_units(L, lc);
     const hipStream_t st = (nside > 0 && q % (nside + 1) != 0) ? h->side[q % (nside + 1) - 1] : s;
     KParams P{};
-    P.X = X; P.ldx = ldx; P.G = G; P.ldg = ldg; P.V = V; P.ldv = ldv;
-    P.items = h->d_items; P.slots = h->d_slots; P.tiles = h->d_tiles;
-    P.nodecol = h->d_nodecol; P.spl = h->d_spl; P.dur = h->d_dur;
-    P.sg = h->sg; P.n_spl = (int32_t)L.spl.size();
-    P.pinfo = h->d_pinfo; P.pcols = h->d_pcols; P.pact = h->d_pact; P.sched = h->d_sched; P.eelin = h->d_eelin;
-    P.terrains = terrains; P.terrain_per_problem = per_problem;
-    P.B = B; P.ntiles = nt;
+    fill_common(h, P, B, X, ldx, G, ldg, V, ldv, want_g, want_jac, terrains, per_problem);
+    P.ntiles = nt;
     if (lc == LC_MISC) {
       P.tile0 = 0;
       P.misc_tiles = h->d_misc; P.misc_lds = h->d_misc_lds;
@@ -1114,7 +1182,7 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
       (r = upload(h, &h->d_spl, L.spl)) || (r = upload(h, &h->d_dur, L.dur)) || (r = upload(h, &h->d_terrain, ter)) ||
       (r = upload(h, &h->d_pinfo, L.pinfo)) || (r = upload(h, &h->d_pcols, L.pcols)) || (r = upload(h, &h->d_pact, L.pact)) || (r = upload(h, &h->d_sched, L.sched)) ||
       (r = upload(h, &h->d_misc, L.misc_tiles)) || (r = upload(h, &h->d_misc_lds, L.misc_lds)) || (r = upload(h, &h->d_eelin, L.eelin)) ||
-      (r = upload(h, &h->d_citems, L.cost_items)) || (r = upload(h, &h->d_cq, L.cost_q)))
+      (r = upload(h, &h->d_citems, L.cost_items)) || (r = upload(h, &h->d_cq, L.cost_q)) || (r = upload(h, &h->d_gtab, gait_blob(L))))
     return bail(r);
   {   // trajectory export: phase durations of the description (fixed gait), counts, contact at start
     const towr_problem_desc_t& d = L.desc;
@@ -1199,7 +1267,7 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
 int towr_gpu_destroy(towr_gpu_handle h) {
   if (!h) return TOWR_OK;
   void* dev[] = {h->d_items, h->d_slots, h->d_tiles, h->d_nodecol, h->d_spl, h->d_dur, h->d_segs, h->d_terrain,
-                 h->d_pinfo, h->d_pcols, h->d_pact, h->d_sched, h->d_misc, h->d_misc_lds, h->d_eelin, h->d_citems, h->d_cq, h->fuse[0].d_units, h->fuse[1].d_units,
+                 h->d_pinfo, h->d_pcols, h->d_pact, h->d_sched, h->d_misc, h->d_misc_lds, h->d_eelin, h->d_gtab, h->d_citems, h->d_cq, h->fuse[0].d_units, h->fuse[1].d_units,
                  h->d_bterrain, h->d_x, h->d_g, h->d_v, h->d_f, h->d_grad,
                  h->d_traj_pd, h->d_traj_n, h->d_traj_c0, h->d_traj_t};
   if (h->device >= 0) for (void* p : dev) if (p) (void)hipFree(p);
