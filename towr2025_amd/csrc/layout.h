@@ -91,10 +91,10 @@ constexpr int kTileRowCap = 2048;
 constexpr int kMiscValueCap = 3072;   // small-kind tiles: 4 share one block's LDS
 constexpr int kMiscRowCap = 512;
 
-// LDS tile value cap under phase-duration optimisation: the block also stages the PhaseSpline tables
-// and their timings (GaitTables), and the tile + x + node table + tables must stay within 80 KB
-// for 2 blocks per CU
-constexpr int kTileValueCapGait = 4864;
+// Tile value cap under phase-duration optimisation: the tile classes have no LDS tile there (they
+// store straight into a zero-filled V, TileEmit DIRECT), so a tile is bounded only by its lanes and
+// the uint16 slot positions (values + 64 dummy slots < kSlotAbsent)
+constexpr int kTileValueCapGait = 65536 - 2 - 64 - 2;
 
 // Row-split items (phase-duration optimisation only). A PhaseSpline item emits its full-pattern
 // windows and schedule columns one candidate at a time, a chain of dependent slot-table and
@@ -102,6 +102,16 @@ constexpr int kTileValueCapGait = 4864;
 // block. Such items are split into one lane per row (ItemDesc::rsel): every lane evaluates the
 // instant, only its row's candidates are emitted. Returns the rows per lane split (1 = not split).
 int split_rows(int type, int group, bool gait);
+
+// Block size of the tile classes. Under phase-duration optimisation every wave holds one row of
+// the split items (lanes = instants), so that a wave's lanes take the same branches: a wave mixing
+// the rows of an item would execute every row's emission path one after the other.
+//   DYN: g0 | g1 | row 0 .. 5 of the endeffector groups (lanes = ee x instant);
+//   ROM: g0 | g1 | row 0 .. 2 of the motion group;  FDISC: rows 0 .. 4;  TQDISC: rows 0 .. 3.
+constexpr int tile_block(int type, bool gait) {
+  return type == IT_DYN ? (gait ? 512 : 256) : type == IT_ROM ? (gait ? 320 : 192) : type == IT_FDISC ? (gait ? 320 : 192)
+       : type == IT_TQDISC ? (gait ? 256 : 192) : 64;
+}
 
 // Launch geometry of each item type (wave-uniform: each wave of a block runs one code path)
 struct TypeSpec { int block; int max_inst; };

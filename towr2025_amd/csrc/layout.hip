@@ -842,6 +842,10 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
       L.type_lds_dummy_off[t] = (maxv + 1) & ~1;
       L.type_lds_rows_off[t] = L.type_lds_dummy_off[t] + 64;   // one per wave lane: waves never collide within an instruction
       L.type_lds[t] = L.type_lds_rows_off[t] + ((maxr + 1) & ~1);
+      if (L.gait && !is_misc_kind(t)) {   // no LDS tile (TileEmit DIRECT): positions only encode absence
+        L.type_lds_rows_off[t] = 0;
+        L.type_lds[t] = 0;
+      }
       if (t == IT_DYN) {   // + per-instant endeffector sum terms (dyn_g0_a)
         L.dyn_scr_off = L.type_lds[t];
         L.type_lds[t] += type_spec(IT_DYN, E, L.gait).max_inst * E * 6;
@@ -954,21 +958,24 @@ int split_rows(int type, int group, bool gait) {
 
 TypeSpec type_spec(int type, int n_ee, bool gait) {
   const int E = std::max(1, n_ee);
+  const int blk = tile_block(type, gait);
   switch (type) {
-    case IT_DYN:   // waves: g0 | g1 | ee, ee (split: 6 lanes per ee instant)
-      return {256, std::max(1, std::min(64, 128 / (E * split_rows(IT_DYN, 2, gait))))};
-    case IT_ROM: return {192, 64 / split_rows(IT_ROM, 2, gait)};                         // waves: g0 | g1 | g2
-    case IT_FDISC: return {192, 192 / split_rows(IT_FDISC, 0, gait)};
-    case IT_TQDISC: return {192, 192 / split_rows(IT_TQDISC, 0, gait)};
+    case IT_DYN: return {blk, std::max(1, std::min(64, gait ? 64 / E : 128 / E))};   // waves: g0 | g1 | ee, ee (gait: rows)
+    case IT_ROM: return {blk, 64};                                                      // waves: g0 | g1 | g2 (gait: rows)
+    case IT_FDISC: case IT_TQDISC: return {blk, gait ? 64 : blk};
     default: return {64, 64};
   }
 }
 
 int type_lane(int type, int group, int k, int n, int n_ee, bool gait, int sub) {
-  const int S = split_rows(type, group, gait);
-  if (type == IT_DYN) return group == 0 ? k : group == 1 ? 64 + k : 128 + ((group - 2) * n + k) * S + sub;
-  if (type == IT_ROM) return 64 * group + k * S + sub;
-  return k * S + sub;
+  if (gait && split_rows(type, group, gait) > 1) {   // one wave per row (tile_block)
+    if (type == IT_DYN) return 64 * (2 + sub) + (group - 2) * n + k;
+    if (type == IT_ROM) return 64 * (2 + sub) + k;
+    return 64 * sub + k;
+  }
+  if (type == IT_DYN) return group == 0 ? k : group == 1 ? 64 + k : 128 + (group - 2) * n + k;
+  if (type == IT_ROM) return 64 * group + k;
+  return k;
 }
 
 int initial_x_for(const towr_problem_desc_t& d, const towr_init_t& init, const towr_terrain_t& ter,

@@ -77,24 +77,35 @@ struct KParams {
 // candidates of arithmetic. The candidate's column is never needed on the device, and no item emits
 // a column twice (engine_math.h), so every position receives exactly one plain LDS store; absent
 // candidates (constant node values) go to a per-lane dummy slot, so the store needs no branch.
-// FILTER (phase-duration optimisation): the lane's item may be row-split (ItemDesc::rsel); only row
-// frow's candidates are emitted (and counted), exactly as the structure pass recorded them.
-template <int BLOCK, int DEPTH, bool FILTER = false>
+// DIRECT (phase-duration optimisation): there is no LDS tile. The full-pattern Jacobian is ~90 %
+// zeros whose positions move with x, and an LDS tile of it held ~13 instants per block (one busy wave
+// of three, 2 blocks per CU), so the launch was bound by the evaluation's latency at low occupancy.
+// Instead V is zero-filled by a streaming memset before the launch (launch()), and lanes store their
+// present candidates straight to HBM: `out` is the tile's first CSR value in V, `gout` the problem's g,
+// absent candidates (positions >= nvals, the dummy slots) are not stored. The lane's item may be
+// row-split (ItemDesc::rsel): only row frow's candidates are emitted (and counted), exactly as the
+// structure pass recorded them, and only that row's g.
+template <int BLOCK, int DEPTH, bool DIRECT = false>
 struct TileEmit {
   const SlotGroup* slot;   // this lane's group 0; group g at slot[g * BLOCK]
-  double* out;             // LDS tile, tile-relative
-  double* gout;            // LDS g rows, tile-relative
+  double* out;             // LDS tile, tile-relative (DIRECT: V at the tile's first value)
+  double* gout;            // LDS g rows, tile-relative (DIRECT: the problem's g)
   SlotGroup q[DEPTH];      // groups g .. g + DEPTH - 1 in flight (q[0] = current)
   int j = 0;
-  int frow = -1;           // FILTER: the selected row, or -1 = all rows
-  static constexpr bool kFilter = FILTER;
-  __device__ __forceinline__ bool want(int row) const { return !FILTER || frow < 0 || row == frow; }
+  int frow = -1;           // DIRECT: the selected row, or -1 = all rows
+  int nvals = 0;           // DIRECT: values of the tile
+  static constexpr bool kFilter = DIRECT;
+  __device__ __forceinline__ bool want(int row) const { return !DIRECT || frow < 0 || row == frow; }
   __device__ __forceinline__ TileEmit(const SlotGroup* s, double* o, double* go) : slot(s), out(o), gout(go) {
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d) q[d] = s[d * BLOCK];
   }
-  __device__ __forceinline__ void g(int row, double v) { gout[row] = v; }
-  // GAIT tiles are zero-filled before the evaluation (tile_body / misc_body), so candidates whose
+  bool gon = true;         // DIRECT: g requested
+  __device__ __forceinline__ void g(int row, double v) {
+    if (!DIRECT) gout[row] = v;
+    else if (gon && want(row)) gout[row] = v;
+  }
+  // GAIT outputs are zero-filled before the evaluation (launch() / misc_body), so candidates whose
   // value is 0 can be skipped: move to candidate j + k, reloading the slot ring if the group changes
   static constexpr bool kSparse = true;
   __device__ __forceinline__ void skip(int k) {
@@ -108,7 +119,7 @@ struct TileEmit {
     }
   }
   __device__ __forceinline__ void operator()(int row, int, double v, bool) {
-    if constexpr (FILTER)
+    if constexpr (DIRECT)
       if (!want(row)) return;
 #ifdef TOWR_EXPERIMENT_NOSLOT   // timing experiment only: wrong positions, no slot-table traffic
     out[(threadIdx.x * 7 + j++) & 1023] = v;
@@ -120,7 +131,11 @@ struct TileEmit {
       for (int d = 0; d + 1 < DEPTH; ++d) q[d] = q[d + 1];
       q[DEPTH - 1] = slot[((j >> 3) + DEPTH - 1) * BLOCK];
     }
-    out[s] = v;   // absent candidates land in the lane's dummy slot
+    if constexpr (DIRECT) {
+      if (s < nvals) out[s] = v;
+    } else {
+      out[s] = v;   // absent candidates land in the lane's dummy slot
+    }
 #endif
   }
   __device__ __forceinline__ void flush() {}
@@ -129,10 +144,12 @@ struct TileEmit {
 // loaded at construction: Dynamic group 0 builds it before the block barrier that separates its two
 // phases, so phase B's slot loads complete during the barrier wait instead of once per 8 candidates
 // after it. Candidate indices must be compile-time constants (fully unrolled emission).
-template <int BLOCK, int J0>
+template <int BLOCK, int J0, bool DIRECT = false>
 struct TileEmitPre {   // four groups: candidates J0 - J0 % 8 .. + 31
   double* out;
   double* gout;
+  int nvals = 0;   // DIRECT (see TileEmit): out / gout are V and g in HBM, dummy slots are not stored
+  bool gon = true;
   SlotGroup q0, q1, q2, q3;   // named registers (a runtime-indexed array would go to scratch)
   int j = J0;
   __device__ __forceinline__ TileEmitPre(const SlotGroup* s, double* o, double* go, bool load) : out(o), gout(go) {
@@ -141,7 +158,9 @@ struct TileEmitPre {   // four groups: candidates J0 - J0 % 8 .. + 31
       q2 = s[((J0 >> 3) + 2) * BLOCK]; q3 = s[((J0 >> 3) + 3) * BLOCK];
     }
   }
-  __device__ __forceinline__ void g(int row, double v) { gout[row] = v; }
+  __device__ __forceinline__ void g(int row, double v) {
+    if (!DIRECT || gon) gout[row] = v;
+  }
   __device__ __forceinline__ void operator()(int, int, double v, bool) {
     const int k = (j >> 3) - (J0 >> 3);
     SlotGroup q;
@@ -149,7 +168,7 @@ struct TileEmitPre {   // four groups: candidates J0 - J0 % 8 .. + 31
     for (int w = 0; w < 4; ++w) q.w[w] = k == 0 ? q0.w[w] : k == 1 ? q1.w[w] : k == 2 ? q2.w[w] : q3.w[w];
     const int s = slot_pick(q, j & 7);
     ++j;
-    out[s] = v;
+    if (!DIRECT || s < nvals) out[s] = v;
   }
   __device__ __forceinline__ void flush() {}
 };
@@ -267,6 +286,28 @@ struct XStage {
   }
 };
 
+// Zero-fill of the first nnz values of each problem's V row (phase-duration optimisation, see
+// TileEmit DIRECT): one block per 4096 values of a problem, 16-byte non-temporal stores. The rows'
+// padding up to ldv is the caller's and is not touched (hipMemset2DAsync does the same job at
+// ~0.8 TB/s on MI355X: 2.5 ms per 1024 ANYmal problems, this kernel runs near the write ceiling).
+constexpr int kZeroBlock = 256, kZeroPer = 8;
+__global__ void __launch_bounds__(kZeroBlock) towr_zero_kernel(double* V, int64_t ldv, int64_t nnz, int bpp) {
+  const int b = (int)(blockIdx.x / bpp), c = (int)(blockIdx.x % bpp);
+  double* row = V + (int64_t)b * ldv;
+  const int head = (reinterpret_cast<uintptr_t>(row) & 15) ? 1 : 0;
+  if (head && c == 0 && threadIdx.x == 0) row[0] = 0.0;
+  const int64_t m = (nnz - head) >> 1;
+  dbl2_t* d2 = reinterpret_cast<dbl2_t*>(row + head);
+  const dbl2_t z = {0.0, 0.0};
+  const int64_t base = (int64_t)c * kZeroBlock * kZeroPer;
+#pragma unroll
+  for (int i = 0; i < kZeroPer; ++i) {
+    const int64_t k = base + i * kZeroBlock + threadIdx.x;
+    if (k < m) __builtin_nontemporal_store(z, d2 + k);
+  }
+  if (((nnz - head) & 1) && c == 0 && threadIdx.x == 0) row[nnz - 1] = 0.0;
+}
+
 // zero n doubles of LDS (16-byte stores; n rounded up to even, the tile regions are even-sized)
 __device__ __forceinline__ void zero_lds(double* d, int n, int tid, int nthr) {
   dbl2_t* d2 = reinterpret_cast<dbl2_t*>(d);
@@ -340,12 +381,16 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
   } else {
     it = ItemDesc{}; it.type = IT_NONE; it.slot = 0;
   }
-  TileEmit<TBLOCK, slot_depth(TYPE), GAIT> em(P.slots + it.slot, smem, smem + lds_rows_off - T.r0);
-  if constexpr (GAIT) em.frow = it.rsel > 0 ? it.row0 + it.rsel - 1 : -1;
+  // GAIT: direct HBM emission into the zero-filled V (see TileEmit)
+  TileEmit<TBLOCK, slot_depth(TYPE), GAIT> em(P.slots + it.slot, GAIT ? Vb + T.v0 : smem, GAIT ? Gb : smem + lds_rows_off - T.r0);
+  if constexpr (GAIT) {
+    em.frow = it.rsel > 0 ? it.row0 + it.rsel - 1 : -1;
+    em.nvals = P.want_jac ? T.v1 - T.v0 : 0;
+    em.gon = P.want_g != 0;
+  }
   double* xs = smem + lds_x_off;
   int32_t* ns = reinterpret_cast<int32_t*>(smem + lds_x_off + P.n_pad);
   char* gt = reinterpret_cast<char*>(smem + lds_x_off + P.n_pad + ((P.n_nodecol + 3) >> 2) * 2);   // GAIT tables
-  if constexpr (GAIT) zero_lds(smem, T.v1 - T.v0, threadIdx.x, KBLOCK);   // sparse PhaseSpline emission
   if constexpr (early_stage(TYPE)) xst.commit(P, xg, xs, ns);
   else stage_x<KBLOCK, stages_nodes(TYPE, GAIT)>(P, xg, xs, ns);
   if constexpr (GAIT) stage16<KBLOCK>(reinterpret_cast<uint4*>(gt), P.gtab, P.gt_n16);
@@ -392,8 +437,10 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
   }
   if constexpr (TYPE == IT_DYN) {   // phase B of group 0: the endeffector sums from LDS
     const bool g0lane = it.type == TYPE && it.group == 0;
-    TileEmitPre<TBLOCK, kDynG0PhaseA> emb(P.slots + it.slot, smem,
-                                                                                     smem + lds_rows_off - T.r0, g0lane);
+    TileEmitPre<TBLOCK, kDynG0PhaseA, GAIT> emb(P.slots + it.slot, GAIT ? Vb + T.v0 : smem,
+                                                GAIT ? Gb : smem + lds_rows_off - T.r0, g0lane);
+    emb.nvals = P.want_jac ? T.v1 - T.v0 : 0;
+    emb.gon = P.want_g != 0;
     __syncthreads();
     if (g0lane) {
       double fs[3] = {0, 0, 0}, ts[3] = {0, 0, 0};
@@ -410,16 +457,18 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
 #ifdef TOWR_PHASE_TIMING
   if (threadIdx.x < 64) TSTAMP(7, TS_MEM());
 #endif
-  if (P.want_jac) copy_out(smem, Vb + T.v0, T.v1 - T.v0, threadIdx.x, KBLOCK);
-  if (P.want_g)
-    for (int i = threadIdx.x; i < T.r1 - T.r0; i += KBLOCK) __builtin_nontemporal_store(smem[lds_rows_off + i], Gb + T.r0 + i);
+  if constexpr (!GAIT) {
+    if (P.want_jac) copy_out(smem, Vb + T.v0, T.v1 - T.v0, threadIdx.x, KBLOCK);
+    if (P.want_g)
+      for (int i = threadIdx.x; i < T.r1 - T.r0; i += KBLOCK) __builtin_nontemporal_store(smem[lds_rows_off + i], Gb + T.r0 + i);
+  }
 #ifdef TOWR_PHASE_TIMING
   if (threadIdx.x < 64) { TSTAMP(8, TS_MEM()); TSTAMP(9, TS_REAL()); }
 #endif
 }
 
 template <int TYPE, int BLOCK, bool GAIT, bool ROTVEC>
-__global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? 2 : 1)) towr_tile_kernel(KParams P) {
+__global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN && BLOCK <= 256 ? 2 : 1)) towr_tile_kernel(KParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int total = P.B * P.ntiles;
   const int per = (total + 7) / 8;
@@ -662,10 +711,10 @@ const void* traj_kernel_for(bool gait) {
 template <bool GAIT, bool ROTVEC>
 const void* kernel_for_mode(int type) {
   switch (type) {
-    case IT_DYN: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_DYN, 256, GAIT, ROTVEC>);
-    case IT_ROM: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_ROM, 192, GAIT, ROTVEC>);
-    case IT_FDISC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_FDISC, 192, GAIT, false>);
-    case IT_TQDISC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_TQDISC, 192, GAIT, false>);
+    case IT_DYN: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_DYN, tile_block(IT_DYN, GAIT), GAIT, ROTVEC>);
+    case IT_ROM: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_ROM, tile_block(IT_ROM, GAIT), GAIT, ROTVEC>);
+    case IT_FDISC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_FDISC, tile_block(IT_FDISC, GAIT), GAIT, false>);
+    case IT_TQDISC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_TQDISC, tile_block(IT_TQDISC, GAIT), GAIT, false>);
   }
   return nullptr;
 }
@@ -919,6 +968,16 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
            int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem, int only_class = -1) {
   if (B <= 0) return TOWR_OK;
   const Layout& L = h->L;
+  // phase-duration optimisation: the tile classes store only their present candidates (TileEmit
+  // DIRECT), into a V zero-filled here by a streaming fill
+  if (L.gait && want_jac && L.nnz > 0) {
+    const int64_t bpp = ((L.nnz / 2 + 1) + kZeroBlock * kZeroPer - 1) / (kZeroBlock * kZeroPer);
+    if ((int64_t)B * bpp > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
+    int64_t nnz = L.nnz;
+    int bppi = (int)bpp;
+    void* za[] = {&V, &ldv, &nnz, &bppi};
+    HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void*>(&towr_zero_kernel), dim3((unsigned)(B * bpp)), dim3(kZeroBlock), za, 0, s));
+  }
   uint32_t fused_mask = 0;
   if (only_class < 0)
     for (int g = 0; g < h->n_fuse; ++g) {
@@ -1086,6 +1145,9 @@ int host_eval(towr_gpu_handle h, int B, const double* X, double* G, double* V) {
 // group needs two classes. Layout-only: the unit tables are uploaded by towr_gpu_create.
 int setup_fusion(towr_gpu_handle h, std::string& err) {
   const Layout& L = h->L;
+  // phase-duration optimisation: the tile classes run wave-per-row blocks of different sizes
+  // (tile_block), which the fused kernel's fixed 192 / 256-lane bodies do not cover
+  if (L.gait) return TOWR_OK;
   const char* fz = std::getenv("TOWR_GPU_FUSE");
   const std::string spec = fz ? fz : kDefaultFuse;
   size_t p0 = 0;
