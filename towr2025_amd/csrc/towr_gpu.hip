@@ -80,8 +80,8 @@ struct KParams {
 // DIRECT (phase-duration optimisation): there is no LDS tile. The full-pattern Jacobian is ~90 %
 // zeros whose positions move with x, and an LDS tile of it held ~13 instants per block (one busy wave
 // of three, 2 blocks per CU), so the launch was bound by the evaluation's latency at low occupancy.
-// Instead V is zero-filled by a streaming memset before the launch (launch()), and lanes store their
-// present candidates straight to HBM: `out` is the tile's first CSR value in V, `gout` the problem's g,
+// Instead each block zero-fills its tile's CSR range in V (zero_out), and after a barrier lanes store
+// their present candidates straight to HBM: `out` is the tile's first CSR value in V, `gout` the problem's g,
 // absent candidates (positions >= nvals, the dummy slots) are not stored. The lane's item may be
 // row-split (ItemDesc::rsel): only row frow's candidates are emitted (and counted), exactly as the
 // structure pass recorded them, and only that row's g.
@@ -105,7 +105,7 @@ struct TileEmit {
     if (!DIRECT) gout[row] = v;
     else if (gon && want(row)) gout[row] = v;
   }
-  // GAIT outputs are zero-filled before the evaluation (launch() / misc_body), so candidates whose
+  // GAIT outputs are zero-filled before the evaluation (tile_body / misc_body), so candidates whose
   // value is 0 can be skipped: move to candidate j + k, reloading the slot ring if the group changes
   static constexpr bool kSparse = true;
   __device__ __forceinline__ void skip(int k) {
@@ -286,26 +286,17 @@ struct XStage {
   }
 };
 
-// Zero-fill of the first nnz values of each problem's V row (phase-duration optimisation, see
-// TileEmit DIRECT): one block per 4096 values of a problem, 16-byte non-temporal stores. The rows'
-// padding up to ldv is the caller's and is not touched (hipMemset2DAsync does the same job at
-// ~0.8 TB/s on MI355X: 2.5 ms per 1024 ANYmal problems, this kernel runs near the write ceiling).
-constexpr int kZeroBlock = 256, kZeroPer = 8;
-__global__ void __launch_bounds__(kZeroBlock) towr_zero_kernel(double* V, int64_t ldv, int64_t nnz, int bpp) {
-  const int b = (int)(blockIdx.x / bpp), c = (int)(blockIdx.x % bpp);
-  double* row = V + (int64_t)b * ldv;
-  const int head = (reinterpret_cast<uintptr_t>(row) & 15) ? 1 : 0;
-  if (head && c == 0 && threadIdx.x == 0) row[0] = 0.0;
-  const int64_t m = (nnz - head) >> 1;
-  dbl2_t* d2 = reinterpret_cast<dbl2_t*>(row + head);
+// Zero-fill of a GAIT tile's CSR range in HBM by its own block (TileEmit DIRECT), 16-byte stores.
+// Plain stores: the scattered value stores that follow then mostly hit the same lines in L2.
+__device__ __forceinline__ void zero_out(double* __restrict__ dst, int n, int tid, int nthr) {
+  if (n <= 0) return;
+  const int head = (reinterpret_cast<uintptr_t>(dst) & 15) ? 1 : 0;
+  if (head && tid == 0) dst[0] = 0.0;
+  const int m = (n - head) >> 1;
+  dbl2_t* d2 = reinterpret_cast<dbl2_t*>(dst + head);
   const dbl2_t z = {0.0, 0.0};
-  const int64_t base = (int64_t)c * kZeroBlock * kZeroPer;
-#pragma unroll
-  for (int i = 0; i < kZeroPer; ++i) {
-    const int64_t k = base + i * kZeroBlock + threadIdx.x;
-    if (k < m) __builtin_nontemporal_store(z, d2 + k);
-  }
-  if (((nnz - head) & 1) && c == 0 && threadIdx.x == 0) row[nnz - 1] = 0.0;
+  for (int i = tid; i < m; i += nthr) d2[i] = z;
+  if (((n - head) & 1) && tid == 0) dst[n - 1] = 0.0;
 }
 
 // zero n doubles of LDS (16-byte stores; n rounded up to even, the tile regions are even-sized)
@@ -391,9 +382,16 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
   double* xs = smem + lds_x_off;
   int32_t* ns = reinterpret_cast<int32_t*>(smem + lds_x_off + P.n_pad);
   char* gt = reinterpret_cast<char*>(smem + lds_x_off + P.n_pad + ((P.n_nodecol + 3) >> 2) * 2);   // GAIT tables
+  // GAIT: the block zero-fills its tile's CSR range first; the value stores of any lane come after
+  // the barrier below, which waits for these stores to complete (vmcnt(0)), so they land on top
+  if constexpr (GAIT)
+    if (P.want_jac) zero_out(Vb + T.v0, T.v1 - T.v0, threadIdx.x, KBLOCK);
   if constexpr (early_stage(TYPE)) xst.commit(P, xg, xs, ns);
   else stage_x<KBLOCK, stages_nodes(TYPE, GAIT)>(P, xg, xs, ns);
-  if constexpr (GAIT) stage16<KBLOCK>(reinterpret_cast<uint4*>(gt), P.gtab, P.gt_n16);
+  if constexpr (GAIT) {
+    stage16<KBLOCK>(reinterpret_cast<uint4*>(gt), P.gtab, P.gt_n16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __syncthreads();
 #ifdef TOWR_PHASE_TIMING
   if (threadIdx.x < 64) TSTAMP(2, TS_MEM());
@@ -968,16 +966,6 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
            int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem, int only_class = -1) {
   if (B <= 0) return TOWR_OK;
   const Layout& L = h->L;
-  // phase-duration optimisation: the tile classes store only their present candidates (TileEmit
-  // DIRECT), into a V zero-filled here by a streaming fill
-  if (L.gait && want_jac && L.nnz > 0) {
-    const int64_t bpp = ((L.nnz / 2 + 1) + kZeroBlock * kZeroPer - 1) / (kZeroBlock * kZeroPer);
-    if ((int64_t)B * bpp > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
-    int64_t nnz = L.nnz;
-    int bppi = (int)bpp;
-    void* za[] = {&V, &ldv, &nnz, &bppi};
-    HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void*>(&towr_zero_kernel), dim3((unsigned)(B * bpp)), dim3(kZeroBlock), za, 0, s));
-  }
   uint32_t fused_mask = 0;
   if (only_class < 0)
     for (int g = 0; g < h->n_fuse; ++g) {
