@@ -14,13 +14,16 @@ namespace {
 // same semantics as the kernel's TileEmit: 8 tile-relative positions per SlotGroup, one plain store
 // per present candidate (a position written twice would be a layout bug: the check leaves NaN)
 struct AccEmit {
-  const SlotGroup* slot; int stride; double* v; double* gout; int nvals; int frow = -1; int j = 0;
+  const SlotGroup* slot; int stride; double* v; double* gout; int nvals; int flo = 0, fcnt = 0; ItemDirect dd{}; int j = 0;
   static constexpr bool kFilter = true;   // row-split items (ItemDesc::rsel), as the kernel's TileEmit
-  bool want(int row) const { return frow < 0 || row == frow; }
+  bool want(int row) const { return fcnt == 0 || (unsigned)(row - flo) < (unsigned)fcnt; }
   void g(int row, double val) { gout[row] = val; }
-  void operator()(int row, int, double val, bool) {
+  void operator()(int row, int col, double val, bool) {
     if (!want(row)) return;
-    const int s = slot_pick(slot[(j / 8) * stride], j % 8);
+    int s = slot_pick(slot[(j / 8) * stride], j % 8);
+    // the kernel's direct ranges (TileEmit DIRECT): must give the slot table's position
+    if (col >= dd.c0[0] && col < dd.c1[0]) s = dd.off[0] + col;
+    else if (col >= dd.c0[1] && col < dd.c1[1]) s = dd.off[1] + col;
     ++j;
     if (s >= nvals) return;   // the lane's dummy slot (absent candidate)
     v[s] = std::isnan(v[s]) ? val : std::nan("");
@@ -45,7 +48,8 @@ extern "C" int emu_eval(const towr_problem_desc_t* d, const double* x, double* g
       const ItemDesc& it = L.items[l];
       if (it.type == IT_NONE) continue;
       AccEmit em{L.slot_groups.data() + it.slot, td.i1 - td.i0, v + td.v0, g, td.v1 - td.v0,
-                 it.rsel > 0 ? it.row0 + it.rsel - 1 : -1};
+                 it.rsel > 0 ? it.row0 + rsel_first(it.rsel) : 0, it.rsel > 0 ? rsel_count(it.rsel) : 0,
+                 L.idirect.empty() ? ItemDirect{} : L.idirect[l]};
       c.seg = it.seg >= 0 ? L.segs.data() + (size_t)it.seg * L.spl.size() : nullptr;
       eval_item(c, it, em);
       em.flush();

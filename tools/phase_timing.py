@@ -46,6 +46,11 @@ def main():
     V = torch.empty((B, prob.nnz), dtype=torch.float64, device=dev)
     st = torch.cuda.current_stream(dev)
     print(f"B={B} n={prob.n} m={prob.m} nnz={prob.nnz}  (us; mean over blocks)")
+    lib.towr_gpu_debug_occupancy.argtypes = [C.c_void_p, C.c_int32]
+    for lc in range(5):
+        r = lib.towr_gpu_debug_occupancy(prob._h, lc)
+        if r >= 0:
+            print(f"  class {lc}: runtime max blocks/CU {r // 1000}, LDS {r % 1000} KiB")
     print(f"{'class':20s} {'blocks':>7s} {'stage':>7s} {'eval w0':>8s} {'w1':>6s} {'w2':>6s} {'w3':>6s} {'bar':>6s} "
           f"{'copy':>6s} {'life':>6s} {'span':>7s} {'resident':>8s}")
     for k, name, nt, _by in prob.kernels():

@@ -21,13 +21,15 @@ def per_kernel(d, counter):
         if r["Counter_Name"] != counter:
             continue
         if "towr_misc_kernel" in k:
-            acc["small_kinds"].append(float(r["Counter_Value"]) * 1024.0)
+            acc["gait_small_kinds" if "towr_misc_kernel<true>" in k else "small_kinds"].append(float(r["Counter_Value"]) * 1024.0)
         elif "towr_step_kernel<" in k:   # fusion group: the default 192-lane group is RangeOfMotion + FDISC
             acc["range_of_motion+force_discretized" if ", 192>(" in k else "fused_256"].append(
                 float(r["Counter_Value"]) * 1024.0)
-        elif "towr_tile_kernel<" in k:
-            t = int(k.split("towr_tile_kernel<")[1].split(",")[0])
-            acc[NAMES[t]].append(float(r["Counter_Value"]) * 1024.0)
+        elif "towr_tile_kernel<" in k:   # <type, block, gait, rotvec>: gait launches reported apart
+            targs = k.split("towr_tile_kernel<")[1].split(">")[0].split(",")
+            t = int(targs[0])
+            name = ("gait_" if targs[2].strip() == "true" else "") + NAMES[t]
+            acc[name].append(float(r["Counter_Value"]) * 1024.0)
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
 

@@ -106,12 +106,19 @@ struct ItemDesc {
   int32_t seg;                  // row of the segment table (time-discretised items), else -1
   int32_t ncand;                // number of candidates the item emits
   int32_t a2;                   // third node id (TorqueConstraint: torque node at phase start)
-  int32_t rsel;                 // row select: 0 = the item emits all its rows' candidates, r > 0 = only
-                                // row row0 + r - 1 (phase-duration optimisation splits the heavy
-                                // PhaseSpline items one row per lane, see layout.h split_rows)
+  int32_t rsel;                 // row select: 0 = the item emits all its rows' candidates, else it emits
+                                // only rows row0 + rsel_first .. + rsel_count - 1 (phase-duration
+                                // optimisation splits the heavy PhaseSpline items over lanes, see
+                                // layout.h split_rows); encoding 1 + first + 16 count + 256 part
   double t;                     // time of the instant (time-discretised sets)
   double p0;                    // scalar parameter (safety distance, t_swing_avg, ...)
 };
+
+// Direct CSR positions of a lane's candidates (phase-duration optimisation, TileEmit DIRECT): for up
+// to two variable-set column ranges [c0, c1) the lane's candidates sit at tile-relative position
+// off + col (the row holds the set's columns contiguously: FDISC force and schedule blocks, RangeOfMotion
+// motion and schedule blocks), so they need no slot-table load; other candidates use the slot table.
+struct alignas(16) ItemDirect { int32_t c0[2], c1[2], off[2], pad[2]; };
 
 // Spline::GetLocalTime result of one spline at one instant (precomputed on the host for fixed
 // polynomial durations: the reference's scan, spline.cc:48-78, run once at setup)
@@ -422,6 +429,17 @@ TG_HD void spline_basis(const SplinePt& o, int d, double H[4]) {
 // of a PhaseSpline's full pattern. The structure pass and the test emulation emit every candidate.
 template <class E, class = void> struct emit_sparse { static constexpr bool value = false; };
 template <class E> struct emit_sparse<E, decltype((void)E::kSparse)> { static constexpr bool value = E::kSparse; };
+
+TG_HD int rsel_first(int rsel) { return (rsel - 1) & 15; }
+TG_HD int rsel_count(int rsel) { return ((rsel - 1) >> 4) & 15; }
+TG_HD int rsel_part(int rsel) { return (rsel - 1) >> 8; }
+// rows of part `part` of an item's `rows` rows split over `parts` lanes: part 0 takes the first
+// rows - parts + 1 rows, every other part one row
+TG_HD void split_part_rows(int rows, int parts, int part, int& first, int& count) {
+  const int lead = rows - parts + 1;
+  first = part == 0 ? 0 : lead + part - 1;
+  count = part == 0 ? lead : 1;
+}
 
 // Emitters that evaluate only some rows of an item (row-split items, ItemDesc::rsel) declare
 // `static constexpr bool kFilter = true` and `want(row)`; their operator() drops the other rows'

@@ -47,6 +47,7 @@ struct Layout {
   std::vector<ItemDesc> items;
   std::vector<int32_t> slots;     // build-time: candidate -> global CSR position (or -1)
   std::vector<SlotGroup> slot_groups;   // device slot table (see SlotGroup); item.slot indexes it
+  std::vector<ItemDirect> idirect;      // gait: per item (lane), direct-position ranges (ItemDirect)
   std::vector<int64_t> row_ptr;
   std::vector<int32_t> col;
   std::vector<TileDesc> tiles;
@@ -99,17 +100,20 @@ constexpr int kTileValueCapGait = 65536 - 2 - 64 - 2;
 // Row-split items (phase-duration optimisation only). A PhaseSpline item emits its full-pattern
 // windows and schedule columns one candidate at a time, a chain of dependent slot-table and
 // PhaseCol loads; one item per instant would leave a tile of ~20 instants on 20 lanes of a 192-lane
-// block. Such items are split into one lane per row (ItemDesc::rsel): every lane evaluates the
-// instant, only its row's candidates are emitted. Returns the rows per lane split (1 = not split).
+// block. Such items are split over lanes by rows (ItemDesc::rsel, split_part_rows): every lane
+// evaluates the instant, only its rows' candidates are emitted. Returns the lanes per item (1 = not split).
 int split_rows(int type, int group, bool gait);
 
 // Block size of the tile classes. Under phase-duration optimisation every wave holds one row of
 // the split items (lanes = instants), so that a wave's lanes take the same branches: a wave mixing
 // the rows of an item would execute every row's emission path one after the other.
 //   DYN: g0 | g1 | row 0 .. 5 of the endeffector groups (lanes = ee x instant);
-//   ROM: g0 | g1 | row 0 .. 2 of the motion group;  FDISC: rows 0 .. 4;  TQDISC: rows 0 .. 3.
+//   ROM: g0 | g1 | rows (0, 1) | row 2 of the motion group;  FDISC: rows (0, 1) | 2 | 3 | 4;
+//   TQDISC: rows 0 .. 3.
+// Whole multiples of 4 waves: the runtime (and the measured residency) places a 5-wave block as if
+// it took 2 waves on every SIMD, so 320-lane blocks ran 1 per CU where 256-lane ones run 3.
 constexpr int tile_block(int type, bool gait) {
-  return type == IT_DYN ? (gait ? 512 : 256) : type == IT_ROM ? (gait ? 320 : 192) : type == IT_FDISC ? (gait ? 320 : 192)
+  return type == IT_DYN ? (gait ? 512 : 256) : type == IT_ROM ? (gait ? 256 : 192) : type == IT_FDISC ? (gait ? 256 : 192)
        : type == IT_TQDISC ? (gait ? 256 : 192) : 64;
 }
 

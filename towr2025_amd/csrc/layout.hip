@@ -146,10 +146,10 @@ struct RecordEmit {
   int g_rows_lo = 0, g_rows_hi = 0;
   bool bad_g = false;
   void g(int row, double) { if (row < g_rows_lo || row >= g_rows_hi) bad_g = true; }
-  // row-split items (ItemDesc::rsel): only the selected row's candidates, as the kernel's TileEmit
-  int frow = -1;
+  // row-split items (ItemDesc::rsel): only the selected rows' candidates, as the kernel's TileEmit
+  int flo = 0, fcnt = 0;   // rows flo .. flo + fcnt - 1, fcnt 0 = all
   static constexpr bool kFilter = true;
-  bool want(int row) const { return frow < 0 || row == frow; }
+  bool want(int row) const { return fcnt == 0 || (unsigned)(row - flo) < (unsigned)fcnt; }
   void operator()(int row, int col, double, bool pres) {
     if (!want(row)) return;
     rows->push_back(row); cols->push_back(col); present->push_back(pres && col >= 0 ? 1 : 0);
@@ -532,7 +532,9 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
       it.t = t; it.a0 = a0; it.a1 = a1; it.p0 = p0;
       const int S = split_rows(type, group, L.gait);   // one lane per row of a PhaseSpline item
       for (int r = 0; r < S; ++r) {
-        it.rsel = S > 1 ? r + 1 : 0;
+        int first = 0, count = 0;
+        split_part_rows(item_rows(type), S, r, first, count);
+        it.rsel = S > 1 ? 1 + first + 16 * count + 256 * r : 0;
         L.items.push_back(it); item_inst.push_back(inst);
       }
     };
@@ -706,7 +708,7 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
       item_cand_begin[i] = (int32_t)crow.size();
       RecordEmit em{&crow, &ccol, &cpres};
       em.g_rows_lo = L.items[i].row0; em.g_rows_hi = L.items[i].row0 + item_rows(L.items[i].type);
-      em.frow = L.items[i].rsel > 0 ? L.items[i].row0 + L.items[i].rsel - 1 : -1;
+      if (L.items[i].rsel > 0) { em.flo = L.items[i].row0 + rsel_first(L.items[i].rsel); em.fcnt = rsel_count(L.items[i].rsel); }
       cx.seg = L.items[i].seg >= 0 ? L.segs.data() + (size_t)L.items[i].seg * L.spl.size() : nullptr;
       eval_item(cx, L.items[i], em);
       if (em.bad_g) { err = "internal: item wrote g outside its rows"; return TOWR_ERR_INVALID; }
@@ -813,7 +815,7 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
         for (int k = a; k < b; ++k)
           for (int q = 0; q < insts[k].count; ++q) {
             const ItemDesc& it = L.items[insts[k].first + q];
-            const int lane = type_lane(type, it.group, k - a, b - a, E, L.gait, it.rsel > 0 ? it.rsel - 1 : 0);
+            const int lane = type_lane(type, it.group, k - a, b - a, E, L.gait, it.rsel > 0 ? rsel_part(it.rsel) : 0);
             if (lane < 0 || lane >= sp.block || lanes[lane].type != IT_NONE) { err = "internal: lane assignment"; return TOWR_ERR_INVALID; }
             lanes[lane] = it;
             if (type == IT_DYN) lanes[lane].a2 = k - a;   // instant within the tile (LDS sum terms)
@@ -891,6 +893,7 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
     // slot table per tile: lane l's candidates 8g..8g+7 in group g at base + g * block + l, as
     // tile-relative uint16 positions; four spare groups per lane absorb the kernel's prefetch
     std::vector<SlotGroup> groups;
+    L.idirect.assign(L.gait ? items.size() : 0, ItemDirect{});
     for (const TileDesc& td : L.tiles) {
       const int block = td.i1 - td.i0;
       int maxc = 0;
@@ -911,6 +914,32 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
             const int sh = (j & 1) ? 16 : 0;
             w = (w & ~(0xFFFFu << sh)) | (rel << sh);
           }
+        if (L.gait && !is_misc_kind(td.type) && it.type != IT_NONE) {
+          // direct ranges: variable sets whose candidates of this lane are all present at position
+          // (tile-relative) = col + a constant; the two with the most candidates
+          struct Rng { int32_t c0, c1, off, cnt; bool ok; };
+          std::vector<Rng> rs;
+          for (int j = 0; j < it.ncand; ++j) {
+            const int32_t col = ccol[it.slot + j], g = L.slots[it.slot + j];
+            if (col < 0) continue;
+            int vs = -1;
+            for (size_t v = 0; v < L.varsets.size(); ++v)
+              if (col >= L.varsets[v].col0 && col < L.varsets[v].col0 + L.varsets[v].n) { vs = (int)v; break; }
+            if (vs < 0) continue;
+            const int32_t c0 = L.varsets[vs].col0, c1 = c0 + L.varsets[vs].n;
+            Rng* r = nullptr;
+            for (Rng& q : rs) if (q.c0 == c0) r = &q;
+            const int32_t off = g < 0 ? 0 : (g - td.v0) - col;
+            if (!r) { rs.push_back({c0, c1, off, 0, g >= 0}); r = &rs.back(); }
+            r->ok = r->ok && g >= 0 && off == r->off;
+            ++r->cnt;
+          }
+          std::sort(rs.begin(), rs.end(), [](const Rng& a, const Rng& b) { return a.cnt > b.cnt; });
+          ItemDirect& dd = L.idirect[td.i0 + l];
+          int k = 0;
+          for (const Rng& q : rs)
+            if (q.ok && k < 2) { dd.c0[k] = q.c0; dd.c1[k] = q.c1; dd.off[k] = q.off; ++k; }
+        }
         it.slot = (int32_t)(base + l);
       }
     }
@@ -949,8 +978,8 @@ int split_rows(int type, int group, bool gait) {
   if (!gait) return 1;
   switch (type) {
     case IT_DYN: return group >= 2 ? 6 : 1;   // the endeffector groups (force / torque / motion PhaseSplines)
-    case IT_ROM: return group == 2 ? 3 : 1;   // the endeffector-motion group
-    case IT_FDISC: return 5;
+    case IT_ROM: return group == 2 ? 2 : 1;   // the endeffector-motion group: rows (0, 1), (2)
+    case IT_FDISC: return 4;                  // rows (0, 1), (2), (3), (4)
     case IT_TQDISC: return 4;
     default: return 1;
   }

@@ -48,6 +48,7 @@ struct KParams {
   const SchedInfo* sched;
   const EELinDef* eelin;
   const uint4* gtab;             // GAIT: the PhaseSpline tables in one blob (GaitTables), staged per tile block
+  const ItemDirect* idir;        // GAIT: per item (lane) direct-position ranges
   int32_t gt_off[5], gt_n16;
   int32_t n_pinfo, ph_stride;    // GAIT: the block's PhaseSpline timings (Ctx::pdur / pend / phend)
   int32_t n_spl;
@@ -83,8 +84,8 @@ struct KParams {
 // Instead each block zero-fills its tile's CSR range in V (zero_out), and after a barrier lanes store
 // their present candidates straight to HBM: `out` is the tile's first CSR value in V, `gout` the problem's g,
 // absent candidates (positions >= nvals, the dummy slots) are not stored. The lane's item may be
-// row-split (ItemDesc::rsel): only row frow's candidates are emitted (and counted), exactly as the
-// structure pass recorded them, and only that row's g.
+// row-split (ItemDesc::rsel): only its rows' candidates are emitted (and counted), exactly as the
+// structure pass recorded them, and only those rows' g.
 template <int BLOCK, int DEPTH, bool DIRECT = false>
 struct TileEmit {
   const SlotGroup* slot;   // this lane's group 0; group g at slot[g * BLOCK]
@@ -92,10 +93,12 @@ struct TileEmit {
   double* gout;            // LDS g rows, tile-relative (DIRECT: the problem's g)
   SlotGroup q[DEPTH];      // groups g .. g + DEPTH - 1 in flight (q[0] = current)
   int j = 0;
-  int frow = -1;           // DIRECT: the selected row, or -1 = all rows
+  int flo = 0, fcnt = 0;   // DIRECT: the selected rows flo .. flo + fcnt - 1 (fcnt 0 = all rows)
   int nvals = 0;           // DIRECT: values of the tile
+  ItemDirect dd{};         // DIRECT: column ranges stored at off + col without the slot table
+  int qg = 0;              // DIRECT: slot group held in q[0] (the ring reloads lazily, on use)
   static constexpr bool kFilter = DIRECT;
-  __device__ __forceinline__ bool want(int row) const { return !DIRECT || frow < 0 || row == frow; }
+  __device__ __forceinline__ bool want(int row) const { return !DIRECT || fcnt == 0 || (unsigned)(row - flo) < (unsigned)fcnt; }
   __device__ __forceinline__ TileEmit(const SlotGroup* s, double* o, double* go) : slot(s), out(o), gout(go) {
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d) q[d] = s[d * BLOCK];
@@ -109,6 +112,10 @@ struct TileEmit {
   // value is 0 can be skipped: move to candidate j + k, reloading the slot ring if the group changes
   static constexpr bool kSparse = true;
   __device__ __forceinline__ void skip(int k) {
+    if constexpr (DIRECT) {   // lazy: the next slot-path candidate loads its group
+      j += k;
+      return;
+    }
     if (k <= 0) return;
     const int g0 = j >> 3;
     j += k;
@@ -118,9 +125,29 @@ struct TileEmit {
       for (int d = 0; d < DEPTH; ++d) q[d] = slot[(g1 + d) * BLOCK];
     }
   }
-  __device__ __forceinline__ void operator()(int row, int, double v, bool) {
-    if constexpr (DIRECT)
+  __device__ __forceinline__ void operator()(int row, int col, double v, bool) {
+    if constexpr (DIRECT) {
+      // Direct-range candidates need no slot load. Slot-path groups load lazily: on gfx950 vmcnt
+      // counts stores too, so a group prefetched across this lane's value stores would wait for them.
       if (!want(row)) return;
+      int s;
+      if (col >= dd.c0[0] && col < dd.c1[0]) {
+        s = dd.off[0] + col;
+      } else if (col >= dd.c0[1] && col < dd.c1[1]) {
+        s = dd.off[1] + col;
+      } else {
+        const int g = j >> 3;
+        if (g != qg) {
+#pragma unroll
+          for (int d = 0; d < DEPTH; ++d) q[d] = slot[(g + d) * BLOCK];
+          qg = g;
+        }
+        s = slot_pick(q[0], j & 7);
+      }
+      ++j;
+      if (s < nvals) out[s] = v;
+      return;
+    }
 #ifdef TOWR_EXPERIMENT_NOSLOT   // timing experiment only: wrong positions, no slot-table traffic
     out[(threadIdx.x * 7 + j++) & 1023] = v;
 #else
@@ -131,11 +158,7 @@ struct TileEmit {
       for (int d = 0; d + 1 < DEPTH; ++d) q[d] = q[d + 1];
       q[DEPTH - 1] = slot[((j >> 3) + DEPTH - 1) * BLOCK];
     }
-    if constexpr (DIRECT) {
-      if (s < nvals) out[s] = v;
-    } else {
-      out[s] = v;   // absent candidates land in the lane's dummy slot
-    }
+    out[s] = v;   // absent candidates land in the lane's dummy slot
 #endif
   }
   __device__ __forceinline__ void flush() {}
@@ -375,9 +398,10 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
   // GAIT: direct HBM emission into the zero-filled V (see TileEmit)
   TileEmit<TBLOCK, slot_depth(TYPE), GAIT> em(P.slots + it.slot, GAIT ? Vb + T.v0 : smem, GAIT ? Gb : smem + lds_rows_off - T.r0);
   if constexpr (GAIT) {
-    em.frow = it.rsel > 0 ? it.row0 + it.rsel - 1 : -1;
+    if (it.rsel > 0) { em.flo = it.row0 + rsel_first(it.rsel); em.fcnt = rsel_count(it.rsel); }
     em.nvals = P.want_jac ? T.v1 - T.v0 : 0;
     em.gon = P.want_g != 0;
+    if (KBLOCK == TBLOCK || (int)threadIdx.x < TBLOCK) em.dd = P.idir[T.i0 + threadIdx.x];
   }
   double* xs = smem + lds_x_off;
   int32_t* ns = reinterpret_cast<int32_t*>(smem + lds_x_off + P.n_pad);
@@ -753,6 +777,7 @@ struct towr_gpu_handle_s {
   int32_t* d_misc_lds = nullptr;
   EELinDef* d_eelin = nullptr;
   uint4* d_gtab = nullptr;     // GAIT: PhaseSpline tables blob (GaitTables)
+  ItemDirect* d_idir = nullptr;
   CostItem* d_citems = nullptr;
   double* d_cq = nullptr;
   // fusion groups (TOWR_GPU_FUSE, see towr_step_kernel): classes that run in one launch
@@ -940,6 +965,7 @@ void fill_common(towr_gpu_handle h, KParams& P, int B, const double* X, int64_t 
   P.lds_scr_off = L.dyn_scr_off;
   const GaitTables gt = gait_tables(L);
   P.gtab = h->d_gtab;
+  P.idir = h->d_idir;
   for (int k = 0; k < 5; ++k) P.gt_off[k] = gt.off[k];
   P.gt_n16 = gt.n16;
   P.n_pinfo = (int32_t)L.pinfo.size();
@@ -1180,6 +1206,15 @@ int towr_gpu_abi_version(void) { return TOWR_GPU_ABI_VERSION; }
 
 #ifdef TOWR_PHASE_TIMING
 // timing build only (tools/phase_timing.py): device buffer of 16 u64 per block, or NULL
+// timing build only: the runtime's max resident blocks per CU of launch class lc (block, LDS as launched)
+int towr_gpu_debug_occupancy(towr_gpu_handle h, int32_t lc) {
+  const Layout& L = h->L;
+  if (lc < 0 || lc >= LC_COUNT || class_units(L, lc) == 0) return -1;
+  const int block = lc == LC_MISC ? 64 * kMiscWaves : L.type_block[class_type(lc)];
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel_for_class(lc, L.gait, L.rotvec), block, lds_bytes(L, lc)) != hipSuccess) return -2;
+  return n * 1000 + (int)(lds_bytes(L, lc) / 1024);
+}
 int towr_gpu_debug_set_timing_buffer(void* p) {
   unsigned long long* v = reinterpret_cast<unsigned long long*>(p);
   return hipMemcpyToSymbol(HIP_SYMBOL(g_tbuf), &v, sizeof(v)) == hipSuccess ? 0 : TOWR_ERR_HIP;
@@ -1232,7 +1267,8 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
       (r = upload(h, &h->d_spl, L.spl)) || (r = upload(h, &h->d_dur, L.dur)) || (r = upload(h, &h->d_terrain, ter)) ||
       (r = upload(h, &h->d_pinfo, L.pinfo)) || (r = upload(h, &h->d_pcols, L.pcols)) || (r = upload(h, &h->d_pact, L.pact)) || (r = upload(h, &h->d_sched, L.sched)) ||
       (r = upload(h, &h->d_misc, L.misc_tiles)) || (r = upload(h, &h->d_misc_lds, L.misc_lds)) || (r = upload(h, &h->d_eelin, L.eelin)) ||
-      (r = upload(h, &h->d_citems, L.cost_items)) || (r = upload(h, &h->d_cq, L.cost_q)) || (r = upload(h, &h->d_gtab, gait_blob(L))))
+      (r = upload(h, &h->d_citems, L.cost_items)) || (r = upload(h, &h->d_cq, L.cost_q)) || (r = upload(h, &h->d_gtab, gait_blob(L))) ||
+      (r = upload(h, &h->d_idir, L.idirect)))
     return bail(r);
   {   // trajectory export: phase durations of the description (fixed gait), counts, contact at start
     const towr_problem_desc_t& d = L.desc;
@@ -1317,7 +1353,7 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
 int towr_gpu_destroy(towr_gpu_handle h) {
   if (!h) return TOWR_OK;
   void* dev[] = {h->d_items, h->d_slots, h->d_tiles, h->d_nodecol, h->d_spl, h->d_dur, h->d_segs, h->d_terrain,
-                 h->d_pinfo, h->d_pcols, h->d_pact, h->d_sched, h->d_misc, h->d_misc_lds, h->d_eelin, h->d_gtab, h->d_citems, h->d_cq, h->fuse[0].d_units, h->fuse[1].d_units,
+                 h->d_pinfo, h->d_pcols, h->d_pact, h->d_sched, h->d_misc, h->d_misc_lds, h->d_eelin, h->d_gtab, h->d_idir, h->d_citems, h->d_cq, h->fuse[0].d_units, h->fuse[1].d_units,
                  h->d_bterrain, h->d_x, h->d_g, h->d_v, h->d_f, h->d_grad,
                  h->d_traj_pd, h->d_traj_n, h->d_traj_c0, h->d_traj_t};
   if (h->device >= 0) for (void* p : dev) if (p) (void)hipFree(p);
