@@ -118,7 +118,9 @@ struct ItemDesc {
 // to two variable-set column ranges [c0, c1) the lane's candidates sit at tile-relative position
 // off + col (the row holds the set's columns contiguously: FDISC force and schedule blocks, RangeOfMotion
 // motion and schedule blocks), so they need no slot-table load; other candidates use the slot table.
-struct alignas(16) ItemDirect { int32_t c0[2], c1[2], off[2], pad[2]; };
+// [z0, z1): the tile-relative CSR range of the rows this lane owns whole (row-split FDISC / TQDISC
+// lanes), which its wave zero-fills itself; else empty.
+struct alignas(16) ItemDirect { int32_t c0[2], c1[2], off[2], z0, z1; };
 
 // Spline::GetLocalTime result of one spline at one instant (precomputed on the host for fixed
 // polynomial durations: the reference's scan, spline.cc:48-78, run once at setup)

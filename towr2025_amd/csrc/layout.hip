@@ -939,8 +939,22 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
           int k = 0;
           for (const Rng& q : rs)
             if (q.ok && k < 2) { dd.c0[k] = q.c0; dd.c1[k] = q.c1; dd.off[k] = q.off; ++k; }
+          if ((td.type == IT_FDISC || td.type == IT_TQDISC) && it.rsel > 0) {   // rows owned whole by this lane
+            const int r_lo = it.row0 + rsel_first(it.rsel), r_hi = r_lo + rsel_count(it.rsel);
+            dd.z0 = (int32_t)(L.row_ptr[r_lo] - td.v0);
+            dd.z1 = (int32_t)(L.row_ptr[r_hi] - td.v0);
+          }
         }
         it.slot = (int32_t)(base + l);
+      }
+      if (L.gait && (td.type == IT_FDISC || td.type == IT_TQDISC)) {   // the lanes' owned ranges tile [v0, v1)
+        std::vector<std::pair<int32_t, int32_t>> zr;
+        for (int l = 0; l < block; ++l)
+          if (items[td.i0 + l].type != IT_NONE) zr.push_back({L.idirect[td.i0 + l].z0, L.idirect[td.i0 + l].z1});
+        std::sort(zr.begin(), zr.end());
+        int32_t at = 0;
+        for (auto& z : zr) { if (z.first != at) { err = "internal: row-split lanes do not cover their tile"; return TOWR_ERR_INVALID; } at = z.second; }
+        if (at != td.v1 - td.v0) { err = "internal: row-split lanes do not cover their tile"; return TOWR_ERR_INVALID; }
       }
     }
     if (groups.size() >= (size_t)INT32_MAX) { err = "slot table too large"; return TOWR_ERR_UNSUPPORTED; }

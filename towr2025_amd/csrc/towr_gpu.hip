@@ -51,6 +51,7 @@ struct KParams {
   const ItemDirect* idir;        // GAIT: per item (lane) direct-position ranges
   int32_t gt_off[5], gt_n16;
   int32_t n_pinfo, ph_stride;    // GAIT: the block's PhaseSpline timings (Ctx::pdur / pend / phend)
+  int32_t gt_ntime;              // GAIT: doubles of those timings (the terrain's LDS copy follows them)
   int32_t n_spl;
   const towr_terrain_t* terrains;
   int32_t terrain_per_problem;
@@ -96,6 +97,7 @@ struct TileEmit {
   int flo = 0, fcnt = 0;   // DIRECT: the selected rows flo .. flo + fcnt - 1 (fcnt 0 = all rows)
   int nvals = 0;           // DIRECT: values of the tile
   ItemDirect dd{};         // DIRECT: column ranges stored at off + col without the slot table
+  bool fence = false;      // DIRECT: the wave's own zero-fill stores must complete before the first value store
   int qg = 0;              // DIRECT: slot group held in q[0] (the ring reloads lazily, on use)
   static constexpr bool kFilter = DIRECT;
   __device__ __forceinline__ bool want(int row) const { return !DIRECT || fcnt == 0 || (unsigned)(row - flo) < (unsigned)fcnt; }
@@ -145,6 +147,10 @@ struct TileEmit {
         s = slot_pick(q[0], j & 7);
       }
       ++j;
+      if (fence) {   // wave-level: the zero stores of this wave's rows (tile_body) land first
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        fence = false;
+      }
       if (s < nvals) out[s] = v;
       return;
     }
@@ -407,14 +413,20 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
   int32_t* ns = reinterpret_cast<int32_t*>(smem + lds_x_off + P.n_pad);
   char* gt = reinterpret_cast<char*>(smem + lds_x_off + P.n_pad + ((P.n_nodecol + 3) >> 2) * 2);   // GAIT tables
   // GAIT: the block zero-fills its tile's CSR range first; the value stores of any lane come after
-  // the barrier below, which waits for these stores to complete (vmcnt(0)), so they land on top
-  if constexpr (GAIT)
+  // the barrier below, which waits for these stores to complete (vmcnt(0)), so they land on top.
+  // FDISC / TQDISC lanes own whole rows (row-split), so there each wave zero-fills its own rows
+  // after the staging instead (below), and waits for them only at its first value store.
+  constexpr bool kWaveZero = GAIT && (TYPE == IT_FDISC || TYPE == IT_TQDISC);
+  if constexpr (GAIT && !kWaveZero)
     if (P.want_jac) zero_out(Vb + T.v0, T.v1 - T.v0, threadIdx.x, KBLOCK);
   if constexpr (early_stage(TYPE)) xst.commit(P, xg, xs, ns);
   else stage_x<KBLOCK, stages_nodes(TYPE, GAIT)>(P, xg, xs, ns);
+  towr_terrain_t* ters = reinterpret_cast<towr_terrain_t*>(gt + 16 * P.gt_n16 + 8 * P.gt_ntime);   // GAIT: the terrain
   if constexpr (GAIT) {
     stage16<KBLOCK>(reinterpret_cast<uint4*>(gt), P.gtab, P.gt_n16);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x < sizeof(towr_terrain_t) / 8)
+      reinterpret_cast<double*>(ters)[threadIdx.x] = reinterpret_cast<const double*>(P.terrains + (P.terrain_per_problem ? b : 0))[threadIdx.x];
+    if constexpr (!kWaveZero) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
 #ifdef TOWR_PHASE_TIMING
@@ -447,6 +459,18 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
     }
     __syncthreads();
     c.pdur = tm; c.pend = tm + P.n_pinfo; c.phend = tm + 2 * P.n_pinfo; c.ph_stride = P.ph_stride;
+    c.ter = ters;   // LDS copy: no global load in the evaluation waits behind the zero-fill stores
+    if constexpr (kWaveZero) {
+      if (P.want_jac) {   // each lane's owned rows, zero-filled by its whole wave (512 B per store)
+        double* vt = Vb + T.v0;
+        const int lane = threadIdx.x & 63;
+        for (int l = 0; l < 64; ++l) {
+          const int z0 = __shfl(em.dd.z0, l, 64), z1 = __shfl(em.dd.z1, l, 64);
+          for (int p = z0 + lane; p < z1; p += 64) vt[p] = 0.0;
+        }
+        em.fence = true;
+      }
+    }
   }
   DynG0 g0;   // DYN group 0 between its two phases
   if (it.type == TYPE) {
@@ -884,7 +908,8 @@ size_t lds_bytes(const Layout& L, int lc) {
   size_t d = lds_region(L, lc);
   d += (size_t)((L.n + 2) & ~1);                                                                  // x + zero slot
   if (lc == LC_MISC || stages_nodes(class_type(lc), L.gait)) d += (L.nodecol.size() + 3) / 4 * 2;  // node table (16-B units)
-  if (lc != LC_MISC && L.gait) d += (size_t)gait_tables(L).n16 * 2 + gait_tables(L).n_time;         // PhaseSpline tables, timings
+  if (lc != LC_MISC && L.gait)   // PhaseSpline tables, timings, terrain
+    d += (size_t)gait_tables(L).n16 * 2 + gait_tables(L).n_time + (sizeof(towr_terrain_t) + 15) / 16 * 2;
   return sizeof(double) * d;
 }
 int class_units(const Layout& L, int lc) {   // tiles (or misc groups) per problem
@@ -970,6 +995,7 @@ void fill_common(towr_gpu_handle h, KParams& P, int B, const double* X, int64_t 
   P.gt_n16 = gt.n16;
   P.n_pinfo = (int32_t)L.pinfo.size();
   P.ph_stride = gt.ph_stride;
+  P.gt_ntime = gt.n_time;
 }
 
 int launch_fused(towr_gpu_handle h, const towr_gpu_handle_s::FuseGroup& fg, int B, const double* X, int64_t ldx, double* G,
