@@ -108,12 +108,13 @@ int split_rows(int type, int group, bool gait);
 // the split items (lanes = instants), so that a wave's lanes take the same branches: a wave mixing
 // the rows of an item would execute every row's emission path one after the other.
 //   DYN: g0 | g1 | row 0 .. 5 of the endeffector groups (lanes = ee x instant);
-//   ROM: g0 | g1 | rows (0, 1) | row 2 of the motion group;  FDISC: rows (0, 1) | 2 | 3 | 4;
-//   TQDISC: rows 0 .. 3.
-// Whole multiples of 4 waves: the runtime (and the measured residency) places a 5-wave block as if
-// it took 2 waves on every SIMD, so 320-lane blocks ran 1 per CU where 256-lane ones run 3.
+//   ROM: two halves of 64 instants, each g0 | g1 | row 0 | 1 | 2 of the motion group;
+//   FDISC: two halves of 64 instants, each row 0 | 1 | 2 | 3 | 4;  TQDISC: rows 0 .. 3.
+// A 5-wave block is placed as if it took 2 waves on every SIMD (hipOccupancy... and the measured
+// residency: 1 block per CU at 168 VGPRs), and a 4-wave block with FDISC rows (0, 1) on one wave
+// waits for that wave (1.5x the others): 10-wave blocks are balanced and fill 10 of the 12 wave slots.
 constexpr int tile_block(int type, bool gait) {
-  return type == IT_DYN ? (gait ? 512 : 256) : type == IT_ROM ? (gait ? 256 : 192) : type == IT_FDISC ? (gait ? 256 : 192)
+  return type == IT_DYN ? (gait ? 512 : 256) : type == IT_ROM ? (gait ? 640 : 192) : type == IT_FDISC ? (gait ? 640 : 192)
        : type == IT_TQDISC ? (gait ? 256 : 192) : 64;
 }
 

@@ -992,8 +992,8 @@ int split_rows(int type, int group, bool gait) {
   if (!gait) return 1;
   switch (type) {
     case IT_DYN: return group >= 2 ? 6 : 1;   // the endeffector groups (force / torque / motion PhaseSplines)
-    case IT_ROM: return group == 2 ? 2 : 1;   // the endeffector-motion group: rows (0, 1), (2)
-    case IT_FDISC: return 4;                  // rows (0, 1), (2), (3), (4)
+    case IT_ROM: return group == 2 ? 3 : 1;   // the endeffector-motion group
+    case IT_FDISC: return 5;
     case IT_TQDISC: return 4;
     default: return 1;
   }
@@ -1004,17 +1004,20 @@ TypeSpec type_spec(int type, int n_ee, bool gait) {
   const int blk = tile_block(type, gait);
   switch (type) {
     case IT_DYN: return {blk, std::max(1, std::min(64, gait ? 64 / E : 128 / E))};   // waves: g0 | g1 | ee, ee (gait: rows)
-    case IT_ROM: return {blk, 64};                                                      // waves: g0 | g1 | g2 (gait: rows)
-    case IT_FDISC: case IT_TQDISC: return {blk, gait ? 64 : blk};
+    case IT_ROM: return {blk, gait ? 128 : 64};                                         // waves: g0 | g1 | g2 (gait: rows, 2 halves)
+    case IT_FDISC: return {blk, gait ? 128 : blk};
+    case IT_TQDISC: return {blk, gait ? 64 : blk};
     default: return {64, 64};
   }
 }
 
 int type_lane(int type, int group, int k, int n, int n_ee, bool gait, int sub) {
-  if (gait && split_rows(type, group, gait) > 1) {   // one wave per row (tile_block)
-    if (type == IT_DYN) return 64 * (2 + sub) + (group - 2) * n + k;
-    if (type == IT_ROM) return 64 * (2 + sub) + k;
-    return 64 * sub + k;
+  if (gait) {   // one wave per row range (tile_block); ROM / FDISC: two halves of 64 instants
+    const int half = k >> 6, kk = k & 63;
+    if (type == IT_DYN && group >= 2) return 64 * (2 + sub) + (group - 2) * n + k;
+    if (type == IT_ROM) return 64 * 5 * half + 64 * (group < 2 ? group : 2 + sub) + kk;
+    if (type == IT_FDISC) return 64 * (5 * half + sub) + kk;
+    if (type == IT_TQDISC) return 64 * sub + k;
   }
   if (type == IT_DYN) return group == 0 ? k : group == 1 ? 64 + k : 128 + (group - 2) * n + k;
   if (type == IT_ROM) return 64 * group + k;
