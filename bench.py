@@ -75,9 +75,9 @@ def shard_first_id(rank, B):
     return rank * B
 
 
-def max_over_ranks(wall, kern_ms, dev, world):
+def max_over_ranks(wall, kern_ms, dev, distributed):
     """Timing reduction: the slowest rank defines the job time."""
-    if world <= 1:
+    if not distributed:
         return wall, kern_ms
     import torch
     import torch.distributed as dist
@@ -120,7 +120,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # under torch.distributed.run (RANK set) the process group is used at every world size, so the
+    # launcher path the multi-GPU runs take is the one a 1-GPU run under the launcher exercises
+    distributed = "RANK" in os.environ and "MASTER_ADDR" in os.environ
+    if distributed:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -148,7 +151,7 @@ def main():
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -158,12 +161,12 @@ def main():
         step(i)
     e1.record(stream)
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     kern_ms = e0.elapsed_time(e1) / args.steps
-    wall, kern_ms = max_over_ranks(wall, kern_ms, dev, world)
+    wall, kern_ms = max_over_ranks(wall, kern_ms, dev, distributed)
 
     calls = B * world * args.steps
     value = calls / wall
@@ -282,7 +285,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(desc, Xh[0, :8], args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 
