@@ -86,19 +86,81 @@ def max_over_ranks(wall, kern_ms, dev, distributed):
     return float(t[0]), float(t[1])
 
 
+def host_cpus():
+    """The measuring host's CPUs: lscpu sockets x cores per socket x threads per core, the CPUs this
+    process may run on (affinity), and the cgroup CPU quota (the GPU box grants each job a share)."""
+    info = {"sockets": None, "cores_per_socket": None, "threads_per_core": None, "model": None}
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=20).stdout
+        keys = {"Socket(s)": "sockets", "Core(s) per socket": "cores_per_socket",
+                "Thread(s) per core": "threads_per_core", "Model name": "model"}
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in keys:
+                v = v.strip()
+                info[keys[k.strip()]] = int(v) if v.isdigit() else v
+    except Exception:
+        pass
+    info["affinity"] = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+    except Exception:
+        pass
+    info["cgroup_quota_cpus"] = quota
+    if isinstance(info["sockets"], int) and isinstance(info["cores_per_socket"], int):
+        info["physical_cores"] = info["sockets"] * info["cores_per_socket"]
+    else:
+        info["physical_cores"] = None
+    return info
+
+
 def cpu_baseline(desc, X, seconds):
-    """The oracle timed on this host's cores, one independent problem per thread."""
+    """The oracle (built -O3 -march=native on this host) timed on this host's cores, one
+    independent problem per thread. Threads = every physical core this job may use: the affinity
+    set, capped by the cgroup CPU quota (more threads than the quota only time-slice) and by the
+    physical core count (no SMT siblings)."""
     from oracle import oracle as O
-    O.build()
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
-    t1, _ = O.bench(desc, 1, 3, X)                         # per-call time estimate (1 thread)
-    per_call = t1 / 3
+    cpus = host_cpus()
+    threads = cpus["affinity"]
+    for cap in (cpus["cgroup_quota_cpus"], cpus["physical_cores"]):
+        if cap:
+            threads = min(threads, cap)
+    threads = max(1, threads)
+    O.bench(desc, 1, 3, X, native=True)                    # builds liboracle_native.so, warms caches
+    t1, _ = O.bench(desc, 1, 20, X, native=True)           # 1-thread per-call time
+    per_call = t1 / 20
     calls = max(4, int(seconds / per_call))
-    secs, done = O.bench(desc, threads, calls, X)
-    return {"value": done / secs, "unit": "calls/s", "cores": threads, "kind": "port",
-            "sample": f"{done} calls ({calls}/thread x {threads} threads) of the CPU oracle "
-                      f"(oracle/towr_oracle.c) on ANYmal trot x-vectors, {secs:.1f} s wall; "
-                      f"1-thread {1.0 / per_call:.1f} calls/s"}
+    secs, done = O.bench(desc, threads, calls, X, native=True)
+    rate = done / secs
+    phys = cpus["physical_cores"]
+    return {"value": rate, "unit": "calls/s", "cores": threads, "kind": "port",
+            "one_thread": 1.0 / per_call, "host": cpus,
+            "all_physical_cores_extrapolated": (rate / threads * phys) if phys else None,
+            "sample": f"{done} calls ({calls}/thread x {threads} threads) of the CPU oracle (oracle/towr_oracle.c, "
+                      f"gcc -O3 -march=native on this host) on ANYmal trot x-vectors, {secs:.1f} s wall; "
+                      f"1 thread {1.0 / per_call:.1f} calls/s; threads = min(affinity {cpus['affinity']}, "
+                      f"cgroup quota {cpus['cgroup_quota_cpus']}, physical cores {phys})"}
+
+
+def single_call(prob, X, reps=300):
+    """B = 1 latency: towr_gpu_eval_g_jac through host pointers (what IpoptAdapter::eval_g + eval_jac_g
+    drive per iteration, hopper_example.cc:175-180): H2D of x, the launches, D2H of g and the values."""
+    x = [np.ascontiguousarray(X[k]) for k in range(len(X))]
+    for k in range(20):
+        prob.eval_g_jac(x[k % len(x)])
+    ts = []
+    for k in range(reps):
+        t0 = time.perf_counter()
+        prob.eval_g_jac(x[k % len(x)])
+        ts.append(time.perf_counter() - t0)
+    ts = np.array(ts) * 1e6
+    return {"us_median": float(np.median(ts)), "us_p10": float(np.percentile(ts, 10)),
+            "us_p90": float(np.percentile(ts, 90)), "calls": reps}
 
 
 def main():
@@ -108,6 +170,9 @@ def main():
     # after 50 warmup steps, same box): the defaults warm up for ~13 ms of work first
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--settle-ms", type=float, default=300.0,
+                    help="after the W warmup steps, keep running untimed steps until this much wall time has "
+                         "passed since warmup began (GPU clocks ramp up over the first ~100 ms)")
     ap.add_argument("--batch", type=int, default=4096, help="problems per GPU (weak scaling)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -150,9 +215,16 @@ def main():
     def step(i):
         prob.eval_batch_device(X[i % N_X], G, V, stream=stream)
 
+    tw = time.perf_counter()
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
+    settle = 0
+    while (time.perf_counter() - tw) * 1e3 < args.settle_ms:
+        for i in range(8):
+            step(i)
+        settle += 8
+        torch.cuda.synchronize()
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
@@ -200,6 +272,7 @@ def main():
         "metric": "full eval_g+eval_jac_g calls/sec, ANYmal trot 2.4s horizon; 1/2/4/8-GPU batch",
         "value": value, "unit": "calls/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "warmup_settle": {"extra_untimed_steps": settle, "settle_ms": args.settle_ms},
         "vs_baseline": None, "dtype": "f64",
         "data": "synthetic: randomised ANYmal trot instances (start/goal/terrain), x = x0 + seeded noise",
         "config": {"workload": "ANYmal trot 2.4s (quadruped C1), NlpFormulation defaults, batch of independent problems",
@@ -283,8 +356,14 @@ def main():
         th = (time.perf_counter() - t0) / reps
         out["host_batch"] = {"value": B / th, "unit": "calls/s", "ms_per_batch": th * 1e3,
                              "note": "host X/G/V buffers, PCIe transfers included (per GPU)"}
+    if rank == 0 and not args.no_host:
+        out["single_call"] = single_call(prob, Xh[:, 0])
+        out["single_call"]["note"] = ("B = 1 through host pointers (towr_gpu_eval_g_jac): H2D x, launches, D2H g + "
+                                      "values; per problem, the latency IPOPT sees per eval_g + eval_jac_g pair")
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(desc, Xh[0, :8], args.cpu_seconds)
+        if "single_call" in out:
+            out["single_call"]["cpu_one_thread_us"] = 1e6 / out["cpu_baseline"]["one_thread"]
     if rank == 0:
         print(json.dumps(out), flush=True)
     if distributed:

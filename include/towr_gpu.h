@@ -244,7 +244,11 @@ int towr_gpu_sample_trajectory_batch_device(towr_gpu_handle h, int32_t B, const 
 
 /* ---- batched evaluation over independent problems that share the layout ---------------------- */
 /* Per-problem terrain parameters (the only per-instance input to g/J besides x). `terrains` is a
- * host array of B entries; all entries must keep the Jacobian pattern identical. */
+ * host array of B entries; all entries must keep the Jacobian pattern identical.
+ * Once set, every BATCH entry point (eval_batch, eval_batch_device[_kernel], eval_cost_batch_device)
+ * uses terrain b for problem b and requires exactly B problems (else TOWR_ERR_INVALID); B = 0 clears
+ * the set. The single-problem entry points (eval_g, eval_jac_values, eval_g_jac, eval_f,
+ * eval_grad_f, sample_trajectory*) always use the description's terrain.                         */
 int towr_gpu_set_batch_terrain(towr_gpu_handle h, int32_t B, const towr_terrain_t* terrains);
 
 /* Device-resident batch: X[b*ldx + j], G[b*ldg + i], V[b*ldv + k] are DEVICE pointers (HBM);

@@ -15,19 +15,21 @@ from towr2025_amd import _capi as capi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(_HERE, "build", "liboracle.so")
-_lib = None
+LIB_NATIVE = os.path.join(_HERE, "build", "liboracle_native.so")
+_libs = {}
 
 
-def build():
-    subprocess.check_call(["make", "-s", "-C", _HERE])
+def build(native=False):
+    subprocess.check_call(["make", "-s", "-C", _HERE] + (["native"] if native else []))
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB):
-            build()
-        L = C.CDLL(LIB)
+def lib(native=False):
+    """The oracle library; native=True: the -O3 -march=native build of this host (CPU baseline only)."""
+    if native not in _libs:
+        path = LIB_NATIVE if native else LIB
+        if native or not os.path.exists(path):
+            build(native)
+        L = C.CDLL(path)
         D, I, Lg = C.POINTER(C.c_double), C.POINTER(C.c_int), C.POINTER(C.c_long)
         L.oracle_create.restype = C.c_void_p
         L.oracle_create.argtypes = [C.POINTER(capi.ProblemDesc), C.c_char_p, C.c_int]
@@ -46,8 +48,8 @@ def lib():
         L.oracle_varset_cols.argtypes = [C.c_void_p, C.c_int, I, I]
         L.oracle_bench.restype = C.c_double
         L.oracle_bench.argtypes = [C.POINTER(capi.ProblemDesc), C.c_int, C.c_int, C.c_int, D, Lg]
-        _lib = L
-    return _lib
+        _libs[native] = L
+    return _libs[native]
 
 
 def _d(a):
@@ -136,8 +138,8 @@ class Oracle:
         return out
 
 
-def bench(desc, threads, calls_per_thread, X):
+def bench(desc, threads, calls_per_thread, X, native=False):
     X = np.ascontiguousarray(X, dtype=np.float64)
     done = C.c_long()
-    secs = lib().oracle_bench(C.byref(desc), threads, calls_per_thread, X.shape[0], _d(X), C.byref(done))
+    secs = lib(native).oracle_bench(C.byref(desc), threads, calls_per_thread, X.shape[0], _d(X), C.byref(done))
     return secs, done.value

@@ -1,13 +1,16 @@
 """Shared parity helpers: the tolerance of BASELINE.md / SURVEY §8(d), written once.
 
-values:  |a - b| <= 1e-9 * max(|a|, |b|) + 1e-12 * max(1, rowscale, colscale)
-where rowscale / colscale = max |J| over the reference row / column. The floor covers entries that
-are exact zeros in exact arithmetic and come out as rounding residue of much larger terms:
-Hermite basis functions that vanish at a polynomial end (the reference rounds to exactly 0.0,
-fused multiply-adds give ~4e-16), and, with phase-duration optimisation, d pos / d duration of a
-PhaseSpline at an instant where the spline is analytically flat (a zero force in swing: its
-velocity is the ~1e-11 residue of ~1e5-sized Hermite terms). Such residue differs with any change
-of operation order, the reference's own build included; the column scale bounds its size.
+values:  |a - b| <= 1e-9 * max(|a|, |b|) + 1e-12 * max(1, rowscale)
+where rowscale = max |J| over the reference row (BASELINE.md's gate, on every entry).
+
+One whitelisted widening, and only where it is needed: a Jacobian entry in a PHASE-DURATION
+(schedule) column of a phase-duration-optimisation problem gets the floor
+1e-12 * max(1, rowscale, colscale), colscale = max |J| over the reference column. These entries are
+d pos / d duration of a PhaseSpline (phase_spline.cc:67-93, polynomial.cc:236-257); where the
+spline is analytically flat at an instant (a zero force in swing) the value is the ~1e-11 residue
+of ~1e5-sized Hermite terms, which differs with any change of operation order, the reference's own
+build included. The column scale bounds its size. No other column is widened (`floor_cols`).
+
 g:       |a - b| <= 1e-9 * max(|a|, |b|) + 1e-12 * max(1, |J row| scale)
 Pattern: bit-exact (same (row, col) list in the same order).
 """
@@ -16,25 +19,60 @@ import numpy as np
 REL = 1e-9
 ABS = 1e-12
 
+VAR_EE_SCHEDULE = 6   # towr_varset_kind (include/towr_gpu.h), PhaseDurations sets
 
-def check_values(g_ref, g, rows_ref, v_ref, v, m, cols_ref=None):
+
+def schedule_cols(desc, n):
+    """Boolean mask over the n columns: True for PhaseDurations (schedule) variable columns."""
+    from oracle.oracle import Oracle   # column offsets: the oracle's layout (ifopt's AddVariableSet order)
+    mask = np.zeros(n, dtype=bool)
+    if not desc.optimize_timings:
+        return mask
+    o = Oracle(desc)
+    for i, (c0, nc) in enumerate(o.varset_cols()):
+        if desc.varsets[i].kind == VAR_EE_SCHEDULE:
+            mask[c0:c0 + nc] = True
+    return mask
+
+
+def check_values(g_ref, g, rows_ref, v_ref, v, m, cols_ref=None, floor_cols=None):
+    """Indices of g and J entries outside the tolerance, and a summary dict:
+    max_rel = largest |a-b| / max(|a|,|b|) over entries above their floor; worst = largest
+    |a-b| / tolerance; widened = entries whose tolerance the schedule-column floor raised."""
     rs = np.zeros(m)
     np.maximum.at(rs, rows_ref, np.abs(v_ref))
     floor = ABS * np.maximum(1.0, rs)
     floor_v = floor[rows_ref]
-    if cols_ref is not None:
-        cs = np.zeros(int(cols_ref.max()) + 1 if len(cols_ref) else 1)
+    widened = 0
+    if cols_ref is not None and floor_cols is not None and floor_cols.any():
+        cs = np.zeros(len(floor_cols))
         np.maximum.at(cs, cols_ref, np.abs(v_ref))
-        floor_v = np.maximum(floor_v, ABS * cs[cols_ref])
-    tol_v = REL * np.maximum(np.abs(v_ref), np.abs(v)) + floor_v
-    bad_v = np.flatnonzero(np.abs(v_ref - v) > tol_v)
-    tol_g = REL * np.maximum(np.abs(g_ref), np.abs(g)) + floor
-    bad_g = np.flatnonzero(np.abs(g_ref - g) > tol_g)
-    return bad_g, bad_v
+        on = floor_cols[cols_ref]
+        col_floor = np.where(on, ABS * cs[cols_ref], 0.0)
+        widened = int(np.count_nonzero(col_floor > floor_v))
+        floor_v = np.maximum(floor_v, col_floor)
+    mag_v = np.maximum(np.abs(v_ref), np.abs(v))
+    err_v = np.abs(v_ref - v)
+    tol_v = REL * mag_v + floor_v
+    bad_v = np.flatnonzero(err_v > tol_v)
+    mag_g = np.maximum(np.abs(g_ref), np.abs(g))
+    err_g = np.abs(g_ref - g)
+    tol_g = REL * mag_g + floor
+    bad_g = np.flatnonzero(err_g > tol_g)
+    big_v = mag_v > floor_v
+    big_g = mag_g > floor
+    stats = {
+        "max_rel": float(max(np.max(err_v[big_v] / mag_v[big_v], initial=0.0),
+                             np.max(err_g[big_g] / mag_g[big_g], initial=0.0))),
+        "worst": float(max(np.max(err_v / tol_v, initial=0.0), np.max(err_g / tol_g, initial=0.0))),
+        "widened": widened,
+    }
+    return bad_g, bad_v, stats
 
 
-def assert_close(g_ref, g, rows_ref, v_ref, v, m, what="", cols_ref=None):
-    bad_g, bad_v = check_values(g_ref, g, rows_ref, v_ref, v, m, cols_ref)
+def assert_close(g_ref, g, rows_ref, v_ref, v, m, what="", cols_ref=None, floor_cols=None):
+    """BASELINE.md's gate; returns the summary of check_values (printed by the parity tests)."""
+    bad_g, bad_v, stats = check_values(g_ref, g, rows_ref, v_ref, v, m, cols_ref, floor_cols)
     msg = []
     if len(bad_g):
         i = bad_g[0]
@@ -42,9 +80,11 @@ def assert_close(g_ref, g, rows_ref, v_ref, v, m, what="", cols_ref=None):
     if len(bad_v):
         i = bad_v[0]
         j = bad_v[np.argmax(np.abs(v_ref[bad_v] - v[bad_v]))]
+        cinfo = f" col {cols_ref[j]}" if cols_ref is not None else ""
         msg.append(f"{len(bad_v)} J mismatches, first nz {i} (row {rows_ref[i]}): ref {v_ref[i]!r} got {v[i]!r}; "
-                   f"largest at nz {j} (row {rows_ref[j]}): ref {v_ref[j]!r} got {v[j]!r}")
+                   f"largest at nz {j} (row {rows_ref[j]}{cinfo}): ref {v_ref[j]!r} got {v[j]!r}")
     assert not msg, what + ": " + "; ".join(msg)
+    return stats
 
 
 def assert_cost_close(f_ref, f, g_ref, g, what=""):

@@ -5,6 +5,8 @@ import re
 import subprocess
 import tempfile
 
+import pytest
+
 from towr2025_amd import _capi as capi
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -54,3 +56,19 @@ def test_no_cpu_fallback_without_extension(tmp_path):
             capi.load_library(str(tmp_path / "missing.so"))
     finally:
         capi._lib = saved
+
+
+def test_device_batch_operands_are_validated():
+    """problem.py refuses operands the C-ABI cannot check (it sees a pointer and a leading dimension):
+    wrong dtype, host tensors, strided rows, too few columns."""
+    import torch
+    from towr2025_amd import TowrGpuProblem
+    from towr2025_amd import formulation as F
+    from towr2025_amd.problem import TowrGpuError, _check_tensor
+    p = TowrGpuProblem(F.procedural_desc(), device=-1)
+    with pytest.raises(TowrGpuError, match="dtype"):
+        _check_tensor(torch.zeros((2, p.n), dtype=torch.float32), "X", p.n)
+    with pytest.raises(TowrGpuError, match="HIP device"):
+        _check_tensor(torch.zeros((2, p.n), dtype=torch.float64), "X", p.n)
+    with pytest.raises(TowrGpuError, match="HIP device"):
+        p.eval_batch_device(torch.zeros((2, p.n), dtype=torch.float64), None, None)

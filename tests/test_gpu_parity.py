@@ -1,12 +1,17 @@
 """GPU parity: the HIP engine through the C-ABI vs the CPU oracle (pattern bit-exact, values within
-the tolerance of tests/parity.py), on every configuration and on seeded perturbations of x0."""
+BASELINE.md's gate, tests/parity.py), on every configuration and on seeded perturbations of x0.
+
+The gate is row-scaled everywhere; only the phase-duration columns of gait-optimisation configs get
+the column-scaled floor (tests/parity.py). Each test prints the largest relative error it saw."""
 import numpy as np
 import pytest
 
 from oracle.oracle import Oracle
 from tests.configs import config_descs, cost_descs
-from tests.parity import assert_close, assert_cost_close
+from tests.parity import assert_close, assert_cost_close, schedule_cols
+from tests.gap_frozen import frozen_reference, is_gap
 from towr2025_amd import TowrGpuProblem
+from towr2025_amd import formulation as F
 
 pytestmark = pytest.mark.gpu
 
@@ -28,18 +33,27 @@ def test_pattern_and_values(name):
     pr, pc = p.jac_structure()
     np.testing.assert_array_equal(pr, r)
     np.testing.assert_array_equal(pc, c)
+    fc = schedule_cols(desc, o.n)
+    worst = {"max_rel": 0.0, "worst": 0.0, "widened": 0}
     for seed in (0, 1, 2):
         x = x0 if seed == 0 else _perturb(x0, 20261015 + seed)
         g_ref = o.eval_g(x)
         rr, cc, v_ref = o.eval_jac(x)
-        if len(rr) != len(r) or not (np.array_equal(rr, r) and np.array_equal(cc, c)):
-            continue   # reference pattern moved at this x (only Gap terrain): out of contract
+        moved = len(rr) != len(r) or not (np.array_equal(rr, r) and np.array_equal(cc, c))
+        if moved:
+            # only curved terrain moves the reference's pattern; compare on the frozen pattern
+            assert is_gap(desc), f"{name} seed {seed}: the reference pattern moved on a non-Gap terrain"
+            v_ref, outside = frozen_reference(o, r, c, x)
+            print(f"{name} seed {seed}: reference pattern moved, {outside} reference entries outside the frozen pattern")
         g = p.eval_g(x)
         v = p.eval_jac_values(x)
-        assert_close(g_ref, g, r, v_ref, v, o.m, f"{name} seed {seed} (separate calls)", cols_ref=c)
+        st = assert_close(g_ref, g, r, v_ref, v, o.m, f"{name} seed {seed} (separate calls)", cols_ref=c, floor_cols=fc)
+        worst = {k: max(worst[k], st[k]) for k in worst}
         g2, v2 = p.eval_g_jac(x)
         np.testing.assert_array_equal(g2, g)
         np.testing.assert_array_equal(v2, v)
+    print(f"{name}: max relative error {worst['max_rel']:.3e}, worst |err|/tol {worst['worst']:.3f}, "
+          f"schedule-column floor widened {worst['widened']} entries")
 
 
 def test_batch_host_matches_single():
@@ -143,7 +157,7 @@ def test_fusion_groups(monkeypatch, spec, name):
     x = _perturb(o.initial_x(), 77)
     r, c, v_ref = o.eval_jac(x)
     g, v = p.eval_g_jac(x)
-    assert_close(o.eval_g(x), g, r, v_ref, v, o.m, f"{name} fuse {spec}", cols_ref=c)
+    assert_close(o.eval_g(x), g, r, v_ref, v, o.m, f"{name} fuse {spec}", cols_ref=c, floor_cols=schedule_cols(desc, o.n))
 
 
 def test_bench_workload_full_size(monkeypatch):
@@ -187,3 +201,93 @@ def test_bench_workload_full_size(monkeypatch):
         o = Oracle(d)
         r, _, v_ref = o.eval_jac(Xh[1, b])
         assert_close(o.eval_g(Xh[1, b]), G[b], r, v_ref, V[b], o.m, f"bench problem {b}")
+
+
+def _batch_vs_single(base_f, name, B=64, optimize_timings=False):
+    """B randomised problems of one layout (bench.make_batch: start/goal, per-problem Flat/Stairs terrain,
+    x = x0 + seeded noise, durations +-3 % with phase-duration optimisation) through the device batch
+    entry point with padded leading dimensions and NaN-prefilled outputs:
+      * every problem bit-identical to its own B = 1 evaluation (a handle whose base terrain is the
+        problem's, towr_gpu_eval_g_jac);
+      * a seeded sample against the oracle (BASELINE.md's gate);
+      * the padding of G and V still NaN (nothing written past m / nnz)."""
+    import torch
+    import bench
+    desc = base_f.to_desc()
+    p = TowrGpuProblem(desc)
+    Xh, terrains = bench.make_batch(p, B, first_id=9000, optimize_timings=optimize_timings)
+    X = np.ascontiguousarray(Xh[0])
+    p.set_batch_terrain(terrains)
+    dev = torch.device("cuda:0")
+    ldx, ldg, ldv = p.n + 7, p.m + 9, p.nnz + 13          # deliberately unaligned leading dimensions
+    Xd = torch.zeros((B, ldx), dtype=torch.float64, device=dev)
+    Xd[:, :p.n] = torch.from_numpy(X).to(dev)
+    Gd = torch.full((B, ldg), np.nan, dtype=torch.float64, device=dev)
+    Vd = torch.full((B, ldv), np.nan, dtype=torch.float64, device=dev)
+    p.eval_batch_device(Xd, Gd, Vd)
+    torch.cuda.synchronize()
+    G, V = Gd.cpu().numpy(), Vd.cpu().numpy()
+    assert np.isnan(G[:, p.m:]).all() and np.isnan(V[:, p.nnz:]).all(), "write past m / nnz"
+    G, V = G[:, :p.m], V[:, :p.nnz]
+    assert np.isfinite(G).all() and np.isfinite(V).all(), "unwritten or non-finite outputs"
+    r, c = p.jac_structure()
+    sample = set(np.random.default_rng(B).choice(B, 6, replace=False).tolist())
+    worst = 0.0
+    for b in range(B):
+        d = base_f.to_desc()
+        d.terrain = terrains[b]
+        q = TowrGpuProblem(d)
+        g1, v1 = q.eval_g_jac(X[b])
+        np.testing.assert_array_equal(G[b], g1, err_msg=f"{name} problem {b}: g differs from its B = 1 evaluation")
+        np.testing.assert_array_equal(V[b], v1, err_msg=f"{name} problem {b}: J differs from its B = 1 evaluation")
+        if b in sample:
+            o = Oracle(d)
+            rr, cc, v_ref = o.eval_jac(X[b])
+            np.testing.assert_array_equal(rr, r)
+            np.testing.assert_array_equal(cc, c)
+            st = assert_close(o.eval_g(X[b]), G[b], r, v_ref, V[b], o.m, f"{name} problem {b}", cols_ref=c,
+                              floor_cols=schedule_cols(d, o.n))
+            worst = max(worst, st["max_rel"])
+        q.close()
+    print(f"{name}: B = {B}, every problem bit-identical to B = 1; sample max relative error {worst:.3e}")
+
+
+def test_batch_device_gait_optimization():
+    """BASELINE configs[3]'s formulation (phase-duration optimisation: GAIT kernels, direct HBM
+    emission into per-wave zero-filled rows) as a randomised device batch."""
+    _batch_vs_single(F.anymal_trot(optimize_timings=True), "anymal_gaitopt_batch", B=64, optimize_timings=True)
+
+
+def test_batch_device_rotvec():
+    """RotVecConverter base orientation (ROTVEC kernels) as a randomised device batch."""
+    f = F.anymal_trot()
+    f.params_.angular_rep_ = 1
+    _batch_vs_single(f, "anymal_rotvec_batch", B=64)
+
+
+def test_batch_terrain_count_must_match():
+    """Per-problem terrains apply to batch entry points only, and only with exactly B problems;
+    single-problem entry points keep the description's terrain (include/towr_gpu.h)."""
+    import torch
+    from towr2025_amd.problem import TowrGpuError
+    desc = F.anymal_trot().to_desc()
+    p = TowrGpuProblem(desc)
+    o = Oracle(desc)
+    x = _perturb(o.initial_x(), 5)
+    ter = [F.HeightMap.Flat(0.2).to_c() for _ in range(4)]
+    p.set_batch_terrain(ter)
+    dev = torch.device("cuda:0")
+    X = torch.from_numpy(np.stack([x] * 3)).to(dev)
+    G = torch.zeros((3, p.m), dtype=torch.float64, device=dev)
+    V = torch.zeros((3, p.nnz), dtype=torch.float64, device=dev)
+    with pytest.raises(TowrGpuError, match="batch terrains are set for 4"):
+        p.eval_batch_device(X, G, V)
+    with pytest.raises(TowrGpuError, match="batch terrains are set for 4"):
+        p.eval_batch(np.stack([x] * 3))
+    g, v = p.eval_g_jac(x)   # single problem: the description's (flat, h = 0) terrain
+    r, _, v_ref = o.eval_jac(x)
+    assert_close(o.eval_g(x), g, r, v_ref, v, o.m, "single call with batch terrains set")
+    p.set_batch_terrain([])
+    p.eval_batch_device(X, G, V)   # cleared: the description's terrain again
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(G.cpu().numpy()[1], g)

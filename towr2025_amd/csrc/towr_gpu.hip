@@ -1160,16 +1160,30 @@ int ensure_stage(towr_gpu_handle h, int B) {
   return TOWR_OK;
 }
 
-int host_eval(towr_gpu_handle h, int B, const double* X, double* G, double* V) {
+// Terrain of a batch launch: the per-problem set (towr_gpu_set_batch_terrain) when one is set, which
+// must then hold exactly B entries; else the description's terrain for every problem. `single`
+// entry points (one problem through host pointers) always use the description's terrain.
+int batch_terrain(towr_gpu_handle h, int B, bool single, const towr_terrain_t** ter, int* per) {
+  *ter = h->d_terrain; *per = 0;
+  if (single || !h->d_bterrain) return TOWR_OK;
+  if (h->bterrain_n != B)
+    return fail(h, TOWR_ERR_INVALID, "batch terrains are set for " + std::to_string(h->bterrain_n) + " problems, the call has " +
+                                         std::to_string(B) + " (set them again, or with B = 0 to clear)");
+  *ter = h->d_bterrain; *per = 1;
+  return TOWR_OK;
+}
+
+int host_eval(towr_gpu_handle h, int B, const double* X, double* G, double* V, bool single) {
+  const towr_terrain_t* ter;
+  int per;
+  if (int rc = batch_terrain(h, B, single, &ter, &per)) return rc;
   if (int rc = ensure_stage(h, B)) return rc;
   const Layout& L = h->L;
   const size_t xb = sizeof(double) * (size_t)B * L.n, gb = sizeof(double) * (size_t)B * L.m,
                vb = sizeof(double) * (size_t)B * L.nnz;
   std::memcpy(h->h_x, X, xb);
   HIPCHK(h, hipMemcpyAsync(h->d_x, h->h_x, xb, hipMemcpyHostToDevice, h->stream));
-  const bool per = h->d_bterrain && h->bterrain_n >= B && B > 1;
-  if (int rc = launch(h, B, h->d_x, L.n, h->d_g, L.m, h->d_v, L.nnz, G != nullptr, V != nullptr, h->stream,
-                      per ? h->d_bterrain : h->d_terrain, per ? 1 : 0))
+  if (int rc = launch(h, B, h->d_x, L.n, h->d_g, L.m, h->d_v, L.nnz, G != nullptr, V != nullptr, h->stream, ter, per))
     return rc;
   if (G) HIPCHK(h, hipMemcpyAsync(h->h_g, h->d_g, gb, hipMemcpyDeviceToHost, h->stream));
   if (V) HIPCHK(h, hipMemcpyAsync(h->h_v, h->d_v, vb, hipMemcpyDeviceToHost, h->stream));
@@ -1446,19 +1460,19 @@ int towr_gpu_varset_info(towr_gpu_handle h, int32_t i, int32_t* kind, int32_t* e
 int towr_gpu_eval_g(towr_gpu_handle h, const double* x, double* g) {
   if (!h || !x || !g) return fail(h, TOWR_ERR_INVALID, "null argument");
   if (int rc = bind(h)) return rc;
-  return host_eval(h, 1, x, g, nullptr);
+  return host_eval(h, 1, x, g, nullptr, true);
 }
 
 int towr_gpu_eval_jac_values(towr_gpu_handle h, const double* x, double* values) {
   if (!h || !x || !values) return fail(h, TOWR_ERR_INVALID, "null argument");
   if (int rc = bind(h)) return rc;
-  return host_eval(h, 1, x, nullptr, values);
+  return host_eval(h, 1, x, nullptr, values, true);
 }
 
 int towr_gpu_eval_g_jac(towr_gpu_handle h, const double* x, double* g, double* values) {
   if (!h || !x || !g || !values) return fail(h, TOWR_ERR_INVALID, "null argument");
   if (int rc = bind(h)) return rc;
-  return host_eval(h, 1, x, g, values);
+  return host_eval(h, 1, x, g, values, true);
 }
 
 // one problem through the staging buffers: x -> HBM, cost launch, f (and gradient) -> host
@@ -1497,9 +1511,10 @@ int towr_gpu_eval_cost_batch_device(towr_gpu_handle h, int32_t B, const double* 
   const Layout& L = h->L;
   if (ldx < L.n || (GRAD && ldgrad < L.n)) return fail(h, TOWR_ERR_INVALID, "leading dimension smaller than n");
   if (int rc = bind(h)) return rc;
-  const bool per = h->d_bterrain && h->bterrain_n >= B;
-  return launch_cost(h, B, X, ldx, F, GRAD, ldgrad, reinterpret_cast<hipStream_t>(stream),
-                     per ? h->d_bterrain : h->d_terrain, per ? 1 : 0);
+  const towr_terrain_t* ter;
+  int per;
+  if (int rc = batch_terrain(h, B, false, &ter, &per)) return rc;
+  return launch_cost(h, B, X, ldx, F, GRAD, ldgrad, reinterpret_cast<hipStream_t>(stream), ter, per);
 }
 
 int towr_gpu_trajectory_size(towr_gpu_handle h, double dt, int32_t* n_samples, int32_t* n_cols) {
@@ -1564,9 +1579,11 @@ int towr_gpu_eval_batch_device(towr_gpu_handle h, int32_t B, const double* X, in
   if (ldx < L.n || (want_g && (!G || ldg < L.m)) || (want_jac && (!V || ldv < L.nnz)))
     return fail(h, TOWR_ERR_INVALID, "leading dimension smaller than n / m / nnz, or missing output");
   if (int rc = bind(h)) return rc;
-  const bool per = h->d_bterrain && h->bterrain_n >= B;
+  const towr_terrain_t* ter;
+  int per;
+  if (int rc = batch_terrain(h, B, false, &ter, &per)) return rc;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);   // NULL = HIP's default stream
-  return launch(h, B, X, ldx, G, ldg, V, ldv, want_g, want_jac, s, per ? h->d_bterrain : h->d_terrain, per ? 1 : 0);
+  return launch(h, B, X, ldx, G, ldg, V, ldv, want_g, want_jac, s, ter, per);
 }
 
 int towr_gpu_kernel_info(towr_gpu_handle h, int32_t kernel, const char** name, int32_t* n_tiles, int64_t* bytes_per_problem) {
@@ -1612,21 +1629,21 @@ int towr_gpu_eval_batch_device_kernel(towr_gpu_handle h, int32_t kernel, int32_t
   const Layout& L = h->L;
   if (ldx < L.n || ldg < L.m || ldv < L.nnz) return fail(h, TOWR_ERR_INVALID, "leading dimension too small");
   if (int rc = bind(h)) return rc;
-  const bool per = h->d_bterrain && h->bterrain_n >= B;
+  const towr_terrain_t* ter;
+  int per;
+  if (int rc = batch_terrain(h, B, false, &ter, &per)) return rc;
   if (kernel >= LC_COUNT) {
     const int g = kernel - LC_COUNT;
     if (g >= h->n_fuse) return fail(h, TOWR_ERR_INVALID, "no fusion group at this kernel index");
-    return launch_fused(h, h->fuse[g], B, X, ldx, G, ldg, V, ldv, 1, 1, reinterpret_cast<hipStream_t>(stream),
-                        per ? h->d_bterrain : h->d_terrain, per ? 1 : 0);
+    return launch_fused(h, h->fuse[g], B, X, ldx, G, ldg, V, ldv, 1, 1, reinterpret_cast<hipStream_t>(stream), ter, per);
   }
-  return launch(h, B, X, ldx, G, ldg, V, ldv, 1, 1, reinterpret_cast<hipStream_t>(stream),
-                per ? h->d_bterrain : h->d_terrain, per ? 1 : 0, kernel);
+  return launch(h, B, X, ldx, G, ldg, V, ldv, 1, 1, reinterpret_cast<hipStream_t>(stream), ter, per, kernel);
 }
 
 int towr_gpu_eval_batch(towr_gpu_handle h, int32_t B, const double* X, double* G, double* V) {
   if (!h || B < 0 || !X) return fail(h, TOWR_ERR_INVALID, "bad argument");
   if (int rc = bind(h)) return rc;
-  return host_eval(h, B, X, G, V);
+  return host_eval(h, B, X, G, V, false);
 }
 
 int towr_gpu_set_tiles_per_block(towr_gpu_handle h, int32_t tiles_per_block) {

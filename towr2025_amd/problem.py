@@ -26,10 +26,33 @@ class TowrGpuError(RuntimeError):
     pass
 
 
+def _check_tensor(t, what, min_cols, device=None):
+    """A device batch operand: float64, on a HIP device (the handle's), rows contiguous (stride(1) == 1),
+    at least min_cols columns. The C-ABI sees only a pointer and a leading dimension, so a float32 or
+    strided tensor would otherwise be read or written out of bounds."""
+    import torch
+    if t.dtype != torch.float64:
+        raise TowrGpuError(f"{what}: dtype {t.dtype}, expected torch.float64")
+    if t.device.type != "cuda":
+        raise TowrGpuError(f"{what}: tensor on {t.device}, expected a HIP device tensor")
+    if device is not None and t.device.index != device:
+        raise TowrGpuError(f"{what}: tensor on {t.device}, the handle is on device {device}")
+    if t.dim() == 2:
+        if t.shape[1] > 1 and t.stride(1) != 1:
+            raise TowrGpuError(f"{what}: stride(1) = {t.stride(1)}, expected 1 (row-major rows)")
+        if t.shape[1] < min_cols:
+            raise TowrGpuError(f"{what}: {t.shape[1]} columns, needs >= {min_cols}")
+        if t.shape[0] > 1 and t.stride(0) < min_cols:
+            raise TowrGpuError(f"{what}: leading dimension {t.stride(0)} < {min_cols}")
+    elif t.dim() != 1:
+        raise TowrGpuError(f"{what}: expected a 1-D or 2-D tensor")
+
+
 class TowrGpuProblem:
     def __init__(self, desc: capi.ProblemDesc, device: int = 0):
         self._lib = capi.load_library()
         self.desc = desc
+        self.device = device
         h = C.c_void_p()
         rc = self._lib.towr_gpu_create(C.byref(desc), device, C.byref(h))
         if rc != capi.TOWR_OK:
@@ -126,6 +149,14 @@ class TowrGpuProblem:
         """Device batch objective on torch HIP tensors: X (B, ldx) -> F (B,), GRAD (B, ldgrad) or None."""
         import torch
         B = X.shape[0]
+        _check_tensor(X, "X", self.n, self.device)
+        _check_tensor(F, "F", 1, self.device)
+        if F.dim() != 1 or F.shape[0] < B or (B > 1 and F.stride(0) != 1):
+            raise TowrGpuError("F: expected a contiguous 1-D tensor of >= B entries")
+        if GRAD is not None:
+            _check_tensor(GRAD, "GRAD", self.n, self.device)
+            if GRAD.shape[0] < B:
+                raise TowrGpuError("GRAD: fewer rows than X")
         if stream is None:
             stream = torch.cuda.current_stream(X.device)
         self._check(self._lib.towr_gpu_eval_cost_batch_device(
@@ -150,6 +181,11 @@ class TowrGpuProblem:
     def sample_trajectory_batch_device(self, X, dt, OUT, stream=None):
         """Device batch on torch HIP tensors: X (B, ldx) -> OUT (B, ldo >= n_samples * n_cols)."""
         import torch
+        _check_tensor(X, "X", self.n, self.device)
+        ns, nc = self.trajectory_size(dt)
+        _check_tensor(OUT, "OUT", ns * nc, self.device)
+        if OUT.shape[0] < X.shape[0]:
+            raise TowrGpuError("OUT: fewer rows than X")
         if stream is None:
             stream = torch.cuda.current_stream(X.device)
         self._check(self._lib.towr_gpu_sample_trajectory_batch_device(
@@ -173,12 +209,22 @@ class TowrGpuProblem:
         `stream`: a torch.cuda.Stream (default: torch's current stream)."""
         import torch
         B = X.shape[0]
+        self._check_batch(X, G, V, want_g, want_jac)
         if stream is None:
             stream = torch.cuda.current_stream(X.device)
         self._check(self._lib.towr_gpu_eval_batch_device(
             self._h, B, C.c_void_p(X.data_ptr()), X.stride(0),
             C.c_void_p(G.data_ptr()), G.stride(0), C.c_void_p(V.data_ptr()), V.stride(0),
             int(want_g), int(want_jac), C.c_void_p(stream.cuda_stream)))
+
+    def _check_batch(self, X, G, V, want_g=True, want_jac=True):
+        B = X.shape[0]
+        _check_tensor(X, "X", self.n, self.device)
+        for t, name, cols, want in ((G, "G", self.m, want_g), (V, "V", self.nnz, want_jac)):
+            if want or t is not None:
+                _check_tensor(t, name, cols, self.device)
+                if t.shape[0] < B:
+                    raise TowrGpuError(f"{name}: fewer rows than X")
 
     def step_launches(self):
         """Kernel indices (see kernels()) that one evaluation launches: fusion groups, then the unfused classes."""
@@ -201,6 +247,7 @@ class TowrGpuProblem:
 
     def eval_batch_device_kernel(self, kernel, X, G, V, stream):
         """Launch one kernel only: a launch class or a fusion group (roofline accounting)."""
+        self._check_batch(X, G, V)
         self._check(self._lib.towr_gpu_eval_batch_device_kernel(
             self._h, kernel, X.shape[0], C.c_void_p(X.data_ptr()), X.stride(0),
             C.c_void_p(G.data_ptr()), G.stride(0), C.c_void_p(V.data_ptr()), V.stride(0),
