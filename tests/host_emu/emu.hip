@@ -54,6 +54,34 @@ extern "C" int emu_eval(const towr_problem_desc_t* d, const double* x, double* g
       eval_item(c, it, em);
       em.flush();
     }
+  if (L.fstream) {   // the kernel's streaming ForceConstraintDiscretized composition (fdisc_stream_body)
+    c.pact = L.pact.data();
+    for (const FsBlock& fb : L.fs_blocks) {
+      std::vector<FdiscInstant> in(fb.n_inst);
+      std::vector<int> ws(fb.n_inst);
+      for (int k = 0; k < fb.n_inst; ++k) {
+        c.seg = nullptr;
+        fdisc_instant(c, fb.ee, L.fs_t[fb.t0 + k], in[k]);
+        ws[k] = L.fs_ws[fb.wsoff + in[k].poly];
+        for (int i = 0; i < 5; ++i) g[fb.r0 + 5 * k + i] = in[k].g[i];
+      }
+      for (int e = 0; e < fb.nv; ++e) {
+        const int r = (int)((e + 0.5) * (1.0 / fb.L)), j = e - r * fb.L, k = r / 5, i = r - 5 * k;
+        const FdiscInstant& o = in[k];
+        double val = 0.0;
+        if ((unsigned)(j - fb.js0) < (unsigned)fb.ns1) {
+          val = fdisc_sched_value(o.b[i], o.Jf, j - fb.js0);
+        } else if ((unsigned)(j - ws[k]) < (unsigned)kFsWin) {
+          const int32_t te = L.fs_tmpl[fb.tmpl + j];
+          if (te >= 0) {
+            const double s = phase_basis_sum(L.pcols[te & 0xFFFFFF], o.poly, o.H[0], o.H[1], o.H[2], o.H[3]);
+            val = s == 0.0 ? 0.0 : o.b[i][(te >> 24) & 3] * s;
+          }
+        }
+        v[fb.v0 + e] = val;
+      }
+    }
+  }
   return 0;
 }
 
@@ -87,6 +115,7 @@ extern "C" int emu_cost(const towr_problem_desc_t* d, const double* x, double* f
 extern "C" int emu_stats(const towr_problem_desc_t* d) {
   Layout L; std::string e;
   if (build_layout(*d, L, e)) return -1;
+  std::printf("fstream %d blocks %zu tmpl_max %d\n", (int)L.fstream, L.fs_blocks.size(), L.fs_tmpl_max);
   std::printf("n %d m %d nnz %lld nodecol %zu | gait tables: spl %zu pinfo %zu pcols %zu pact %zu sched %zu\n", L.n, L.m,
               (long long)L.nnz, L.nodecol.size(), L.spl.size(), L.pinfo.size(), L.pcols.size(), L.pact.size(), L.sched.size());
   for (int t = 0; t < IT_COUNT; ++t) {

@@ -1375,6 +1375,52 @@ TG_HD void eval_fdisc(const Ctx& c, const ItemDesc& it, Emit& em) {
   }
 }
 
+// ForceConstraintDiscretized under phase-duration optimisation on a terrain without curvature
+// (no motion block, fdisc_motion == 0), split for the streaming composer (towr_gpu.hip
+// fdisc_stream_body): fdisc_instant computes once per instant what eval_fdisc computes per lane
+// (force_constraint_discretized.cc:71-221), and every Jacobian entry of the instant's 5 rows is
+// then a function of it and the entry's column: a force column is b[i][e] times the Hermite basis
+// of the active force polynomial at the column's node values (phase_basis_sum, emit_dim's
+// full-pattern arithmetic), a schedule column a combination of the force spline's d pos / d schedule
+// (fdisc_sched_value, eval_fdisc's arithmetic). The operations are eval_fdisc's, in its order.
+struct FdiscInstant {
+  int poly;          // active polynomial of the force PhaseSpline
+  double H[4];       // its position basis at the instant
+  double nb[3][3];   // the normalized terrain basis n, t1, t2 at the foot
+  double b[5][3];    // the 5 pyramid rows (normal, friction +- mu normal) of the terrain basis
+  SchedJac Jf;       // d force(t) / d schedule
+  double g[5];
+};
+TG_HD void fdisc_instant(const Ctx& c, int ee, double t, FdiscInstant& o) {
+  const double mu = c.ter->friction_coeff;
+  SplinePt P, F;
+  spline_eval(c, sp_motion(ee), t, P);
+  spline_eval(c, sp_force(ee), t, F);
+  ter_nbasis(*c.ter, 0, P.p[0], P.p[1], o.nb[0]);
+  ter_nbasis(*c.ter, 1, P.p[0], P.p[1], o.nb[1]);
+  ter_nbasis(*c.ter, 2, P.p[0], P.p[1], o.nb[2]);
+  pyramid(o.nb[0], o.nb[1], o.nb[2], mu, o.b);
+  for (int i = 0; i < 5; ++i) o.g[i] = dot3(F.p, o.b[i]);
+  spline_basis(F, kPos, o.H);
+  o.poly = F.poly;
+  sched_jac(c, sp_force(ee), t, F, o.Jf);
+}
+// emit_dim's full-pattern basis sum of PhaseSpline column pq at polynomial `poly` (the entry is then
+// scale * sum, scale = b[i][e]); 0.0 off the active polynomial
+TG_HD double phase_basis_sum(const PhaseCol& pq, int poly, double h0, double h1, double h2, double h3) {
+  double v = 0.0;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {   // constant indices: a runtime-indexed pq.id / deriv goes to scratch
+    if (k >= pq.n) break;
+    if (pq.id[k] == poly) v += pq.deriv[k] ? h1 : h0;
+    else if (pq.id[k] == poly + 1) v += pq.deriv[k] ? h3 : h2;
+  }
+  return v;
+}
+TG_HD double fdisc_sched_value(const double bi[3], const SchedJac& Jf, int col) {
+  return bi[0] * sched_val(Jf, 0, col) + bi[1] * sched_val(Jf, 1, col) + bi[2] * sched_val(Jf, 2, col);
+}
+
 // ForceConstraint node (force_constraint.cc:62-171); a0 = force node, a1 = motion node at phase start
 template <class Emit>
 TG_HD void eval_fnode(const Ctx& c, const ItemDesc& it, Emit& em) {

@@ -1,0 +1,203 @@
+// kernel_common.h — device-side definitions shared by the engine's translation units
+// (towr_gpu.hip: tile / small-kind / cost / trajectory kernels and the C-ABI; fstream.hip: the
+// streaming ForceConstraintDiscretized kernels): the launch parameter block and the staging and
+// copy-out helpers.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "engine_math.h"
+#include "layout.h"
+
+namespace tg {
+
+// one unit of the fused launch: a tile of a tile class, or a small-kind group (LC_MISC)
+struct UnitDesc { int32_t lc, tile, lds_x_off, lds_rows_off; };
+
+struct KParams {
+  const double* X; int64_t ldx;
+  double* G; int64_t ldg;
+  double* V; int64_t ldv;
+  const ItemDesc* items;
+  const SlotGroup* slots;
+  const TileDesc* tiles;
+  const int32_t* nodecol;
+  const SplineMeta* spl;
+  const double* dur;
+  SegSoA sg;                     // segment table (structure of arrays)
+  const PolyPhase* pinfo;        // phase-duration optimisation tables (see engine_math.h)
+  const PhaseCol* pcols;
+  const int32_t* pact;
+  const SchedInfo* sched;
+  const EELinDef* eelin;
+  const uint4* gtab;             // GAIT: the PhaseSpline tables in one blob (GaitTables), staged per tile block
+  const ItemDirect* idir;        // GAIT: per item (lane) direct-position ranges
+  int32_t gt_off[5], gt_n16;
+  int32_t n_pinfo, ph_stride;    // GAIT: the block's PhaseSpline timings (Ctx::pdur / pend / phend)
+  int32_t gt_ntime;              // GAIT: doubles of those timings (the terrain's LDS copy follows them)
+  int32_t n_spl;
+  const towr_terrain_t* terrains;
+  int32_t terrain_per_problem;
+  int32_t B, tile0, ntiles;
+  int32_t lds_rows_off;          // start of the g buffer in the dynamic LDS (doubles)
+  int32_t lds_x_off;             // start of the staged x (+ zero slot) and node-column table
+  int32_t lds_scr_off;           // DYN: per-instant endeffector sum terms (instants x n_ee x 6)
+  int32_t n, n_pad, n_nodecol;
+  int32_t want_g, want_jac, fdisc_motion;
+  const int32_t* misc_tiles;      // merged small-kind launch: kMiscWaves tile ids per group
+  const int32_t* misc_lds;        // per (group, wave): LDS offset, g-row offset
+  RobotC rb;
+  const UnitDesc* units;          // fused launch: a problem's units (UnitDesc), n_units per problem
+  int32_t n_units;
+  const FsBlock* fsb;             // streaming ForceConstraintDiscretized (layout.h FsBlock)
+  const double* fs_t;
+  const int32_t* fs_tmpl;
+  const int32_t* fs_ws;
+  const int32_t* fs_iee;          // per FDISC instant: endeffector, first g row
+  const int32_t* fs_irow;
+  const CostItem* citems;         // cost launch: work items, objective and gradient outputs
+  const double* cq;               // cost launch: CT_ENERGYQ Gram matrices
+  int32_t n_citems, lds_red_off;
+  double* F;
+  double* GR; int64_t ldgr;
+};
+
+// global -> LDS copy of n16 16-byte units: each thread issues up to K independent loads before its
+// first LDS write, so the staging costs one memory latency rather than one per loop trip
+template <int BLOCK>
+__device__ __forceinline__ void stage16(uint4* __restrict__ dst, const uint4* __restrict__ src, int n16) {
+  for (int i = threadIdx.x; i < n16; i += 4 * BLOCK) {   // 4 loads in flight per thread
+    const int i1 = i + BLOCK, i2 = i + 2 * BLOCK, i3 = i + 3 * BLOCK;
+    const uint4 r0 = src[i];
+    uint4 r1{}, r2{}, r3{};
+    if (i1 < n16) r1 = src[i1];
+    if (i2 < n16) r2 = src[i2];
+    if (i3 < n16) r3 = src[i3];
+    dst[i] = r0;
+    if (i1 < n16) dst[i1] = r1;
+    if (i2 < n16) dst[i2] = r2;
+    if (i3 < n16) dst[i3] = r3;
+  }
+}
+
+// LDS -> HBM, 16-byte non-temporal stores where the destination allows it. The outputs are
+// streamed (never re-read by the kernel); plain stores cost ~25 % more kernel time on MI355X
+// (ANYmal, B = 4096: 0.532 -> 0.444 ms per step with non-temporal stores).
+typedef double dbl2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void copy_out(const double* __restrict__ src, double* __restrict__ dst, int n,
+                                         int tid, int nthr) {
+  if (n <= 0) return;
+  const int head = (reinterpret_cast<uintptr_t>(dst) & 15) ? 1 : 0;
+  if (head && tid == 0) __builtin_nontemporal_store(src[0], dst);
+  const int m = (n - head) >> 1;
+  dbl2_t* d2 = reinterpret_cast<dbl2_t*>(dst + head);
+  for (int i = tid; i < m; i += nthr) {
+    dbl2_t v;
+    v.x = src[head + 2 * i];
+    v.y = src[head + 2 * i + 1];
+    __builtin_nontemporal_store(v, d2 + i);
+  }
+  if (((n - head) & 1) && tid == 0) __builtin_nontemporal_store(src[n - 1], dst + n - 1);
+}
+
+// Split staging: issue() puts the first K 16-byte units per thread of x (and the node table) in
+// flight before the block's item / slot-table loads, commit() stores them to LDS afterwards, so the
+// staging's memory latency overlaps the item loads instead of following them. Units beyond K per
+// thread (problems larger than the bench's) go through stage16 in commit().
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+template <int BLOCK, bool NODES>
+struct XStage {
+  static constexpr int K = 3;   // named native-vector registers (HIP's uint4 class or an array goes to scratch)
+  u32x4_t x0 = {}, x1 = {}, x2 = {}, n0 = {}, n1 = {}, n2 = {};
+  bool aligned;
+  __device__ __forceinline__ void issue(const KParams& P, const double* xg) {
+    aligned = (reinterpret_cast<uintptr_t>(xg) & 15) == 0;
+    const int nx = P.n >> 1, i = threadIdx.x;
+    const u32x4_t* sx = reinterpret_cast<const u32x4_t*>(xg);
+    if (aligned) {
+      if (i < nx) x0 = sx[i];
+      if (i + BLOCK < nx) x1 = sx[i + BLOCK];
+      if (i + 2 * BLOCK < nx) x2 = sx[i + 2 * BLOCK];
+    }
+    if constexpr (NODES) {
+      const int nn = (P.n_nodecol + 3) >> 2;
+      const u32x4_t* sn = reinterpret_cast<const u32x4_t*>(P.nodecol);
+      if (i < nn) n0 = sn[i];
+      if (i + BLOCK < nn) n1 = sn[i + BLOCK];
+      if (i + 2 * BLOCK < nn) n2 = sn[i + 2 * BLOCK];
+    }
+  }
+  __device__ __forceinline__ void commit(const KParams& P, const double* xg, double* xs, int32_t* ns) {
+    const int nx = P.n >> 1, i = threadIdx.x;
+    if (aligned) {
+      u32x4_t* dx = reinterpret_cast<u32x4_t*>(xs);
+      if (i < nx) dx[i] = x0;
+      if (i + BLOCK < nx) dx[i + BLOCK] = x1;
+      if (i + 2 * BLOCK < nx) dx[i + 2 * BLOCK] = x2;
+      if (nx > K * BLOCK)
+        stage16<BLOCK>(reinterpret_cast<uint4*>(xs) + K * BLOCK, reinterpret_cast<const uint4*>(xg) + K * BLOCK, nx - K * BLOCK);
+      if ((P.n & 1) && threadIdx.x == 0) xs[P.n - 1] = xg[P.n - 1];
+    } else {
+      for (int k = threadIdx.x; k < P.n; k += BLOCK) xs[k] = xg[k];
+    }
+    if (threadIdx.x == 0) xs[P.n] = 0.0;
+    if constexpr (NODES) {
+      const int nn = (P.n_nodecol + 3) >> 2;
+      u32x4_t* dn = reinterpret_cast<u32x4_t*>(ns);
+      if (i < nn) dn[i] = n0;
+      if (i + BLOCK < nn) dn[i + BLOCK] = n1;
+      if (i + 2 * BLOCK < nn) dn[i + 2 * BLOCK] = n2;
+      if (nn > K * BLOCK)
+        stage16<BLOCK>(reinterpret_cast<uint4*>(ns) + K * BLOCK, reinterpret_cast<const uint4*>(P.nodecol) + K * BLOCK, nn - K * BLOCK);
+    }
+  }
+};
+
+// Zero-fill of a GAIT tile's CSR range in HBM by its own block (TileEmit DIRECT), 16-byte stores.
+// Plain stores: the scattered value stores that follow then mostly hit the same lines in L2.
+__device__ __forceinline__ void zero_out(double* __restrict__ dst, int n, int tid, int nthr) {
+  if (n <= 0) return;
+  const int head = (reinterpret_cast<uintptr_t>(dst) & 15) ? 1 : 0;
+  if (head && tid == 0) dst[0] = 0.0;
+  const int m = (n - head) >> 1;
+  dbl2_t* d2 = reinterpret_cast<dbl2_t*>(dst + head);
+  const dbl2_t z = {0.0, 0.0};
+  for (int i = tid; i < m; i += nthr) d2[i] = z;
+  if (((n - head) & 1) && tid == 0) dst[n - 1] = 0.0;
+}
+
+// zero n doubles of LDS (16-byte stores; n rounded up to even, the tile regions are even-sized)
+__device__ __forceinline__ void zero_lds(double* d, int n, int tid, int nthr) {
+  dbl2_t* d2 = reinterpret_cast<dbl2_t*>(d);
+  const dbl2_t z = {0.0, 0.0};
+  for (int i = tid; i < (n + 1) >> 1; i += nthr) d2[i] = z;
+}
+
+// global -> LDS staging of the problem's x (+ zero slot at n) and optionally the node table
+template <int BLOCK, bool NODES>
+__device__ __forceinline__ void stage_x(const KParams& P, const double* xg, double* xs, int32_t* ns) {
+  if ((reinterpret_cast<uintptr_t>(xg) & 15) == 0) {
+    stage16<BLOCK>(reinterpret_cast<uint4*>(xs), reinterpret_cast<const uint4*>(xg), P.n >> 1);
+    if ((P.n & 1) && threadIdx.x == 0) xs[P.n - 1] = xg[P.n - 1];
+  } else {
+    for (int i = threadIdx.x; i < P.n; i += BLOCK) xs[i] = xg[i];
+  }
+  if (threadIdx.x == 0) xs[P.n] = 0.0;
+  if constexpr (NODES)
+    stage16<BLOCK>(reinterpret_cast<uint4*>(ns), reinterpret_cast<const uint4*>(P.nodecol), (P.n_nodecol + 3) >> 2);
+}
+
+// Phase timing (tools/phase_timing.py; only in the -DTOWR_PHASE_TIMING build, never in the product):
+// per block, 16 timestamps: [0] realtime start, [1] memtime start, [2] after staging, [3..6] each
+// wave's end of evaluation, [7] after the evaluation barrier, [8] end of wave 0's copy-out,
+// [9] realtime end.
+#ifdef TOWR_PHASE_TIMING
+static __device__ unsigned long long* g_tbuf;   // one per translation unit
+#define TSTAMP(slot, v) do { if (g_tbuf && (threadIdx.x & 63) == 0) g_tbuf[(size_t)blockIdx.x * 16 + (slot)] = (v); } while (0)
+#define TS_MEM() ((unsigned long long)__builtin_amdgcn_s_memtime())
+#define TS_REAL() ((unsigned long long)__builtin_amdgcn_s_memrealtime())
+#else
+#define TSTAMP(slot, v) do { } while (0)
+#endif
+
+}  // namespace tg

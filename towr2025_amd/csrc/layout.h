@@ -25,6 +25,24 @@ struct TileDesc {
   int32_t type, reserved;
 };
 
+// Streaming composition of ForceConstraintDiscretized under phase-duration optimisation on a terrain
+// without curvature (towr_gpu.hip fdisc_stream_body). One block per (problem, FsBlock) evaluates up to
+// kFsInst instants once each (fdisc_instant), then writes the block's whole CSR range [v0, v0 + nv)
+// — every 16-byte unit exactly once, zeros included — composing each entry from its instant's
+// quantities. All rows of one constraint hold the same columns (checked): the force set's full
+// PhaseSpline pattern and the schedule columns. Template entry j (fs_tmpl) = column j of a row:
+//   >= 0: force column, PhaseCol index (bits 0-23) and dimension (bits 24-25); < 0: schedule column.
+// The force entries polynomial p can make non-zero (its two nodes' variables) lie in the window
+// [fs_ws[wsoff + p], + kFsWin) of row positions (checked); schedule columns at [js0, js0 + ns1).
+constexpr int kFsInst = 16;   // measured on MI355X (ANYmal gait, B = 1024): 64 -> 0.501 ms, 32 -> 0.463, 16 -> 0.452, 8 -> 0.478
+constexpr int kFsBlock = 256;
+constexpr int kFsWin = 12;
+struct FsBlock {
+  int32_t ee, n_inst, t0, r0;   // endeffector, instants, first instant's time index (fs_t), first row
+  int32_t v0, nv, L, tmpl;      // CSR range [v0, v0 + nv), row length, template offset (fs_tmpl)
+  int32_t js0, ns1, wsoff, reserved;
+};
+
 struct VarSetInfo { int kind, ee, col0, n; };
 struct ConsInfo { int kind, ee, row0, rows; };
 
@@ -72,6 +90,15 @@ struct Layout {
   std::vector<int32_t> misc_lds;     // per (group, wave): LDS offset of the wave's tile, its g-row offset (doubles)
   int32_t misc_region = 0;           // LDS of the largest group (doubles)
   int64_t misc_bytes = 0;
+  // streaming ForceConstraintDiscretized (FsBlock): enabled under phase-duration optimisation on
+  // terrains without curvature when every row of each constraint holds the same columns
+  bool fstream = false;
+  std::vector<FsBlock> fs_blocks;
+  std::vector<double> fs_t;
+  std::vector<int32_t> fs_tmpl;
+  std::vector<int32_t> fs_ws;        // window start per (constraint, force polynomial)
+  std::vector<int32_t> fs_iee, fs_irow;   // per instant (fs_t order): endeffector, first row
+  int32_t fs_tmpl_max = 0;
   // cost terms (eval_f / eval_grad_f): work items sorted by CostType, one block per problem
   std::vector<CostItem> cost_items;
   std::vector<double> cost_q;        // CT_ENERGYQ Gram matrices, 16 doubles per item (CostItem::q)
@@ -124,6 +151,13 @@ TypeSpec type_spec(int type, int n_ee, bool gait);
 // thread (lane) of the block that evaluates row-part `sub` (0 .. split_rows - 1) of group `g` of
 // the k-th of n instances in a tile
 int type_lane(int type, int group, int k, int n, int n_ee, bool gait, int sub);
+
+// The streaming ForceConstraintDiscretized kernels (fstream.hip): their LDS, record size, entry points.
+size_t fs_region(const Layout& L);
+int64_t fs_record_doubles();
+const void* fs_inst_kernel();
+const void* fs_stream_kernel();
+int fs_inst_block();
 
 // Returns TOWR_OK or an error code with a message in `err`.
 int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err);

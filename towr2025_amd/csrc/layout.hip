@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <array>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 
@@ -419,6 +420,97 @@ int build_costs(const towr_problem_desc_t& d, const std::vector<double>& base_d,
 }
 
 }  // namespace
+
+// FsBlocks of the streaming ForceConstraintDiscretized path (layout.h): per constraint, its instants
+// in chunks of <= kFsInst, provided every row of the constraint holds the same column list, each column
+// is a force-set PhaseSpline column or a schedule column of the constraint's endeffector, and each force
+// polynomial's columns fit a kFsWin window of the row. Otherwise the tile path stays.
+int build_fstream(Layout& L, std::string& err) {
+  L.fstream = false;
+  L.fs_blocks.clear(); L.fs_t.clear(); L.fs_tmpl.clear(); L.fs_ws.clear(); L.fs_iee.clear(); L.fs_irow.clear(); L.fs_tmpl_max = 0;
+  if (!L.gait || L.fdisc_motion) return TOWR_OK;
+  std::vector<FsBlock> blocks;
+  std::vector<double> ts;
+  std::vector<int32_t> tmpl, wsv, iee, irow;
+  int lmax = 0;
+  for (const ConsInfo& cs : L.cons) {
+    if (cs.kind != TOWR_C_FORCE_DISCRETIZED) continue;
+    const int ee = cs.ee, fs = sp_force(ee);
+    const SchedInfo& si = L.sched[ee];
+    const SplineMeta& m = L.spl[fs];
+    if (si.col0 < 0 || m.ee != ee) return TOWR_OK;
+    const int r0 = cs.row0, nrow = cs.rows, K = nrow / 5;
+    const int64_t L0 = L.row_ptr[r0 + 1] - L.row_ptr[r0];
+    for (int r = r0; r < r0 + nrow; ++r) {
+      if (L.row_ptr[r + 1] - L.row_ptr[r] != L0) return TOWR_OK;
+      if (!std::equal(L.col.begin() + L.row_ptr[r], L.col.begin() + L.row_ptr[r + 1], L.col.begin() + L.row_ptr[r0])) return TOWR_OK;
+    }
+    const int toff = (int)tmpl.size();
+    int js0 = -1, nsch = 0;
+    std::vector<int> pos_of_pcol(L.pcols.size(), -1);
+    for (int64_t j = 0; j < L0; ++j) {
+      const int32_t col = L.col[L.row_ptr[r0] + j];
+      if (col >= si.col0 && col < si.col0 + si.n_phases - 1) {
+        if (js0 < 0) js0 = (int)j;
+        if (col - si.col0 != (int)j - js0) return TOWR_OK;   // schedule columns contiguous, in order
+        tmpl.push_back((int32_t)(0x80000000u | (uint32_t)(col - si.col0)));
+        ++nsch;
+        continue;
+      }
+      int32_t code = -1;
+      for (int e = 0; e < 3 && code < 0; ++e)
+        for (int q = 0; q < m.pcol_n[e]; ++q)
+          if (L.pcols[m.pcol_off[e] + q].col == col && m.pcol_off[e] + q < (1 << 24)) {
+            code = (m.pcol_off[e] + q) | (e << 24);
+            pos_of_pcol[m.pcol_off[e] + q] = (int)j;
+            break;
+          }
+      if (code < 0) return TOWR_OK;   // a column the template cannot express
+      tmpl.push_back(code);
+    }
+    if (nsch != si.n_phases - 1) return TOWR_OK;
+    // window start of each force polynomial: the columns it touches (pact ranges of its 3 dims)
+    const int wsoff = (int)wsv.size();
+    for (int p = 0; p < m.n_polys; ++p) {
+      int lo = INT32_MAX, hi = -1;
+      for (int e = 0; e < 3; ++e) {
+        const int32_t* r = L.pact.data() + m.pact_off + 2 * (e * m.n_polys + p);
+        for (int q = r[0]; q <= r[1]; ++q) {
+          const int pos = pos_of_pcol[m.pcol_off[e] + q];
+          if (pos < 0) return TOWR_OK;
+          lo = std::min(lo, pos); hi = std::max(hi, pos);
+        }
+      }
+      if (hi >= 0 && hi - lo >= kFsWin) return TOWR_OK;
+      wsv.push_back(hi >= 0 ? lo : 0);
+    }
+    lmax = std::max(lmax, (int)L0);
+    // the constraint's instants, in row order (one instant per 5 rows)
+    std::vector<double> its(K, -1.0);
+    for (const ItemDesc& it : L.items)
+      if (it.type == IT_FDISC && it.row0 >= r0 && it.row0 < r0 + nrow) its[(it.row0 - r0) / 5] = it.t;
+    for (double t : its) if (t < 0) { err = "internal: ForceConstraintDiscretized instant missing"; return TOWR_ERR_INVALID; }
+    // instants per block: kFsInst at most (the stream kernel's LDS records); TOWR_GPU_FS_INST (tuning) lowers it
+    int cap = kFsInst;
+    if (const char* e = std::getenv("TOWR_GPU_FS_INST")) cap = std::max(1, std::min(kFsInst, std::atoi(e)));
+    const int nb = (K + cap - 1) / cap;
+    for (int q = 0; q < nb; ++q) {
+      const int a = (int)((int64_t)q * K / nb), b = (int)((int64_t)(q + 1) * K / nb);
+      FsBlock fb{};
+      fb.ee = ee; fb.n_inst = b - a; fb.t0 = (int32_t)ts.size() + a; fb.r0 = r0 + 5 * a;
+      fb.v0 = (int32_t)L.row_ptr[r0 + 5 * a]; fb.nv = (int32_t)(L.row_ptr[r0 + 5 * b] - L.row_ptr[r0 + 5 * a]);
+      fb.L = (int32_t)L0; fb.tmpl = toff; fb.js0 = js0 < 0 ? (int32_t)L0 : js0; fb.ns1 = nsch; fb.wsoff = wsoff;
+      blocks.push_back(fb);
+    }
+    ts.insert(ts.end(), its.begin(), its.end());
+    for (int k = 0; k < K; ++k) { iee.push_back(ee); irow.push_back(r0 + 5 * k); }
+  }
+  if (blocks.empty()) return TOWR_OK;
+  L.fstream = true;
+  L.fs_blocks.swap(blocks); L.fs_t.swap(ts); L.fs_tmpl.swap(tmpl); L.fs_ws.swap(wsv); L.fs_tmpl_max = lmax;
+  L.fs_iee.swap(iee); L.fs_irow.swap(irow);
+  return TOWR_OK;
+}
 
 int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
   if (d.abi_version != TOWR_GPU_ABI_VERSION) { err = "abi version mismatch"; return TOWR_ERR_INVALID; }
@@ -972,6 +1064,7 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
       for (uint8_t u : used) nx += u;
       L.type_bytes[t] = 8 * (nv + nr + nx);
     }
+    if (int rc = build_fstream(L, err)) return rc;
     {   // the merged small-kind launch: union of their x columns
       int64_t nv = 0, nr = 0, nx = 0;
       std::vector<uint8_t> used((size_t)L.n, 0);

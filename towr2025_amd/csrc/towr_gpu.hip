@@ -22,56 +22,13 @@
 #include <vector>
 
 #include "engine_math.h"
+#include "kernel_common.h"
 #include "layout.h"
 
 using namespace tg;
 
 namespace {
 
-// one unit of the fused launch: a tile of a tile class, or a small-kind group (LC_MISC)
-struct UnitDesc { int32_t lc, tile, lds_x_off, lds_rows_off; };
-
-struct KParams {
-  const double* X; int64_t ldx;
-  double* G; int64_t ldg;
-  double* V; int64_t ldv;
-  const ItemDesc* items;
-  const SlotGroup* slots;
-  const TileDesc* tiles;
-  const int32_t* nodecol;
-  const SplineMeta* spl;
-  const double* dur;
-  SegSoA sg;                     // segment table (structure of arrays)
-  const PolyPhase* pinfo;        // phase-duration optimisation tables (see engine_math.h)
-  const PhaseCol* pcols;
-  const int32_t* pact;
-  const SchedInfo* sched;
-  const EELinDef* eelin;
-  const uint4* gtab;             // GAIT: the PhaseSpline tables in one blob (GaitTables), staged per tile block
-  const ItemDirect* idir;        // GAIT: per item (lane) direct-position ranges
-  int32_t gt_off[5], gt_n16;
-  int32_t n_pinfo, ph_stride;    // GAIT: the block's PhaseSpline timings (Ctx::pdur / pend / phend)
-  int32_t gt_ntime;              // GAIT: doubles of those timings (the terrain's LDS copy follows them)
-  int32_t n_spl;
-  const towr_terrain_t* terrains;
-  int32_t terrain_per_problem;
-  int32_t B, tile0, ntiles;
-  int32_t lds_rows_off;          // start of the g buffer in the dynamic LDS (doubles)
-  int32_t lds_x_off;             // start of the staged x (+ zero slot) and node-column table
-  int32_t lds_scr_off;           // DYN: per-instant endeffector sum terms (instants x n_ee x 6)
-  int32_t n, n_pad, n_nodecol;
-  int32_t want_g, want_jac, fdisc_motion;
-  const int32_t* misc_tiles;      // merged small-kind launch: kMiscWaves tile ids per group
-  const int32_t* misc_lds;        // per (group, wave): LDS offset, g-row offset
-  RobotC rb;
-  const UnitDesc* units;          // fused launch: a problem's units (UnitDesc), n_units per problem
-  int32_t n_units;
-  const CostItem* citems;         // cost launch: work items, objective and gradient outputs
-  const double* cq;               // cost launch: CT_ENERGYQ Gram matrices
-  int32_t n_citems, lds_red_off;
-  double* F;
-  double* GR; int64_t ldgr;
-};
 
 // Stores candidate j of this lane into the LDS tile at its tile-relative CSR position. Positions
 // come 8 per 16-byte SlotGroup; the next group is prefetched while the current one is consumed, so
@@ -151,7 +108,11 @@ struct TileEmit {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         fence = false;
       }
+#ifdef TOWR_EXP_GAIT_NOSTORE   // timing experiment only: evaluate, but (almost) never store
+      if (s < nvals && v == 12345.678) out[s] = v;
+#else
       if (s < nvals) out[s] = v;
+#endif
       return;
     }
 #ifdef TOWR_EXPERIMENT_NOSLOT   // timing experiment only: wrong positions, no slot-table traffic
@@ -224,131 +185,6 @@ __device__ __forceinline__ void eval_typed(const Ctx& c, const ItemDesc& it, Emi
   else if constexpr (TYPE == IT_TQDISC) eval_tqdisc(c, it, em);
 }
 
-// global -> LDS copy of n16 16-byte units: each thread issues up to K independent loads before its
-// first LDS write, so the staging costs one memory latency rather than one per loop trip
-template <int BLOCK>
-__device__ __forceinline__ void stage16(uint4* __restrict__ dst, const uint4* __restrict__ src, int n16) {
-  for (int i = threadIdx.x; i < n16; i += 4 * BLOCK) {   // 4 loads in flight per thread
-    const int i1 = i + BLOCK, i2 = i + 2 * BLOCK, i3 = i + 3 * BLOCK;
-    const uint4 r0 = src[i];
-    uint4 r1{}, r2{}, r3{};
-    if (i1 < n16) r1 = src[i1];
-    if (i2 < n16) r2 = src[i2];
-    if (i3 < n16) r3 = src[i3];
-    dst[i] = r0;
-    if (i1 < n16) dst[i1] = r1;
-    if (i2 < n16) dst[i2] = r2;
-    if (i3 < n16) dst[i3] = r3;
-  }
-}
-
-// LDS -> HBM, 16-byte non-temporal stores where the destination allows it. The outputs are
-// streamed (never re-read by the kernel); plain stores cost ~25 % more kernel time on MI355X
-// (ANYmal, B = 4096: 0.532 -> 0.444 ms per step with non-temporal stores).
-typedef double dbl2_t __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void copy_out(const double* __restrict__ src, double* __restrict__ dst, int n,
-                                         int tid, int nthr) {
-  if (n <= 0) return;
-  const int head = (reinterpret_cast<uintptr_t>(dst) & 15) ? 1 : 0;
-  if (head && tid == 0) __builtin_nontemporal_store(src[0], dst);
-  const int m = (n - head) >> 1;
-  dbl2_t* d2 = reinterpret_cast<dbl2_t*>(dst + head);
-  for (int i = tid; i < m; i += nthr) {
-    dbl2_t v;
-    v.x = src[head + 2 * i];
-    v.y = src[head + 2 * i + 1];
-    __builtin_nontemporal_store(v, d2 + i);
-  }
-  if (((n - head) & 1) && tid == 0) __builtin_nontemporal_store(src[n - 1], dst + n - 1);
-}
-
-// Split staging: issue() puts the first K 16-byte units per thread of x (and the node table) in
-// flight before the block's item / slot-table loads, commit() stores them to LDS afterwards, so the
-// staging's memory latency overlaps the item loads instead of following them. Units beyond K per
-// thread (problems larger than the bench's) go through stage16 in commit().
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-template <int BLOCK, bool NODES>
-struct XStage {
-  static constexpr int K = 3;   // named native-vector registers (HIP's uint4 class or an array goes to scratch)
-  u32x4_t x0 = {}, x1 = {}, x2 = {}, n0 = {}, n1 = {}, n2 = {};
-  bool aligned;
-  __device__ __forceinline__ void issue(const KParams& P, const double* xg) {
-    aligned = (reinterpret_cast<uintptr_t>(xg) & 15) == 0;
-    const int nx = P.n >> 1, i = threadIdx.x;
-    const u32x4_t* sx = reinterpret_cast<const u32x4_t*>(xg);
-    if (aligned) {
-      if (i < nx) x0 = sx[i];
-      if (i + BLOCK < nx) x1 = sx[i + BLOCK];
-      if (i + 2 * BLOCK < nx) x2 = sx[i + 2 * BLOCK];
-    }
-    if constexpr (NODES) {
-      const int nn = (P.n_nodecol + 3) >> 2;
-      const u32x4_t* sn = reinterpret_cast<const u32x4_t*>(P.nodecol);
-      if (i < nn) n0 = sn[i];
-      if (i + BLOCK < nn) n1 = sn[i + BLOCK];
-      if (i + 2 * BLOCK < nn) n2 = sn[i + 2 * BLOCK];
-    }
-  }
-  __device__ __forceinline__ void commit(const KParams& P, const double* xg, double* xs, int32_t* ns) {
-    const int nx = P.n >> 1, i = threadIdx.x;
-    if (aligned) {
-      u32x4_t* dx = reinterpret_cast<u32x4_t*>(xs);
-      if (i < nx) dx[i] = x0;
-      if (i + BLOCK < nx) dx[i + BLOCK] = x1;
-      if (i + 2 * BLOCK < nx) dx[i + 2 * BLOCK] = x2;
-      if (nx > K * BLOCK)
-        stage16<BLOCK>(reinterpret_cast<uint4*>(xs) + K * BLOCK, reinterpret_cast<const uint4*>(xg) + K * BLOCK, nx - K * BLOCK);
-      if ((P.n & 1) && threadIdx.x == 0) xs[P.n - 1] = xg[P.n - 1];
-    } else {
-      for (int k = threadIdx.x; k < P.n; k += BLOCK) xs[k] = xg[k];
-    }
-    if (threadIdx.x == 0) xs[P.n] = 0.0;
-    if constexpr (NODES) {
-      const int nn = (P.n_nodecol + 3) >> 2;
-      u32x4_t* dn = reinterpret_cast<u32x4_t*>(ns);
-      if (i < nn) dn[i] = n0;
-      if (i + BLOCK < nn) dn[i + BLOCK] = n1;
-      if (i + 2 * BLOCK < nn) dn[i + 2 * BLOCK] = n2;
-      if (nn > K * BLOCK)
-        stage16<BLOCK>(reinterpret_cast<uint4*>(ns) + K * BLOCK, reinterpret_cast<const uint4*>(P.nodecol) + K * BLOCK, nn - K * BLOCK);
-    }
-  }
-};
-
-// Zero-fill of a GAIT tile's CSR range in HBM by its own block (TileEmit DIRECT), 16-byte stores.
-// Plain stores: the scattered value stores that follow then mostly hit the same lines in L2.
-__device__ __forceinline__ void zero_out(double* __restrict__ dst, int n, int tid, int nthr) {
-  if (n <= 0) return;
-  const int head = (reinterpret_cast<uintptr_t>(dst) & 15) ? 1 : 0;
-  if (head && tid == 0) dst[0] = 0.0;
-  const int m = (n - head) >> 1;
-  dbl2_t* d2 = reinterpret_cast<dbl2_t*>(dst + head);
-  const dbl2_t z = {0.0, 0.0};
-  for (int i = tid; i < m; i += nthr) d2[i] = z;
-  if (((n - head) & 1) && tid == 0) dst[n - 1] = 0.0;
-}
-
-// zero n doubles of LDS (16-byte stores; n rounded up to even, the tile regions are even-sized)
-__device__ __forceinline__ void zero_lds(double* d, int n, int tid, int nthr) {
-  dbl2_t* d2 = reinterpret_cast<dbl2_t*>(d);
-  const dbl2_t z = {0.0, 0.0};
-  for (int i = tid; i < (n + 1) >> 1; i += nthr) d2[i] = z;
-}
-
-// global -> LDS staging of the problem's x (+ zero slot at n) and optionally the node table
-template <int BLOCK, bool NODES>
-__device__ __forceinline__ void stage_x(const KParams& P, const double* xg, double* xs, int32_t* ns) {
-  if ((reinterpret_cast<uintptr_t>(xg) & 15) == 0) {
-    stage16<BLOCK>(reinterpret_cast<uint4*>(xs), reinterpret_cast<const uint4*>(xg), P.n >> 1);
-    if ((P.n & 1) && threadIdx.x == 0) xs[P.n - 1] = xg[P.n - 1];
-  } else {
-    for (int i = threadIdx.x; i < P.n; i += BLOCK) xs[i] = xg[i];
-  }
-  if (threadIdx.x == 0) xs[P.n] = 0.0;
-  if constexpr (NODES)
-    stage16<BLOCK>(reinterpret_cast<uint4*>(ns), reinterpret_cast<const uint4*>(P.nodecol), (P.n_nodecol + 3) >> 2);
-}
-
 // One block = one tile (consecutive instances of one constraint kind) of one problem; one item per
 // thread, laid out so every wave runs a single code path. Blocks of one problem share an XCD (the
 // mapping below), so its ~9 KB x is fetched from HBM once and then served by that XCD's L2.
@@ -365,18 +201,6 @@ constexpr bool stages_nodes(int type, bool gait) { return gait || is_misc_kind(t
 // they stage after their item loads as before.
 constexpr bool early_stage(int type) { return type == IT_DYN || type == IT_FDISC; }
 
-// Phase timing (tools/phase_timing.py; only in the -DTOWR_PHASE_TIMING build, never in the product):
-// per block, 16 timestamps: [0] realtime start, [1] memtime start, [2] after staging, [3..6] each
-// wave's end of evaluation, [7] after the evaluation barrier, [8] end of wave 0's copy-out,
-// [9] realtime end.
-#ifdef TOWR_PHASE_TIMING
-__device__ unsigned long long* g_tbuf;
-#define TSTAMP(slot, v) do { if (g_tbuf && (threadIdx.x & 63) == 0) g_tbuf[(size_t)blockIdx.x * 16 + (slot)] = (v); } while (0)
-#define TS_MEM() ((unsigned long long)__builtin_amdgcn_s_memtime())
-#define TS_REAL() ((unsigned long long)__builtin_amdgcn_s_memrealtime())
-#else
-#define TSTAMP(slot, v) do { } while (0)
-#endif
 
 // Body of one tile block. TBLOCK = the tile's lane count (its slot-table stride), KBLOCK = the
 // launch's block size (>= TBLOCK): in the fused launch a 192-lane tile runs in a 256-thread block,
@@ -417,8 +241,10 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
   // FDISC / TQDISC lanes own whole rows (row-split), so there each wave zero-fills its own rows
   // after the staging instead (below), and waits for them only at its first value store.
   constexpr bool kWaveZero = GAIT && (TYPE == IT_FDISC || TYPE == IT_TQDISC);
+#ifndef TOWR_EXP_GAIT_NOZERO   // timing experiment only: no zero-fill
   if constexpr (GAIT && !kWaveZero)
     if (P.want_jac) zero_out(Vb + T.v0, T.v1 - T.v0, threadIdx.x, KBLOCK);
+#endif
   if constexpr (early_stage(TYPE)) xst.commit(P, xg, xs, ns);
   else stage_x<KBLOCK, stages_nodes(TYPE, GAIT)>(P, xg, xs, ns);
   towr_terrain_t* ters = reinterpret_cast<towr_terrain_t*>(gt + 16 * P.gt_n16 + 8 * P.gt_ntime);   // GAIT: the terrain
@@ -461,7 +287,11 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
     c.pdur = tm; c.pend = tm + P.n_pinfo; c.phend = tm + 2 * P.n_pinfo; c.ph_stride = P.ph_stride;
     c.ter = ters;   // LDS copy: no global load in the evaluation waits behind the zero-fill stores
     if constexpr (kWaveZero) {
+#ifdef TOWR_EXP_GAIT_NOZERO
+      if (false) {
+#else
       if (P.want_jac) {   // each lane's owned rows, zero-filled by its whole wave (512 B per store)
+#endif
         double* vt = Vb + T.v0;
         const int lane = threadIdx.x & 63;
         for (int l = 0; l < 64; ++l) {
@@ -473,7 +303,11 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
     }
   }
   DynG0 g0;   // DYN group 0 between its two phases
+#ifdef TOWR_EXP_GAIT_NOEVAL   // timing experiment only: staging + zero-fill, no evaluation
+  if (GAIT ? false : it.type == TYPE) {
+#else
   if (it.type == TYPE) {
+#endif
     if constexpr (TYPE == IT_DYN) {
       if (it.group == 0) dyn_g0_a(c, it, em, g0);
       else eval_dyn(c, it, em);   // group 1 and the endeffector groups (these deposit their sum terms)
@@ -768,7 +602,8 @@ const void* kernel_for(int type, bool gait, bool rotvec) {
   if (gait) return rotvec ? kernel_for_mode<true, true>(type) : kernel_for_mode<true, false>(type);
   return rotvec ? kernel_for_mode<false, true>(type) : kernel_for_mode<false, false>(type);
 }
-const void* kernel_for_class(int lc, bool gait, bool rotvec) {
+const void* kernel_for_class(int lc, bool gait, bool rotvec, bool fstream = false) {
+  if (lc == LC_FDISC && gait && fstream) return fs_stream_kernel();   // the stream kernel (B); A: fs_inst_kernel()
   if (lc == LC_MISC) return gait ? reinterpret_cast<const void*>(&towr_misc_kernel<true>) : reinterpret_cast<const void*>(&towr_misc_kernel<false>);
   return kernel_for(class_type(lc), gait, rotvec);
 }
@@ -804,6 +639,14 @@ struct towr_gpu_handle_s {
   ItemDirect* d_idir = nullptr;
   CostItem* d_citems = nullptr;
   double* d_cq = nullptr;
+  FsBlock* d_fsb = nullptr;    // streaming ForceConstraintDiscretized tables (layout.h FsBlock)
+  double* d_fs_t = nullptr;
+  int32_t* d_fs_tmpl = nullptr;
+  int32_t* d_fs_ws = nullptr;
+  int32_t* d_fs_iee = nullptr;
+  int32_t* d_fs_irow = nullptr;
+  double* d_fsrec = nullptr;   // per-problem instant records of the streaming path (scratch, grown on demand)
+  int64_t fsrec_cap = 0;       // problems it holds
   // fusion groups (TOWR_GPU_FUSE, see towr_step_kernel): classes that run in one launch
   struct FuseGroup {
     uint32_t mask = 0;        // bit lc: launch class lc belongs to the group
@@ -903,8 +746,18 @@ std::vector<uint4> gait_blob(const Layout& L) {
 }
 
 // LDS of a launch class: [tile region(s) | x + zero slot | node table | GAIT: PhaseSpline tables]
-size_t lds_region(const Layout& L, int lc) { return lc == LC_MISC ? (size_t)((L.misc_region + 1) & ~1) : (size_t)L.type_lds[class_type(lc)]; }
+// (the streaming ForceConstraintDiscretized path: its per-instant records and row template first)
+bool fstream_class(const Layout& L, int lc) { return lc == LC_FDISC && L.fstream; }
+size_t lds_region(const Layout& L, int lc) {
+  if (fstream_class(L, lc)) return fs_region(L);
+  return lc == LC_MISC ? (size_t)((L.misc_region + 1) & ~1) : (size_t)L.type_lds[class_type(lc)];
+}
+int class_block(const Layout& L, int lc) {
+  if (fstream_class(L, lc)) return kFsBlock;
+  return lc == LC_MISC ? 64 * kMiscWaves : L.type_block[class_type(lc)];
+}
 size_t lds_bytes(const Layout& L, int lc) {
+  if (fstream_class(L, lc)) return sizeof(double) * fs_region(L);   // the stream kernel (B) stages no x
   size_t d = lds_region(L, lc);
   d += (size_t)((L.n + 2) & ~1);                                                                  // x + zero slot
   if (lc == LC_MISC || stages_nodes(class_type(lc), L.gait)) d += (L.nodecol.size() + 3) / 4 * 2;  // node table (16-B units)
@@ -912,12 +765,18 @@ size_t lds_bytes(const Layout& L, int lc) {
     d += (size_t)gait_tables(L).n16 * 2 + gait_tables(L).n_time + (sizeof(towr_terrain_t) + 15) / 16 * 2;
   return sizeof(double) * d;
 }
-int class_units(const Layout& L, int lc) {   // tiles (or misc groups) per problem
+int class_units(const Layout& L, int lc) {   // tiles (or misc groups, or FsBlocks) per problem
   if (lc == LC_MISC) return (int)(L.misc_tiles.size() / kMiscWaves);
+  if (fstream_class(L, lc)) return (int)L.fs_blocks.size();
   const int t = class_type(lc);
   return L.type_tile0[t + 1] - L.type_tile0[t];
 }
 int64_t class_bytes(const Layout& L, int lc) { return lc == LC_MISC ? L.misc_bytes : L.type_bytes[class_type(lc)]; }
+// the streaming path's instant kernel (A): [x + zero slot | node table | PhaseSpline tables | timings | terrain]
+size_t fs_inst_lds_bytes(const Layout& L) {
+  return sizeof(double) * ((size_t)((L.n + 2) & ~1) + (L.nodecol.size() + 3) / 4 * 2 + (size_t)gait_tables(L).n16 * 2 +
+                           gait_tables(L).n_time + (sizeof(towr_terrain_t) + 15) / 16 * 2);
+}
 
 // RangeOfMotion + ForceConstraintDiscretized in one launch (both 192-lane, their registers and LDS
 // allow 3 blocks per CU either way). Measured on MI355X (ANYmal, B = 4096, 3 alternating runs each):
@@ -996,6 +855,8 @@ void fill_common(towr_gpu_handle h, KParams& P, int B, const double* X, int64_t 
   P.n_pinfo = (int32_t)L.pinfo.size();
   P.ph_stride = gt.ph_stride;
   P.gt_ntime = gt.n_time;
+  P.fsb = h->d_fsb; P.fs_t = h->d_fs_t; P.fs_tmpl = h->d_fs_tmpl; P.fs_ws = h->d_fs_ws;
+  P.fs_iee = h->d_fs_iee; P.fs_irow = h->d_fs_irow;
 }
 
 int launch_fused(towr_gpu_handle h, const towr_gpu_handle_s::FuseGroup& fg, int B, const double* X, int64_t ldx, double* G,
@@ -1011,6 +872,33 @@ int launch_fused(towr_gpu_handle h, const towr_gpu_handle_s::FuseGroup& fg, int 
   void* args[] = {&P};
   HIPCHK(h, hipLaunchKernel(step_kernel_for(L.gait, L.rotvec, fg.kblock), dim3((unsigned)grid), dim3((unsigned)fg.kblock),
                             args, fg.lds, s));
+  return TOWR_OK;
+}
+
+// The streaming ForceConstraintDiscretized path: instant kernel (A) into the handle's record scratch,
+// then the stream kernel (B) over the FsBlocks. P comes from fill_common with ntiles = FsBlocks.
+int launch_fstream(towr_gpu_handle h, KParams& P, hipStream_t st) {
+  const Layout& L = h->L;
+  const int B = P.B;
+  const int32_t ni = (int32_t)L.fs_t.size();
+  const int64_t ldr = fs_record_doubles() * ni;
+  if (h->fsrec_cap < B) {
+    if (h->d_fsrec) { (void)hipFree(h->d_fsrec); h->d_fsrec = nullptr; h->fsrec_cap = 0; }
+    HIPCHK(h, hipMalloc(&h->d_fsrec, sizeof(double) * (size_t)B * ldr));
+    h->fsrec_cap = B;
+  }
+  P.lds_x_off = 0;
+  double* rec = h->d_fsrec;
+  int64_t ldr_a = ldr;
+  int32_t ni_a = ni;
+  void* aa[] = {&P, &rec, &ldr_a, &ni_a};
+  HIPCHK(h, hipLaunchKernel(fs_inst_kernel(), dim3((unsigned)B), dim3(fs_inst_block()), aa, fs_inst_lds_bytes(L), st));
+  const int64_t total = (int64_t)B * P.ntiles;
+  const int64_t grid = ((total + 7) / 8) * 8;
+  if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
+  const double* crec = rec;
+  void* ab[] = {&P, const_cast<double**>(&crec), &ldr_a, &ni_a};
+  HIPCHK(h, hipLaunchKernel(fs_stream_kernel(), dim3((unsigned)grid), dim3(kFsBlock), ab, sizeof(double) * fs_region(L), st));
   return TOWR_OK;
 }
 
@@ -1042,6 +930,10 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
     KParams P{};
     fill_common(h, P, B, X, ldx, G, ldg, V, ldv, want_g, want_jac, terrains, per_problem);
     P.ntiles = nt;
+    if (fstream_class(L, lc)) {
+      if (int rc = launch_fstream(h, P, st)) return rc;
+      continue;
+    }
     if (lc == LC_MISC) {
       P.tile0 = 0;
       P.misc_tiles = h->d_misc; P.misc_lds = h->d_misc_lds;
@@ -1057,9 +949,9 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
     const int64_t total = (int64_t)B * nt;
     const int64_t grid = ((total + 7) / 8) * 8;
     if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
-    const int block = lc == LC_MISC ? 64 * kMiscWaves : L.type_block[class_type(lc)];
+    const int block = class_block(L, lc);
     void* args[] = {&P};
-    HIPCHK(h, hipLaunchKernel(kernel_for_class(lc, L.gait, L.rotvec), dim3((unsigned)grid), dim3((unsigned)block), args,
+    HIPCHK(h, hipLaunchKernel(kernel_for_class(lc, L.gait, L.rotvec, L.fstream), dim3((unsigned)grid), dim3((unsigned)block), args,
                               lds_bytes(L, lc), st));
   }
   for (int i = 0; i < nside; ++i) {
@@ -1250,13 +1142,14 @@ int towr_gpu_abi_version(void) { return TOWR_GPU_ABI_VERSION; }
 int towr_gpu_debug_occupancy(towr_gpu_handle h, int32_t lc) {
   const Layout& L = h->L;
   if (lc < 0 || lc >= LC_COUNT || class_units(L, lc) == 0) return -1;
-  const int block = lc == LC_MISC ? 64 * kMiscWaves : L.type_block[class_type(lc)];
+  const int block = class_block(L, lc);
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel_for_class(lc, L.gait, L.rotvec), block, lds_bytes(L, lc)) != hipSuccess) return -2;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel_for_class(lc, L.gait, L.rotvec, L.fstream), block, lds_bytes(L, lc)) != hipSuccess) return -2;
   return n * 1000 + (int)(lds_bytes(L, lc) / 1024);
 }
 int towr_gpu_debug_set_timing_buffer(void* p) {
   unsigned long long* v = reinterpret_cast<unsigned long long*>(p);
+  if (fs_set_timing_buffer(p) != hipSuccess) return TOWR_ERR_HIP;
   return hipMemcpyToSymbol(HIP_SYMBOL(g_tbuf), &v, sizeof(v)) == hipSuccess ? 0 : TOWR_ERR_HIP;
 }
 #endif
@@ -1308,7 +1201,9 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
       (r = upload(h, &h->d_pinfo, L.pinfo)) || (r = upload(h, &h->d_pcols, L.pcols)) || (r = upload(h, &h->d_pact, L.pact)) || (r = upload(h, &h->d_sched, L.sched)) ||
       (r = upload(h, &h->d_misc, L.misc_tiles)) || (r = upload(h, &h->d_misc_lds, L.misc_lds)) || (r = upload(h, &h->d_eelin, L.eelin)) ||
       (r = upload(h, &h->d_citems, L.cost_items)) || (r = upload(h, &h->d_cq, L.cost_q)) || (r = upload(h, &h->d_gtab, gait_blob(L))) ||
-      (r = upload(h, &h->d_idir, L.idirect)))
+      (r = upload(h, &h->d_idir, L.idirect)) || (r = upload(h, &h->d_fsb, L.fs_blocks)) || (r = upload(h, &h->d_fs_t, L.fs_t)) ||
+      (r = upload(h, &h->d_fs_tmpl, L.fs_tmpl)) || (r = upload(h, &h->d_fs_ws, L.fs_ws)) ||
+      (r = upload(h, &h->d_fs_iee, L.fs_iee)) || (r = upload(h, &h->d_fs_irow, L.fs_irow)))
     return bail(r);
   {   // trajectory export: phase durations of the description (fixed gait), counts, contact at start
     const towr_problem_desc_t& d = L.desc;
@@ -1373,7 +1268,15 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
     if (class_units(L, lc) == 0) continue;
     const size_t lds = lds_bytes(L, lc);
     if (lds > 160 * 1024) { h->err = "tile too large for LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
-    if (lds > 64 * 1024 && hipFuncSetAttribute(kernel_for_class(lc, L.gait, L.rotvec), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+    if (lds > 64 * 1024 && hipFuncSetAttribute(kernel_for_class(lc, L.gait, L.rotvec, L.fstream), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+      h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
+    }
+  }
+  if (L.fstream) {
+    const size_t lds = fs_inst_lds_bytes(L);
+    if (lds > 160 * 1024) { h->err = "problem too large for the streaming instant kernel's LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
+    if (lds > 64 * 1024 && hipFuncSetAttribute(fs_inst_kernel(),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
       h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
     }
   }
@@ -1395,7 +1298,8 @@ int towr_gpu_destroy(towr_gpu_handle h) {
   void* dev[] = {h->d_items, h->d_slots, h->d_tiles, h->d_nodecol, h->d_spl, h->d_dur, h->d_segs, h->d_terrain,
                  h->d_pinfo, h->d_pcols, h->d_pact, h->d_sched, h->d_misc, h->d_misc_lds, h->d_eelin, h->d_gtab, h->d_idir, h->d_citems, h->d_cq, h->fuse[0].d_units, h->fuse[1].d_units,
                  h->d_bterrain, h->d_x, h->d_g, h->d_v, h->d_f, h->d_grad,
-                 h->d_traj_pd, h->d_traj_n, h->d_traj_c0, h->d_traj_t};
+                 h->d_traj_pd, h->d_traj_n, h->d_traj_c0, h->d_traj_t, h->d_fsb, h->d_fs_t, h->d_fs_tmpl, h->d_fs_ws,
+                 h->d_fs_iee, h->d_fs_irow, h->d_fsrec};
   if (h->device >= 0) for (void* p : dev) if (p) (void)hipFree(p);
   void* host[] = {h->h_x, h->h_g, h->h_v};
   for (void* p : host) if (p) (void)hipHostFree(p);
