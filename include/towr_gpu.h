@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TOWR_GPU_ABI_VERSION 3
+#define TOWR_GPU_ABI_VERSION 4
 
 #define TOWR_MAX_EE          4
 #define TOWR_MAX_PHASES      48
@@ -109,10 +109,20 @@ enum towr_constraint_kind {
                                      p[4] = k_friction                     (torque_constraint_discretized.cc:69-235) */
   TOWR_C_TORQUE           = 11, /* TorqueConstraint (node-based) ee; p[0..4] as above      (torque_constraint.cc:36-194)  */
   TOWR_C_TERRAIN_HARD     = 12, /* TerrainConstraintHard       ee; T; dt              (terrain_constraint_hard.cc:35-132)       */
-  TOWR_C_EE_LINEAR        = 13  /* EELinearConstraint          T; dt; ip[0] = target (0 motion, 1 ang), ip[1] = deriv (0 pos,
+  TOWR_C_EE_LINEAR        = 13, /* EELinearConstraint          T; dt; ip[0] = target (0 motion, 1 ang), ip[1] = deriv (0 pos,
                                      1 vel), ip[2] = n_terms (<= 6), ip[3 + i] = ee_i * 3 + dim_i; p[i] = coeff_i;
                                      (ee_linear_constraint.cc:5-48; the bound tolerance is setup data, not used here)  */
+  TOWR_C_LINEAR_EQ        = 14  /* LinearEqualityConstraint    g = M x_set (linear_constraint.cc:35-80): ip[0] = variable set
+                                     (index in AddVariableSet order), ip[1] = rows of M; M itself is side data
+                                     TOWR_DATA_LINEAR_M (towr_gpu_create_ex). Jacobian = M.sparseView(): the nonzeros of M.
+                                     The offset v only enters the bounds (-v), which stay with the caller            */
 };
+
+/* Role of a constraint set in the description:
+ *   TOWR_ROLE_HARD: an ifopt constraint set (AddConstraintSet) — its rows are part of g and J;
+ *   TOWR_ROLE_SOFT: only wrapped by a SoftConstraint cost term (AddCostSet(SoftConstraint(c)),
+ *                   soft_constraint.cc:34-69) — not part of g / J; the cost term evaluates it.       */
+enum towr_constraint_role { TOWR_ROLE_HARD = 0, TOWR_ROLE_SOFT = 1 };
 
 typedef struct {
   int32_t kind;   /* towr_constraint_kind                                                       */
@@ -120,8 +130,8 @@ typedef struct {
   double  T;      /* total horizon the constraint was constructed with                         */
   double  dt;     /* discretisation step of TimeDiscretizationConstraint subclasses            */
   double  p[6];   /* per-kind parameters (see enum)                                            */
-  int32_t ip[9];  /* per-kind integer parameters (EELinear)                                    */
-  int32_t reserved;
+  int32_t ip[9];  /* per-kind integer parameters (EELinear, LinearEquality)                     */
+  int32_t role;   /* towr_constraint_role (0 = hard)                                            */
 } towr_constraint_t;
 
 /* ---- cost terms: NlpFormulation::GetCosts (nlp_formulation.cc:604-680) ------------------------ */
@@ -130,7 +140,13 @@ enum towr_cost_kind {
                                 (0 pos, 1 vel), ip[2] = dim; weight             (node_cost.cc:36-79)       */
   TOWR_COST_ENERGY      = 1, /* EnergyCost: weight, dt, p[0] = torque weight   (energy_cost.cc:36-152)    */
   TOWR_COST_ANG_MOMENTUM= 2, /* AngularMomentumCost: weight, dt                 (angular_momentum_cost.cc:39-208) */
-  TOWR_COST_EE_BASE_POS = 3  /* EEBasePosCost: ee, weight, dt, p[0..2] = p_ref_B  (ee_base_pos_cost.cc:38-162) */
+  TOWR_COST_EE_BASE_POS = 3, /* EEBasePosCost: ee, weight, dt, p[0..2] = p_ref_B  (ee_base_pos_cost.cc:38-162) */
+  TOWR_COST_BASE_HEIGHT = 4, /* BaseHeightCost of the fork: weight, dt (the reference's default 0.01 must be given),
+                                p[0] = target base height above the mean stance-foot height
+                                (base_height_cost.cc:36-142, added by hand in test/biped_example.cc:199-203)     */
+  TOWR_COST_SOFT        = 5  /* SoftConstraint: 0.5 (g - b)^T (g - b) over constraint set ip[0] (any role), b = mid-point
+                                of its bounds, given as side data TOWR_DATA_SOFT_BOUNDS (soft_constraint.cc:34-69);
+                                W = identity as in the reference (no weight: `weight` is ignored)                 */
 };
 typedef struct {
   int32_t kind;    /* towr_cost_kind                                                             */
@@ -185,12 +201,31 @@ typedef struct {
 
 typedef struct towr_gpu_handle_s* towr_gpu_handle;
 
+/* ---- side data: what the POD description cannot hold (towr_gpu_create_ex) --------------------- */
+enum towr_data_kind {
+  TOWR_DATA_LINEAR_M    = 0, /* index = constraint (TOWR_C_LINEAR_EQ); count = rows * n_set; data = M row-major
+                                (LinearEqualityConstraint::M_, linear_constraint.cc:35-45)                       */
+  TOWR_DATA_SOFT_BOUNDS = 1  /* index = cost term (TOWR_COST_SOFT); count = 2 * rows of the wrapped set;
+                                data = lower[0..rows-1], upper[0..rows-1] = the wrapped set's GetBounds(), from
+                                which the engine forms b = (upper + lower) / 2 as SoftConstraint's ctor does  */
+};
+typedef struct {
+  int32_t       kind;    /* towr_data_kind                                                          */
+  int32_t       index;   /* constraint or cost index in the description                             */
+  int64_t       count;   /* doubles at `data`                                                       */
+  const double* data;    /* host memory, copied at creation                                         */
+} towr_data_t;
+
 /* ---- lifecycle ------------------------------------------------------------------------------- */
 /* Builds the layout (variable maps, time grids, CSR pattern, per-item slot tables) on the host and
  * uploads it to `device`. device < 0 creates a layout-only handle (sizes, structure, x0; every
  * evaluation entry point then returns TOWR_ERR_NO_DEVICE) — used by host-side structure checks. Replaces NlpFormulation::GetVariableSets/GetConstraints + ifopt
  * Problem::AddVariableSet/AddConstraintSet (nlp_formulation.cc:76-378, hopper_example.cc:154-161). */
 int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle* out);
+/* Same, with side data (LinearEqualityConstraint matrices, SoftConstraint bounds); every
+ * TOWR_C_LINEAR_EQ set and TOWR_COST_SOFT term needs its entry (else TOWR_ERR_INVALID).            */
+int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const towr_data_t* data, int device,
+                       towr_gpu_handle* out);
 int towr_gpu_destroy(towr_gpu_handle h);
 const char* towr_gpu_last_error(towr_gpu_handle h);   /* h may be NULL: last global error         */
 int towr_gpu_abi_version(void);

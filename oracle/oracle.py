@@ -33,6 +33,8 @@ def lib(native=False):
         D, I, Lg = C.POINTER(C.c_double), C.POINTER(C.c_int), C.POINTER(C.c_long)
         L.oracle_create.restype = C.c_void_p
         L.oracle_create.argtypes = [C.POINTER(capi.ProblemDesc), C.c_char_p, C.c_int]
+        L.oracle_create_ex.restype = C.c_void_p
+        L.oracle_create_ex.argtypes = [C.POINTER(capi.ProblemDesc), C.c_int, C.POINTER(capi.SideData), C.c_char_p, C.c_int]
         L.oracle_destroy.argtypes = [C.c_void_p]
         L.oracle_sizes.argtypes = [C.c_void_p, I, I]
         L.oracle_initial_x.argtypes = [C.c_void_p, D]
@@ -61,12 +63,14 @@ def _i(a):
 
 
 class Oracle:
-    """ifopt::Problem-shaped view of the CPU restatement."""
+    """ifopt::Problem-shaped view of the CPU restatement. `data`: side data as for towr_gpu_create_ex,
+    a list of (towr_data_kind, index, float64 array)."""
 
-    def __init__(self, desc: capi.ProblemDesc):
+    def __init__(self, desc: capi.ProblemDesc, data=None):
         self.desc = desc
         err = C.create_string_buffer(256)
-        self.h = lib().oracle_create(C.byref(desc), err, 256)
+        arr, self._keep = capi.side_data(data)
+        self.h = lib().oracle_create_ex(C.byref(desc), len(data or []), arr, err, 256)
         if not self.h:
             raise ValueError("oracle_create failed: " + err.value.decode())
         n, m = C.c_int(), C.c_int()

@@ -1293,6 +1293,8 @@ typedef struct {
   int n_ids; int* ids;             /* node ids (force/terrain/swing/base-height)           */
   /* SplineAccConstraint (spline_acc_constraint.cc:34-46) */
   const Spline* acc_spline; int acc_varset_kind; int n_junctions; double* acc_T;
+  int role;                        /* towr_constraint_role: soft sets are not part of g / J     */
+  int lin_vs; double* lin_M;       /* LinearEqualityConstraint: variable set index, M (rows x n_set) */
 } Cons;
 
 struct oracle_s {
@@ -1307,6 +1309,8 @@ struct oracle_s {
   int n_vs; VarSet vs[TOWR_MAX_VARSETS];
   int n_cons; Cons cons[TOWR_MAX_CONSTRAINTS];
   int n, m;
+  double* x;                        /* the current x (LinearEqualityConstraint reads its set's values) */
+  double* soft_b[TOWR_MAX_COSTS];   /* SoftConstraint terms: b = (upper + lower) / 2 per wrapped row   */
 };
 
 /* TimeDiscretizationConstraint ctor, time_discretization_constraint.cc:37-50 */
@@ -1480,6 +1484,16 @@ static void cons_values(oracle_t* o, const Cons* c, double* g) {
       const PhaseDur* p = o->pd[c->ee]; double s = 0.0;
       for (int i = 0; i < p->n - 1; ++i) s += p->d[i];
       g[0] = s;
+      break;
+    }
+    case TOWR_C_LINEAR_EQ: {      /* linear_constraint.cc:47-52: M * (the set's values), dense */
+      const VarSet* v = &o->vs[c->lin_vs];
+      const double* xs = o->x + v->col0;
+      for (int i = 0; i < c->rows; ++i) {
+        double s = 0.0;
+        for (int j = 0; j < v->n; ++j) s += c->lin_M[(size_t)i * v->n + j] * xs[j];
+        g[i] = s;
+      }
       break;
     }
   }
@@ -1864,11 +1878,20 @@ static void cons_fill_jac(oracle_t* o, const Cons* c, const VarSet* v, spmat* ja
       if (vs_is(v, TOWR_VAR_EE_SCHEDULE, c->ee))
         for (int col = 0; col < o->pd[c->ee]->n - 1; ++col) *sp_coeffref(jac, 0, col) = 1.0;
       break;
+    case TOWR_C_LINEAR_EQ:         /* linear_constraint.cc:68-76: jac = M.sparseView() (exact zeros pruned) */
+      if (v == &o->vs[c->lin_vs])
+        for (int i = 0; i < c->rows; ++i)
+          for (int j = 0; j < v->n; ++j) {
+            const double mij = c->lin_M[(size_t)i * v->n + j];
+            if (mij != 0.0) *sp_coeffref(jac, i, j) = mij;
+          }
+      break;
   }
 }
 
 /* ifopt Composite::SetVariables -> each VariableSet::SetVariables */
 static void set_variables(oracle_t* o, const double* x) {
+  memcpy(o->x, x, sizeof(double) * (size_t)o->n);
   for (int i = 0; i < o->n_vs; ++i) {
     VarSet* v = &o->vs[i];
     if (v->nv) nv_set_variables(v->nv, x + v->col0);
@@ -1906,6 +1929,7 @@ static void build_jacobian(oracle_t* o, TripList* all) {
   all->n = 0;
   for (int ci = 0; ci < o->n_cons; ++ci) {
     Cons* c = &o->cons[ci];
+    if (c->role == TOWR_ROLE_SOFT) continue;   /* wrapped by a SoftConstraint cost only */
     TripList L = {0, 0, 0};
     for (int vi = 0; vi < o->n_vs; ++vi) {
       VarSet* v = &o->vs[vi];
@@ -1927,8 +1951,16 @@ static void build_jacobian(oracle_t* o, TripList* all) {
  * ==========================================================================================*/
 static void set_err(char* err, int len, const char* msg) { if (err && len > 0) { snprintf(err, (size_t)len, "%s", msg); } }
 
-oracle_t* oracle_create(const towr_problem_desc_t* d, char* err, int errlen) {
+oracle_t* oracle_create(const towr_problem_desc_t* d, char* err, int errlen) { return oracle_create_ex(d, 0, NULL, err, errlen); }
+
+static const towr_data_t* find_data(int n_data, const towr_data_t* data, int kind, int index) {
+  for (int i = 0; i < n_data; ++i) if (data[i].kind == kind && data[i].index == index) return &data[i];
+  return NULL;
+}
+
+oracle_t* oracle_create_ex(const towr_problem_desc_t* d, int n_data, const towr_data_t* data, char* err, int errlen) {
   if (!d || d->abi_version != TOWR_GPU_ABI_VERSION) { set_err(err, errlen, "bad abi version"); return NULL; }
+  if (n_data < 0 || (n_data > 0 && !data)) { set_err(err, errlen, "bad side data"); return NULL; }
   if (d->angular_rep != 0 && d->angular_rep != 1) { set_err(err, errlen, "angular_rep must be 0 (EulerZYX) or 1 (RotationVector)"); return NULL; }
   int E = d->robot.n_ee;
   if (E < 1 || E > MAXE) { set_err(err, errlen, "bad n_ee"); return NULL; }
@@ -2035,12 +2067,15 @@ oracle_t* oracle_create(const towr_problem_desc_t* d, char* err, int errlen) {
     v->col0 = col; col += v->n;
   }
   o->n = col;
+  o->x = (double*)calloc((size_t)(col > 0 ? col : 1), sizeof(double));
 
   /* ---- cost terms ---- */
   if (d->n_costs < 0 || d->n_costs > TOWR_MAX_COSTS) { set_err(err, errlen, "bad n_costs"); oracle_destroy(o); return NULL; }
   for (int i = 0; i < d->n_costs; ++i) {
     const towr_cost_t* c = &d->costs[i];
-    int ok = c->kind >= TOWR_COST_NODE && c->kind <= TOWR_COST_EE_BASE_POS;
+    int ok = c->kind >= TOWR_COST_NODE && c->kind <= TOWR_COST_SOFT;
+    if (c->kind == TOWR_COST_BASE_HEIGHT) ok = ok && c->dt > 0.0;   /* the reference loops forever otherwise */
+    if (c->kind == TOWR_COST_SOFT) ok = ok && c->ip[0] >= 0 && c->ip[0] < d->n_constraints;
     if (c->kind == TOWR_COST_NODE)
       ok = ok && c->ip[0] >= TOWR_VAR_BASE_LIN && c->ip[0] <= TOWR_VAR_EE_TORQUE && c->ip[1] >= 0 && c->ip[1] <= 1 &&
            c->ip[2] >= 0 && c->ip[2] <= 2 && (c->ip[0] <= TOWR_VAR_BASE_ANG || (c->ee >= 0 && c->ee < E));
@@ -2057,6 +2092,8 @@ oracle_t* oracle_create(const towr_problem_desc_t* d, char* err, int errlen) {
     c->kind = s->kind; c->ee = s->ee; c->T = s->T; c->dt = s->dt;
     memcpy(c->p, s->p, sizeof(c->p));
     memcpy(c->ip, s->ip, sizeof(c->ip));
+    c->role = s->role;
+    if (c->role != TOWR_ROLE_HARD && c->role != TOWR_ROLE_SOFT) { set_err(err, errlen, "bad constraint role"); oracle_destroy(o); return NULL; }
     switch (c->kind) {
       case TOWR_C_TORQUE_DISCRETIZED: make_dts(c); c->rows = 4 * c->n_dts; break;      /* torque_constraint_discretized.cc:92-93 */
       case TOWR_C_TERRAIN_HARD: make_dts(c); c->rows = c->n_dts; break;                /* terrain_constraint_hard.cc:47 */
@@ -2115,11 +2152,30 @@ oracle_t* oracle_create(const towr_problem_desc_t* d, char* err, int errlen) {
         break;
       }
       case TOWR_C_TOTAL_DURATION: c->rows = 1; break;
+      case TOWR_C_LINEAR_EQ: {    /* LinearEqualityConstraint ctor, linear_constraint.cc:35-45 */
+        const towr_data_t* m = find_data(n_data, data, TOWR_DATA_LINEAR_M, i);
+        if (c->ip[0] < 0 || c->ip[0] >= o->n_vs || c->ip[1] < 0 || !m || !m->data ||
+            m->count != (int64_t)c->ip[1] * o->vs[c->ip[0]].n) { set_err(err, errlen, "bad LinearEquality constraint or matrix"); oracle_destroy(o); return NULL; }
+        c->lin_vs = c->ip[0]; c->rows = c->ip[1];
+        c->lin_M = (double*)malloc(sizeof(double) * (size_t)(m->count > 0 ? m->count : 1));
+        memcpy(c->lin_M, m->data, sizeof(double) * (size_t)m->count);
+        break;
+      }
       default: set_err(err, errlen, "unsupported constraint kind"); oracle_destroy(o); return NULL;
     }
+    if (c->role == TOWR_ROLE_SOFT) { c->row0 = -1; continue; }   /* not a row block of g */
     c->row0 = row; row += c->rows;
   }
   o->m = row;
+  /* SoftConstraint ctor (soft_constraint.cc:34-50): b = (upper + lower) / 2 of the wrapped set */
+  for (int i = 0; i < d->n_costs; ++i) {
+    if (d->costs[i].kind != TOWR_COST_SOFT) continue;
+    const Cons* w = &o->cons[d->costs[i].ip[0]];
+    const towr_data_t* b = find_data(n_data, data, TOWR_DATA_SOFT_BOUNDS, i);
+    if (!b || !b->data || b->count != 2 * (int64_t)w->rows) { set_err(err, errlen, "SoftConstraint term without bounds of its set's size"); oracle_destroy(o); return NULL; }
+    o->soft_b[i] = (double*)malloc(sizeof(double) * (size_t)(w->rows > 0 ? w->rows : 1));
+    for (int r = 0; r < w->rows; ++r) o->soft_b[i][r] = (b->data[w->rows + r] + b->data[r]) / 2.;
+  }
   return o;
 }
 
@@ -2128,7 +2184,9 @@ static void spline_free(Spline* s) { if (!s) return; free(s->polys); sp_free(&s-
 
 void oracle_destroy(oracle_t* o) {
   if (!o) return;
-  for (int i = 0; i < o->n_cons; ++i) { free(o->cons[i].dts); free(o->cons[i].ids); free(o->cons[i].acc_T); }
+  for (int i = 0; i < o->n_cons; ++i) { free(o->cons[i].dts); free(o->cons[i].ids); free(o->cons[i].acc_T); free(o->cons[i].lin_M); }
+  for (int i = 0; i < TOWR_MAX_COSTS; ++i) free(o->soft_b[i]);
+  free(o->x);
   spline_free(o->s_lin); spline_free(o->s_ang);
   for (int ee = 0; ee < MAXE; ++ee) {
     spline_free(o->s_motion[ee]); spline_free(o->s_ang_ee[ee]); spline_free(o->s_force[ee]); spline_free(o->s_torque[ee]);
@@ -2189,7 +2247,8 @@ static void grad_add_rows(double* grad, int col0, const spmat* J, const double m
 }
 
 /* value of one term, and (grad != NULL) its gradient added into grad */
-static double cost_term(oracle_t* o, const towr_cost_t* c, double* grad) {
+static double cost_term(oracle_t* o, int ci, double* grad) {
+  const towr_cost_t* c = &o->d.costs[ci];
   double cost = 0.0;   /* NodeCost::GetCost leaves its accumulator uninitialised (node_cost.cc:58): 0 here */
   switch (c->kind) {
     case TOWR_COST_NODE: {          /* node_cost.cc:55-79 */
@@ -2304,6 +2363,51 @@ static double cost_term(oracle_t* o, const towr_cost_t* c, double* grad) {
       free(ts);
       break;
     }
+    case TOWR_COST_BASE_HEIGHT: {   /* base_height_cost.cc:55-142 (the fork's biped driver, test/biped_example.cc:199) */
+      /* GetCost / FillJacobianBlock: t = 0, dt, ... (accumulated) while t <= T + 1e-9, T = base_linear_->GetTotalTime() */
+      double* ts; int nt = cost_times(o, c->dt, &ts);
+      const double dt = c->dt, w = c->weight, th = c->p[0];
+      int col0 = varset_col0(o, TOWR_VAR_BASE_LIN, 0);
+      for (int k = 0; k < nt; ++k) {
+        const double t = ts[k];
+        double b[3][3]; spline_point(o->s_lin, t, b);
+        /* GetSupportPointAverageHeight (:100-125): mean z of the feet in contact, else the terrain
+         * height under the base */
+        double total = 0.0; int cnt = 0;
+        for (int ee = 0; ee < o->n_ee; ++ee)
+          if (pd_is_contact(o->pd[ee], t)) { double pe[3][3]; spline_point(o->s_motion[ee], t, pe); total += pe[kPos][Z]; cnt++; }
+        const double avg = cnt == 0 ? ter_h(&o->terrain, b[kPos][X], b[kPos][Y]) : total / cnt;
+        const double dev = b[kPos][Z] - (avg + th);   /* GetHeightDeviation (:88-98) */
+        cost += w * dev * dev * dt;
+        if (!grad || col0 < 0) continue;
+        /* FillJacobianBlock (:70-86): base-lin only, 2 w dev dt * d p_z / d nodes; the dependence of the
+         * target on the feet and the terrain is not differentiated (reference behaviour) */
+        spmat J = spline_jac(o->s_lin, t, kPos);
+        const double s2 = 2.0 * w * dev * dt;
+        for (int q = 0; q < J.r[Z].n; ++q) grad[col0 + J.r[Z].e[q].col] += s2 * J.r[Z].e[q].val;
+        sp_free(&J);
+      }
+      free(ts);
+      break;
+    }
+    case TOWR_COST_SOFT: {          /* soft_constraint.cc:52-69: 0.5 (g-b)^T W (g-b), gradient J^T W (g-b), W = 1 */
+      const Cons* w = &o->cons[c->ip[0]];
+      const double* b = o->soft_b[ci];
+      double* g = (double*)calloc((size_t)(w->rows > 0 ? w->rows : 1), sizeof(double));
+      cons_values(o, w, g);
+      for (int r = 0; r < w->rows; ++r) { g[r] -= b[r]; cost += (0.5 * g[r]) * g[r]; }
+      if (grad)   /* constraint_->GetJacobian(): every variable set's block */
+        for (int vi = 0; vi < o->n_vs; ++vi) {
+          VarSet* v = &o->vs[vi];
+          spmat jac = sp_zero(w->rows, v->n);
+          cons_fill_jac(o, w, v, &jac);
+          for (int r = 0; r < jac.rows; ++r)
+            for (int q = 0; q < jac.r[r].n; ++q) grad[v->col0 + jac.r[r].e[q].col] += jac.r[r].e[q].val * g[r];
+          sp_free(&jac);
+        }
+      free(g);
+      break;
+    }
   }
   return cost;
 }
@@ -2311,7 +2415,7 @@ static double cost_term(oracle_t* o, const towr_cost_t* c, double* grad) {
 int oracle_eval_f(oracle_t* o, const double* x, double* f) {
   set_variables(o, x);
   double s = 0.0;
-  for (int i = 0; i < o->d.n_costs; ++i) s += cost_term(o, &o->d.costs[i], NULL);
+  for (int i = 0; i < o->d.n_costs; ++i) s += cost_term(o, i, NULL);
   *f = s;
   return 0;
 }
@@ -2319,7 +2423,7 @@ int oracle_eval_f(oracle_t* o, const double* x, double* f) {
 int oracle_eval_grad_f(oracle_t* o, const double* x, double* grad) {
   set_variables(o, x);
   for (int j = 0; j < o->n; ++j) grad[j] = 0.0;
-  for (int i = 0; i < o->d.n_costs; ++i) cost_term(o, &o->d.costs[i], grad);
+  for (int i = 0; i < o->d.n_costs; ++i) cost_term(o, i, grad);
   return 0;
 }
 
@@ -2371,7 +2475,8 @@ int oracle_initial_x(oracle_t* o, double* x0) {
 
 int oracle_eval_g(oracle_t* o, const double* x, double* g) {
   set_variables(o, x);
-  for (int i = 0; i < o->n_cons; ++i) cons_values(o, &o->cons[i], g + o->cons[i].row0);
+  for (int i = 0; i < o->n_cons; ++i)
+    if (o->cons[i].role != TOWR_ROLE_SOFT) cons_values(o, &o->cons[i], g + o->cons[i].row0);
   return g_segment_overflow ? 1 : 0;
 }
 

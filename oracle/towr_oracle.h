@@ -27,6 +27,8 @@ extern "C" {
 typedef struct oracle_s oracle_t;
 
 oracle_t* oracle_create(const towr_problem_desc_t* desc, char* err, int errlen);
+/* with side data (LinearEqualityConstraint M, SoftConstraint bounds), as towr_gpu_create_ex      */
+oracle_t* oracle_create_ex(const towr_problem_desc_t* desc, int n_data, const towr_data_t* data, char* err, int errlen);
 void      oracle_destroy(oracle_t* o);
 int       oracle_sizes(oracle_t* o, int* n, int* m);
 int       oracle_initial_x(oracle_t* o, double* x0);

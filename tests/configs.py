@@ -1,4 +1,6 @@
 """The BASELINE.json configurations as ProblemDescs (+ extra parity cases)."""
+import math
+
 from towr2025_amd import formulation as F
 
 
@@ -128,3 +130,101 @@ def cost_descs():
 def _gaitopt_f(f):
     f.params_.OptimizePhaseDurations()
     return f
+
+
+# ---- LinearEqualityConstraint, BaseHeightCost, SoftConstraint (VERDICT r1 "missing" 1-2) ----------
+def _varset_cols(desc):
+    """[(col0, n)] of the description's variable sets (a layout-only handle: no GPU)."""
+    from towr2025_amd import TowrGpuProblem
+    p = TowrGpuProblem(desc, device=-1)
+    return [(c0, n) for (_, _, c0, n) in p.varset_info()]
+
+
+def _sparse_matrix(rows, cols, seed, density=0.3, zero_row=None):
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    M = rng.standard_normal((rows, cols)) * (rng.random((rows, cols)) < density)
+    if zero_row is not None:
+        M[zero_row] = 0.0
+    return M
+
+
+def _soft_bounds(rows, seed):
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    lo = -rng.random(rows)
+    return np.concatenate([lo, lo + 2.0 * rng.random(rows)])
+
+
+def _biped_example_costs(f, target, with_nodes=True):
+    """The cost list of towr/test/biped_example.cc:196-215: BaseHeightCost(target, 1e-1, dt 0.01) and
+    NodeCosts on the base motion."""
+    from towr2025_amd import _capi as capi
+    costs = [dict(kind=capi.COST_BASE_HEIGHT, weight=1e-1, dt=0.01, p=[target])]
+    if with_nodes:
+        for dim, w in ((0, 1e-4), (1, 1e-2), (2, 1e-3)):
+            costs.append(dict(kind=capi.COST_NODE, weight=w, ip=[capi.VAR_BASE_LIN, 1, dim]))
+        for dim in range(3):
+            costs.append(dict(kind=capi.COST_NODE, weight=1e-3, ip=[capi.VAR_BASE_ANG, 0, dim]))
+            costs.append(dict(kind=capi.COST_NODE, weight=1e-4, ip=[capi.VAR_BASE_ANG, 1, dim]))
+    return costs
+
+
+def ext_cases():
+    """name -> (ProblemDesc, side data [(towr_data_kind, index, array)]) for the LinearEquality
+    constraint, the fork's BaseHeightCost and SoftConstraint terms."""
+    from towr2025_amd import _capi as capi
+    out = {}
+    # LinearEqualityConstraint on base-lin (a zero row of M) and on an ee-motion set, procedural monoped
+    f, vs, cs, goal, T = F.procedural_monoped()
+    d0 = f.to_desc(varsets=vs, constraints=cs, init_mode=capi.INIT_PROCEDURAL, ee_goal=goal, total_time=T)
+    cols = _varset_cols(d0)
+    M0 = _sparse_matrix(6, cols[0][1], 11, zero_row=2)
+    M1 = _sparse_matrix(3, cols[2][1], 12, density=0.5)
+    cs2 = cs + [dict(kind=capi.C_LINEAR_EQ, ip=[0, 6]), dict(kind=capi.C_LINEAR_EQ, ip=[2, 3])]
+    d = f.to_desc(varsets=vs, constraints=cs2, init_mode=capi.INIT_PROCEDURAL, ee_goal=goal, total_time=T)
+    out["procedural_lineq"] = (d, [(capi.DATA_LINEAR_M, len(cs), M0), (capi.DATA_LINEAR_M, len(cs) + 1, M1)])
+    # ... on the schedule set of a phase-duration-optimisation problem (ANYmal stairs, configs[3])
+    fg = F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.StairsID), optimize_timings=True)
+    cols_g = _varset_cols(fg.to_desc())
+    vsg = fg.variable_sets()
+    si = [i for i, (k, ee) in enumerate(vsg) if k == capi.VAR_EE_SCHEDULE][0]
+    csg = fg.constraint_sets() + [dict(kind=capi.C_LINEAR_EQ, ip=[si, 2])]
+    dg = fg.to_desc(constraints=csg)
+    out["anymal_gait_lineq"] = (dg, [(capi.DATA_LINEAR_M, len(csg) - 1,
+                                      _sparse_matrix(2, cols_g[si][1], 13, density=0.7))])
+    # BaseHeightCost: the fork's biped driver (fixed gait), its phase-duration-optimisation variant, and
+    # ANYmal's flying trot on stairs (no foot in contact: the terrain height under the base)
+    fb = F.biped_walk()
+    z0 = fb.initial_base_.lin_p[2]
+    out["biped_base_height_cost"] = (fb.to_desc(costs=_biped_example_costs(fb, z0)), [])
+    fbg = _gaitopt_f(F.biped_walk())
+    out["biped_gait_base_height_cost"] = (fbg.to_desc(costs=_biped_example_costs(fbg, z0)), [])
+    fa = F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.StairsID))
+    out["anymal_stairs_base_height_cost"] = (fa.to_desc(costs=_biped_example_costs(fa, 0.5, with_nodes=False)), [])
+    # SoftConstraint: a soft-only BaseMotion set and a wrapped hard Dynamic set, procedural monoped
+    f, vs, cs, goal, T = F.procedural_monoped()
+    cs3 = cs + [dict(kind=capi.C_BASE_MOTION, T=T, dt=0.1, role=capi.ROLE_SOFT)]
+    costs = [dict(kind=capi.COST_SOFT, weight=1.0, ip=[len(cs3) - 1]), dict(kind=capi.COST_SOFT, weight=1.0, ip=[0]),
+             dict(kind=capi.COST_NODE, weight=1e-3, ip=[capi.VAR_EE_FORCE, 0, 2])]
+    d = f.to_desc(varsets=vs, constraints=cs3, init_mode=capi.INIT_PROCEDURAL, ee_goal=goal, total_time=T, costs=costs)
+    rows_bm = 6 * (math.floor(T / 0.1) + 2)     # TimeDiscretizationConstraint instants (time_discretization_constraint.cc:41-49)
+    rows_dyn = 6 * (math.floor(T / 0.1) + 2)
+    out["procedural_soft"] = (d, [(capi.DATA_SOFT_BOUNDS, 0, _soft_bounds(rows_bm, 21)),
+                                  (capi.DATA_SOFT_BOUNDS, 1, _soft_bounds(rows_dyn, 22))])
+    # ... under phase-duration optimisation: a soft ForceConstraintDiscretized (the streaming path in the
+    # soft child) and a soft LinearEquality set (its matrix re-indexed for the child)
+    fg = F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.StairsID), optimize_timings=True)
+    P = fg.params_
+    cols_g = _varset_cols(fg.to_desc())
+    csg = fg.constraint_sets()
+    nfd = 5 * (math.floor(P.GetTotalTime() / P.dt_constraint_force_) + 2)
+    csg = csg + [dict(kind=capi.C_FORCE_DISCRETIZED, ee=1, T=P.GetTotalTime(), dt=P.dt_constraint_force_,
+                      p=[P.force_limit_in_normal_direction_], role=capi.ROLE_SOFT),
+                 dict(kind=capi.C_LINEAR_EQ, ip=[0, 4], role=capi.ROLE_SOFT)]
+    costs = [dict(kind=capi.COST_SOFT, weight=1.0, ip=[len(csg) - 2]), dict(kind=capi.COST_SOFT, weight=1.0, ip=[len(csg) - 1])]
+    dg = fg.to_desc(constraints=csg, costs=costs)
+    out["anymal_gait_soft"] = (dg, [(capi.DATA_LINEAR_M, len(csg) - 1, _sparse_matrix(4, cols_g[0][1], 14)),
+                                    (capi.DATA_SOFT_BOUNDS, 0, _soft_bounds(nfd, 23)),
+                                    (capi.DATA_SOFT_BOUNDS, 1, _soft_bounds(4, 24))])
+    return out

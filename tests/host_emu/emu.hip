@@ -32,9 +32,10 @@ struct AccEmit {
 };
 }
 
-extern "C" int emu_eval(const towr_problem_desc_t* d, const double* x, double* g, double* v, char* err, int errlen) {
+extern "C" int emu_eval_ex(const towr_problem_desc_t* d, int n_data, const towr_data_t* data, const double* x, double* g,
+                           double* v, char* err, int errlen) {
   Layout L; std::string e;
-  int rc = build_layout(*d, L, e);
+  int rc = build_layout_ex(*d, n_data, data, L, e);
   if (rc) { if (err) std::snprintf(err, errlen, "%s", e.c_str()); return rc; }
   std::memset(g, 0, sizeof(double) * L.m);
   for (int64_t k = 0; k < L.nnz; ++k) v[k] = std::nan("");   // every slot must be stored
@@ -42,7 +43,7 @@ extern "C" int emu_eval(const towr_problem_desc_t* d, const double* x, double* g
   c.x = x; c.nodecol = L.nodecol.data(); c.spl = L.spl.data(); c.dur = L.dur.data();
   c.ter = &L.terrain; c.rb = L.rb; c.fdisc_motion = L.fdisc_motion;
   c.gait = L.gait; c.pinfo = L.pinfo.data(); c.pcols = L.pcols.data(); c.sched = L.sched.data();
-  c.eelin = L.eelin.data(); c.rotvec = L.rotvec;
+  c.eelin = L.eelin.data(); c.lin = L.lin.data(); c.rotvec = L.rotvec;
   for (const TileDesc& td : L.tiles)
     for (int l = td.i0; l < td.i1; ++l) {
       const ItemDesc& it = L.items[l];
@@ -83,6 +84,9 @@ extern "C" int emu_eval(const towr_problem_desc_t* d, const double* x, double* g
     }
   }
   return 0;
+}
+extern "C" int emu_eval(const towr_problem_desc_t* d, const double* x, double* g, double* v, char* err, int errlen) {
+  return emu_eval_ex(d, 0, nullptr, x, g, v, err, errlen);
 }
 
 // objective and dense gradient through engine_math.h's cost items (host instantiation)

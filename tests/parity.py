@@ -22,13 +22,13 @@ ABS = 1e-12
 VAR_EE_SCHEDULE = 6   # towr_varset_kind (include/towr_gpu.h), PhaseDurations sets
 
 
-def schedule_cols(desc, n):
+def schedule_cols(desc, n, data=None):
     """Boolean mask over the n columns: True for PhaseDurations (schedule) variable columns."""
     from oracle.oracle import Oracle   # column offsets: the oracle's layout (ifopt's AddVariableSet order)
     mask = np.zeros(n, dtype=bool)
     if not desc.optimize_timings:
         return mask
-    o = Oracle(desc)
+    o = Oracle(desc, data)
     for i, (c0, nc) in enumerate(o.varset_cols()):
         if desc.varsets[i].kind == VAR_EE_SCHEDULE:
             mask[c0:c0 + nc] = True

@@ -31,8 +31,9 @@ def test_struct_layout_matches_c():
 #include <stddef.h>
 #include "towr_gpu.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(towr_terrain_t), sizeof(towr_robot_t), sizeof(towr_constraint_t),
-         sizeof(towr_init_t), sizeof(towr_problem_desc_t), offsetof(towr_problem_desc_t, init));
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(towr_terrain_t), sizeof(towr_robot_t), sizeof(towr_constraint_t),
+         sizeof(towr_init_t), sizeof(towr_problem_desc_t), offsetof(towr_problem_desc_t, init),
+         offsetof(towr_constraint_t, role), sizeof(towr_data_t), offsetof(towr_data_t, data));
   return 0;
 }'''
     with tempfile.TemporaryDirectory() as d:
@@ -42,7 +43,8 @@ int main(void) {
         subprocess.check_call(["gcc", "-I", os.path.dirname(HDR), c, "-o", exe])
         got = [int(v) for v in subprocess.check_output([exe]).split()]
     want = [C.sizeof(capi.Terrain), C.sizeof(capi.Robot), C.sizeof(capi.ConstraintDesc),
-            C.sizeof(capi.InitDesc), C.sizeof(capi.ProblemDesc), capi.ProblemDesc.init.offset]
+            C.sizeof(capi.InitDesc), C.sizeof(capi.ProblemDesc), capi.ProblemDesc.init.offset,
+            capi.ConstraintDesc.role.offset, C.sizeof(capi.SideData), capi.SideData.data.offset]
     assert got == want
 
 

@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 MAX_EE = 4
 MAX_PHASES = 48
 MAX_VARSETS = 2 + 5 * MAX_EE
@@ -31,7 +31,8 @@ VAR_BASE_LIN, VAR_BASE_ANG, VAR_EE_MOTION, VAR_EE_ANG, VAR_EE_FORCE, VAR_EE_TORQ
 # towr_constraint_kind
 C_DYNAMIC, C_RANGE_OF_MOTION, C_FORCE, C_FORCE_DISCRETIZED, C_TERRAIN, C_BASE_MOTION, \
     C_SPLINE_ACC, C_BASE_HEIGHT, C_SWING, C_TOTAL_DURATION, C_TORQUE_DISCRETIZED, C_TORQUE, C_TERRAIN_HARD, \
-    C_EE_LINEAR = range(14)
+    C_EE_LINEAR, C_LINEAR_EQ = range(15)
+ROLE_HARD, ROLE_SOFT = 0, 1   # towr_constraint_role
 
 INIT_FORMULATION, INIT_PROCEDURAL = 0, 1
 
@@ -55,7 +56,7 @@ class VarSetDesc(C.Structure):
 
 class ConstraintDesc(C.Structure):
     _fields_ = [("kind", C.c_int32), ("ee", C.c_int32), ("T", C.c_double), ("dt", C.c_double),
-                ("p", C.c_double * 6), ("ip", C.c_int32 * 9), ("reserved", C.c_int32)]
+                ("p", C.c_double * 6), ("ip", C.c_int32 * 9), ("role", C.c_int32)]
 
 
 class InitDesc(C.Structure):
@@ -68,7 +69,9 @@ class InitDesc(C.Structure):
 
 
 # towr_cost_kind
-COST_NODE, COST_ENERGY, COST_ANG_MOMENTUM, COST_EE_BASE_POS = range(4)
+COST_NODE, COST_ENERGY, COST_ANG_MOMENTUM, COST_EE_BASE_POS, COST_BASE_HEIGHT, COST_SOFT = range(6)
+# towr_data_kind (side data of towr_gpu_create_ex)
+DATA_LINEAR_M, DATA_SOFT_BOUNDS = 0, 1
 MAX_COSTS = 128
 
 
@@ -96,6 +99,11 @@ class ProblemDesc(C.Structure):
                 ("costs", CostDesc * MAX_COSTS)]
 
 
+class SideData(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("index", C.c_int32), ("count", C.c_int64),
+                ("data", C.POINTER(C.c_double))]
+
+
 # symbol table of include/towr_gpu.h: name -> (restype, argtypes)
 _HANDLE = C.c_void_p
 _DP = C.POINTER(C.c_double)
@@ -103,6 +111,8 @@ _IP = C.POINTER(C.c_int32)
 _LP = C.POINTER(C.c_int64)
 SYMBOLS = {
     "towr_gpu_create": (C.c_int, [C.POINTER(ProblemDesc), C.c_int, C.POINTER(_HANDLE)]),
+    "towr_gpu_create_ex": (C.c_int, [C.POINTER(ProblemDesc), C.c_int32, C.POINTER(SideData), C.c_int,
+                                      C.POINTER(_HANDLE)]),
     "towr_gpu_destroy": (C.c_int, [_HANDLE]),
     "towr_gpu_last_error": (C.c_char_p, [_HANDLE]),
     "towr_gpu_abi_version": (C.c_int, []),
@@ -163,6 +173,19 @@ def load_library(path: str = LIB_PATH):
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def side_data(entries):
+    """[(kind, index, array)] -> (SideData array or None, the float64 arrays it points into)."""
+    import numpy as np
+    if not entries:
+        return None, []
+    keep = [np.ascontiguousarray(a, dtype=np.float64).ravel() for (_, _, a) in entries]
+    arr = (SideData * len(entries))()
+    for i, ((kind, index, _), a) in enumerate(zip(entries, keep)):
+        arr[i].kind, arr[i].index, arr[i].count = kind, index, a.size
+        arr[i].data = a.ctypes.data_as(_DP)
+    return arr, keep
 
 
 def dptr(a):

@@ -52,7 +52,8 @@ enum ItemType {
   IT_TQNODE = 11,  // TorqueConstraint node (a0 torque node, a1 motion node / a2 torque node at phase start)
   IT_THARD = 12,   // TerrainConstraintHard instant
   IT_EELIN = 13,   // EELinearConstraint instant (a0 = definition index)
-  IT_COUNT = 14
+  IT_LINEQ = 14,   // LinearEqualityConstraint row (a0 = first LinNz entry, a1 = entries)
+  IT_COUNT = 15
 };
 
 struct SplineMeta {
@@ -90,6 +91,9 @@ struct EELinDef {
   int32_t code[6];   // ee * 3 + dim
   double coeff[6];
 };
+
+// LinearEqualityConstraint (linear_constraint.cc:35-80): the nonzeros of one row of M, by column
+struct LinNz { int32_t col, reserved; double v; };
 
 struct RobotC {
   double m, g;
@@ -182,6 +186,7 @@ struct Ctx {
                                 // columns polynomial p touches, at pact[spl.pact_off + 2 (e n_polys + p)]
   const SchedInfo* sched;       // per endeffector
   const EELinDef* eelin;        // EELinearConstraint definitions
+  const LinNz* lin;             // LinearEqualityConstraint rows (IT_LINEQ)
   const double* cq;             // cost kernel: CT_ENERGYQ Gram matrices (16 doubles each)
   // Device tile blocks under phase-duration optimisation: the x-dependent PhaseSpline timings,
   // computed once per block (gait_timings in towr_gpu.hip) with the same operations in the same order
@@ -1675,6 +1680,19 @@ TG_HD void eval_eelin(const Ctx& c, const ItemDesc& it, Emit& em) {
   em.g(it.row0, val);
 }
 
+// LinearEqualityConstraint row (linear_constraint.cc:47-76): g = M x_set, Jacobian = M.sparseView().
+// The reference's dense product also adds the zero entries' 0 * x_j, which changes no finite sum.
+template <class Emit>
+TG_HD void eval_lineq(const Ctx& c, const ItemDesc& it, Emit& em) {
+  double s = 0.0;
+  for (int k = 0; k < it.a1; ++k) {
+    const LinNz e = c.lin[it.a0 + k];
+    s += e.v * xval(c, e.col);
+    em(it.row0, e.col, e.v, true);
+  }
+  em.g(it.row0, s);
+}
+
 // TotalDurationConstraint (total_duration_constraint.cc:49-72): sum of the ee's optimised durations
 template <class Emit>
 TG_HD void eval_tdur(const Ctx& c, const ItemDesc& it, Emit& em) {
@@ -1695,13 +1713,15 @@ TG_HD void eval_tdur(const Ctx& c, const ItemDesc& it, Emit& em) {
 // ----------------------------------------------------------------------------------------------
 // CT_ENERGYQ: EnergyCost of one polynomial of a force / torque spline with fixed durations (see
 // cost_energy_q); CT_ENERGY: one (sample, ee) of EnergyCost under phase-duration optimisation
-enum CostType { CT_NODE = 0, CT_ENERGY = 1, CT_ANGMOM = 2, CT_EEBP = 3, CT_ENERGYQ = 4, CT_COUNT = 5 };
+// CT_BHC: one sample of BaseHeightCost
+enum CostType { CT_NODE = 0, CT_ENERGY = 1, CT_ANGMOM = 2, CT_EEBP = 3, CT_ENERGYQ = 4, CT_BHC = 5, CT_COUNT = 6 };
 
 struct CostItem {
   int32_t type, ee, seg, s;        // seg: segment-table row of the sample time; s: spline (CT_NODE)
   int32_t deriv, dim;              // CT_NODE: node value penalised; CT_ENERGYQ: deriv = polynomial of spline s
   int32_t a0, a1;                  // CT_NODE: nodes [a0, a1); CT_EEBP: a0 = ee in contact at start (swing
-                                   // test under gait optimisation); CT_ENERGYQ: a0 = Gram matrix index (Ctx::cq)
+                                   // test under gait optimisation); CT_ENERGYQ: a0 = Gram matrix index (Ctx::cq);
+                                   // CT_BHC: a0 = contact-at-start bits, a1 = contact bits at t (fixed gait) or -1
   double t, w, wdt, tw;            // sample time, weight, weight * dt, EnergyCost torque weight
   double p[3], pad;                // CT_EEBP: reference ee position in base frame
 };
@@ -1913,6 +1933,33 @@ TG_HD void cost_eebp(const Ctx& c, const CostItem& it, Emit& em) {
   }
 }
 
+// BaseHeightCost sample (base_height_cost.cc:55-142, the fork's biped driver): w dt dev^2 with
+// dev = p_z(base) - (mean z of the feet in contact + target), or the terrain height under the base
+// when no foot is in contact. Its gradient is the reference's: only the base-linear nodes, through
+// d p_z / d nodes; the target's dependence on the feet and the terrain is not differentiated.
+template <class Emit>
+TG_HD void cost_bhc(const Ctx& c, const CostItem& it, Emit& em) {
+  SplinePt L;
+  spline_eval(c, SP_BASE_LIN, it.t, L);
+  double total = 0.0;
+  int cnt = 0;
+  for (int ee = 0; ee < c.rb.n_ee; ++ee) {
+    const bool contact = it.a1 >= 0 ? ((it.a1 >> ee) & 1) != 0 : sched_is_contact(c, ee, ((it.a0 >> ee) & 1) != 0, it.t);
+    if (!contact) continue;
+    SplinePt P;
+    spline_eval(c, sp_motion(ee), it.t, P);
+    total += P.p[2];
+    ++cnt;
+  }
+  const double avg = cnt == 0 ? ter_h(*c.ter, L.p[0], L.p[1]) : total / cnt;
+  const double dev = L.p[2] - (avg + it.p[0]);
+  em.f += it.w * dev * dev * it.wdt;   // weight_ * deviation * deviation * dt_ (it.wdt = dt here)
+  const double s = 2.0 * it.w * dev * it.wdt;
+  double H[4];
+  spline_basis(L, kPos, H);
+  for (int bb = 0; bb < 4; ++bb) em(0, basis_col(c, SP_BASE_LIN, L.poly, bb, 2), s * H[bb], true);
+}
+
 template <class Emit>
 TG_HD void eval_cost_item(const Ctx& c, const CostItem& it, Emit& em) {
   switch (it.type) {
@@ -1921,6 +1968,7 @@ TG_HD void eval_cost_item(const Ctx& c, const CostItem& it, Emit& em) {
     case CT_ANGMOM: cost_angmom(c, it, em); break;
     case CT_EEBP: cost_eebp(c, it, em); break;
     case CT_ENERGYQ: cost_energy_q(c, it, em); break;
+    case CT_BHC: cost_bhc(c, it, em); break;
   }
 }
 
@@ -2002,6 +2050,7 @@ TG_HD void eval_item(const Ctx& c, const ItemDesc& it, Emit& em) {
     case IT_TQNODE: eval_tqnode(c, it, em); break;
     case IT_THARD: eval_thard(c, it, em); break;
     case IT_EELIN: eval_eelin(c, it, em); break;
+    case IT_LINEQ: eval_lineq(c, it, em); break;
   }
 }
 

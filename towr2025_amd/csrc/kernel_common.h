@@ -30,6 +30,7 @@ struct KParams {
   const int32_t* pact;
   const SchedInfo* sched;
   const EELinDef* eelin;
+  const LinNz* lin;              // LinearEqualityConstraint rows
   const uint4* gtab;             // GAIT: the PhaseSpline tables in one blob (GaitTables), staged per tile block
   const ItemDirect* idir;        // GAIT: per item (lane) direct-position ranges
   int32_t gt_off[5], gt_n16;
@@ -60,6 +61,14 @@ struct KParams {
   int32_t n_citems, lds_red_off;
   double* F;
   double* GR; int64_t ldgr;
+  // cost launch, SoftConstraint terms: the soft child's g (and CSR values) of this batch, its CSR
+  // pattern, b = the bounds' mid-points; s_m = 0 without soft terms
+  const double* sG; int64_t s_ldg;
+  const double* sV; int64_t s_ldv;
+  const int32_t* s_rp;
+  const int32_t* s_col;
+  const double* s_b;
+  int32_t s_m;
 };
 
 // global -> LDS copy of n16 16-byte units: each thread issues up to K independent loads before its

@@ -62,6 +62,7 @@ struct Layout {
   std::vector<int32_t> pact;    // PhaseSpline active PhaseCol ranges (SplineMeta::pact_off)
   std::vector<SchedInfo> sched; // per endeffector (col0 = -1 without schedule variables)
   std::vector<EELinDef> eelin;  // EELinearConstraint definitions (ItemDesc::a0 indexes them)
+  std::vector<LinNz> lin;       // LinearEqualityConstraint rows (IT_LINEQ: ItemDesc::a0 / a1)
   std::vector<ItemDesc> items;
   std::vector<int32_t> slots;     // build-time: candidate -> global CSR position (or -1)
   std::vector<SlotGroup> slot_groups;   // device slot table (see SlotGroup); item.slot indexes it
@@ -103,6 +104,10 @@ struct Layout {
   std::vector<CostItem> cost_items;
   std::vector<double> cost_q;        // CT_ENERGYQ Gram matrices, 16 doubles per item (CostItem::q)
   int32_t cost_type0[CT_COUNT + 1] = {};
+  // SoftConstraint terms (TOWR_COST_SOFT), in cost order: the cost index and the wrapped constraint.
+  // The wrapped sets are evaluated by a second layout (the handle's soft child) whose constraint
+  // list is exactly these sets in this order (soft_desc).
+  std::vector<std::pair<int32_t, int32_t>> soft;
 };
 
 constexpr int kMiscWaves = 4;
@@ -159,8 +164,13 @@ const void* fs_inst_kernel();
 const void* fs_stream_kernel();
 int fs_inst_block();
 
-// Returns TOWR_OK or an error code with a message in `err`.
+// Returns TOWR_OK or an error code with a message in `err`. Side data (towr_gpu_create_ex): the
+// LinearEqualityConstraint matrices; the SoftConstraint bounds are checked by the handle.
 int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err);
+int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t* data, Layout& L, std::string& err);
+// the description of the soft child: the SoftConstraint terms' wrapped sets as hard constraints, no costs
+towr_problem_desc_t soft_desc(const towr_problem_desc_t& d, const Layout& L);
+const towr_data_t* find_data(int n_data, const towr_data_t* data, int kind, int index);
 
 // x0 for another init/terrain on the layout built from `d` (nlp_formulation.cc:121-346).
 int initial_x_for(const towr_problem_desc_t& d, const towr_init_t& init, const towr_terrain_t& ter,

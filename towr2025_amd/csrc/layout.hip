@@ -277,7 +277,7 @@ int item_rows(int type) {
     case IT_DYN: case IT_BMOT: return 6;
     case IT_ROM: case IT_SACC: return 3;
     case IT_FDISC: case IT_FNODE: return 5;
-    case IT_TERR: case IT_BHGT: case IT_TDUR: case IT_THARD: case IT_EELIN: return 1;
+    case IT_TERR: case IT_BHGT: case IT_TDUR: case IT_THARD: case IT_EELIN: case IT_LINEQ: return 1;
     case IT_TQDISC: return 4;
     case IT_TQNODE: return 3;
     case IT_SWING: return 4;
@@ -406,6 +406,28 @@ int build_costs(const towr_problem_desc_t& d, const std::vector<double>& base_d,
         }
         break;
       }
+      case TOWR_COST_BASE_HEIGHT: {   // base_height_cost.cc:55-142: one item per sample time
+        if (!(c.dt > 0.0)) { err = "BaseHeightCost needs dt > 0"; return TOWR_ERR_INVALID; }
+        it.type = CT_BHC; it.wdt = c.dt; it.p[0] = c.p[0]; it.a0 = 0;
+        for (int ee = 0; ee < E; ++ee) if (d.contact_at_start[ee]) it.a0 |= 1 << ee;
+        for (double t : sample_times(c.dt)) {
+          it.a1 = -1;
+          if (!L.gait) {   // fixed phase durations: PhaseDurations::IsContactPhase once, here
+            it.a1 = 0;
+            for (int ee = 0; ee < E; ++ee) {
+              double tl;
+              const int ph = seg_lookup(d.phase_durations[ee], d.n_phases[ee], t, &tl);
+              if ((ph % 2 == 0) == (d.contact_at_start[ee] != 0)) it.a1 |= 1 << ee;
+            }
+          }
+          it.t = t; it.seg = seg_of(t); items.push_back(it);
+        }
+        break;
+      }
+      case TOWR_COST_SOFT:   // soft_constraint.cc:34-69: evaluated by the handle's soft child
+        if (c.ip[0] < 0 || c.ip[0] >= d.n_constraints) { err = "SoftConstraint: constraint index out of range"; return TOWR_ERR_INVALID; }
+        L.soft.push_back({i, c.ip[0]});
+        break;
       default: err = "unknown cost kind"; return TOWR_ERR_INVALID;
     }
   }
@@ -512,7 +534,27 @@ int build_fstream(Layout& L, std::string& err) {
   return TOWR_OK;
 }
 
-int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
+const towr_data_t* find_data(int n_data, const towr_data_t* data, int kind, int index) {
+  for (int i = 0; i < n_data; ++i)
+    if (data[i].kind == kind && data[i].index == index) return &data[i];
+  return nullptr;
+}
+
+towr_problem_desc_t soft_desc(const towr_problem_desc_t& d, const Layout& L) {
+  towr_problem_desc_t s = d;
+  s.n_constraints = (int32_t)L.soft.size();
+  for (size_t k = 0; k < L.soft.size(); ++k) {
+    s.constraints[k] = d.constraints[L.soft[k].second];
+    s.constraints[k].role = TOWR_ROLE_HARD;
+  }
+  s.n_costs = 0;
+  return s;
+}
+
+int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) { return build_layout_ex(d, 0, nullptr, L, err); }
+
+int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t* data, Layout& L, std::string& err) {
+  if (n_data < 0 || (n_data > 0 && !data)) { err = "bad side data"; return TOWR_ERR_INVALID; }
   if (d.abi_version != TOWR_GPU_ABI_VERSION) { err = "abi version mismatch"; return TOWR_ERR_INVALID; }
   if (d.angular_rep != 0 && d.angular_rep != 1) { err = "angular_rep must be 0 (EulerZYX) or 1 (RotationVector)"; return TOWR_ERR_INVALID; }
   const int E = d.robot.n_ee;
@@ -607,7 +649,7 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
   }
 
   // ---- constraint sets and work items (AddConstraintSet order)
-  L.cons.clear(); L.items.clear(); L.eelin.clear();
+  L.cons.clear(); L.items.clear(); L.eelin.clear(); L.lin.clear(); L.soft.clear();
   std::vector<int> item_inst;   // instance id (items of one instance share rows)
   int row = 0, inst = 0;
   auto dts_of = [](double Tc, double dt) {   // time_discretization_constraint.cc:37-50
@@ -616,8 +658,14 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
     v.push_back(Tc);
     return v;
   };
+  if (d.n_constraints < 0 || d.n_constraints > TOWR_MAX_CONSTRAINTS) { err = "n_constraints out of range"; return TOWR_ERR_INVALID; }
   for (int ci = 0; ci < d.n_constraints; ++ci) {
     const towr_constraint_t& c = d.constraints[ci];
+    if (c.role != TOWR_ROLE_HARD && c.role != TOWR_ROLE_SOFT) { err = "bad constraint role"; return TOWR_ERR_INVALID; }
+    if (c.role == TOWR_ROLE_SOFT) {   // not a row block of g: only its SoftConstraint term evaluates it
+      L.cons.push_back(ConsInfo{-1, c.ee, row, 0});
+      continue;
+    }
     ConsInfo info{c.kind, c.ee, row, 0};
     auto add = [&](int type, int group, int ee, int k, int row0, double t, int a0, int a1, double p0) {
       ItemDesc it{}; it.type = type; it.group = group; it.ee = ee; it.k = k; it.row0 = row0; it.seg = -1;
@@ -755,6 +803,23 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
         info.rows = (int)ts.size();
         break;
       }
+      case TOWR_C_LINEAR_EQ: {     // linear_constraint.cc:35-45: one item per row of M
+        const int vi = c.ip[0], rows = c.ip[1];
+        if (vi < 0 || vi >= (int)L.varsets.size() || rows < 0) { err = "LinearEquality: bad variable set or row count"; return TOWR_ERR_INVALID; }
+        const VarSetInfo& vs = L.varsets[vi];
+        const towr_data_t* md = find_data(n_data, data, TOWR_DATA_LINEAR_M, ci);
+        if (!md || (rows > 0 && !md->data) || md->count != (int64_t)rows * vs.n) { err = "LinearEquality: matrix (side data TOWR_DATA_LINEAR_M) missing or not rows x n_set"; return TOWR_ERR_INVALID; }
+        for (int i = 0; i < rows; ++i, ++inst) {
+          const int a0 = (int)L.lin.size();
+          for (int j = 0; j < vs.n; ++j) {
+            const double v = md->data[(size_t)i * vs.n + j];
+            if (v != 0.0) L.lin.push_back(LinNz{vs.col0 + j, 0, v});   // M.sparseView(): exact zeros pruned
+          }
+          add(IT_LINEQ, 0, 0, i, row + i, 0.0, a0, (int)L.lin.size() - a0, 0.0);
+        }
+        info.rows = rows;
+        break;
+      }
       case TOWR_C_TOTAL_DURATION:  // total_duration_constraint.cc:36-47
         if (c.ee < 0 || c.ee >= E || L.sched[c.ee].col0 < 0) { err = "TotalDurationConstraint needs the ee's schedule variables"; return TOWR_ERR_INVALID; }
         add(IT_TDUR, 0, c.ee, 0, row, 0.0, 0, 0, 0.0); ++inst;
@@ -795,7 +860,7 @@ int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) {
     cx.x = L.x0.data(); cx.nodecol = L.nodecol.data(); cx.spl = L.spl.data(); cx.dur = L.dur.data();
     cx.ter = &L.terrain; cx.rb = L.rb; cx.fdisc_motion = L.fdisc_motion;
     cx.gait = L.gait; cx.pinfo = L.pinfo.data(); cx.pcols = L.pcols.data(); cx.sched = L.sched.data(); cx.pact = L.pact.data();
-    cx.eelin = L.eelin.data(); cx.rotvec = L.rotvec;
+    cx.eelin = L.eelin.data(); cx.lin = L.lin.data(); cx.rotvec = L.rotvec;
     for (size_t i = 0; i < L.items.size(); ++i) {
       item_cand_begin[i] = (int32_t)crow.size();
       RecordEmit em{&crow, &ccol, &cpres};

@@ -263,7 +263,7 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
   c.x = xs; c.nodecol = ns; c.spl = P.spl; c.dur = P.dur;
   c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
   c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
-  c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.pact = P.pact; c.sched = P.sched; c.eelin = P.eelin;
+  c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.pact = P.pact; c.sched = P.sched; c.eelin = P.eelin; c.lin = P.lin;
   if constexpr (GAIT) {   // the PhaseSpline searches and window emission read their tables from LDS
     c.spl = reinterpret_cast<const SplineMeta*>(gt + P.gt_off[0]);
     c.sched = reinterpret_cast<const SchedInfo*>(gt + P.gt_off[1]);
@@ -396,7 +396,7 @@ __device__ __forceinline__ void misc_body(const KParams& P, double* smem, int b,
     c.x = xs; c.nodecol = ns; c.spl = P.spl; c.dur = P.dur;
     c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
     c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
-    c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.pact = P.pact; c.sched = P.sched; c.eelin = P.eelin;
+    c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.pact = P.pact; c.sched = P.sched; c.eelin = P.eelin; c.lin = P.lin;
     c.rotvec = false;   // no small kind uses the base orientation
     c.dyn_scratch = nullptr;
     switch (it.type) {   // wave-uniform: a wave holds one tile of one kind
@@ -410,6 +410,7 @@ __device__ __forceinline__ void misc_body(const KParams& P, double* smem, int b,
       case IT_TQNODE: eval_tqnode(c, it, em); break;
       case IT_THARD: eval_thard(c, it, em); break;
       case IT_EELIN: eval_eelin(c, it, em); break;
+      case IT_LINEQ: eval_lineq(c, it, em); break;
       default: break;
     }
   }
@@ -518,7 +519,7 @@ __global__ void __launch_bounds__(kCostBlock, 1) towr_cost_kernel(KParams P) {
   c.x = xs; c.nodecol = ns; c.spl = P.spl; c.dur = P.dur;
   c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
   c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
-  c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.pact = P.pact; c.sched = P.sched; c.eelin = P.eelin;
+  c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.pact = P.pact; c.sched = P.sched; c.eelin = P.eelin; c.lin = P.lin;
   c.rotvec = ROTVEC;
   c.dyn_scratch = nullptr;
   c.cq = P.cq;
@@ -526,6 +527,22 @@ __global__ void __launch_bounds__(kCostBlock, 1) towr_cost_kernel(KParams P) {
     const CostItem it = P.citems[i];
     c.seg = nullptr; c.sg = P.sg; c.row = it.seg;
     eval_cost_item(c, it, em);
+  }
+  // SoftConstraint terms (soft_constraint.cc:52-69): 0.5 (g - b)^T (g - b) and J^T (g - b) over the
+  // wrapped sets' rows, from the soft child's g and CSR values of this problem (one row per lane)
+  if (P.s_m > 0) {
+    const double* sg = P.sG + (int64_t)b * P.s_ldg;
+    for (int r = threadIdx.x; r < P.s_m; r += kCostBlock) {
+      const double d = sg[r] - P.s_b[r];
+      em.f += (0.5 * d) * d;
+      if constexpr (GRAD) {
+        const double* sv = P.sV + (int64_t)b * P.s_ldv;
+        for (int k = P.s_rp[r]; k < P.s_rp[r + 1]; ++k) {
+          const double v = sv[k] * d;
+          if (v != 0.0) atomicAdd(gs + P.s_col[k], v);
+        }
+      }
+    }
   }
   // f: wave butterfly, then the waves' partials in order
   double f = em.f;
@@ -571,7 +588,7 @@ __global__ void __launch_bounds__(kTrajBlock, 1) towr_traj_kernel(KParams P, con
     c.seg = nullptr; c.row = -1;
     c.x = xs; c.nodecol = nsp; c.spl = P.spl; c.dur = P.dur;
     c.ter = P.terrains; c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
-    c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.pact = P.pact; c.sched = P.sched; c.eelin = P.eelin;
+    c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.pact = P.pact; c.sched = P.sched; c.eelin = P.eelin; c.lin = P.lin;
     c.rotvec = false; c.dyn_scratch = nullptr;
     traj_row(c, ph, times[k], rows + threadIdx.x, stride);
   }
@@ -635,6 +652,7 @@ struct towr_gpu_handle_s {
   int32_t* d_misc = nullptr;
   int32_t* d_misc_lds = nullptr;
   EELinDef* d_eelin = nullptr;
+  LinNz* d_lin = nullptr;
   uint4* d_gtab = nullptr;     // GAIT: PhaseSpline tables blob (GaitTables)
   ItemDirect* d_idir = nullptr;
   CostItem* d_citems = nullptr;
@@ -679,6 +697,15 @@ struct towr_gpu_handle_s {
   double* d_traj_t = nullptr;
   double traj_dt = 0.0;
   int32_t traj_ns = 0;
+  // SoftConstraint terms: a second handle over the wrapped sets (soft_desc), its CSR pattern, the
+  // bounds' mid-points b (rows in its order) and its per-batch g / values scratch
+  towr_gpu_handle_s* soft = nullptr;
+  std::vector<double> soft_b;
+  double* d_soft_b = nullptr;
+  int32_t* d_soft_rp = nullptr;
+  int32_t* d_soft_col = nullptr;
+  double *d_sg = nullptr, *d_sv = nullptr;
+  int64_t soft_cap_g = 0, soft_cap_v = 0;   // problems the scratch holds
 };
 
 namespace {
@@ -839,7 +866,7 @@ void fill_common(towr_gpu_handle h, KParams& P, int B, const double* X, int64_t 
   P.items = h->d_items; P.slots = h->d_slots; P.tiles = h->d_tiles;
   P.nodecol = h->d_nodecol; P.spl = h->d_spl; P.dur = h->d_dur;
   P.sg = h->sg; P.n_spl = (int32_t)L.spl.size();
-  P.pinfo = h->d_pinfo; P.pcols = h->d_pcols; P.pact = h->d_pact; P.sched = h->d_sched; P.eelin = h->d_eelin;
+  P.pinfo = h->d_pinfo; P.pcols = h->d_pcols; P.pact = h->d_pact; P.sched = h->d_sched; P.eelin = h->d_eelin; P.lin = h->d_lin;
   P.terrains = terrains; P.terrain_per_problem = per_problem;
   P.B = B;
   P.n = L.n; P.n_pad = (L.n + 2) & ~1; P.n_nodecol = (int32_t)L.nodecol.size();
@@ -903,7 +930,7 @@ int launch_fstream(towr_gpu_handle h, KParams& P, hipStream_t st) {
 }
 
 int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, int64_t ldg, double* V, int64_t ldv,
-           int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem, int only_class = -1) {
+           int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem, int only_class) {
   if (B <= 0) return TOWR_OK;
   const Layout& L = h->L;
   uint32_t fused_mask = 0;
@@ -965,15 +992,45 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
 size_t cost_red_off(const Layout& L) { return 2 * (size_t)((L.n + 2) & ~1) + (L.nodecol.size() + 3) / 4 * 2; }
 size_t cost_lds_bytes(const Layout& L) { return sizeof(double) * (cost_red_off(L) + kCostBlock / 64); }
 
+int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, int64_t ldg, double* V, int64_t ldv,
+           int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem, int only_class);
+
+// SoftConstraint terms: the soft child evaluates the wrapped sets' g (and, for the gradient, their
+// Jacobian values) of the batch into the handle's scratch, on the same stream, before the cost launch
+int launch_soft(towr_gpu_handle h, int B, const double* X, int64_t ldx, bool grad, hipStream_t s,
+                const towr_terrain_t* terrains, int per_problem, KParams& P) {
+  towr_gpu_handle c = h->soft;
+  const int64_t ms = std::max(1, c->L.m), nzs = std::max<int64_t>(1, c->L.nnz);
+  if (h->soft_cap_g < B) {
+    if (h->d_sg) (void)hipFree(h->d_sg);
+    h->d_sg = nullptr; h->soft_cap_g = 0;
+    HIPCHK(h, hipMalloc(&h->d_sg, sizeof(double) * (size_t)B * ms));
+    h->soft_cap_g = B;
+  }
+  if (grad && h->soft_cap_v < B) {
+    if (h->d_sv) (void)hipFree(h->d_sv);
+    h->d_sv = nullptr; h->soft_cap_v = 0;
+    HIPCHK(h, hipMalloc(&h->d_sv, sizeof(double) * (size_t)B * nzs));
+    h->soft_cap_v = B;
+  }
+  if (int rc = launch(c, B, X, ldx, h->d_sg, ms, grad ? h->d_sv : nullptr, nzs, 1, grad ? 1 : 0, s, terrains, per_problem, -1))
+    return fail(h, rc, "SoftConstraint sets: " + c->err);
+  P.sG = h->d_sg; P.s_ldg = ms; P.sV = h->d_sv; P.s_ldv = nzs;
+  P.s_rp = h->d_soft_rp; P.s_col = h->d_soft_col; P.s_b = h->d_soft_b; P.s_m = c->L.m;
+  return TOWR_OK;
+}
+
 int launch_cost(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* F, double* GR, int64_t ldgr,
                 hipStream_t s, const towr_terrain_t* terrains, int per_problem) {
   if (B <= 0) return TOWR_OK;
   const Layout& L = h->L;
   KParams P{};
+  if (h->soft)
+    if (int rc = launch_soft(h, B, X, ldx, GR != nullptr, s, terrains, per_problem, P)) return rc;
   P.X = X; P.ldx = ldx;
   P.nodecol = h->d_nodecol; P.spl = h->d_spl; P.dur = h->d_dur;
   P.sg = h->sg; P.n_spl = (int32_t)L.spl.size();
-  P.pinfo = h->d_pinfo; P.pcols = h->d_pcols; P.pact = h->d_pact; P.sched = h->d_sched; P.eelin = h->d_eelin;
+  P.pinfo = h->d_pinfo; P.pcols = h->d_pcols; P.pact = h->d_pact; P.sched = h->d_sched; P.eelin = h->d_eelin; P.lin = h->d_lin;
   P.terrains = terrains; P.terrain_per_problem = per_problem;
   P.B = B;
   P.n = L.n; P.n_pad = (L.n + 2) & ~1; P.n_nodecol = (int32_t)L.nodecol.size();
@@ -1015,7 +1072,7 @@ int launch_traj(towr_gpu_handle h, int B, const double* X, int64_t ldx, double d
   KParams P{};
   P.X = X; P.ldx = ldx;
   P.nodecol = h->d_nodecol; P.spl = h->d_spl; P.dur = h->d_dur;
-  P.pinfo = h->d_pinfo; P.pcols = h->d_pcols; P.pact = h->d_pact; P.sched = h->d_sched; P.eelin = h->d_eelin;
+  P.pinfo = h->d_pinfo; P.pcols = h->d_pcols; P.pact = h->d_pact; P.sched = h->d_sched; P.eelin = h->d_eelin; P.lin = h->d_lin;
   P.terrains = h->d_terrain;
   P.n = L.n; P.n_pad = (L.n + 2) & ~1; P.n_nodecol = (int32_t)L.nodecol.size();
   P.rb = L.rb;
@@ -1075,7 +1132,7 @@ int host_eval(towr_gpu_handle h, int B, const double* X, double* G, double* V, b
                vb = sizeof(double) * (size_t)B * L.nnz;
   std::memcpy(h->h_x, X, xb);
   HIPCHK(h, hipMemcpyAsync(h->d_x, h->h_x, xb, hipMemcpyHostToDevice, h->stream));
-  if (int rc = launch(h, B, h->d_x, L.n, h->d_g, L.m, h->d_v, L.nnz, G != nullptr, V != nullptr, h->stream, ter, per))
+  if (int rc = launch(h, B, h->d_x, L.n, h->d_g, L.m, h->d_v, L.nnz, G != nullptr, V != nullptr, h->stream, ter, per, -1))
     return rc;
   if (G) HIPCHK(h, hipMemcpyAsync(h->h_g, h->d_g, gb, hipMemcpyDeviceToHost, h->stream));
   if (V) HIPCHK(h, hipMemcpyAsync(h->h_v, h->d_v, vb, hipMemcpyDeviceToHost, h->stream));
@@ -1162,13 +1219,39 @@ const char* towr_gpu_last_error(towr_gpu_handle h) {
 }
 
 int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle* out) {
-  if (!desc || !out) return fail(nullptr, TOWR_ERR_INVALID, "null argument");
+  return towr_gpu_create_ex(desc, 0, nullptr, device, out);
+}
+
+int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const towr_data_t* data, int device, towr_gpu_handle* out) {
+  if (!desc || !out || n_data < 0 || (n_data > 0 && !data)) return fail(nullptr, TOWR_ERR_INVALID, "null argument");
   *out = nullptr;
   towr_gpu_handle h = new towr_gpu_handle_s();
   std::string err;
-  const int rc = build_layout(*desc, h->L, err);
+  const int rc = build_layout_ex(*desc, n_data, data, h->L, err);
   if (rc != TOWR_OK) { fail(nullptr, rc, err); delete h; return rc; }
   if (int rf = setup_fusion(h, err)) { fail(nullptr, rf, err); delete h; return rf; }
+  if (!h->L.soft.empty()) {   // SoftConstraint terms: the wrapped sets as the hard constraints of a child handle
+    const towr_problem_desc_t sd = soft_desc(*desc, h->L);
+    std::vector<towr_data_t> cd;   // their LinearEquality matrices, re-indexed to the child's constraint list
+    for (size_t k = 0; k < h->L.soft.size(); ++k)
+      if (const towr_data_t* m = find_data(n_data, data, TOWR_DATA_LINEAR_M, h->L.soft[k].second)) {
+        towr_data_t e = *m;
+        e.index = (int32_t)k;
+        cd.push_back(e);
+      }
+    if (int rs = towr_gpu_create_ex(&sd, (int32_t)cd.size(), cd.data(), device, &h->soft)) { delete h; return rs; }
+    const Layout& C = h->soft->L;
+    for (size_t k = 0; k < h->L.soft.size(); ++k) {   // b = (upper + lower) / 2 (soft_constraint.cc:40-45)
+      const int rows = C.cons[k].rows;
+      const towr_data_t* bd = find_data(n_data, data, TOWR_DATA_SOFT_BOUNDS, h->L.soft[k].first);
+      if (!bd || (rows > 0 && !bd->data) || bd->count != 2 * (int64_t)rows) {
+        towr_gpu_destroy(h);
+        return fail(nullptr, TOWR_ERR_INVALID, "SoftConstraint term " + std::to_string(h->L.soft[k].first) +
+                                                   ": bounds (side data TOWR_DATA_SOFT_BOUNDS, lower then upper) missing or not 2 x the set's rows");
+      }
+      for (int r = 0; r < rows; ++r) h->soft_b.push_back((bd->data[rows + r] + bd->data[r]) / 2.);
+    }
+  }
   if (device < 0) {   // layout-only handle: sizes / structure / x0, no evaluation (CPU-side tests)
     h->device = -1;
     *out = h;
@@ -1200,6 +1283,7 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
       (r = upload(h, &h->d_spl, L.spl)) || (r = upload(h, &h->d_dur, L.dur)) || (r = upload(h, &h->d_terrain, ter)) ||
       (r = upload(h, &h->d_pinfo, L.pinfo)) || (r = upload(h, &h->d_pcols, L.pcols)) || (r = upload(h, &h->d_pact, L.pact)) || (r = upload(h, &h->d_sched, L.sched)) ||
       (r = upload(h, &h->d_misc, L.misc_tiles)) || (r = upload(h, &h->d_misc_lds, L.misc_lds)) || (r = upload(h, &h->d_eelin, L.eelin)) ||
+      (r = upload(h, &h->d_lin, L.lin)) ||
       (r = upload(h, &h->d_citems, L.cost_items)) || (r = upload(h, &h->d_cq, L.cost_q)) || (r = upload(h, &h->d_gtab, gait_blob(L))) ||
       (r = upload(h, &h->d_idir, L.idirect)) || (r = upload(h, &h->d_fsb, L.fs_blocks)) || (r = upload(h, &h->d_fs_t, L.fs_t)) ||
       (r = upload(h, &h->d_fs_tmpl, L.fs_tmpl)) || (r = upload(h, &h->d_fs_ws, L.fs_ws)) ||
@@ -1214,6 +1298,11 @@ int towr_gpu_create(const towr_problem_desc_t* desc, int device, towr_gpu_handle
       for (int q = 0; q < d.n_phases[ee]; ++q) pd[(size_t)ee * TOWR_MAX_PHASES + q] = d.phase_durations[ee][q];
     }
     if ((r = upload(h, &h->d_traj_pd, pd)) || (r = upload(h, &h->d_traj_n, pn)) || (r = upload(h, &h->d_traj_c0, pc))) return bail(r);
+  }
+  if (h->soft) {   // the soft child's pattern (int32 row pointers: its nnz is small) and b
+    const Layout& C = h->soft->L;
+    std::vector<int32_t> rp(C.row_ptr.begin(), C.row_ptr.end());
+    if ((r = upload(h, &h->d_soft_rp, rp)) || (r = upload(h, &h->d_soft_col, C.col)) || (r = upload(h, &h->d_soft_b, h->soft_b))) return bail(r);
   }
   {   // segment table in 32-row blocks (see SegSoA)
     const int nspl = (int)L.spl.size();
@@ -1299,7 +1388,7 @@ int towr_gpu_destroy(towr_gpu_handle h) {
                  h->d_pinfo, h->d_pcols, h->d_pact, h->d_sched, h->d_misc, h->d_misc_lds, h->d_eelin, h->d_gtab, h->d_idir, h->d_citems, h->d_cq, h->fuse[0].d_units, h->fuse[1].d_units,
                  h->d_bterrain, h->d_x, h->d_g, h->d_v, h->d_f, h->d_grad,
                  h->d_traj_pd, h->d_traj_n, h->d_traj_c0, h->d_traj_t, h->d_fsb, h->d_fs_t, h->d_fs_tmpl, h->d_fs_ws,
-                 h->d_fs_iee, h->d_fs_irow, h->d_fsrec};
+                 h->d_fs_iee, h->d_fs_irow, h->d_fsrec, h->d_lin, h->d_soft_b, h->d_soft_rp, h->d_soft_col, h->d_sg, h->d_sv};
   if (h->device >= 0) for (void* p : dev) if (p) (void)hipFree(p);
   void* host[] = {h->h_x, h->h_g, h->h_v};
   for (void* p : host) if (p) (void)hipHostFree(p);
@@ -1309,6 +1398,7 @@ int towr_gpu_destroy(towr_gpu_handle h) {
     if (h->join[i]) (void)hipEventDestroy(h->join[i]);
   }
   if (h->fork) (void)hipEventDestroy(h->fork);
+  if (h->soft) towr_gpu_destroy(h->soft);
   delete h;
   return TOWR_OK;
 }
@@ -1487,7 +1577,7 @@ int towr_gpu_eval_batch_device(towr_gpu_handle h, int32_t B, const double* X, in
   int per;
   if (int rc = batch_terrain(h, B, false, &ter, &per)) return rc;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);   // NULL = HIP's default stream
-  return launch(h, B, X, ldx, G, ldg, V, ldv, want_g, want_jac, s, ter, per);
+  return launch(h, B, X, ldx, G, ldg, V, ldv, want_g, want_jac, s, ter, per, -1);
 }
 
 int towr_gpu_kernel_info(towr_gpu_handle h, int32_t kernel, const char** name, int32_t* n_tiles, int64_t* bytes_per_problem) {

@@ -627,6 +627,7 @@ class NlpFormulation:
                 d.constraints[i].p[j] = v
             for j, v in enumerate(c.get("ip", [])):
                 d.constraints[i].ip[j] = v
+            d.constraints[i].role = c.get("role", capi.ROLE_HARD)
         cts = self.cost_terms() if costs is None else costs
         if len(cts) > capi.MAX_COSTS:
             raise ValueError("too many cost terms")

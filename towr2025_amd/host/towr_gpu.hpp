@@ -30,9 +30,10 @@ namespace towr_gpu {
 
 class Engine {
  public:
-  // device < 0: layout-only (sizes, structure, x0; evaluation throws)
-  Engine(const towr_problem_desc_t& desc, int device = 0) {
-    const int rc = towr_gpu_create(&desc, device, &h_);
+  // device < 0: layout-only (sizes, structure, x0; evaluation throws). `data`: side data of
+  // towr_gpu_create_ex (LinearEqualityConstraint matrices, SoftConstraint bounds), copied at creation.
+  Engine(const towr_problem_desc_t& desc, int device = 0, const std::vector<towr_data_t>& data = {}) {
+    const int rc = towr_gpu_create_ex(&desc, (int32_t)data.size(), data.data(), device, &h_);
     if (rc != TOWR_OK) throw std::runtime_error("towr_gpu_create failed (" + std::to_string(rc) + "): " + towr_gpu_last_error(nullptr));
     int32_t n = 0, m = 0;
     int64_t nnz = 0;

@@ -49,12 +49,17 @@ def _check_tensor(t, what, min_cols, device=None):
 
 
 class TowrGpuProblem:
-    def __init__(self, desc: capi.ProblemDesc, device: int = 0):
+    """`data`: side data of towr_gpu_create_ex, [(towr_data_kind, index, float64 array)]: the matrix M of
+    each LinearEqualityConstraint (capi.DATA_LINEAR_M, constraint index, rows x n_set row-major) and the
+    wrapped set's bounds of each SoftConstraint term (capi.DATA_SOFT_BOUNDS, cost index, [lower, upper])."""
+
+    def __init__(self, desc: capi.ProblemDesc, device: int = 0, data=None):
         self._lib = capi.load_library()
         self.desc = desc
         self.device = device
         h = C.c_void_p()
-        rc = self._lib.towr_gpu_create(C.byref(desc), device, C.byref(h))
+        arr, keep = capi.side_data(data)
+        rc = self._lib.towr_gpu_create_ex(C.byref(desc), len(data or []), arr, device, C.byref(h))
         if rc != capi.TOWR_OK:
             raise TowrGpuError(f"towr_gpu_create failed ({rc}): {self._lib.towr_gpu_last_error(None).decode()}")
         self._h = h
