@@ -110,7 +110,10 @@ struct Layout {
   std::vector<std::pair<int32_t, int32_t>> soft;
 };
 
-constexpr int kMiscWaves = 4;
+#ifndef TOWR_MISC_WAVES
+#define TOWR_MISC_WAVES 4
+#endif
+constexpr int kMiscWaves = TOWR_MISC_WAVES;   // one-wave small-kind tiles per group (block)
 constexpr int kSlotSpare = 4;   // spare slot groups per lane: the kernels prefetch up to this many ahead
 constexpr bool is_misc_kind(int t) { return t != IT_DYN && t != IT_ROM && t != IT_FDISC && t != IT_TQDISC; }
 

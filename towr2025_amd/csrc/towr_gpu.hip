@@ -361,11 +361,12 @@ __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN && BLOCK <= 256 ? 2 : 1
 // The small kinds (node-value constraints, SplineAcc, BaseMotion, TotalDuration: a few kB of output
 // per problem each) in one launch: a block = kMiscWaves one-wave tiles of one problem, sharing the
 // staged x and node table; each wave evaluates and writes out its own tile.
-template <bool GAIT>
+// BLOCK = the launch's block size (>= 64 kMiscWaves): waves past the group's tiles only help stage x.
+template <bool GAIT, int BLOCK = 64 * kMiscWaves>
 __device__ __forceinline__ void misc_body(const KParams& P, double* smem, int b, int group, int lds_x_off) {
-  constexpr int BLOCK = 64 * kMiscWaves;
+  static_assert(BLOCK >= 64 * kMiscWaves, "a small-kind group needs a wave per tile");
   const int wave = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
-  const int ti = P.misc_tiles[group * kMiscWaves + wave];
+  const int ti = wave < kMiscWaves ? P.misc_tiles[group * kMiscWaves + wave] : -1;
   TileDesc T{};
   ItemDesc it{};
   it.type = IT_NONE;
@@ -374,8 +375,8 @@ __device__ __forceinline__ void misc_body(const KParams& P, double* smem, int b,
     T = P.tiles[ti];
     it = P.items[T.i0 + lane];
   }
-  const int32_t wl_off = P.misc_lds[2 * (group * kMiscWaves + wave)];
-  const int32_t rows_off = P.misc_lds[2 * (group * kMiscWaves + wave) + 1];
+  const int32_t wl_off = ti >= 0 ? P.misc_lds[2 * (group * kMiscWaves + wave)] : 0;
+  const int32_t rows_off = ti >= 0 ? P.misc_lds[2 * (group * kMiscWaves + wave) + 1] : 0;
   double* wl = smem + wl_off;
   TileEmit<64, 3> em(P.slots + it.slot, wl, wl + rows_off - T.r0);
   double* xs = smem + lds_x_off;
@@ -469,7 +470,9 @@ __global__ void __launch_bounds__(KBLOCK, (KBLOCK == 256 ? 2 : 1)) towr_step_ker
     default:
       if constexpr (KBLOCK == 256) {
         if (u.lc == LC_DYN) tile_body<IT_DYN, 256, KBLOCK, GAIT, ROTVEC>(P, smem, b, u.tile, u.lds_x_off, u.lds_rows_off);
-        else misc_body<GAIT>(P, smem, b, u.tile, u.lds_x_off);
+        else misc_body<GAIT, KBLOCK>(P, smem, b, u.tile, u.lds_x_off);
+      } else if constexpr (KBLOCK >= 64 * kMiscWaves) {
+        if (u.lc == LC_MISC) misc_body<GAIT, KBLOCK>(P, smem, b, u.tile, u.lds_x_off);
       }
       break;
   }
@@ -1168,7 +1171,8 @@ int setup_fusion(towr_gpu_handle h, std::string& err) {
     if (__builtin_popcount(mask) >= 2) {
       towr_gpu_handle_s::FuseGroup& fg = h->fuse[h->n_fuse++];
       fg.mask = mask;
-      fg.kblock = (mask & ((1u << LC_DYN) | (1u << LC_MISC))) ? 256 : 192;
+      // 256 with Dynamic; 192-lane tiles otherwise, small-kind groups of 3 waves fit those blocks
+      fg.kblock = (mask & (1u << LC_DYN)) || ((mask & (1u << LC_MISC)) && 64 * kMiscWaves > 192) ? 256 : 192;
       for (int lc = 0; lc < LC_COUNT; ++lc)
         if ((mask >> lc) & 1) {
           fg.lds = std::max(fg.lds, lds_bytes(L, lc));
