@@ -296,8 +296,19 @@ int towr_gpu_eval_batch_device(towr_gpu_handle h, int32_t B,
                                double* V, int64_t ldv,
                                int32_t want_g, int32_t want_jac, void* stream);
 
-/* Host batch (H2D of X, D2H of G and V through pinned staging; contiguous lds = n, m, nnz).      */
+/* Host batch (H2D of X, D2H of G and V; contiguous lds = n, m, nnz). Outputs move in chunks: the
+ * kernels of chunk i overlap the PCIe transfer of chunk i - 1. Arrays inside memory registered with
+ * towr_gpu_register_host are transferred in place; others go through the handle's pinned staging.  */
 int towr_gpu_eval_batch(towr_gpu_handle h, int32_t B, const double* X, double* G, double* V);
+
+/* Page-locks caller memory [ptr, ptr + bytes) (hipHostRegister) for this handle until
+ * towr_gpu_unregister_host or towr_gpu_destroy. Every host-pointer entry point whose x / g / values
+ * (or X / G / V) array lies inside a registered range DMAs straight to / from it, without the
+ * staging copy: an IPOPT driver registers its x, g and values arrays once (they are reused by every
+ * IpoptAdapter callback, hopper_example.cc:175-180). Ranges must not overlap; the memory must stay
+ * allocated while registered.                                                                    */
+int towr_gpu_register_host(towr_gpu_handle h, void* ptr, int64_t bytes);
+int towr_gpu_unregister_host(towr_gpu_handle h, void* ptr);
 
 /* Launch classes and launches, for roofline accounting. Kernel indices 0..4 are the launch
  * classes: Dynamic, RangeOfMotion, ForceConstraintDiscretized, TorqueConstraintDiscretized and the

@@ -74,3 +74,18 @@ def test_device_batch_operands_are_validated():
         _check_tensor(torch.zeros((2, p.n), dtype=torch.float64), "X", p.n)
     with pytest.raises(TowrGpuError, match="HIP device"):
         p.eval_batch_device(torch.zeros((2, p.n), dtype=torch.float64), None, None)
+
+
+def test_register_host_refused_without_device():
+    """towr_gpu_register_host needs a device (layout-only handles evaluate nothing); unregistering a
+    pointer that was never registered is an argument error."""
+    import numpy as np
+    import pytest
+    from towr2025_amd import TowrGpuProblem, formulation as F
+    from towr2025_amd.problem import TowrGpuError
+    p = TowrGpuProblem(F.anymal_trot().to_desc(), device=-1)
+    a = np.zeros(16)
+    with pytest.raises(TowrGpuError, match=str(capi.TOWR_ERR_NO_DEVICE)):
+        p.register_host(a)
+    with pytest.raises(TowrGpuError, match="not registered"):
+        p.unregister_host(a)

@@ -291,3 +291,65 @@ def test_batch_terrain_count_must_match():
     p.eval_batch_device(X, G, V)   # cleared: the description's terrain again
     torch.cuda.synchronize()
     np.testing.assert_array_equal(G.cpu().numpy()[1], g)
+
+
+def test_host_batch_chunks_and_registered_buffers():
+    """towr_gpu_eval_batch over several output chunks (kernels of chunk i overlap the D2H of chunk
+    i - 1, per-problem terrains offset per chunk), through the pinned staging and in place into
+    registered G / V, and the B = 1 host calls with registered g / values: all bit-identical to the
+    device batch of the same problems."""
+    import torch
+    import bench
+    desc = F.anymal_trot().to_desc()
+    p = TowrGpuProblem(desc)
+    B = 600                                   # ~64 MB of output per chunk: 3 chunks
+    Xh, terrains = bench.make_batch(p, B, first_id=123)
+    X = np.ascontiguousarray(Xh[2])
+    p.set_batch_terrain(terrains)
+    dev = torch.device("cuda:0")
+    Gd = torch.zeros((B, p.m), dtype=torch.float64, device=dev)
+    Vd = torch.zeros((B, p.nnz), dtype=torch.float64, device=dev)
+    p.eval_batch_device(torch.from_numpy(X).to(dev), Gd, Vd)
+    torch.cuda.synchronize()
+    G_ref, V_ref = Gd.cpu().numpy(), Vd.cpu().numpy()
+    G1, V1 = p.eval_batch(X)                                   # staged
+    np.testing.assert_array_equal(G1, G_ref)
+    np.testing.assert_array_equal(V1, V_ref)
+    G2, V2 = np.full((B, p.m), np.nan), np.full((B, p.nnz), np.nan)
+    p.register_host(G2)
+    p.register_host(V2)
+    p.eval_batch(X, G2, V2)                                    # in place
+    np.testing.assert_array_equal(G2, G_ref)
+    np.testing.assert_array_equal(V2, V_ref)
+    p.unregister_host(G2)
+    p.unregister_host(V2)
+    # B = 1 host calls (one launch of every class) with registered outputs vs staged
+    q = TowrGpuProblem(desc)
+    o = Oracle(desc)
+    xs = [_perturb(o.initial_x(), 31 + k) for k in range(3)]
+    staged = [q.eval_g_jac(x) for x in xs]
+    for k, x in enumerate(xs):   # the zero-copy single launch vs the device batch's launches
+        Xd1 = torch.from_numpy(x.reshape(1, -1).copy()).to(dev)
+        Gd1 = torch.zeros((1, q.m), dtype=torch.float64, device=dev)
+        Vd1 = torch.zeros((1, q.nnz), dtype=torch.float64, device=dev)
+        q.eval_batch_device(Xd1, Gd1, Vd1)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(staged[k][0], Gd1.cpu().numpy()[0])
+        np.testing.assert_array_equal(staged[k][1], Vd1.cpu().numpy()[0])
+    g, v = np.full(q.m, np.nan), np.full(q.nnz, np.nan)
+    q.register_host(g)
+    q.register_host(v)
+    xr = np.zeros(q.n)
+    q.register_host(xr)
+    for rep in range(2):   # alternating x: every call's zero-copy outputs are that call's, none stale
+        for k, x in enumerate(xs):
+            if rep:
+                xr[:] = x                     # x from registered memory too
+                q.eval_g_jac_into(xr, g, v)
+            else:
+                q.eval_g_jac_into(np.ascontiguousarray(x), g, v)
+            np.testing.assert_array_equal(g, staged[k][0])
+            np.testing.assert_array_equal(v, staged[k][1])
+    r, c, v_ref = o.eval_jac(xs[2])
+    assert_close(o.eval_g(xs[2]), g, r, v_ref, v, o.m, "registered single call")
+    q.close()   # destroy unregisters

@@ -19,6 +19,8 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
+#include <utility>
 #include <vector>
 
 #include "engine_math.h"
@@ -679,6 +681,16 @@ struct towr_gpu_handle_s {
   static constexpr int kMaxFuse = 2;
   FuseGroup fuse[kMaxFuse];
   int n_fuse = 0;
+  // one problem through host pointers (eval_g / eval_jac_values / eval_g_jac): every class in ONE
+  // launch (the fused kernel over all units), so the per-call latency is one kernel, not three
+  FuseGroup single;
+  // host entry points: caller memory page-locked by towr_gpu_register_host (DMA straight to / from
+  // it), the copy stream of the chunked host batch and its per-chunk events
+  struct Pinned { const char* p; size_t n; char* dev; };   // host range and its device address
+  std::vector<Pinned> pinned;
+  double *hd_x = nullptr, *hd_g = nullptr, *hd_v = nullptr;   // device addresses of the pinned staging
+  hipStream_t copy_stream = nullptr;
+  std::vector<hipEvent_t> ev_c, ev_d;
   std::string fuse_name[kMaxFuse];   // towr_gpu_kernel_info
   // fork-join of the per-kind launches (TOWR_GPU_STREAMS = total streams incl. the caller's, 1..4)
   static constexpr int kMaxSide = 3;
@@ -1108,6 +1120,9 @@ int ensure_stage(towr_gpu_handle h, int B) {
   HIPCHK(h, hipHostMalloc(&h->h_x, sizeof(double) * (size_t)B * L.n, hipHostMallocDefault));
   HIPCHK(h, hipHostMalloc(&h->h_g, sizeof(double) * (size_t)B * std::max(1, L.m), hipHostMallocDefault));
   HIPCHK(h, hipHostMalloc(&h->h_v, sizeof(double) * (size_t)B * std::max<int64_t>(1, L.nnz), hipHostMallocDefault));
+  HIPCHK(h, hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hd_x), h->h_x, 0));
+  HIPCHK(h, hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hd_g), h->h_g, 0));
+  HIPCHK(h, hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hd_v), h->h_v, 0));
   h->stage_B = B;
   return TOWR_OK;
 }
@@ -1125,23 +1140,122 @@ int batch_terrain(towr_gpu_handle h, int B, bool single, const towr_terrain_t** 
   return TOWR_OK;
 }
 
+// [p, p + bytes) inside caller memory registered with towr_gpu_register_host
+bool is_registered(towr_gpu_handle h, const void* p, size_t bytes) {
+  const char* c = static_cast<const char*>(p);
+  for (const auto& r : h->pinned)
+    if (c >= r.p && c + bytes <= r.p + r.n) return true;
+  return false;
+}
+// device address of registered host memory (zero-copy access from a kernel), or nullptr
+template <class T>
+T* device_view(towr_gpu_handle h, T* p, size_t bytes) {
+  const char* c = reinterpret_cast<const char*>(p);
+  for (const auto& r : h->pinned)
+    if (c >= r.p && c + bytes <= r.p + r.n) return reinterpret_cast<T*>(r.dev + (c - r.p));
+  return nullptr;
+}
+
+// host memcpy over a few threads: one thread reaches ~10 GB/s on the box's EPYC cores, below what a
+// PCIe Gen5 x16 DMA delivers into the pinned staging, so large copies are split
+void par_copy(void* dst, const void* src, size_t bytes) {
+  constexpr size_t kMinPerThread = 4u << 20;
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const int nt = (int)std::min<size_t>(std::min(8u, hw), bytes / kMinPerThread);
+  if (nt <= 1) { std::memcpy(dst, src, bytes); return; }
+  const size_t part = (bytes / nt + 63) & ~(size_t)63;
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) {
+    const size_t o = (size_t)t * part;
+    if (o >= bytes) break;
+    th.emplace_back([=] { std::memcpy(static_cast<char*>(dst) + o, static_cast<const char*>(src) + o, std::min(part, bytes - o)); });
+  }
+  std::memcpy(dst, src, std::min(part, bytes));
+  for (auto& t : th) t.join();
+}
+
+int ensure_events(towr_gpu_handle h, size_t n) {
+  while (h->ev_c.size() < n) {
+    hipEvent_t a = nullptr, b = nullptr;
+    HIPCHK(h, hipEventCreateWithFlags(&a, hipEventDisableTiming));
+    if (hipEventCreateWithFlags(&b, hipEventDisableTiming) != hipSuccess) { (void)hipEventDestroy(a); return fail(h, TOWR_ERR_HIP, "hipEventCreate failed"); }
+    h->ev_c.push_back(a); h->ev_d.push_back(b);
+  }
+  return TOWR_OK;
+}
+
+// Host-pointer evaluation (IpoptAdapter-shaped entry points and the host batch).
+//   * x goes H2D straight from the caller's array when it is registered (towr_gpu_register_host),
+//     else through the pinned staging;
+//   * B = 1 runs the single-launch group (every class in one kernel) when the layout has one, zero-copy
+//     (x read and g / values written through mapped host memory, see below);
+//   * B > 1 is cut into chunks of ~64 MB of output: the handle's stream evaluates chunk i while the
+//     copy stream moves chunk i - 1 to the host (a PCIe DMA overlaps the next chunk's kernels), and
+//     the host thread copies finished chunks out of the staging in parallel with both. Outputs in
+//     registered caller memory are DMA'd in place (no host copy at all).
 int host_eval(towr_gpu_handle h, int B, const double* X, double* G, double* V, bool single) {
   const towr_terrain_t* ter;
   int per;
   if (int rc = batch_terrain(h, B, single, &ter, &per)) return rc;
   if (int rc = ensure_stage(h, B)) return rc;
   const Layout& L = h->L;
-  const size_t xb = sizeof(double) * (size_t)B * L.n, gb = sizeof(double) * (size_t)B * L.m,
-               vb = sizeof(double) * (size_t)B * L.nnz;
-  std::memcpy(h->h_x, X, xb);
-  HIPCHK(h, hipMemcpyAsync(h->d_x, h->h_x, xb, hipMemcpyHostToDevice, h->stream));
-  if (int rc = launch(h, B, h->d_x, L.n, h->d_g, L.m, h->d_v, L.nnz, G != nullptr, V != nullptr, h->stream, ter, per, -1))
-    return rc;
-  if (G) HIPCHK(h, hipMemcpyAsync(h->h_g, h->d_g, gb, hipMemcpyDeviceToHost, h->stream));
-  if (V) HIPCHK(h, hipMemcpyAsync(h->h_v, h->d_v, vb, hipMemcpyDeviceToHost, h->stream));
+  const size_t xb = sizeof(double) * (size_t)B * L.n;
+  const size_t gp = sizeof(double) * (size_t)L.m, vp = sizeof(double) * (size_t)L.nnz;   // per problem
+  const bool xr = is_registered(h, X, xb);
+  const bool gr = G && is_registered(h, G, gp * B), vr = V && is_registered(h, V, vp * B);
+  double* gdst = gr ? G : h->h_g;   // D2H destinations
+  double* vdst = vr ? V : h->h_v;
+  if (B == 1 && h->single.n_units > 0) {
+    // one problem, one launch, zero-copy: the kernel stages x from host memory and its copy-out writes
+    // g and the CSR values straight into host memory over PCIe (each value stored exactly once), so
+    // the call is one kernel and one synchronisation — no DMA command on either side
+    const double* xd = device_view(h, X, xb);
+    if (!xd) { std::memcpy(h->h_x, X, xb); xd = h->hd_x; }
+    double* gd = G ? device_view(h, G, gp) : nullptr;
+    double* vd = V ? device_view(h, V, vp) : nullptr;
+    if (int rc = launch_fused(h, h->single, 1, xd, L.n, gd ? gd : h->hd_g, L.m, vd ? vd : h->hd_v, L.nnz, G != nullptr, V != nullptr,
+                              h->stream, ter, per))
+      return rc;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (G && !gd) std::memcpy(G, h->h_g, gp);
+    if (V && !vd) par_copy(V, h->h_v, vp);
+    return TOWR_OK;
+  }
+  const double* xsrc = X;
+  if (!xr) { par_copy(h->h_x, X, xb); xsrc = h->h_x; }
+  HIPCHK(h, hipMemcpyAsync(h->d_x, xsrc, xb, hipMemcpyHostToDevice, h->stream));
+  const size_t out_pp = (G ? gp : 0) + (V ? vp : 0) + 1;
+  const int C = (int)std::max<size_t>(1, std::min<size_t>((size_t)B, (64u << 20) / out_pp));
+  const int nch = (B + C - 1) / C;
+  if (nch == 1) {   // one chunk (and B = 1): everything on the handle's stream
+    if (int rc = launch(h, B, h->d_x, L.n, h->d_g, L.m, h->d_v, L.nnz, G != nullptr, V != nullptr, h->stream, ter, per, -1))
+      return rc;
+    if (G) HIPCHK(h, hipMemcpyAsync(gdst, h->d_g, gp * B, hipMemcpyDeviceToHost, h->stream));
+    if (V) HIPCHK(h, hipMemcpyAsync(vdst, h->d_v, vp * B, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (G && !gr) par_copy(G, h->h_g, gp * B);
+    if (V && !vr) par_copy(V, h->h_v, vp * B);
+    return TOWR_OK;
+  }
+  if (int rc = ensure_events(h, (size_t)nch)) return rc;
+  for (int i = 0; i < nch; ++i) {   // enqueue: kernels on the stream, DMA on the copy stream
+    const int c0 = i * C, cb = std::min(C, B - c0);
+    if (int rc = launch(h, cb, h->d_x + (size_t)c0 * L.n, L.n, h->d_g + (size_t)c0 * L.m, L.m, h->d_v + (size_t)c0 * L.nnz, L.nnz,
+                        G != nullptr, V != nullptr, h->stream, per ? ter + c0 : ter, per, -1))
+      return rc;
+    HIPCHK(h, hipEventRecord(h->ev_c[i], h->stream));
+    HIPCHK(h, hipStreamWaitEvent(h->copy_stream, h->ev_c[i], 0));
+    if (G) HIPCHK(h, hipMemcpyAsync(gdst + (size_t)c0 * L.m, h->d_g + (size_t)c0 * L.m, gp * cb, hipMemcpyDeviceToHost, h->copy_stream));
+    if (V) HIPCHK(h, hipMemcpyAsync(vdst + (size_t)c0 * L.nnz, h->d_v + (size_t)c0 * L.nnz, vp * cb, hipMemcpyDeviceToHost, h->copy_stream));
+    HIPCHK(h, hipEventRecord(h->ev_d[i], h->copy_stream));
+  }
+  for (int i = 0; i < nch; ++i) {   // drain: each chunk leaves the staging while later ones move
+    const int c0 = i * C, cb = std::min(C, B - c0);
+    HIPCHK(h, hipEventSynchronize(h->ev_d[i]));
+    if (G && !gr) par_copy(G + (size_t)c0 * L.m, h->h_g + (size_t)c0 * L.m, gp * cb);
+    if (V && !vr) par_copy(V + (size_t)c0 * L.nnz, h->h_v + (size_t)c0 * L.nnz, vp * cb);
+  }
   HIPCHK(h, hipStreamSynchronize(h->stream));
-  if (G) std::memcpy(G, h->h_g, gb);
-  if (V) std::memcpy(V, h->h_v, vb);
   return TOWR_OK;
 }
 
@@ -1184,6 +1298,23 @@ int setup_fusion(towr_gpu_handle h, std::string& err) {
       if (fg.lds > 160 * 1024) { err = "tile too large for LDS"; return TOWR_ERR_UNSUPPORTED; }
     }
     p0 = p1 + 1;
+  }
+  // the single-problem group: every class of the layout in one launch (at B = 1 a launch is one wave
+  // of latency however wide, so one launch instead of three is the whole gain)
+  uint32_t all = 0;
+  bool fits = true;
+  for (int lc = 0; lc < LC_COUNT; ++lc)
+    if (class_units(L, lc) > 0) {
+      all |= 1u << lc;
+      if (lc != LC_MISC && L.type_block[class_type(lc)] != (lc == LC_DYN ? 256 : 192)) fits = false;
+    }
+  if (fits && __builtin_popcount(all) >= 2) {
+    towr_gpu_handle_s::FuseGroup& sg = h->single;
+    sg.mask = all;
+    sg.kblock = (all & (1u << LC_DYN)) || ((all & (1u << LC_MISC)) && 64 * kMiscWaves > 192) ? 256 : 192;
+    for (int lc = 0; lc < LC_COUNT; ++lc)
+      if ((all >> lc) & 1) sg.lds = std::max(sg.lds, lds_bytes(L, lc));
+    sg.n_units = sg.lds <= 160 * 1024 ? (int32_t)fused_units(L, all).size() : 0;
   }
   return TOWR_OK;
 }
@@ -1357,6 +1488,14 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
       h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
     }
   }
+  if (h->single.n_units > 0) {
+    towr_gpu_handle_s::FuseGroup& sg = h->single;
+    if ((r = upload(h, &sg.d_units, fused_units(L, sg.mask)))) return bail(r);
+    if (sg.lds > 64 * 1024 && hipFuncSetAttribute(step_kernel_for(L.gait, L.rotvec, sg.kblock), hipFuncAttributeMaxDynamicSharedMemorySize, (int)sg.lds) != hipSuccess) {
+      h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
+    }
+  }
+  if (hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking) != hipSuccess) { h->err = "hipStreamCreate failed"; return bail(TOWR_ERR_HIP); }
   for (int lc = 0; lc < LC_COUNT; ++lc) {
     if (class_units(L, lc) == 0) continue;
     const size_t lds = lds_bytes(L, lc);
@@ -1392,10 +1531,15 @@ int towr_gpu_destroy(towr_gpu_handle h) {
                  h->d_pinfo, h->d_pcols, h->d_pact, h->d_sched, h->d_misc, h->d_misc_lds, h->d_eelin, h->d_gtab, h->d_idir, h->d_citems, h->d_cq, h->fuse[0].d_units, h->fuse[1].d_units,
                  h->d_bterrain, h->d_x, h->d_g, h->d_v, h->d_f, h->d_grad,
                  h->d_traj_pd, h->d_traj_n, h->d_traj_c0, h->d_traj_t, h->d_fsb, h->d_fs_t, h->d_fs_tmpl, h->d_fs_ws,
-                 h->d_fs_iee, h->d_fs_irow, h->d_fsrec, h->d_lin, h->d_soft_b, h->d_soft_rp, h->d_soft_col, h->d_sg, h->d_sv};
+                 h->d_fs_iee, h->d_fs_irow, h->d_fsrec, h->d_lin, h->d_soft_b, h->d_soft_rp, h->d_soft_col, h->d_sg, h->d_sv,
+                 h->single.d_units};
   if (h->device >= 0) for (void* p : dev) if (p) (void)hipFree(p);
   void* host[] = {h->h_x, h->h_g, h->h_v};
   for (void* p : host) if (p) (void)hipHostFree(p);
+  for (const auto& r : h->pinned) (void)hipHostUnregister(const_cast<char*>(r.p));
+  for (hipEvent_t e : h->ev_c) (void)hipEventDestroy(e);
+  for (hipEvent_t e : h->ev_d) (void)hipEventDestroy(e);
+  if (h->copy_stream) (void)hipStreamDestroy(h->copy_stream);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   for (int i = 0; i < towr_gpu_handle_s::kMaxSide; ++i) {
     if (h->side[i]) (void)hipStreamDestroy(h->side[i]);
@@ -1642,6 +1786,38 @@ int towr_gpu_eval_batch(towr_gpu_handle h, int32_t B, const double* X, double* G
   if (!h || B < 0 || !X) return fail(h, TOWR_ERR_INVALID, "bad argument");
   if (int rc = bind(h)) return rc;
   return host_eval(h, B, X, G, V, false);
+}
+
+int towr_gpu_register_host(towr_gpu_handle h, void* ptr, int64_t bytes) {
+  if (!h || !ptr || bytes <= 0) return fail(h, TOWR_ERR_INVALID, "bad argument");
+  if (int rc = bind(h)) return rc;
+  const char* c = static_cast<const char*>(ptr);
+  for (const auto& r : h->pinned)
+    if (c < r.p + r.n && r.p < c + bytes) return fail(h, TOWR_ERR_INVALID, "range overlaps a registered range");
+  HIPCHK(h, hipHostRegister(ptr, (size_t)bytes, hipHostRegisterMapped));
+  void* dev = nullptr;
+  if (hipHostGetDevicePointer(&dev, ptr, 0) != hipSuccess || !dev) {
+    (void)hipHostUnregister(ptr);
+    return fail(h, TOWR_ERR_HIP, "hipHostGetDevicePointer failed for the registered range");
+  }
+  h->pinned.push_back({c, (size_t)bytes, static_cast<char*>(dev)});
+  return TOWR_OK;
+}
+
+int towr_gpu_unregister_host(towr_gpu_handle h, void* ptr) {
+  if (!h || !ptr) return fail(h, TOWR_ERR_INVALID, "bad argument");
+  for (size_t i = 0; i < h->pinned.size(); ++i)
+    if (h->pinned[i].p == static_cast<const char*>(ptr)) {
+      if (h->device >= 0) {
+        if (int rc = bind(h)) return rc;
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->copy_stream));
+        HIPCHK(h, hipHostUnregister(ptr));
+      }
+      h->pinned.erase(h->pinned.begin() + (std::ptrdiff_t)i);
+      return TOWR_OK;
+    }
+  return fail(h, TOWR_ERR_INVALID, "pointer was not registered with this handle");
 }
 
 int towr_gpu_set_tiles_per_block(towr_gpu_handle h, int32_t tiles_per_block) {

@@ -77,6 +77,9 @@ class Engine {
   int EvalBatchDevice(int B, const double* X, int64_t ldx, double* G, int64_t ldg, double* V, int64_t ldv, void* stream) const {
     return towr_gpu_eval_batch_device(h_, B, X, ldx, G, ldg, V, ldv, 1, 1, stream);
   }
+  // page-lock caller memory for in-place host transfers (towr_gpu_register_host); returns the status
+  int RegisterHost(void* p, size_t bytes) const { return towr_gpu_register_host(h_, p, (int64_t)bytes); }
+  int UnregisterHost(void* p) const { return towr_gpu_unregister_host(h_, p); }
   towr_gpu_handle handle() const { return h_; }
 
  private:
@@ -92,7 +95,18 @@ class Engine {
 // Number = double), as ifopt's IpoptAdapter implements them for towr, served by the engine.
 class NlpCallbacks {
  public:
-  explicit NlpCallbacks(Engine& e) : e_(e), g_(e.GetNumberOfConstraints()), v_(e.GetNumberOfJacobianNonzeros()) {}
+  // The g / values cache lives in page-locked memory, so every fused evaluation DMAs straight into it
+  // (a layout-only engine refuses the registration; the cache then stays pageable).
+  explicit NlpCallbacks(Engine& e) : e_(e), g_(e.GetNumberOfConstraints()), v_(e.GetNumberOfJacobianNonzeros()) {
+    pin_g_ = !g_.empty() && e_.RegisterHost(g_.data(), g_.size() * sizeof(double)) == TOWR_OK;
+    pin_v_ = !v_.empty() && e_.RegisterHost(v_.data(), v_.size() * sizeof(double)) == TOWR_OK;
+  }
+  ~NlpCallbacks() {
+    if (pin_g_) e_.UnregisterHost(g_.data());
+    if (pin_v_) e_.UnregisterHost(v_.data());
+  }
+  NlpCallbacks(const NlpCallbacks&) = delete;
+  NlpCallbacks& operator=(const NlpCallbacks&) = delete;
 
   bool eval_f(int n, const double* x, bool new_x, double& obj_value) {
     if (n != e_.GetNumberOfOptimizationVariables()) return false;
@@ -145,6 +159,7 @@ class NlpCallbacks {
   }
   Engine& e_;
   std::vector<double> g_, v_;
+  bool pin_g_ = false, pin_v_ = false;
   bool valid_ = false;
 };
 

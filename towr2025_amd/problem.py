@@ -63,6 +63,7 @@ class TowrGpuProblem:
         if rc != capi.TOWR_OK:
             raise TowrGpuError(f"towr_gpu_create failed ({rc}): {self._lib.towr_gpu_last_error(None).decode()}")
         self._h = h
+        self._pinned = {}
         n, m, nnz = C.c_int32(), C.c_int32(), C.c_int64()
         self._check(self._lib.towr_gpu_sizes(h, C.byref(n), C.byref(m), C.byref(nnz)))
         self.n, self.m, self.nnz = n.value, m.value, nnz.value
@@ -73,8 +74,9 @@ class TowrGpuProblem:
 
     def close(self):
         if getattr(self, "_h", None):
-            self._lib.towr_gpu_destroy(self._h)
+            self._lib.towr_gpu_destroy(self._h)   # unregisters the registered host arrays
             self._h = None
+            self._pinned = {}
 
     def __del__(self):
         try:
@@ -135,6 +137,25 @@ class TowrGpuProblem:
         g, v = np.zeros(self.m), np.zeros(self.nnz)
         self._check(self._lib.towr_gpu_eval_g_jac(self._h, capi.dptr(x), capi.dptr(g), capi.dptr(v)))
         return g, v
+
+    def eval_g_jac_into(self, x, g, v):
+        """eval_g + eval_jac_g into caller arrays (contiguous float64): with x, g, v registered
+        (register_host) the transfers run in place, as an IPOPT driver reusing its buffers would."""
+        for a, k in ((x, self.n), (g, self.m), (v, self.nnz)):
+            if a.dtype != np.float64 or not a.flags.c_contiguous or a.size < k:
+                raise TowrGpuError("eval_g_jac_into: contiguous float64 arrays of n / m / nnz entries expected")
+        self._check(self._lib.towr_gpu_eval_g_jac(self._h, capi.dptr(x), capi.dptr(g), capi.dptr(v)))
+
+    def register_host(self, a):
+        """Page-lock a contiguous numpy array for in-place host transfers (towr_gpu_register_host)."""
+        if not a.flags.c_contiguous:
+            raise TowrGpuError("register_host: contiguous array expected")
+        self._check(self._lib.towr_gpu_register_host(self._h, C.c_void_p(a.ctypes.data), a.nbytes))
+        self._pinned[a.ctypes.data] = a   # keep it alive while registered
+
+    def unregister_host(self, a):
+        self._check(self._lib.towr_gpu_unregister_host(self._h, C.c_void_p(a.ctypes.data)))
+        self._pinned.pop(a.ctypes.data, None)
 
     def eval_f(self, x) -> float:
         """Objective (IpoptAdapter::eval_f): the sum of every cost term."""
@@ -201,11 +222,17 @@ class TowrGpuProblem:
         arr = (capi.Terrain * len(terrains))(*terrains)
         self._check(self._lib.towr_gpu_set_batch_terrain(self._h, len(terrains), arr))
 
-    def eval_batch(self, X):
-        """Host batch: X (B, n) -> G (B, m), V (B, nnz)."""
+    def eval_batch(self, X, G=None, V=None):
+        """Host batch: X (B, n) -> G (B, m), V (B, nnz) (new arrays, or the given contiguous ones)."""
         X = np.ascontiguousarray(X, dtype=np.float64)
         B = X.shape[0]
-        G, V = np.zeros((B, self.m)), np.zeros((B, self.nnz))
+        if G is None:
+            G = np.zeros((B, self.m))
+        if V is None:
+            V = np.zeros((B, self.nnz))
+        for a, k, name in ((G, self.m, "G"), (V, self.nnz, "V")):
+            if a.dtype != np.float64 or not a.flags.c_contiguous or a.shape != (B, k):
+                raise TowrGpuError(f"eval_batch: {name} must be a contiguous float64 array of shape ({B}, {k})")
         self._check(self._lib.towr_gpu_eval_batch(self._h, B, capi.dptr(X), capi.dptr(G), capi.dptr(V)))
         return G, V
 
