@@ -196,6 +196,8 @@ __device__ __forceinline__ void stage_x(const KParams& P, const double* xg, doub
     stage16<BLOCK>(reinterpret_cast<uint4*>(ns), reinterpret_cast<const uint4*>(P.nodecol), (P.n_nodecol + 3) >> 2);
 }
 
+hipError_t fs_set_timing_buffer(void* p);   // fstream.hip: its translation unit's timing buffer
+
 // Phase timing (tools/phase_timing.py; only in the -DTOWR_PHASE_TIMING build, never in the product):
 // per block, 16 timestamps: [0] realtime start, [1] memtime start, [2] after staging, [3..6] each
 // wave's end of evaluation, [7] after the evaluation barrier, [8] end of wave 0's copy-out,
