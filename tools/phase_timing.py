@@ -80,6 +80,10 @@ def main():
         evs = [f"{(e.mean() if len(e) else 0.0):6.2f}" for e in ev]
         print(f"{name:20s} {len(t):7d} {stage.mean():7.2f} {evs[0]:>8s} {evs[1]} {evs[2]} {evs[3]} {bar.mean():6.2f} {copy.mean():6.2f} "
               f"{real_life.mean():6.2f} {span:7.1f} {resident:8.1f}")
+        probes = [(s, t[:, s]) for s in range(10, 16) if (t[:, s] > 0).any()]
+        if probes:   # engine_math.h TG_STAMP probes (wave 2), us after the staging barrier
+            print("    probes (wave 2, us after staging): " +
+                  "  ".join(f"[{s}] {((v[v > 0] - t[v > 0, 2]) * us_per_tick).mean():.2f}" for s, v in probes))
 
 
 if __name__ == "__main__":

@@ -1263,6 +1263,14 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
   }
 }
 
+// in-kernel timestamps of the phase-timing build (kernel_common.h tg_stamp_hook), else nothing
+#if defined(TOWR_PHASE_TIMING) && defined(__HIP_DEVICE_COMPILE__)
+__device__ void tg_stamp_hook(int slot);
+#define TG_STAMP(slot) tg_stamp_hook(slot)
+#else
+#define TG_STAMP(slot) do { } while (0)
+#endif
+
 // RangeOfMotionConstraint instant (range_of_motion_constraint.cc:72-131)
 template <class Emit>
 TG_HD void eval_rom(const Ctx& c, const ItemDesc& it, Emit& em) {
@@ -1271,11 +1279,14 @@ TG_HD void eval_rom(const Ctx& c, const ItemDesc& it, Emit& em) {
   SplinePt L, A, P;
   spline_eval(c, SP_BASE_LIN, t, L);
   spline_eval(c, SP_BASE_ANG, t, A);
+  TG_STAMP(10);
   spline_eval(c, sp_motion(ee), t, P);
+  TG_STAMP(11);
   double R[3][3];
   Trig q{};
   if (c.rotvec) rv_rodrigues(A.p, R);
   else { q = trig(A.p); euler_R(q, R); }
+  TG_STAMP(12);
   const double rW[3] = {P.p[0] - L.p[0], P.p[1] - L.p[1], P.p[2] - L.p[2]};
   double H[4];
   if (it.group == 1 && c.rotvec) {
@@ -1315,9 +1326,11 @@ TG_HD void eval_rom(const Ctx& c, const ItemDesc& it, Emit& em) {
     for (int r = 0; r < 3; ++r)
       #pragma unroll
       for (int e = 0; e < 3; ++e) emit_dim(c, em, r0 + r, sp_motion(ee), P, H, e, R[e][r]);
+    TG_STAMP(13);
     if (c.gait) {   // b_R_w * d pos / d schedule (range_of_motion_constraint.cc:123-130)
       SchedJac Jx;
       sched_jac(c, sp_motion(ee), t, P, Jx);
+      TG_STAMP(14);
       #pragma unroll
       for (int r = 0; r < 3; ++r)
         if (em_wants(em, r0 + r))

@@ -109,6 +109,10 @@ __global__ void __launch_bounds__(BLOCK, 1) towr_fdisc_inst_kernel(KParams P, do
 // Records are instant-major with an odd stride: a wave's lanes mostly read different fields of one or
 // two instants, which then fall in different banks (field-major, every field of an instant sat in
 // the same bank and the window reads serialized).
+#ifndef TOWR_FS_UNITS
+#define TOWR_FS_UNITS 4
+#endif
+constexpr int kFsUnits = TOWR_FS_UNITS;   // 16-byte units composed per lane before their stores
 constexpr int kFsD = 33;   // doubles per instant: window sums, b, d force / d schedule (dx, v)
 constexpr int kFsHv = 0, kFsB = kFsWin, kFsDx = kFsWin + 15, kFsV = kFsWin + 18;
 static_assert(kFsV + 3 == kFsD, "FsBlock LDS record");
@@ -157,10 +161,9 @@ __global__ void __launch_bounds__(BLOCK, 1) towr_fdisc_stream_kernel(KParams P, 
     for (int i = 0; i < 5; ++i)
 #pragma unroll
       for (int e = 0; e < 3; ++e) cd[k * kFsD + kFsB + 3 * i + e] = bb[i][e];
-    const int ws = P.fs_ws[fb.wsoff + poly];
+    const int ws = P.fs_ws[2 * (fb.wsoff + poly)], wd = P.fs_ws[2 * (fb.wsoff + poly) + 1];
     double h0 = h[0], h1 = h[1], h2 = h[2], h3 = h[3];
     asm volatile("" : "+v"(h0), "+v"(h1), "+v"(h2), "+v"(h3));
-    int wd = 0;
 #pragma unroll
     for (int q = 0; q < kFsWin; ++q) {
       const int pos = ws + q;
@@ -168,7 +171,6 @@ __global__ void __launch_bounds__(BLOCK, 1) towr_fdisc_stream_kernel(KParams P, 
       if (pos < fb.L) {
         const PhaseCol pq = pcl[pos];
         v = phase_basis_sum(pq, poly, h0, h1, h2, h3);
-        wd |= ((P.fs_tmpl[fb.tmpl + pos] >> 24) & 3) << (2 * q);
       }
       cd[k * kFsD + kFsHv + q] = v;
     }
@@ -223,19 +225,26 @@ __global__ void __launch_bounds__(BLOCK, 1) towr_fdisc_stream_kernel(KParams P, 
     if (head && tid == 0) __builtin_nontemporal_store(value(0), out);
     const int m2 = (n - head) >> 1;
     dbl2_t* d2 = reinterpret_cast<dbl2_t*>(out + head);
-#pragma unroll 2
-    for (int u = tid; u < m2; u += BLOCK) {   // one row computation per 16-byte unit
-      const int e = head + 2 * u;
-      const int r = (int)(((float)e + 0.5f) * invL);
-      const int j = e - r * Lr;
-      dbl2_t v;
+    // kFsUnits units per lane composed into registers first, then stored together, so a lane keeps
+    // kFsUnits stores in flight instead of one store per LDS round trip
+    for (int u0 = tid; u0 < m2; u0 += BLOCK * kFsUnits) {
+      dbl2_t v[kFsUnits];
+#pragma unroll
+      for (int q = 0; q < kFsUnits; ++q) {
+        const int u = u0 + q * BLOCK;
+        const int e = head + 2 * u;
+        const int r = (int)(((float)e + 0.5f) * invL);
+        const int j = e - r * Lr;
 #if TOWR_FS_EXP == 1   // timing experiment only: zeros, no composition
-      v.x = 0.0 * r; v.y = 0.0 * j;
+        v[q].x = 0.0 * r; v[q].y = 0.0 * j;
 #else
-      v.x = entry(r, j);
-      v.y = j + 1 < Lr ? entry(r, j + 1) : entry(r + 1, 0);
+        v[q].x = u < m2 ? entry(r, j) : 0.0;
+        v[q].y = u < m2 ? (j + 1 < Lr ? entry(r, j + 1) : entry(r + 1, 0)) : 0.0;
 #endif
-      __builtin_nontemporal_store(v, d2 + u);
+      }
+#pragma unroll
+      for (int q = 0; q < kFsUnits; ++q)
+        if (u0 + q * BLOCK < m2) __builtin_nontemporal_store(v[q], d2 + u0 + q * BLOCK);
     }
     if (((n - head) & 1) && tid == 0) __builtin_nontemporal_store(value(n - 1), out + n - 1);
   }

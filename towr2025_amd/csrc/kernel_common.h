@@ -207,6 +207,7 @@ static __device__ unsigned long long* g_tbuf;   // one per translation unit
 #define TSTAMP(slot, v) do { if (g_tbuf && (threadIdx.x & 63) == 0) g_tbuf[(size_t)blockIdx.x * 16 + (slot)] = (v); } while (0)
 #define TS_MEM() ((unsigned long long)__builtin_amdgcn_s_memtime())
 #define TS_REAL() ((unsigned long long)__builtin_amdgcn_s_memrealtime())
+__device__ __attribute__((noinline)) void tg_stamp_hook(int slot) { if ((threadIdx.x >> 6) == 2) TSTAMP(slot, TS_MEM()); }   // engine_math.h probes: wave 2
 #else
 #define TSTAMP(slot, v) do { } while (0)
 #endif

@@ -97,7 +97,7 @@ struct Layout {
   std::vector<FsBlock> fs_blocks;
   std::vector<double> fs_t;
   std::vector<int32_t> fs_tmpl;
-  std::vector<int32_t> fs_ws;        // window start per (constraint, force polynomial)
+  std::vector<int32_t> fs_ws;        // per (constraint, force polynomial): window start, window dimension codes
   std::vector<int32_t> fs_iee, fs_irow;   // per instant (fs_t order): endeffector, first row
   int32_t fs_tmpl_max = 0;
   // cost terms (eval_f / eval_grad_f): work items sorted by CostType, one block per problem

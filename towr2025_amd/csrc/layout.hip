@@ -492,7 +492,7 @@ int build_fstream(Layout& L, std::string& err) {
     }
     if (nsch != si.n_phases - 1) return TOWR_OK;
     // window start of each force polynomial: the columns it touches (pact ranges of its 3 dims)
-    const int wsoff = (int)wsv.size();
+    const int wsoff = (int)wsv.size() / 2;
     for (int p = 0; p < m.n_polys; ++p) {
       int lo = INT32_MAX, hi = -1;
       for (int e = 0; e < 3; ++e) {
@@ -504,7 +504,12 @@ int build_fstream(Layout& L, std::string& err) {
         }
       }
       if (hi >= 0 && hi - lo >= kFsWin) return TOWR_OK;
-      wsv.push_back(hi >= 0 ? lo : 0);
+      const int ws = hi >= 0 ? lo : 0;
+      int32_t wd = 0;   // dimension code of each window position (the stream kernel's prologue reads it once)
+      for (int q = 0; q < kFsWin; ++q)
+        if (ws + q < L0) wd |= ((tmpl[toff + ws + q] >> 24) & 3) << (2 * q);
+      wsv.push_back(ws);
+      wsv.push_back(wd);
     }
     lmax = std::max(lmax, (int)L0);
     // the constraint's instants, in row order (one instant per 5 rows)

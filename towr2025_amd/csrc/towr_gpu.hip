@@ -46,8 +46,9 @@ namespace {
 // absent candidates (positions >= nvals, the dummy slots) are not stored. The lane's item may be
 // row-split (ItemDesc::rsel): only its rows' candidates are emitted (and counted), exactly as the
 // structure pass recorded them, and only those rows' g.
-template <int BLOCK, int DEPTH, bool DIRECT = false>
+template <int BLOCK, int DEPTH, bool DIRECT = false, int PRE = 1>
 struct TileEmit {
+  static_assert(PRE >= 0 && PRE <= 6 && PRE <= kSlotSpare + 2, "preloaded slot groups: 0 .. 6, within the spare groups");
   const SlotGroup* slot;   // this lane's group 0; group g at slot[g * BLOCK]
   double* out;             // LDS tile, tile-relative (DIRECT: V at the tile's first value)
   double* gout;            // LDS g rows, tile-relative (DIRECT: the problem's g)
@@ -60,9 +61,26 @@ struct TileEmit {
   int qg = 0;              // DIRECT: slot group held in q[0] (the ring reloads lazily, on use)
   static constexpr bool kFilter = DIRECT;
   __device__ __forceinline__ bool want(int row) const { return !DIRECT || fcnt == 0 || (unsigned)(row - flo) < (unsigned)fcnt; }
+  // DIRECT: slot groups 0 .. kPre - 1 are loaded at construction into named registers (a runtime-
+  // indexed array would go to scratch); on gfx950 vmcnt counts stores too, so a group loaded after the
+  // lane's first value stores waits for all of them (measured: the RangeOfMotion base lanes, 36
+  // slot-path candidates, were the gait tile's slowest waves)
+  static constexpr int kPre = DIRECT ? PRE : 0;
+  u32x4_t p0 = {}, p1 = {}, p2 = {}, p3 = {}, p4 = {}, p5 = {};   // native vectors: a SlotGroup (array) would go to scratch
   __device__ __forceinline__ TileEmit(const SlotGroup* s, double* o, double* go) : slot(s), out(o), gout(go) {
+    if constexpr (DIRECT) {
+      const u32x4_t* sv = reinterpret_cast<const u32x4_t*>(s);
+      if (kPre > 0) p0 = sv[0];
+      if (kPre > 1) p1 = sv[BLOCK];
+      if (kPre > 2) p2 = sv[2 * BLOCK];
+      if (kPre > 3) p3 = sv[3 * BLOCK];
+      if (kPre > 4) p4 = sv[4 * BLOCK];
+      if (kPre > 5) p5 = sv[5 * BLOCK];
+      qg = -1;
+    } else {
 #pragma unroll
-    for (int d = 0; d < DEPTH; ++d) q[d] = s[d * BLOCK];
+      for (int d = 0; d < DEPTH; ++d) q[d] = s[d * BLOCK];
+    }
   }
   bool gon = true;         // DIRECT: g requested
   __device__ __forceinline__ void g(int row, double v) {
@@ -98,12 +116,19 @@ struct TileEmit {
         s = dd.off[1] + col;
       } else {
         const int g = j >> 3;
-        if (g != qg) {
-#pragma unroll
-          for (int d = 0; d < DEPTH; ++d) q[d] = slot[(g + d) * BLOCK];
-          qg = g;
+        if (g < kPre) {   // preloaded before any store of this lane (no wait behind the value stores)
+          const u32x4_t v = g == 0 ? p0 : g == 1 ? p1 : g == 2 ? p2 : g == 3 ? p3 : g == 4 ? p4 : p5;
+          const int k = j & 7;
+          const uint32_t lo = (k & 2) ? v.y : v.x, hi = (k & 2) ? v.w : v.z;
+          const uint32_t w = (k & 4) ? hi : lo;
+          s = (k & 1) ? (int)(w >> 16) : (int)(w & 0xFFFFu);
+        } else {
+          if (g != qg) {
+            q[0] = slot[g * BLOCK];
+            qg = g;
+          }
+          s = slot_pick(q[0], j & 7);
         }
-        s = slot_pick(q[0], j & 7);
       }
       ++j;
       if (fence) {   // wave-level: the zero stores of this wave's rows (tile_body) land first
@@ -172,6 +197,13 @@ static_assert(kDynG0Cand - (kDynG0PhaseA - kDynG0PhaseA % 8) <= 32, "phase B of 
 constexpr int slot_depth(int) { return 2; }
 static_assert(slot_depth(IT_ROM) <= kSlotSpare, "slot prefetch past the spare groups");
 
+// Slot groups preloaded by the gait (DIRECT) emitter per tile class: RangeOfMotion's base lanes emit
+// 33-36 slot-path candidates each (5 groups); Dynamic's kernel is at 256 VGPRs already (more spills)
+#ifndef TOWR_GAIT_SLOT_PRE_ROM
+#define TOWR_GAIT_SLOT_PRE_ROM 6
+#endif
+constexpr int gait_slot_pre(int type) { return type == IT_ROM ? TOWR_GAIT_SLOT_PRE_ROM : 1; }
+
 template <int TYPE, class Emit>
 __device__ __forceinline__ void eval_typed(const Ctx& c, const ItemDesc& it, Emit& em) {
   if constexpr (TYPE == IT_DYN) eval_dyn(c, it, em);
@@ -228,7 +260,7 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
     it = ItemDesc{}; it.type = IT_NONE; it.slot = 0;
   }
   // GAIT: direct HBM emission into the zero-filled V (see TileEmit)
-  TileEmit<TBLOCK, slot_depth(TYPE), GAIT> em(P.slots + it.slot, GAIT ? Vb + T.v0 : smem, GAIT ? Gb : smem + lds_rows_off - T.r0);
+  TileEmit<TBLOCK, slot_depth(TYPE), GAIT, gait_slot_pre(TYPE)> em(P.slots + it.slot, GAIT ? Vb + T.v0 : smem, GAIT ? Gb : smem + lds_rows_off - T.r0);
   if constexpr (GAIT) {
     if (it.rsel > 0) { em.flo = it.row0 + rsel_first(it.rsel); em.fcnt = rsel_count(it.rsel); }
     em.nvals = P.want_jac ? T.v1 - T.v0 : 0;
