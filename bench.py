@@ -376,6 +376,30 @@ def main():
                                     "note": "BASELINE configs[3] formulation (ANYmal, phase-duration optimisation), "
                                             "randomised Flat/Stairs instances, durations +-3 %"}
         gprob.close()
+    if rank == 0 and not args.no_gait:
+        # RotVecConverter base orientation (Parameters::RotationVector) on the same
+        # randomised instances: the headline formulation with the rotation-vector base parameterisation
+        fr = F.anymal_trot()
+        fr.params_.angular_rep_ = 1
+        rprob = TowrGpuProblem(fr.to_desc(), device=local)
+        rprob.set_batch_terrain(terrains)
+        Gr = torch.empty((B, (rprob.m + 15) // 16 * 16), dtype=torch.float64, device=dev)
+        Vr = torch.empty((B, (rprob.nnz + 15) // 16 * 16), dtype=torch.float64, device=dev)
+        for i in range(2):
+            rprob.eval_batch_device(X[i % N_X], Gr, Vr, stream=stream)
+        a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for i in range(reps):
+            rprob.eval_batch_device(X[i % N_X], Gr, Vr, stream=stream)
+        z.record(stream)
+        torch.cuda.synchronize()
+        ms = a.elapsed_time(z) / reps
+        rb = rprob.algorithmic_bytes_per_call()
+        out["rotvec"] = {"value": B / (ms * 1e-3), "unit": "calls/s", "ms_per_batch": ms, "problems": B,
+                         "n": rprob.n, "m": rprob.m, "nnz": rprob.nnz, "GB/s": B * rb / (ms * 1e-3) / 1e9,
+                         "note": "ANYmal trot with the RotVecConverter base orientation (angular_rep = 1), the "
+                                 "headline's randomised instances and x"}
+        rprob.close()
     if rank == 0 and not args.no_host:
         # PCIe-inclusive rate through the host-buffer entry point (towr_gpu_eval_batch: H2D of X,
         # chunked launches, D2H of G and V overlapping the next chunk) — reported beside, never as `value`

@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rotvec", action="store_true")
+    ap.add_argument("--no-gait", action="store_true", help="the headline formulation (fixed phase durations)")
     args = ap.parse_args()
     import torch
     from towr2025_amd import _capi as capi
@@ -26,12 +27,12 @@ def main():
     from towr2025_amd import TowrGpuProblem
     from towr2025_amd import formulation as F
     import bench
-    f = F.anymal_trot(optimize_timings=True)
+    f = F.anymal_trot(optimize_timings=not args.no_gait)
     if args.rotvec:
         f.params_.angular_rep_ = 1
     p = TowrGpuProblem(f.to_desc(), device=0)
     B = args.batch
-    Xh, ter = bench.make_batch(p, B, 0, optimize_timings=True)
+    Xh, ter = bench.make_batch(p, B, 0, optimize_timings=not args.no_gait)
     p.set_batch_terrain(ter)
     dev = torch.device("cuda", 0)
     X = torch.from_numpy(np.ascontiguousarray(Xh[0])).to(dev)

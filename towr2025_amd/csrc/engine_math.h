@@ -648,7 +648,7 @@ TG_HD void mat3_vec(const double A[3][3], const double v[3], double o[3]) {
 // axis l. The reference's skip rules (|.| > 1e-15) and its small-angle branches are kept.
 // ----------------------------------------------------------------------------------------------
 constexpr double kRvEps = 1e-10;   // kEps, rotvec_converter.cc:10
-struct RvCoeffs { double alpha, beta, gamma, dalpha, dbeta, dgamma; };
+struct RvCoeffs { double alpha, beta, gamma, dalpha, dbeta, dgamma, st, ct; };   // st, ct: sin, cos (theta >= eps)
 TG_HD double rv_norm(const double v[3]) { return sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); }
 // ComputeCoeffs (:30-59)
 TG_HD RvCoeffs rv_coeffs(double theta) {
@@ -657,8 +657,10 @@ TG_HD RvCoeffs rv_coeffs(double theta) {
   if (theta < kRvEps) {
     c.alpha = 1.0 - t2 / 6.0; c.beta = 1.0 / 6.0 - t2 / 120.0; c.gamma = 0.5 - t2 / 24.0;
     c.dalpha = -theta / 3.0; c.dbeta = -theta / 60.0; c.dgamma = -theta / 12.0;
+    c.st = c.ct = 0.0;
   } else {
     const double st = sin(theta), ct = cos(theta), t3 = t2 * theta, t4 = t3 * theta;
+    c.st = st; c.ct = ct;
     c.alpha = st / theta; c.beta = (theta - st) / t3; c.gamma = (1.0 - ct) / t2;
     c.dalpha = (theta * ct - st) / t2;
     c.dbeta = (-2.0 * theta - theta * ct + 3.0 * st) / t4;
@@ -675,44 +677,53 @@ TG_HD void m3_mul(const double A[3][3], const double B[3][3], double C[3][3]) { 
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) C[i][j] = A[i][0] * B[0][j] + A[i][1] * B[1][j] + A[i][2] * B[2][j];
 }
-// Rodrigues (:61-72)
-TG_HD void rv_rodrigues(const double rv[3], double R[3][3]) {
-  const double theta = rv_norm(rv);
+// Rodrigues (:61-72); the _c variants take theta = |rv| and rv_coeffs(theta) from the caller, so a
+// lane evaluating several converter quantities at one instant forms the trigonometry once
+// (sin(theta) / theta and (1 - cos(theta)) / theta^2 are ComputeCoeffs' alpha and gamma)
+TG_HD void rv_rodrigues_c(const double rv[3], double theta, const RvCoeffs& c, double R[3][3]) {
   double K[3][3]; rv_skew(rv, K);
   if (theta < kRvEps) {
     for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) R[i][j] = (i == j ? 1.0 : 0.0) + K[i][j];
     return;
   }
-  const double sn = sin(theta) / theta, h = (1.0 - cos(theta)) / (theta * theta);
+  const double sn = c.alpha, h = c.gamma;
   double KK[3][3]; m3_mul(K, K, KK);
   for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) R[i][j] = ((i == j ? 1.0 : 0.0) + sn * K[i][j]) + h * KK[i][j];
 }
-// LeftJacobian (:74-85)
-TG_HD void rv_left_jac(const double rv[3], double J[3][3]) {
+TG_HD void rv_rodrigues(const double rv[3], double R[3][3]) {
   const double theta = rv_norm(rv);
+  rv_rodrigues_c(rv, theta, rv_coeffs(theta), R);
+}
+// LeftJacobian (:74-85)
+TG_HD void rv_left_jac_c(const double rv[3], double theta, const RvCoeffs& c, double J[3][3]) {
   double S[3][3]; rv_skew(rv, S);
   if (theta < kRvEps) {
     for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) J[i][j] = (i == j ? 1.0 : 0.0) + 0.5 * S[i][j];
     return;
   }
-  const RvCoeffs c = rv_coeffs(theta);
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) J[i][j] = (c.alpha * (i == j ? 1.0 : 0.0) + c.beta * (rv[i] * rv[j])) + c.gamma * S[i][j];
 }
-// LeftJacobianDot (:87-107)
-TG_HD void rv_left_jac_dot(const double rv[3], const double rvd[3], double J[3][3]) {
+TG_HD void rv_left_jac(const double rv[3], double J[3][3]) {
   const double theta = rv_norm(rv);
+  rv_left_jac_c(rv, theta, rv_coeffs(theta), J);
+}
+// LeftJacobianDot (:87-107)
+TG_HD void rv_left_jac_dot_c(const double rv[3], const double rvd[3], double theta, const RvCoeffs& c, double J[3][3]) {
   double S[3][3], Sd[3][3]; rv_skew(rv, S); rv_skew(rvd, Sd);
   if (theta < kRvEps) {
     for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) J[i][j] = 0.5 * Sd[i][j];
     return;
   }
-  const RvCoeffs c = rv_coeffs(theta);
   const double td = (rv[0] * rvd[0] + rv[1] * rvd[1] + rv[2] * rvd[2]) / theta;
   const double ad = c.dalpha * td, bd = c.dbeta * td, gd = c.dgamma * td;
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j)
       J[i][j] = (((ad * (i == j ? 1.0 : 0.0) + bd * (rv[i] * rv[j])) + c.beta * (rvd[i] * rv[j] + rv[i] * rvd[j])) + gd * S[i][j]) + c.gamma * Sd[i][j];
+}
+TG_HD void rv_left_jac_dot(const double rv[3], const double rvd[3], double J[3][3]) {
+  const double theta = rv_norm(rv);
+  rv_left_jac_dot_c(rv, rvd, theta, rv_coeffs(theta), J);
 }
 TG_HD double rv_sign(int dim, int j) { return ((j - dim + 3) % 3 == 1) ? -1.0 : 1.0; }   // [theta]x_{dim,j} = sign theta_k
 
@@ -741,6 +752,88 @@ TG_HD void rv_dJL(const double rv[3], double P[3][3][3]) {
       if (fabs(sk) > 1e-15) for (int l = 0; l < 3; ++l) p[l] += sk * (c.dgamma * nh[l]);
       if (fabs(c.gamma) > 1e-15 && dim != j) p[3 - dim - j] += c.gamma * rv_sign(dim, j);
     }
+}
+
+// Column l of rv_dJL: Pc[dim][j] = d J_L[dim][j] / d theta_l, the same operations in the same order
+// restricted to one l (the device's RotVec Dynamic evaluates its base-angular block one column at a time)
+TG_HD void rv_dJL_col(const double rv[3], const RvCoeffs& c, const double nh[3], int l, double Pc[3][3]) {
+  for (int dim = 0; dim < 3; ++dim)
+    for (int j = 0; j < 3; ++j) {
+      double p = 0.0;
+      if (dim == j) p += c.dalpha * nh[l];
+      const double rvdj = rv[dim] * rv[j];
+      if (fabs(rvdj) > 1e-15) p += rvdj * (c.dbeta * nh[l]);
+      if (fabs(c.beta) > 1e-15) {
+        if (fabs(rv[j]) > 1e-15 && l == dim) p += c.beta * rv[j];
+        if (fabs(rv[dim]) > 1e-15 && l == j) p += c.beta * rv[dim];
+      }
+      const double sk = dim == j ? 0.0 : rv_sign(dim, j) * rv[3 - dim - j];   // Skew(rv)[dim][j]
+      if (fabs(sk) > 1e-15) p += sk * (c.dgamma * nh[l]);
+      if (fabs(c.gamma) > 1e-15 && dim != j && l == 3 - dim - j) p += c.gamma * rv_sign(dim, j);
+      Pc[dim][j] = p;
+    }
+}
+// n_hat of rv_dJL (theta^T jac_pos / theta, components with |theta_l| > 1e-15)
+TG_HD void rv_dJL_nh(const double rv[3], double theta, double nh[3]) {
+  nh[0] = nh[1] = nh[2] = 0.0;
+  if (theta >= kRvEps) {
+    const double inv = 1.0 / theta;
+    for (int l = 0; l < 3; ++l) nh[l] = fabs(rv[l]) > 1e-15 ? rv[l] * inv : 0.0;
+  }
+}
+// Column l of rv_angacc_jac's Pa and Va (Aa = J_L): the same operations restricted to one l
+TG_HD void rv_angacc_col(const double rv[3], const double rvd[3], const double rva[3], int l, double theta, const RvCoeffs& c,
+                         const double JLd[3][3], const double nhd[3], double pa_l[3], double va_l[3]) {
+  double td = 0.0;
+  if (theta > kRvEps) td = (rv[0] * rvd[0] + rv[1] * rvd[1] + rv[2] * rvd[2]) / theta;
+  const double beta_dot = c.dbeta * td, gamma_dot = c.dgamma * td;
+  double nh = 0.0, dap = 0.0, dav = 0.0, dbp = 0.0, dbv = 0.0, dgp = 0.0, dgv = 0.0, nh_l[3] = {0.0, 0.0, 0.0};
+  if (theta > kRvEps) {
+    const double inv = 1.0 / theta, t2 = theta * theta, st = c.st, ct = c.ct;
+    nh = rv[l] * inv;
+    for (int k = 0; k < 3; ++k) nh_l[k] = rv[k] * inv;
+    const double dtp = rvd[l] * inv - (td * inv) * nh, dtv = rv[l] * inv;
+    const double alpha_pp = (-theta * st - 2.0 * (theta * ct - st) / theta) / t2;
+    double beta_pp, gamma_pp;
+    { const double num = -2.0 * theta - theta * ct + 3.0 * st, dnum = -2.0 - ct + theta * st + 3.0 * ct;
+      beta_pp = (dnum - 4.0 * num / theta) / (t2 * t2); }
+    { const double num = theta * st - 2.0 + 2.0 * ct, dnum = st + theta * ct - 2.0 * st;
+      gamma_pp = (dnum - 3.0 * num / theta) / (t2 * theta); }
+    dap = (alpha_pp * td) * nh + c.dalpha * dtp; dav = c.dalpha * dtv;
+    dbp = (beta_pp * td) * nh + c.dbeta * dtp;   dbv = c.dbeta * dtv;
+    dgp = (gamma_pp * td) * nh + c.dgamma * dtp; dgv = c.dgamma * dtv;
+  }
+  double P1[3][3]; rv_dJL_col(rv, c, nhd, l, P1);   // acc * dJL_du, column l
+  for (int dim = 0; dim < 3; ++dim) {
+    double pa = 0.0, va = 0.0;
+    for (int j = 0; j < 3; ++j) {
+      double p = 0.0, v = 0.0;   // d J_L_dot[dim][j] / d (theta_l, theta_dot_l)
+      if (dim == j) { p += dap; v += dav; }
+      const double rv_dj = rv[dim] * rv[j];
+      if (fabs(rv_dj) > 1e-15) { p += rv_dj * dbp; v += rv_dj * dbv; }
+      if (fabs(beta_dot) > 1e-15) {
+        if (fabs(rv[j]) > 1e-15 && l == dim) p += beta_dot * rv[j];
+        if (fabs(rv[dim]) > 1e-15 && l == j) p += beta_dot * rv[dim];
+      }
+      const double td_dj = rvd[dim] * rv[j] + rv[dim] * rvd[j];
+      if (fabs(td_dj) > 1e-15 && fabs(c.beta) > 1e-15 && theta > kRvEps) p += (c.dbeta * td_dj) * nh_l[l];
+      if (fabs(c.beta) > 1e-15) {
+        if (fabs(rv[j]) > 1e-15 && l == dim) v += c.beta * rv[j];
+        if (fabs(rvd[dim]) > 1e-15 && l == j) p += c.beta * rvd[dim];
+        if (fabs(rvd[j]) > 1e-15 && l == dim) p += c.beta * rvd[j];
+        if (fabs(rv[dim]) > 1e-15 && l == j) v += c.beta * rv[dim];
+      }
+      const double sk = dim == j ? 0.0 : rv_sign(dim, j) * rv[3 - dim - j];
+      if (fabs(sk) > 1e-15) { p += sk * dgp; v += sk * dgv; }
+      if (fabs(gamma_dot) > 1e-15 && dim != j && l == 3 - dim - j) p += gamma_dot * rv_sign(dim, j);
+      const double skd = dim == j ? 0.0 : rv_sign(dim, j) * rvd[3 - dim - j];
+      if (fabs(skd) > 1e-15 && fabs(c.gamma) > 1e-15 && theta > kRvEps) p += (c.dgamma * skd) * nh_l[l];
+      if (fabs(c.gamma) > 1e-15 && dim != j && l == 3 - dim - j) v += c.gamma * rv_sign(dim, j);
+      pa += rvd[j] * p; va += rvd[j] * v;
+    }
+    pa_l[dim] = pa + (rva[0] * P1[dim][0] + rva[1] * P1[dim][1] + rva[2] * P1[dim][2]);
+    va_l[dim] = va + JLd[dim][l];
+  }
 }
 
 // d omega / d nodes (GetDerivOfAngVelWrtNodes, :508-528): Pw (theta), Vw (theta_dot)
@@ -830,6 +923,22 @@ TG_HD void rv_rotvec_mult(const double R[3][3], const double JL[3][3], const dou
     rv_skew(Rv, S);
     for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) S[i][j] = -S[i][j];
     m3_mul(S, JL, A);
+  }
+}
+
+// column e of rv_rotvec_mult's coefficient matrix (its element expressions, one column)
+TG_HD void rv_rotvec_mult_col(const double R[3][3], const double JL[3][3], const double v[3], bool inverse, int e, double a[3]) {
+  double S[3][3];
+  if (inverse) {
+    double Sv[3][3], T[3][3], Rt[3][3];
+    for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) Rt[i][j] = R[j][i];
+    rv_skew(v, Sv); m3_mul(Rt, Sv, T);
+    for (int i = 0; i < 3; ++i) a[i] = T[i][0] * JL[0][e] + T[i][1] * JL[1][e] + T[i][2] * JL[2][e];
+  } else {
+    double Rv[3]; mat3_vec(R, v, Rv);
+    rv_skew(Rv, S);
+    for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) S[i][j] = -S[i][j];
+    for (int i = 0; i < 3; ++i) a[i] = S[i][0] * JL[0][e] + S[i][1] * JL[1][e] + S[i][2] * JL[2][e];
   }
 }
 
@@ -1071,63 +1180,87 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
     dyn_g0_b(c, it, em, st, fs, ts);
     return;
   }
+#ifdef TOWR_EXP_DYN_NOG1   // register-pressure experiment only: no base-angular group
+  if (it.group == 1) return;
+#endif
+#ifdef TOWR_EXP_DYN_NOEE   // register-pressure experiment only: no endeffector groups
+  if (it.group >= 2) return;
+#endif
   if (it.group == 1 && c.rotvec) {
     // d/d base-ang, RotVecConverter (GetJacobianWrtBaseAng :124-166 with the converter's
     // DerivOfRotVecMult / GetDerivOfAngVelWrtNodes / GetDerivOfAngAccWrtNodes), coefficient form:
     //   jac1 = d(R v11)/. + R I_b d(R^T wd)/. + I_w d wd/.
     //   jac2 = [w]x (d(R v21)/. + R I_b d(R^T w)/. + I_w d w/.) - [I_w w]x d w/.
+    // One rotation-vector component e (a column of every coefficient matrix) at a time, each column
+    // by the full-matrix code's element expressions: the whole matrices at once needed ~400 live
+    // doubles and spilled 884 bytes per lane to scratch.
     SplinePt A; spline_eval(c, SP_BASE_ANG, t, A);
-    double R[3][3], w[3], wd[3];
-    rv_state(A, R, w, wd);
-    double JL[3][3]; rv_left_jac(A.p, JL);
+    const double theta = rv_norm(A.p);
+    const RvCoeffs cf = rv_coeffs(theta);   // the instant's converter coefficients, formed once
+    double R[3][3], w[3], wd[3], JL[3][3], JLd[3][3];
+    rv_rodrigues_c(A.p, theta, cf, R);
+    rv_left_jac_c(A.p, theta, cf, JL);
+    rv_left_jac_dot_c(A.p, A.v, theta, cf, JLd);
+    {   // rv_state
+      double a[3], b[3];
+      mat3_vec(JL, A.v, w);
+      mat3_vec(JLd, A.v, a); mat3_vec(JL, A.a, b);
+      for (int k = 0; k < 3; ++k) wd[k] = a[k] + b[k];
+    }
     double RI[3][3], Iw[3][3];
     for (int i = 0; i < 3; ++i)
       for (int j = 0; j < 3; ++j) RI[i][j] = R[i][0] * c.rb.Ib[0 * 3 + j] + R[i][1] * c.rb.Ib[1 * 3 + j] + R[i][2] * c.rb.Ib[2 * 3 + j];
     for (int i = 0; i < 3; ++i)
       for (int j = 0; j < 3; ++j) Iw[i][j] = RI[i][0] * R[j][0] + RI[i][1] * R[j][1] + RI[i][2] * R[j][2];
-    double Mp[3][3], Mv[3][3], Ma[3][3];
-    {
-      double Pw[3][3], Vw[3][3], Pa[3][3], Va[3][3], Aa[3][3], T1[3][3], T2[3][3], T3[3][3];
-      rv_angvel_jac(A.p, A.v, Pw, Vw);
-      rv_angacc_jac(A.p, A.v, A.a, Pa, Va, Aa);
-      double u[3], v11[3], v21[3];
-      for (int j = 0; j < 3; ++j) u[j] = R[0][j] * wd[0] + R[1][j] * wd[1] + R[2][j] * wd[2];
-      for (int i = 0; i < 3; ++i) v11[i] = c.rb.Ib[i * 3 + 0] * u[0] + c.rb.Ib[i * 3 + 1] * u[1] + c.rb.Ib[i * 3 + 2] * u[2];
-      for (int j = 0; j < 3; ++j) u[j] = R[0][j] * w[0] + R[1][j] * w[1] + R[2][j] * w[2];
-      for (int i = 0; i < 3; ++i) v21[i] = c.rb.Ib[i * 3 + 0] * u[0] + c.rb.Ib[i * 3 + 1] * u[1] + c.rb.Ib[i * 3 + 2] * u[2];
-      // jac1, theta part
-      rv_rotvec_mult(R, JL, v11, false, Mp);
-      rv_rotvec_mult(R, JL, wd, true, T1); m3_mul(RI, T1, T2);
-      m3_mul(Iw, Pa, T3);
-      for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) Mp[i][j] = (Mp[i][j] + T2[i][j]) + T3[i][j];
-      // jac2 inner sum, theta part
-      double S[3][3];
-      rv_rotvec_mult(R, JL, v21, false, S);
-      rv_rotvec_mult(R, JL, w, true, T1); m3_mul(RI, T1, T2);
-      m3_mul(Iw, Pw, T3);
-      for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) S[i][j] = (S[i][j] + T2[i][j]) + T3[i][j];
-      double Iww[3]; mat3_vec(Iw, w, Iww);
-      for (int r = 0; r < 3; ++r)
-        for (int e = 0; e < 3; ++e) {
-          double a = 0.0, b = 0.0, av = 0.0, bv = 0.0;
-          for (int k = 0; k < 3; ++k) {
-            const double cw = cross_el(w, r, k), ci = cross_el(Iww, r, k);
-            a += cw * S[k][e]; b += ci * Pw[k][e];
-            double iv = Iw[k][0] * Vw[0][e] + Iw[k][1] * Vw[1][e] + Iw[k][2] * Vw[2][e];
-            av += cw * iv; bv += ci * Vw[k][e];
-          }
-          Mp[r][e] += a - b;
-          Mv[r][e] = (Iw[r][0] * Va[0][e] + Iw[r][1] * Va[1][e] + Iw[r][2] * Va[2][e]) + (av - bv);
-          Ma[r][e] = Iw[r][0] * Aa[0][e] + Iw[r][1] * Aa[1][e] + Iw[r][2] * Aa[2][e];
-        }
-    }
+    double u[3], v11[3], v21[3];
+    for (int j = 0; j < 3; ++j) u[j] = R[0][j] * wd[0] + R[1][j] * wd[1] + R[2][j] * wd[2];
+    for (int i = 0; i < 3; ++i) v11[i] = c.rb.Ib[i * 3 + 0] * u[0] + c.rb.Ib[i * 3 + 1] * u[1] + c.rb.Ib[i * 3 + 2] * u[2];
+    for (int j = 0; j < 3; ++j) u[j] = R[0][j] * w[0] + R[1][j] * w[1] + R[2][j] * w[2];
+    for (int i = 0; i < 3; ++i) v21[i] = c.rb.Ib[i * 3 + 0] * u[0] + c.rb.Ib[i * 3 + 1] * u[1] + c.rb.Ib[i * 3 + 2] * u[2];
+    double Iww[3]; mat3_vec(Iw, w, Iww);
+    double nhd[3]; rv_dJL_nh(A.p, theta, nhd);
     double Hp[4], Hv[4], Ha[4];
     spline_basis(A, kPos, Hp); spline_basis(A, kVel, Hv); spline_basis(A, kAcc, Ha);
-#pragma unroll 1
-    for (int e = 0; e < 3; ++e)
-      for (int r = 0; r < 3; ++r)
+    // one column per call: a RotVec g1 item carries its component in a1 (1 + e, layout.hip); the
+    // device evaluates exactly that column (a loop over three columns spilled to scratch), the host
+    // structure pass and emulation take every column of an unsplit item in order
+    auto column = [&](auto ec) {   // ec: std::integral_constant (the device instantiates each column)
+      constexpr int e = decltype(ec)::value;
+      double m1[3], t1[3], pa[3], va[3], pw[3];
+      {
+        double Pc[3][3]; rv_dJL_col(A.p, cf, nhd, e, Pc);   // Pw[:, e] (rv_angvel_jac)
+        for (int d = 0; d < 3; ++d) pw[d] = A.v[0] * Pc[d][0] + A.v[1] * Pc[d][1] + A.v[2] * Pc[d][2];
+      }
+      rv_angacc_col(A.p, A.v, A.a, e, theta, cf, JLd, nhd, pa, va);   // Pa[:, e], Va[:, e]
+      rv_rotvec_mult_col(R, JL, v11, false, e, m1);
+      rv_rotvec_mult_col(R, JL, wd, true, e, t1);
+      double mp[3], sc[3];
+      for (int i = 0; i < 3; ++i)
+        mp[i] = (m1[i] + (RI[i][0] * t1[0] + RI[i][1] * t1[1] + RI[i][2] * t1[2])) + (Iw[i][0] * pa[0] + Iw[i][1] * pa[1] + Iw[i][2] * pa[2]);
+      rv_rotvec_mult_col(R, JL, v21, false, e, m1);
+      rv_rotvec_mult_col(R, JL, w, true, e, t1);
+      for (int i = 0; i < 3; ++i)
+        sc[i] = (m1[i] + (RI[i][0] * t1[0] + RI[i][1] * t1[1] + RI[i][2] * t1[2])) + (Iw[i][0] * pw[0] + Iw[i][1] * pw[1] + Iw[i][2] * pw[2]);
+      for (int r = 0; r < 3; ++r) {
+        double a = 0.0, b = 0.0, av = 0.0, bv = 0.0;
+        for (int k = 0; k < 3; ++k) {
+          const double cw = cross_el(w, r, k), ci = cross_el(Iww, r, k);
+          a += cw * sc[k]; b += ci * pw[k];
+          double iv = Iw[k][0] * JL[0][e] + Iw[k][1] * JL[1][e] + Iw[k][2] * JL[2][e];
+          av += cw * iv; bv += ci * JL[k][e];
+        }
+        const double Mp = mp[r] + (a - b);
+        const double Mv = (Iw[r][0] * va[0] + Iw[r][1] * va[1] + Iw[r][2] * va[2]) + (av - bv);
+        const double Ma = Iw[r][0] * JL[0][e] + Iw[r][1] * JL[1][e] + Iw[r][2] * JL[2][e];
         for (int bb = 0; bb < 4; ++bb)
-          em(r0 + AX + r, basis_col(c, SP_BASE_ANG, A.poly, bb, e), Mp[r][e] * Hp[bb] + Mv[r][e] * Hv[bb] + Ma[r][e] * Ha[bb], true);
+          em(r0 + AX + r, basis_col(c, SP_BASE_ANG, A.poly, bb, e), Mp * Hp[bb] + Mv * Hv[bb] + Ma * Ha[bb], true);
+      }
+    };
+    // compile-time column indices: a runtime e indexes the 3x3 arrays dynamically, which puts them in scratch
+    const int e_lo = it.a1 > 0 ? it.a1 - 1 : 0, e_hi = it.a1 > 0 ? it.a1 : 3;
+    if (e_lo <= 0 && 0 < e_hi) column(std::integral_constant<int, 0>{});
+    if (e_lo <= 1 && 1 < e_hi) column(std::integral_constant<int, 1>{});
+    if (e_lo <= 2 && 2 < e_hi) column(std::integral_constant<int, 2>{});
     return;
   }
   if (it.group == 1) {

@@ -155,7 +155,7 @@ constexpr int tile_block(int type, bool gait) {
 
 // Launch geometry of each item type (wave-uniform: each wave of a block runs one code path)
 struct TypeSpec { int block; int max_inst; };
-TypeSpec type_spec(int type, int n_ee, bool gait);
+TypeSpec type_spec(int type, int n_ee, bool gait, bool rotvec = false);
 // thread (lane) of the block that evaluates row-part `sub` (0 .. split_rows - 1) of group `g` of
 // the k-th of n instances in a tile
 int type_lane(int type, int group, int k, int n, int n_ee, bool gait, int sub);

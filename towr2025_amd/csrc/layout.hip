@@ -695,7 +695,13 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
       case TOWR_C_DYNAMIC: {
         auto ts = dts_of(c.T, c.dt);
         for (int k = 0; k < (int)ts.size(); ++k, ++inst)
-          for (int g = 0; g < 2 + E; ++g) add(IT_DYN, g, 0, k, row + 6 * k, ts[k], 0, 0, 0.0);
+          for (int g = 0; g < 2 + E; ++g) {
+            if (g == 1 && L.rotvec) {   // RotVec base-angular block: one item per rotation-vector component
+              for (int ax = 0; ax < 3; ++ax) add(IT_DYN, g, 0, k, row + 6 * k, ts[k], 0, 1 + ax, 0.0);
+            } else {
+              add(IT_DYN, g, 0, k, row + 6 * k, ts[k], 0, 0, 0.0);
+            }
+          }
         info.rows = 6 * (int)ts.size();
         break;
       }
@@ -944,7 +950,7 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
         insts.push_back({(int32_t)j, (int32_t)(k - j)});
         j = k;
       }
-      const TypeSpec sp = type_spec(type, E, L.gait);
+      const TypeSpec sp = type_spec(type, E, L.gait, L.rotvec);
       const int n_inst = (int)insts.size();
       auto inst_rows = [&](int a, int b) {   // rows of instances [a, b)
         const int r0 = L.items[insts[a].first].row0;
@@ -977,7 +983,8 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
         for (int k = a; k < b; ++k)
           for (int q = 0; q < insts[k].count; ++q) {
             const ItemDesc& it = L.items[insts[k].first + q];
-            const int lane = type_lane(type, it.group, k - a, b - a, E, L.gait, it.rsel > 0 ? rsel_part(it.rsel) : 0);
+            int lane = type_lane(type, it.group, k - a, b - a, E, L.gait, it.rsel > 0 ? rsel_part(it.rsel) : 0);
+            if (type == IT_DYN && it.group == 1 && it.a1 > 0) lane = 64 + (it.a1 - 1) * (b - a) + (k - a);   // RotVec axis items
             if (lane < 0 || lane >= sp.block || lanes[lane].type != IT_NONE) { err = "internal: lane assignment"; return TOWR_ERR_INVALID; }
             lanes[lane] = it;
             if (type == IT_DYN) lanes[lane].a2 = k - a;   // instant within the tile (LDS sum terms)
@@ -1001,7 +1008,7 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
         L.tiles.push_back(td);
       }
       items.insert(items.end(), per_type_items[t].begin(), per_type_items[t].end());
-      L.type_block[t] = type_spec(t, E, L.gait).block;
+      L.type_block[t] = type_spec(t, E, L.gait, L.rotvec).block;
       // LDS: [tile values | 64 dummy slots (absent candidates, by wave lane) | g rows]
       L.type_lds_dummy_off[t] = (maxv + 1) & ~1;
       L.type_lds_rows_off[t] = L.type_lds_dummy_off[t] + 64;   // one per wave lane: waves never collide within an instruction
@@ -1012,7 +1019,7 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
       }
       if (t == IT_DYN) {   // + per-instant endeffector sum terms (dyn_g0_a)
         L.dyn_scr_off = L.type_lds[t];
-        L.type_lds[t] += type_spec(IT_DYN, E, L.gait).max_inst * E * 6;
+        L.type_lds[t] += type_spec(IT_DYN, E, L.gait, L.rotvec).max_inst * E * 6;
       }
     }
     L.type_tile0[IT_COUNT] = (int32_t)L.tiles.size();
@@ -1025,7 +1032,7 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
       int stride[IT_COUNT] = {}, rows_off[IT_COUNT] = {};
       for (int t = 0; t < IT_COUNT; ++t) {
         if (!is_misc_kind(t)) continue;
-        if (type_spec(t, E, L.gait).block != 64) { err = "internal: small kinds must use one-wave tiles"; return TOWR_ERR_INVALID; }
+        if (type_spec(t, E, L.gait, L.rotvec).block != 64) { err = "internal: small kinds must use one-wave tiles"; return TOWR_ERR_INVALID; }
         int mv = 0, mr = 0;
         for (int ti = L.type_tile0[t]; ti < L.type_tile0[t + 1]; ++ti) {
           mt.push_back(ti);
@@ -1162,11 +1169,12 @@ int split_rows(int type, int group, bool gait) {
   }
 }
 
-TypeSpec type_spec(int type, int n_ee, bool gait) {
+TypeSpec type_spec(int type, int n_ee, bool gait, bool rotvec) {
   const int E = std::max(1, n_ee);
   const int blk = tile_block(type, gait);
   switch (type) {
-    case IT_DYN: return {blk, std::max(1, std::min(64, gait ? 64 / E : 128 / E))};   // waves: g0 | g1 | ee, ee (gait: rows)
+    case IT_DYN:   // waves: g0 | g1 | ee, ee (gait: rows); RotVec: the g1 wave holds 3 lanes per instant
+      return {blk, std::max(1, std::min(rotvec ? 64 / 3 : 64, gait ? 64 / E : 128 / E))};
     case IT_ROM: return {blk, gait ? 128 : 64};                                         // waves: g0 | g1 | g2 (gait: rows, 2 halves)
     case IT_FDISC: return {blk, gait ? 128 : blk};
     case IT_TQDISC: return {blk, gait ? 64 : blk};
