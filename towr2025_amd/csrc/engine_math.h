@@ -1100,6 +1100,17 @@ TG_HD double dot3(const double a[3], const double b[3]) { return a[0] * b[0] + a
 // work items
 // ----------------------------------------------------------------------------------------------
 
+// Dynamic's base-angular block (group 1) as one item per axis (3 lanes per instant, ItemDesc::a1 = 1 +
+// axis). RotVec always (its three columns in one lane spilled 884 B/lane); Euler per TOWR_DYN_SPLIT_G1
+// (mask: bit 0 fixed gait, bit 1 phase-duration optimisation), off by default: the split kernel needs
+// 164 VGPRs instead of 242 (3 waves per SIMD), but measured slower on MI355X (ANYmal, B = 4096:
+// 0.063 ms unsplit, 0.074 ms split in one tile, 0.078 ms split in two tiles per problem) — every
+// axis lane recomputes the instant's shared state, and the block still waits for its slowest wave
+#ifndef TOWR_DYN_SPLIT_G1
+#define TOWR_DYN_SPLIT_G1 0
+#endif
+TG_HD constexpr bool split_base_ang(bool gait) { return ((TOWR_DYN_SPLIT_G1 >> (gait ? 1 : 0)) & 1) != 0; }
+
 // DynamicConstraint instant (dynamic_constraint.cc:63-148, single_rigid_body_dynamics.cc:76-204)
 // Group 0 of a DynamicConstraint instant (g: GetDynamicViolation :76-102; d/d base-lin:
 // GetJacobianWrtBaseLin :104-122) in two phases. Phase A needs no endeffector sum; phase B takes
@@ -1290,8 +1301,11 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
     double Iww[3]; mat3_vec(Iw, w, Iww);
     double Hp[4], Hv[4], Ha[4];
     spline_basis(A, kPos, Hp); spline_basis(A, kVel, Hv); spline_basis(A, kAcc, Ha);
-#pragma unroll
-    for (int e = 0; e < 3; ++e) {
+    // One Euler axis per item (layout.hip: 3 lanes per instant, a1 = 1 + axis): on the device each
+    // lane instantiates its axis with a compile-time index; all three axes in one lane needed 242
+    // VGPRs (2 waves per SIMD), one axis 166. The host (structure pass, emulation) and an unsplit
+    // item (a1 = 0) take the axes in order.
+    auto axis = [&](const int e) {
       double dR[3][3]; euler_dR_axis(q, e, dR);
       // dw = dM_e thd; dwd = dMdot_e thd + dM_e thdd (GetDerivMwrtNodes :168-198, GetDerivMdotwrtNodes :270-304)
       double dw[3] = {0.0, 0.0, 0.0}, dwd[3] = {0.0, 0.0, 0.0};
@@ -1335,7 +1349,18 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
       for (int r = 0; r < 3; ++r)
         for (int bb = 0; bb < 4; ++bb)
           em(r0 + AX + r, basis_col(c, SP_BASE_ANG, A.poly, bb, e), Ap[r] * Hp[bb] + Av[r] * Hv[bb] + Aa[r] * Ha[bb], true);
+    };
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (split_base_ang(c.gait)) {   // compile-time in the kernels (GAIT): the layout split every item
+      axis(it.a1 - 1);              // one axis per lane (runtime index: the axis code indexes no array by it)
+    } else {
+#pragma unroll
+      for (int e = 0; e < 3; ++e) axis(e);
     }
+#else
+    for (int e = 0; e < 3; ++e)
+      if (it.a1 == 0 || it.a1 == 1 + e) axis(e);
+#endif
     return;
   }
   // group 2 + ee: force (GetJacobianWrtForce :168-180), torque (:182-191), motion (:193-204)
