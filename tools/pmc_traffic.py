@@ -22,14 +22,18 @@ def per_kernel(d, counter):
             continue
         if "towr_misc_kernel" in k:
             acc["gait_small_kinds" if "towr_misc_kernel<true>" in k else "small_kinds"].append(float(r["Counter_Value"]) * 1024.0)
-        elif "towr_step_kernel<" in k:   # fusion group: the default 192-lane group is RangeOfMotion + FDISC
-            acc["range_of_motion+force_discretized" if ", 192>(" in k else "fused_256"].append(
+        elif "towr_step_kernel<" in k:   # <gait, rotvec, block>: the default 192-lane group is RangeOfMotion + FDISC
+            targs = [a.strip() for a in k.split("towr_step_kernel<")[1].split(">")[0].split(",")]
+            pre = ("gait_" if targs[0] == "true" else "") + ("rotvec_" if targs[1] == "true" else "")
+            acc[pre + ("range_of_motion+force_discretized" if targs[2] == "192" else "fused_256")].append(
                 float(r["Counter_Value"]) * 1024.0)
-        elif "towr_tile_kernel<" in k:   # <type, block, gait, rotvec>: gait launches reported apart
-            targs = k.split("towr_tile_kernel<")[1].split(">")[0].split(",")
+        elif "towr_tile_kernel<" in k:   # <type, block, gait, rotvec>: gait and RotVec launches reported apart
+            targs = [a.strip() for a in k.split("towr_tile_kernel<")[1].split(">")[0].split(",")]
             t = int(targs[0])
-            name = ("gait_" if targs[2].strip() == "true" else "") + NAMES[t]
+            name = ("gait_" if targs[2] == "true" else "") + ("rotvec_" if targs[3] == "true" else "") + NAMES[t]
             acc[name].append(float(r["Counter_Value"]) * 1024.0)
+        elif "towr_fdisc_inst_kernel" in k or "towr_fdisc_stream_kernel" in k:   # gait streaming FDISC
+            acc["gait_fdisc_" + ("inst" if "inst" in k else "stream")].append(float(r["Counter_Value"]) * 1024.0)
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
 

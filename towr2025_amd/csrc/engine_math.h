@@ -454,6 +454,12 @@ TG_HD void split_part_rows(int rows, int parts, int part, int& first, int& count
 template <class E, class = void> struct emit_filter { static constexpr bool value = false; };
 template <class E> struct emit_filter<E, decltype((void)E::kFilter)> { static constexpr bool value = E::kFilter; };
 
+// Emitters that evaluate only part of Dynamic's groups declare `static constexpr int kDynGroups`:
+// 1 = every group but the base-angular block (group 1), 2 = group 1 only (eval_dyn returns early for
+// the others, so the kernel instantiating it carries only those groups' registers).
+template <class E, class = void> struct emit_dyn_groups { static constexpr int value = 0; };
+template <class E> struct emit_dyn_groups<E, decltype((void)E::kDynGroups)> { static constexpr int value = E::kDynGroups; };
+
 template <class E> TG_HD bool em_wants(const E& em, int row) {
   if constexpr (emit_filter<E>::value) return em.want(row);
   else return true;
@@ -1174,6 +1180,8 @@ TG_HD void dyn_g0_b(const Ctx& c, const ItemDesc& it, Emit& em, const DynG0& st,
 
 template <class Emit>
 TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
+  if constexpr (emit_dyn_groups<Emit>::value == 1) { if (it.group == 1) return; }
+  if constexpr (emit_dyn_groups<Emit>::value == 2) { if (it.group != 1) return; }
   const double t = it.t;
   const int r0 = it.row0, E = c.rb.n_ee;
   if (it.group == 0) {   // both phases inline (host structure pass; see dyn_g0_a)

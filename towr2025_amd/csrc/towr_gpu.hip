@@ -46,8 +46,9 @@ namespace {
 // absent candidates (positions >= nvals, the dummy slots) are not stored. The lane's item may be
 // row-split (ItemDesc::rsel): only its rows' candidates are emitted (and counted), exactly as the
 // structure pass recorded them, and only those rows' g.
-template <int BLOCK, int DEPTH, bool DIRECT = false, int PRE = 1>
+template <int BLOCK, int DEPTH, bool DIRECT = false, int PRE = 1, int DYNG = 0>
 struct TileEmit {
+  static constexpr int kDynGroups = DYNG;   // Dynamic groups this emitter's kernel evaluates (engine_math.h)
   static_assert(PRE >= 0 && PRE <= 6 && PRE <= kSlotSpare + 2, "preloaded slot groups: 0 .. 6, within the spare groups");
   const SlotGroup* slot;   // this lane's group 0; group g at slot[g * BLOCK]
   double* out;             // LDS tile, tile-relative (DIRECT: V at the tile's first value)
@@ -260,7 +261,9 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
     it = ItemDesc{}; it.type = IT_NONE; it.slot = 0;
   }
   // GAIT: direct HBM emission into the zero-filled V (see TileEmit)
-  TileEmit<TBLOCK, slot_depth(TYPE), GAIT, gait_slot_pre(TYPE)> em(P.slots + it.slot, GAIT ? Vb + T.v0 : smem, GAIT ? Gb : smem + lds_rows_off - T.r0);
+  // gait Dynamic: the base-angular block runs in its own launch (towr_dyn_g1_kernel), after this one
+  TileEmit<TBLOCK, slot_depth(TYPE), GAIT, gait_slot_pre(TYPE), (GAIT && TYPE == IT_DYN) ? 1 : 0> em(
+      P.slots + it.slot, GAIT ? Vb + T.v0 : smem, GAIT ? Gb : smem + lds_rows_off - T.r0);
   if constexpr (GAIT) {
     if (it.rsel > 0) { em.flo = it.row0 + rsel_first(it.rsel); em.fcnt = rsel_count(it.rsel); }
     em.nvals = P.want_jac ? T.v1 - T.v0 : 0;
@@ -382,7 +385,10 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
 }
 
 template <int TYPE, int BLOCK, bool GAIT, bool ROTVEC>
-__global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN && BLOCK <= 256 ? 2 : 1)) towr_tile_kernel(KParams P) {
+// second argument: minimum waves per SIMD. Dynamic: 2 blocks per CU (fixed gait: 256 lanes, 2 waves per
+// SIMD, <= 256 VGPRs; gait: 512 lanes with the base-angular block in towr_dyn_g1_kernel, 4 waves per SIMD,
+// <= 128 VGPRs)
+__global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? (GAIT ? 4 : 2) : 1)) towr_tile_kernel(KParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int total = P.B * P.ntiles;
   const int per = (total + 7) / 8;
@@ -390,6 +396,43 @@ __global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN && BLOCK <= 256 ? 2 : 1
   const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
   if (w >= total) return;
   tile_body<TYPE, BLOCK, BLOCK, GAIT, ROTVEC>(P, smem, w / P.ntiles, P.tile0 + w % P.ntiles, P.lds_x_off, P.lds_rows_off);
+}
+
+// Gait Dynamic's base-angular block (group 1: the Euler / RotVec chain rule through the base
+// orientation) in its own launch after the Dynamic tile kernel, one 64-lane block per (problem, tile):
+// its lanes are the tile's group-1 lanes (64 .. 127 of the tile block). In the tile kernel this path set
+// the register allocation of every wave (256 VGPRs, 1 block per CU); without it the tile kernel needs
+// ~135. The values land in the rows the tile kernel zero-filled (stream order), at their slot positions.
+template <bool ROTVEC>
+__global__ void __launch_bounds__(64, 1) towr_dyn_g1_kernel(KParams P) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int total = P.B * P.ntiles;
+  const int per = (total + 7) / 8;
+  const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+  if (w >= total) return;
+  const int b = w / P.ntiles;
+  const TileDesc T = P.tiles[P.tile0 + w % P.ntiles];
+  const ItemDesc it = P.items[T.i0 + 64 + threadIdx.x];
+  TileEmit<tile_block(IT_DYN, true), 2, true, 6, 2> em(P.slots + it.slot, P.V + (int64_t)b * P.ldv + T.v0, P.G + (int64_t)b * P.ldg);
+  em.nvals = P.want_jac ? T.v1 - T.v0 : 0;
+  em.gon = false;   // group 1 writes no g rows
+  double* xs = smem;
+  int32_t* ns = reinterpret_cast<int32_t*>(smem + P.n_pad);
+  stage_x<64, false>(P, P.X + (int64_t)b * P.ldx, xs, ns);
+  __syncthreads();
+  if (it.type != IT_DYN || it.group != 1) return;
+  Ctx c;
+  c.seg = nullptr; c.sg = P.sg; c.row = it.seg;
+  c.x = xs; c.nodecol = ns; c.spl = P.spl; c.dur = P.dur;
+  c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
+  c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
+  c.gait = true; c.pinfo = P.pinfo; c.pcols = P.pcols; c.pact = P.pact; c.sched = P.sched; c.eelin = P.eelin; c.lin = P.lin;
+  c.rotvec = ROTVEC;
+  c.dyn_scratch = nullptr;
+  eval_dyn(c, it, em);
+}
+const void* dyn_g1_kernel_for(bool rotvec) {
+  return rotvec ? reinterpret_cast<const void*>(&towr_dyn_g1_kernel<true>) : reinterpret_cast<const void*>(&towr_dyn_g1_kernel<false>);
 }
 
 // The small kinds (node-value constraints, SplineAcc, BaseMotion, TotalDuration: a few kB of output
@@ -1027,6 +1070,9 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
     void* args[] = {&P};
     HIPCHK(h, hipLaunchKernel(kernel_for_class(lc, L.gait, L.rotvec, L.fstream), dim3((unsigned)grid), dim3((unsigned)block), args,
                               lds_bytes(L, lc), st));
+    if (lc == LC_DYN && L.gait)   // its base-angular block, into the rows the tile kernel zero-filled
+      HIPCHK(h, hipLaunchKernel(dyn_g1_kernel_for(L.rotvec), dim3((unsigned)grid), dim3(64), args,
+                                sizeof(double) * (size_t)((L.n + 2) & ~1), st));
   }
   for (int i = 0; i < nside; ++i) {
     HIPCHK(h, hipEventRecord(h->join[i], h->side[i]));
