@@ -33,7 +33,7 @@ struct TileDesc {
 // PhaseSpline pattern and the schedule columns. Template entry j (fs_tmpl) = column j of a row:
 //   >= 0: force column, PhaseCol index (bits 0-23) and dimension (bits 24-25); < 0: schedule column.
 // The force entries polynomial p can make non-zero (its two nodes' variables) lie in the window
-// [fs_ws[wsoff + p], + kFsWin) of row positions (checked); schedule columns at [js0, js0 + ns1).
+// [fs_ws[2 (wsoff + p)], + kFsWin) of row positions (checked); schedule columns at [js0, js0 + ns1).
 constexpr int kFsInst = 16;   // measured on MI355X (ANYmal gait, B = 1024): 64 -> 0.501 ms, 32 -> 0.463, 16 -> 0.452, 8 -> 0.478
 constexpr int kFsBlock = 256;
 constexpr int kFsWin = 12;
