@@ -21,6 +21,9 @@
 #include "../../include/towr_gpu.h"
 
 #define TG_HD __host__ __device__ __forceinline__
+#ifndef TOWR_DYN_LINROW   // gait Dynamic: linear-row lanes evaluate the force spline only (0 = every spline, A/B)
+#define TOWR_DYN_LINROW 1
+#endif
 
 namespace tg {
 
@@ -1373,53 +1376,70 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
   }
   // group 2 + ee: force (GetJacobianWrtForce :168-180), torque (:182-191), motion (:193-204)
   const int ee = it.group - 2;
+  // A row-split lane (gait, ItemDesc::rsel) whose rows are all linear (LX..LZ) needs only the force
+  // spline and its schedule Jacobian: the base, torque and motion terms enter the angular rows only.
+  // Emission order is unchanged (a filtered row's candidates are neither emitted nor counted).
+  bool ang = true;
+#if TOWR_DYN_LINROW
+  if constexpr (emit_filter<Emit>::value) ang = em_wants(em, r0 + AX) || em_wants(em, r0 + AY) || em_wants(em, r0 + AZ);
+#endif
   SplinePt L, F, Tq, P;
-  spline_eval(c, SP_BASE_LIN, t, L);
   spline_eval(c, sp_force(ee), t, F);
-  spline_eval(c, sp_torque(ee), t, Tq);
-  spline_eval(c, sp_motion(ee), t, P);
-  if (c.dyn_scratch) {   // this endeffector's terms of the group-0 sums (it.a2 = instant within the tile)
-    double v[6]; dyn_ee_terms(L.p, F, Tq, P, v);
-    double* d = c.dyn_scratch + (it.a2 * E + ee) * 6;
-    for (int q = 0; q < 6; ++q) d[q] = v[q];
+  double rv[3] = {0.0, 0.0, 0.0};
+  if (ang) {
+    spline_eval(c, SP_BASE_LIN, t, L);
+    spline_eval(c, sp_torque(ee), t, Tq);
+    spline_eval(c, sp_motion(ee), t, P);
+    if (c.dyn_scratch) {   // this endeffector's terms of the group-0 sums (it.a2 = instant within the tile)
+      double v[6]; dyn_ee_terms(L.p, F, Tq, P, v);
+      double* d = c.dyn_scratch + (it.a2 * E + ee) * 6;
+      for (int q = 0; q < 6; ++q) d[q] = v[q];
+    }
+    for (int k = 0; k < 3; ++k) rv[k] = L.p[k] - P.p[k];
   }
-  const double rv[3] = {L.p[0] - P.p[0], L.p[1] - P.p[1], L.p[2] - P.p[2]};
   double H[4];
   spline_basis(F, kPos, H);
-  #pragma unroll
-  for (int r = 0; r < 3; ++r)
+  if (ang) {
     #pragma unroll
-    for (int d = 1; d <= 2; ++d) {
-      const int e = (r + d) % 3;
-      emit_dim(c, em, r0 + AX + r, sp_force(ee), F, H, e, cross_el(rv, r, e));
-    }
+    for (int r = 0; r < 3; ++r)
+      #pragma unroll
+      for (int d = 1; d <= 2; ++d) {
+        const int e = (r + d) % 3;
+        emit_dim(c, em, r0 + AX + r, sp_force(ee), F, H, e, cross_el(rv, r, e));
+      }
+  }
   #pragma unroll
   for (int e = 0; e < 3; ++e) emit_dim(c, em, r0 + LX + e, sp_force(ee), F, H, e, -1.0);
-  spline_basis(Tq, kPos, H);
-  #pragma unroll
-  for (int e = 0; e < 3; ++e) emit_dim(c, em, r0 + AX + e, sp_torque(ee), Tq, H, e, -1.0);
-  spline_basis(P, kPos, H);
-  #pragma unroll
-  for (int r = 0; r < 3; ++r)
+  if (ang) {
+    spline_basis(Tq, kPos, H);
     #pragma unroll
-    for (int d = 1; d <= 2; ++d) {
-      const int e = (r + d) % 3;
-      emit_dim(c, em, r0 + AX + r, sp_motion(ee), P, H, e, cross_el(F.p, r, e));
-    }
+    for (int e = 0; e < 3; ++e) emit_dim(c, em, r0 + AX + e, sp_torque(ee), Tq, H, e, -1.0);
+    spline_basis(P, kPos, H);
+    #pragma unroll
+    for (int r = 0; r < 3; ++r)
+      #pragma unroll
+      for (int d = 1; d <= 2; ++d) {
+        const int e = (r + d) % 3;
+        emit_dim(c, em, r0 + AX + r, sp_motion(ee), P, H, e, cross_el(F.p, r, e));
+      }
+  }
   if (c.gait) {
     // d/d ee schedule (dynamic_constraint.cc:116-122): force and ee-position terms; the reference
     // omits the torque term here and so does this engine
-    SchedJac Jf, Jx;
+    SchedJac Jf;
     sched_jac(c, sp_force(ee), t, F, Jf);
-    sched_jac(c, sp_motion(ee), t, P, Jx);
-    #pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      if (!em_wants(em, r0 + AX + r)) continue;
-      const int e1 = (r + 1) % 3, e2 = (r + 2) % 3;
-      for (int col = 0; col < Jf.n - 1; ++col) {
-        const double a = cross_el(rv, r, e1) * sched_val(Jf, e1, col) + cross_el(rv, r, e2) * sched_val(Jf, e2, col);
-        const double b = cross_el(F.p, r, e1) * sched_val(Jx, e1, col) + cross_el(F.p, r, e2) * sched_val(Jx, e2, col);
-        em(r0 + AX + r, Jf.col0 + col, a + b, true);
+    if (ang) {
+      SchedJac Jx;
+      sched_jac(c, sp_motion(ee), t, P, Jx);
+      #pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        if (!em_wants(em, r0 + AX + r)) continue;
+        const int e1 = (r + 1) % 3, e2 = (r + 2) % 3;
+        for (int col = 0; col < Jf.n - 1; ++col) {
+          const double a = cross_el(rv, r, e1) * sched_val(Jf, e1, col) + cross_el(rv, r, e2) * sched_val(Jf, e2, col);
+          const double b = cross_el(F.p, r, e1) * sched_val(Jx, e1, col) + cross_el(F.p, r, e2) * sched_val(Jx, e2, col);
+          em(r0 + AX + r, Jf.col0 + col, a + b, true);
+        }
       }
     }
     #pragma unroll

@@ -29,6 +29,12 @@
 
 using namespace tg;
 
+#ifndef TOWR_MISC_MINW   // small kinds: minimum waves per SIMD (A/B build option)
+#define TOWR_MISC_MINW 1
+#endif
+#ifndef TOWR_ROM_GAIT_MINW   // gait RangeOfMotion (640 lanes): 5 = two blocks per CU (A/B build option)
+#define TOWR_ROM_GAIT_MINW 1
+#endif
 namespace {
 
 
@@ -388,7 +394,7 @@ template <int TYPE, int BLOCK, bool GAIT, bool ROTVEC>
 // second argument: minimum waves per SIMD. Dynamic: 2 blocks per CU (fixed gait: 256 lanes, 2 waves per
 // SIMD, <= 256 VGPRs; gait: 512 lanes with the base-angular block in towr_dyn_g1_kernel, 4 waves per SIMD,
 // <= 128 VGPRs)
-__global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? (GAIT ? 4 : 2) : 1)) towr_tile_kernel(KParams P) {
+__global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? (GAIT ? 4 : 2) : (TYPE == IT_ROM && GAIT) ? TOWR_ROM_GAIT_MINW : 1)) towr_tile_kernel(KParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int total = P.B * P.ntiles;
   const int per = (total + 7) / 8;
@@ -514,7 +520,7 @@ __device__ __forceinline__ void misc_body(const KParams& P, double* smem, int b,
 // per problem each) in one launch: a block = kMiscWaves one-wave tiles of one problem, sharing the
 // staged x and node table; each wave evaluates and writes out its own tile.
 template <bool GAIT>
-__global__ void __launch_bounds__(64 * kMiscWaves, 1) towr_misc_kernel(KParams P) {
+__global__ void __launch_bounds__(64 * kMiscWaves, TOWR_MISC_MINW) towr_misc_kernel(KParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int total = P.B * P.ntiles;   // ntiles = groups per problem
   const int per = (total + 7) / 8;
