@@ -148,8 +148,15 @@ int split_rows(int type, int group, bool gait);
 // A 5-wave block is placed as if it took 2 waves on every SIMD (hipOccupancy... and the measured
 // residency: 1 block per CU at 168 VGPRs), and a 4-wave block with FDISC rows (0, 1) on one wave
 // waits for that wave (1.5x the others): 10-wave blocks are balanced and fill 10 of the 12 wave slots.
+//   DYN, build option TOWR_DYN_GAIT_LIN1: rows 0, 1, 2 on a wave each and the linear rows 3 .. 5 of an
+//   endeffector on one lane (they need only the force spline), g0 | g1 | row 0 | 1 | 2 | 3-5, 6 waves
+//   at <= 168 VGPRs. Measured slower (gait Dynamic 0.296 vs 0.185 ms per 1024 problems): off.
+#ifndef TOWR_DYN_GAIT_LIN1
+#define TOWR_DYN_GAIT_LIN1 0
+#endif
+constexpr int kDynGaitRowParts = TOWR_DYN_GAIT_LIN1 ? 4 : 6;
 constexpr int tile_block(int type, bool gait) {
-  return type == IT_DYN ? (gait ? 512 : 256) : type == IT_ROM ? (gait ? 640 : 192) : type == IT_FDISC ? (gait ? 640 : 192)
+  return type == IT_DYN ? (gait ? 64 * (2 + kDynGaitRowParts) : 256) : type == IT_ROM ? (gait ? 640 : 192) : type == IT_FDISC ? (gait ? 640 : 192)
        : type == IT_TQDISC ? (gait ? 256 : 192) : 64;
 }
 

@@ -678,7 +678,12 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
       const int S = split_rows(type, group, L.gait);   // one lane per row of a PhaseSpline item
       for (int r = 0; r < S; ++r) {
         int first = 0, count = 0;
-        split_part_rows(item_rows(type), S, r, first, count);
+        if (type == IT_DYN) {   // one row per part, the last part takes the trailing (linear) rows
+          first = r < S - 1 ? r : S - 1;
+          count = r < S - 1 ? 1 : item_rows(type) - S + 1;
+        } else {
+          split_part_rows(item_rows(type), S, r, first, count);
+        }
         it.rsel = S > 1 ? 1 + first + 16 * count + 256 * r : 0;
         L.items.push_back(it); item_inst.push_back(inst);
       }
@@ -1167,7 +1172,7 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
 int split_rows(int type, int group, bool gait) {
   if (!gait) return 1;
   switch (type) {
-    case IT_DYN: return group >= 2 ? 6 : 1;   // the endeffector groups (force / torque / motion PhaseSplines)
+    case IT_DYN: return group >= 2 ? kDynGaitRowParts : 1;   // the endeffector groups (force / torque / motion PhaseSplines)
     case IT_ROM: return group == 2 ? 3 : 1;   // the endeffector-motion group
     case IT_FDISC: return 5;
     case IT_TQDISC: return 4;

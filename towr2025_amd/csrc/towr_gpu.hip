@@ -29,8 +29,8 @@
 
 using namespace tg;
 
-#ifndef TOWR_MISC_MINW   // small kinds: minimum waves per SIMD (A/B build option)
-#define TOWR_MISC_MINW 1
+#ifndef TOWR_MISC_MINW   // small kinds: minimum waves per SIMD (5: 0.0267 -> 0.0257 ms per 4096 problems, A/B on one box)
+#define TOWR_MISC_MINW 5
 #endif
 #ifndef TOWR_ROM_GAIT_MINW   // gait RangeOfMotion (640 lanes): 5 = two blocks per CU (A/B build option)
 #define TOWR_ROM_GAIT_MINW 1
@@ -392,9 +392,9 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
 
 template <int TYPE, int BLOCK, bool GAIT, bool ROTVEC>
 // second argument: minimum waves per SIMD. Dynamic: 2 blocks per CU (fixed gait: 256 lanes, 2 waves per
-// SIMD, <= 256 VGPRs; gait: 512 lanes with the base-angular block in towr_dyn_g1_kernel, 4 waves per SIMD,
-// <= 128 VGPRs)
-__global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? (GAIT ? 4 : 2) : (TYPE == IT_ROM && GAIT) ? TOWR_ROM_GAIT_MINW : 1)) towr_tile_kernel(KParams P) {
+// SIMD, <= 256 VGPRs; gait, base-angular block in towr_dyn_g1_kernel: 384 lanes, 3 waves per SIMD,
+// <= 168 VGPRs, or with one wave per row 512 lanes, 4 waves per SIMD, <= 128 VGPRs)
+__global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? (GAIT ? (BLOCK <= 384 ? 3 : 4) : 2) : (TYPE == IT_ROM && GAIT) ? TOWR_ROM_GAIT_MINW : 1)) towr_tile_kernel(KParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int total = P.B * P.ntiles;
   const int per = (total + 7) / 8;
@@ -1553,9 +1553,11 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
   }
   {
     const char* ns = std::getenv("TOWR_GPU_STREAMS");
-    // default: serial launches. Measured on MI355X (ANYmal, B = 4096): 1, 2, 4 streams gave 0.524,
-    // 0.521, 0.550 ms per step — every kind already fills the CUs' LDS, so kinds cannot co-reside.
-    const int want = ns ? std::atoi(ns) - 1 : 0;
+    // Default with fixed phase durations: serial launches. Measured on MI355X (ANYmal, B = 4096): 1, 2, 4
+    // streams gave 0.524, 0.521, 0.550 ms per step — every kind already fills the CUs' LDS, so kinds
+    // cannot co-reside. Under phase-duration optimisation (streaming FDISC) two streams: the write-bound
+    // FDISC stream kernel runs beside the latency-bound Dynamic tiles.
+    const int want = ns ? std::atoi(ns) - 1 : (h->L.gait && h->L.fstream ? 1 : 0);
     h->n_side = std::max(0, std::min(towr_gpu_handle_s::kMaxSide, want));
     if (h->n_side > 0 && hipEventCreateWithFlags(&h->fork, hipEventDisableTiming) != hipSuccess) { h->err = "hipEventCreate failed"; return bail(TOWR_ERR_HIP); }
     for (int i = 0; i < h->n_side; ++i)
