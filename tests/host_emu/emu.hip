@@ -119,7 +119,7 @@ extern "C" int emu_cost(const towr_problem_desc_t* d, const double* x, double* f
 extern "C" int emu_stats(const towr_problem_desc_t* d) {
   Layout L; std::string e;
   if (build_layout(*d, L, e)) return -1;
-  std::printf("fstream %d blocks %zu tmpl_max %d\n", (int)L.fstream, L.fs_blocks.size(), L.fs_tmpl_max);
+  std::printf("fstream %d blocks %zu tmpl_max %d rom_wave_zero %d\n", (int)L.fstream, L.fs_blocks.size(), L.fs_tmpl_max, (int)L.rom_wave_zero);
   std::printf("n %d m %d nnz %lld nodecol %zu | gait tables: spl %zu pinfo %zu pcols %zu pact %zu sched %zu\n", L.n, L.m,
               (long long)L.nnz, L.nodecol.size(), L.spl.size(), L.pinfo.size(), L.pcols.size(), L.pact.size(), L.sched.size());
   for (int t = 0; t < IT_COUNT; ++t) {

@@ -45,6 +45,7 @@ struct KParams {
   int32_t lds_scr_off;           // DYN: per-instant endeffector sum terms (instants x n_ee x 6)
   int32_t n, n_pad, n_nodecol;
   int32_t want_g, want_jac, fdisc_motion;
+  int32_t rom_wz;   // gait RangeOfMotion: per-wave zero ranges (Layout::rom_wave_zero) instead of the block zero-fill
   const int32_t* misc_tiles;      // merged small-kind launch: kMiscWaves tile ids per group
   const int32_t* misc_lds;        // per (group, wave): LDS offset, g-row offset
   RobotC rb;

@@ -94,6 +94,11 @@ struct Layout {
   // streaming ForceConstraintDiscretized (FsBlock): enabled under phase-duration optimisation on
   // terrains without curvature when every row of each constraint holds the same columns
   bool fstream = false;
+  // gait RangeOfMotion: each row lane's wave zero-fills the row's columns after the base blocks (ItemDirect
+  // z0 / z1) just before its own value stores, and the base-block lanes store every position of the rows'
+  // base prefixes, instead of a block zero-fill of the whole tile (whose lines left L2 before the values came:
+  // 2.66x the algorithmic write bytes). Set when every tile is covered exactly that way (checked).
+  bool rom_wave_zero = false;
   std::vector<FsBlock> fs_blocks;
   std::vector<double> fs_t;
   std::vector<int32_t> fs_tmpl;

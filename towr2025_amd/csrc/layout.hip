@@ -1074,8 +1074,10 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
     // tile-relative uint16 positions; four spare groups per lane absorb the kernel's prefetch
     std::vector<SlotGroup> groups;
     L.idirect.assign(L.gait ? items.size() : 0, ItemDirect{});
+    L.rom_wave_zero = L.gait;
     for (const TileDesc& td : L.tiles) {
       const int block = td.i1 - td.i0;
+      std::vector<int32_t> bslot((size_t)block, -1);   // build-time slot offsets (L.slots) of the lanes
       int maxc = 0;
       for (int l = 0; l < block; ++l) maxc = std::max(maxc, items[td.i0 + l].type == IT_NONE ? 0 : items[td.i0 + l].ncand);
       const int ng = (maxc + 7) / 8 + kSlotSpare;   // + spare groups for the kernels' slot prefetch
@@ -1125,7 +1127,37 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
             dd.z1 = (int32_t)(L.row_ptr[r_hi] - td.v0);
           }
         }
+        bslot[l] = it.slot;
         it.slot = (int32_t)(base + l);
+      }
+      if (L.gait && td.type == IT_ROM && L.rom_wave_zero) {
+        // row lanes (group 2, one row each): zero range = the row after its base-block prefix; the base
+        // lanes (groups 0, 1) must store every position of those prefixes, and the two must tile [v0, v1)
+        const int nv = td.v1 - td.v0;
+        std::vector<uint8_t> cov((size_t)nv, 0);
+        bool ok = true;
+        for (int l = 0; l < block && ok; ++l) {
+          const ItemDesc& it = items[td.i0 + l];
+          if (it.type == IT_NONE || it.group == 2) continue;
+          for (int j = 0; j < it.ncand; ++j) {
+            const int32_t g = L.slots[bslot[l] + j];
+            if (g >= 0) cov[g - td.v0] = 1;
+          }
+        }
+        for (int l = 0; l < block && ok; ++l) {
+          const ItemDesc& it = items[td.i0 + l];
+          if (it.type == IT_NONE || it.group != 2) continue;
+          if (it.rsel <= 0 || rsel_count(it.rsel) != 1) { ok = false; break; }
+          const int r = it.row0 + rsel_first(it.rsel);
+          int32_t a = (int32_t)(L.row_ptr[r] - td.v0);
+          const int32_t e = (int32_t)(L.row_ptr[r + 1] - td.v0);
+          while (a < e && cov[a] == 1) ++a;   // the base prefix
+          ItemDirect& dd = L.idirect[td.i0 + l];
+          dd.z0 = a; dd.z1 = e;
+          for (int32_t q = a; q < e; ++q) { if (cov[q]) { ok = false; break; } cov[q] = 2; }
+        }
+        for (int q = 0; q < nv && ok; ++q) ok = cov[q] != 0;
+        if (!ok) L.rom_wave_zero = false;   // the block zero-fill then (the z ranges are not read)
       }
       if (L.gait && (td.type == IT_FDISC || td.type == IT_TQDISC)) {   // the lanes' owned ranges tile [v0, v1)
         std::vector<std::pair<int32_t, int32_t>> zr;

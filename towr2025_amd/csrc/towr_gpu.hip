@@ -29,6 +29,9 @@
 
 using namespace tg;
 
+#ifndef TOWR_DYN_GAIT_LIN1_W   // minimum waves per SIMD of the 6-wave gait Dynamic block (layout.h TOWR_DYN_GAIT_LIN1)
+#define TOWR_DYN_GAIT_LIN1_W 4
+#endif
 #ifndef TOWR_MISC_MINW   // small kinds: minimum waves per SIMD (5: 0.0267 -> 0.0257 ms per 4096 problems, A/B on one box)
 #define TOWR_MISC_MINW 5
 #endif
@@ -284,9 +287,12 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
   // FDISC / TQDISC lanes own whole rows (row-split), so there each wave zero-fills its own rows
   // after the staging instead (below), and waits for them only at its first value store.
   constexpr bool kWaveZero = GAIT && (TYPE == IT_FDISC || TYPE == IT_TQDISC);
+  // gait RangeOfMotion (Layout::rom_wave_zero): row lanes zero their rows after the base prefix, per wave,
+  // just before their own value stores; the base lanes store every base-prefix position
+  const bool rom_wz = GAIT && TYPE == IT_ROM && P.rom_wz != 0;
 #ifndef TOWR_EXP_GAIT_NOZERO   // timing experiment only: no zero-fill
   if constexpr (GAIT && !kWaveZero)
-    if (P.want_jac) zero_out(Vb + T.v0, T.v1 - T.v0, threadIdx.x, KBLOCK);
+    if (P.want_jac && !rom_wz) zero_out(Vb + T.v0, T.v1 - T.v0, threadIdx.x, KBLOCK);
 #endif
   if constexpr (early_stage(TYPE)) xst.commit(P, xg, xs, ns);
   else stage_x<KBLOCK, stages_nodes(TYPE, GAIT)>(P, xg, xs, ns);
@@ -329,7 +335,7 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
     __syncthreads();
     c.pdur = tm; c.pend = tm + P.n_pinfo; c.phend = tm + 2 * P.n_pinfo; c.ph_stride = P.ph_stride;
     c.ter = ters;   // LDS copy: no global load in the evaluation waits behind the zero-fill stores
-    if constexpr (kWaveZero) {
+    if (kWaveZero || rom_wz) {
 #ifdef TOWR_EXP_GAIT_NOZERO
       if (false) {
 #else
@@ -394,7 +400,7 @@ template <int TYPE, int BLOCK, bool GAIT, bool ROTVEC>
 // second argument: minimum waves per SIMD. Dynamic: 2 blocks per CU (fixed gait: 256 lanes, 2 waves per
 // SIMD, <= 256 VGPRs; gait, base-angular block in towr_dyn_g1_kernel: 384 lanes, 3 waves per SIMD,
 // <= 168 VGPRs, or with one wave per row 512 lanes, 4 waves per SIMD, <= 128 VGPRs)
-__global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? (GAIT ? (BLOCK <= 384 ? 3 : 4) : 2) : (TYPE == IT_ROM && GAIT) ? TOWR_ROM_GAIT_MINW : 1)) towr_tile_kernel(KParams P) {
+__global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? (GAIT ? (BLOCK <= 384 ? TOWR_DYN_GAIT_LIN1_W : 4) : 2) : (TYPE == IT_ROM && GAIT) ? TOWR_ROM_GAIT_MINW : 1)) towr_tile_kernel(KParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int total = P.B * P.ntiles;
   const int per = (total + 7) / 8;
@@ -1068,6 +1074,8 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
     P.n = L.n; P.n_pad = (L.n + 2) & ~1; P.n_nodecol = (int32_t)L.nodecol.size();
     P.lds_x_off = (int32_t)lds_region(L, lc);
     P.want_g = want_g; P.want_jac = want_jac; P.fdisc_motion = L.fdisc_motion;
+    static const bool rom_block_zero = std::getenv("TOWR_GPU_ROM_BLOCKZERO") != nullptr;   // A/B switch: the block zero-fill
+    P.rom_wz = L.rom_wave_zero && !rom_block_zero ? 1 : 0;
     P.rb = L.rb;
     const int64_t total = (int64_t)B * nt;
     const int64_t grid = ((total + 7) / 8) * 8;
