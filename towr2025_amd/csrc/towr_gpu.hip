@@ -32,6 +32,9 @@ using namespace tg;
 #ifndef TOWR_DYN_GAIT_LIN1_W   // minimum waves per SIMD of the 6-wave gait Dynamic block (layout.h TOWR_DYN_GAIT_LIN1)
 #define TOWR_DYN_GAIT_LIN1_W 4
 #endif
+#ifndef TOWR_EMIT_PAIR   // gait tile kernels: consecutive value stores paired into 16-byte stores (TileEmit::put);
+#define TOWR_EMIT_PAIR 0   // build option, not yet measured on the GPU (the box pool was unavailable): off
+#endif
 #ifndef TOWR_MISC_MINW   // small kinds: minimum waves per SIMD (5: 0.0267 -> 0.0257 ms per 4096 problems, A/B on one box)
 #define TOWR_MISC_MINW 5
 #endif
@@ -148,7 +151,7 @@ struct TileEmit {
 #ifdef TOWR_EXP_GAIT_NOSTORE   // timing experiment only: evaluate, but (almost) never store
       if (s < nvals && v == 12345.678) out[s] = v;
 #else
-      if (s < nvals) out[s] = v;
+      if (s < nvals) put(s, v);
 #endif
       return;
     }
@@ -165,7 +168,30 @@ struct TileEmit {
     out[s] = v;   // absent candidates land in the lane's dummy slot
 #endif
   }
-  __device__ __forceinline__ void flush() {}
+  // DIRECT value stores: an isolated 8-byte store costs a 32-byte write granule (tools/wcal.hip), so a value
+  // is held until the next one and two consecutive positions at a 16-byte boundary leave as one 16-byte store
+  int ps = -1;
+  double pv = 0.0;
+  __device__ __forceinline__ void put(int s, double v) {
+#if TOWR_EMIT_PAIR
+    if (ps >= 0) {
+      if (s == ps + 1 && (reinterpret_cast<uintptr_t>(out + ps) & 15) == 0) {
+        *reinterpret_cast<dbl2_t*>(out + ps) = dbl2_t{pv, v};
+        ps = -1;
+        return;
+      }
+      out[ps] = pv;
+    }
+    ps = s; pv = v;
+#else
+    out[s] = v;
+#endif
+  }
+  __device__ __forceinline__ void flush() {
+    if constexpr (DIRECT) {
+      if (ps >= 0) { out[ps] = pv; ps = -1; }
+    }
+  }
 };
 // Emitter for a fixed stretch of a lane's candidates J0 .. J0 + 8 NG - 1 whose slot groups are all
 // loaded at construction: Dynamic group 0 builds it before the block barrier that separates its two
@@ -363,6 +389,7 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
     } else {
       eval_typed<TYPE>(c, it, em);
     }
+    em.flush();
   }
   if constexpr (TYPE == IT_DYN) {   // phase B of group 0: the endeffector sums from LDS
     const bool g0lane = it.type == TYPE && it.group == 0;
@@ -442,6 +469,7 @@ __global__ void __launch_bounds__(64, 1) towr_dyn_g1_kernel(KParams P) {
   c.rotvec = ROTVEC;
   c.dyn_scratch = nullptr;
   eval_dyn(c, it, em);
+  em.flush();
 }
 const void* dyn_g1_kernel_for(bool rotvec) {
   return rotvec ? reinterpret_cast<const void*>(&towr_dyn_g1_kernel<true>) : reinterpret_cast<const void*>(&towr_dyn_g1_kernel<false>);
