@@ -289,7 +289,11 @@ int towr_gpu_set_batch_terrain(towr_gpu_handle h, int32_t B, const towr_terrain_
 /* Device-resident batch: X[b*ldx + j], G[b*ldg + i], V[b*ldv + k] are DEVICE pointers (HBM);
  * `stream` is the hipStream_t to launch on (NULL = HIP's default stream, as in the HIP API).
  * want_g / want_jac select outputs.
- * Asynchronous with respect to the host.                                                         */
+ * Asynchronous with respect to the host. Streams: some layouts evaluate through scratch owned by
+ * the handle (the per-instant records of the phase-duration-optimisation kernels, the SoftConstraint
+ * child's g / values). A call issued on a different stream than the handle's previous call waits
+ * (on the GPU, through an event) for that call's work before it touches the scratch, so calls on one
+ * handle never race but serialise across streams; use one handle per stream to overlap them.     */
 int towr_gpu_eval_batch_device(towr_gpu_handle h, int32_t B,
                                const double* X, int64_t ldx,
                                double* G, int64_t ldg,
@@ -326,6 +330,10 @@ int towr_gpu_eval_batch_device_kernel(towr_gpu_handle h, int32_t kernel, int32_t
                                       double* V, int64_t ldv, void* stream);
 int towr_gpu_num_kernels(void);
 int towr_gpu_step_launches(towr_gpu_handle h, int32_t* kernels, int32_t cap);
+/* The implementation launch class `kernel` (0..4) uses on this handle: 0 = tile kernel, 1 = record +
+ * stream kernels (every CSR unit composed and written once; phase-duration optimisation), -1 = the
+ * class is not used. Introspection for tests and profiling.                                      */
+int towr_gpu_kernel_path(towr_gpu_handle h, int32_t kernel);
 
 /* Sets the launch geometry (tiles per workgroup); 0 = automatic. For benchmarking.              */
 int towr_gpu_set_tiles_per_block(towr_gpu_handle h, int32_t tiles_per_block);

@@ -1109,17 +1109,6 @@ TG_HD double dot3(const double a[3], const double b[3]) { return a[0] * b[0] + a
 // work items
 // ----------------------------------------------------------------------------------------------
 
-// Dynamic's base-angular block (group 1) as one item per axis (3 lanes per instant, ItemDesc::a1 = 1 +
-// axis). RotVec always (its three columns in one lane spilled 884 B/lane); Euler per TOWR_DYN_SPLIT_G1
-// (mask: bit 0 fixed gait, bit 1 phase-duration optimisation), off by default: the split kernel needs
-// 164 VGPRs instead of 242 (3 waves per SIMD), but measured slower on MI355X (ANYmal, B = 4096:
-// 0.063 ms unsplit, 0.074 ms split in one tile, 0.078 ms split in two tiles per problem) — every
-// axis lane recomputes the instant's shared state, and the block still waits for its slowest wave
-#ifndef TOWR_DYN_SPLIT_G1
-#define TOWR_DYN_SPLIT_G1 0
-#endif
-TG_HD constexpr bool split_base_ang(bool gait) { return ((TOWR_DYN_SPLIT_G1 >> (gait ? 1 : 0)) & 1) != 0; }
-
 // DynamicConstraint instant (dynamic_constraint.cc:63-148, single_rigid_body_dynamics.cc:76-204)
 // Group 0 of a DynamicConstraint instant (g: GetDynamicViolation :76-102; d/d base-lin:
 // GetJacobianWrtBaseLin :104-122) in two phases. Phase A needs no endeffector sum; phase B takes
@@ -1127,7 +1116,7 @@ TG_HD constexpr bool split_base_ang(bool gait) { return ((TOWR_DYN_SPLIT_G1 >> (
 // deposit their terms in LDS (Ctx::dyn_scratch) and phase B runs after a block barrier, so the
 // group-0 lane no longer evaluates 3 E splines in a latency-bound loop; the host sums inline in the
 // same order.
-struct DynG0 { double ab[3], La[3], Lp[3], Hp[4]; int poly; };
+struct DynG0 { double ab[3], La[3], Lp[3], Hp[4], Ha[4]; int poly; };
 constexpr int kDynG0PhaseA = 12;   // candidates of dyn_g0_a (base-linear acceleration block)
 constexpr int kDynG0Cand = 36;     // + dyn_g0_b's 24 (the base-linear block of the angular rows)
 template <class Emit>
@@ -1153,10 +1142,9 @@ TG_HD void dyn_g0_a(const Ctx& c, const ItemDesc& it, Emit& em, DynG0& st) {
   mat3_vec(Iw, wd, a); mat3_vec(Iw, w, Iww); cross3(w, Iww, b);
   for (int e = 0; e < 3; ++e) { st.ab[e] = a[e] + b[e]; st.La[e] = L.a[e]; st.Lp[e] = L.p[e]; }
   st.poly = L.poly;
-  double Ha[4];
-  spline_basis(L, kPos, st.Hp); spline_basis(L, kAcc, Ha);
+  spline_basis(L, kPos, st.Hp); spline_basis(L, kAcc, st.Ha);
   for (int e = 0; e < 3; ++e)
-    for (int bb = 0; bb < 4; ++bb) em(r0 + LX + e, basis_col(c, SP_BASE_LIN, L.poly, bb, e), c.rb.m * Ha[bb], true);
+    for (int bb = 0; bb < 4; ++bb) em(r0 + LX + e, basis_col(c, SP_BASE_LIN, L.poly, bb, e), c.rb.m * st.Ha[bb], true);
 }
 // one endeffector's terms of the sums at an instant: ts = f x (c - p) + tau, fs = f
 TG_HD void dyn_ee_terms(const double Lp[3], const SplinePt& F, const SplinePt& Tq, const SplinePt& P, double out[6]) {
@@ -1181,6 +1169,170 @@ TG_HD void dyn_g0_b(const Ctx& c, const ItemDesc& it, Emit& em, const DynG0& st,
     }
 }
 
+// Dynamic's base-angular block (group 1: GetJacobianWrtBaseAng :124-166) in coefficient form: the
+// entry at basis column (b, axis e) of angular row r is Ap[r] Hp[b] + Av[r] Hv[b] + Aa[r] Ha[b], with
+// (Ap, Av, Aa) the derivatives w.r.t. (theta_e, theta_dot_e, theta_ddot_e) and H the base-angular
+// spline's position / velocity / acceleration basis. The state shared by the axes of one instant is
+// formed once (dyn_*_state); each axis / component then costs its own chain (dyn_euler_axis,
+// dyn_rv_column). Used by eval_dyn (tile path, host structure pass) and by the gait Dynamic record
+// kernel (gstream.hip), which stores the coefficients for the composer.
+struct DynEulerState {
+  SplinePt A;
+  Trig q;
+  double R[3][3], M0[3], M1[3], Md0[3], Md1[3], w[3], wd[3], RI[3][3], Iw[3][3], Iww[3];
+};
+// Euler ZYX: A(.) = I_w wd + w x (I_w w);  I_w = R I_b R^T,  w = M thd,  wd = Mdot thd + M thdd
+TG_HD void dyn_euler_state(const Ctx& c, double t, DynEulerState& S) {
+  spline_eval(c, SP_BASE_ANG, t, S.A);
+  const SplinePt& A = S.A;
+  S.q = trig(A.p);
+  const double sy = S.q.sy, cy = S.q.cy, sz = S.q.sz, cz = S.q.cz;
+  const double xd = A.v[0], yd = A.v[1], zd = A.v[2];
+  euler_R(S.q, S.R);
+  // M columns (GetM :133-148) and Mdot columns (GetMdot :150-166)
+  S.M0[0] = cy * cz; S.M0[1] = cy * sz; S.M0[2] = -sy;
+  S.M1[0] = -sz; S.M1[1] = cz; S.M1[2] = 0.0;
+  S.Md0[0] = -cz * sy * yd - cy * sz * zd; S.Md0[1] = cy * cz * zd - sy * sz * yd; S.Md0[2] = -cy * yd;
+  S.Md1[0] = -cz * zd; S.Md1[1] = -sz * zd; S.Md1[2] = 0.0;
+  for (int i = 0; i < 3; ++i) {
+    const double M2i = i == 2 ? 1.0 : 0.0;
+    S.w[i] = S.M0[i] * xd + S.M1[i] * yd + M2i * zd;
+    S.wd[i] = (S.Md0[i] * xd + S.Md1[i] * yd) + (S.M0[i] * A.a[0] + S.M1[i] * A.a[1] + M2i * A.a[2]);
+  }
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) S.RI[i][j] = S.R[i][0] * c.rb.Ib[0 * 3 + j] + S.R[i][1] * c.rb.Ib[1 * 3 + j] + S.R[i][2] * c.rb.Ib[2 * 3 + j];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) S.Iw[i][j] = S.RI[i][0] * S.R[j][0] + S.RI[i][1] * S.R[j][1] + S.RI[i][2] * S.R[j][2];
+  mat3_vec(S.Iw, S.w, S.Iww);
+}
+// one Euler axis e: the chain rule through (theta_e, theta_dot_e, theta_ddot_e)
+TG_HD void dyn_euler_axis(const Ctx& c, const DynEulerState& S, const int e, double Ap[3], double Av[3], double Aa[3]) {
+  const double sy = S.q.sy, cy = S.q.cy, sz = S.q.sz, cz = S.q.cz;
+  const double xd = S.A.v[0], yd = S.A.v[1], zd = S.A.v[2];
+  const double(&R)[3][3] = S.R;
+  const double(&RI)[3][3] = S.RI;
+  const double(&Iw)[3][3] = S.Iw;
+  const double *w = S.w, *wd = S.wd;
+  double dR[3][3]; euler_dR_axis(S.q, e, dR);
+  // dw = dM_e thd; dwd = dMdot_e thd + dM_e thdd (GetDerivMwrtNodes :168-198, GetDerivMdotwrtNodes :270-304)
+  double dw[3] = {0.0, 0.0, 0.0}, dwd[3] = {0.0, 0.0, 0.0};
+  if (e == 1) {
+    const double dM0[3] = {-sy * cz, -sy * sz, -cy};
+    const double dMd0[3] = {-cy * cz * yd + sy * sz * zd, -cy * sz * yd - sy * cz * zd, sy * yd};
+    for (int i = 0; i < 3; ++i) { dw[i] = dM0[i] * xd; dwd[i] = dMd0[i] * xd + dM0[i] * S.A.a[0]; }
+  } else if (e == 2) {
+    const double dM0[3] = {-cy * sz, cy * cz, 0.0}, dM1[3] = {-cz, -sz, 0.0};
+    const double dMd0[3] = {sy * sz * yd - cy * cz * zd, -sy * cz * yd - cy * sz * zd, 0.0};
+    const double dMd1[3] = {sz * zd, -cz * zd, 0.0};
+    for (int i = 0; i < 3; ++i) {
+      dw[i] = dM0[i] * xd + dM1[i] * yd;
+      dwd[i] = (dMd0[i] * xd + dMd1[i] * yd) + (dM0[i] * S.A.a[0] + dM1[i] * S.A.a[1]);
+    }
+  }
+  // dI_w/dtheta_e = dR I_b R^T + R I_b dR^T, applied to wd and w
+  double dRI[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) dRI[i][j] = dR[i][0] * c.rb.Ib[0 * 3 + j] + dR[i][1] * c.rb.Ib[1 * 3 + j] + dR[i][2] * c.rb.Ib[2 * 3 + j];
+  double dIwd[3], dIw_w[3];
+  {
+    double u[3], v[3];   // R^T wd, dR^T wd (and the same for w)
+    for (int j = 0; j < 3; ++j) { u[j] = R[0][j] * wd[0] + R[1][j] * wd[1] + R[2][j] * wd[2]; v[j] = dR[0][j] * wd[0] + dR[1][j] * wd[1] + dR[2][j] * wd[2]; }
+    for (int i = 0; i < 3; ++i) dIwd[i] = (dRI[i][0] * u[0] + dRI[i][1] * u[1] + dRI[i][2] * u[2]) + (RI[i][0] * v[0] + RI[i][1] * v[1] + RI[i][2] * v[2]);
+    for (int j = 0; j < 3; ++j) { u[j] = R[0][j] * w[0] + R[1][j] * w[1] + R[2][j] * w[2]; v[j] = dR[0][j] * w[0] + dR[1][j] * w[1] + dR[2][j] * w[2]; }
+    for (int i = 0; i < 3; ++i) dIw_w[i] = (dRI[i][0] * u[0] + dRI[i][1] * u[1] + dRI[i][2] * u[2]) + (RI[i][0] * v[0] + RI[i][1] * v[1] + RI[i][2] * v[2]);
+  }
+  double t1[3], t2[3], t3[3];
+  // theta_e: dI_w wd + I_w dwd + dw x (I_w w) + w x (dI_w w + I_w dw)
+  mat3_vec(Iw, dwd, t1); cross3(dw, S.Iww, t2); mat3_vec(Iw, dw, t3);
+  for (int i = 0; i < 3; ++i) t3[i] += dIw_w[i];
+  double t4[3]; cross3(w, t3, t4);
+  for (int i = 0; i < 3; ++i) Ap[i] = dIwd[i] + t1[i] + t2[i] + t4[i];
+  // theta_dot_e: dw = M[:,e], dwd = dM_e thd + Mdot[:,e]
+  const double Me[3] = {e == 0 ? S.M0[0] : e == 1 ? S.M1[0] : 0.0, e == 0 ? S.M0[1] : e == 1 ? S.M1[1] : 0.0,
+                        e == 0 ? S.M0[2] : e == 1 ? S.M1[2] : 1.0};
+  double dwv[3];
+  for (int i = 0; i < 3; ++i) dwv[i] = dw[i] + (e == 0 ? S.Md0[i] : e == 1 ? S.Md1[i] : 0.0);
+  mat3_vec(Iw, dwv, t1); cross3(Me, S.Iww, t2); mat3_vec(Iw, Me, t3); cross3(w, t3, t4);
+  for (int i = 0; i < 3; ++i) { Av[i] = t1[i] + t2[i] + t4[i]; Aa[i] = t3[i]; }   // theta_ddot_e: I_w M[:,e]
+}
+
+// RotVecConverter (GetJacobianWrtBaseAng :124-166 with the converter's DerivOfRotVecMult /
+// GetDerivOfAngVelWrtNodes / GetDerivOfAngAccWrtNodes), coefficient form:
+//   jac1 = d(R v11)/. + R I_b d(R^T wd)/. + I_w d wd/.
+//   jac2 = [w]x (d(R v21)/. + R I_b d(R^T w)/. + I_w d w/.) - [I_w w]x d w/.
+// One rotation-vector component e (a column of every coefficient matrix) at a time, each column by the
+// full-matrix code's element expressions: the whole matrices at once needed ~400 live doubles and
+// spilled 884 bytes per lane to scratch.
+struct DynRvState {
+  SplinePt A;
+  double theta;
+  RvCoeffs cf;   // the instant's converter coefficients, formed once
+  double R[3][3], w[3], wd[3], JL[3][3], JLd[3][3], RI[3][3], Iw[3][3], v11[3], v21[3], Iww[3], nhd[3];
+};
+TG_HD void dyn_rv_state(const Ctx& c, double t, DynRvState& S) {
+  spline_eval(c, SP_BASE_ANG, t, S.A);
+  const SplinePt& A = S.A;
+  S.theta = rv_norm(A.p);
+  S.cf = rv_coeffs(S.theta);
+  rv_rodrigues_c(A.p, S.theta, S.cf, S.R);
+  rv_left_jac_c(A.p, S.theta, S.cf, S.JL);
+  rv_left_jac_dot_c(A.p, A.v, S.theta, S.cf, S.JLd);
+  {   // rv_state
+    double a[3], b[3];
+    mat3_vec(S.JL, A.v, S.w);
+    mat3_vec(S.JLd, A.v, a); mat3_vec(S.JL, A.a, b);
+    for (int k = 0; k < 3; ++k) S.wd[k] = a[k] + b[k];
+  }
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) S.RI[i][j] = S.R[i][0] * c.rb.Ib[0 * 3 + j] + S.R[i][1] * c.rb.Ib[1 * 3 + j] + S.R[i][2] * c.rb.Ib[2 * 3 + j];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) S.Iw[i][j] = S.RI[i][0] * S.R[j][0] + S.RI[i][1] * S.R[j][1] + S.RI[i][2] * S.R[j][2];
+  double u[3];
+  for (int j = 0; j < 3; ++j) u[j] = S.R[0][j] * S.wd[0] + S.R[1][j] * S.wd[1] + S.R[2][j] * S.wd[2];
+  for (int i = 0; i < 3; ++i) S.v11[i] = c.rb.Ib[i * 3 + 0] * u[0] + c.rb.Ib[i * 3 + 1] * u[1] + c.rb.Ib[i * 3 + 2] * u[2];
+  for (int j = 0; j < 3; ++j) u[j] = S.R[0][j] * S.w[0] + S.R[1][j] * S.w[1] + S.R[2][j] * S.w[2];
+  for (int i = 0; i < 3; ++i) S.v21[i] = c.rb.Ib[i * 3 + 0] * u[0] + c.rb.Ib[i * 3 + 1] * u[1] + c.rb.Ib[i * 3 + 2] * u[2];
+  mat3_vec(S.Iw, S.w, S.Iww);
+  rv_dJL_nh(A.p, S.theta, S.nhd);
+}
+// component E (compile-time: a runtime index puts the 3x3 arrays in scratch) of every coefficient matrix
+template <int E>
+TG_HD void dyn_rv_column(const DynRvState& S, double Mp[3], double Mv[3], double Ma[3]) {
+  constexpr int e = E;
+  const SplinePt& A = S.A;
+  const double(&R)[3][3] = S.R;
+  const double(&JL)[3][3] = S.JL;
+  const double(&RI)[3][3] = S.RI;
+  const double(&Iw)[3][3] = S.Iw;
+  double m1[3], t1[3], pa[3], va[3], pw[3];
+  {
+    double Pc[3][3]; rv_dJL_col(A.p, S.cf, S.nhd, e, Pc);   // Pw[:, e] (rv_angvel_jac)
+    for (int d = 0; d < 3; ++d) pw[d] = A.v[0] * Pc[d][0] + A.v[1] * Pc[d][1] + A.v[2] * Pc[d][2];
+  }
+  rv_angacc_col(A.p, A.v, A.a, e, S.theta, S.cf, S.JLd, S.nhd, pa, va);   // Pa[:, e], Va[:, e]
+  rv_rotvec_mult_col(R, JL, S.v11, false, e, m1);
+  rv_rotvec_mult_col(R, JL, S.wd, true, e, t1);
+  double mp[3], sc[3];
+  for (int i = 0; i < 3; ++i)
+    mp[i] = (m1[i] + (RI[i][0] * t1[0] + RI[i][1] * t1[1] + RI[i][2] * t1[2])) + (Iw[i][0] * pa[0] + Iw[i][1] * pa[1] + Iw[i][2] * pa[2]);
+  rv_rotvec_mult_col(R, JL, S.v21, false, e, m1);
+  rv_rotvec_mult_col(R, JL, S.w, true, e, t1);
+  for (int i = 0; i < 3; ++i)
+    sc[i] = (m1[i] + (RI[i][0] * t1[0] + RI[i][1] * t1[1] + RI[i][2] * t1[2])) + (Iw[i][0] * pw[0] + Iw[i][1] * pw[1] + Iw[i][2] * pw[2]);
+  for (int r = 0; r < 3; ++r) {
+    double a = 0.0, b = 0.0, av = 0.0, bv = 0.0;
+    for (int k = 0; k < 3; ++k) {
+      const double cw = cross_el(S.w, r, k), ci = cross_el(S.Iww, r, k);
+      a += cw * sc[k]; b += ci * pw[k];
+      double iv = Iw[k][0] * JL[0][e] + Iw[k][1] * JL[1][e] + Iw[k][2] * JL[2][e];
+      av += cw * iv; bv += ci * JL[k][e];
+    }
+    Mp[r] = mp[r] + (a - b);
+    Mv[r] = (Iw[r][0] * va[0] + Iw[r][1] * va[1] + Iw[r][2] * va[2]) + (av - bv);
+    Ma[r] = Iw[r][0] * JL[0][e] + Iw[r][1] * JL[1][e] + Iw[r][2] * JL[2][e];
+  }
+}
+
 template <class Emit>
 TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
   if constexpr (emit_dyn_groups<Emit>::value == 1) { if (it.group == 1) return; }
@@ -1202,83 +1354,22 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
     dyn_g0_b(c, it, em, st, fs, ts);
     return;
   }
-#ifdef TOWR_EXP_DYN_NOG1   // register-pressure experiment only: no base-angular group
-  if (it.group == 1) return;
-#endif
-#ifdef TOWR_EXP_DYN_NOEE   // register-pressure experiment only: no endeffector groups
-  if (it.group >= 2) return;
-#endif
   if (it.group == 1 && c.rotvec) {
-    // d/d base-ang, RotVecConverter (GetJacobianWrtBaseAng :124-166 with the converter's
-    // DerivOfRotVecMult / GetDerivOfAngVelWrtNodes / GetDerivOfAngAccWrtNodes), coefficient form:
-    //   jac1 = d(R v11)/. + R I_b d(R^T wd)/. + I_w d wd/.
-    //   jac2 = [w]x (d(R v21)/. + R I_b d(R^T w)/. + I_w d w/.) - [I_w w]x d w/.
-    // One rotation-vector component e (a column of every coefficient matrix) at a time, each column
-    // by the full-matrix code's element expressions: the whole matrices at once needed ~400 live
-    // doubles and spilled 884 bytes per lane to scratch.
-    SplinePt A; spline_eval(c, SP_BASE_ANG, t, A);
-    const double theta = rv_norm(A.p);
-    const RvCoeffs cf = rv_coeffs(theta);   // the instant's converter coefficients, formed once
-    double R[3][3], w[3], wd[3], JL[3][3], JLd[3][3];
-    rv_rodrigues_c(A.p, theta, cf, R);
-    rv_left_jac_c(A.p, theta, cf, JL);
-    rv_left_jac_dot_c(A.p, A.v, theta, cf, JLd);
-    {   // rv_state
-      double a[3], b[3];
-      mat3_vec(JL, A.v, w);
-      mat3_vec(JLd, A.v, a); mat3_vec(JL, A.a, b);
-      for (int k = 0; k < 3; ++k) wd[k] = a[k] + b[k];
-    }
-    double RI[3][3], Iw[3][3];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) RI[i][j] = R[i][0] * c.rb.Ib[0 * 3 + j] + R[i][1] * c.rb.Ib[1 * 3 + j] + R[i][2] * c.rb.Ib[2 * 3 + j];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) Iw[i][j] = RI[i][0] * R[j][0] + RI[i][1] * R[j][1] + RI[i][2] * R[j][2];
-    double u[3], v11[3], v21[3];
-    for (int j = 0; j < 3; ++j) u[j] = R[0][j] * wd[0] + R[1][j] * wd[1] + R[2][j] * wd[2];
-    for (int i = 0; i < 3; ++i) v11[i] = c.rb.Ib[i * 3 + 0] * u[0] + c.rb.Ib[i * 3 + 1] * u[1] + c.rb.Ib[i * 3 + 2] * u[2];
-    for (int j = 0; j < 3; ++j) u[j] = R[0][j] * w[0] + R[1][j] * w[1] + R[2][j] * w[2];
-    for (int i = 0; i < 3; ++i) v21[i] = c.rb.Ib[i * 3 + 0] * u[0] + c.rb.Ib[i * 3 + 1] * u[1] + c.rb.Ib[i * 3 + 2] * u[2];
-    double Iww[3]; mat3_vec(Iw, w, Iww);
-    double nhd[3]; rv_dJL_nh(A.p, theta, nhd);
+    DynRvState S;
+    dyn_rv_state(c, t, S);
     double Hp[4], Hv[4], Ha[4];
-    spline_basis(A, kPos, Hp); spline_basis(A, kVel, Hv); spline_basis(A, kAcc, Ha);
+    spline_basis(S.A, kPos, Hp); spline_basis(S.A, kVel, Hv); spline_basis(S.A, kAcc, Ha);
     // one column per call: a RotVec g1 item carries its component in a1 (1 + e, layout.hip); the
     // device evaluates exactly that column (a loop over three columns spilled to scratch), the host
     // structure pass and emulation take every column of an unsplit item in order
     auto column = [&](auto ec) {   // ec: std::integral_constant (the device instantiates each column)
       constexpr int e = decltype(ec)::value;
-      double m1[3], t1[3], pa[3], va[3], pw[3];
-      {
-        double Pc[3][3]; rv_dJL_col(A.p, cf, nhd, e, Pc);   // Pw[:, e] (rv_angvel_jac)
-        for (int d = 0; d < 3; ++d) pw[d] = A.v[0] * Pc[d][0] + A.v[1] * Pc[d][1] + A.v[2] * Pc[d][2];
-      }
-      rv_angacc_col(A.p, A.v, A.a, e, theta, cf, JLd, nhd, pa, va);   // Pa[:, e], Va[:, e]
-      rv_rotvec_mult_col(R, JL, v11, false, e, m1);
-      rv_rotvec_mult_col(R, JL, wd, true, e, t1);
-      double mp[3], sc[3];
-      for (int i = 0; i < 3; ++i)
-        mp[i] = (m1[i] + (RI[i][0] * t1[0] + RI[i][1] * t1[1] + RI[i][2] * t1[2])) + (Iw[i][0] * pa[0] + Iw[i][1] * pa[1] + Iw[i][2] * pa[2]);
-      rv_rotvec_mult_col(R, JL, v21, false, e, m1);
-      rv_rotvec_mult_col(R, JL, w, true, e, t1);
-      for (int i = 0; i < 3; ++i)
-        sc[i] = (m1[i] + (RI[i][0] * t1[0] + RI[i][1] * t1[1] + RI[i][2] * t1[2])) + (Iw[i][0] * pw[0] + Iw[i][1] * pw[1] + Iw[i][2] * pw[2]);
-      for (int r = 0; r < 3; ++r) {
-        double a = 0.0, b = 0.0, av = 0.0, bv = 0.0;
-        for (int k = 0; k < 3; ++k) {
-          const double cw = cross_el(w, r, k), ci = cross_el(Iww, r, k);
-          a += cw * sc[k]; b += ci * pw[k];
-          double iv = Iw[k][0] * JL[0][e] + Iw[k][1] * JL[1][e] + Iw[k][2] * JL[2][e];
-          av += cw * iv; bv += ci * JL[k][e];
-        }
-        const double Mp = mp[r] + (a - b);
-        const double Mv = (Iw[r][0] * va[0] + Iw[r][1] * va[1] + Iw[r][2] * va[2]) + (av - bv);
-        const double Ma = Iw[r][0] * JL[0][e] + Iw[r][1] * JL[1][e] + Iw[r][2] * JL[2][e];
+      double Mp[3], Mv[3], Ma[3];
+      dyn_rv_column<e>(S, Mp, Mv, Ma);
+      for (int r = 0; r < 3; ++r)
         for (int bb = 0; bb < 4; ++bb)
-          em(r0 + AX + r, basis_col(c, SP_BASE_ANG, A.poly, bb, e), Mp * Hp[bb] + Mv * Hv[bb] + Ma * Ha[bb], true);
-      }
+          em(r0 + AX + r, basis_col(c, SP_BASE_ANG, S.A.poly, bb, e), Mp[r] * Hp[bb] + Mv[r] * Hv[bb] + Ma[r] * Ha[bb], true);
     };
-    // compile-time column indices: a runtime e indexes the 3x3 arrays dynamically, which puts them in scratch
     const int e_lo = it.a1 > 0 ? it.a1 - 1 : 0, e_hi = it.a1 > 0 ? it.a1 : 3;
     if (e_lo <= 0 && 0 < e_hi) column(std::integral_constant<int, 0>{});
     if (e_lo <= 1 && 1 < e_hi) column(std::integral_constant<int, 1>{});
@@ -1286,88 +1377,22 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
     return;
   }
   if (it.group == 1) {
-    // d/d base-ang (GetJacobianWrtBaseAng :124-166): chain rule through (theta, theta_dot,
-    // theta_ddot) of the Euler spline, one Euler axis e at a time to keep the live set small.
-    //   A(.) = I_w wd + w x (I_w w);  I_w = R I_b R^T,  w = M thd,  wd = Mdot thd + M thdd
-    SplinePt A; spline_eval(c, SP_BASE_ANG, t, A);
-    const Trig q = trig(A.p);
-    const double sy = q.sy, cy = q.cy, sz = q.sz, cz = q.cz;
-    const double xd = A.v[0], yd = A.v[1], zd = A.v[2];
-    double R[3][3]; euler_R(q, R);
-    // M columns (GetM :133-148) and Mdot columns (GetMdot :150-166)
-    const double M0[3] = {cy * cz, cy * sz, -sy}, M1[3] = {-sz, cz, 0.0};
-    const double Md0[3] = {-cz * sy * yd - cy * sz * zd, cy * cz * zd - sy * sz * yd, -cy * yd};
-    const double Md1[3] = {-cz * zd, -sz * zd, 0.0};
-    double w[3], wd[3];
-    for (int i = 0; i < 3; ++i) {
-      const double M2i = i == 2 ? 1.0 : 0.0;
-      w[i] = M0[i] * xd + M1[i] * yd + M2i * zd;
-      wd[i] = (Md0[i] * xd + Md1[i] * yd) + (M0[i] * A.a[0] + M1[i] * A.a[1] + M2i * A.a[2]);
-    }
-    double RI[3][3], Iw[3][3];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) RI[i][j] = R[i][0] * c.rb.Ib[0 * 3 + j] + R[i][1] * c.rb.Ib[1 * 3 + j] + R[i][2] * c.rb.Ib[2 * 3 + j];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) Iw[i][j] = RI[i][0] * R[j][0] + RI[i][1] * R[j][1] + RI[i][2] * R[j][2];
-    double Iww[3]; mat3_vec(Iw, w, Iww);
+    DynEulerState S;
+    dyn_euler_state(c, t, S);
     double Hp[4], Hv[4], Ha[4];
-    spline_basis(A, kPos, Hp); spline_basis(A, kVel, Hv); spline_basis(A, kAcc, Ha);
-    // One Euler axis per item (layout.hip: 3 lanes per instant, a1 = 1 + axis): on the device each
-    // lane instantiates its axis with a compile-time index; all three axes in one lane needed 242
-    // VGPRs (2 waves per SIMD), one axis 166. The host (structure pass, emulation) and an unsplit
-    // item (a1 = 0) take the axes in order.
+    spline_basis(S.A, kPos, Hp); spline_basis(S.A, kVel, Hv); spline_basis(S.A, kAcc, Ha);
+    // all three axes in one lane (242 VGPRs on the fixed-gait device tile); the host (structure pass,
+    // emulation) takes the axes of an unsplit item (a1 = 0) in order
     auto axis = [&](const int e) {
-      double dR[3][3]; euler_dR_axis(q, e, dR);
-      // dw = dM_e thd; dwd = dMdot_e thd + dM_e thdd (GetDerivMwrtNodes :168-198, GetDerivMdotwrtNodes :270-304)
-      double dw[3] = {0.0, 0.0, 0.0}, dwd[3] = {0.0, 0.0, 0.0};
-      if (e == 1) {
-        const double dM0[3] = {-sy * cz, -sy * sz, -cy};
-        const double dMd0[3] = {-cy * cz * yd + sy * sz * zd, -cy * sz * yd - sy * cz * zd, sy * yd};
-        for (int i = 0; i < 3; ++i) { dw[i] = dM0[i] * xd; dwd[i] = dMd0[i] * xd + dM0[i] * A.a[0]; }
-      } else if (e == 2) {
-        const double dM0[3] = {-cy * sz, cy * cz, 0.0}, dM1[3] = {-cz, -sz, 0.0};
-        const double dMd0[3] = {sy * sz * yd - cy * cz * zd, -sy * cz * yd - cy * sz * zd, 0.0};
-        const double dMd1[3] = {sz * zd, -cz * zd, 0.0};
-        for (int i = 0; i < 3; ++i) {
-          dw[i] = dM0[i] * xd + dM1[i] * yd;
-          dwd[i] = (dMd0[i] * xd + dMd1[i] * yd) + (dM0[i] * A.a[0] + dM1[i] * A.a[1]);
-        }
-      }
-      // dI_w/dtheta_e = dR I_b R^T + R I_b dR^T, applied to wd and w
-      double dRI[3][3];
-      for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) dRI[i][j] = dR[i][0] * c.rb.Ib[0 * 3 + j] + dR[i][1] * c.rb.Ib[1 * 3 + j] + dR[i][2] * c.rb.Ib[2 * 3 + j];
-      double dIwd[3], dIw_w[3];
-      {
-        double u[3], v[3];   // R^T wd, dR^T wd (and the same for w)
-        for (int j = 0; j < 3; ++j) { u[j] = R[0][j] * wd[0] + R[1][j] * wd[1] + R[2][j] * wd[2]; v[j] = dR[0][j] * wd[0] + dR[1][j] * wd[1] + dR[2][j] * wd[2]; }
-        for (int i = 0; i < 3; ++i) dIwd[i] = (dRI[i][0] * u[0] + dRI[i][1] * u[1] + dRI[i][2] * u[2]) + (RI[i][0] * v[0] + RI[i][1] * v[1] + RI[i][2] * v[2]);
-        for (int j = 0; j < 3; ++j) { u[j] = R[0][j] * w[0] + R[1][j] * w[1] + R[2][j] * w[2]; v[j] = dR[0][j] * w[0] + dR[1][j] * w[1] + dR[2][j] * w[2]; }
-        for (int i = 0; i < 3; ++i) dIw_w[i] = (dRI[i][0] * u[0] + dRI[i][1] * u[1] + dRI[i][2] * u[2]) + (RI[i][0] * v[0] + RI[i][1] * v[1] + RI[i][2] * v[2]);
-      }
-      double Ap[3], Av[3], Aa[3], t1[3], t2[3], t3[3];
-      // theta_e: dI_w wd + I_w dwd + dw x (I_w w) + w x (dI_w w + I_w dw)
-      mat3_vec(Iw, dwd, t1); cross3(dw, Iww, t2); mat3_vec(Iw, dw, t3);
-      for (int i = 0; i < 3; ++i) t3[i] += dIw_w[i];
-      double t4[3]; cross3(w, t3, t4);
-      for (int i = 0; i < 3; ++i) Ap[i] = dIwd[i] + t1[i] + t2[i] + t4[i];
-      // theta_dot_e: dw = M[:,e], dwd = dM_e thd + Mdot[:,e]
-      const double Me[3] = {e == 0 ? M0[0] : e == 1 ? M1[0] : 0.0, e == 0 ? M0[1] : e == 1 ? M1[1] : 0.0, e == 0 ? M0[2] : e == 1 ? M1[2] : 1.0};
-      double dwv[3];
-      for (int i = 0; i < 3; ++i) dwv[i] = dw[i] + (e == 0 ? Md0[i] : e == 1 ? Md1[i] : 0.0);
-      mat3_vec(Iw, dwv, t1); cross3(Me, Iww, t2); mat3_vec(Iw, Me, t3); cross3(w, t3, t4);
-      for (int i = 0; i < 3; ++i) { Av[i] = t1[i] + t2[i] + t4[i]; Aa[i] = t3[i]; }   // theta_ddot_e: I_w M[:,e]
+      double Ap[3], Av[3], Aa[3];
+      dyn_euler_axis(c, S, e, Ap, Av, Aa);
       for (int r = 0; r < 3; ++r)
         for (int bb = 0; bb < 4; ++bb)
-          em(r0 + AX + r, basis_col(c, SP_BASE_ANG, A.poly, bb, e), Ap[r] * Hp[bb] + Av[r] * Hv[bb] + Aa[r] * Ha[bb], true);
+          em(r0 + AX + r, basis_col(c, SP_BASE_ANG, S.A.poly, bb, e), Ap[r] * Hp[bb] + Av[r] * Hv[bb] + Aa[r] * Ha[bb], true);
     };
 #if defined(__HIP_DEVICE_COMPILE__)
-    if (split_base_ang(c.gait)) {   // compile-time in the kernels (GAIT): the layout split every item
-      axis(it.a1 - 1);              // one axis per lane (runtime index: the axis code indexes no array by it)
-    } else {
 #pragma unroll
-      for (int e = 0; e < 3; ++e) axis(e);
-    }
+    for (int e = 0; e < 3; ++e) axis(e);
 #else
     for (int e = 0; e < 3; ++e)
       if (it.a1 == 0 || it.a1 == 1 + e) axis(e);

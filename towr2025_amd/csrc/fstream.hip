@@ -37,45 +37,13 @@ template <int BLOCK>
 __global__ void __launch_bounds__(BLOCK, 1) towr_fdisc_inst_kernel(KParams P, double* rec, int64_t ldr, int32_t ni) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int b = blockIdx.x;
-  const double* xg = P.X + (int64_t)b * P.ldx;
   double* Gb = P.G + (int64_t)b * P.ldg;
   double* R = rec + (int64_t)b * ldr;
-  double* xs = smem;
-  int32_t* ns = reinterpret_cast<int32_t*>(xs + P.n_pad);
-  char* gt = reinterpret_cast<char*>(xs + P.n_pad + ((P.n_nodecol + 3) >> 2) * 2);
-  towr_terrain_t* ters = reinterpret_cast<towr_terrain_t*>(gt + 16 * P.gt_n16 + 8 * P.gt_ntime);
   const int tid = threadIdx.x;
 #ifdef TOWR_PHASE_TIMING
   if (tid < 64) { TSTAMP(0, TS_REAL()); TSTAMP(1, TS_MEM()); }
 #endif
-  stage_x<BLOCK, true>(P, xg, xs, ns);
-  stage16<BLOCK>(reinterpret_cast<uint4*>(gt), P.gtab, P.gt_n16);
-  if (tid < (int)(sizeof(towr_terrain_t) / 8))
-    reinterpret_cast<double*>(ters)[tid] = reinterpret_cast<const double*>(P.terrains + (P.terrain_per_problem ? b : 0))[tid];
-  __syncthreads();
-  Ctx c;
-  c.seg = nullptr; c.sg = P.sg; c.row = -1;
-  c.x = xs; c.nodecol = ns; c.dur = P.dur;
-  c.ter = ters;
-  c.rb = P.rb; c.fdisc_motion = 0;
-  c.gait = true; c.eelin = P.eelin;
-  c.spl = reinterpret_cast<const SplineMeta*>(gt + P.gt_off[0]);
-  c.sched = reinterpret_cast<const SchedInfo*>(gt + P.gt_off[1]);
-  c.pinfo = reinterpret_cast<const PolyPhase*>(gt + P.gt_off[2]);
-  c.pact = reinterpret_cast<const int32_t*>(gt + P.gt_off[3]);
-  c.pcols = reinterpret_cast<const PhaseCol*>(gt + P.gt_off[4]);
-  c.rotvec = false;
-  c.dyn_scratch = nullptr;
-  // the x-dependent PhaseSpline timings once per block (as tile_body under GAIT)
-  double* tmg = reinterpret_cast<double*>(gt + 16 * P.gt_n16);
-  const int nspl = P.n_spl, nee = P.rb.n_ee;
-  if (tid < nspl) {
-    if (c.spl[tid].ee >= 0) phase_spline_timings(c, tid, tmg, tmg + P.n_pinfo);
-  } else if (tid < nspl + nee) {
-    if (c.sched[tid - nspl].col0 >= 0) phase_end_timings(c, tid - nspl, tmg + 2 * P.n_pinfo + (tid - nspl) * P.ph_stride);
-  }
-  __syncthreads();
-  c.pdur = tmg; c.pend = tmg + P.n_pinfo; c.phend = tmg + 2 * P.n_pinfo; c.ph_stride = P.ph_stride;
+  Ctx c = gait_record_setup<BLOCK>(P, b, smem);
 #ifdef TOWR_PHASE_TIMING
   if (tid < 64) TSTAMP(2, TS_MEM());
 #endif

@@ -57,6 +57,11 @@ struct KParams {
   const int32_t* fs_ws;
   const int32_t* fs_iee;          // per FDISC instant: endeffector, first g row
   const int32_t* fs_irow;
+  const GsGeo* gs_geo;            // streaming RangeOfMotion / Dynamic (layout.h GsGeo)
+  const GsBlock* gs_blk;          // the launched class's compose blocks
+  const GsInst* gs_inst;          // the launched class's record instants
+  const int32_t* gs_tmpl;
+  const uint8_t* gs_pcode;
   const CostItem* citems;         // cost launch: work items, objective and gradient outputs
   const double* cq;               // cost launch: CT_ENERGYQ Gram matrices
   int32_t n_citems, lds_red_off;
@@ -195,6 +200,48 @@ __device__ __forceinline__ void stage_x(const KParams& P, const double* xg, doub
   if (threadIdx.x == 0) xs[P.n] = 0.0;
   if constexpr (NODES)
     stage16<BLOCK>(reinterpret_cast<uint4*>(ns), reinterpret_cast<const uint4*>(P.nodecol), (P.n_nodecol + 3) >> 2);
+}
+
+// Prologue of the per-problem record kernels under phase-duration optimisation (fstream.hip,
+// gstream.hip): x (+ zero slot), the node table, the PhaseSpline tables and the terrain staged in LDS
+// ([x | node table | tables | timings | terrain], fs_inst_lds_bytes), then the x-dependent PhaseSpline
+// timings formed once per block (as tile_body does); returns the evaluation context over them.
+template <int BLOCK>
+__device__ __forceinline__ Ctx gait_record_setup(const KParams& P, int b, double* smem) {
+  const double* xg = P.X + (int64_t)b * P.ldx;
+  double* xs = smem;
+  int32_t* ns = reinterpret_cast<int32_t*>(xs + P.n_pad);
+  char* gt = reinterpret_cast<char*>(xs + P.n_pad + ((P.n_nodecol + 3) >> 2) * 2);
+  towr_terrain_t* ters = reinterpret_cast<towr_terrain_t*>(gt + 16 * P.gt_n16 + 8 * P.gt_ntime);
+  const int tid = threadIdx.x;
+  stage_x<BLOCK, true>(P, xg, xs, ns);
+  stage16<BLOCK>(reinterpret_cast<uint4*>(gt), P.gtab, P.gt_n16);
+  if (tid < (int)(sizeof(towr_terrain_t) / 8))
+    reinterpret_cast<double*>(ters)[tid] = reinterpret_cast<const double*>(P.terrains + (P.terrain_per_problem ? b : 0))[tid];
+  __syncthreads();
+  Ctx c;
+  c.seg = nullptr; c.sg = P.sg; c.row = -1;
+  c.x = xs; c.nodecol = ns; c.dur = P.dur;
+  c.ter = ters;
+  c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
+  c.gait = true; c.eelin = P.eelin; c.lin = P.lin;
+  c.spl = reinterpret_cast<const SplineMeta*>(gt + P.gt_off[0]);
+  c.sched = reinterpret_cast<const SchedInfo*>(gt + P.gt_off[1]);
+  c.pinfo = reinterpret_cast<const PolyPhase*>(gt + P.gt_off[2]);
+  c.pact = reinterpret_cast<const int32_t*>(gt + P.gt_off[3]);
+  c.pcols = reinterpret_cast<const PhaseCol*>(gt + P.gt_off[4]);
+  c.rotvec = false;
+  c.dyn_scratch = nullptr;
+  double* tmg = reinterpret_cast<double*>(gt + 16 * P.gt_n16);
+  const int nspl = P.n_spl, nee = P.rb.n_ee;
+  if (tid < nspl) {
+    if (c.spl[tid].ee >= 0) phase_spline_timings(c, tid, tmg, tmg + P.n_pinfo);
+  } else if (tid < nspl + nee) {
+    if (c.sched[tid - nspl].col0 >= 0) phase_end_timings(c, tid - nspl, tmg + 2 * P.n_pinfo + (tid - nspl) * P.ph_stride);
+  }
+  __syncthreads();
+  c.pdur = tmg; c.pend = tmg + P.n_pinfo; c.phend = tmg + 2 * P.n_pinfo; c.ph_stride = P.ph_stride;
+  return c;
 }
 
 hipError_t fs_set_timing_buffer(void* p);   // fstream.hip: its translation unit's timing buffer

@@ -43,6 +43,43 @@ struct FsBlock {
   int32_t js0, ns1, wsoff, reserved;
 };
 
+// Streaming RangeOfMotion and Dynamic under phase-duration optimisation (gstream.hip), the FsBlock
+// scheme generalised to rows whose columns differ by row type. Two launches per class:
+//   record:  one block per problem, one lane per instant (Dynamic: per instant, per base-angular axis,
+//            per (instant, endeffector)) evaluates the instant once and stores what every Jacobian
+//            entry of its rows is a function of (the record, field-major in the handle's scratch);
+//   compose: one block per (problem, GsBlock) streams the block's whole CSR range with 16-byte
+//            stores, each unit written once, forming every entry from its instant's record and the
+//            entry's position.
+// Row r of an instant (its row type) is [base prefix | template]: the prefix holds the base-linear and
+// base-angular columns of the instant's active base polynomials, coded per (instant, row) as
+// blk << 4 | dim << 2 | basis (gs_pcode; the base node sets hold the smallest columns); the template is
+// the same for every instant (checked) and codes each remaining column (gs_tmpl):
+//   bit 31 set: schedule column, bits 16-18 endeffector, bits 0-15 column within its PhaseDurations;
+//   else: a PhaseSpline column, bits 28-29 spline kind (0 motion, 1 force, 2 torque), 25-27
+//   endeffector, 22-23 dimension, 0-21 PhaseCol index within that dimension's list.
+// A PhaseSpline column is non-zero only in its instant's active window, at most kGsAct PhaseCols per
+// dimension from the polynomial's first (pact); the composer's prologue forms their basis sums.
+enum GsClass { GS_ROM = 0, GS_DYN = 1, GS_COUNT = 2 };
+constexpr int kGsRowTypes = 6;
+constexpr int kGsAct = 4;
+constexpr int kGsBlock = 256;
+constexpr int kGsInstRom = 32;   // instants per compose block
+constexpr int kGsInstDyn = 8;
+struct GsGeo {
+  int32_t cls, ee, nrt, Li;   // class, endeffector (RangeOfMotion), row types, values per instant
+  int32_t L[kGsRowTypes], P[kGsRowTypes], T[kGsRowTypes], poff[kGsRowTypes];   // per row type: length, prefix, template offset, prefix codes offset
+  int32_t Psum, pc0, rec0, r0;   // prefix codes per instant, gs_pcode offset of instant 0, first record index, first row
+};
+struct GsBlock { int32_t geo, k0, n_inst, v0, nv, reserved[3]; };   // instants [k0, k0 + n_inst) of the geometry
+struct GsInst { double t; int32_t seg, ee, row0, reserved; };       // a record lane's instant
+constexpr int kRomRec = 38;    // R[9] | HL[4] | Ag[9] | HA[4] | poly | HP[4] | Jx.dx[3] v[3] cur
+constexpr int kDynBaseRec = 17;   // per instant: ab[3] | La[3] | Lp[3] | HpL[4] | HaL[4]
+constexpr int kDynAxisRec = 9;    // per (axis, instant): Ap[3] | Av[3] | Aa[3]
+constexpr int kDynHangRec = 12;   // per instant: the base-angular Hp[4] | Hv[4] | Ha[4]
+constexpr int kDynEeRec = 38;     // per (endeffector, instant): Fp Tqp Pp | polyF HF[4] | polyT HT[4] | polyP HP[4] | Jf | Jx
+TG_HD constexpr int64_t dyn_rec_doubles(int K, int E) { return (int64_t)(kDynBaseRec + 3 * kDynAxisRec + kDynHangRec + kDynEeRec * E) * K; }
+
 struct VarSetInfo { int kind, ee, col0, n; };
 struct ConsInfo { int kind, ee, row0, rows; };
 
@@ -105,6 +142,15 @@ struct Layout {
   std::vector<int32_t> fs_ws;        // per (constraint, force polynomial): window start, window dimension codes
   std::vector<int32_t> fs_iee, fs_irow;   // per instant (fs_t order): endeffector, first row
   int32_t fs_tmpl_max = 0;
+  // streaming RangeOfMotion / Dynamic (GsGeo): per class enabled when every constraint of the class fits
+  bool gstream[GS_COUNT] = {};
+  std::vector<GsGeo> gs_geo;
+  std::vector<GsBlock> gs_blocks[GS_COUNT];
+  std::vector<GsInst> gs_inst[GS_COUNT];   // record lanes' instants (Dynamic: one per instant)
+  std::vector<int32_t> gs_tmpl;
+  std::vector<uint8_t> gs_pcode;
+  int32_t gs_tmpl_max[GS_COUNT] = {};      // template ints of the largest geometry (compose LDS)
+  int32_t gs_pcode_max[GS_COUNT] = {};     // prefix codes per instant, largest geometry
   // cost terms (eval_f / eval_grad_f): work items sorted by CostType, one block per problem
   std::vector<CostItem> cost_items;
   std::vector<double> cost_q;        // CT_ENERGYQ Gram matrices, 16 doubles per item (CostItem::q)
@@ -178,6 +224,14 @@ int64_t fs_record_doubles();
 const void* fs_inst_kernel();
 const void* fs_stream_kernel();
 int fs_inst_block();
+
+// The streaming RangeOfMotion / Dynamic kernels (gstream.hip): compose LDS (bytes), record doubles
+// per problem, entry points. The record kernels use fs_inst_lds_bytes' LDS layout.
+size_t gs_stream_lds(const Layout& L, int cls);
+int64_t gs_record_doubles(const Layout& L, int cls);
+const void* gs_rec_kernel(int cls, bool rotvec);
+const void* gs_stream_kernel(int cls);
+int gs_rec_block();
 
 // Returns TOWR_OK or an error code with a message in `err`. Side data (towr_gpu_create_ex): the
 // LinearEqualityConstraint matrices; the SoftConstraint bounds are checked by the handle.

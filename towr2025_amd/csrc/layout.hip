@@ -426,6 +426,8 @@ int build_costs(const towr_problem_desc_t& d, const std::vector<double>& base_d,
       }
       case TOWR_COST_SOFT:   // soft_constraint.cc:34-69: evaluated by the handle's soft child
         if (c.ip[0] < 0 || c.ip[0] >= d.n_constraints) { err = "SoftConstraint: constraint index out of range"; return TOWR_ERR_INVALID; }
+        // the child's description holds one constraint per term (soft_desc)
+        if ((int)L.soft.size() >= TOWR_MAX_CONSTRAINTS) { err = "more SoftConstraint terms than TOWR_MAX_CONSTRAINTS"; return TOWR_ERR_INVALID; }
         L.soft.push_back({i, c.ip[0]});
         break;
       default: err = "unknown cost kind"; return TOWR_ERR_INVALID;
@@ -536,6 +538,156 @@ int build_fstream(Layout& L, std::string& err) {
   L.fstream = true;
   L.fs_blocks.swap(blocks); L.fs_t.swap(ts); L.fs_tmpl.swap(tmpl); L.fs_ws.swap(wsv); L.fs_tmpl_max = lmax;
   L.fs_iee.swap(iee); L.fs_irow.swap(irow);
+  return TOWR_OK;
+}
+
+// GsGeo / GsBlock tables of the streaming RangeOfMotion and Dynamic paths (layout.h). A class streams
+// when every one of its constraints passes the checks below; otherwise it keeps the tile path.
+namespace {
+struct BaseDec { int8_t s = -1, deriv = 0, dim = 0; int32_t node = 0; };   // base node-set column
+struct PhaseDec { int8_t kind = -1, ee = 0, dim = 0; int32_t q = 0; };     // PhaseSpline column (kind 0 motion, 1 force, 2 torque)
+
+bool build_gstream_class(Layout& L, int cls, const std::vector<BaseDec>& bdec, const std::vector<PhaseDec>& pdec,
+                         const std::vector<int>& sdec_ee, const std::vector<int>& sdec_j, std::string& why) {
+  const int nspl = (int)L.spl.size();
+  const int ctype = cls == GS_ROM ? TOWR_C_RANGE_OF_MOTION : TOWR_C_DYNAMIC;
+  const int itype = cls == GS_ROM ? IT_ROM : IT_DYN;
+  const int R = cls == GS_ROM ? 3 : 6;
+  std::vector<GsGeo> geos;
+  std::vector<GsBlock> blocks;
+  std::vector<GsInst> insts;
+  std::vector<int32_t> tmpl;
+  std::vector<uint8_t> pcode;
+  int tmax = 0, pmax = 0;
+  for (const ConsInfo& cs : L.cons) {
+    if (cs.kind != ctype || cs.rows == 0) continue;
+    const int K = cs.rows / R;
+    GsGeo g{};
+    g.cls = cls; g.ee = cls == GS_ROM ? cs.ee : -1; g.nrt = R; g.r0 = cs.row0;
+    g.rec0 = (int32_t)insts.size();
+    // the instants: time and segment row from the items of the set
+    std::vector<GsInst> its((size_t)K, GsInst{-1.0, -1, 0, 0, 0});
+    for (const ItemDesc& it : L.items)
+      if (it.type == itype && it.row0 >= cs.row0 && it.row0 < cs.row0 + cs.rows) {
+        GsInst& q = its[(it.row0 - cs.row0) / R];
+        q.t = it.t; q.seg = it.seg; q.ee = cls == GS_ROM ? cs.ee : 0; q.row0 = it.row0;
+      }
+    for (const GsInst& q : its) if (q.seg < 0) { why = "instant without items"; return false; }
+    const int toff = (int)tmpl.size();
+    int Lsum = 0, Psum = 0;
+    for (int r = 0; r < R; ++r) {
+      const int64_t b0 = L.row_ptr[cs.row0 + r], len = L.row_ptr[cs.row0 + r + 1] - b0;
+      int P = 0;
+      while (P < len && bdec[L.col[b0 + P]].s >= 0) ++P;
+      for (int k = 0; k < K; ++k) {   // same length and prefix length, same template columns
+        const int64_t a = L.row_ptr[cs.row0 + R * k + r], n = L.row_ptr[cs.row0 + R * k + r + 1] - a;
+        if (n != len) { why = "row lengths differ between instants"; return false; }
+        for (int64_t j = 0; j < n; ++j)
+          if ((bdec[L.col[a + j]].s >= 0) != (j < P)) { why = "base columns are not a prefix of constant length"; return false; }
+        if (!std::equal(L.col.begin() + a + P, L.col.begin() + a + n, L.col.begin() + b0 + P)) { why = "template differs between instants"; return false; }
+      }
+      g.L[r] = (int32_t)len; g.P[r] = P; g.T[r] = (int32_t)tmpl.size(); g.poff[r] = Psum;
+      for (int64_t j = P; j < len; ++j) {
+        const int32_t col = L.col[b0 + j];
+        if (sdec_ee[col] >= 0) {
+          if (cls == GS_ROM && sdec_ee[col] != cs.ee) { why = "schedule of another endeffector"; return false; }
+          tmpl.push_back((int32_t)(0x80000000u | ((uint32_t)sdec_ee[col] << 16) | (uint32_t)sdec_j[col]));
+          continue;
+        }
+        const PhaseDec& d = pdec[col];
+        if (d.kind < 0 || (cls == GS_ROM && (d.kind != 0 || d.ee != cs.ee))) { why = "a column the template cannot express"; return false; }
+        tmpl.push_back((int32_t)(((uint32_t)d.kind << 28) | ((uint32_t)d.ee << 25) | ((uint32_t)d.dim << 22) | (uint32_t)d.q));
+      }
+      Lsum += (int)len; Psum += P;
+      tmax = std::max(tmax, (int)tmpl.size() - toff);
+    }
+    g.Li = Lsum; g.Psum = Psum; g.pc0 = (int32_t)pcode.size();
+    pmax = std::max(pmax, Psum);
+    for (int k = 0; k < K; ++k) {   // prefix codes: blk << 4 | dim << 2 | basis of the instant's base polynomials
+      const int pl = L.segs[(size_t)its[k].seg * nspl + SP_BASE_LIN].poly, pa = L.segs[(size_t)its[k].seg * nspl + SP_BASE_ANG].poly;
+      for (int r = 0; r < R; ++r) {
+        const int64_t a = L.row_ptr[cs.row0 + R * k + r];
+        for (int j = 0; j < g.P[r]; ++j) {
+          const BaseDec& d = bdec[L.col[a + j]];
+          const int nb = d.node - (d.s == 0 ? pl : pa);
+          if (nb < 0 || nb > 1) { why = "base column outside the active polynomial"; return false; }
+          pcode.push_back((uint8_t)((d.s << 4) | (d.dim << 2) | (2 * nb + d.deriv)));
+        }
+      }
+    }
+    const int cap = cls == GS_ROM ? kGsInstRom : kGsInstDyn;
+    const int nb = (K + cap - 1) / cap;
+    for (int q = 0; q < nb; ++q) {
+      const int a = (int)((int64_t)q * K / nb), b = (int)((int64_t)(q + 1) * K / nb);
+      GsBlock bl{};
+      bl.geo = (int32_t)(L.gs_geo.size() + geos.size()); bl.k0 = a; bl.n_inst = b - a;
+      bl.v0 = (int32_t)L.row_ptr[cs.row0 + R * a]; bl.nv = (int32_t)(L.row_ptr[cs.row0 + R * b] - L.row_ptr[cs.row0 + R * a]);
+      if ((int64_t)bl.nv != (int64_t)(b - a) * Lsum) { why = "internal: block range"; return false; }
+      blocks.push_back(bl);
+    }
+    insts.insert(insts.end(), its.begin(), its.end());
+    geos.push_back(g);
+  }
+  if (geos.empty()) { why = "no constraint"; return false; }
+  // commit: geometries, templates and prefix codes are appended to the shared tables
+  const int32_t t0 = (int32_t)L.gs_tmpl.size(), p0 = (int32_t)L.gs_pcode.size();
+  for (GsGeo& g : geos) {
+    for (int r = 0; r < g.nrt; ++r) g.T[r] += t0;
+    g.pc0 += p0;
+    L.gs_geo.push_back(g);
+  }
+  L.gs_tmpl.insert(L.gs_tmpl.end(), tmpl.begin(), tmpl.end());
+  L.gs_pcode.insert(L.gs_pcode.end(), pcode.begin(), pcode.end());
+  L.gs_blocks[cls].swap(blocks);
+  L.gs_inst[cls].swap(insts);
+  L.gs_tmpl_max[cls] = tmax;
+  L.gs_pcode_max[cls] = pmax;
+  L.gstream[cls] = true;
+  return true;
+}
+}  // namespace
+
+int build_gstream(Layout& L, std::string& err) {
+  for (int c = 0; c < GS_COUNT; ++c) { L.gstream[c] = false; L.gs_blocks[c].clear(); L.gs_inst[c].clear(); L.gs_tmpl_max[c] = L.gs_pcode_max[c] = 0; }
+  L.gs_geo.clear(); L.gs_tmpl.clear(); L.gs_pcode.clear();
+  if (!L.gait || std::getenv("TOWR_GPU_GAIT_TILES")) return TOWR_OK;   // the tile path (A/B and parity of both paths)
+  const int E = L.rb.n_ee;
+  std::vector<BaseDec> bdec((size_t)L.n);
+  for (int s = 0; s < 2; ++s)
+    for (int node = 0; node <= L.spl[s].n_polys; ++node)
+      for (int deriv = 0; deriv < 2; ++deriv)
+        for (int dim = 0; dim < 3; ++dim) {
+          const int32_t col = L.nodecol[(size_t)(L.spl[s].node_off + node) * 6 + deriv * 3 + dim];
+          if (col >= 0) bdec[col] = BaseDec{(int8_t)s, (int8_t)deriv, (int8_t)dim, node};
+        }
+  std::vector<PhaseDec> pdec((size_t)L.n);
+  for (int ee = 0; ee < E; ++ee)
+    for (int kind = 0; kind < 3; ++kind) {
+      const int s = kind == 0 ? sp_motion(ee) : kind == 1 ? sp_force(ee) : sp_torque(ee);
+      const SplineMeta& m = L.spl[s];
+      if (m.ee != ee) return TOWR_OK;
+      for (int e = 0; e < 3; ++e) {
+        for (int q = 0; q < m.pcol_n[e]; ++q) pdec[L.pcols[m.pcol_off[e] + q].col] = PhaseDec{(int8_t)kind, (int8_t)ee, (int8_t)e, q};
+        for (int p = 0; p < m.n_polys; ++p) {   // active window of at most kGsAct PhaseCols
+          const int32_t* w = L.pact.data() + m.pact_off + 2 * (e * m.n_polys + p);
+          if (w[1] - w[0] + 1 > kGsAct) return TOWR_OK;
+        }
+      }
+    }
+  std::vector<int> sdec_ee((size_t)L.n, -1), sdec_j((size_t)L.n, 0);
+  for (int ee = 0; ee < E; ++ee) {
+    const SchedInfo& si = L.sched[ee];
+    if (si.col0 < 0) return TOWR_OK;
+    for (int j = 0; j < si.n_phases - 1; ++j) { sdec_ee[si.col0 + j] = ee; sdec_j[si.col0 + j] = j; }
+  }
+  for (int cls = 0; cls < GS_COUNT; ++cls) {
+    std::string why;
+    if (!build_gstream_class(L, cls, bdec, pdec, sdec_ee, sdec_j, why) && why.rfind("internal", 0) == 0) {
+      err = why;
+      return TOWR_ERR_INVALID;
+    }
+  }
+  (void)err;
   return TOWR_OK;
 }
 
@@ -701,7 +853,7 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
         auto ts = dts_of(c.T, c.dt);
         for (int k = 0; k < (int)ts.size(); ++k, ++inst)
           for (int g = 0; g < 2 + E; ++g) {
-            if (g == 1 && (L.rotvec || split_base_ang(L.gait))) {   // base-angular block: one item per Euler axis / rotation-vector component
+            if (g == 1 && L.rotvec) {   // RotVec base-angular block: one item per rotation-vector component
               for (int ax = 0; ax < 3; ++ax) add(IT_DYN, g, 0, k, row + 6 * k, ts[k], 0, 1 + ax, 0.0);
             } else {
               add(IT_DYN, g, 0, k, row + 6 * k, ts[k], 0, 0, 0.0);
@@ -994,7 +1146,7 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
             // the endeffector groups after the three axis groups (one wave may hold the last axis and
             // the first endeffectors); two tiles with whole waves per group measured slower (0.078 vs
             // 0.063 ms: twice the x staging and block overhead)
-            if (type == IT_DYN && !L.gait && it.group >= 2 && (L.rotvec || split_base_ang(false)))
+            if (type == IT_DYN && !L.gait && it.group >= 2 && L.rotvec)
               lane = 64 + 3 * (b - a) + (it.group - 2) * (b - a) + (k - a);
             if (lane < 0 || lane >= sp.block || lanes[lane].type != IT_NONE) { err = "internal: lane assignment"; return TOWR_ERR_INVALID; }
             lanes[lane] = it;
@@ -1185,6 +1337,7 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
       L.type_bytes[t] = 8 * (nv + nr + nx);
     }
     if (int rc = build_fstream(L, err)) return rc;
+    if (int rc = build_gstream(L, err)) return rc;
     {   // the merged small-kind launch: union of their x columns
       int64_t nv = 0, nr = 0, nx = 0;
       std::vector<uint8_t> used((size_t)L.n, 0);
@@ -1217,7 +1370,7 @@ TypeSpec type_spec(int type, int n_ee, bool gait, bool rotvec) {
   const int blk = tile_block(type, gait);
   switch (type) {
     case IT_DYN:   // waves: g0 | g1 | ee, ee (gait: rows); per-axis base-angular items: 3 g1 lanes per instant
-      if (rotvec || split_base_ang(gait))
+      if (rotvec)
         return {blk, std::max(1, gait ? std::min(64 / 3, 64 / E) : std::min(64, (blk - 64) / (3 + E)))};
       return {blk, std::max(1, std::min(64, gait ? 64 / E : 128 / E))};
     case IT_ROM: return {blk, gait ? 128 : 64};                                         // waves: g0 | g1 | g2 (gait: rows, 2 halves)

@@ -739,8 +739,9 @@ const void* kernel_for(int type, bool gait, bool rotvec) {
   if (gait) return rotvec ? kernel_for_mode<true, true>(type) : kernel_for_mode<true, false>(type);
   return rotvec ? kernel_for_mode<false, true>(type) : kernel_for_mode<false, false>(type);
 }
-const void* kernel_for_class(int lc, bool gait, bool rotvec, bool fstream = false) {
+const void* kernel_for_class(int lc, bool gait, bool rotvec, bool fstream = false, int gcls = -1) {
   if (lc == LC_FDISC && gait && fstream) return fs_stream_kernel();   // the stream kernel (B); A: fs_inst_kernel()
+  if (gcls >= 0) return gs_stream_kernel(gcls);                       // the composer; the record kernel: gs_rec_kernel
   if (lc == LC_MISC) return gait ? reinterpret_cast<const void*>(&towr_misc_kernel<true>) : reinterpret_cast<const void*>(&towr_misc_kernel<false>);
   return kernel_for(class_type(lc), gait, rotvec);
 }
@@ -785,6 +786,19 @@ struct towr_gpu_handle_s {
   int32_t* d_fs_irow = nullptr;
   double* d_fsrec = nullptr;   // per-problem instant records of the streaming path (scratch, grown on demand)
   int64_t fsrec_cap = 0;       // problems it holds
+  GsGeo* d_gs_geo = nullptr;   // streaming RangeOfMotion / Dynamic tables (layout.h GsGeo)
+  int32_t* d_gs_tmpl = nullptr;
+  uint8_t* d_gs_pcode = nullptr;
+  GsBlock* d_gs_blk[GS_COUNT] = {};
+  GsInst* d_gs_inst[GS_COUNT] = {};
+  double* d_gsrec[GS_COUNT] = {};   // their records (scratch, grown on demand)
+  int64_t gsrec_cap[GS_COUNT] = {};
+  // The scratch above (and the soft child's g / values, d_sg / d_sv) is shared by every call on the
+  // handle: a call on another stream than the previous one waits for the previous call's work (this
+  // event), and growing a buffer waits for it on the host before the old one is freed.
+  hipEvent_t scr_ev = nullptr;
+  hipStream_t scr_stream = nullptr;
+  bool scr_used = false;
   // fusion groups (TOWR_GPU_FUSE, see towr_step_kernel): classes that run in one launch
   struct FuseGroup {
     uint32_t mask = 0;        // bit lc: launch class lc belongs to the group
@@ -870,6 +884,31 @@ int bind(towr_gpu_handle h) {
   return TOWR_OK;
 }
 
+// Handle scratch ordering (see towr_gpu_handle_s::scr_ev): acquire before a call's first use on stream s,
+// release after its last; grow() reallocates a per-problem buffer once every earlier use has finished.
+int scratch_acquire(towr_gpu_handle h, hipStream_t s) {
+  if (h->scr_used && h->scr_stream != s) HIPCHK(h, hipStreamWaitEvent(s, h->scr_ev, 0));
+  return TOWR_OK;
+}
+int scratch_release(towr_gpu_handle h, hipStream_t s) {
+  HIPCHK(h, hipEventRecord(h->scr_ev, s));
+  h->scr_stream = s;
+  h->scr_used = true;
+  return TOWR_OK;
+}
+int scratch_grow(towr_gpu_handle h, double** buf, int64_t* cap, int64_t problems, int64_t doubles_per_problem) {
+  if (*cap >= problems) return TOWR_OK;
+  if (*buf) {
+    if (h->scr_used) HIPCHK(h, hipEventSynchronize(h->scr_ev));
+    (void)hipFree(*buf);
+    *buf = nullptr;
+    *cap = 0;
+  }
+  HIPCHK(h, hipMalloc(buf, sizeof(double) * (size_t)problems * (size_t)std::max<int64_t>(1, doubles_per_problem)));
+  *cap = problems;
+  return TOWR_OK;
+}
+
 // The PhaseSpline tables a tile block stages in LDS under phase-duration optimisation, as one blob of
 // 16-byte aligned sections [SplineMeta | SchedInfo | PolyPhase | pact | PhaseCol] (~18 KB for ANYmal):
 // the device-side duration searches (phase_spline_locate, sched_jac) and the full-pattern window
@@ -905,16 +944,24 @@ std::vector<uint4> gait_blob(const Layout& L) {
 // LDS of a launch class: [tile region(s) | x + zero slot | node table | GAIT: PhaseSpline tables]
 // (the streaming ForceConstraintDiscretized path: its per-instant records and row template first)
 bool fstream_class(const Layout& L, int lc) { return lc == LC_FDISC && L.fstream; }
+int gstream_cls(const Layout& L, int lc) {   // the streaming class of launch class lc, or -1
+  if (lc == LC_ROM && L.gstream[GS_ROM]) return GS_ROM;
+  if (lc == LC_DYN && L.gstream[GS_DYN]) return GS_DYN;
+  return -1;
+}
 size_t lds_region(const Layout& L, int lc) {
   if (fstream_class(L, lc)) return fs_region(L);
+  if (gstream_cls(L, lc) >= 0) return gs_stream_lds(L, gstream_cls(L, lc)) / sizeof(double);
   return lc == LC_MISC ? (size_t)((L.misc_region + 1) & ~1) : (size_t)L.type_lds[class_type(lc)];
 }
 int class_block(const Layout& L, int lc) {
   if (fstream_class(L, lc)) return kFsBlock;
+  if (gstream_cls(L, lc) >= 0) return kGsBlock;
   return lc == LC_MISC ? 64 * kMiscWaves : L.type_block[class_type(lc)];
 }
 size_t lds_bytes(const Layout& L, int lc) {
   if (fstream_class(L, lc)) return sizeof(double) * fs_region(L);   // the stream kernel (B) stages no x
+  if (gstream_cls(L, lc) >= 0) return gs_stream_lds(L, gstream_cls(L, lc));
   size_t d = lds_region(L, lc);
   d += (size_t)((L.n + 2) & ~1);                                                                  // x + zero slot
   if (lc == LC_MISC || stages_nodes(class_type(lc), L.gait)) d += (L.nodecol.size() + 3) / 4 * 2;  // node table (16-B units)
@@ -925,6 +972,7 @@ size_t lds_bytes(const Layout& L, int lc) {
 int class_units(const Layout& L, int lc) {   // tiles (or misc groups, or FsBlocks) per problem
   if (lc == LC_MISC) return (int)(L.misc_tiles.size() / kMiscWaves);
   if (fstream_class(L, lc)) return (int)L.fs_blocks.size();
+  if (gstream_cls(L, lc) >= 0) return (int)L.gs_blocks[gstream_cls(L, lc)].size();
   const int t = class_type(lc);
   return L.type_tile0[t + 1] - L.type_tile0[t];
 }
@@ -1014,6 +1062,7 @@ void fill_common(towr_gpu_handle h, KParams& P, int B, const double* X, int64_t 
   P.gt_ntime = gt.n_time;
   P.fsb = h->d_fsb; P.fs_t = h->d_fs_t; P.fs_tmpl = h->d_fs_tmpl; P.fs_ws = h->d_fs_ws;
   P.fs_iee = h->d_fs_iee; P.fs_irow = h->d_fs_irow;
+  P.gs_geo = h->d_gs_geo; P.gs_tmpl = h->d_gs_tmpl; P.gs_pcode = h->d_gs_pcode;
 }
 
 int launch_fused(towr_gpu_handle h, const towr_gpu_handle_s::FuseGroup& fg, int B, const double* X, int64_t ldx, double* G,
@@ -1039,11 +1088,7 @@ int launch_fstream(towr_gpu_handle h, KParams& P, hipStream_t st) {
   const int B = P.B;
   const int32_t ni = (int32_t)L.fs_t.size();
   const int64_t ldr = fs_record_doubles() * ni;
-  if (h->fsrec_cap < B) {
-    if (h->d_fsrec) { (void)hipFree(h->d_fsrec); h->d_fsrec = nullptr; h->fsrec_cap = 0; }
-    HIPCHK(h, hipMalloc(&h->d_fsrec, sizeof(double) * (size_t)B * ldr));
-    h->fsrec_cap = B;
-  }
+  if (int rc = scratch_grow(h, &h->d_fsrec, &h->fsrec_cap, B, ldr)) return rc;
   P.lds_x_off = 0;
   double* rec = h->d_fsrec;
   int64_t ldr_a = ldr;
@@ -1059,9 +1104,46 @@ int launch_fstream(towr_gpu_handle h, KParams& P, hipStream_t st) {
   return TOWR_OK;
 }
 
+// The streaming RangeOfMotion / Dynamic path of class cls: record kernel into the handle's scratch, then
+// the composer over the class's GsBlocks. P comes from fill_common with ntiles = GsBlocks.
+int launch_gstream(towr_gpu_handle h, KParams& P, int cls, hipStream_t st) {
+  const Layout& L = h->L;
+  const int B = P.B;
+  const int32_t ni = (int32_t)L.gs_inst[cls].size();
+  const int64_t ldr = gs_record_doubles(L, cls);
+  if (int rc = scratch_grow(h, &h->d_gsrec[cls], &h->gsrec_cap[cls], B, ldr)) return rc;
+  P.gs_blk = h->d_gs_blk[cls];
+  P.gs_inst = h->d_gs_inst[cls];
+  double* rec = h->d_gsrec[cls];
+  int64_t ldr_a = ldr;
+  int32_t ni_a = ni;
+  void* aa[] = {&P, &rec, &ldr_a, &ni_a};
+  HIPCHK(h, hipLaunchKernel(gs_rec_kernel(cls, L.rotvec), dim3((unsigned)B), dim3(gs_rec_block()), aa, fs_inst_lds_bytes(L), st));
+  const int64_t total = (int64_t)B * P.ntiles;
+  const int64_t grid = ((total + 7) / 8) * 8;
+  if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
+  const double* crec = rec;
+  void* ab[] = {&P, const_cast<double**>(&crec), &ldr_a, &ni_a};
+  HIPCHK(h, hipLaunchKernel(gs_stream_kernel(cls), dim3((unsigned)grid), dim3(kGsBlock), ab, gs_stream_lds(L, cls), st));
+  return TOWR_OK;
+}
+
+bool uses_scratch(const Layout& L) { return L.fstream || L.gstream[GS_ROM] || L.gstream[GS_DYN]; }
+
+int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, int64_t ldg, double* V, int64_t ldv,
+                   int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem, int only_class);
 int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, int64_t ldg, double* V, int64_t ldv,
            int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem, int only_class) {
   if (B <= 0) return TOWR_OK;
+  const bool scr = uses_scratch(h->L);
+  if (scr)
+    if (int rc = scratch_acquire(h, s)) return rc;
+  if (int rc = launch_classes(h, B, X, ldx, G, ldg, V, ldv, want_g, want_jac, s, terrains, per_problem, only_class)) return rc;
+  return scr ? scratch_release(h, s) : TOWR_OK;
+}
+
+int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, int64_t ldg, double* V, int64_t ldv,
+                   int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem, int only_class) {
   const Layout& L = h->L;
   uint32_t fused_mask = 0;
   if (only_class < 0)
@@ -1091,6 +1173,10 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
       if (int rc = launch_fstream(h, P, st)) return rc;
       continue;
     }
+    if (gstream_cls(L, lc) >= 0) {
+      if (int rc = launch_gstream(h, P, gstream_cls(L, lc), st)) return rc;
+      continue;
+    }
     if (lc == LC_MISC) {
       P.tile0 = 0;
       P.misc_tiles = h->d_misc; P.misc_lds = h->d_misc_lds;
@@ -1110,9 +1196,9 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
     if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
     const int block = class_block(L, lc);
     void* args[] = {&P};
-    HIPCHK(h, hipLaunchKernel(kernel_for_class(lc, L.gait, L.rotvec, L.fstream), dim3((unsigned)grid), dim3((unsigned)block), args,
+    HIPCHK(h, hipLaunchKernel(kernel_for_class(lc, L.gait, L.rotvec, L.fstream, gstream_cls(L, lc)), dim3((unsigned)grid), dim3((unsigned)block), args,
                               lds_bytes(L, lc), st));
-    if (lc == LC_DYN && L.gait)   // its base-angular block, into the rows the tile kernel zero-filled
+    if (lc == LC_DYN && L.gait)   // (tile path) its base-angular block, into the rows the tile kernel zero-filled
       HIPCHK(h, hipLaunchKernel(dyn_g1_kernel_for(L.rotvec), dim3((unsigned)grid), dim3(64), args,
                                 sizeof(double) * (size_t)((L.n + 2) & ~1), st));
   }
@@ -1136,18 +1222,9 @@ int launch_soft(towr_gpu_handle h, int B, const double* X, int64_t ldx, bool gra
                 const towr_terrain_t* terrains, int per_problem, KParams& P) {
   towr_gpu_handle c = h->soft;
   const int64_t ms = std::max(1, c->L.m), nzs = std::max<int64_t>(1, c->L.nnz);
-  if (h->soft_cap_g < B) {
-    if (h->d_sg) (void)hipFree(h->d_sg);
-    h->d_sg = nullptr; h->soft_cap_g = 0;
-    HIPCHK(h, hipMalloc(&h->d_sg, sizeof(double) * (size_t)B * ms));
-    h->soft_cap_g = B;
-  }
-  if (grad && h->soft_cap_v < B) {
-    if (h->d_sv) (void)hipFree(h->d_sv);
-    h->d_sv = nullptr; h->soft_cap_v = 0;
-    HIPCHK(h, hipMalloc(&h->d_sv, sizeof(double) * (size_t)B * nzs));
-    h->soft_cap_v = B;
-  }
+  if (int rc = scratch_grow(h, &h->d_sg, &h->soft_cap_g, B, ms)) return rc;
+  if (grad)
+    if (int rc = scratch_grow(h, &h->d_sv, &h->soft_cap_v, B, nzs)) return rc;
   if (int rc = launch(c, B, X, ldx, h->d_sg, ms, grad ? h->d_sv : nullptr, nzs, 1, grad ? 1 : 0, s, terrains, per_problem, -1))
     return fail(h, rc, "SoftConstraint sets: " + c->err);
   P.sG = h->d_sg; P.s_ldg = ms; P.sV = h->d_sv; P.s_ldv = nzs;
@@ -1160,8 +1237,10 @@ int launch_cost(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* 
   if (B <= 0) return TOWR_OK;
   const Layout& L = h->L;
   KParams P{};
-  if (h->soft)
+  if (h->soft) {
+    if (int rc = scratch_acquire(h, s)) return rc;
     if (int rc = launch_soft(h, B, X, ldx, GR != nullptr, s, terrains, per_problem, P)) return rc;
+  }
   P.X = X; P.ldx = ldx;
   P.nodecol = h->d_nodecol; P.spl = h->d_spl; P.dur = h->d_dur;
   P.sg = h->sg; P.n_spl = (int32_t)L.spl.size();
@@ -1176,7 +1255,7 @@ int launch_cost(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* 
   void* args[] = {&P};
   HIPCHK(h, hipLaunchKernel(cost_kernel_for(L.gait, GR != nullptr, L.rotvec), dim3((unsigned)B), dim3(kCostBlock), args,
                             cost_lds_bytes(L), s));
-  return TOWR_OK;
+  return h->soft ? scratch_release(h, s) : TOWR_OK;
 }
 
 // SaveTrajectoryToCSV's sample times: t = 0, dt, ... accumulated while t <= T + 1e-9, with
@@ -1456,7 +1535,7 @@ int towr_gpu_debug_occupancy(towr_gpu_handle h, int32_t lc) {
   if (lc < 0 || lc >= LC_COUNT || class_units(L, lc) == 0) return -1;
   const int block = class_block(L, lc);
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel_for_class(lc, L.gait, L.rotvec, L.fstream), block, lds_bytes(L, lc)) != hipSuccess) return -2;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel_for_class(lc, L.gait, L.rotvec, L.fstream, gstream_cls(L, lc)), block, lds_bytes(L, lc)) != hipSuccess) return -2;
   return n * 1000 + (int)(lds_bytes(L, lc) / 1024);
 }
 int towr_gpu_debug_set_timing_buffer(void* p) {
@@ -1500,9 +1579,10 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
       const int rows = C.cons[k].rows;
       const towr_data_t* bd = find_data(n_data, data, TOWR_DATA_SOFT_BOUNDS, h->L.soft[k].first);
       if (!bd || (rows > 0 && !bd->data) || bd->count != 2 * (int64_t)rows) {
-        towr_gpu_destroy(h);
-        return fail(nullptr, TOWR_ERR_INVALID, "SoftConstraint term " + std::to_string(h->L.soft[k].first) +
-                                                   ": bounds (side data TOWR_DATA_SOFT_BOUNDS, lower then upper) missing or not 2 x the set's rows");
+        const std::string msg = "SoftConstraint term " + std::to_string(h->L.soft[k].first) +
+                                ": bounds (side data TOWR_DATA_SOFT_BOUNDS, lower then upper) missing or not 2 x the set's rows";
+        towr_gpu_destroy(h);   // the message is built first: destroy frees h
+        return fail(nullptr, TOWR_ERR_INVALID, msg);
       }
       for (int r = 0; r < rows; ++r) h->soft_b.push_back((bd->data[rows + r] + bd->data[r]) / 2.);
     }
@@ -1542,8 +1622,12 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
       (r = upload(h, &h->d_citems, L.cost_items)) || (r = upload(h, &h->d_cq, L.cost_q)) || (r = upload(h, &h->d_gtab, gait_blob(L))) ||
       (r = upload(h, &h->d_idir, L.idirect)) || (r = upload(h, &h->d_fsb, L.fs_blocks)) || (r = upload(h, &h->d_fs_t, L.fs_t)) ||
       (r = upload(h, &h->d_fs_tmpl, L.fs_tmpl)) || (r = upload(h, &h->d_fs_ws, L.fs_ws)) ||
-      (r = upload(h, &h->d_fs_iee, L.fs_iee)) || (r = upload(h, &h->d_fs_irow, L.fs_irow)))
+      (r = upload(h, &h->d_fs_iee, L.fs_iee)) || (r = upload(h, &h->d_fs_irow, L.fs_irow)) ||
+      (r = upload(h, &h->d_gs_geo, L.gs_geo)) || (r = upload(h, &h->d_gs_tmpl, L.gs_tmpl)) || (r = upload(h, &h->d_gs_pcode, L.gs_pcode)) ||
+      (r = upload(h, &h->d_gs_blk[GS_ROM], L.gs_blocks[GS_ROM])) || (r = upload(h, &h->d_gs_blk[GS_DYN], L.gs_blocks[GS_DYN])) ||
+      (r = upload(h, &h->d_gs_inst[GS_ROM], L.gs_inst[GS_ROM])) || (r = upload(h, &h->d_gs_inst[GS_DYN], L.gs_inst[GS_DYN])))
     return bail(r);
+  if (hipEventCreateWithFlags(&h->scr_ev, hipEventDisableTiming) != hipSuccess) { h->err = "hipEventCreate failed"; return bail(TOWR_ERR_HIP); }
   {   // trajectory export: phase durations of the description (fixed gait), counts, contact at start
     const towr_problem_desc_t& d = L.desc;
     std::vector<double> pd((size_t)TOWR_MAX_EE * TOWR_MAX_PHASES, 0.0);
@@ -1622,16 +1706,19 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
     if (class_units(L, lc) == 0) continue;
     const size_t lds = lds_bytes(L, lc);
     if (lds > 160 * 1024) { h->err = "tile too large for LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
-    if (lds > 64 * 1024 && hipFuncSetAttribute(kernel_for_class(lc, L.gait, L.rotvec, L.fstream), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+    if (lds > 64 * 1024 && hipFuncSetAttribute(kernel_for_class(lc, L.gait, L.rotvec, L.fstream, gstream_cls(L, lc)), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
       h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
     }
   }
-  if (L.fstream) {
+  if (L.fstream || L.gstream[GS_ROM] || L.gstream[GS_DYN]) {   // the record kernels share fs_inst_lds_bytes' layout
     const size_t lds = fs_inst_lds_bytes(L);
     if (lds > 160 * 1024) { h->err = "problem too large for the streaming instant kernel's LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
-    if (lds > 64 * 1024 && hipFuncSetAttribute(fs_inst_kernel(),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
-      h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
+    if (lds > 64 * 1024) {
+      const void* ks[] = {fs_inst_kernel(), gs_rec_kernel(GS_ROM, L.rotvec), gs_rec_kernel(GS_DYN, L.rotvec)};
+      for (const void* k : ks)
+        if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+          h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
+        }
     }
   }
   {
@@ -1654,7 +1741,8 @@ int towr_gpu_destroy(towr_gpu_handle h) {
                  h->d_bterrain, h->d_x, h->d_g, h->d_v, h->d_f, h->d_grad,
                  h->d_traj_pd, h->d_traj_n, h->d_traj_c0, h->d_traj_t, h->d_fsb, h->d_fs_t, h->d_fs_tmpl, h->d_fs_ws,
                  h->d_fs_iee, h->d_fs_irow, h->d_fsrec, h->d_lin, h->d_soft_b, h->d_soft_rp, h->d_soft_col, h->d_sg, h->d_sv,
-                 h->single.d_units};
+                 h->single.d_units, h->d_gs_geo, h->d_gs_tmpl, h->d_gs_pcode, h->d_gs_blk[0], h->d_gs_blk[1], h->d_gs_inst[0],
+                 h->d_gs_inst[1], h->d_gsrec[0], h->d_gsrec[1]};
   if (h->device >= 0) for (void* p : dev) if (p) (void)hipFree(p);
   void* host[] = {h->h_x, h->h_g, h->h_v};
   for (void* p : host) if (p) (void)hipHostFree(p);
@@ -1668,6 +1756,7 @@ int towr_gpu_destroy(towr_gpu_handle h) {
     if (h->join[i]) (void)hipEventDestroy(h->join[i]);
   }
   if (h->fork) (void)hipEventDestroy(h->fork);
+  if (h->scr_ev) (void)hipEventDestroy(h->scr_ev);
   if (h->soft) towr_gpu_destroy(h->soft);
   delete h;
   return TOWR_OK;
@@ -1886,6 +1975,11 @@ int towr_gpu_step_launches(towr_gpu_handle h, int32_t* kernels, int32_t cap) {
       ++cnt;
     }
   return cnt;
+}
+int towr_gpu_kernel_path(towr_gpu_handle h, int32_t kernel) {
+  if (!h || kernel < 0 || kernel >= LC_COUNT) return fail(h, TOWR_ERR_INVALID, "bad kernel index");
+  if (class_units(h->L, kernel) == 0) return -1;
+  return fstream_class(h->L, kernel) || gstream_cls(h->L, kernel) >= 0 ? 1 : 0;
 }
 int towr_gpu_eval_batch_device_kernel(towr_gpu_handle h, int32_t kernel, int32_t B, const double* X, int64_t ldx,
                                       double* G, int64_t ldg, double* V, int64_t ldv, void* stream) {

@@ -97,6 +97,8 @@ class NlpCallbacks {
  public:
   // The g / values cache lives in page-locked memory, so every fused evaluation DMAs straight into it
   // (a layout-only engine refuses the registration; the cache then stays pageable).
+  // Lifetime: the Engine must outlive these callbacks (declare the Engine first): the destructor
+  // unregisters the cache through the Engine's handle.
   explicit NlpCallbacks(Engine& e) : e_(e), g_(e.GetNumberOfConstraints()), v_(e.GetNumberOfJacobianNonzeros()) {
     pin_g_ = !g_.empty() && e_.RegisterHost(g_.data(), g_.size() * sizeof(double)) == TOWR_OK;
     pin_v_ = !v_.empty() && e_.RegisterHost(v_.data(), v_.size() * sizeof(double)) == TOWR_OK;

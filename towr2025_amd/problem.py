@@ -277,6 +277,13 @@ class TowrGpuProblem:
                 out.append((k, name.value.decode(), nt.value, by.value))
         return out
 
+    def kernel_path(self, kernel: int) -> int:
+        """Implementation of launch class `kernel` (0..4): 0 tile kernel, 1 record + stream kernels, -1 unused."""
+        rc = self._lib.towr_gpu_kernel_path(self._h, kernel)
+        if rc < -1:
+            self._check(rc)
+        return rc
+
     def eval_batch_device_kernel(self, kernel, X, G, V, stream):
         """Launch one kernel only: a launch class or a fusion group (roofline accounting)."""
         self._check_batch(X, G, V)
