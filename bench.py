@@ -75,13 +75,14 @@ def shard_first_id(rank, B):
     return rank * B
 
 
-def max_over_ranks(wall, kern_ms, dev, distributed):
-    """Timing reduction: the slowest rank defines the job time."""
+def max_over_ranks(wall, kern_ms, distributed):
+    """Timing reduction: the slowest rank defines the job time (gloo, host tensors: the data path has no
+    collective, so RCCL is never initialised)."""
     if not distributed:
         return wall, kern_ms
     import torch
     import torch.distributed as dist
-    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([wall, kern_ms], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t[0]), float(t[1])
 
@@ -172,6 +173,26 @@ def single_call(prob, X, reps=300, register=True):
             "us_p90": float(np.percentile(ts, 90)), "calls": reps, "registered_outputs": register}
 
 
+def single_leg(desc, name, note, device, reps=300, cpu=True, sigma=0.02):
+    """B = 1 latency of one BASELINE configuration (single_call, registered outputs) beside the oracle's
+    one-thread time per eval_g + eval_jac_g on the same x vectors."""
+    from towr2025_amd import TowrGpuProblem
+    p = TowrGpuProblem(desc, device=device)
+    x0 = p.initial_x()
+    rng = np.random.default_rng(SEED)
+    X = np.stack([x0 + sigma * np.abs(x0).clip(0.1, 1.0) * rng.standard_normal(p.n) for _ in range(N_X)])
+    out = single_call(p, X, reps=reps)
+    out.update({"config": name, "n": p.n, "m": p.m, "nnz": p.nnz, "note": note})
+    if cpu:
+        from oracle import oracle as O
+        O.bench(desc, 1, 2, X, native=True)
+        secs, done = O.bench(desc, 1, 10, X, native=True)
+        out["cpu_one_thread_us"] = secs / done * 1e6
+        out["speedup_vs_cpu_one_thread"] = out["cpu_one_thread_us"] / out["us_median"]
+    p.close()
+    return out
+
+
 def host_batch(prob, Xh, reps=3):
     """PCIe-inclusive rate of towr_gpu_eval_batch (host X, G, V; the caller's G / V reused across
     calls): through the pinned staging, and with G / V registered (in-place DMA)."""
@@ -221,8 +242,8 @@ def main():
     # under torch.distributed.run (RANK set) the process group is used at every world size, so the
     # launcher path the multi-GPU runs take is the one a 1-GPU run under the launcher exercises
     distributed = "RANK" in os.environ and "MASTER_ADDR" in os.environ
-    if distributed:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if distributed:   # timing barrier + max-over-ranks only: gloo (the problem shards never communicate)
+        dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -271,7 +292,7 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     kern_ms = e0.elapsed_time(e1) / args.steps
-    wall, kern_ms = max_over_ranks(wall, kern_ms, dev, distributed)
+    wall, kern_ms = max_over_ranks(wall, kern_ms, distributed)
 
     calls = B * world * args.steps
     value = calls / wall
@@ -418,6 +439,17 @@ def main():
         out["cpu_baseline"] = cpu_baseline(desc, Xh[0, :8], args.cpu_seconds)
         if "single_call" in out:
             out["single_call"]["cpu_one_thread_us"] = 1e6 / out["cpu_baseline"]["one_thread"]
+    if rank == 0 and not args.no_host:
+        # B = 1 latency of the other single-problem configurations: BASELINE configs[1] (biped walk 2 s)
+        # and configs[3] (ANYmal on stairs with phase-duration optimisation, the fork's hopper driver's
+        # formulation class, hopper_example.cc:145-180), each beside the oracle's one-thread time
+        cpu = world == 1 and not args.no_cpu
+        out["single_call_biped"] = single_leg(F.biped_walk().to_desc(), "BASELINE configs[1]: biped walk 2 s",
+                                              "B = 1 through host pointers, registered outputs", local, cpu=cpu)
+        out["single_call_gait"] = single_leg(
+            F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.StairsID), optimize_timings=True).to_desc(),
+            "BASELINE configs[3]: ANYmal on stairs, phase-duration optimisation",
+            "B = 1 through host pointers, registered outputs", local, cpu=cpu)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if distributed:

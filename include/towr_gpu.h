@@ -279,12 +279,27 @@ int towr_gpu_sample_trajectory_batch_device(towr_gpu_handle h, int32_t B, const 
 
 /* ---- batched evaluation over independent problems that share the layout ---------------------- */
 /* Per-problem terrain parameters (the only per-instance input to g/J besides x). `terrains` is a
- * host array of B entries; all entries must keep the Jacobian pattern identical.
+ * host array of B entries of the description terrain's curvature class (Gap or not; see
+ * towr_gpu_pattern_outside for what curved terrain does to the pattern).
  * Once set, every BATCH entry point (eval_batch, eval_batch_device[_kernel], eval_cost_batch_device)
  * uses terrain b for problem b and requires exactly B problems (else TOWR_ERR_INVALID); B = 0 clears
  * the set. The single-problem entry points (eval_g, eval_jac_values, eval_g_jac, eval_f,
  * eval_grad_f, sample_trajectory*) always use the description's terrain.                         */
 int towr_gpu_set_batch_terrain(towr_gpu_handle h, int32_t B, const towr_terrain_t* terrains);
+
+/* Frozen-pattern check (curved terrain). On Gap terrain ForceConstraintDiscretized and
+ * TorqueConstraintDiscretized add a row's motion block only where its scale is non-zero
+ * (force_constraint_discretized.cc:58, torque_constraint_discretized.cc:57), so the reference's
+ * Jacobian pattern moves with x; IPOPT's structure, and this engine's CSR, are fixed at x0 (the
+ * description's). These return how many entries the reference's Jacobian at x holds OUTSIDE that
+ * frozen pattern (0 on terrains without curvature): entries the frozen structure cannot deliver. The
+ * values on the frozen pattern are always the reference's, or 0.0 where the reference has no entry.
+ * Evaluated on the host with the reference's own operations (the predicate is a floating-point tie),
+ * so both are synchronous; the batch form copies X (device) to the host, uses the batch terrains like
+ * eval_batch_device, and writes counts[B] in host memory. Layout-only handles answer the single form. */
+int towr_gpu_pattern_outside(towr_gpu_handle h, const double* x, int64_t* count);
+int towr_gpu_pattern_outside_batch_device(towr_gpu_handle h, int32_t B, const double* X, int64_t ldx,
+                                          int32_t* counts, void* stream);
 
 /* Device-resident batch: X[b*ldx + j], G[b*ldg + i], V[b*ldv + k] are DEVICE pointers (HBM);
  * `stream` is the hipStream_t to launch on (NULL = HIP's default stream, as in the HIP API).

@@ -33,7 +33,7 @@ def _worker(rank, world, port, outdir):
     X, terrains = bench.make_batch(prob, B, first_id=first)
     np.save(os.path.join(outdir, f"x{rank}.npy"), X)
     np.save(os.path.join(outdir, f"t{rank}.npy"), np.array([[t.id, *list(t.p)] for t in terrains]))
-    wall, kern = bench.max_over_ranks(float(rank + 1), 10.0 * (rank + 1), torch.device("cpu"), world > 1)
+    wall, kern = bench.max_over_ranks(float(rank + 1), 10.0 * (rank + 1), world > 1)
     np.save(os.path.join(outdir, f"r{rank}.npy"), np.array([wall, kern]))
     dist.barrier()
     dist.destroy_process_group()

@@ -46,7 +46,7 @@ def _worker(rank, world, port, outdir):
     mine = _device_eval(bench.shard_first_id(rank, B), B)
     parts = [torch.zeros_like(mine) for _ in range(world)]
     dist.all_gather(parts, mine)
-    wall, _ = bench.max_over_ranks(float(rank + 1), 0.0, torch.device("cpu"), True)
+    wall, _ = bench.max_over_ranks(float(rank + 1), 0.0, True)
     if rank == 0:
         np.save(os.path.join(outdir, "gathered.npy"), torch.cat(parts).numpy())
         np.save(os.path.join(outdir, "wall.npy"), np.array([wall]))

@@ -144,6 +144,8 @@ SYMBOLS = {
     "towr_gpu_num_kernels": (C.c_int, []),
     "towr_gpu_step_launches": (C.c_int, [_HANDLE, _IP, C.c_int32]),
     "towr_gpu_kernel_path": (C.c_int, [_HANDLE, C.c_int32]),
+    "towr_gpu_pattern_outside": (C.c_int, [_HANDLE, _DP, _LP]),
+    "towr_gpu_pattern_outside_batch_device": (C.c_int, [_HANDLE, C.c_int32, C.c_void_p, C.c_int64, _IP, C.c_void_p]),
     "towr_gpu_register_host": (C.c_int, [_HANDLE, C.c_void_p, C.c_int64]),
     "towr_gpu_unregister_host": (C.c_int, [_HANDLE, C.c_void_p]),
     "towr_gpu_set_tiles_per_block": (C.c_int, [_HANDLE, C.c_int32]),

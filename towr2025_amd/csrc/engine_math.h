@@ -21,9 +21,6 @@
 #include "../../include/towr_gpu.h"
 
 #define TG_HD __host__ __device__ __forceinline__
-#ifndef TOWR_DYN_LINROW   // gait Dynamic: linear-row lanes evaluate the force spline only (0 = every spline, A/B)
-#define TOWR_DYN_LINROW 1
-#endif
 
 namespace tg {
 
@@ -419,6 +416,24 @@ TG_HD void spline_eval(const Ctx& c, int s, double t, SplinePt& o) {
   }
   poly_state(c, s, o.poly, o.T, o.tl, o);
 #endif
+}
+
+// spline_eval with the reference's operations everywhere (Spline::GetPoint: the polynomial's coefficients and
+// std::pow-rounded powers, poly_state), also on the device for fixed durations, where spline_eval uses the
+// precomputed basis instead: for predicates on spline values that must resolve exactly as in the source
+TG_HD void spline_eval_ref(const Ctx& c, int s, double t, SplinePt& o) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (!(c.gait && c.spl[s].ee >= 0)) {
+    const size_t blk = (size_t)s * c.sg.ng + (c.row >> 5);
+    const double* D = c.sg.d + blk * (kSegDoubles * kSegGroup) + (c.row & 31);
+    const int32_t* I = c.sg.i + blk * (kSegInts * kSegGroup) + (c.row & 31);
+    o.dyn = false; o.H = nullptr;
+    o.poly = I[0]; o.tl = D[0]; o.T = D[kSegGroup];
+    poly_state(c, s, o.poly, o.T, o.tl, o);
+    return;
+  }
+#endif
+  spline_eval(c, s, t, o);
 }
 
 // Hermite basis of a spline point for derivative d (precomputed on the device, evaluated on the host)
@@ -973,6 +988,7 @@ TG_HD void base_rot(const Ctx& c, const SplinePt& A, double R[3][3]) {
 // terrain (towr/src/terrain/height_map.cc, height_map_examples.cc)
 // ----------------------------------------------------------------------------------------------
 TG_HD double ter_h(const towr_terrain_t& T, double x, double y) {
+#pragma clang fp contract(off)
   const double* p = T.p;
   switch (T.id) {
     case TOWR_TERRAIN_FLAT: return p[0];
@@ -1017,6 +1033,7 @@ TG_HD double ter_h(const towr_terrain_t& T, double x, double y) {
   return 0.0;
 }
 TG_HD double ter_dh(const towr_terrain_t& T, int dim, double x, double y) {
+#pragma clang fp contract(off)   // the reference's operations: curved-terrain predicates depend on exact zeros
   const double* p = T.p;
   if (dim == X) {
     switch (T.id) {
@@ -1071,28 +1088,35 @@ TG_HD void ter_basis(const towr_terrain_t& T, int basis, double x, double y, int
     v[2] = req ? ter_dh(T, Y, x, y) : ter_d2h(T, Y, deriv, x, y);
   }
 }
-// Eigen normalized(): v / sqrt(|v|^2) if |v|^2 > 0
+// Eigen normalized(): v / sqrt(|v|^2) if |v|^2 > 0. REF: the reference's own operations on the device too
+// (three divisions, no FMA contraction), for predicates that must resolve exactly as the source does
+template <bool REF = false>
 TG_HD void normalize3(const double v[3], double o[3]) {
+#pragma clang fp contract(off)
   const double z = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
 #if defined(__HIP_DEVICE_COMPILE__)
-  const double s = z > 0 ? 1.0 / sqrt(z) : 1.0;   // one division instead of three
-  o[0] = v[0] * s; o[1] = v[1] * s; o[2] = v[2] * s;
-#else
+  if constexpr (!REF) {
+    const double s = z > 0 ? 1.0 / sqrt(z) : 1.0;   // one division instead of three
+    o[0] = v[0] * s; o[1] = v[1] * s; o[2] = v[2] * s;
+    return;
+  }
+#endif
   if (z > 0) { const double s = sqrt(z); o[0] = v[0] / s; o[1] = v[1] / s; o[2] = v[2] / s; }
   else { o[0] = v[0]; o[1] = v[1]; o[2] = v[2]; }
-#endif
 }
 // GetNormalizedBasis (:62-66)
 TG_HD void ter_nbasis(const towr_terrain_t& T, int basis, double x, double y, double o[3]) {
   double v[3]; ter_basis(T, basis, x, y, -1, v); normalize3(v, o);
 }
 // GetDerivativeOfNormalizedBasisWrt (:80-91, 141-148)
+template <bool REF = false>
 TG_HD void ter_d_nbasis(const towr_terrain_t& T, int basis, int dim, double x, double y, double o[3]) {
+#pragma clang fp contract(off)
   double dv[3], v[3], vn[3];
   ter_basis(T, basis, x, y, dim, dv);
   ter_basis(T, basis, x, y, -1, v);
   const double sq = v[0] * v[0] + v[1] * v[1] + v[2] * v[2], nrm = sqrt(sq);
-  normalize3(v, vn);
+  normalize3<REF>(v, vn);
   for (int k = 0; k < 3; ++k) o[k] = (1 / sq * ((k == dim ? nrm : 0.0) - v[dim] * vn[k])) * dv[k];
 }
 // friction-pyramid directions b0..b4 = n, t1-mu n, t1+mu n, t2-mu n, t2+mu n
@@ -1405,9 +1429,7 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
   // spline and its schedule Jacobian: the base, torque and motion terms enter the angular rows only.
   // Emission order is unchanged (a filtered row's candidates are neither emitted nor counted).
   bool ang = true;
-#if TOWR_DYN_LINROW
   if constexpr (emit_filter<Emit>::value) ang = em_wants(em, r0 + AX) || em_wants(em, r0 + AY) || em_wants(em, r0 + AZ);
-#endif
   SplinePt L, F, Tq, P;
   spline_eval(c, sp_force(ee), t, F);
   double rv[3] = {0.0, 0.0, 0.0};
@@ -1474,13 +1496,6 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
   }
 }
 
-// in-kernel timestamps of the phase-timing build (kernel_common.h tg_stamp_hook), else nothing
-#if defined(TOWR_PHASE_TIMING) && defined(__HIP_DEVICE_COMPILE__)
-__device__ void tg_stamp_hook(int slot);
-#define TG_STAMP(slot) tg_stamp_hook(slot)
-#else
-#define TG_STAMP(slot) do { } while (0)
-#endif
 
 // RangeOfMotionConstraint instant (range_of_motion_constraint.cc:72-131)
 template <class Emit>
@@ -1490,14 +1505,11 @@ TG_HD void eval_rom(const Ctx& c, const ItemDesc& it, Emit& em) {
   SplinePt L, A, P;
   spline_eval(c, SP_BASE_LIN, t, L);
   spline_eval(c, SP_BASE_ANG, t, A);
-  TG_STAMP(10);
   spline_eval(c, sp_motion(ee), t, P);
-  TG_STAMP(11);
   double R[3][3];
   Trig q{};
   if (c.rotvec) rv_rodrigues(A.p, R);
   else { q = trig(A.p); euler_R(q, R); }
-  TG_STAMP(12);
   const double rW[3] = {P.p[0] - L.p[0], P.p[1] - L.p[1], P.p[2] - L.p[2]};
   double H[4];
   if (it.group == 1 && c.rotvec) {
@@ -1537,17 +1549,55 @@ TG_HD void eval_rom(const Ctx& c, const ItemDesc& it, Emit& em) {
     for (int r = 0; r < 3; ++r)
       #pragma unroll
       for (int e = 0; e < 3; ++e) emit_dim(c, em, r0 + r, sp_motion(ee), P, H, e, R[e][r]);
-    TG_STAMP(13);
     if (c.gait) {   // b_R_w * d pos / d schedule (range_of_motion_constraint.cc:123-130)
       SchedJac Jx;
       sched_jac(c, sp_motion(ee), t, P, Jx);
-      TG_STAMP(14);
       #pragma unroll
       for (int r = 0; r < 3; ++r)
         if (em_wants(em, r0 + r))
           for (int col = 0; col < Jx.n - 1; ++col)
             em(r0 + r, Jx.col0 + col, R[0][r] * sched_val(Jx, 0, col) + R[1][r] * sched_val(Jx, 1, col) + R[2][r] * sched_val(Jx, 2, col), true);
     }
+  }
+}
+
+// The motion-block scales of a ForceConstraintDiscretized instant on curved terrain: row i, position
+// dimension dim gets F . d(pyramid row i)/d p_dim (force_constraint_discretized.cc:125-155), added through
+// AccumulateScaledRowJacobian, which skips the whole block when the scale is exactly 0.0 (:58): the
+// Jacobian pattern then depends on x. Shared by eval_fdisc and the pattern watch (towr_gpu_pattern_outside).
+// Evaluated with the reference's operations on the device too (ter_d_nbasis<true>, no contraction): whether
+// a scale is exactly 0.0 decides the pattern.
+TG_HD void fdisc_motion_scales(const towr_terrain_t& T, double mu, const double p[3], const double f[3], double sc[2][5]) {
+#pragma clang fp contract(off)
+  for (int dim = 0; dim < 2; ++dim) {
+    double dn[3], dt1[3], dt2[3], db[5][3];
+    ter_d_nbasis<true>(T, 0, dim, p[0], p[1], dn);
+    ter_d_nbasis<true>(T, 1, dim, p[0], p[1], dt1);
+    ter_d_nbasis<true>(T, 2, dim, p[0], p[1], dt2);
+    for (int q = 0; q < 3; ++q) {   // pyramid
+      db[0][q] = dn[q];
+      db[1][q] = dt1[q] - mu * dn[q]; db[2][q] = dt1[q] + mu * dn[q];
+      db[3][q] = dt2[q] - mu * dn[q]; db[4][q] = dt2[q] + mu * dn[q];
+    }
+    for (int i = 0; i < 5; ++i) sc[dim][i] = f[0] * db[i][0] + f[1] * db[i][1] + f[2] * db[i][2];
+  }
+}
+// The same for a TorqueConstraintDiscretized instant (torque_constraint_discretized.cc:175-198): rows
+// tau . d t1, tau . d t2, +-(tau . d n) - k mu f . d n
+TG_HD void tqdisc_motion_scales(const towr_terrain_t& T, double mu, double kf, const double p[3], const double f[3], const double tq[3],
+                                double sc[2][4]) {
+#pragma clang fp contract(off)
+  auto dot = [](const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; };
+  for (int dim = 0; dim < 2; ++dim) {
+    double dn[3], dt1[3], dt2[3];
+    ter_d_nbasis<true>(T, 0, dim, p[0], p[1], dn);
+    ter_d_nbasis<true>(T, 1, dim, p[0], p[1], dt1);
+    ter_d_nbasis<true>(T, 2, dim, p[0], p[1], dt2);
+    const double s_tau_n = dot(tq, dn), s_lim = kf * mu * dot(f, dn);
+    sc[dim][0] = dot(tq, dt1);
+    sc[dim][1] = dot(tq, dt2);
+    sc[dim][2] = s_tau_n - s_lim;
+    sc[dim][3] = -s_tau_n - s_lim;
   }
 }
 
@@ -1574,19 +1624,11 @@ TG_HD void eval_fdisc(const Ctx& c, const ItemDesc& it, Emit& em) {
   double sc[2][5] = {{0, 0, 0, 0, 0}, {0, 0, 0, 0, 0}};   // F . d(pyramid)/d p_dim
   if (c.fdisc_motion) {   // AccumulateScaledRowJacobian: skipped when scale == 0.0 (:58)
     spline_basis(P, kPos, H);
+    fdisc_motion_scales(*c.ter, mu, P.p, F.p, sc);
     #pragma unroll
-    for (int dim = 0; dim < 2; ++dim) {
-      double dn[3], dt1[3], dt2[3], db[5][3];
-      ter_d_nbasis(*c.ter, 0, dim, P.p[0], P.p[1], dn);
-      ter_d_nbasis(*c.ter, 1, dim, P.p[0], P.p[1], dt1);
-      ter_d_nbasis(*c.ter, 2, dim, P.p[0], P.p[1], dt2);
-      pyramid(dn, dt1, dt2, mu, db);
+    for (int dim = 0; dim < 2; ++dim)
       #pragma unroll
-      for (int i = 0; i < 5; ++i) {
-        sc[dim][i] = dot3(F.p, db[i]);
-        emit_dim(c, em, r0 + i, sp_motion(ee), P, H, dim, sc[dim][i], sc[dim][i] != 0.0);
-      }
-    }
+      for (int i = 0; i < 5; ++i) emit_dim(c, em, r0 + i, sp_motion(ee), P, H, dim, sc[dim][i], sc[dim][i] != 0.0);
   }
   if (c.gait) {   // schedule (force_constraint_discretized.cc:158-190): force linear form + motion scaled rows
     SchedJac Jf, Jx;
@@ -1785,20 +1827,11 @@ TG_HD void eval_tqdisc(const Ctx& c, const ItemDesc& it, Emit& em) {
   double sc[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};   // d rows / d p_dim through the terrain basis
   if (c.fdisc_motion) {   // AccumulateScaledRowJacobian: skipped when scale == 0.0 (:58)
     spline_basis(P, kPos, H);
+    tqdisc_motion_scales(*c.ter, mu, kf, P.p, F.p, Tq.p, sc);
     #pragma unroll
-    for (int dim = 0; dim < 2; ++dim) {
-      double dn[3], dt1[3], dt2[3];
-      ter_d_nbasis(*c.ter, 0, dim, P.p[0], P.p[1], dn);
-      ter_d_nbasis(*c.ter, 1, dim, P.p[0], P.p[1], dt1);
-      ter_d_nbasis(*c.ter, 2, dim, P.p[0], P.p[1], dt2);
-      const double s_tau_n = dot3(Tq.p, dn), s_lim = kf * mu * dot3(F.p, dn);
-      sc[dim][0] = dot3(Tq.p, dt1);
-      sc[dim][1] = dot3(Tq.p, dt2);
-      sc[dim][2] = s_tau_n - s_lim;
-      sc[dim][3] = -s_tau_n - s_lim;
+    for (int dim = 0; dim < 2; ++dim)
       #pragma unroll
       for (int r = 0; r < 4; ++r) emit_dim(c, em, r0 + r, sp_motion(ee), P, H, dim, sc[dim][r], sc[dim][r] != 0.0);
-    }
   }
   if (c.gait) {   // schedule (:210-234): torque and force linear forms, motion scaled rows
     SchedJac Jt, Jf, Jx;

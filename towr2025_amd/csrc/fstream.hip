@@ -7,9 +7,6 @@
 #include "kernel_common.h"
 #include "layout.h"
 
-#ifndef TOWR_FS_EXP
-#define TOWR_FS_EXP 0
-#endif
 
 namespace tg {
 namespace {
@@ -40,13 +37,7 @@ __global__ void __launch_bounds__(BLOCK, 1) towr_fdisc_inst_kernel(KParams P, do
   double* Gb = P.G + (int64_t)b * P.ldg;
   double* R = rec + (int64_t)b * ldr;
   const int tid = threadIdx.x;
-#ifdef TOWR_PHASE_TIMING
-  if (tid < 64) { TSTAMP(0, TS_REAL()); TSTAMP(1, TS_MEM()); }
-#endif
   Ctx c = gait_record_setup<BLOCK>(P, b, smem);
-#ifdef TOWR_PHASE_TIMING
-  if (tid < 64) TSTAMP(2, TS_MEM());
-#endif
   for (int k = tid; k < ni; k += BLOCK) {
     FdiscInstant o;
     fdisc_instant(c, P.fs_iee[k], P.fs_t[k], o);
@@ -67,20 +58,13 @@ __global__ void __launch_bounds__(BLOCK, 1) towr_fdisc_inst_kernel(KParams P, do
       for (int i = 0; i < 5; ++i) __builtin_nontemporal_store(o.g[i], Gb + row + i);
     }
   }
-#ifdef TOWR_PHASE_TIMING
-  if ((tid & 63) == 0 && (tid >> 6) < 4) TSTAMP(3 + (tid >> 6), TS_MEM());
-  if (tid < 64) { TSTAMP(7, TS_MEM()); TSTAMP(8, TS_MEM()); TSTAMP(9, TS_REAL()); }
-#endif
 }
 
 // B. LDS: [per-instant records kFsInst x kFsD doubles | ints ws, wd, cur (kFsInst x 3) | PhaseCol per template entry]
 // Records are instant-major with an odd stride: a wave's lanes mostly read different fields of one or
 // two instants, which then fall in different banks (field-major, every field of an instant sat in
 // the same bank and the window reads serialized).
-#ifndef TOWR_FS_UNITS
-#define TOWR_FS_UNITS 4
-#endif
-constexpr int kFsUnits = TOWR_FS_UNITS;   // 16-byte units composed per lane before their stores
+constexpr int kFsUnits = 4;   // 16-byte units composed per lane before their stores
 constexpr int kFsD = 33;   // doubles per instant: window sums, b, d force / d schedule (dx, v)
 constexpr int kFsHv = 0, kFsB = kFsWin, kFsDx = kFsWin + 15, kFsV = kFsWin + 18;
 static_assert(kFsV + 3 == kFsD, "FsBlock LDS record");
@@ -95,9 +79,6 @@ __global__ void __launch_bounds__(BLOCK, 1) towr_fdisc_stream_kernel(KParams P, 
   const int b = w / P.ntiles;
   const FsBlock fb = P.fsb[w % P.ntiles];
   const int tid = threadIdx.x;
-#ifdef TOWR_PHASE_TIMING
-  if (tid < 64) { TSTAMP(0, TS_REAL()); TSTAMP(1, TS_MEM()); }
-#endif
   double* cd = smem;
   int32_t* ci = reinterpret_cast<int32_t*>(smem + kFsD * kFsInst);
   PhaseCol* pcl = reinterpret_cast<PhaseCol*>(ci + 3 * kFsInst);
@@ -145,11 +126,6 @@ __global__ void __launch_bounds__(BLOCK, 1) towr_fdisc_stream_kernel(KParams P, 
     ci[3 * k] = ws; ci[3 * k + 1] = wd;
   }
   __syncthreads();
-#ifdef TOWR_PHASE_TIMING
-  if (tid < 64) TSTAMP(2, TS_MEM());
-  if ((tid & 63) == 0 && (tid >> 6) < 4) TSTAMP(3 + (tid >> 6), TS_MEM());
-  if (tid < 64) TSTAMP(7, TS_MEM());
-#endif
   const int Lr = fb.L, js0 = fb.js0, ns1 = fb.ns1;
   const float invL = 1.0f / (float)Lr;   // exact row of element e < 2^20 for rows <= 4096 long (|err| << 0.5 / Lr)
   // entry j of row r (instant k = r / 5, pyramid row i): eval_fdisc's value (see fdisc_sched_value / emit_dim)
@@ -203,12 +179,8 @@ __global__ void __launch_bounds__(BLOCK, 1) towr_fdisc_stream_kernel(KParams P, 
         const int e = head + 2 * u;
         const int r = (int)(((float)e + 0.5f) * invL);
         const int j = e - r * Lr;
-#if TOWR_FS_EXP == 1   // timing experiment only: zeros, no composition
-        v[q].x = 0.0 * r; v[q].y = 0.0 * j;
-#else
         v[q].x = u < m2 ? entry(r, j) : 0.0;
         v[q].y = u < m2 ? (j + 1 < Lr ? entry(r, j + 1) : entry(r + 1, 0)) : 0.0;
-#endif
       }
 #pragma unroll
       for (int q = 0; q < kFsUnits; ++q)
@@ -216,9 +188,6 @@ __global__ void __launch_bounds__(BLOCK, 1) towr_fdisc_stream_kernel(KParams P, 
     }
     if (((n - head) & 1) && tid == 0) __builtin_nontemporal_store(value(n - 1), out + n - 1);
   }
-#ifdef TOWR_PHASE_TIMING
-  if (tid < 64) { TSTAMP(8, TS_MEM()); TSTAMP(9, TS_REAL()); }
-#endif
 }
 
 
@@ -231,14 +200,4 @@ int64_t fs_record_doubles() { return kFsRec; }
 const void* fs_inst_kernel() { return reinterpret_cast<const void*>(&towr_fdisc_inst_kernel<kFsInstBlock>); }
 const void* fs_stream_kernel() { return reinterpret_cast<const void*>(&towr_fdisc_stream_kernel<kFsBlock>); }
 int fs_inst_block() { return kFsInstBlock; }
-hipError_t fs_set_timing_buffer(void* p) {
-#ifdef TOWR_PHASE_TIMING
-  unsigned long long* v = reinterpret_cast<unsigned long long*>(p);
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_tbuf), &v, sizeof(v));
-#else
-  (void)p;
-  return hipSuccess;
-#endif
-}
-
 }  // namespace tg

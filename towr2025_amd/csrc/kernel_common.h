@@ -45,7 +45,6 @@ struct KParams {
   int32_t lds_scr_off;           // DYN: per-instant endeffector sum terms (instants x n_ee x 6)
   int32_t n, n_pad, n_nodecol;
   int32_t want_g, want_jac, fdisc_motion;
-  int32_t rom_wz;   // gait RangeOfMotion: per-wave zero ranges (Layout::rom_wave_zero) instead of the block zero-fill
   const int32_t* misc_tiles;      // merged small-kind launch: kMiscWaves tile ids per group
   const int32_t* misc_lds;        // per (group, wave): LDS offset, g-row offset
   RobotC rb;
@@ -62,6 +61,11 @@ struct KParams {
   const GsInst* gs_inst;          // the launched class's record instants
   const int32_t* gs_tmpl;
   const uint8_t* gs_pcode;
+  const GsSeg* gs_segs;
+  const uint8_t* gs_tseg;
+  const uint32_t* gs_vmap;
+  const int16_t* gs_ws;
+  const uint4* gs_blob;
   const CostItem* citems;         // cost launch: work items, objective and gradient outputs
   const double* cq;               // cost launch: CT_ENERGYQ Gram matrices
   int32_t n_citems, lds_red_off;
@@ -244,20 +248,23 @@ __device__ __forceinline__ Ctx gait_record_setup(const KParams& P, int b, double
   return c;
 }
 
-hipError_t fs_set_timing_buffer(void* p);   // fstream.hip: its translation unit's timing buffer
+// Kernels of the other translation units, for the host side (towr_gpu.hip): tiles.hip (tile, small-kind
+// and fused kernels), cost_traj.hip (objective, trajectory export)
+const void* tile_kernel_for(int type, bool gait, bool rotvec);
+const void* misc_kernel_for(bool gait);
+const void* step_kernel_for(bool gait, bool rotvec, int kblock);
+const void* cost_kernel_for(bool gait, bool grad, bool rotvec);
+const void* traj_kernel_for(bool gait);
+constexpr int kCostBlock = 256;   // objective kernel: one block per problem
+constexpr int kTrajBlock = 64;    // trajectory kernel: one block per (problem, 64 sample times)
 
-// Phase timing (tools/phase_timing.py; only in the -DTOWR_PHASE_TIMING build, never in the product):
-// per block, 16 timestamps: [0] realtime start, [1] memtime start, [2] after staging, [3..6] each
-// wave's end of evaluation, [7] after the evaluation barrier, [8] end of wave 0's copy-out,
-// [9] realtime end.
-#ifdef TOWR_PHASE_TIMING
-static __device__ unsigned long long* g_tbuf;   // one per translation unit
-#define TSTAMP(slot, v) do { if (g_tbuf && (threadIdx.x & 63) == 0) g_tbuf[(size_t)blockIdx.x * 16 + (slot)] = (v); } while (0)
-#define TS_MEM() ((unsigned long long)__builtin_amdgcn_s_memtime())
-#define TS_REAL() ((unsigned long long)__builtin_amdgcn_s_memrealtime())
-__device__ __attribute__((noinline)) void tg_stamp_hook(int slot) { if ((threadIdx.x >> 6) == 2) TSTAMP(slot, TS_MEM()); }   // engine_math.h probes: wave 2
-#else
-#define TSTAMP(slot, v) do { } while (0)
-#endif
+// The heavy kinds read spline nodes through the segment records; with phase-duration optimisation
+// (GAIT) their PhaseSplines evaluate polynomials from the node table, which is then staged too.
+constexpr bool stages_nodes(int type, bool gait) { return gait || is_misc_kind(type); }
+// Split staging (XStage: x loads issued before the item / slot loads) where it measured faster on
+// MI355X (ANYmal, B = 4096): Dynamic 0.0617 -> 0.0582 ms, ForceConstraintDiscretized 0.1018 ->
+// 0.098 ms; RangeOfMotion got slower (0.0838 -> 0.0878 ms) and the small kinds were unchanged, so
+// they stage after their item loads as before.
+constexpr bool early_stage(int type) { return type == IT_DYN || type == IT_FDISC; }
 
 }  // namespace tg

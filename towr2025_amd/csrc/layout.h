@@ -64,12 +64,26 @@ enum GsClass { GS_ROM = 0, GS_DYN = 1, GS_COUNT = 2 };
 constexpr int kGsRowTypes = 6;
 constexpr int kGsAct = 4;
 constexpr int kGsBlock = 256;
-constexpr int kGsInstRom = 32;   // instants per compose block
-constexpr int kGsInstDyn = 8;
+constexpr int kGsInstRom = 16;   // instants per compose block
+constexpr int kGsInstDyn = 4;
+// A row type is cut into segments: its base prefix, each maximal run of template columns of one
+// (spline kind, endeffector) or of one endeffector's schedule. Per instant a segment owns W values
+// (GsSeg::vbase): the prefix and schedule segments all their positions, a PhaseSpline segment the
+// window of W positions starting at ws(poly) (gs_ws[wsoff + poly], the active polynomial's first
+// position in the segment); positions outside it are 0. The composer computes an instant's values once
+// (one lane each), then every entry of the CSR range is one lookup: segment (gs_tseg, by position in
+// the instant), window start, value.
+// p0: first position in the instant; toff: gs_tmpl index = toff + position (prefix: gs_pcode index within the
+// instant's codes = toff + position)
+struct GsSeg { int8_t r, type, kind, ee; int16_t p0, len, W, vbase; int32_t wsoff, toff; };   // type 0 prefix, 1 window, 2 schedule
 struct GsGeo {
   int32_t cls, ee, nrt, Li;   // class, endeffector (RangeOfMotion), row types, values per instant
   int32_t L[kGsRowTypes], P[kGsRowTypes], T[kGsRowTypes], poff[kGsRowTypes];   // per row type: length, prefix, template offset, prefix codes offset
   int32_t Psum, pc0, rec0, r0;   // prefix codes per instant, gs_pcode offset of instant 0, first record index, first row
+  int32_t ns, seg0, vt, ts0;     // segments (gs_segs[seg0..]), values per instant, gs_tseg offset (Li bytes)
+  int32_t vm0, K, blob0, blob_n16;   // gs_vmap offset (vt entries: segment << 16 | value index), instants,
+                                     // the composer blob (gs_blob[blob0 ..], 16-byte units)
+  int32_t o_vmap, o_tmpl, o_tseg, o_pcode, o_ws, reserved[3];   // byte offsets of its sections (segments at 0)
 };
 struct GsBlock { int32_t geo, k0, n_inst, v0, nv, reserved[3]; };   // instants [k0, k0 + n_inst) of the geometry
 struct GsInst { double t; int32_t seg, ee, row0, reserved; };       // a record lane's instant
@@ -79,6 +93,19 @@ constexpr int kDynAxisRec = 9;    // per (axis, instant): Ap[3] | Av[3] | Aa[3]
 constexpr int kDynHangRec = 12;   // per instant: the base-angular Hp[4] | Hv[4] | Ha[4]
 constexpr int kDynEeRec = 38;     // per (endeffector, instant): Fp Tqp Pp | polyF HF[4] | polyT HT[4] | polyP HP[4] | Jf | Jx
 TG_HD constexpr int64_t dyn_rec_doubles(int K, int E) { return (int64_t)(kDynBaseRec + 3 * kDynAxisRec + kDynHangRec + kDynEeRec * E) * K; }
+
+// Pattern watch (curved terrain): ForceConstraintDiscretized / TorqueConstraintDiscretized add their
+// motion block of row i, dimension dim only where its scale is non-zero (force_constraint_discretized.cc:58,
+// torque_constraint_discretized.cc:57), so the reference's pattern moves with x while IPOPT's structure
+// (and the engine's CSR) is frozen at x0. One WatchItem per such instant: the x0 presence of each
+// (dim, row) block and the entries a block holds; towr_gpu_pattern_outside counts, at any x, the
+// reference entries outside the frozen pattern (blocks present at x, absent at x0), on the host.
+struct WatchItem {
+  double t, kf;           // instant; TorqueConstraintDiscretized's k_friction
+  int32_t seg, type;      // segment-table row, IT_FDISC / IT_TQDISC
+  int32_t ee, mask;       // endeffector; bit dim * rows + row: block present at x0
+  int32_t cnt[2];         // entries of a block of dimension 0 / 1 (the motion spline's Jacobian row)
+};
 
 struct VarSetInfo { int kind, ee, col0, n; };
 struct ConsInfo { int kind, ee, row0, rows; };
@@ -131,11 +158,6 @@ struct Layout {
   // streaming ForceConstraintDiscretized (FsBlock): enabled under phase-duration optimisation on
   // terrains without curvature when every row of each constraint holds the same columns
   bool fstream = false;
-  // gait RangeOfMotion: each row lane's wave zero-fills the row's columns after the base blocks (ItemDirect
-  // z0 / z1) just before its own value stores, and the base-block lanes store every position of the rows'
-  // base prefixes, instead of a block zero-fill of the whole tile (whose lines left L2 before the values came:
-  // 2.66x the algorithmic write bytes). Set when every tile is covered exactly that way (checked).
-  bool rom_wave_zero = false;
   std::vector<FsBlock> fs_blocks;
   std::vector<double> fs_t;
   std::vector<int32_t> fs_tmpl;
@@ -149,8 +171,19 @@ struct Layout {
   std::vector<GsInst> gs_inst[GS_COUNT];   // record lanes' instants (Dynamic: one per instant)
   std::vector<int32_t> gs_tmpl;
   std::vector<uint8_t> gs_pcode;
+  std::vector<GsSeg> gs_segs;
+  std::vector<uint8_t> gs_tseg;
+  std::vector<uint32_t> gs_vmap;
+  std::vector<int16_t> gs_ws;
+  // per geometry, the composer's static tables in one blob staged to LDS in one pass:
+  // [segments | value map | template | position -> segment | prefix codes of every instant | window starts]
+  // (GsSeg::toff of a template segment indexes the blob's template, GsSeg::wsoff its window starts)
+  std::vector<uint4> gs_blob;
+  std::vector<WatchItem> watch;     // pattern watch (curved terrain only)
+  int32_t gs_geo_max[GS_COUNT][4] = {};  // largest geometry of the class: Li, segments, values per instant, blob bytes
   int32_t gs_tmpl_max[GS_COUNT] = {};      // template ints of the largest geometry (compose LDS)
   int32_t gs_pcode_max[GS_COUNT] = {};     // prefix codes per instant, largest geometry
+  int32_t gs_nmax[GS_COUNT] = {};          // instants of the largest compose block
   // cost terms (eval_f / eval_grad_f): work items sorted by CostType, one block per problem
   std::vector<CostItem> cost_items;
   std::vector<double> cost_q;        // CT_ENERGYQ Gram matrices, 16 doubles per item (CostItem::q)
@@ -161,10 +194,7 @@ struct Layout {
   std::vector<std::pair<int32_t, int32_t>> soft;
 };
 
-#ifndef TOWR_MISC_WAVES
-#define TOWR_MISC_WAVES 4
-#endif
-constexpr int kMiscWaves = TOWR_MISC_WAVES;   // one-wave small-kind tiles per group (block)
+constexpr int kMiscWaves = 4;   // one-wave small-kind tiles per group (block)
 constexpr int kSlotSpare = 4;   // spare slot groups per lane: the kernels prefetch up to this many ahead
 constexpr bool is_misc_kind(int t) { return t != IT_DYN && t != IT_ROM && t != IT_FDISC && t != IT_TQDISC; }
 
@@ -199,13 +229,7 @@ int split_rows(int type, int group, bool gait);
 // A 5-wave block is placed as if it took 2 waves on every SIMD (hipOccupancy... and the measured
 // residency: 1 block per CU at 168 VGPRs), and a 4-wave block with FDISC rows (0, 1) on one wave
 // waits for that wave (1.5x the others): 10-wave blocks are balanced and fill 10 of the 12 wave slots.
-//   DYN, build option TOWR_DYN_GAIT_LIN1: rows 0, 1, 2 on a wave each and the linear rows 3 .. 5 of an
-//   endeffector on one lane (they need only the force spline), g0 | g1 | row 0 | 1 | 2 | 3-5, 6 waves
-//   at <= 168 VGPRs. Measured slower (gait Dynamic 0.296 vs 0.185 ms per 1024 problems): off.
-#ifndef TOWR_DYN_GAIT_LIN1
-#define TOWR_DYN_GAIT_LIN1 0
-#endif
-constexpr int kDynGaitRowParts = TOWR_DYN_GAIT_LIN1 ? 4 : 6;
+constexpr int kDynGaitRowParts = 6;
 constexpr int tile_block(int type, bool gait) {
   return type == IT_DYN ? (gait ? 64 * (2 + kDynGaitRowParts) : 256) : type == IT_ROM ? (gait ? 640 : 192) : type == IT_FDISC ? (gait ? 640 : 192)
        : type == IT_TQDISC ? (gait ? 256 : 192) : 64;
@@ -232,6 +256,10 @@ int64_t gs_record_doubles(const Layout& L, int cls);
 const void* gs_rec_kernel(int cls, bool rotvec);
 const void* gs_stream_kernel(int cls);
 int gs_rec_block();
+size_t gs_dyn_state_bytes(bool rotvec);   // the Dynamic record kernel's per-instant LDS state
+// The frozen-pattern check (WatchItem): reference Jacobian entries at x outside the x0 pattern, evaluated
+// with the structure pass's arithmetic on the host
+int64_t pattern_outside_host(const Layout& L, const double* x, const towr_terrain_t& terrain);
 
 // Returns TOWR_OK or an error code with a message in `err`. Side data (towr_gpu_create_ex): the
 // LinearEqualityConstraint matrices; the SoftConstraint bounds are checked by the handle.

@@ -445,6 +445,49 @@ int build_costs(const towr_problem_desc_t& d, const std::vector<double>& base_d,
 
 }  // namespace
 
+// The host evaluation context of the structure pass (reference operation order, std::pow) at x
+Ctx host_ctx(const Layout& L, const double* x, const towr_terrain_t& ter) {
+  Ctx cx{};
+  cx.x = x; cx.nodecol = L.nodecol.data(); cx.spl = L.spl.data(); cx.dur = L.dur.data();
+  cx.ter = &ter; cx.rb = L.rb; cx.fdisc_motion = L.fdisc_motion;
+  cx.gait = L.gait; cx.pinfo = L.pinfo.data(); cx.pcols = L.pcols.data(); cx.sched = L.sched.data(); cx.pact = L.pact.data();
+  cx.eelin = L.eelin.data(); cx.lin = L.lin.data(); cx.rotvec = L.rotvec;
+  return cx;
+}
+// presence bits (dim * rows + row) of a watched instant's motion blocks at cx.x: the scales eval_fdisc /
+// eval_tqdisc emit with, exactly as the structure pass evaluates them
+int watch_presence(const Layout& L, Ctx& cx, const WatchItem& w) {
+  cx.seg = L.segs.data() + (size_t)w.seg * L.spl.size();
+  SplinePt P, F, Tq;
+  spline_eval(cx, sp_motion(w.ee), w.t, P);
+  spline_eval(cx, sp_force(w.ee), w.t, F);
+  const double mu = cx.ter->friction_coeff;
+  int mask = 0;
+  if (w.type == IT_FDISC) {
+    double sc[2][5];
+    fdisc_motion_scales(*cx.ter, mu, P.p, F.p, sc);
+    for (int dim = 0; dim < 2; ++dim) for (int i = 0; i < 5; ++i) if (sc[dim][i] != 0.0) mask |= 1 << (dim * 5 + i);
+  } else {
+    spline_eval(cx, sp_torque(w.ee), w.t, Tq);
+    double sc[2][4];
+    tqdisc_motion_scales(*cx.ter, mu, w.kf, P.p, F.p, Tq.p, sc);
+    for (int dim = 0; dim < 2; ++dim) for (int i = 0; i < 4; ++i) if (sc[dim][i] != 0.0) mask |= 1 << (dim * 4 + i);
+  }
+  return mask;
+}
+
+int64_t pattern_outside_host(const Layout& L, const double* x, const towr_terrain_t& terrain) {
+  if (L.watch.empty()) return 0;
+  Ctx cx = host_ctx(L, x, terrain);
+  int64_t n = 0;
+  for (const WatchItem& w : L.watch) {
+    const int rows = w.type == IT_FDISC ? 5 : 4, lo = (1 << rows) - 1;
+    const int added = watch_presence(L, cx, w) & ~w.mask;   // present at x, outside the frozen pattern
+    n += (int64_t)__builtin_popcount(added & lo) * w.cnt[0] + (int64_t)__builtin_popcount((added >> rows) & lo) * w.cnt[1];
+  }
+  return n;
+}
+
 // FsBlocks of the streaming ForceConstraintDiscretized path (layout.h): per constraint, its instants
 // in chunks of <= kFsInst, provided every row of the constraint holds the same column list, each column
 // is a force-set PhaseSpline column or a schedule column of the constraint's endeffector, and each force
@@ -519,9 +562,7 @@ int build_fstream(Layout& L, std::string& err) {
     for (const ItemDesc& it : L.items)
       if (it.type == IT_FDISC && it.row0 >= r0 && it.row0 < r0 + nrow) its[(it.row0 - r0) / 5] = it.t;
     for (double t : its) if (t < 0) { err = "internal: ForceConstraintDiscretized instant missing"; return TOWR_ERR_INVALID; }
-    // instants per block: kFsInst at most (the stream kernel's LDS records); TOWR_GPU_FS_INST (tuning) lowers it
-    int cap = kFsInst;
-    if (const char* e = std::getenv("TOWR_GPU_FS_INST")) cap = std::max(1, std::min(kFsInst, std::atoi(e)));
+    const int cap = kFsInst;   // instants per block (the stream kernel's LDS records)
     const int nb = (K + cap - 1) / cap;
     for (int q = 0; q < nb; ++q) {
       const int a = (int)((int64_t)q * K / nb), b = (int)((int64_t)(q + 1) * K / nb);
@@ -558,6 +599,13 @@ bool build_gstream_class(Layout& L, int cls, const std::vector<BaseDec>& bdec, c
   std::vector<GsInst> insts;
   std::vector<int32_t> tmpl;
   std::vector<uint8_t> pcode;
+  std::vector<GsSeg> segs;
+  std::vector<uint8_t> tseg;
+  std::vector<uint32_t> vmap;
+  std::vector<int16_t> wsv;
+  int gmax[3] = {0, 0, 0}, nmax = 0;
+  int cap = cls == GS_ROM ? kGsInstRom : kGsInstDyn;
+  if (const char* e = std::getenv(cls == GS_ROM ? "TOWR_GS_ROM_INST" : "TOWR_GS_DYN_INST")) cap = std::max(1, std::min(64, std::atoi(e)));   // tuning (A/B)
   int tmax = 0, pmax = 0;
   for (const ConsInfo& cs : L.cons) {
     if (cs.kind != ctype || cs.rows == 0) continue;
@@ -601,7 +649,64 @@ bool build_gstream_class(Layout& L, int cls, const std::vector<BaseDec>& bdec, c
       Lsum += (int)len; Psum += P;
       tmax = std::max(tmax, (int)tmpl.size() - toff);
     }
-    g.Li = Lsum; g.Psum = Psum; g.pc0 = (int32_t)pcode.size();
+    g.Li = Lsum; g.Psum = Psum; g.pc0 = (int32_t)pcode.size(); g.K = K;
+    {   // segments (layout.h GsSeg), the position -> segment map, the value map, window starts
+      g.seg0 = (int32_t)(L.gs_segs.size() + segs.size());
+      g.ts0 = (int32_t)(L.gs_tseg.size() + tseg.size());
+      g.vm0 = (int32_t)(L.gs_vmap.size() + vmap.size());
+      const int s0 = (int)segs.size();
+      int vbase = 0, S = 0;
+      std::vector<uint8_t> ts((size_t)Lsum, 0);
+      auto key = [&](int32_t t) { return t < 0 ? (int)(0x100 | ((t >> 16) & 7)) : (int)(((t >> 28) & 3) << 3 | ((t >> 25) & 7)); };
+      for (int r = 0; r < R; ++r) {
+        auto add = [&](GsSeg q) {   // q.p0 row-relative on entry
+          q.r = (int8_t)r; q.vbase = (int16_t)vbase; vbase += q.W;
+          for (int j = q.p0; j < q.p0 + q.len; ++j) ts[S + j] = (uint8_t)(segs.size() - s0);
+          q.toff = q.type == 0 ? g.poff[r] - S : g.T[r] - g.P[r] - S;   // local template offset (rebased at commit)
+          q.p0 = (int16_t)(S + q.p0);
+          segs.push_back(q);
+        };
+        if (g.P[r] > 0) add(GsSeg{0, 0, 0, 0, 0, (int16_t)g.P[r], (int16_t)g.P[r], 0, -1, 0});
+        for (int j = g.P[r]; j < g.L[r];) {
+          auto tr_at = [&](int pos) { return tmpl[(size_t)(g.T[r] + pos - g.P[r])]; };   // code of position pos
+          const int k0 = key(tr_at(j));
+          int j2 = j;
+          while (j2 < g.L[r] && key(tr_at(j2)) == k0) ++j2;
+          GsSeg q{};
+          q.p0 = (int16_t)j; q.len = (int16_t)(j2 - j); q.wsoff = -1;
+          if (tr_at(j) < 0) {
+            q.type = 2; q.ee = (int8_t)((tr_at(j) >> 16) & 7); q.W = q.len;
+          } else {
+            q.type = 1; q.kind = (int8_t)((tr_at(j) >> 28) & 3); q.ee = (int8_t)((tr_at(j) >> 25) & 7);
+            const int sp = q.kind == 0 ? sp_motion(q.ee) : q.kind == 1 ? sp_force(q.ee) : sp_torque(q.ee);
+            const SplineMeta& m = L.spl[sp];
+            q.wsoff = (int32_t)(L.gs_ws.size() + wsv.size());
+            int W = 0;
+            for (int p = 0; p < m.n_polys; ++p) {   // the polynomial's active positions in the segment
+              int first = -1, last = -1;
+              for (int pos = j; pos < j2; ++pos) {
+                const int e = (tr_at(pos) >> 22) & 3, qq = tr_at(pos) & 0x3FFFFF;
+                const int32_t* w = L.pact.data() + m.pact_off + 2 * (e * m.n_polys + p);
+                if (qq >= w[0] && qq <= w[1]) { if (first < 0) first = pos; last = pos; }
+              }
+              wsv.push_back((int16_t)(first >= 0 ? first - j : 0));
+              if (first >= 0) W = std::max(W, last - first + 1);
+            }
+            q.W = (int16_t)W;
+          }
+          add(q);
+          j = j2;
+        }
+        S += g.L[r];
+      }
+      g.ns = (int32_t)segs.size() - s0;
+      g.vt = vbase;
+      if (g.ns > 255 || vbase > 4096 || Lsum > 65535 || (int64_t)vbase * cap > 65535) { why = "segment tables exceed their encodings"; return false; }
+      for (int sg = 0; sg < g.ns; ++sg)
+        for (int q = 0; q < segs[s0 + sg].W; ++q) vmap.push_back((uint32_t)(sg << 16 | q));
+      tseg.insert(tseg.end(), ts.begin(), ts.end());
+      gmax[0] = std::max(gmax[0], Lsum); gmax[1] = std::max(gmax[1], g.ns); gmax[2] = std::max(gmax[2], vbase);
+    }
     pmax = std::max(pmax, Psum);
     for (int k = 0; k < K; ++k) {   // prefix codes: blk << 4 | dim << 2 | basis of the instant's base polynomials
       const int pl = L.segs[(size_t)its[k].seg * nspl + SP_BASE_LIN].poly, pa = L.segs[(size_t)its[k].seg * nspl + SP_BASE_ANG].poly;
@@ -615,12 +720,12 @@ bool build_gstream_class(Layout& L, int cls, const std::vector<BaseDec>& bdec, c
         }
       }
     }
-    const int cap = cls == GS_ROM ? kGsInstRom : kGsInstDyn;
     const int nb = (K + cap - 1) / cap;
     for (int q = 0; q < nb; ++q) {
       const int a = (int)((int64_t)q * K / nb), b = (int)((int64_t)(q + 1) * K / nb);
       GsBlock bl{};
       bl.geo = (int32_t)(L.gs_geo.size() + geos.size()); bl.k0 = a; bl.n_inst = b - a;
+      nmax = std::max(nmax, b - a);
       bl.v0 = (int32_t)L.row_ptr[cs.row0 + R * a]; bl.nv = (int32_t)(L.row_ptr[cs.row0 + R * b] - L.row_ptr[cs.row0 + R * a]);
       if ((int64_t)bl.nv != (int64_t)(b - a) * Lsum) { why = "internal: block range"; return false; }
       blocks.push_back(bl);
@@ -638,9 +743,16 @@ bool build_gstream_class(Layout& L, int cls, const std::vector<BaseDec>& bdec, c
   }
   L.gs_tmpl.insert(L.gs_tmpl.end(), tmpl.begin(), tmpl.end());
   L.gs_pcode.insert(L.gs_pcode.end(), pcode.begin(), pcode.end());
+  for (GsSeg& q : segs) if (q.type != 0) q.toff += t0;
+  L.gs_segs.insert(L.gs_segs.end(), segs.begin(), segs.end());
+  L.gs_tseg.insert(L.gs_tseg.end(), tseg.begin(), tseg.end());
+  L.gs_vmap.insert(L.gs_vmap.end(), vmap.begin(), vmap.end());
+  L.gs_ws.insert(L.gs_ws.end(), wsv.begin(), wsv.end());
+  for (int q = 0; q < 3; ++q) L.gs_geo_max[cls][q] = gmax[q];
   L.gs_blocks[cls].swap(blocks);
   L.gs_inst[cls].swap(insts);
   L.gs_tmpl_max[cls] = tmax;
+  L.gs_nmax[cls] = nmax;
   L.gs_pcode_max[cls] = pmax;
   L.gstream[cls] = true;
   return true;
@@ -649,7 +761,7 @@ bool build_gstream_class(Layout& L, int cls, const std::vector<BaseDec>& bdec, c
 
 int build_gstream(Layout& L, std::string& err) {
   for (int c = 0; c < GS_COUNT; ++c) { L.gstream[c] = false; L.gs_blocks[c].clear(); L.gs_inst[c].clear(); L.gs_tmpl_max[c] = L.gs_pcode_max[c] = 0; }
-  L.gs_geo.clear(); L.gs_tmpl.clear(); L.gs_pcode.clear();
+  L.gs_geo.clear(); L.gs_tmpl.clear(); L.gs_pcode.clear(); L.gs_segs.clear(); L.gs_tseg.clear(); L.gs_vmap.clear(); L.gs_ws.clear();
   if (!L.gait || std::getenv("TOWR_GPU_GAIT_TILES")) return TOWR_OK;   // the tile path (A/B and parity of both paths)
   const int E = L.rb.n_ee;
   std::vector<BaseDec> bdec((size_t)L.n);
@@ -686,6 +798,42 @@ int build_gstream(Layout& L, std::string& err) {
       err = why;
       return TOWR_ERR_INVALID;
     }
+  }
+  // the composer blobs (layout.h gs_blob)
+  L.gs_blob.clear();
+  for (int c = 0; c < GS_COUNT; ++c) L.gs_geo_max[c][3] = 0;
+  for (GsGeo& g : L.gs_geo) {
+    int ntl = 0;
+    for (int r = 0; r < g.nrt; ++r) ntl = std::max(ntl, g.T[r] + g.L[r] - g.P[r] - g.T[0]);
+    int nws = 0;
+    for (int q = 0; q < g.ns; ++q) {
+      const GsSeg& sg = L.gs_segs[g.seg0 + q];
+      if (sg.type == 1) nws = std::max(nws, sg.wsoff + L.spl[sg.kind == 0 ? sp_motion(sg.ee) : sg.kind == 1 ? sp_force(sg.ee) : sp_torque(sg.ee)].n_polys);
+    }
+    int ws0 = INT32_MAX;
+    for (int q = 0; q < g.ns; ++q) if (L.gs_segs[g.seg0 + q].type == 1) ws0 = std::min(ws0, L.gs_segs[g.seg0 + q].wsoff);
+    if (ws0 == INT32_MAX) { ws0 = 0; nws = 0; }
+    auto al = [](size_t b) { return (b + 15) & ~(size_t)15; };
+    const size_t o_vmap = al(sizeof(GsSeg) * g.ns), o_tmpl = o_vmap + al(4 * (size_t)g.vt), o_tseg = o_tmpl + al(4 * (size_t)ntl),
+                 o_pcode = o_tseg + al((size_t)g.Li), o_ws = o_pcode + al((size_t)g.K * g.Psum), end = o_ws + al(2 * (size_t)(nws - ws0));
+    std::vector<uint8_t> b(end, 0);
+    for (int q = 0; q < g.ns; ++q) {
+      GsSeg sg = L.gs_segs[g.seg0 + q];
+      if (sg.type != 0) sg.toff -= g.T[0];
+      if (sg.type == 1) sg.wsoff -= ws0;
+      std::memcpy(b.data() + sizeof(GsSeg) * q, &sg, sizeof(GsSeg));
+    }
+    std::memcpy(b.data() + o_vmap, L.gs_vmap.data() + g.vm0, 4 * (size_t)g.vt);
+    std::memcpy(b.data() + o_tmpl, L.gs_tmpl.data() + g.T[0], 4 * (size_t)ntl);
+    std::memcpy(b.data() + o_tseg, L.gs_tseg.data() + g.ts0, (size_t)g.Li);
+    std::memcpy(b.data() + o_pcode, L.gs_pcode.data() + g.pc0, (size_t)g.K * g.Psum);
+    if (nws > ws0) std::memcpy(b.data() + o_ws, L.gs_ws.data() + ws0, 2 * (size_t)(nws - ws0));
+    g.blob0 = (int32_t)L.gs_blob.size();
+    g.blob_n16 = (int32_t)(end / 16);
+    g.o_vmap = (int32_t)o_vmap; g.o_tmpl = (int32_t)o_tmpl; g.o_tseg = (int32_t)o_tseg; g.o_pcode = (int32_t)o_pcode; g.o_ws = (int32_t)o_ws;
+    L.gs_blob.resize(L.gs_blob.size() + end / 16);
+    std::memcpy(L.gs_blob.data() + g.blob0, b.data(), end);
+    L.gs_geo_max[g.cls][3] = std::max(L.gs_geo_max[g.cls][3], (int32_t)end);
   }
   (void)err;
   return TOWR_OK;
@@ -1041,6 +1189,34 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
     item_cand_begin[L.items.size()] = (int32_t)crow.size();
   }
 
+  // ---- pattern watch: x0 presence of the data-dependent motion blocks (curved terrain)
+  L.watch.clear();
+  if (L.fdisc_motion) {
+    Ctx cx = host_ctx(L, L.x0.data(), L.terrain);
+    for (const ItemDesc& it : L.items) {
+      if ((it.type != IT_FDISC && it.type != IT_TQDISC) || (it.rsel > 0 && rsel_part(it.rsel) != 0)) continue;
+      WatchItem w{};
+      w.t = it.t; w.kf = it.p0; w.seg = it.seg; w.type = it.type; w.ee = it.ee;
+      w.mask = watch_presence(L, cx, w);
+      cx.seg = L.segs.data() + (size_t)it.seg * L.spl.size();
+      SplinePt P;
+      spline_eval(cx, sp_motion(it.ee), it.t, P);
+      for (int dim = 0; dim < 2; ++dim) {   // distinct variables of the spline's Jacobian row dim
+        const SplineMeta& m = L.spl[sp_motion(it.ee)];
+        if (L.gait) { w.cnt[dim] = m.pcol_n[dim]; continue; }   // PhaseSpline: the full pattern
+        int cols[4], n = 0;
+        for (int bb = 0; bb < 4; ++bb) {
+          const int32_t col = basis_col(cx, sp_motion(it.ee), P.poly, bb, dim);
+          bool dup = col < 0;
+          for (int q = 0; q < n && !dup; ++q) dup = cols[q] == col;
+          if (!dup) cols[n++] = col;
+        }
+        w.cnt[dim] = n;
+      }
+      L.watch.push_back(w);
+    }
+  }
+
   // ---- CSR pattern (setFromTriplets: sorted columns, duplicates merged)
   std::vector<std::vector<int32_t>> rc((size_t)L.m);
   for (size_t q = 0; q < crow.size(); ++q)
@@ -1226,7 +1402,6 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
     // tile-relative uint16 positions; four spare groups per lane absorb the kernel's prefetch
     std::vector<SlotGroup> groups;
     L.idirect.assign(L.gait ? items.size() : 0, ItemDirect{});
-    L.rom_wave_zero = L.gait;
     for (const TileDesc& td : L.tiles) {
       const int block = td.i1 - td.i0;
       std::vector<int32_t> bslot((size_t)block, -1);   // build-time slot offsets (L.slots) of the lanes
@@ -1281,35 +1456,6 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
         }
         bslot[l] = it.slot;
         it.slot = (int32_t)(base + l);
-      }
-      if (L.gait && td.type == IT_ROM && L.rom_wave_zero) {
-        // row lanes (group 2, one row each): zero range = the row after its base-block prefix; the base
-        // lanes (groups 0, 1) must store every position of those prefixes, and the two must tile [v0, v1)
-        const int nv = td.v1 - td.v0;
-        std::vector<uint8_t> cov((size_t)nv, 0);
-        bool ok = true;
-        for (int l = 0; l < block && ok; ++l) {
-          const ItemDesc& it = items[td.i0 + l];
-          if (it.type == IT_NONE || it.group == 2) continue;
-          for (int j = 0; j < it.ncand; ++j) {
-            const int32_t g = L.slots[bslot[l] + j];
-            if (g >= 0) cov[g - td.v0] = 1;
-          }
-        }
-        for (int l = 0; l < block && ok; ++l) {
-          const ItemDesc& it = items[td.i0 + l];
-          if (it.type == IT_NONE || it.group != 2) continue;
-          if (it.rsel <= 0 || rsel_count(it.rsel) != 1) { ok = false; break; }
-          const int r = it.row0 + rsel_first(it.rsel);
-          int32_t a = (int32_t)(L.row_ptr[r] - td.v0);
-          const int32_t e = (int32_t)(L.row_ptr[r + 1] - td.v0);
-          while (a < e && cov[a] == 1) ++a;   // the base prefix
-          ItemDirect& dd = L.idirect[td.i0 + l];
-          dd.z0 = a; dd.z1 = e;
-          for (int32_t q = a; q < e; ++q) { if (cov[q]) { ok = false; break; } cov[q] = 2; }
-        }
-        for (int q = 0; q < nv && ok; ++q) ok = cov[q] != 0;
-        if (!ok) L.rom_wave_zero = false;   // the block zero-fill then (the z ranges are not read)
       }
       if (L.gait && (td.type == IT_FDISC || td.type == IT_TQDISC)) {   // the lanes' owned ranges tile [v0, v1)
         std::vector<std::pair<int32_t, int32_t>> zr;

@@ -1,0 +1,481 @@
+// tiles.hip — the tile kernels of the eval_g / eval_jac_g engine (include/towr_gpu.h):
+// one block per (problem, tile) of a constraint class, the merged small-kind launch and the fused
+// launch of several classes (towr_step_kernel). The host side (towr_gpu.hip) reaches them through the
+// getters at the end of this file (kernel_common.h).
+//   * block = (problem, group of LDS tiles); blocks of one problem are placed on one XCD
+//     (blockIdx % 8 round-robin), so x is fetched from HBM once per problem;
+//   * the problem's x (NodesVariables / PhaseDurations values) is staged in LDS;
+//   * a tile = consecutive instances of one constraint set whose CSR value range fits in LDS;
+//     lanes evaluate work items (node-per-lane Hermite splines, SRBD, terrain) and accumulate
+//     Jacobian candidates into LDS at precomputed slots; then the tile's contiguous CSR range and
+//     g range are written with 16-byte coalesced stores.
+// No MFMA: there is no dense contraction; the kernels are HBM-write bound.
+#include <hip/hip_runtime.h>
+
+#include "engine_math.h"
+#include "kernel_common.h"
+#include "layout.h"
+
+namespace tg {
+constexpr int kMiscMinWaves = 5;   // small kinds: minimum waves per SIMD (0.0267 -> 0.0257 ms per 4096 problems, A/B on one box)
+namespace {
+
+
+// Stores candidate j of this lane into the LDS tile at its tile-relative CSR position. Positions
+// come 8 per 16-byte SlotGroup; the next group is prefetched while the current one is consumed, so
+// the slot-table latency (L2: the table is shared by every problem of the batch) hides behind 8
+// candidates of arithmetic. The candidate's column is never needed on the device, and no item emits
+// a column twice (engine_math.h), so every position receives exactly one plain LDS store; absent
+// candidates (constant node values) go to a per-lane dummy slot, so the store needs no branch.
+// DIRECT (phase-duration optimisation): there is no LDS tile. The full-pattern Jacobian is ~90 %
+// zeros whose positions move with x, and an LDS tile of it held ~13 instants per block (one busy wave
+// of three, 2 blocks per CU), so the launch was bound by the evaluation's latency at low occupancy.
+// Instead each block zero-fills its tile's CSR range in V (zero_out), and after a barrier lanes store
+// their present candidates straight to HBM: `out` is the tile's first CSR value in V, `gout` the problem's g,
+// absent candidates (positions >= nvals, the dummy slots) are not stored. The lane's item may be
+// row-split (ItemDesc::rsel): only its rows' candidates are emitted (and counted), exactly as the
+// structure pass recorded them, and only those rows' g.
+template <int BLOCK, int DEPTH, bool DIRECT = false, int PRE = 1, int DYNG = 0>
+struct TileEmit {
+  static constexpr int kDynGroups = DYNG;   // Dynamic groups this emitter's kernel evaluates (engine_math.h)
+  static_assert(PRE >= 0 && PRE <= 6 && PRE <= kSlotSpare + 2, "preloaded slot groups: 0 .. 6, within the spare groups");
+  const SlotGroup* slot;   // this lane's group 0; group g at slot[g * BLOCK]
+  double* out;             // LDS tile, tile-relative (DIRECT: V at the tile's first value)
+  double* gout;            // LDS g rows, tile-relative (DIRECT: the problem's g)
+  SlotGroup q[DEPTH];      // groups g .. g + DEPTH - 1 in flight (q[0] = current)
+  int j = 0;
+  int flo = 0, fcnt = 0;   // DIRECT: the selected rows flo .. flo + fcnt - 1 (fcnt 0 = all rows)
+  int nvals = 0;           // DIRECT: values of the tile
+  ItemDirect dd{};         // DIRECT: column ranges stored at off + col without the slot table
+  bool fence = false;      // DIRECT: the wave's own zero-fill stores must complete before the first value store
+  int qg = 0;              // DIRECT: slot group held in q[0] (the ring reloads lazily, on use)
+  static constexpr bool kFilter = DIRECT;
+  __device__ __forceinline__ bool want(int row) const { return !DIRECT || fcnt == 0 || (unsigned)(row - flo) < (unsigned)fcnt; }
+  // DIRECT: slot groups 0 .. kPre - 1 are loaded at construction into named registers (a runtime-
+  // indexed array would go to scratch); on gfx950 vmcnt counts stores too, so a group loaded after the
+  // lane's first value stores waits for all of them (measured: the RangeOfMotion base lanes, 36
+  // slot-path candidates, were the gait tile's slowest waves)
+  static constexpr int kPre = DIRECT ? PRE : 0;
+  u32x4_t p0 = {}, p1 = {}, p2 = {}, p3 = {}, p4 = {}, p5 = {};   // native vectors: a SlotGroup (array) would go to scratch
+  __device__ __forceinline__ TileEmit(const SlotGroup* s, double* o, double* go) : slot(s), out(o), gout(go) {
+    if constexpr (DIRECT) {
+      const u32x4_t* sv = reinterpret_cast<const u32x4_t*>(s);
+      if (kPre > 0) p0 = sv[0];
+      if (kPre > 1) p1 = sv[BLOCK];
+      if (kPre > 2) p2 = sv[2 * BLOCK];
+      if (kPre > 3) p3 = sv[3 * BLOCK];
+      if (kPre > 4) p4 = sv[4 * BLOCK];
+      if (kPre > 5) p5 = sv[5 * BLOCK];
+      qg = -1;
+    } else {
+#pragma unroll
+      for (int d = 0; d < DEPTH; ++d) q[d] = s[d * BLOCK];
+    }
+  }
+  bool gon = true;         // DIRECT: g requested
+  __device__ __forceinline__ void g(int row, double v) {
+    if (!DIRECT) gout[row] = v;
+    else if (gon && want(row)) gout[row] = v;
+  }
+  // GAIT outputs are zero-filled before the evaluation (tile_body / misc_body), so candidates whose
+  // value is 0 can be skipped: move to candidate j + k, reloading the slot ring if the group changes
+  static constexpr bool kSparse = true;
+  __device__ __forceinline__ void skip(int k) {
+    if constexpr (DIRECT) {   // lazy: the next slot-path candidate loads its group
+      j += k;
+      return;
+    }
+    if (k <= 0) return;
+    const int g0 = j >> 3;
+    j += k;
+    const int g1 = j >> 3;
+    if (g1 != g0) {
+#pragma unroll
+      for (int d = 0; d < DEPTH; ++d) q[d] = slot[(g1 + d) * BLOCK];
+    }
+  }
+  __device__ __forceinline__ void operator()(int row, int col, double v, bool) {
+    if constexpr (DIRECT) {
+      // Direct-range candidates need no slot load. Slot-path groups load lazily: on gfx950 vmcnt
+      // counts stores too, so a group prefetched across this lane's value stores would wait for them.
+      if (!want(row)) return;
+      int s;
+      if (col >= dd.c0[0] && col < dd.c1[0]) {
+        s = dd.off[0] + col;
+      } else if (col >= dd.c0[1] && col < dd.c1[1]) {
+        s = dd.off[1] + col;
+      } else {
+        const int g = j >> 3;
+        if (g < kPre) {   // preloaded before any store of this lane (no wait behind the value stores)
+          const u32x4_t v = g == 0 ? p0 : g == 1 ? p1 : g == 2 ? p2 : g == 3 ? p3 : g == 4 ? p4 : p5;
+          const int k = j & 7;
+          const uint32_t lo = (k & 2) ? v.y : v.x, hi = (k & 2) ? v.w : v.z;
+          const uint32_t w = (k & 4) ? hi : lo;
+          s = (k & 1) ? (int)(w >> 16) : (int)(w & 0xFFFFu);
+        } else {
+          if (g != qg) {
+            q[0] = slot[g * BLOCK];
+            qg = g;
+          }
+          s = slot_pick(q[0], j & 7);
+        }
+      }
+      ++j;
+      if (fence) {   // wave-level: the zero stores of this wave's rows (tile_body) land first
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        fence = false;
+      }
+      if (s < nvals) out[s] = v;
+      return;
+    }
+    const int s = slot_pick(q[0], j & 7);
+    ++j;
+    if ((j & 7) == 0) {
+#pragma unroll
+      for (int d = 0; d + 1 < DEPTH; ++d) q[d] = q[d + 1];
+      q[DEPTH - 1] = slot[((j >> 3) + DEPTH - 1) * BLOCK];
+    }
+    out[s] = v;   // absent candidates land in the lane's dummy slot
+  }
+  __device__ __forceinline__ void flush() {}
+};
+// Emitter for a fixed stretch of a lane's candidates J0 .. J0 + 8 NG - 1 whose slot groups are all
+// loaded at construction: Dynamic group 0 builds it before the block barrier that separates its two
+// phases, so phase B's slot loads complete during the barrier wait instead of once per 8 candidates
+// after it. Candidate indices must be compile-time constants (fully unrolled emission).
+template <int BLOCK, int J0, bool DIRECT = false>
+struct TileEmitPre {   // four groups: candidates J0 - J0 % 8 .. + 31
+  double* out;
+  double* gout;
+  int nvals = 0;   // DIRECT (see TileEmit): out / gout are V and g in HBM, dummy slots are not stored
+  bool gon = true;
+  SlotGroup q0, q1, q2, q3;   // named registers (a runtime-indexed array would go to scratch)
+  int j = J0;
+  __device__ __forceinline__ TileEmitPre(const SlotGroup* s, double* o, double* go, bool load) : out(o), gout(go) {
+    if (load) {
+      q0 = s[(J0 >> 3) * BLOCK]; q1 = s[((J0 >> 3) + 1) * BLOCK];
+      q2 = s[((J0 >> 3) + 2) * BLOCK]; q3 = s[((J0 >> 3) + 3) * BLOCK];
+    }
+  }
+  __device__ __forceinline__ void g(int row, double v) {
+    if (!DIRECT || gon) gout[row] = v;
+  }
+  __device__ __forceinline__ void operator()(int, int, double v, bool) {
+    const int k = (j >> 3) - (J0 >> 3);
+    SlotGroup q;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) q.w[w] = k == 0 ? q0.w[w] : k == 1 ? q1.w[w] : k == 2 ? q2.w[w] : q3.w[w];
+    const int s = slot_pick(q, j & 7);
+    ++j;
+    if (!DIRECT || s < nvals) out[s] = v;
+  }
+  __device__ __forceinline__ void flush() {}
+};
+static_assert(kDynG0Cand - (kDynG0PhaseA - kDynG0PhaseA % 8) <= 32, "phase B of Dynamic group 0 exceeds the preloaded groups");
+
+// Slot-group prefetch depth. Deeper rings only pay off where the emission index is a compile-time
+// constant: in a runtime loop, rotating the ring copies registers whose loads are still in flight
+// and waits for the newest one (measured: depth 4 made RangeOfMotion's base-angular wave slower).
+constexpr int slot_depth(int) { return 2; }
+static_assert(slot_depth(IT_ROM) <= kSlotSpare, "slot prefetch past the spare groups");
+
+// Slot groups preloaded by the gait (DIRECT) emitter per tile class: RangeOfMotion's base lanes emit
+// 33-36 slot-path candidates each (5 groups); Dynamic's kernel is at 256 VGPRs already (more spills)
+constexpr int gait_slot_pre(int type) { return type == IT_ROM ? 6 : 1; }
+
+template <int TYPE, class Emit>
+__device__ __forceinline__ void eval_typed(const Ctx& c, const ItemDesc& it, Emit& em) {
+  if constexpr (TYPE == IT_DYN) eval_dyn(c, it, em);
+  else if constexpr (TYPE == IT_ROM) eval_rom(c, it, em);
+  else if constexpr (TYPE == IT_FDISC) eval_fdisc(c, it, em);
+  else if constexpr (TYPE == IT_FNODE) eval_fnode(c, it, em);
+  else if constexpr (TYPE == IT_TERR) eval_height(c, it, sp_motion(it.ee), 0.0, em);
+  else if constexpr (TYPE == IT_BMOT) eval_bmot(c, it, em);
+  else if constexpr (TYPE == IT_SACC) eval_sacc(c, it, em);
+  else if constexpr (TYPE == IT_BHGT) eval_height(c, it, SP_BASE_LIN, it.p0, em);
+  else if constexpr (TYPE == IT_SWING) eval_swing(c, it, em);
+  else if constexpr (TYPE == IT_TDUR) eval_tdur(c, it, em);
+  else if constexpr (TYPE == IT_TQDISC) eval_tqdisc(c, it, em);
+}
+
+// One block = one tile (consecutive instances of one constraint kind) of one problem; one item per
+// thread, laid out so every wave runs a single code path. Blocks of one problem share an XCD (the
+// mapping below), so its ~9 KB x is fetched from HBM once and then served by that XCD's L2.
+// Candidates land in an LDS tile (no global store before the end, so no load ever waits behind a
+// store: gfx950's vmcnt counts both); the tile's contiguous CSR range and g rows then leave with
+// 16-byte coalesced stores. Every kernel stages the problem's x in LDS (spline items gather their
+// nodes through the segment record's columns); node-value kinds also stage the node->column table.
+
+
+
+// Body of one tile block. TBLOCK = the tile's lane count (its slot-table stride), KBLOCK = the
+// launch's block size (>= TBLOCK): in the fused launch a 192-lane tile runs in a 256-thread block,
+// whose extra wave only helps stage x and copy out.
+template <int TYPE, int TBLOCK, int KBLOCK, bool GAIT, bool ROTVEC>
+__device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b, int tile, int lds_x_off, int lds_rows_off) {
+  const TileDesc T = P.tiles[tile];
+  double* Vb = P.V + (int64_t)b * P.ldv;
+  double* Gb = P.G + (int64_t)b * P.ldg;
+  const double* xg = P.X + (int64_t)b * P.ldx;
+  // issue the lane's item, first slot groups and (below) the x / node-table staging loads together
+  // x (+ a zero at index n for constant node values) and, for node-value kinds, the node table:
+  // loads in flight first, then the lane's item and slot groups, then the LDS stores
+  XStage<KBLOCK, stages_nodes(TYPE, GAIT)> xst;
+  if constexpr (early_stage(TYPE)) xst.issue(P, xg);
+  ItemDesc it;
+  if (KBLOCK == TBLOCK || (int)threadIdx.x < TBLOCK) {
+    it = P.items[T.i0 + threadIdx.x];
+  } else {
+    it = ItemDesc{}; it.type = IT_NONE; it.slot = 0;
+  }
+  // GAIT: direct HBM emission into the zero-filled V (see TileEmit)
+  TileEmit<TBLOCK, slot_depth(TYPE), GAIT, gait_slot_pre(TYPE)> em(
+      P.slots + it.slot, GAIT ? Vb + T.v0 : smem, GAIT ? Gb : smem + lds_rows_off - T.r0);
+  if constexpr (GAIT) {
+    if (it.rsel > 0) { em.flo = it.row0 + rsel_first(it.rsel); em.fcnt = rsel_count(it.rsel); }
+    em.nvals = P.want_jac ? T.v1 - T.v0 : 0;
+    em.gon = P.want_g != 0;
+    if (KBLOCK == TBLOCK || (int)threadIdx.x < TBLOCK) em.dd = P.idir[T.i0 + threadIdx.x];
+  }
+  double* xs = smem + lds_x_off;
+  int32_t* ns = reinterpret_cast<int32_t*>(smem + lds_x_off + P.n_pad);
+  char* gt = reinterpret_cast<char*>(smem + lds_x_off + P.n_pad + ((P.n_nodecol + 3) >> 2) * 2);   // GAIT tables
+  // GAIT: the block zero-fills its tile's CSR range first; the value stores of any lane come after
+  // the barrier below, which waits for these stores to complete (vmcnt(0)), so they land on top.
+  // FDISC / TQDISC lanes own whole rows (row-split), so there each wave zero-fills its own rows
+  // after the staging instead (below), and waits for them only at its first value store.
+  constexpr bool kWaveZero = GAIT && (TYPE == IT_FDISC || TYPE == IT_TQDISC);
+  if constexpr (GAIT && !kWaveZero)
+    if (P.want_jac) zero_out(Vb + T.v0, T.v1 - T.v0, threadIdx.x, KBLOCK);
+  if constexpr (early_stage(TYPE)) xst.commit(P, xg, xs, ns);
+  else stage_x<KBLOCK, stages_nodes(TYPE, GAIT)>(P, xg, xs, ns);
+  towr_terrain_t* ters = reinterpret_cast<towr_terrain_t*>(gt + 16 * P.gt_n16 + 8 * P.gt_ntime);   // GAIT: the terrain
+  if constexpr (GAIT) {
+    stage16<KBLOCK>(reinterpret_cast<uint4*>(gt), P.gtab, P.gt_n16);
+    if (threadIdx.x < sizeof(towr_terrain_t) / 8)
+      reinterpret_cast<double*>(ters)[threadIdx.x] = reinterpret_cast<const double*>(P.terrains + (P.terrain_per_problem ? b : 0))[threadIdx.x];
+    if constexpr (!kWaveZero) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  Ctx c;
+  c.seg = nullptr; c.sg = P.sg; c.row = it.seg;
+  c.x = xs; c.nodecol = ns; c.spl = P.spl; c.dur = P.dur;
+  c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
+  c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
+  c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.pact = P.pact; c.sched = P.sched; c.eelin = P.eelin; c.lin = P.lin;
+  if constexpr (GAIT) {   // the PhaseSpline searches and window emission read their tables from LDS
+    c.spl = reinterpret_cast<const SplineMeta*>(gt + P.gt_off[0]);
+    c.sched = reinterpret_cast<const SchedInfo*>(gt + P.gt_off[1]);
+    c.pinfo = reinterpret_cast<const PolyPhase*>(gt + P.gt_off[2]);
+    c.pact = reinterpret_cast<const int32_t*>(gt + P.gt_off[3]);
+    c.pcols = reinterpret_cast<const PhaseCol*>(gt + P.gt_off[4]);
+  }
+  c.rotvec = ROTVEC;
+  c.dyn_scratch = TYPE == IT_DYN ? smem + P.lds_scr_off : nullptr;
+  if constexpr (GAIT) {
+    // the x-dependent PhaseSpline timings once per block (one thread per spline / endeffector)
+    // instead of a division-carrying scan per lane and spline evaluation
+    double* tm = reinterpret_cast<double*>(gt + 16 * P.gt_n16);
+    const int tid = threadIdx.x, nspl = P.n_spl, nee = P.rb.n_ee;
+    if (tid < nspl) {
+      if (c.spl[tid].ee >= 0) phase_spline_timings(c, tid, tm, tm + P.n_pinfo);
+    } else if (tid < nspl + nee) {
+      if (c.sched[tid - nspl].col0 >= 0) phase_end_timings(c, tid - nspl, tm + 2 * P.n_pinfo + (tid - nspl) * P.ph_stride);
+    }
+    __syncthreads();
+    c.pdur = tm; c.pend = tm + P.n_pinfo; c.phend = tm + 2 * P.n_pinfo; c.ph_stride = P.ph_stride;
+    c.ter = ters;   // LDS copy: no global load in the evaluation waits behind the zero-fill stores
+    if constexpr (kWaveZero) {
+      if (P.want_jac) {   // each lane's owned rows, zero-filled by its whole wave (512 B per store)
+        double* vt = Vb + T.v0;
+        const int lane = threadIdx.x & 63;
+        for (int l = 0; l < 64; ++l) {
+          const int z0 = __shfl(em.dd.z0, l, 64), z1 = __shfl(em.dd.z1, l, 64);
+          for (int p = z0 + lane; p < z1; p += 64) vt[p] = 0.0;
+        }
+        em.fence = true;
+      }
+    }
+  }
+  DynG0 g0;   // DYN group 0 between its two phases
+  if (it.type == TYPE) {
+    if constexpr (TYPE == IT_DYN) {
+      if (it.group == 0) dyn_g0_a(c, it, em, g0);
+      else eval_dyn(c, it, em);   // group 1 and the endeffector groups (these deposit their sum terms)
+    } else {
+      eval_typed<TYPE>(c, it, em);
+    }
+    em.flush();
+  }
+  if constexpr (TYPE == IT_DYN) {   // phase B of group 0: the endeffector sums from LDS
+    const bool g0lane = it.type == TYPE && it.group == 0;
+    TileEmitPre<TBLOCK, kDynG0PhaseA, GAIT> emb(P.slots + it.slot, GAIT ? Vb + T.v0 : smem,
+                                                GAIT ? Gb : smem + lds_rows_off - T.r0, g0lane);
+    emb.nvals = P.want_jac ? T.v1 - T.v0 : 0;
+    emb.gon = P.want_g != 0;
+    __syncthreads();
+    if (g0lane) {
+      double fs[3] = {0, 0, 0}, ts[3] = {0, 0, 0};
+      const double* d = c.dyn_scratch + it.a2 * P.rb.n_ee * 6;
+      for (int ee = 0; ee < P.rb.n_ee; ++ee)
+        for (int e = 0; e < 3; ++e) { ts[e] += d[ee * 6 + e]; fs[e] += d[ee * 6 + 3 + e]; }
+      dyn_g0_b(c, it, emb, g0, fs, ts);
+    }
+  }
+  __syncthreads();
+  if constexpr (!GAIT) {
+    if (P.want_jac) copy_out(smem, Vb + T.v0, T.v1 - T.v0, threadIdx.x, KBLOCK);
+    if (P.want_g)
+      for (int i = threadIdx.x; i < T.r1 - T.r0; i += KBLOCK) __builtin_nontemporal_store(smem[lds_rows_off + i], Gb + T.r0 + i);
+  }
+}
+
+template <int TYPE, int BLOCK, bool GAIT, bool ROTVEC>
+// second argument: minimum waves per SIMD. Dynamic: 2 (fixed gait: 256 lanes, 2 blocks per CU; gait: the
+// 512-lane row-split block, <= 256 VGPRs)
+__global__ void __launch_bounds__(BLOCK, TYPE == IT_DYN ? 2 : 1) towr_tile_kernel(KParams P) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int total = P.B * P.ntiles;
+  const int per = (total + 7) / 8;
+  // XCD-aware mapping: work ids w and w+1 (tiles of one problem) share blockIdx % 8
+  const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+  if (w >= total) return;
+  tile_body<TYPE, BLOCK, BLOCK, GAIT, ROTVEC>(P, smem, w / P.ntiles, P.tile0 + w % P.ntiles, P.lds_x_off, P.lds_rows_off);
+}
+
+// The small kinds (node-value constraints, SplineAcc, BaseMotion, TotalDuration: a few kB of output
+// per problem each) in one launch: a block = kMiscWaves one-wave tiles of one problem, sharing the
+// staged x and node table; each wave evaluates and writes out its own tile.
+// BLOCK = the launch's block size (>= 64 kMiscWaves): waves past the group's tiles only help stage x.
+template <bool GAIT, int BLOCK = 64 * kMiscWaves>
+__device__ __forceinline__ void misc_body(const KParams& P, double* smem, int b, int group, int lds_x_off) {
+  static_assert(BLOCK >= 64 * kMiscWaves, "a small-kind group needs a wave per tile");
+  const int wave = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+  const int ti = wave < kMiscWaves ? P.misc_tiles[group * kMiscWaves + wave] : -1;
+  TileDesc T{};
+  ItemDesc it{};
+  it.type = IT_NONE;
+  it.slot = 0;
+  if (ti >= 0) {
+    T = P.tiles[ti];
+    it = P.items[T.i0 + lane];
+  }
+  const int32_t wl_off = ti >= 0 ? P.misc_lds[2 * (group * kMiscWaves + wave)] : 0;
+  const int32_t rows_off = ti >= 0 ? P.misc_lds[2 * (group * kMiscWaves + wave) + 1] : 0;
+  double* wl = smem + wl_off;
+  TileEmit<64, 3> em(P.slots + it.slot, wl, wl + rows_off - T.r0);
+  double* xs = smem + lds_x_off;
+  int32_t* ns = reinterpret_cast<int32_t*>(smem + lds_x_off + P.n_pad);
+  if constexpr (GAIT)   // sparse PhaseSpline emission: each wave zero-fills its own tile
+    if (ti >= 0) zero_lds(wl, T.v1 - T.v0, lane, 64);
+  stage_x<BLOCK, true>(P, P.X + (int64_t)b * P.ldx, xs, ns);
+  __syncthreads();
+  if (it.type != IT_NONE) {
+    Ctx c;
+    c.seg = nullptr; c.sg = P.sg; c.row = it.seg;
+    c.x = xs; c.nodecol = ns; c.spl = P.spl; c.dur = P.dur;
+    c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
+    c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
+    c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.pact = P.pact; c.sched = P.sched; c.eelin = P.eelin; c.lin = P.lin;
+    c.rotvec = false;   // no small kind uses the base orientation
+    c.dyn_scratch = nullptr;
+    switch (it.type) {   // wave-uniform: a wave holds one tile of one kind
+      case IT_FNODE: eval_fnode(c, it, em); break;
+      case IT_TERR: eval_height(c, it, sp_motion(it.ee), 0.0, em); break;
+      case IT_BMOT: eval_bmot(c, it, em); break;
+      case IT_SACC: eval_sacc(c, it, em); break;
+      case IT_BHGT: eval_height(c, it, SP_BASE_LIN, it.p0, em); break;
+      case IT_SWING: eval_swing(c, it, em); break;
+      case IT_TDUR: eval_tdur(c, it, em); break;
+      case IT_TQNODE: eval_tqnode(c, it, em); break;
+      case IT_THARD: eval_thard(c, it, em); break;
+      case IT_EELIN: eval_eelin(c, it, em); break;
+      case IT_LINEQ: eval_lineq(c, it, em); break;
+      default: break;
+    }
+  }
+  __syncthreads();
+  if (ti < 0) return;
+  double* Vb = P.V + (int64_t)b * P.ldv;
+  double* Gb = P.G + (int64_t)b * P.ldg;
+  if (P.want_jac) copy_out(wl, Vb + T.v0, T.v1 - T.v0, lane, 64);
+  if (P.want_g)
+    for (int i = lane; i < T.r1 - T.r0; i += 64) __builtin_nontemporal_store(wl[rows_off + i], Gb + T.r0 + i);
+}
+
+// The small kinds (node-value constraints, SplineAcc, BaseMotion, TotalDuration: a few kB of output
+// per problem each) in one launch: a block = kMiscWaves one-wave tiles of one problem, sharing the
+// staged x and node table; each wave evaluates and writes out its own tile.
+template <bool GAIT>
+__global__ void __launch_bounds__(64 * kMiscWaves, kMiscMinWaves) towr_misc_kernel(KParams P) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int total = P.B * P.ntiles;   // ntiles = groups per problem
+  const int per = (total + 7) / 8;
+  const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+  if (w >= total) return;
+  misc_body<GAIT>(P, smem, w / P.ntiles, w % P.ntiles, P.lds_x_off);
+}
+
+// Fused launches: a fusion group's classes run in ONE launch. A problem's units (its tiles of the
+// group's classes and its small-kind groups) are consecutive work ids, interleaved round-robin over
+// the classes, so latency-bound units (Dynamic, small kinds) share the CUs with write-bound ones and
+// no launch boundary drains the machine between the group's classes. Every unit runs the same code
+// as its per-class kernel (tile_body / misc_body). KBLOCK = the group's block size: 256 when it holds
+// Dynamic or the small kinds (192-lane tiles then leave the fourth wave to staging and copy-out),
+// else 192. The unit table is uniform per block (scalar loads). The kernel's register allocation is
+// the largest of its classes' (Dynamic: 242 VGPRs), which is what decides whether a group pays off.
+template <bool GAIT, bool ROTVEC, int KBLOCK>
+__global__ void __launch_bounds__(KBLOCK, (KBLOCK == 256 ? 2 : 1)) towr_step_kernel(KParams P) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int total = P.B * P.n_units;
+  const int per = (total + 7) / 8;
+  const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+  if (w >= total) return;
+  const int b = w / P.n_units;
+  const UnitDesc u = P.units[w % P.n_units];
+  switch (u.lc) {
+    case LC_ROM: tile_body<IT_ROM, 192, KBLOCK, GAIT, ROTVEC>(P, smem, b, u.tile, u.lds_x_off, u.lds_rows_off); break;
+    case LC_FDISC: tile_body<IT_FDISC, 192, KBLOCK, GAIT, false>(P, smem, b, u.tile, u.lds_x_off, u.lds_rows_off); break;
+    case LC_TQDISC: tile_body<IT_TQDISC, 192, KBLOCK, GAIT, false>(P, smem, b, u.tile, u.lds_x_off, u.lds_rows_off); break;
+    default:
+      if constexpr (KBLOCK == 256) {
+        if (u.lc == LC_DYN) tile_body<IT_DYN, 256, KBLOCK, GAIT, ROTVEC>(P, smem, b, u.tile, u.lds_x_off, u.lds_rows_off);
+        else misc_body<GAIT, KBLOCK>(P, smem, b, u.tile, u.lds_x_off);
+      } else if constexpr (KBLOCK >= 64 * kMiscWaves) {
+        if (u.lc == LC_MISC) misc_body<GAIT, KBLOCK>(P, smem, b, u.tile, u.lds_x_off);
+      }
+      break;
+  }
+}
+
+template <bool GAIT, bool ROTVEC>
+const void* kernel_for_mode(int type) {
+  switch (type) {
+    case IT_DYN: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_DYN, tile_block(IT_DYN, GAIT), GAIT, ROTVEC>);
+    case IT_ROM: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_ROM, tile_block(IT_ROM, GAIT), GAIT, ROTVEC>);
+    case IT_FDISC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_FDISC, tile_block(IT_FDISC, GAIT), GAIT, false>);
+    case IT_TQDISC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_TQDISC, tile_block(IT_TQDISC, GAIT), GAIT, false>);
+  }
+  return nullptr;
+}
+
+}  // namespace
+
+template <int KBLOCK>
+const void* step_kernel_kb(bool gait, bool rotvec) {
+  if (gait) return rotvec ? reinterpret_cast<const void*>(&towr_step_kernel<true, true, KBLOCK>) : reinterpret_cast<const void*>(&towr_step_kernel<true, false, KBLOCK>);
+  return rotvec ? reinterpret_cast<const void*>(&towr_step_kernel<false, true, KBLOCK>) : reinterpret_cast<const void*>(&towr_step_kernel<false, false, KBLOCK>);
+}
+const void* step_kernel_for(bool gait, bool rotvec, int kblock) {
+  return kblock == 256 ? step_kernel_kb<256>(gait, rotvec) : step_kernel_kb<192>(gait, rotvec);
+}
+
+const void* tile_kernel_for(int type, bool gait, bool rotvec) {
+  if (gait) return rotvec ? kernel_for_mode<true, true>(type) : kernel_for_mode<true, false>(type);
+  return rotvec ? kernel_for_mode<false, true>(type) : kernel_for_mode<false, false>(type);
+}
+const void* misc_kernel_for(bool gait) {
+  return gait ? reinterpret_cast<const void*>(&towr_misc_kernel<true>) : reinterpret_cast<const void*>(&towr_misc_kernel<false>);
+}
+
+}  // namespace tg

@@ -1,4 +1,6 @@
-// towr_gpu.hip — gfx950 kernel and C-ABI (include/towr_gpu.h) of the eval_g / eval_jac_g engine.
+// towr_gpu.hip — the C-ABI (include/towr_gpu.h) and host side of the eval_g / eval_jac_g engine: handle,
+// device tables, launch sequencing, host-pointer entry points. The kernels live in tiles.hip, fstream.hip,
+// gstream.hip and cost_traj.hip.
 //
 // One fused launch evaluates, for a batch of B problems sharing one layout, every constraint value
 // g and every Jacobian nonzero of ifopt's RowMajor CSR (what IpoptAdapter::eval_g / eval_jac_g
@@ -29,725 +31,6 @@
 
 using namespace tg;
 
-#ifndef TOWR_DYN_GAIT_LIN1_W   // minimum waves per SIMD of the 6-wave gait Dynamic block (layout.h TOWR_DYN_GAIT_LIN1)
-#define TOWR_DYN_GAIT_LIN1_W 4
-#endif
-#ifndef TOWR_EMIT_PAIR   // gait tile kernels: consecutive value stores paired into 16-byte stores (TileEmit::put);
-#define TOWR_EMIT_PAIR 0   // build option, not yet measured on the GPU (the box pool was unavailable): off
-#endif
-#ifndef TOWR_MISC_MINW   // small kinds: minimum waves per SIMD (5: 0.0267 -> 0.0257 ms per 4096 problems, A/B on one box)
-#define TOWR_MISC_MINW 5
-#endif
-#ifndef TOWR_ROM_GAIT_MINW   // gait RangeOfMotion (640 lanes): 5 = two blocks per CU (A/B build option)
-#define TOWR_ROM_GAIT_MINW 1
-#endif
-namespace {
-
-
-// Stores candidate j of this lane into the LDS tile at its tile-relative CSR position. Positions
-// come 8 per 16-byte SlotGroup; the next group is prefetched while the current one is consumed, so
-// the slot-table latency (L2: the table is shared by every problem of the batch) hides behind 8
-// candidates of arithmetic. The candidate's column is never needed on the device, and no item emits
-// a column twice (engine_math.h), so every position receives exactly one plain LDS store; absent
-// candidates (constant node values) go to a per-lane dummy slot, so the store needs no branch.
-// DIRECT (phase-duration optimisation): there is no LDS tile. The full-pattern Jacobian is ~90 %
-// zeros whose positions move with x, and an LDS tile of it held ~13 instants per block (one busy wave
-// of three, 2 blocks per CU), so the launch was bound by the evaluation's latency at low occupancy.
-// Instead each block zero-fills its tile's CSR range in V (zero_out), and after a barrier lanes store
-// their present candidates straight to HBM: `out` is the tile's first CSR value in V, `gout` the problem's g,
-// absent candidates (positions >= nvals, the dummy slots) are not stored. The lane's item may be
-// row-split (ItemDesc::rsel): only its rows' candidates are emitted (and counted), exactly as the
-// structure pass recorded them, and only those rows' g.
-template <int BLOCK, int DEPTH, bool DIRECT = false, int PRE = 1, int DYNG = 0>
-struct TileEmit {
-  static constexpr int kDynGroups = DYNG;   // Dynamic groups this emitter's kernel evaluates (engine_math.h)
-  static_assert(PRE >= 0 && PRE <= 6 && PRE <= kSlotSpare + 2, "preloaded slot groups: 0 .. 6, within the spare groups");
-  const SlotGroup* slot;   // this lane's group 0; group g at slot[g * BLOCK]
-  double* out;             // LDS tile, tile-relative (DIRECT: V at the tile's first value)
-  double* gout;            // LDS g rows, tile-relative (DIRECT: the problem's g)
-  SlotGroup q[DEPTH];      // groups g .. g + DEPTH - 1 in flight (q[0] = current)
-  int j = 0;
-  int flo = 0, fcnt = 0;   // DIRECT: the selected rows flo .. flo + fcnt - 1 (fcnt 0 = all rows)
-  int nvals = 0;           // DIRECT: values of the tile
-  ItemDirect dd{};         // DIRECT: column ranges stored at off + col without the slot table
-  bool fence = false;      // DIRECT: the wave's own zero-fill stores must complete before the first value store
-  int qg = 0;              // DIRECT: slot group held in q[0] (the ring reloads lazily, on use)
-  static constexpr bool kFilter = DIRECT;
-  __device__ __forceinline__ bool want(int row) const { return !DIRECT || fcnt == 0 || (unsigned)(row - flo) < (unsigned)fcnt; }
-  // DIRECT: slot groups 0 .. kPre - 1 are loaded at construction into named registers (a runtime-
-  // indexed array would go to scratch); on gfx950 vmcnt counts stores too, so a group loaded after the
-  // lane's first value stores waits for all of them (measured: the RangeOfMotion base lanes, 36
-  // slot-path candidates, were the gait tile's slowest waves)
-  static constexpr int kPre = DIRECT ? PRE : 0;
-  u32x4_t p0 = {}, p1 = {}, p2 = {}, p3 = {}, p4 = {}, p5 = {};   // native vectors: a SlotGroup (array) would go to scratch
-  __device__ __forceinline__ TileEmit(const SlotGroup* s, double* o, double* go) : slot(s), out(o), gout(go) {
-    if constexpr (DIRECT) {
-      const u32x4_t* sv = reinterpret_cast<const u32x4_t*>(s);
-      if (kPre > 0) p0 = sv[0];
-      if (kPre > 1) p1 = sv[BLOCK];
-      if (kPre > 2) p2 = sv[2 * BLOCK];
-      if (kPre > 3) p3 = sv[3 * BLOCK];
-      if (kPre > 4) p4 = sv[4 * BLOCK];
-      if (kPre > 5) p5 = sv[5 * BLOCK];
-      qg = -1;
-    } else {
-#pragma unroll
-      for (int d = 0; d < DEPTH; ++d) q[d] = s[d * BLOCK];
-    }
-  }
-  bool gon = true;         // DIRECT: g requested
-  __device__ __forceinline__ void g(int row, double v) {
-    if (!DIRECT) gout[row] = v;
-    else if (gon && want(row)) gout[row] = v;
-  }
-  // GAIT outputs are zero-filled before the evaluation (tile_body / misc_body), so candidates whose
-  // value is 0 can be skipped: move to candidate j + k, reloading the slot ring if the group changes
-  static constexpr bool kSparse = true;
-  __device__ __forceinline__ void skip(int k) {
-    if constexpr (DIRECT) {   // lazy: the next slot-path candidate loads its group
-      j += k;
-      return;
-    }
-    if (k <= 0) return;
-    const int g0 = j >> 3;
-    j += k;
-    const int g1 = j >> 3;
-    if (g1 != g0) {
-#pragma unroll
-      for (int d = 0; d < DEPTH; ++d) q[d] = slot[(g1 + d) * BLOCK];
-    }
-  }
-  __device__ __forceinline__ void operator()(int row, int col, double v, bool) {
-    if constexpr (DIRECT) {
-      // Direct-range candidates need no slot load. Slot-path groups load lazily: on gfx950 vmcnt
-      // counts stores too, so a group prefetched across this lane's value stores would wait for them.
-      if (!want(row)) return;
-      int s;
-      if (col >= dd.c0[0] && col < dd.c1[0]) {
-        s = dd.off[0] + col;
-      } else if (col >= dd.c0[1] && col < dd.c1[1]) {
-        s = dd.off[1] + col;
-      } else {
-        const int g = j >> 3;
-        if (g < kPre) {   // preloaded before any store of this lane (no wait behind the value stores)
-          const u32x4_t v = g == 0 ? p0 : g == 1 ? p1 : g == 2 ? p2 : g == 3 ? p3 : g == 4 ? p4 : p5;
-          const int k = j & 7;
-          const uint32_t lo = (k & 2) ? v.y : v.x, hi = (k & 2) ? v.w : v.z;
-          const uint32_t w = (k & 4) ? hi : lo;
-          s = (k & 1) ? (int)(w >> 16) : (int)(w & 0xFFFFu);
-        } else {
-          if (g != qg) {
-            q[0] = slot[g * BLOCK];
-            qg = g;
-          }
-          s = slot_pick(q[0], j & 7);
-        }
-      }
-      ++j;
-      if (fence) {   // wave-level: the zero stores of this wave's rows (tile_body) land first
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        fence = false;
-      }
-#ifdef TOWR_EXP_GAIT_NOSTORE   // timing experiment only: evaluate, but (almost) never store
-      if (s < nvals && v == 12345.678) out[s] = v;
-#else
-      if (s < nvals) put(s, v);
-#endif
-      return;
-    }
-#ifdef TOWR_EXPERIMENT_NOSLOT   // timing experiment only: wrong positions, no slot-table traffic
-    out[(threadIdx.x * 7 + j++) & 1023] = v;
-#else
-    const int s = slot_pick(q[0], j & 7);
-    ++j;
-    if ((j & 7) == 0) {
-#pragma unroll
-      for (int d = 0; d + 1 < DEPTH; ++d) q[d] = q[d + 1];
-      q[DEPTH - 1] = slot[((j >> 3) + DEPTH - 1) * BLOCK];
-    }
-    out[s] = v;   // absent candidates land in the lane's dummy slot
-#endif
-  }
-  // DIRECT value stores: an isolated 8-byte store costs a 32-byte write granule (tools/wcal.hip), so a value
-  // is held until the next one and two consecutive positions at a 16-byte boundary leave as one 16-byte store
-  int ps = -1;
-  double pv = 0.0;
-  __device__ __forceinline__ void put(int s, double v) {
-#if TOWR_EMIT_PAIR
-    if (ps >= 0) {
-      if (s == ps + 1 && (reinterpret_cast<uintptr_t>(out + ps) & 15) == 0) {
-        *reinterpret_cast<dbl2_t*>(out + ps) = dbl2_t{pv, v};
-        ps = -1;
-        return;
-      }
-      out[ps] = pv;
-    }
-    ps = s; pv = v;
-#else
-    out[s] = v;
-#endif
-  }
-  __device__ __forceinline__ void flush() {
-    if constexpr (DIRECT) {
-      if (ps >= 0) { out[ps] = pv; ps = -1; }
-    }
-  }
-};
-// Emitter for a fixed stretch of a lane's candidates J0 .. J0 + 8 NG - 1 whose slot groups are all
-// loaded at construction: Dynamic group 0 builds it before the block barrier that separates its two
-// phases, so phase B's slot loads complete during the barrier wait instead of once per 8 candidates
-// after it. Candidate indices must be compile-time constants (fully unrolled emission).
-template <int BLOCK, int J0, bool DIRECT = false>
-struct TileEmitPre {   // four groups: candidates J0 - J0 % 8 .. + 31
-  double* out;
-  double* gout;
-  int nvals = 0;   // DIRECT (see TileEmit): out / gout are V and g in HBM, dummy slots are not stored
-  bool gon = true;
-  SlotGroup q0, q1, q2, q3;   // named registers (a runtime-indexed array would go to scratch)
-  int j = J0;
-  __device__ __forceinline__ TileEmitPre(const SlotGroup* s, double* o, double* go, bool load) : out(o), gout(go) {
-    if (load) {
-      q0 = s[(J0 >> 3) * BLOCK]; q1 = s[((J0 >> 3) + 1) * BLOCK];
-      q2 = s[((J0 >> 3) + 2) * BLOCK]; q3 = s[((J0 >> 3) + 3) * BLOCK];
-    }
-  }
-  __device__ __forceinline__ void g(int row, double v) {
-    if (!DIRECT || gon) gout[row] = v;
-  }
-  __device__ __forceinline__ void operator()(int, int, double v, bool) {
-    const int k = (j >> 3) - (J0 >> 3);
-    SlotGroup q;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) q.w[w] = k == 0 ? q0.w[w] : k == 1 ? q1.w[w] : k == 2 ? q2.w[w] : q3.w[w];
-    const int s = slot_pick(q, j & 7);
-    ++j;
-    if (!DIRECT || s < nvals) out[s] = v;
-  }
-  __device__ __forceinline__ void flush() {}
-};
-static_assert(kDynG0Cand - (kDynG0PhaseA - kDynG0PhaseA % 8) <= 32, "phase B of Dynamic group 0 exceeds the preloaded groups");
-
-// Slot-group prefetch depth. Deeper rings only pay off where the emission index is a compile-time
-// constant: in a runtime loop, rotating the ring copies registers whose loads are still in flight
-// and waits for the newest one (measured: depth 4 made RangeOfMotion's base-angular wave slower).
-constexpr int slot_depth(int) { return 2; }
-static_assert(slot_depth(IT_ROM) <= kSlotSpare, "slot prefetch past the spare groups");
-
-// Slot groups preloaded by the gait (DIRECT) emitter per tile class: RangeOfMotion's base lanes emit
-// 33-36 slot-path candidates each (5 groups); Dynamic's kernel is at 256 VGPRs already (more spills)
-#ifndef TOWR_GAIT_SLOT_PRE_ROM
-#define TOWR_GAIT_SLOT_PRE_ROM 6
-#endif
-constexpr int gait_slot_pre(int type) { return type == IT_ROM ? TOWR_GAIT_SLOT_PRE_ROM : 1; }
-
-template <int TYPE, class Emit>
-__device__ __forceinline__ void eval_typed(const Ctx& c, const ItemDesc& it, Emit& em) {
-  if constexpr (TYPE == IT_DYN) eval_dyn(c, it, em);
-  else if constexpr (TYPE == IT_ROM) eval_rom(c, it, em);
-  else if constexpr (TYPE == IT_FDISC) eval_fdisc(c, it, em);
-  else if constexpr (TYPE == IT_FNODE) eval_fnode(c, it, em);
-  else if constexpr (TYPE == IT_TERR) eval_height(c, it, sp_motion(it.ee), 0.0, em);
-  else if constexpr (TYPE == IT_BMOT) eval_bmot(c, it, em);
-  else if constexpr (TYPE == IT_SACC) eval_sacc(c, it, em);
-  else if constexpr (TYPE == IT_BHGT) eval_height(c, it, SP_BASE_LIN, it.p0, em);
-  else if constexpr (TYPE == IT_SWING) eval_swing(c, it, em);
-  else if constexpr (TYPE == IT_TDUR) eval_tdur(c, it, em);
-  else if constexpr (TYPE == IT_TQDISC) eval_tqdisc(c, it, em);
-}
-
-// One block = one tile (consecutive instances of one constraint kind) of one problem; one item per
-// thread, laid out so every wave runs a single code path. Blocks of one problem share an XCD (the
-// mapping below), so its ~9 KB x is fetched from HBM once and then served by that XCD's L2.
-// Candidates land in an LDS tile (no global store before the end, so no load ever waits behind a
-// store: gfx950's vmcnt counts both); the tile's contiguous CSR range and g rows then leave with
-// 16-byte coalesced stores. Every kernel stages the problem's x in LDS (spline items gather their
-// nodes through the segment record's columns); node-value kinds also stage the node->column table.
-// The heavy kinds read spline nodes through the segment records; with phase-duration optimisation
-// (GAIT) their PhaseSplines evaluate polynomials from the node table, which is then staged too.
-constexpr bool stages_nodes(int type, bool gait) { return gait || is_misc_kind(type); }
-// Split staging (XStage: x loads issued before the item / slot loads) where it measured faster on
-// MI355X (ANYmal, B = 4096): Dynamic 0.0617 -> 0.0582 ms, ForceConstraintDiscretized 0.1018 ->
-// 0.098 ms; RangeOfMotion got slower (0.0838 -> 0.0878 ms) and the small kinds were unchanged, so
-// they stage after their item loads as before.
-constexpr bool early_stage(int type) { return type == IT_DYN || type == IT_FDISC; }
-
-
-// Body of one tile block. TBLOCK = the tile's lane count (its slot-table stride), KBLOCK = the
-// launch's block size (>= TBLOCK): in the fused launch a 192-lane tile runs in a 256-thread block,
-// whose extra wave only helps stage x and copy out.
-template <int TYPE, int TBLOCK, int KBLOCK, bool GAIT, bool ROTVEC>
-__device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b, int tile, int lds_x_off, int lds_rows_off) {
-  const TileDesc T = P.tiles[tile];
-  double* Vb = P.V + (int64_t)b * P.ldv;
-  double* Gb = P.G + (int64_t)b * P.ldg;
-  const double* xg = P.X + (int64_t)b * P.ldx;
-  // issue the lane's item, first slot groups and (below) the x / node-table staging loads together
-#ifdef TOWR_PHASE_TIMING
-  if (threadIdx.x < 64) { TSTAMP(0, TS_REAL()); TSTAMP(1, TS_MEM()); }
-#endif
-  // x (+ a zero at index n for constant node values) and, for node-value kinds, the node table:
-  // loads in flight first, then the lane's item and slot groups, then the LDS stores
-  XStage<KBLOCK, stages_nodes(TYPE, GAIT)> xst;
-  if constexpr (early_stage(TYPE)) xst.issue(P, xg);
-  ItemDesc it;
-  if (KBLOCK == TBLOCK || (int)threadIdx.x < TBLOCK) {
-    it = P.items[T.i0 + threadIdx.x];
-  } else {
-    it = ItemDesc{}; it.type = IT_NONE; it.slot = 0;
-  }
-  // GAIT: direct HBM emission into the zero-filled V (see TileEmit)
-  // gait Dynamic: the base-angular block runs in its own launch (towr_dyn_g1_kernel), after this one
-  TileEmit<TBLOCK, slot_depth(TYPE), GAIT, gait_slot_pre(TYPE), (GAIT && TYPE == IT_DYN) ? 1 : 0> em(
-      P.slots + it.slot, GAIT ? Vb + T.v0 : smem, GAIT ? Gb : smem + lds_rows_off - T.r0);
-  if constexpr (GAIT) {
-    if (it.rsel > 0) { em.flo = it.row0 + rsel_first(it.rsel); em.fcnt = rsel_count(it.rsel); }
-    em.nvals = P.want_jac ? T.v1 - T.v0 : 0;
-    em.gon = P.want_g != 0;
-    if (KBLOCK == TBLOCK || (int)threadIdx.x < TBLOCK) em.dd = P.idir[T.i0 + threadIdx.x];
-  }
-  double* xs = smem + lds_x_off;
-  int32_t* ns = reinterpret_cast<int32_t*>(smem + lds_x_off + P.n_pad);
-  char* gt = reinterpret_cast<char*>(smem + lds_x_off + P.n_pad + ((P.n_nodecol + 3) >> 2) * 2);   // GAIT tables
-  // GAIT: the block zero-fills its tile's CSR range first; the value stores of any lane come after
-  // the barrier below, which waits for these stores to complete (vmcnt(0)), so they land on top.
-  // FDISC / TQDISC lanes own whole rows (row-split), so there each wave zero-fills its own rows
-  // after the staging instead (below), and waits for them only at its first value store.
-  constexpr bool kWaveZero = GAIT && (TYPE == IT_FDISC || TYPE == IT_TQDISC);
-  // gait RangeOfMotion (Layout::rom_wave_zero): row lanes zero their rows after the base prefix, per wave,
-  // just before their own value stores; the base lanes store every base-prefix position
-  const bool rom_wz = GAIT && TYPE == IT_ROM && P.rom_wz != 0;
-#ifndef TOWR_EXP_GAIT_NOZERO   // timing experiment only: no zero-fill
-  if constexpr (GAIT && !kWaveZero)
-    if (P.want_jac && !rom_wz) zero_out(Vb + T.v0, T.v1 - T.v0, threadIdx.x, KBLOCK);
-#endif
-  if constexpr (early_stage(TYPE)) xst.commit(P, xg, xs, ns);
-  else stage_x<KBLOCK, stages_nodes(TYPE, GAIT)>(P, xg, xs, ns);
-  towr_terrain_t* ters = reinterpret_cast<towr_terrain_t*>(gt + 16 * P.gt_n16 + 8 * P.gt_ntime);   // GAIT: the terrain
-  if constexpr (GAIT) {
-    stage16<KBLOCK>(reinterpret_cast<uint4*>(gt), P.gtab, P.gt_n16);
-    if (threadIdx.x < sizeof(towr_terrain_t) / 8)
-      reinterpret_cast<double*>(ters)[threadIdx.x] = reinterpret_cast<const double*>(P.terrains + (P.terrain_per_problem ? b : 0))[threadIdx.x];
-    if constexpr (!kWaveZero) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-#ifdef TOWR_PHASE_TIMING
-  if (threadIdx.x < 64) TSTAMP(2, TS_MEM());
-#endif
-  Ctx c;
-  c.seg = nullptr; c.sg = P.sg; c.row = it.seg;
-  c.x = xs; c.nodecol = ns; c.spl = P.spl; c.dur = P.dur;
-  c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
-  c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
-  c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.pact = P.pact; c.sched = P.sched; c.eelin = P.eelin; c.lin = P.lin;
-  if constexpr (GAIT) {   // the PhaseSpline searches and window emission read their tables from LDS
-    c.spl = reinterpret_cast<const SplineMeta*>(gt + P.gt_off[0]);
-    c.sched = reinterpret_cast<const SchedInfo*>(gt + P.gt_off[1]);
-    c.pinfo = reinterpret_cast<const PolyPhase*>(gt + P.gt_off[2]);
-    c.pact = reinterpret_cast<const int32_t*>(gt + P.gt_off[3]);
-    c.pcols = reinterpret_cast<const PhaseCol*>(gt + P.gt_off[4]);
-  }
-  c.rotvec = ROTVEC;
-  c.dyn_scratch = TYPE == IT_DYN ? smem + P.lds_scr_off : nullptr;
-  if constexpr (GAIT) {
-    // the x-dependent PhaseSpline timings once per block (one thread per spline / endeffector)
-    // instead of a division-carrying scan per lane and spline evaluation
-    double* tm = reinterpret_cast<double*>(gt + 16 * P.gt_n16);
-    const int tid = threadIdx.x, nspl = P.n_spl, nee = P.rb.n_ee;
-    if (tid < nspl) {
-      if (c.spl[tid].ee >= 0) phase_spline_timings(c, tid, tm, tm + P.n_pinfo);
-    } else if (tid < nspl + nee) {
-      if (c.sched[tid - nspl].col0 >= 0) phase_end_timings(c, tid - nspl, tm + 2 * P.n_pinfo + (tid - nspl) * P.ph_stride);
-    }
-    __syncthreads();
-    c.pdur = tm; c.pend = tm + P.n_pinfo; c.phend = tm + 2 * P.n_pinfo; c.ph_stride = P.ph_stride;
-    c.ter = ters;   // LDS copy: no global load in the evaluation waits behind the zero-fill stores
-    if (kWaveZero || rom_wz) {
-#ifdef TOWR_EXP_GAIT_NOZERO
-      if (false) {
-#else
-      if (P.want_jac) {   // each lane's owned rows, zero-filled by its whole wave (512 B per store)
-#endif
-        double* vt = Vb + T.v0;
-        const int lane = threadIdx.x & 63;
-        for (int l = 0; l < 64; ++l) {
-          const int z0 = __shfl(em.dd.z0, l, 64), z1 = __shfl(em.dd.z1, l, 64);
-          for (int p = z0 + lane; p < z1; p += 64) vt[p] = 0.0;
-        }
-        em.fence = true;
-      }
-    }
-  }
-  DynG0 g0;   // DYN group 0 between its two phases
-#ifdef TOWR_EXP_GAIT_NOEVAL   // timing experiment only: staging + zero-fill, no evaluation
-  if (GAIT ? false : it.type == TYPE) {
-#else
-  if (it.type == TYPE) {
-#endif
-    if constexpr (TYPE == IT_DYN) {
-      if (it.group == 0) dyn_g0_a(c, it, em, g0);
-      else eval_dyn(c, it, em);   // group 1 and the endeffector groups (these deposit their sum terms)
-    } else {
-      eval_typed<TYPE>(c, it, em);
-    }
-    em.flush();
-  }
-  if constexpr (TYPE == IT_DYN) {   // phase B of group 0: the endeffector sums from LDS
-    const bool g0lane = it.type == TYPE && it.group == 0;
-    TileEmitPre<TBLOCK, kDynG0PhaseA, GAIT> emb(P.slots + it.slot, GAIT ? Vb + T.v0 : smem,
-                                                GAIT ? Gb : smem + lds_rows_off - T.r0, g0lane);
-    emb.nvals = P.want_jac ? T.v1 - T.v0 : 0;
-    emb.gon = P.want_g != 0;
-    __syncthreads();
-    if (g0lane) {
-      double fs[3] = {0, 0, 0}, ts[3] = {0, 0, 0};
-      const double* d = c.dyn_scratch + it.a2 * P.rb.n_ee * 6;
-      for (int ee = 0; ee < P.rb.n_ee; ++ee)
-        for (int e = 0; e < 3; ++e) { ts[e] += d[ee * 6 + e]; fs[e] += d[ee * 6 + 3 + e]; }
-      dyn_g0_b(c, it, emb, g0, fs, ts);
-    }
-  }
-#ifdef TOWR_PHASE_TIMING
-  if ((threadIdx.x >> 6) < 4) TSTAMP(3 + (threadIdx.x >> 6), TS_MEM());
-#endif
-  __syncthreads();
-#ifdef TOWR_PHASE_TIMING
-  if (threadIdx.x < 64) TSTAMP(7, TS_MEM());
-#endif
-  if constexpr (!GAIT) {
-    if (P.want_jac) copy_out(smem, Vb + T.v0, T.v1 - T.v0, threadIdx.x, KBLOCK);
-    if (P.want_g)
-      for (int i = threadIdx.x; i < T.r1 - T.r0; i += KBLOCK) __builtin_nontemporal_store(smem[lds_rows_off + i], Gb + T.r0 + i);
-  }
-#ifdef TOWR_PHASE_TIMING
-  if (threadIdx.x < 64) { TSTAMP(8, TS_MEM()); TSTAMP(9, TS_REAL()); }
-#endif
-}
-
-template <int TYPE, int BLOCK, bool GAIT, bool ROTVEC>
-// second argument: minimum waves per SIMD. Dynamic: 2 blocks per CU (fixed gait: 256 lanes, 2 waves per
-// SIMD, <= 256 VGPRs; gait, base-angular block in towr_dyn_g1_kernel: 384 lanes, 3 waves per SIMD,
-// <= 168 VGPRs, or with one wave per row 512 lanes, 4 waves per SIMD, <= 128 VGPRs)
-__global__ void __launch_bounds__(BLOCK, (TYPE == IT_DYN ? (GAIT ? (BLOCK <= 384 ? TOWR_DYN_GAIT_LIN1_W : 4) : 2) : (TYPE == IT_ROM && GAIT) ? TOWR_ROM_GAIT_MINW : 1)) towr_tile_kernel(KParams P) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int total = P.B * P.ntiles;
-  const int per = (total + 7) / 8;
-  // XCD-aware mapping: work ids w and w+1 (tiles of one problem) share blockIdx % 8
-  const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
-  if (w >= total) return;
-  tile_body<TYPE, BLOCK, BLOCK, GAIT, ROTVEC>(P, smem, w / P.ntiles, P.tile0 + w % P.ntiles, P.lds_x_off, P.lds_rows_off);
-}
-
-// Gait Dynamic's base-angular block (group 1: the Euler / RotVec chain rule through the base
-// orientation) in its own launch after the Dynamic tile kernel, one 64-lane block per (problem, tile):
-// its lanes are the tile's group-1 lanes (64 .. 127 of the tile block). In the tile kernel this path set
-// the register allocation of every wave (256 VGPRs, 1 block per CU); without it the tile kernel needs
-// ~135. The values land in the rows the tile kernel zero-filled (stream order), at their slot positions.
-template <bool ROTVEC>
-__global__ void __launch_bounds__(64, 1) towr_dyn_g1_kernel(KParams P) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int total = P.B * P.ntiles;
-  const int per = (total + 7) / 8;
-  const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
-  if (w >= total) return;
-  const int b = w / P.ntiles;
-  const TileDesc T = P.tiles[P.tile0 + w % P.ntiles];
-  const ItemDesc it = P.items[T.i0 + 64 + threadIdx.x];
-  TileEmit<tile_block(IT_DYN, true), 2, true, 6, 2> em(P.slots + it.slot, P.V + (int64_t)b * P.ldv + T.v0, P.G + (int64_t)b * P.ldg);
-  em.nvals = P.want_jac ? T.v1 - T.v0 : 0;
-  em.gon = false;   // group 1 writes no g rows
-  double* xs = smem;
-  int32_t* ns = reinterpret_cast<int32_t*>(smem + P.n_pad);
-  stage_x<64, false>(P, P.X + (int64_t)b * P.ldx, xs, ns);
-  __syncthreads();
-  if (it.type != IT_DYN || it.group != 1) return;
-  Ctx c;
-  c.seg = nullptr; c.sg = P.sg; c.row = it.seg;
-  c.x = xs; c.nodecol = ns; c.spl = P.spl; c.dur = P.dur;
-  c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
-  c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
-  c.gait = true; c.pinfo = P.pinfo; c.pcols = P.pcols; c.pact = P.pact; c.sched = P.sched; c.eelin = P.eelin; c.lin = P.lin;
-  c.rotvec = ROTVEC;
-  c.dyn_scratch = nullptr;
-  eval_dyn(c, it, em);
-  em.flush();
-}
-const void* dyn_g1_kernel_for(bool rotvec) {
-  return rotvec ? reinterpret_cast<const void*>(&towr_dyn_g1_kernel<true>) : reinterpret_cast<const void*>(&towr_dyn_g1_kernel<false>);
-}
-
-// The small kinds (node-value constraints, SplineAcc, BaseMotion, TotalDuration: a few kB of output
-// per problem each) in one launch: a block = kMiscWaves one-wave tiles of one problem, sharing the
-// staged x and node table; each wave evaluates and writes out its own tile.
-// BLOCK = the launch's block size (>= 64 kMiscWaves): waves past the group's tiles only help stage x.
-template <bool GAIT, int BLOCK = 64 * kMiscWaves>
-__device__ __forceinline__ void misc_body(const KParams& P, double* smem, int b, int group, int lds_x_off) {
-  static_assert(BLOCK >= 64 * kMiscWaves, "a small-kind group needs a wave per tile");
-  const int wave = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
-  const int ti = wave < kMiscWaves ? P.misc_tiles[group * kMiscWaves + wave] : -1;
-  TileDesc T{};
-  ItemDesc it{};
-  it.type = IT_NONE;
-  it.slot = 0;
-  if (ti >= 0) {
-    T = P.tiles[ti];
-    it = P.items[T.i0 + lane];
-  }
-  const int32_t wl_off = ti >= 0 ? P.misc_lds[2 * (group * kMiscWaves + wave)] : 0;
-  const int32_t rows_off = ti >= 0 ? P.misc_lds[2 * (group * kMiscWaves + wave) + 1] : 0;
-  double* wl = smem + wl_off;
-  TileEmit<64, 3> em(P.slots + it.slot, wl, wl + rows_off - T.r0);
-  double* xs = smem + lds_x_off;
-  int32_t* ns = reinterpret_cast<int32_t*>(smem + lds_x_off + P.n_pad);
-#ifdef TOWR_PHASE_TIMING
-  if (threadIdx.x < 64) { TSTAMP(0, TS_REAL()); TSTAMP(1, TS_MEM()); }
-#endif
-  if constexpr (GAIT)   // sparse PhaseSpline emission: each wave zero-fills its own tile
-    if (ti >= 0) zero_lds(wl, T.v1 - T.v0, lane, 64);
-  stage_x<BLOCK, true>(P, P.X + (int64_t)b * P.ldx, xs, ns);
-  __syncthreads();
-#ifdef TOWR_PHASE_TIMING
-  if (threadIdx.x < 64) TSTAMP(2, TS_MEM());
-#endif
-  if (it.type != IT_NONE) {
-    Ctx c;
-    c.seg = nullptr; c.sg = P.sg; c.row = it.seg;
-    c.x = xs; c.nodecol = ns; c.spl = P.spl; c.dur = P.dur;
-    c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
-    c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
-    c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.pact = P.pact; c.sched = P.sched; c.eelin = P.eelin; c.lin = P.lin;
-    c.rotvec = false;   // no small kind uses the base orientation
-    c.dyn_scratch = nullptr;
-    switch (it.type) {   // wave-uniform: a wave holds one tile of one kind
-      case IT_FNODE: eval_fnode(c, it, em); break;
-      case IT_TERR: eval_height(c, it, sp_motion(it.ee), 0.0, em); break;
-      case IT_BMOT: eval_bmot(c, it, em); break;
-      case IT_SACC: eval_sacc(c, it, em); break;
-      case IT_BHGT: eval_height(c, it, SP_BASE_LIN, it.p0, em); break;
-      case IT_SWING: eval_swing(c, it, em); break;
-      case IT_TDUR: eval_tdur(c, it, em); break;
-      case IT_TQNODE: eval_tqnode(c, it, em); break;
-      case IT_THARD: eval_thard(c, it, em); break;
-      case IT_EELIN: eval_eelin(c, it, em); break;
-      case IT_LINEQ: eval_lineq(c, it, em); break;
-      default: break;
-    }
-  }
-#ifdef TOWR_PHASE_TIMING
-  TSTAMP(3 + wave, TS_MEM());
-#endif
-  __syncthreads();
-#ifdef TOWR_PHASE_TIMING
-  if (threadIdx.x < 64) TSTAMP(7, TS_MEM());
-#endif
-  if (ti < 0) return;
-  double* Vb = P.V + (int64_t)b * P.ldv;
-  double* Gb = P.G + (int64_t)b * P.ldg;
-  if (P.want_jac) copy_out(wl, Vb + T.v0, T.v1 - T.v0, lane, 64);
-  if (P.want_g)
-    for (int i = lane; i < T.r1 - T.r0; i += 64) __builtin_nontemporal_store(wl[rows_off + i], Gb + T.r0 + i);
-#ifdef TOWR_PHASE_TIMING
-  if (threadIdx.x < 64) { TSTAMP(8, TS_MEM()); TSTAMP(9, TS_REAL()); }
-#endif
-}
-
-// The small kinds (node-value constraints, SplineAcc, BaseMotion, TotalDuration: a few kB of output
-// per problem each) in one launch: a block = kMiscWaves one-wave tiles of one problem, sharing the
-// staged x and node table; each wave evaluates and writes out its own tile.
-template <bool GAIT>
-__global__ void __launch_bounds__(64 * kMiscWaves, TOWR_MISC_MINW) towr_misc_kernel(KParams P) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int total = P.B * P.ntiles;   // ntiles = groups per problem
-  const int per = (total + 7) / 8;
-  const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
-  if (w >= total) return;
-  misc_body<GAIT>(P, smem, w / P.ntiles, w % P.ntiles, P.lds_x_off);
-}
-
-// Fused launches: a fusion group's classes run in ONE launch. A problem's units (its tiles of the
-// group's classes and its small-kind groups) are consecutive work ids, interleaved round-robin over
-// the classes, so latency-bound units (Dynamic, small kinds) share the CUs with write-bound ones and
-// no launch boundary drains the machine between the group's classes. Every unit runs the same code
-// as its per-class kernel (tile_body / misc_body). KBLOCK = the group's block size: 256 when it holds
-// Dynamic or the small kinds (192-lane tiles then leave the fourth wave to staging and copy-out),
-// else 192. The unit table is uniform per block (scalar loads). The kernel's register allocation is
-// the largest of its classes' (Dynamic: 242 VGPRs), which is what decides whether a group pays off.
-template <bool GAIT, bool ROTVEC, int KBLOCK>
-__global__ void __launch_bounds__(KBLOCK, (KBLOCK == 256 ? 2 : 1)) towr_step_kernel(KParams P) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int total = P.B * P.n_units;
-  const int per = (total + 7) / 8;
-  const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
-  if (w >= total) return;
-  const int b = w / P.n_units;
-  const UnitDesc u = P.units[w % P.n_units];
-  switch (u.lc) {
-    case LC_ROM: tile_body<IT_ROM, 192, KBLOCK, GAIT, ROTVEC>(P, smem, b, u.tile, u.lds_x_off, u.lds_rows_off); break;
-    case LC_FDISC: tile_body<IT_FDISC, 192, KBLOCK, GAIT, false>(P, smem, b, u.tile, u.lds_x_off, u.lds_rows_off); break;
-    case LC_TQDISC: tile_body<IT_TQDISC, 192, KBLOCK, GAIT, false>(P, smem, b, u.tile, u.lds_x_off, u.lds_rows_off); break;
-    default:
-      if constexpr (KBLOCK == 256) {
-        if (u.lc == LC_DYN) tile_body<IT_DYN, 256, KBLOCK, GAIT, ROTVEC>(P, smem, b, u.tile, u.lds_x_off, u.lds_rows_off);
-        else misc_body<GAIT, KBLOCK>(P, smem, b, u.tile, u.lds_x_off);
-      } else if constexpr (KBLOCK >= 64 * kMiscWaves) {
-        if (u.lc == LC_MISC) misc_body<GAIT, KBLOCK>(P, smem, b, u.tile, u.lds_x_off);
-      }
-      break;
-  }
-}
-template <int KBLOCK>
-const void* step_kernel_kb(bool gait, bool rotvec) {
-  if (gait) return rotvec ? reinterpret_cast<const void*>(&towr_step_kernel<true, true, KBLOCK>) : reinterpret_cast<const void*>(&towr_step_kernel<true, false, KBLOCK>);
-  return rotvec ? reinterpret_cast<const void*>(&towr_step_kernel<false, true, KBLOCK>) : reinterpret_cast<const void*>(&towr_step_kernel<false, false, KBLOCK>);
-}
-const void* step_kernel_for(bool gait, bool rotvec, int kblock) {
-  return kblock == 256 ? step_kernel_kb<256>(gait, rotvec) : step_kernel_kb<192>(gait, rotvec);
-}
-
-// Objective and gradient (IpoptAdapter::eval_f / eval_grad_f): one block per problem. The block
-// stages x and the node table in LDS and keeps the problem's dense gradient there; lanes take the
-// cost work items round-robin (grouped by kind, so waves mostly run one path) and add their
-// gradient entries with LDS atomics (ds_add_f64); f is reduced over the block. The gradient then
-// leaves with 16-byte non-temporal stores. The gradient's summation order is not fixed (atomics),
-// so it is reproducible to rounding only; f's order is fixed.
-template <bool GRAD>
-struct CostEmit {
-  double* grad;   // LDS; the dump slot at index n absorbs constant node values
-  double f = 0.0;
-  static constexpr bool kSparse = true;   // zero gradient contributions need no atomic
-  __device__ __forceinline__ void skip(int) {}
-  __device__ __forceinline__ void operator()(int, int col, double v, bool pres) {
-    if constexpr (GRAD)
-      if (pres && v != 0.0) atomicAdd(grad + col, v);
-  }
-};
-
-constexpr int kCostBlock = 256;
-template <bool GAIT, bool GRAD, bool ROTVEC>
-__global__ void __launch_bounds__(kCostBlock, 1) towr_cost_kernel(KParams P) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int b = blockIdx.x;
-  double* gs = smem;                       // [n_pad] gradient (+ dump slot at n)
-  double* xs = smem + P.n_pad;             // [n_pad] x (+ zero slot at n)
-  int32_t* ns = reinterpret_cast<int32_t*>(smem + 2 * P.n_pad);
-  double* red = smem + P.lds_red_off;     // [kCostBlock / 64] per-wave partial objectives
-  stage_x<kCostBlock, true>(P, P.X + (int64_t)b * P.ldx, xs, ns);
-  if constexpr (GRAD)
-    for (int i = threadIdx.x; i < P.n_pad; i += kCostBlock) gs[i] = 0.0;
-  __syncthreads();
-  CostEmit<GRAD> em{gs};
-  Ctx c;
-  c.x = xs; c.nodecol = ns; c.spl = P.spl; c.dur = P.dur;
-  c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
-  c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
-  c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.pact = P.pact; c.sched = P.sched; c.eelin = P.eelin; c.lin = P.lin;
-  c.rotvec = ROTVEC;
-  c.dyn_scratch = nullptr;
-  c.cq = P.cq;
-  for (int i = threadIdx.x; i < P.n_citems; i += kCostBlock) {
-    const CostItem it = P.citems[i];
-    c.seg = nullptr; c.sg = P.sg; c.row = it.seg;
-    eval_cost_item(c, it, em);
-  }
-  // SoftConstraint terms (soft_constraint.cc:52-69): 0.5 (g - b)^T (g - b) and J^T (g - b) over the
-  // wrapped sets' rows, from the soft child's g and CSR values of this problem (one row per lane)
-  if (P.s_m > 0) {
-    const double* sg = P.sG + (int64_t)b * P.s_ldg;
-    for (int r = threadIdx.x; r < P.s_m; r += kCostBlock) {
-      const double d = sg[r] - P.s_b[r];
-      em.f += (0.5 * d) * d;
-      if constexpr (GRAD) {
-        const double* sv = P.sV + (int64_t)b * P.s_ldv;
-        for (int k = P.s_rp[r]; k < P.s_rp[r + 1]; ++k) {
-          const double v = sv[k] * d;
-          if (v != 0.0) atomicAdd(gs + P.s_col[k], v);
-        }
-      }
-    }
-  }
-  // f: wave butterfly, then the waves' partials in order
-  double f = em.f;
-  for (int o = 32; o > 0; o >>= 1) f += __shfl_xor(f, o, 64);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = f;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double s = 0.0;
-    for (int w = 0; w < kCostBlock / 64; ++w) s += red[w];
-    P.F[b] = s;
-  }
-  if constexpr (GRAD) copy_out(gs, P.GR + (int64_t)b * P.ldgr, P.n, threadIdx.x, kCostBlock);
-}
-template <bool GAIT, bool GRAD>
-const void* cost_kernel_rv(bool rotvec) {
-  return rotvec ? reinterpret_cast<const void*>(&towr_cost_kernel<GAIT, GRAD, true>)
-                : reinterpret_cast<const void*>(&towr_cost_kernel<GAIT, GRAD, false>);
-}
-const void* cost_kernel_for(bool gait, bool grad, bool rotvec) {
-  if (gait) return grad ? cost_kernel_rv<true, true>(rotvec) : cost_kernel_rv<true, false>(rotvec);
-  return grad ? cost_kernel_rv<false, true>(rotvec) : cost_kernel_rv<false, false>(rotvec);
-}
-
-// Trajectory export (SaveTrajectoryToCSV): one 64-lane block per (problem, 64 sample times). Each
-// lane evaluates its sample's row into an LDS buffer kept column-major with an odd stride (writes and
-// reads both conflict-free); the block's rows are one contiguous output range, copied out coalesced.
-constexpr int kTrajBlock = 64;
-template <bool GAIT>
-__global__ void __launch_bounds__(kTrajBlock, 1) towr_traj_kernel(KParams P, const double* times, int ns, TrajPhases ph,
-                                                                   double* OUT, int64_t ldo, int32_t lds_x_off) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int nb = (ns + kTrajBlock - 1) / kTrajBlock;
-  const int b = blockIdx.x / nb, k0 = (blockIdx.x % nb) * kTrajBlock;
-  const int cols = traj_cols(P.rb.n_ee), stride = kTrajBlock + 1;
-  double* rows = smem;
-  double* xs = smem + lds_x_off;
-  int32_t* nsp = reinterpret_cast<int32_t*>(xs + P.n_pad);
-  stage_x<kTrajBlock, true>(P, P.X + (int64_t)b * P.ldx, xs, nsp);
-  __syncthreads();
-  const int k = k0 + (int)threadIdx.x;
-  if (k < ns) {
-    Ctx c;
-    c.seg = nullptr; c.row = -1;
-    c.x = xs; c.nodecol = nsp; c.spl = P.spl; c.dur = P.dur;
-    c.ter = P.terrains; c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
-    c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.pact = P.pact; c.sched = P.sched; c.eelin = P.eelin; c.lin = P.lin;
-    c.rotvec = false; c.dyn_scratch = nullptr;
-    traj_row(c, ph, times[k], rows + threadIdx.x, stride);
-  }
-  __syncthreads();
-  const int cnt = min(kTrajBlock, ns - k0);
-  double* out = OUT + (int64_t)b * ldo + (int64_t)k0 * cols;
-  for (int i = threadIdx.x; i < cnt * cols; i += kTrajBlock) {
-    const int r = i / cols, col = i - r * cols;
-    __builtin_nontemporal_store(rows[col * stride + r], out + i);
-  }
-}
-const void* traj_kernel_for(bool gait) {
-  return gait ? reinterpret_cast<const void*>(&towr_traj_kernel<true>) : reinterpret_cast<const void*>(&towr_traj_kernel<false>);
-}
-
-// DYN and ROM read the base orientation and come in Euler / RotVec variants; the others do not
-template <bool GAIT, bool ROTVEC>
-const void* kernel_for_mode(int type) {
-  switch (type) {
-    case IT_DYN: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_DYN, tile_block(IT_DYN, GAIT), GAIT, ROTVEC>);
-    case IT_ROM: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_ROM, tile_block(IT_ROM, GAIT), GAIT, ROTVEC>);
-    case IT_FDISC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_FDISC, tile_block(IT_FDISC, GAIT), GAIT, false>);
-    case IT_TQDISC: return reinterpret_cast<const void*>(&towr_tile_kernel<IT_TQDISC, tile_block(IT_TQDISC, GAIT), GAIT, false>);
-  }
-  return nullptr;
-}
-const void* kernel_for(int type, bool gait, bool rotvec) {
-  if (gait) return rotvec ? kernel_for_mode<true, true>(type) : kernel_for_mode<true, false>(type);
-  return rotvec ? kernel_for_mode<false, true>(type) : kernel_for_mode<false, false>(type);
-}
-const void* kernel_for_class(int lc, bool gait, bool rotvec, bool fstream = false, int gcls = -1) {
-  if (lc == LC_FDISC && gait && fstream) return fs_stream_kernel();   // the stream kernel (B); A: fs_inst_kernel()
-  if (gcls >= 0) return gs_stream_kernel(gcls);                       // the composer; the record kernel: gs_rec_kernel
-  if (lc == LC_MISC) return gait ? reinterpret_cast<const void*>(&towr_misc_kernel<true>) : reinterpret_cast<const void*>(&towr_misc_kernel<false>);
-  return kernel_for(class_type(lc), gait, rotvec);
-}
-
-
-}  // namespace
 
 // =================================================================================================
 // handle
@@ -789,6 +72,11 @@ struct towr_gpu_handle_s {
   GsGeo* d_gs_geo = nullptr;   // streaming RangeOfMotion / Dynamic tables (layout.h GsGeo)
   int32_t* d_gs_tmpl = nullptr;
   uint8_t* d_gs_pcode = nullptr;
+  GsSeg* d_gs_segs = nullptr;
+  uint8_t* d_gs_tseg = nullptr;
+  uint32_t* d_gs_vmap = nullptr;
+  int16_t* d_gs_ws = nullptr;
+  uint4* d_gs_blob = nullptr;
   GsBlock* d_gs_blk[GS_COUNT] = {};
   GsInst* d_gs_inst[GS_COUNT] = {};
   double* d_gsrec[GS_COUNT] = {};   // their records (scratch, grown on demand)
@@ -829,6 +117,7 @@ struct towr_gpu_handle_s {
   towr_terrain_t* d_terrain = nullptr;      // base terrain (1 entry)
   towr_terrain_t* d_bterrain = nullptr;     // per-problem batch terrains
   int32_t bterrain_n = 0;
+  std::vector<towr_terrain_t> bterrain_h;   // their host copy (the frozen-pattern check)
   // staging for host-pointer entry points
   double *d_x = nullptr, *d_g = nullptr, *d_v = nullptr;
   double *h_x = nullptr, *h_g = nullptr, *h_v = nullptr;
@@ -939,6 +228,13 @@ std::vector<uint4> gait_blob(const Layout& L) {
   std::memcpy(p + g.off[3], L.pact.data(), sizeof(int32_t) * L.pact.size());
   std::memcpy(p + g.off[4], L.pcols.data(), sizeof(PhaseCol) * L.pcols.size());
   return b;
+}
+
+const void* kernel_for_class(int lc, bool gait, bool rotvec, bool fstream = false, int gcls = -1) {
+  if (lc == LC_FDISC && gait && fstream) return fs_stream_kernel();   // the stream kernel (B); A: fs_inst_kernel()
+  if (gcls >= 0) return gs_stream_kernel(gcls);                       // the composer; the record kernel: gs_rec_kernel
+  if (lc == LC_MISC) return misc_kernel_for(gait);
+  return tile_kernel_for(class_type(lc), gait, rotvec);
 }
 
 // LDS of a launch class: [tile region(s) | x + zero slot | node table | GAIT: PhaseSpline tables]
@@ -1063,6 +359,7 @@ void fill_common(towr_gpu_handle h, KParams& P, int B, const double* X, int64_t 
   P.fsb = h->d_fsb; P.fs_t = h->d_fs_t; P.fs_tmpl = h->d_fs_tmpl; P.fs_ws = h->d_fs_ws;
   P.fs_iee = h->d_fs_iee; P.fs_irow = h->d_fs_irow;
   P.gs_geo = h->d_gs_geo; P.gs_tmpl = h->d_gs_tmpl; P.gs_pcode = h->d_gs_pcode;
+  P.gs_segs = h->d_gs_segs; P.gs_tseg = h->d_gs_tseg; P.gs_vmap = h->d_gs_vmap; P.gs_ws = h->d_gs_ws; P.gs_blob = h->d_gs_blob;
 }
 
 int launch_fused(towr_gpu_handle h, const towr_gpu_handle_s::FuseGroup& fg, int B, const double* X, int64_t ldx, double* G,
@@ -1104,6 +401,14 @@ int launch_fstream(towr_gpu_handle h, KParams& P, hipStream_t st) {
   return TOWR_OK;
 }
 
+// LDS of the record kernel of streaming class cls: the staging of fs_inst_lds_bytes (+ Dynamic: one
+// base-angular converter state per instant)
+size_t gs_rec_lds(const Layout& L, int cls) {
+  size_t b = fs_inst_lds_bytes(L);
+  if (cls == GS_DYN) b += L.gs_inst[GS_DYN].size() * ((gs_dyn_state_bytes(L.rotvec) + 15) & ~(size_t)15);
+  return b;
+}
+
 // The streaming RangeOfMotion / Dynamic path of class cls: record kernel into the handle's scratch, then
 // the composer over the class's GsBlocks. P comes from fill_common with ntiles = GsBlocks.
 int launch_gstream(towr_gpu_handle h, KParams& P, int cls, hipStream_t st) {
@@ -1117,8 +422,9 @@ int launch_gstream(towr_gpu_handle h, KParams& P, int cls, hipStream_t st) {
   double* rec = h->d_gsrec[cls];
   int64_t ldr_a = ldr;
   int32_t ni_a = ni;
-  void* aa[] = {&P, &rec, &ldr_a, &ni_a};
-  HIPCHK(h, hipLaunchKernel(gs_rec_kernel(cls, L.rotvec), dim3((unsigned)B), dim3(gs_rec_block()), aa, fs_inst_lds_bytes(L), st));
+  int32_t st_off = (int32_t)(fs_inst_lds_bytes(L) / sizeof(double));   // Dynamic: the per-instant states after the staging
+  void* aa[] = {&P, &rec, &ldr_a, &ni_a, &st_off};
+  HIPCHK(h, hipLaunchKernel(gs_rec_kernel(cls, L.rotvec), dim3((unsigned)B), dim3(gs_rec_block()), aa, gs_rec_lds(L, cls), st));
   const int64_t total = (int64_t)B * P.ntiles;
   const int64_t grid = ((total + 7) / 8) * 8;
   if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
@@ -1188,8 +494,6 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
     P.n = L.n; P.n_pad = (L.n + 2) & ~1; P.n_nodecol = (int32_t)L.nodecol.size();
     P.lds_x_off = (int32_t)lds_region(L, lc);
     P.want_g = want_g; P.want_jac = want_jac; P.fdisc_motion = L.fdisc_motion;
-    static const bool rom_block_zero = std::getenv("TOWR_GPU_ROM_BLOCKZERO") != nullptr;   // A/B switch: the block zero-fill
-    P.rom_wz = L.rom_wave_zero && !rom_block_zero ? 1 : 0;
     P.rb = L.rb;
     const int64_t total = (int64_t)B * nt;
     const int64_t grid = ((total + 7) / 8) * 8;
@@ -1198,9 +502,6 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
     void* args[] = {&P};
     HIPCHK(h, hipLaunchKernel(kernel_for_class(lc, L.gait, L.rotvec, L.fstream, gstream_cls(L, lc)), dim3((unsigned)grid), dim3((unsigned)block), args,
                               lds_bytes(L, lc), st));
-    if (lc == LC_DYN && L.gait)   // (tile path) its base-angular block, into the rows the tile kernel zero-filled
-      HIPCHK(h, hipLaunchKernel(dyn_g1_kernel_for(L.rotvec), dim3((unsigned)grid), dim3(64), args,
-                                sizeof(double) * (size_t)((L.n + 2) & ~1), st));
   }
   for (int i = 0; i < nside; ++i) {
     HIPCHK(h, hipEventRecord(h->join[i], h->side[i]));
@@ -1404,17 +705,22 @@ int host_eval(towr_gpu_handle h, int B, const double* X, double* G, double* V, b
   const bool gr = G && is_registered(h, G, gp * B), vr = V && is_registered(h, V, vp * B);
   double* gdst = gr ? G : h->h_g;   // D2H destinations
   double* vdst = vr ? V : h->h_v;
-  if (B == 1 && h->single.n_units > 0) {
-    // one problem, one launch, zero-copy: the kernel stages x from host memory and its copy-out writes
-    // g and the CSR values straight into host memory over PCIe (each value stored exactly once), so
-    // the call is one kernel and one synchronisation — no DMA command on either side
+  if (B == 1) {
+    // one problem, zero-copy: the kernels stage x from host memory and write g and the CSR values straight
+    // into host memory over PCIe (the tile copy-outs and the composers store each value exactly once), so
+    // the call is its launches and one synchronisation — no DMA command on either side. With fixed phase
+    // durations every class runs in ONE launch (the single group); under phase-duration optimisation the
+    // record kernels read x over PCIe and the composers stream the ~2 MB of values to the host.
     const double* xd = device_view(h, X, xb);
     if (!xd) { std::memcpy(h->h_x, X, xb); xd = h->hd_x; }
     double* gd = G ? device_view(h, G, gp) : nullptr;
     double* vd = V ? device_view(h, V, vp) : nullptr;
-    if (int rc = launch_fused(h, h->single, 1, xd, L.n, gd ? gd : h->hd_g, L.m, vd ? vd : h->hd_v, L.nnz, G != nullptr, V != nullptr,
-                              h->stream, ter, per))
-      return rc;
+    const int rc = h->single.n_units > 0
+                       ? launch_fused(h, h->single, 1, xd, L.n, gd ? gd : h->hd_g, L.m, vd ? vd : h->hd_v, L.nnz, G != nullptr,
+                                      V != nullptr, h->stream, ter, per)
+                       : launch(h, 1, xd, L.n, gd ? gd : h->hd_g, L.m, vd ? vd : h->hd_v, L.nnz, G != nullptr, V != nullptr, h->stream,
+                                ter, per, -1);
+    if (rc) return rc;
     HIPCHK(h, hipStreamSynchronize(h->stream));
     if (G && !gd) std::memcpy(G, h->h_g, gp);
     if (V && !vd) par_copy(V, h->h_v, vp);
@@ -1426,7 +732,7 @@ int host_eval(towr_gpu_handle h, int B, const double* X, double* G, double* V, b
   const size_t out_pp = (G ? gp : 0) + (V ? vp : 0) + 1;
   const int C = (int)std::max<size_t>(1, std::min<size_t>((size_t)B, (64u << 20) / out_pp));
   const int nch = (B + C - 1) / C;
-  if (nch == 1) {   // one chunk (and B = 1): everything on the handle's stream
+  if (nch == 1) {   // one chunk: everything on the handle's stream
     if (int rc = launch(h, B, h->d_x, L.n, h->d_g, L.m, h->d_v, L.nnz, G != nullptr, V != nullptr, h->stream, ter, per, -1))
       return rc;
     if (G) HIPCHK(h, hipMemcpyAsync(gdst, h->d_g, gp * B, hipMemcpyDeviceToHost, h->stream));
@@ -1527,23 +833,6 @@ extern "C" {
 
 int towr_gpu_abi_version(void) { return TOWR_GPU_ABI_VERSION; }
 
-#ifdef TOWR_PHASE_TIMING
-// timing build only (tools/phase_timing.py): device buffer of 16 u64 per block, or NULL
-// timing build only: the runtime's max resident blocks per CU of launch class lc (block, LDS as launched)
-int towr_gpu_debug_occupancy(towr_gpu_handle h, int32_t lc) {
-  const Layout& L = h->L;
-  if (lc < 0 || lc >= LC_COUNT || class_units(L, lc) == 0) return -1;
-  const int block = class_block(L, lc);
-  int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel_for_class(lc, L.gait, L.rotvec, L.fstream, gstream_cls(L, lc)), block, lds_bytes(L, lc)) != hipSuccess) return -2;
-  return n * 1000 + (int)(lds_bytes(L, lc) / 1024);
-}
-int towr_gpu_debug_set_timing_buffer(void* p) {
-  unsigned long long* v = reinterpret_cast<unsigned long long*>(p);
-  if (fs_set_timing_buffer(p) != hipSuccess) return TOWR_ERR_HIP;
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_tbuf), &v, sizeof(v)) == hipSuccess ? 0 : TOWR_ERR_HIP;
-}
-#endif
 int towr_gpu_num_kernels(void) { return LC_COUNT + towr_gpu_handle_s::kMaxFuse; }
 
 const char* towr_gpu_last_error(towr_gpu_handle h) {
@@ -1625,7 +914,9 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
       (r = upload(h, &h->d_fs_iee, L.fs_iee)) || (r = upload(h, &h->d_fs_irow, L.fs_irow)) ||
       (r = upload(h, &h->d_gs_geo, L.gs_geo)) || (r = upload(h, &h->d_gs_tmpl, L.gs_tmpl)) || (r = upload(h, &h->d_gs_pcode, L.gs_pcode)) ||
       (r = upload(h, &h->d_gs_blk[GS_ROM], L.gs_blocks[GS_ROM])) || (r = upload(h, &h->d_gs_blk[GS_DYN], L.gs_blocks[GS_DYN])) ||
-      (r = upload(h, &h->d_gs_inst[GS_ROM], L.gs_inst[GS_ROM])) || (r = upload(h, &h->d_gs_inst[GS_DYN], L.gs_inst[GS_DYN])))
+      (r = upload(h, &h->d_gs_inst[GS_ROM], L.gs_inst[GS_ROM])) || (r = upload(h, &h->d_gs_inst[GS_DYN], L.gs_inst[GS_DYN])) ||
+      (r = upload(h, &h->d_gs_segs, L.gs_segs)) || (r = upload(h, &h->d_gs_tseg, L.gs_tseg)) || (r = upload(h, &h->d_gs_vmap, L.gs_vmap)) ||
+      (r = upload(h, &h->d_gs_ws, L.gs_ws)) || (r = upload(h, &h->d_gs_blob, L.gs_blob)))
     return bail(r);
   if (hipEventCreateWithFlags(&h->scr_ev, hipEventDisableTiming) != hipSuccess) { h->err = "hipEventCreate failed"; return bail(TOWR_ERR_HIP); }
   {   // trajectory export: phase durations of the description (fixed gait), counts, contact at start
@@ -1713,12 +1004,13 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
   if (L.fstream || L.gstream[GS_ROM] || L.gstream[GS_DYN]) {   // the record kernels share fs_inst_lds_bytes' layout
     const size_t lds = fs_inst_lds_bytes(L);
     if (lds > 160 * 1024) { h->err = "problem too large for the streaming instant kernel's LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
-    if (lds > 64 * 1024) {
-      const void* ks[] = {fs_inst_kernel(), gs_rec_kernel(GS_ROM, L.rotvec), gs_rec_kernel(GS_DYN, L.rotvec)};
-      for (const void* k : ks)
-        if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
-          h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
-        }
+    const void* ks[] = {fs_inst_kernel(), gs_rec_kernel(GS_ROM, L.rotvec), gs_rec_kernel(GS_DYN, L.rotvec)};
+    const size_t need[] = {lds, gs_rec_lds(L, GS_ROM), gs_rec_lds(L, GS_DYN)};
+    for (int q = 0; q < 3; ++q) {
+      if (need[q] > 160 * 1024) { h->err = "problem too large for a record kernel's LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
+      if (need[q] > 64 * 1024 && hipFuncSetAttribute(ks[q], hipFuncAttributeMaxDynamicSharedMemorySize, (int)need[q]) != hipSuccess) {
+        h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
+      }
     }
   }
   {
@@ -1742,7 +1034,7 @@ int towr_gpu_destroy(towr_gpu_handle h) {
                  h->d_traj_pd, h->d_traj_n, h->d_traj_c0, h->d_traj_t, h->d_fsb, h->d_fs_t, h->d_fs_tmpl, h->d_fs_ws,
                  h->d_fs_iee, h->d_fs_irow, h->d_fsrec, h->d_lin, h->d_soft_b, h->d_soft_rp, h->d_soft_col, h->d_sg, h->d_sv,
                  h->single.d_units, h->d_gs_geo, h->d_gs_tmpl, h->d_gs_pcode, h->d_gs_blk[0], h->d_gs_blk[1], h->d_gs_inst[0],
-                 h->d_gs_inst[1], h->d_gsrec[0], h->d_gsrec[1]};
+                 h->d_gs_inst[1], h->d_gsrec[0], h->d_gsrec[1], h->d_gs_segs, h->d_gs_tseg, h->d_gs_vmap, h->d_gs_ws, h->d_gs_blob};
   if (h->device >= 0) for (void* p : dev) if (p) (void)hipFree(p);
   void* host[] = {h->h_x, h->h_g, h->h_v};
   for (void* p : host) if (p) (void)hipHostFree(p);
@@ -1910,17 +1202,19 @@ int towr_gpu_set_batch_terrain(towr_gpu_handle h, int32_t B, const towr_terrain_
   if (!h || B < 0 || (B > 0 && !terrains)) return fail(h, TOWR_ERR_INVALID, "bad argument");
   // The shared pattern holds only while every terrain keeps the base terrain's curvature class:
   // ForceConstraintDiscretized inserts motion entries only where f . d(basis) != 0 (quirk A22 iv).
-  for (int i = 0; i < B; ++i) {
+  // The shared pattern is the description's at x0. On a terrain without curvature it never moves; on curved
+  // (Gap) terrain the reference's moves with x and terrain: every problem is evaluated on the frozen pattern,
+  // and towr_gpu_pattern_outside_batch_device reports what the reference would add outside it. A batch
+  // terrain of another curvature class than the description's would change which blocks exist at all.
+  for (int i = 0; i < B; ++i)
     if (ter_has_curvature(terrains[i].id) != ter_has_curvature(h->L.terrain.id))
       return fail(h, TOWR_ERR_UNSUPPORTED, "batch terrain changes the Jacobian pattern (curvature class differs from the base terrain)");
-    if (ter_has_curvature(terrains[i].id) && B > 1)
-      return fail(h, TOWR_ERR_UNSUPPORTED, "Gap terrain has an x-dependent pattern; batch it one problem per handle");
-  }
   if (int rc = bind(h)) return rc;
-  if (h->d_bterrain) { (void)hipFree(h->d_bterrain); h->d_bterrain = nullptr; h->bterrain_n = 0; }
+  if (h->d_bterrain) { (void)hipFree(h->d_bterrain); h->d_bterrain = nullptr; h->bterrain_n = 0; h->bterrain_h.clear(); }
   if (B == 0) return TOWR_OK;
   std::vector<towr_terrain_t> v(terrains, terrains + B);
   if (int rc = upload(h, &h->d_bterrain, v)) return rc;
+  h->bterrain_h = v;
   h->bterrain_n = B;
   return TOWR_OK;
 }
@@ -1996,6 +1290,41 @@ int towr_gpu_eval_batch_device_kernel(towr_gpu_handle h, int32_t kernel, int32_t
     return launch_fused(h, h->fuse[g], B, X, ldx, G, ldg, V, ldv, 1, 1, reinterpret_cast<hipStream_t>(stream), ter, per);
   }
   return launch(h, B, X, ldx, G, ldg, V, ldv, 1, 1, reinterpret_cast<hipStream_t>(stream), ter, per, kernel);
+}
+
+// The frozen-pattern check runs on the host, with the structure pass's own arithmetic (engine_math.h at the
+// reference's operation order and std::pow): whether a motion block's scale is exactly 0.0 is a
+// floating-point tie that the device's correctly rounded powers can resolve differently from the
+// reference's libm (measured: a force residue of 2^-44 N at a phase junction on HyQ Gap).
+int towr_gpu_pattern_outside_batch_device(towr_gpu_handle h, int32_t B, const double* X, int64_t ldx, int32_t* counts, void* stream) {
+  if (!h || B < 0 || !X || !counts) return fail(h, TOWR_ERR_INVALID, "bad argument");
+  const Layout& L = h->L;
+  if (ldx < L.n) return fail(h, TOWR_ERR_INVALID, "leading dimension smaller than n");
+  if (B == 0) return TOWR_OK;
+  if (h->bterrain_n && h->bterrain_n != B)
+    return fail(h, TOWR_ERR_INVALID, "batch terrains are set for " + std::to_string(h->bterrain_n) + " problems, the call has " + std::to_string(B));
+  if (L.watch.empty()) { std::memset(counts, 0, sizeof(int32_t) * (size_t)B); return TOWR_OK; }
+  if (int rc = bind(h)) return rc;
+  std::vector<double> xh((size_t)B * L.n);
+  const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  HIPCHK(h, hipMemcpy2DAsync(xh.data(), sizeof(double) * L.n, X, sizeof(double) * ldx, sizeof(double) * L.n, B, hipMemcpyDeviceToHost, s));
+  HIPCHK(h, hipStreamSynchronize(s));
+  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const int nt = (int)std::min<int64_t>(hw, B);
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      for (int b = t; b < B; b += nt)
+        counts[b] = (int32_t)pattern_outside_host(L, xh.data() + (size_t)b * L.n, h->bterrain_n ? h->bterrain_h[b] : L.terrain);
+    });
+  for (auto& q : th) q.join();
+  return TOWR_OK;
+}
+
+int towr_gpu_pattern_outside(towr_gpu_handle h, const double* x, int64_t* count) {
+  if (!h || !x || !count) return fail(h, TOWR_ERR_INVALID, "null argument");
+  *count = pattern_outside_host(h->L, x, h->L.terrain);   // host only: layout-only handles answer too
+  return TOWR_OK;
 }
 
 int towr_gpu_eval_batch(towr_gpu_handle h, int32_t B, const double* X, double* G, double* V) {

@@ -277,6 +277,25 @@ class TowrGpuProblem:
                 out.append((k, name.value.decode(), nt.value, by.value))
         return out
 
+    def pattern_outside(self, x) -> int:
+        """Reference Jacobian entries at x outside the frozen (x0) pattern: non-zero only on curved terrain,
+        where ForceConstraintDiscretized / TorqueConstraintDiscretized blocks appear with x (towr_gpu.h)."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        c = C.c_int64()
+        self._check(self._lib.towr_gpu_pattern_outside(self._h, x.ctypes.data_as(capi._DP), C.byref(c)))
+        return int(c.value)
+
+    def pattern_outside_batch(self, X, counts, stream=None):
+        """pattern_outside of every problem of a device batch X (per-problem batch terrains as eval_batch_device)
+        into the host int32 array `counts`; synchronous (X is copied to the host and checked there)."""
+        import torch
+        _check_tensor(X, "X", self.n, self.device)
+        if not (isinstance(counts, np.ndarray) and counts.dtype == np.int32 and counts.flags.c_contiguous and counts.size >= X.shape[0]):
+            raise TowrGpuError("counts: contiguous int32 numpy array with one entry per problem expected")
+        s = stream.cuda_stream if stream is not None else torch.cuda.current_stream(X.device).cuda_stream
+        self._check(self._lib.towr_gpu_pattern_outside_batch_device(self._h, X.shape[0], C.c_void_p(X.data_ptr()), X.stride(0),
+                                                                     counts.ctypes.data_as(capi._IP), C.c_void_p(s)))
+
     def kernel_path(self, kernel: int) -> int:
         """Implementation of launch class `kernel` (0..4): 0 tile kernel, 1 record + stream kernels, -1 unused."""
         rc = self._lib.towr_gpu_kernel_path(self._h, kernel)
