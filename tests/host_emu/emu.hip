@@ -119,9 +119,29 @@ extern "C" int emu_cost(const towr_problem_desc_t* d, const double* x, double* f
 extern "C" int emu_stats(const towr_problem_desc_t* d) {
   Layout L; std::string e;
   if (build_layout(*d, L, e)) return -1;
-  std::printf("fstream %d blocks %zu tmpl_max %d rom_wave_zero %d\n", (int)L.fstream, L.fs_blocks.size(), L.fs_tmpl_max, (int)L.rom_wave_zero);
+  std::printf("fstream %d blocks %zu tmpl_max %d | gstream rom %d (%zu blocks) dyn %d (%zu blocks)\n", (int)L.fstream, L.fs_blocks.size(),
+              L.fs_tmpl_max, (int)L.gstream[GS_ROM], L.gs_blocks[GS_ROM].size(), (int)L.gstream[GS_DYN], L.gs_blocks[GS_DYN].size());
   std::printf("n %d m %d nnz %lld nodecol %zu | gait tables: spl %zu pinfo %zu pcols %zu pact %zu sched %zu\n", L.n, L.m,
               (long long)L.nnz, L.nodecol.size(), L.spl.size(), L.pinfo.size(), L.pcols.size(), L.pact.size(), L.sched.size());
+  {
+    auto a16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+    int phs = 0;
+    for (const SchedInfo& si : L.sched) phs = std::max(phs, (int)si.n_phases);
+    const size_t tabs = a16(sizeof(SplineMeta) * L.spl.size()) + a16(sizeof(SchedInfo) * L.sched.size()) + a16(sizeof(PolyPhase) * L.pinfo.size()) +
+                        a16(sizeof(int32_t) * L.pact.size()) + a16(sizeof(PhaseCol) * L.pcols.size());
+    std::printf("record staging bytes: x %zu nodecol %zu tables %zu (spl %zu pinfo %zu pact %zu pcols %zu) timings %zu | state euler %zu rv %zu\n",
+                8 * (size_t)((L.n + 2) & ~1), 16 * ((L.nodecol.size() + 3) / 4), tabs, sizeof(SplineMeta) * L.spl.size(),
+                sizeof(PolyPhase) * L.pinfo.size(), sizeof(int32_t) * L.pact.size(), sizeof(PhaseCol) * L.pcols.size(),
+                8 * (2 * L.pinfo.size() + L.sched.size() * phs), sizeof(DynEulerState), sizeof(DynRvState));
+  }
+  for (int cls = 0; cls < 2; ++cls) {
+    if (!L.gstream[cls]) continue;
+    long nv = 0; int maxnv = 0;
+    for (const GsBlock& bl : L.gs_blocks[cls]) { nv += bl.nv; maxnv = std::max(maxnv, bl.nv); }
+    std::printf("gstream %d: instants %zu blocks %zu nmax %d geo_max {%d %d %d %d} values %ld max/block %d\n", cls, L.gs_inst[cls].size(),
+                L.gs_blocks[cls].size(), L.gs_nmax[cls], L.gs_geo_max[cls][0], L.gs_geo_max[cls][1], L.gs_geo_max[cls][2],
+                L.gs_geo_max[cls][3], nv, maxnv);
+  }
   for (int t = 0; t < IT_COUNT; ++t) {
     int nt = L.type_tile0[t + 1] - L.type_tile0[t];
     if (!nt) continue;

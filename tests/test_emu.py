@@ -10,7 +10,7 @@ import pytest
 
 from oracle.oracle import Oracle
 from tests.configs import config_descs
-from tests.parity import assert_close, schedule_cols
+from tests.parity import assert_close, residue_cols
 from tests.gap_frozen import frozen_reference, is_gap
 from towr2025_amd import _capi as capi
 
@@ -46,4 +46,4 @@ def test_emulated_values_match_oracle(emu, name):
         g, ve = np.zeros(o.m), np.zeros(len(v))
         err = C.create_string_buffer(256)
         assert emu.emu_eval(C.byref(desc), x.ctypes.data_as(D), g.ctypes.data_as(D), ve.ctypes.data_as(D), err, 256) == 0, err.value
-        assert_close(o.eval_g(x), g, r, v, ve, o.m, f"{name} seed {seed}", cols_ref=c, floor_cols=schedule_cols(desc, o.n))
+        assert_close(o.eval_g(x), g, r, v, ve, o.m, f"{name} seed {seed}", cols_ref=c, floor_cols=residue_cols(desc, o.n))

@@ -21,7 +21,7 @@ import pytest
 
 from oracle.oracle import Oracle
 from tests.configs import ext_cases
-from tests.parity import assert_close, assert_cost_close, schedule_cols
+from tests.parity import assert_close, assert_cost_close, residue_cols
 from towr2025_amd import TowrGpuProblem
 from towr2025_amd import _capi as capi
 from towr2025_amd.problem import TowrGpuError
@@ -190,7 +190,7 @@ def test_emulated_linear_equality_matches_oracle(emu, name):
         assert emu.emu_eval_ex(C.byref(desc), len(data), arr, x.ctypes.data_as(D), g.ctypes.data_as(D),
                                v.ctypes.data_as(D), err, 256) == 0, err.value
         assert_close(o.eval_g(x), g, r, v_ref, v, o.m, f"{name} seed {seed}", cols_ref=c,
-                     floor_cols=schedule_cols(desc, o.n, data))
+                     floor_cols=residue_cols(desc, o.n, data))
 
 
 @pytest.mark.parametrize("name", ["biped_base_height_cost", "biped_gait_base_height_cost", "anymal_stairs_base_height_cost"])
@@ -257,7 +257,7 @@ def test_gpu_linear_equality(name):
     desc, data = CASES[name]
     o = Oracle(desc, data)
     p = TowrGpuProblem(desc, device=0, data=data)
-    fc = schedule_cols(desc, o.n, data)
+    fc = residue_cols(desc, o.n, data)
     for seed in (0, 1, 2):
         x = _x(o, seed)
         r, c, v_ref = o.eval_jac(x)

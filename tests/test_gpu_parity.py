@@ -8,7 +8,7 @@ import pytest
 
 from oracle.oracle import Oracle
 from tests.configs import config_descs, cost_descs
-from tests.parity import assert_close, assert_cost_close, schedule_cols
+from tests.parity import assert_close, assert_cost_close, residue_cols
 from tests.gap_frozen import frozen_reference, is_gap
 from towr2025_amd import TowrGpuProblem
 from towr2025_amd import formulation as F
@@ -33,7 +33,7 @@ def test_pattern_and_values(name):
     pr, pc = p.jac_structure()
     np.testing.assert_array_equal(pr, r)
     np.testing.assert_array_equal(pc, c)
-    fc = schedule_cols(desc, o.n)
+    fc = residue_cols(desc, o.n)
     worst = {"max_rel": 0.0, "worst": 0.0, "widened": 0}
     for seed in (0, 1, 2):
         x = x0 if seed == 0 else _perturb(x0, 20261015 + seed)
@@ -160,7 +160,7 @@ def test_fusion_groups(monkeypatch, spec, name):
     x = _perturb(o.initial_x(), 77)
     r, c, v_ref = o.eval_jac(x)
     g, v = p.eval_g_jac(x)
-    assert_close(o.eval_g(x), g, r, v_ref, v, o.m, f"{name} fuse {spec}", cols_ref=c, floor_cols=schedule_cols(desc, o.n))
+    assert_close(o.eval_g(x), g, r, v_ref, v, o.m, f"{name} fuse {spec}", cols_ref=c, floor_cols=residue_cols(desc, o.n))
 
 
 # Phase-duration optimisation: the streaming record + compose path (default) and the tile path it
@@ -173,7 +173,7 @@ def test_gait_paths(monkeypatch, name):
     x = _perturb(o.initial_x(), 91)
     r, c, _ = o.eval_jac(o.initial_x())   # the pattern is frozen at x0 (Gap: the reference's moves with x)
     v_ref = frozen_reference(o, r, c, x)[0] if is_gap(desc) else o.eval_jac(x)[2]
-    fc = schedule_cols(desc, o.n)
+    fc = residue_cols(desc, o.n)
     outs = {}
     for tiles, streams in ((None, None), ("1", None), (None, "1"), (None, "3")):
         for var, val in (("TOWR_GPU_GAIT_TILES", tiles), ("TOWR_GPU_STREAMS", streams)):
@@ -229,7 +229,7 @@ def test_gap_batch(name):
         o = Oracle(d)
         v_ref, outside = frozen_reference(o, r, c, X[b])
         assert counts[b] == outside, f"{name} problem {b}: {counts[b]} != {outside}"
-        assert_close(o.eval_g(X[b]), G[b], r, v_ref, V[b], o.m, f"{name} gap batch {b}", cols_ref=c, floor_cols=schedule_cols(d, o.n))
+        assert_close(o.eval_g(X[b]), G[b], r, v_ref, V[b], o.m, f"{name} gap batch {b}", cols_ref=c, floor_cols=residue_cols(d, o.n))
     assert np.isnan(Vd.cpu().numpy()[:, p.nnz:]).all()
 
 
@@ -319,7 +319,7 @@ def _batch_vs_single(base_f, name, B=64, optimize_timings=False):
             np.testing.assert_array_equal(rr, r)
             np.testing.assert_array_equal(cc, c)
             st = assert_close(o.eval_g(X[b]), G[b], r, v_ref, V[b], o.m, f"{name} problem {b}", cols_ref=c,
-                              floor_cols=schedule_cols(d, o.n))
+                              floor_cols=residue_cols(d, o.n))
             worst = max(worst, st["max_rel"])
         q.close()
     print(f"{name}: B = {B}, every problem bit-identical to B = 1; sample max relative error {worst:.3e}")

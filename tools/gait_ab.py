@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rotvec", action="store_true")
     ap.add_argument("--no-gait", action="store_true", help="the headline formulation (fixed phase durations)")
+    ap.add_argument("--only", default=None, help="comma-separated part names: time only these, no whole step")
     args = ap.parse_args()
     import torch
     from towr2025_amd import _capi as capi
@@ -39,10 +40,13 @@ def main():
     G = torch.empty((B, (p.m + 15) // 16 * 16), dtype=torch.float64, device=dev)
     V = torch.empty((B, (p.nnz + 15) // 16 * 16), dtype=torch.float64, device=dev)
     st = torch.cuda.current_stream(dev)
-    for _ in range(30):
+    only = args.only.split(",") if args.only else None
+    for _ in range(0 if only else 30):
         p.eval_batch_device(X, G, V)
     out = {}
     for k, name, nt, by in p.kernels():
+        if only and name not in only:
+            continue
         for _ in range(3):
             p.eval_batch_device_kernel(k, X, G, V, st)
         a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -54,6 +58,8 @@ def main():
         ms = a.elapsed_time(z) / args.reps
         out[name] = ms
         print(f"{args.lib or 'product':40s} {name:20s} {ms:8.4f} ms  {B * by / (ms * 1e-3) / 1e9:7.0f} GB/s", flush=True)
+    if only:
+        return
     a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record(st)
     for _ in range(args.reps):

@@ -11,7 +11,7 @@ for d in sys.argv[1:]:
         k = r["Kernel_Name"]
         if "towr" not in k:
             continue
-        key = k.split("towr_tile_kernel<")[-1].split(">")[0] if "towr_tile_kernel" in k else ("misc" if "misc" in k else k[:40])
+        key = k.split("towr_tile_kernel<")[-1].split(">")[0] if "towr_tile_kernel" in k else ("misc" if "misc" in k else k.replace("void tg::(anonymous namespace)::", "").split("(")[0])
         acc[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
         meta[key] = (r["Grid_Size"], r["Workgroup_Size"], r["LDS_Block_Size"], r["VGPR_Count"], r["Accum_VGPR_Count"], r["SGPR_Count"])
 for key, cs in acc.items():

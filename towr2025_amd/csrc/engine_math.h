@@ -264,46 +264,54 @@ TG_HD double cpow(double x, int k) {
 #endif
 }
 
-// GetDerivativeOf{Pos,Vel,Acc}Wrt{Start,End}Node (polynomial.cc:135-234); b = 0 n0.p, 1 n0.v, 2 n1.p, 3 n1.v
+// GetDerivativeOf{Pos,Vel,Acc}Wrt{Start,End}Node (polynomial.cc:140-234); b = 0 n0.p, 1 n0.v, 2 n1.p, 3 n1.v.
+// The reference's operations: std::pow powers (cpow), no contraction. At a polynomial's end a basis function
+// vanishes only up to rounding, and the residue, times a large scale, is an entry the reference emits; the
+// host precomputes the fixed-duration bases (SegRec) with these, so they are the reference's bit for bit.
 TG_HD void hermite_dpos(double T, double t, double H[4]) {
-  const double T2 = T * T, T3 = T2 * T, t2 = t * t, t3 = t2 * t;
+#pragma clang fp contract(off)
+  const double T2 = cpow(T, 2), T3 = cpow(T, 3), t2 = cpow(t, 2), t3 = cpow(t, 3);
   H[0] = (2 * t3) / T3 - (3 * t2) / T2 + 1;
   H[1] = t - (2 * t2) / T + t3 / T2;
   H[2] = (3 * t2) / T2 - (2 * t3) / T3;
   H[3] = t3 / T2 - t2 / T;
 }
 TG_HD void hermite_dvel(double T, double t, double H[4]) {
-  const double T2 = T * T, T3 = T2 * T, t2 = t * t;
+#pragma clang fp contract(off)
+  const double T2 = cpow(T, 2), T3 = cpow(T, 3), t2 = cpow(t, 2);
   H[0] = (6 * t2) / T3 - (6 * t) / T2;
   H[1] = (3 * t2) / T2 - (4 * t) / T + 1;
   H[2] = (6 * t) / T2 - (6 * t2) / T3;
   H[3] = (3 * t2) / T2 - (2 * t) / T;
 }
 TG_HD void hermite_dacc(double T, double t, double H[4]) {
-  const double T2 = T * T, T3 = T2 * T;
+#pragma clang fp contract(off)
+  const double T2 = cpow(T, 2), T3 = cpow(T, 3);
   H[0] = (12 * t) / T3 - 6 / T2;
   H[1] = (6 * t) / T2 - 4 / T;
   H[2] = 6 / T2 - (12 * t) / T3;
   H[3] = (6 * t) / T2 - 2 / T;
 }
 
-// CubicHermitePolynomial::UpdateCoeff (:97-104) + Polynomial::GetPoint (:47-58)
+// one dimension of poly_state from the polynomial's node values (n0.p, n0.v, n1.p, n1.v)
+TG_HD void poly_state_dim(double p0, double v0, double p1, double v1, double T, double tl, double& pp, double& vv, double& aa) {
+#pragma clang fp contract(off)
+  const double cf[4] = {p0, v0, -(3 * (p0 - p1) + T * (2 * v0 + v1)) / cpow(T, 2),
+                        (2 * (p0 - p1) + T * (v0 + v1)) / cpow(T, 3)};
+  pp = 0.0; vv = 0.0; aa = 0.0;
+  for (int k = 0; k < 4; ++k) pp += cpow(tl, k) * cf[k];
+  for (int k = 0; k < 4; ++k) vv += (k >= 1 ? k * cpow(tl, k - 1) : 0.0) * cf[k];
+  for (int k = 0; k < 4; ++k) aa += (k >= 2 ? k * (k - 1) * cpow(tl, k - 2) : 0.0) * cf[k];
+}
 TG_HD void poly_state(const Ctx& c, int s, int poly, double T, double tl, SplinePt& o) {
   // The reference's own operation order (std::pow, sum over coefficients), on the host and the
   // device alike: data-dependent structure predicates (ForceConstraintDiscretized's `scale == 0.0`,
   // force_constraint_discretized.cc:58) must resolve floating-point ties as the source does, and
   // near-zero velocities of PhaseSplines enter the duration derivatives.
-#pragma clang fp contract(off)
   for (int e = 0; e < 3; ++e) {
     const double p0 = xval(c, node_col(c, s, poly, kPos, e)), v0 = xval(c, node_col(c, s, poly, kVel, e));
     const double p1 = xval(c, node_col(c, s, poly + 1, kPos, e)), v1 = xval(c, node_col(c, s, poly + 1, kVel, e));
-    const double cf[4] = {p0, v0, -(3 * (p0 - p1) + T * (2 * v0 + v1)) / cpow(T, 2),
-                          (2 * (p0 - p1) + T * (v0 + v1)) / cpow(T, 3)};
-    double pp = 0.0, vv = 0.0, aa = 0.0;
-    for (int k = 0; k < 4; ++k) pp += cpow(tl, k) * cf[k];
-    for (int k = 0; k < 4; ++k) vv += (k >= 1 ? k * cpow(tl, k - 1) : 0.0) * cf[k];
-    for (int k = 0; k < 4; ++k) aa += (k >= 2 ? k * (k - 1) * cpow(tl, k - 2) : 0.0) * cf[k];
-    o.p[e] = pp; o.v[e] = vv; o.a[e] = aa;
+    poly_state_dim(p0, v0, p1, v1, T, tl, o.p[e], o.v[e], o.a[e]);
   }
 }
 
@@ -416,24 +424,6 @@ TG_HD void spline_eval(const Ctx& c, int s, double t, SplinePt& o) {
   }
   poly_state(c, s, o.poly, o.T, o.tl, o);
 #endif
-}
-
-// spline_eval with the reference's operations everywhere (Spline::GetPoint: the polynomial's coefficients and
-// std::pow-rounded powers, poly_state), also on the device for fixed durations, where spline_eval uses the
-// precomputed basis instead: for predicates on spline values that must resolve exactly as in the source
-TG_HD void spline_eval_ref(const Ctx& c, int s, double t, SplinePt& o) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  if (!(c.gait && c.spl[s].ee >= 0)) {
-    const size_t blk = (size_t)s * c.sg.ng + (c.row >> 5);
-    const double* D = c.sg.d + blk * (kSegDoubles * kSegGroup) + (c.row & 31);
-    const int32_t* I = c.sg.i + blk * (kSegInts * kSegGroup) + (c.row & 31);
-    o.dyn = false; o.H = nullptr;
-    o.poly = I[0]; o.tl = D[0]; o.T = D[kSegGroup];
-    poly_state(c, s, o.poly, o.T, o.tl, o);
-    return;
-  }
-#endif
-  spline_eval(c, s, t, o);
 }
 
 // Hermite basis of a spline point for derivative d (precomputed on the device, evaluated on the host)

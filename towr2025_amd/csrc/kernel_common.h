@@ -58,7 +58,6 @@ struct KParams {
   const int32_t* fs_irow;
   const GsGeo* gs_geo;            // streaming RangeOfMotion / Dynamic (layout.h GsGeo)
   const GsBlock* gs_blk;          // the launched class's compose blocks
-  const GsInst* gs_inst;          // the launched class's record instants
   const int32_t* gs_tmpl;
   const uint8_t* gs_pcode;
   const GsSeg* gs_segs;
@@ -83,10 +82,12 @@ struct KParams {
 
 // global -> LDS copy of n16 16-byte units: each thread issues up to K independent loads before its
 // first LDS write, so the staging costs one memory latency rather than one per loop trip
+// (BLOCK 0: the launch's block size, blockDim.x)
 template <int BLOCK>
 __device__ __forceinline__ void stage16(uint4* __restrict__ dst, const uint4* __restrict__ src, int n16) {
-  for (int i = threadIdx.x; i < n16; i += 4 * BLOCK) {   // 4 loads in flight per thread
-    const int i1 = i + BLOCK, i2 = i + 2 * BLOCK, i3 = i + 3 * BLOCK;
+  const int S = BLOCK > 0 ? BLOCK : (int)blockDim.x;
+  for (int i = threadIdx.x; i < n16; i += 4 * S) {   // 4 loads in flight per thread
+    const int i1 = i + S, i2 = i + 2 * S, i3 = i + 3 * S;
     const uint4 r0 = src[i];
     uint4 r1{}, r2{}, r3{};
     if (i1 < n16) r1 = src[i1];
@@ -199,7 +200,7 @@ __device__ __forceinline__ void stage_x(const KParams& P, const double* xg, doub
     stage16<BLOCK>(reinterpret_cast<uint4*>(xs), reinterpret_cast<const uint4*>(xg), P.n >> 1);
     if ((P.n & 1) && threadIdx.x == 0) xs[P.n - 1] = xg[P.n - 1];
   } else {
-    for (int i = threadIdx.x; i < P.n; i += BLOCK) xs[i] = xg[i];
+    for (int i = threadIdx.x; i < P.n; i += (BLOCK > 0 ? BLOCK : (int)blockDim.x)) xs[i] = xg[i];
   }
   if (threadIdx.x == 0) xs[P.n] = 0.0;
   if constexpr (NODES)

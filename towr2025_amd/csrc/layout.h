@@ -65,7 +65,7 @@ constexpr int kGsRowTypes = 6;
 constexpr int kGsAct = 4;
 constexpr int kGsBlock = 256;
 constexpr int kGsInstRom = 16;   // instants per compose block
-constexpr int kGsInstDyn = 4;
+constexpr int kGsInstDyn = 2;   // measured on MI355X (ANYmal gait, B = 1024, grouped composer): 2 -> 0.201 ms, 4 -> 0.230, 8 -> 0.219
 // A row type is cut into segments: its base prefix, each maximal run of template columns of one
 // (spline kind, endeffector) or of one endeffector's schedule. Per instant a segment owns W values
 // (GsSeg::vbase): the prefix and schedule segments all their positions, a PhaseSpline segment the
@@ -86,13 +86,33 @@ struct GsGeo {
   int32_t o_vmap, o_tmpl, o_tseg, o_pcode, o_ws, reserved[3];   // byte offsets of its sections (segments at 0)
 };
 struct GsBlock { int32_t geo, k0, n_inst, v0, nv, reserved[3]; };   // instants [k0, k0 + n_inst) of the geometry
-struct GsInst { double t; int32_t seg, ee, row0, reserved; };       // a record lane's instant
-constexpr int kRomRec = 38;    // R[9] | HL[4] | Ag[9] | HA[4] | poly | HP[4] | Jx.dx[3] v[3] cur
-constexpr int kDynBaseRec = 17;   // per instant: ab[3] | La[3] | Lp[3] | HpL[4] | HaL[4]
-constexpr int kDynAxisRec = 9;    // per (axis, instant): Ap[3] | Av[3] | Aa[3]
-constexpr int kDynHangRec = 12;   // per instant: the base-angular Hp[4] | Hv[4] | Ha[4]
-constexpr int kDynEeRec = 38;     // per (endeffector, instant): Fp Tqp Pp | polyF HF[4] | polyT HT[4] | polyP HP[4] | Jf | Jx
-TG_HD constexpr int64_t dyn_rec_doubles(int K, int E) { return (int64_t)(kDynBaseRec + 3 * kDynAxisRec + kDynHangRec + kDynEeRec * E) * K; }
+// a record lane's instant; kk / nb: its index in its GsBlock and the block's instants (the record chunk)
+struct GsInst { double t; int32_t seg, row0; int16_t ee, kk, nb, reserved; };
+// Records (gstream.hip towr_gs_rec_kernel): per instant RS fields, the composer's view of the instant —
+// ND doubles then NI ints (stored as doubles) — so that a composer block's prologue is one contiguous
+// copy. The fields of the GsBlock of instants [k0, k0 + n) form one chunk at RS * k0 (class-global
+// instant index), field-major inside it (field f of instant k0 + kk at RS * k0 + f * n + kk).
+//   RangeOfMotion: R[9] | HL[4] | Ag[axis][r] (9) | HA[4] | Jx.dx[3] v[3] | sums[dim][4] (12);
+//                  ints cur | qa[dim] (3) | poly
+//   Dynamic:       fs[3] | Lp[3] | HpL[4] | HaL[4] | A[axis][p v a][r] (27) | HpA HvA HaA (12), then per
+//                  endeffector Fp[3] | rv[3] | Jf.dx v[6] | Jx.dx v[6] | sums[kind][dim][4] (36);
+//                  ints per endeffector curF | curX | qa[kind][dim] (9) | poly[kind] (3)
+// (kind 0 motion, 1 force, 2 torque; sums / qa: the active-window basis sums of the PhaseSpline, the
+// first active PhaseCol of each dimension and the basis sums of up to kGsAct PhaseCols from it)
+constexpr int kRomND = 44, kRomNI = 5;
+constexpr int kDynBaseND = 53, kDynEeND = 54, kDynEeNI = 14;
+TG_HD constexpr int gs_rec_nd(int cls, int E) { return cls == GS_ROM ? kRomND : kDynBaseND + kDynEeND * E; }
+TG_HD constexpr int gs_rec_ni(int cls, int E) { return cls == GS_ROM ? kRomNI : kDynEeNI * E; }
+TG_HD constexpr int gs_rec_fields(int cls, int E) { return gs_rec_nd(cls, E) + gs_rec_ni(cls, E); }
+constexpr int kGsPre = 8;   // a composer thread's prefetched record doubles: chunks of at most kGsBlock * kGsPre
+// the record kernel's arguments (towr_gs_rec_kernel)
+struct GsRecArgs {
+  double* rec;                 // per problem: RangeOfMotion records at 0, Dynamic records at dyn_off
+  int64_t ldr, dyn_off;
+  const GsInst* inst[GS_COUNT];
+  int32_t K[GS_COUNT];         // instants per class (0: the class is not streamed)
+  int32_t st_off, scr_off;     // LDS (doubles): the Dynamic states, the scratch (9 per instant, 9 per (ee, instant))
+};
 
 // Pattern watch (curved terrain): ForceConstraintDiscretized / TorqueConstraintDiscretized add their
 // motion block of row i, dimension dim only where its scale is non-zero (force_constraint_discretized.cc:58,
@@ -250,13 +270,14 @@ const void* fs_stream_kernel();
 int fs_inst_block();
 
 // The streaming RangeOfMotion / Dynamic kernels (gstream.hip): compose LDS (bytes), record doubles
-// per problem, entry points. The record kernels use fs_inst_lds_bytes' LDS layout.
+// per problem of one class, entry points. The record kernel (both classes in one launch) uses
+// fs_inst_lds_bytes' LDS layout, then its Dynamic states and scratch (gs_rec_lds).
 size_t gs_stream_lds(const Layout& L, int cls);
 int64_t gs_record_doubles(const Layout& L, int cls);
-const void* gs_rec_kernel(int cls, bool rotvec);
+const void* gs_rec_kernel(bool rotvec);
 const void* gs_stream_kernel(int cls);
-int gs_rec_block();
-size_t gs_dyn_state_bytes(bool rotvec);   // the Dynamic record kernel's per-instant LDS state
+size_t gs_dyn_state_bytes(bool rotvec);   // the record kernel's per-Dynamic-instant LDS state
+constexpr int kGsRecMaxBlock = 512;
 // The frozen-pattern check (WatchItem): reference Jacobian entries at x outside the x0 pattern, evaluated
 // with the structure pass's arithmetic on the host
 int64_t pattern_outside_host(const Layout& L, const double* x, const towr_terrain_t& terrain);

@@ -606,6 +606,8 @@ bool build_gstream_class(Layout& L, int cls, const std::vector<BaseDec>& bdec, c
   int gmax[3] = {0, 0, 0}, nmax = 0;
   int cap = cls == GS_ROM ? kGsInstRom : kGsInstDyn;
   if (const char* e = std::getenv(cls == GS_ROM ? "TOWR_GS_ROM_INST" : "TOWR_GS_DYN_INST")) cap = std::max(1, std::min(64, std::atoi(e)));   // tuning (A/B)
+  cap = std::max(1, std::min(cap, kGsBlock * kGsPre / gs_rec_fields(cls, L.rb.n_ee)));   // a block's record chunk fits the prefetch
+  if (gs_rec_fields(cls, L.rb.n_ee) > kGsBlock * kGsPre) { why = "record larger than the composer's prefetch"; return false; }
   int tmax = 0, pmax = 0;
   for (const ConsInfo& cs : L.cons) {
     if (cs.kind != ctype || cs.rows == 0) continue;
@@ -614,11 +616,11 @@ bool build_gstream_class(Layout& L, int cls, const std::vector<BaseDec>& bdec, c
     g.cls = cls; g.ee = cls == GS_ROM ? cs.ee : -1; g.nrt = R; g.r0 = cs.row0;
     g.rec0 = (int32_t)insts.size();
     // the instants: time and segment row from the items of the set
-    std::vector<GsInst> its((size_t)K, GsInst{-1.0, -1, 0, 0, 0});
+    std::vector<GsInst> its((size_t)K, GsInst{-1.0, -1, 0, 0, 0, 0, 0});
     for (const ItemDesc& it : L.items)
       if (it.type == itype && it.row0 >= cs.row0 && it.row0 < cs.row0 + cs.rows) {
         GsInst& q = its[(it.row0 - cs.row0) / R];
-        q.t = it.t; q.seg = it.seg; q.ee = cls == GS_ROM ? cs.ee : 0; q.row0 = it.row0;
+        q.t = it.t; q.seg = it.seg; q.ee = (int16_t)(cls == GS_ROM ? cs.ee : 0); q.row0 = it.row0;
       }
     for (const GsInst& q : its) if (q.seg < 0) { why = "instant without items"; return false; }
     const int toff = (int)tmpl.size();
@@ -701,9 +703,17 @@ bool build_gstream_class(Layout& L, int cls, const std::vector<BaseDec>& bdec, c
       }
       g.ns = (int32_t)segs.size() - s0;
       g.vt = vbase;
+      // value slots grouped by segment kind (prefix, schedule, then windows by spline kind): the composer's
+      // value lanes run in wave-sized runs of one code path
+      std::vector<int> order((size_t)g.ns);
+      for (int q = 0; q < g.ns; ++q) order[q] = s0 + q;
+      auto rank = [&](const GsSeg& q) { return q.type == 0 ? 0 : q.type == 2 ? 1 : 2 + q.kind; };
+      std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return rank(segs[a]) < rank(segs[b]); });
+      vbase = 0;
+      for (int q : order) { segs[q].vbase = (int16_t)vbase; vbase += segs[q].W; }
       if (g.ns > 255 || vbase > 4096 || Lsum > 65535 || (int64_t)vbase * cap > 65535) { why = "segment tables exceed their encodings"; return false; }
-      for (int sg = 0; sg < g.ns; ++sg)
-        for (int q = 0; q < segs[s0 + sg].W; ++q) vmap.push_back((uint32_t)(sg << 16 | q));
+      for (int sg : order)
+        for (int q = 0; q < segs[sg].W; ++q) vmap.push_back((uint32_t)((sg - s0) << 16 | q));
       tseg.insert(tseg.end(), ts.begin(), ts.end());
       gmax[0] = std::max(gmax[0], Lsum); gmax[1] = std::max(gmax[1], g.ns); gmax[2] = std::max(gmax[2], vbase);
     }
@@ -728,6 +738,7 @@ bool build_gstream_class(Layout& L, int cls, const std::vector<BaseDec>& bdec, c
       nmax = std::max(nmax, b - a);
       bl.v0 = (int32_t)L.row_ptr[cs.row0 + R * a]; bl.nv = (int32_t)(L.row_ptr[cs.row0 + R * b] - L.row_ptr[cs.row0 + R * a]);
       if ((int64_t)bl.nv != (int64_t)(b - a) * Lsum) { why = "internal: block range"; return false; }
+      for (int k = a; k < b; ++k) { its[k].kk = (int16_t)(k - a); its[k].nb = (int16_t)(b - a); }
       blocks.push_back(bl);
     }
     insts.insert(insts.end(), its.begin(), its.end());

@@ -462,12 +462,13 @@ const void* kernel_for_mode(int type) {
 }  // namespace
 
 template <int KBLOCK>
-const void* step_kernel_kb(bool gait, bool rotvec) {
-  if (gait) return rotvec ? reinterpret_cast<const void*>(&towr_step_kernel<true, true, KBLOCK>) : reinterpret_cast<const void*>(&towr_step_kernel<true, false, KBLOCK>);
+const void* step_kernel_kb(bool rotvec) {
   return rotvec ? reinterpret_cast<const void*>(&towr_step_kernel<false, true, KBLOCK>) : reinterpret_cast<const void*>(&towr_step_kernel<false, false, KBLOCK>);
 }
+// fused launches exist only with fixed phase durations (setup_fusion: the gait layouts' tile blocks differ)
 const void* step_kernel_for(bool gait, bool rotvec, int kblock) {
-  return kblock == 256 ? step_kernel_kb<256>(gait, rotvec) : step_kernel_kb<192>(gait, rotvec);
+  if (gait) return nullptr;
+  return kblock == 256 ? step_kernel_kb<256>(rotvec) : step_kernel_kb<192>(rotvec);
 }
 
 const void* tile_kernel_for(int type, bool gait, bool rotvec) {

@@ -79,12 +79,13 @@ struct towr_gpu_handle_s {
   uint4* d_gs_blob = nullptr;
   GsBlock* d_gs_blk[GS_COUNT] = {};
   GsInst* d_gs_inst[GS_COUNT] = {};
-  double* d_gsrec[GS_COUNT] = {};   // their records (scratch, grown on demand)
-  int64_t gsrec_cap[GS_COUNT] = {};
+  double* d_gsrec = nullptr;   // their records, both classes (scratch, grown on demand)
+  int64_t gsrec_cap = 0;
   // The scratch above (and the soft child's g / values, d_sg / d_sv) is shared by every call on the
   // handle: a call on another stream than the previous one waits for the previous call's work (this
   // event), and growing a buffer waits for it on the host before the old one is freed.
   hipEvent_t scr_ev = nullptr;
+  int n_cu = 256;   // the device's compute units (launch sizing)
   hipStream_t scr_stream = nullptr;
   bool scr_used = false;
   // fusion groups (TOWR_GPU_FUSE, see towr_step_kernel): classes that run in one launch
@@ -401,36 +402,59 @@ int launch_fstream(towr_gpu_handle h, KParams& P, hipStream_t st) {
   return TOWR_OK;
 }
 
-// LDS of the record kernel of streaming class cls: the staging of fs_inst_lds_bytes (+ Dynamic: one
-// base-angular converter state per instant)
-size_t gs_rec_lds(const Layout& L, int cls) {
-  size_t b = fs_inst_lds_bytes(L);
-  if (cls == GS_DYN) b += L.gs_inst[GS_DYN].size() * ((gs_dyn_state_bytes(L.rotvec) + 15) & ~(size_t)15);
-  return b;
+// The record kernel (both streaming classes, one block per problem): its LDS is the staging of
+// fs_inst_lds_bytes, one base-angular converter state per Dynamic instant, then the Dynamic scratch
+// (9 doubles per instant and per (endeffector, instant)); its lanes, whole waves per kind (gstream.hip).
+int64_t gs_kd(const Layout& L) { return L.gstream[GS_DYN] ? (int64_t)L.gs_inst[GS_DYN].size() : 0; }
+size_t gs_state_stride(const Layout& L) { return (gs_dyn_state_bytes(L.rotvec) + 15) & ~(size_t)15; }
+size_t gs_rec_lds(const Layout& L) {
+  const size_t Kd = (size_t)gs_kd(L);
+  return fs_inst_lds_bytes(L) + Kd * gs_state_stride(L) + sizeof(double) * 9 * Kd * (1 + (size_t)L.rb.n_ee);
+}
+int gs_rec_threads(const Layout& L) {
+  const int64_t Kd = gs_kd(L), Kr = L.gstream[GS_ROM] ? (int64_t)L.gs_inst[GS_ROM].size() : 0;
+  const int64_t ee0 = (Kd + 63) & ~63, r0 = (ee0 + L.rb.n_ee * Kd + 63) & ~63;
+  const int64_t lanes = std::max<int64_t>(r0 + Kr, 4 * ((Kd + 63) & ~63));
+  return (int)std::min<int64_t>(kGsRecMaxBlock, std::max<int64_t>(64, (lanes + 63) & ~63));
 }
 
-// The streaming RangeOfMotion / Dynamic path of class cls: record kernel into the handle's scratch, then
-// the composer over the class's GsBlocks. P comes from fill_common with ntiles = GsBlocks.
-int launch_gstream(towr_gpu_handle h, KParams& P, int cls, hipStream_t st) {
+// The streaming RangeOfMotion / Dynamic path: the record kernel into the handle's scratch, then the
+// composer of each class (only: one class, for the per-class timings; -1 both) over its GsBlocks. A
+// composer block takes one GsBlock for a group of problems (b = g, g + ng, ...), the grid sized to one
+// round of resident blocks (its LDS and registers allow kGsResident per CU).
+constexpr int kGsResident = 6;   // 4-wave composer blocks per CU its registers allow (79 VGPRs)
+int launch_gstream(towr_gpu_handle h, KParams& P, int only, hipStream_t st) {
   const Layout& L = h->L;
   const int B = P.B;
-  const int32_t ni = (int32_t)L.gs_inst[cls].size();
-  const int64_t ldr = gs_record_doubles(L, cls);
-  if (int rc = scratch_grow(h, &h->d_gsrec[cls], &h->gsrec_cap[cls], B, ldr)) return rc;
-  P.gs_blk = h->d_gs_blk[cls];
-  P.gs_inst = h->d_gs_inst[cls];
-  double* rec = h->d_gsrec[cls];
-  int64_t ldr_a = ldr;
-  int32_t ni_a = ni;
-  int32_t st_off = (int32_t)(fs_inst_lds_bytes(L) / sizeof(double));   // Dynamic: the per-instant states after the staging
-  void* aa[] = {&P, &rec, &ldr_a, &ni_a, &st_off};
-  HIPCHK(h, hipLaunchKernel(gs_rec_kernel(cls, L.rotvec), dim3((unsigned)B), dim3(gs_rec_block()), aa, gs_rec_lds(L, cls), st));
-  const int64_t total = (int64_t)B * P.ntiles;
-  const int64_t grid = ((total + 7) / 8) * 8;
-  if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
-  const double* crec = rec;
-  void* ab[] = {&P, const_cast<double**>(&crec), &ldr_a, &ni_a};
-  HIPCHK(h, hipLaunchKernel(gs_stream_kernel(cls), dim3((unsigned)grid), dim3(kGsBlock), ab, gs_stream_lds(L, cls), st));
+  const int64_t lr = L.gstream[GS_ROM] ? gs_record_doubles(L, GS_ROM) : 0, ld = L.gstream[GS_DYN] ? gs_record_doubles(L, GS_DYN) : 0;
+  if (int rc = scratch_grow(h, &h->d_gsrec, &h->gsrec_cap, B, lr + ld)) return rc;
+  GsRecArgs A{};
+  A.rec = h->d_gsrec; A.ldr = lr + ld; A.dyn_off = lr;
+  for (int c = 0; c < GS_COUNT; ++c) {
+    A.inst[c] = h->d_gs_inst[c];
+    A.K[c] = L.gstream[c] ? (int32_t)L.gs_inst[c].size() : 0;
+  }
+  A.st_off = (int32_t)(fs_inst_lds_bytes(L) / sizeof(double));
+  A.scr_off = A.st_off + (int32_t)(gs_kd(L) * gs_state_stride(L) / sizeof(double));
+  void* aa[] = {&P, &A};
+  HIPCHK(h, hipLaunchKernel(gs_rec_kernel(L.rotvec), dim3((unsigned)B), dim3((unsigned)gs_rec_threads(L)), aa, gs_rec_lds(L), st));
+  if (!P.want_jac) return TOWR_OK;   // the g rows are the record kernel's
+  for (int cls = GS_COUNT - 1; cls >= 0; --cls) {
+    if (!L.gstream[cls] || (only >= 0 && only != cls)) continue;
+    P.gs_blk = h->d_gs_blk[cls];
+    P.ntiles = (int32_t)L.gs_blocks[cls].size();
+    const size_t lds = gs_stream_lds(L, cls);
+    const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(kGsResident, (int64_t)(160 * 1024) / (int64_t)lds));
+    const int64_t slots = per_cu * h->n_cu;
+    const int64_t ppb = std::max<int64_t>(1, ((int64_t)B * P.ntiles + slots - 1) / slots);   // problems per block
+    int32_t ng = (int32_t)((B + ppb - 1) / ppb);
+    const int64_t grid = (int64_t)ng * P.ntiles;
+    if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
+    const double* crec = h->d_gsrec + (cls == GS_DYN ? lr : 0);
+    int64_t ldr = lr + ld;
+    void* ab[] = {&P, const_cast<double**>(&crec), &ldr, &ng};
+    HIPCHK(h, hipLaunchKernel(gs_stream_kernel(cls), dim3((unsigned)grid), dim3(kGsBlock), ab, lds, st));
+  }
   return TOWR_OK;
 }
 
@@ -468,6 +492,7 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
     HIPCHK(h, hipEventRecord(h->fork, s));
     for (int i = 0; i < nside; ++i) HIPCHK(h, hipStreamWaitEvent(h->side[i], h->fork, 0));
   }
+  bool gs_done = false;
   for (int q = 0; q < nk; ++q) {
     const int lc = order[q];
     const int nt = class_units(L, lc);
@@ -479,8 +504,10 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
       if (int rc = launch_fstream(h, P, st)) return rc;
       continue;
     }
-    if (gstream_cls(L, lc) >= 0) {
-      if (int rc = launch_gstream(h, P, gstream_cls(L, lc), st)) return rc;
+    if (gstream_cls(L, lc) >= 0) {   // both streaming classes at the first one (one record kernel)
+      if (only_class < 0 && gs_done) continue;
+      gs_done = true;
+      if (int rc = launch_gstream(h, P, only_class < 0 ? -1 : gstream_cls(L, lc), st)) return rc;
       continue;
     }
     if (lc == LC_MISC) {
@@ -890,6 +917,7 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
   h->device = device;
   auto bail = [&](int code) { std::string m = h->err; towr_gpu_destroy(h); fail(nullptr, code, m); return code; };
   if (hipSetDevice(device) != hipSuccess) { h->err = "hipSetDevice failed"; return bail(TOWR_ERR_HIP); }
+  if (hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || h->n_cu <= 0) h->n_cu = 256;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
     h->err = std::string("device is ") + prop.gcnArchName + ", this build targets gfx950 only";
@@ -1004,9 +1032,9 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
   if (L.fstream || L.gstream[GS_ROM] || L.gstream[GS_DYN]) {   // the record kernels share fs_inst_lds_bytes' layout
     const size_t lds = fs_inst_lds_bytes(L);
     if (lds > 160 * 1024) { h->err = "problem too large for the streaming instant kernel's LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
-    const void* ks[] = {fs_inst_kernel(), gs_rec_kernel(GS_ROM, L.rotvec), gs_rec_kernel(GS_DYN, L.rotvec)};
-    const size_t need[] = {lds, gs_rec_lds(L, GS_ROM), gs_rec_lds(L, GS_DYN)};
-    for (int q = 0; q < 3; ++q) {
+    const void* ks[] = {fs_inst_kernel(), gs_rec_kernel(L.rotvec)};
+    const size_t need[] = {lds, gs_rec_lds(L)};
+    for (int q = 0; q < 2; ++q) {
       if (need[q] > 160 * 1024) { h->err = "problem too large for a record kernel's LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
       if (need[q] > 64 * 1024 && hipFuncSetAttribute(ks[q], hipFuncAttributeMaxDynamicSharedMemorySize, (int)need[q]) != hipSuccess) {
         h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
@@ -1034,7 +1062,7 @@ int towr_gpu_destroy(towr_gpu_handle h) {
                  h->d_traj_pd, h->d_traj_n, h->d_traj_c0, h->d_traj_t, h->d_fsb, h->d_fs_t, h->d_fs_tmpl, h->d_fs_ws,
                  h->d_fs_iee, h->d_fs_irow, h->d_fsrec, h->d_lin, h->d_soft_b, h->d_soft_rp, h->d_soft_col, h->d_sg, h->d_sv,
                  h->single.d_units, h->d_gs_geo, h->d_gs_tmpl, h->d_gs_pcode, h->d_gs_blk[0], h->d_gs_blk[1], h->d_gs_inst[0],
-                 h->d_gs_inst[1], h->d_gsrec[0], h->d_gsrec[1], h->d_gs_segs, h->d_gs_tseg, h->d_gs_vmap, h->d_gs_ws, h->d_gs_blob};
+                 h->d_gs_inst[1], h->d_gsrec, h->d_gs_segs, h->d_gs_tseg, h->d_gs_vmap, h->d_gs_ws, h->d_gs_blob};
   if (h->device >= 0) for (void* p : dev) if (p) (void)hipFree(p);
   void* host[] = {h->h_x, h->h_g, h->h_v};
   for (void* p : host) if (p) (void)hipHostFree(p);
