@@ -13,23 +13,26 @@ namespace {
 
 // Streaming ForceConstraintDiscretized under phase-duration optimisation (layout.h FsBlock). Every
 // Jacobian row of the path is the force set's full PhaseSpline pattern plus the schedule columns,
-// ~90 % exact zeros whose positions move with x. The tile path zero-filled the rows and scattered
-// 8-byte value stores over them (partial lines written twice, 1.25x the algorithmic bytes) and
-// evaluated each instant once per row. Here two launches split the work:
+// ~90 % exact zeros whose positions move with x. Two launches:
 //   A. towr_fdisc_inst_kernel, one block per problem, one lane per instant: fdisc_instant's result
-//      (the force polynomial, its position basis, the terrain basis n t1 t2, d force / d schedule)
-//      goes to a per-problem record array in HBM (the handle's scratch, kFsRec doubles per instant,
-//      field-major so a wave's stores coalesce); the instant's g rows go straight out;
-//   B. towr_fdisc_stream_kernel, one block per (problem, FsBlock): the block's records come in, each
-//      instant's pyramid rows b and the basis sums of the kFsWin columns its force polynomial can
-//      touch are formed in LDS, and the block's whole CSR range streams out with 16-byte
-//      non-temporal stores, each unit written once: an entry is b[i][e] * (basis sum) inside its
-//      instant's window, the schedule combination in the schedule columns, else 0.0
+//      in the stream kernel's form — the basis sums of the kFsWin columns the force polynomial can
+//      touch (phase_basis_sum over the instant's window of the template), the 5 pyramid rows b,
+//      d force / d schedule, the window start and dimension codes — goes to a per-problem record
+//      array in HBM (the handle's scratch); the instant's g rows go straight out. Records are
+//      chunk-major per FsBlock (field f of the block's instant kk at kFsRS t0 + f n + kk), so a
+//      stream block's prologue is one contiguous copy;
+//   B. towr_fdisc_stream_kernel, one block per (FsBlock, group of problems): per problem the block's
+//      record chunk (prefetched into registers while the previous problem streamed) goes to LDS,
+//      each row's window values b[i][e] * (basis sum) are formed once, and the block's whole CSR range
+//      streams out with 16-byte non-temporal stores, each unit written once: an entry is its row's
+//      window value inside the window, the schedule combination in the schedule columns, else 0.0
 //      (pyramid / phase_basis_sum / fdisc_sched_value: eval_fdisc's operations).
-// A is latency-bound but holds every instant of the batch in flight at once; B carries no
-// evaluation chain, so its blocks are small (LDS ~20 KB) and many, and it streams at the write ceiling.
-constexpr int kFsRec = 21;   // record: H[4] | n t1 t2 [9] | Jf.dx[3] | Jf.v[3] | poly | cur
+// record: Hv[kFsWin] | b[5][3] | Jf.dx[3] | Jf.v[3] | ints ws, wd, cur (64-bit integer bit patterns)
+constexpr int kFsB = kFsWin, kFsDx = kFsWin + 15, kFsV = kFsWin + 18, kFsND = kFsWin + 21;
+constexpr int kFsRS = kFsND + 3, kFsCS = kFsRS | 1;   // record fields; LDS stride per instant
 constexpr int kFsInstBlock = 512;
+__device__ __forceinline__ double fs_int(int v) { return __longlong_as_double((long long)v); }
+
 template <int BLOCK>
 __global__ void __launch_bounds__(BLOCK, 1) towr_fdisc_inst_kernel(KParams P, double* rec, int64_t ldr, int32_t ni) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -41,162 +44,159 @@ __global__ void __launch_bounds__(BLOCK, 1) towr_fdisc_inst_kernel(KParams P, do
   for (int k = tid; k < ni; k += BLOCK) {
     FdiscInstant o;
     fdisc_instant(c, P.fs_iee[k], P.fs_t[k], o);
-    double* r = R + k;
+    const FsBlock fb = P.fsb[P.fs_iblk[k]];
+    const int kk = k - fb.t0, nb = fb.n_inst;
+    double* r = R + (int64_t)kFsRS * fb.t0 + kk;
+    auto put = [&](int f, double v) { r[f * nb] = v; };
 #pragma unroll
-    for (int q = 0; q < 4; ++q) r[q * (int64_t)ni] = o.H[q];
+    for (int i = 0; i < 5; ++i)
 #pragma unroll
-    for (int q = 0; q < 3; ++q)
+      for (int e = 0; e < 3; ++e) put(kFsB + 3 * i + e, o.b[i][e]);
 #pragma unroll
-      for (int e = 0; e < 3; ++e) r[(4 + 3 * q + e) * (int64_t)ni] = o.nb[q][e];
-#pragma unroll
-    for (int e = 0; e < 3; ++e) { r[(13 + e) * (int64_t)ni] = o.Jf.dx[e]; r[(16 + e) * (int64_t)ni] = o.Jf.v[e]; }
-    r[19 * (int64_t)ni] = (double)o.poly;
-    r[20 * (int64_t)ni] = (double)o.Jf.cur;
+    for (int e = 0; e < 3; ++e) { put(kFsDx + e, o.Jf.dx[e]); put(kFsV + e, o.Jf.v[e]); }
+    put(kFsND + 2, fs_int(o.Jf.cur));
     if (P.want_g) {
       const int row = P.fs_irow[k];
 #pragma unroll
       for (int i = 0; i < 5; ++i) __builtin_nontemporal_store(o.g[i], Gb + row + i);
     }
+    const int poly = o.poly;
+    const int ws = P.fs_ws[2 * (fb.wsoff + poly)], wd = P.fs_ws[2 * (fb.wsoff + poly) + 1];
+    put(kFsND, fs_int(ws));
+    put(kFsND + 1, fs_int(wd));
+    double h0 = o.H[0], h1 = o.H[1], h2 = o.H[2], h3 = o.H[3];
+    asm volatile("" : "+v"(h0), "+v"(h1), "+v"(h2), "+v"(h3));
+    const int32_t* tm = P.fs_tmpl + fb.tmpl;
+#pragma unroll 4
+    for (int q = 0; q < kFsWin; ++q) {   // the window's basis sums (schedule entries: never read, 0)
+      const int pos = ws + q;
+      const int32_t te = pos < fb.L ? tm[pos] : -1;
+      put(q, te >= 0 ? phase_basis_sum(c.pcols[te & 0xFFFFFF], poly, h0, h1, h2, h3) : 0.0);
+    }
   }
 }
 
-// B. LDS: [per-instant records kFsInst x kFsD doubles | ints ws, wd, cur (kFsInst x 3) | PhaseCol per template entry]
-// Records are instant-major with an odd stride: a wave's lanes mostly read different fields of one or
-// two instants, which then fall in different banks (field-major, every field of an instant sat in
-// the same bank and the window reads serialized).
+// B. LDS: [per-instant records (stride kFsCS) | row window values (5 n x kFsWin) | row window starts (5 n)]
 constexpr int kFsUnits = 4;   // 16-byte units composed per lane before their stores
-constexpr int kFsD = 33;   // doubles per instant: window sums, b, d force / d schedule (dx, v)
-constexpr int kFsHv = 0, kFsB = kFsWin, kFsDx = kFsWin + 15, kFsV = kFsWin + 18;
-static_assert(kFsV + 3 == kFsD, "FsBlock LDS record");
+constexpr int kFsPre = (kFsInst * kFsRS + kFsBlock - 1) / kFsBlock;   // prefetched record doubles per thread
 template <int BLOCK>
-__global__ void __launch_bounds__(BLOCK, 1) towr_fdisc_stream_kernel(KParams P, const double* rec, int64_t ldr, int32_t ni) {
-  static_assert(BLOCK >= kFsInst, "one lane per instant in the prologue");
+__global__ void __launch_bounds__(BLOCK, 1) towr_fdisc_stream_kernel(KParams P, const double* rec, int64_t ldr, int32_t ng) {
+  static_assert(BLOCK == kFsBlock, "the prefetch is sized for kFsBlock");
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int total = P.B * P.ntiles;
-  const int per = (total + 7) / 8;
-  const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);   // a problem's blocks share an XCD
-  if (w >= total) return;
-  const int b = w / P.ntiles;
-  const FsBlock fb = P.fsb[w % P.ntiles];
-  const int tid = threadIdx.x;
+  // XCD-aware: blocks are dealt round-robin over the 8 XCDs; XCD x takes the contiguous range
+  // [x per, (x + 1) per) of (group, block) pairs, so each XCD writes whole problems' CSR ranges
+  const int per = (int)((gridDim.x + 7) / 8);
+  const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+  const int jt = w % P.ntiles, g0 = w / P.ntiles;
+  if (g0 >= ng || g0 >= P.B) return;   // the grid is rounded up to a multiple of 8
+  const FsBlock fb = P.fsb[jt];
+  const int tid = threadIdx.x, n = fb.n_inst, nr = 5 * n;
   double* cd = smem;
-  int32_t* ci = reinterpret_cast<int32_t*>(smem + kFsD * kFsInst);
-  PhaseCol* pcl = reinterpret_cast<PhaseCol*>(ci + 3 * kFsInst);
-  for (int j = tid; j < fb.L; j += BLOCK) {
-    const int32_t te = P.fs_tmpl[fb.tmpl + j];
-    // schedule entries: n = 0, a zero basis sum (never read: schedule columns are tested first)
-    const PhaseCol pq = P.pcols[te >= 0 ? (te & 0xFFFFFF) : 0];
-    pcl[j] = pq;
-    if (te < 0) pcl[j].n = 0;
+  double* rowv = cd + ((n * kFsCS + 1) & ~1);
+  int32_t* wsr = reinterpret_cast<int32_t*>(rowv + nr * kFsWin);
+  auto ci = [&](int k, int f) -> int { return *reinterpret_cast<const int32_t*>(cd + k * kFsCS + kFsND + f); };   // ws, wd, cur
+  // the chunk: element e = f * n + kk -> LDS kk * kFsCS + f
+  const int nch = n * kFsRS;
+  const int64_t chunk0 = (int64_t)kFsRS * fb.t0;
+  int dst[kFsPre];
+#pragma unroll
+  for (int q = 0; q < kFsPre; ++q) {
+    const int e = tid + q * BLOCK;
+    const int f = e / n, kk = e - f * n;
+    dst[q] = e >= nch ? -1 : kk * kFsCS + f;
   }
-  __syncthreads();
-  if (tid < fb.n_inst) {   // the instant's record -> b, window sums, schedule terms
-    const int k = tid;
-    const double* r = rec + (int64_t)b * ldr + fb.t0 + k;
-    double h[4], nb[3][3], bb[5][3];
+  double pre[kFsPre];
+  auto fetch = [&](int b) {
+    const double* src = rec + (int64_t)b * ldr + chunk0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) h[q] = r[q * (int64_t)ni];
-#pragma unroll
-    for (int q = 0; q < 3; ++q)
-#pragma unroll
-      for (int e = 0; e < 3; ++e) nb[q][e] = r[(4 + 3 * q + e) * (int64_t)ni];
-#pragma unroll
-    for (int e = 0; e < 3; ++e) { cd[k * kFsD + kFsDx + e] = r[(13 + e) * (int64_t)ni]; cd[k * kFsD + kFsV + e] = r[(16 + e) * (int64_t)ni]; }
-    const int poly = (int)r[19 * (int64_t)ni];
-    ci[3 * k + 2] = (int)r[20 * (int64_t)ni];
-    const double mu = P.terrains[P.terrain_per_problem ? b : 0].friction_coeff;
-    pyramid(nb[0], nb[1], nb[2], mu, bb);
-#pragma unroll
-    for (int i = 0; i < 5; ++i)
-#pragma unroll
-      for (int e = 0; e < 3; ++e) cd[k * kFsD + kFsB + 3 * i + e] = bb[i][e];
-    const int ws = P.fs_ws[2 * (fb.wsoff + poly)], wd = P.fs_ws[2 * (fb.wsoff + poly) + 1];
-    double h0 = h[0], h1 = h[1], h2 = h[2], h3 = h[3];
-    asm volatile("" : "+v"(h0), "+v"(h1), "+v"(h2), "+v"(h3));
-#pragma unroll
-    for (int q = 0; q < kFsWin; ++q) {
-      const int pos = ws + q;
-      double v = 0.0;
-      if (pos < fb.L) {
-        const PhaseCol pq = pcl[pos];
-        v = phase_basis_sum(pq, poly, h0, h1, h2, h3);
-      }
-      cd[k * kFsD + kFsHv + q] = v;
-    }
-    ci[3 * k] = ws; ci[3 * k + 1] = wd;
-  }
-  __syncthreads();
+    for (int q = 0; q < kFsPre; ++q) pre[q] = dst[q] >= 0 ? src[tid + q * BLOCK] : 0.0;
+  };
   const int Lr = fb.L, js0 = fb.js0, ns1 = fb.ns1;
   const float invL = 1.0f / (float)Lr;   // exact row of element e < 2^20 for rows <= 4096 long (|err| << 0.5 / Lr)
   // entry j of row r (instant k = r / 5, pyramid row i): eval_fdisc's value (see fdisc_sched_value / emit_dim)
   auto entry = [&](int r, int j) -> double {
-    const int k = r / 5, i = r - 5 * k;
     const unsigned js = (unsigned)(j - js0);
     if (js < (unsigned)ns1) {   // schedule column js: sched_val per dimension, then the b-weighted sum
-      const int cur = ci[3 * k + 2], col = (int)js;
+      const int k = r / 5, i = r - 5 * k;
+      const double* d = cd + k * kFsCS;
+      const int cur = ci(k, 2), col = (int)js;
       const bool last = cur == ns1;   // J.cur == J.n - 1
       double s0 = 0.0, s1 = 0.0, s2 = 0.0;
       if (col == cur && !last) {
-        s0 = cd[k * kFsD + kFsDx + 0]; s1 = cd[k * kFsD + kFsDx + 1]; s2 = cd[k * kFsD + kFsDx + 2];
+        s0 = d[kFsDx + 0]; s1 = d[kFsDx + 1]; s2 = d[kFsDx + 2];
       } else if (col < cur) {
-        const double v0 = cd[k * kFsD + kFsV + 0], v1 = cd[k * kFsD + kFsV + 1], v2 = cd[k * kFsD + kFsV + 2];
+        const double v0 = d[kFsV + 0], v1 = d[kFsV + 1], v2 = d[kFsV + 2];
         if (last) {
-          s0 = -v0 - cd[k * kFsD + kFsDx + 0]; s1 = -v1 - cd[k * kFsD + kFsDx + 1]; s2 = -v2 - cd[k * kFsD + kFsDx + 2];
+          s0 = -v0 - d[kFsDx + 0]; s1 = -v1 - d[kFsDx + 1]; s2 = -v2 - d[kFsDx + 2];
         } else {
           s0 = -v0; s1 = -v1; s2 = -v2;
         }
       }
-      return cd[k * kFsD + kFsB + 3 * i] * s0 + cd[k * kFsD + kFsB + 3 * i + 1] * s1 +
-             cd[k * kFsD + kFsB + 3 * i + 2] * s2;
+      return d[kFsB + 3 * i] * s0 + d[kFsB + 3 * i + 1] * s1 + d[kFsB + 3 * i + 2] * s2;
     }
-    const unsigned q = (unsigned)(j - ci[3 * k]);
-    if (q < (unsigned)kFsWin) {
-      const double v = cd[k * kFsD + kFsHv + q];
-      if (v == 0.0) return 0.0;
-      const int ed = (ci[3 * k + 1] >> (2 * q)) & 3;
-      return cd[k * kFsD + kFsB + 3 * i + ed] * v;
-    }
-    return 0.0;
+    const unsigned q = (unsigned)(j - wsr[r]);
+    return q < (unsigned)kFsWin ? rowv[r * kFsWin + q] : 0.0;
   };
   auto value = [&](int e) -> double {
     const int r = (int)(((float)e + 0.5f) * invL);
     return entry(r, e - r * Lr);
   };
-  if (P.want_jac) {
-    double* out = P.V + (int64_t)b * P.ldv + fb.v0;
-    const int n = fb.nv;
-    const int head = (reinterpret_cast<uintptr_t>(out) & 15) ? 1 : 0;
-    if (head && tid == 0) __builtin_nontemporal_store(value(0), out);
-    const int m2 = (n - head) >> 1;
-    dbl2_t* d2 = reinterpret_cast<dbl2_t*>(out + head);
-    // kFsUnits units per lane composed into registers first, then stored together, so a lane keeps
-    // kFsUnits stores in flight instead of one store per LDS round trip
-    for (int u0 = tid; u0 < m2; u0 += BLOCK * kFsUnits) {
-      dbl2_t v[kFsUnits];
+  int b = g0;
+  fetch(b);
+  for (;;) {
 #pragma unroll
-      for (int q = 0; q < kFsUnits; ++q) {
-        const int u = u0 + q * BLOCK;
-        const int e = head + 2 * u;
-        const int r = (int)(((float)e + 0.5f) * invL);
-        const int j = e - r * Lr;
-        v[q].x = u < m2 ? entry(r, j) : 0.0;
-        v[q].y = u < m2 ? (j + 1 < Lr ? entry(r, j + 1) : entry(r + 1, 0)) : 0.0;
-      }
-#pragma unroll
-      for (int q = 0; q < kFsUnits; ++q)
-        if (u0 + q * BLOCK < m2) __builtin_nontemporal_store(v[q], d2 + u0 + q * BLOCK);
+    for (int q = 0; q < kFsPre; ++q)
+      if (dst[q] >= 0) cd[dst[q]] = pre[q];
+    __syncthreads();
+    for (int t = tid; t < nr * kFsWin; t += BLOCK) {   // window value q of row r: b[i][e(q)] * basis sum (emit_dim)
+      const int r = t / kFsWin, q = t - r * kFsWin;
+      const int k = r / 5, i = r - 5 * k;
+      const double v = cd[k * kFsCS + q];
+      const int ed = (ci(k, 1) >> (2 * q)) & 3;
+      rowv[t] = v == 0.0 ? 0.0 : cd[k * kFsCS + kFsB + 3 * i + ed] * v;
     }
-    if (((n - head) & 1) && tid == 0) __builtin_nontemporal_store(value(n - 1), out + n - 1);
+    for (int t = tid; t < nr; t += BLOCK) wsr[t] = ci(t / 5, 0);
+    __syncthreads();
+    const int bn = b + ng;
+    if (bn < P.B) fetch(bn);   // in flight while this problem streams
+    if (P.want_jac) {
+      double* out = P.V + (int64_t)b * P.ldv + fb.v0;
+      const int nv = fb.nv;
+      const int head = (reinterpret_cast<uintptr_t>(out) & 15) ? 1 : 0;
+      if (head && tid == 0) __builtin_nontemporal_store(value(0), out);
+      const int m2 = (nv - head) >> 1;
+      dbl2_t* d2 = reinterpret_cast<dbl2_t*>(out + head);
+      // kFsUnits units per lane composed into registers first, then stored together, so a lane keeps
+      // kFsUnits stores in flight instead of one store per LDS round trip
+      for (int u0 = tid; u0 < m2; u0 += BLOCK * kFsUnits) {
+        dbl2_t v[kFsUnits];
+#pragma unroll
+        for (int q = 0; q < kFsUnits; ++q) {
+          const int u = u0 + q * BLOCK;
+          const int e = head + 2 * u;
+          const int r = (int)(((float)e + 0.5f) * invL);
+          const int j = e - r * Lr;
+          v[q].x = u < m2 ? entry(r, j) : 0.0;
+          v[q].y = u < m2 ? (j + 1 < Lr ? entry(r, j + 1) : entry(r + 1, 0)) : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < kFsUnits; ++q)
+          if (u0 + q * BLOCK < m2) __builtin_nontemporal_store(v[q], d2 + u0 + q * BLOCK);
+      }
+      if (((nv - head) & 1) && tid == 0) __builtin_nontemporal_store(value(nv - 1), out + nv - 1);
+    }
+    if (bn >= P.B) break;
+    b = bn;
+    __syncthreads();   // this problem's records and row values read before the next deposit
   }
 }
 
-
 }  // namespace
 
-size_t fs_region(const Layout& L) {   // stream kernel (B) LDS in doubles: records, ints, template PhaseCols
-  return (size_t)((kFsD * kFsInst + (3 * kFsInst) / 2 + (L.fs_tmpl_max * sizeof(PhaseCol) + 7) / 8 + 1) & ~1);
+size_t fs_region(const Layout& L) {   // stream kernel (B) LDS in doubles: records, row window values, row window starts
+  return (size_t)(((kFsInst * kFsCS + 1) & ~1) + 5 * kFsInst * kFsWin + (5 * kFsInst + 1) / 2 + 1) & ~(size_t)1;
 }
-int64_t fs_record_doubles() { return kFsRec; }
+int64_t fs_record_doubles() { return kFsRS; }
 const void* fs_inst_kernel() { return reinterpret_cast<const void*>(&towr_fdisc_inst_kernel<kFsInstBlock>); }
 const void* fs_stream_kernel() { return reinterpret_cast<const void*>(&towr_fdisc_stream_kernel<kFsBlock>); }
 int fs_inst_block() { return kFsInstBlock; }

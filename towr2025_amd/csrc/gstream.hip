@@ -51,8 +51,9 @@ __device__ __forceinline__ void gs_window(const Ctx& c, int s, int poly, const d
 //   [0, Kd)                  Dynamic instant k: the base-angular converter state (dyn_euler_state /
 //                            dyn_rv_state) into LDS; the base-linear and base-angular bases; ab, La, Lp
 //                            to the scratch;
-//   [ee0, ee0 + E Kd)        Dynamic (endeffector, instant): force / torque / motion PhaseSplines, their
-//                            active-window sums and schedule Jacobians; F, Tq, M to the scratch;
+//   [ee0, ee0 + 3 E Kd)      Dynamic (spline kind, endeffector, instant): the motion / force / torque
+//                            PhaseSpline, its active-window sums and schedule Jacobian; F, Tq, M to the
+//                            scratch (one chain per lane: the three splines no longer run in series);
 //   [r0, r0 + Kr)            RangeOfMotion instant (range_of_motion_constraint.cc:72-131, eval_rom); its
 //                            3 g rows go straight out;
 // then, after a barrier, per Dynamic instant: one lane per base-angular axis e reads the state and writes
@@ -87,7 +88,7 @@ __global__ void __launch_bounds__(kGsRecMaxBlock) __attribute__((amdgpu_waves_pe
   double* Rd = Rr + A.dyn_off;
   double* Gb = P.G + (int64_t)b * P.ldg;
   const int RSr = gs_rec_fields(GS_ROM, E), RSd = gs_rec_fields(GS_DYN, E), NDd = gs_rec_nd(GS_DYN, E);
-  const int ee0 = (Kd + 63) & ~63, r0 = (ee0 + EK + 63) & ~63;
+  const int ee0 = (Kd + 63) & ~63, r0 = (ee0 + 3 * EK + 63) & ~63;
   for (int i = tid; i < r0 + Kr; i += nthr) {
     if (i < Kd) {   // Dynamic instant
       const int k = i;
@@ -123,24 +124,22 @@ __global__ void __launch_bounds__(kGsRecMaxBlock) __attribute__((amdgpu_waves_pe
       spline_basis(st.A, kAcc, H);
 #pragma unroll
       for (int q = 0; q < 4; ++q) put(49 + q, H[q]);
-    } else if (i >= ee0 && i < ee0 + EK) {   // Dynamic endeffector ee of instant k
+    } else if (i >= ee0 && i < ee0 + 3 * EK) {   // Dynamic (spline kind, endeffector ee, instant k)
       const int idx = i - ee0;
-      const int ee = idx / Kd, k = idx - ee * Kd;
+      const int kind = idx / EK, rem = idx - kind * EK;   // kind 0 motion, 1 force, 2 torque
+      const int ee = rem / Kd, k = rem - ee * Kd;
       const GsInst gi = A.inst[GS_DYN][k];
       c.row = gi.seg;
       const double t = gi.t;
-      SplinePt F, Tq, M;
-      spline_eval(c, sp_force(ee), t, F);
-      spline_eval(c, sp_torque(ee), t, Tq);
-      spline_eval(c, sp_motion(ee), t, M);
-      double* sk = scr + 9 * Kd + 9 * idx;
+      const int sp = kind == 0 ? sp_motion(ee) : kind == 1 ? sp_force(ee) : sp_torque(ee);
+      SplinePt Sp;
+      spline_eval(c, sp, t, Sp);
+      double* sk = scr + 9 * Kd + 9 * rem + (kind == 0 ? 6 : kind == 1 ? 0 : 3);   // F | Tq | M
 #pragma unroll
-      for (int e = 0; e < 3; ++e) { sk[e] = F.p[e]; sk[3 + e] = Tq.p[e]; sk[6 + e] = M.p[e]; }
+      for (int e = 0; e < 3; ++e) sk[e] = Sp.p[e];
       const int fd = kDynBaseND + kDynEeND * ee, fi = NDd + kDynEeNI * ee;
       auto put = [&](int f, double v) { *gs_field(Rd, RSd, k, gi, f) = v; };
-#pragma unroll
-      for (int e = 0; e < 3; ++e) put(fd + e, F.p[e]);
-      auto window = [&](int kind, const SplinePt& Sp, int sp) {   // kind 0 motion, 1 force, 2 torque
+      {   // the active window's basis sums
         double H[4], sums[3][kGsAct];
         int qa[3];
         spline_basis(Sp, kPos, H);
@@ -152,17 +151,18 @@ __global__ void __launch_bounds__(kGsRecMaxBlock) __attribute__((amdgpu_waves_pe
 #pragma unroll
           for (int q = 0; q < kGsAct; ++q) put(fd + 18 + (3 * kind + e) * kGsAct + q, sums[e][q]);
         }
-      };
-      window(0, M, sp_motion(ee));
-      window(1, F, sp_force(ee));
-      window(2, Tq, sp_torque(ee));
-      SchedJac Jf, Jx;   // force and ee-position terms (dynamic_constraint.cc:116-122; no torque term)
-      sched_jac(c, sp_force(ee), t, F, Jf);
-      sched_jac(c, sp_motion(ee), t, M, Jx);
+      }
+      if (kind < 2) {   // force and ee-position schedule terms (dynamic_constraint.cc:116-122; no torque term)
+        SchedJac J;
+        sched_jac(c, sp, t, Sp, J);
+        const int o = kind == 1 ? 6 : 12;
 #pragma unroll
-      for (int e = 0; e < 3; ++e) { put(fd + 6 + e, Jf.dx[e]); put(fd + 9 + e, Jf.v[e]); put(fd + 12 + e, Jx.dx[e]); put(fd + 15 + e, Jx.v[e]); }
-      put(fi, gs_int(Jf.cur));
-      put(fi + 1, gs_int(Jx.cur));
+        for (int e = 0; e < 3; ++e) { put(fd + o + e, J.dx[e]); put(fd + o + 3 + e, J.v[e]); }
+        put(fi + (kind == 1 ? 0 : 1), gs_int(J.cur));
+        if (kind == 1)
+#pragma unroll
+          for (int e = 0; e < 3; ++e) put(fd + e, Sp.p[e]);
+      }
     } else if (i >= r0) {   // RangeOfMotion instant
       const int k = i - r0;
       const GsInst gi = A.inst[GS_ROM][k];
@@ -365,8 +365,12 @@ template <int CLS>
 __global__ void __launch_bounds__(kGsBlock, 1) towr_gs_stream_kernel(KParams P, const double* rec, int64_t ldr, int32_t ng) {
   using C = typename std::conditional<CLS == GS_ROM, RomCls, DynCls>::type;
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int j = (int)(blockIdx.x % (unsigned)P.ntiles), g0 = (int)(blockIdx.x / (unsigned)P.ntiles);
-  if (g0 >= P.B) return;
+  // XCD-aware: blocks are dealt round-robin over the 8 XCDs; XCD x takes the contiguous range
+  // [x per, (x + 1) per) of (group, block) pairs, so each XCD writes whole problems' CSR ranges
+  const int per = (int)((gridDim.x + 7) / 8);
+  const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+  const int j = w % P.ntiles, g0 = w / P.ntiles;
+  if (g0 >= ng || g0 >= P.B) return;   // the grid is rounded up to a multiple of 8
   const GsBlock bl = P.gs_blk[j];
   const GsGeo g = P.gs_geo[bl.geo];
   const int E = P.rb.n_ee, n = bl.n_inst, tid = threadIdx.x;

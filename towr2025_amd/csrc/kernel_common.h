@@ -56,6 +56,7 @@ struct KParams {
   const int32_t* fs_ws;
   const int32_t* fs_iee;          // per FDISC instant: endeffector, first g row
   const int32_t* fs_irow;
+  const int32_t* fs_iblk;
   const GsGeo* gs_geo;            // streaming RangeOfMotion / Dynamic (layout.h GsGeo)
   const GsBlock* gs_blk;          // the launched class's compose blocks
   const int32_t* gs_tmpl;

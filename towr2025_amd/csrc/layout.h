@@ -35,7 +35,7 @@ struct TileDesc {
 // The force entries polynomial p can make non-zero (its two nodes' variables) lie in the window
 // [fs_ws[2 (wsoff + p)], + kFsWin) of row positions (checked); schedule columns at [js0, js0 + ns1).
 constexpr int kFsInst = 16;   // measured on MI355X (ANYmal gait, B = 1024): 64 -> 0.501 ms, 32 -> 0.463, 16 -> 0.452, 8 -> 0.478
-constexpr int kFsBlock = 256;
+constexpr int kFsBlock = 512;   // stream kernel threads (MI355X, ANYmal gait B = 1024: 256 -> 0.359 ms, 512 -> 0.333 at one problem per block)
 constexpr int kFsWin = 12;
 struct FsBlock {
   int32_t ee, n_inst, t0, r0;   // endeffector, instants, first instant's time index (fs_t), first row
@@ -104,6 +104,8 @@ constexpr int kDynBaseND = 53, kDynEeND = 54, kDynEeNI = 14;
 TG_HD constexpr int gs_rec_nd(int cls, int E) { return cls == GS_ROM ? kRomND : kDynBaseND + kDynEeND * E; }
 TG_HD constexpr int gs_rec_ni(int cls, int E) { return cls == GS_ROM ? kRomNI : kDynEeNI * E; }
 TG_HD constexpr int gs_rec_fields(int cls, int E) { return gs_rec_nd(cls, E) + gs_rec_ni(cls, E); }
+constexpr int kGsGroup = 2;   // problems per composer block (gstream and fstream; 1 -> 0.333 ms, 2 -> 0.321, 8+ slower: a block
+                              // waits for its stores to drain before the next problem's records land)
 constexpr int kGsPre = 8;   // a composer thread's prefetched record doubles: chunks of at most kGsBlock * kGsPre
 // the record kernel's arguments (towr_gs_rec_kernel)
 struct GsRecArgs {
@@ -182,7 +184,7 @@ struct Layout {
   std::vector<double> fs_t;
   std::vector<int32_t> fs_tmpl;
   std::vector<int32_t> fs_ws;        // per (constraint, force polynomial): window start, window dimension codes
-  std::vector<int32_t> fs_iee, fs_irow;   // per instant (fs_t order): endeffector, first row
+  std::vector<int32_t> fs_iee, fs_irow, fs_iblk;   // per instant (fs_t order): endeffector, first row, FsBlock
   int32_t fs_tmpl_max = 0;
   // streaming RangeOfMotion / Dynamic (GsGeo): per class enabled when every constraint of the class fits
   bool gstream[GS_COUNT] = {};

@@ -494,7 +494,7 @@ int64_t pattern_outside_host(const Layout& L, const double* x, const towr_terrai
 // polynomial's columns fit a kFsWin window of the row. Otherwise the tile path stays.
 int build_fstream(Layout& L, std::string& err) {
   L.fstream = false;
-  L.fs_blocks.clear(); L.fs_t.clear(); L.fs_tmpl.clear(); L.fs_ws.clear(); L.fs_iee.clear(); L.fs_irow.clear(); L.fs_tmpl_max = 0;
+  L.fs_blocks.clear(); L.fs_t.clear(); L.fs_tmpl.clear(); L.fs_ws.clear(); L.fs_iee.clear(); L.fs_irow.clear(); L.fs_iblk.clear(); L.fs_tmpl_max = 0;
   if (!L.gait || L.fdisc_motion) return TOWR_OK;
   std::vector<FsBlock> blocks;
   std::vector<double> ts;
@@ -579,6 +579,9 @@ int build_fstream(Layout& L, std::string& err) {
   L.fstream = true;
   L.fs_blocks.swap(blocks); L.fs_t.swap(ts); L.fs_tmpl.swap(tmpl); L.fs_ws.swap(wsv); L.fs_tmpl_max = lmax;
   L.fs_iee.swap(iee); L.fs_irow.swap(irow);
+  L.fs_iblk.assign(L.fs_t.size(), 0);
+  for (size_t q = 0; q < L.fs_blocks.size(); ++q)
+    for (int k = 0; k < L.fs_blocks[q].n_inst; ++k) L.fs_iblk[(size_t)L.fs_blocks[q].t0 + k] = (int32_t)q;
   return TOWR_OK;
 }
 

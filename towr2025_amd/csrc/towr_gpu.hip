@@ -67,6 +67,7 @@ struct towr_gpu_handle_s {
   int32_t* d_fs_ws = nullptr;
   int32_t* d_fs_iee = nullptr;
   int32_t* d_fs_irow = nullptr;
+  int32_t* d_fs_iblk = nullptr;
   double* d_fsrec = nullptr;   // per-problem instant records of the streaming path (scratch, grown on demand)
   int64_t fsrec_cap = 0;       // problems it holds
   GsGeo* d_gs_geo = nullptr;   // streaming RangeOfMotion / Dynamic tables (layout.h GsGeo)
@@ -85,7 +86,6 @@ struct towr_gpu_handle_s {
   // handle: a call on another stream than the previous one waits for the previous call's work (this
   // event), and growing a buffer waits for it on the host before the old one is freed.
   hipEvent_t scr_ev = nullptr;
-  int n_cu = 256;   // the device's compute units (launch sizing)
   hipStream_t scr_stream = nullptr;
   bool scr_used = false;
   // fusion groups (TOWR_GPU_FUSE, see towr_step_kernel): classes that run in one launch
@@ -358,7 +358,7 @@ void fill_common(towr_gpu_handle h, KParams& P, int B, const double* X, int64_t 
   P.ph_stride = gt.ph_stride;
   P.gt_ntime = gt.n_time;
   P.fsb = h->d_fsb; P.fs_t = h->d_fs_t; P.fs_tmpl = h->d_fs_tmpl; P.fs_ws = h->d_fs_ws;
-  P.fs_iee = h->d_fs_iee; P.fs_irow = h->d_fs_irow;
+  P.fs_iee = h->d_fs_iee; P.fs_irow = h->d_fs_irow; P.fs_iblk = h->d_fs_iblk;
   P.gs_geo = h->d_gs_geo; P.gs_tmpl = h->d_gs_tmpl; P.gs_pcode = h->d_gs_pcode;
   P.gs_segs = h->d_gs_segs; P.gs_tseg = h->d_gs_tseg; P.gs_vmap = h->d_gs_vmap; P.gs_ws = h->d_gs_ws; P.gs_blob = h->d_gs_blob;
 }
@@ -393,12 +393,14 @@ int launch_fstream(towr_gpu_handle h, KParams& P, hipStream_t st) {
   int32_t ni_a = ni;
   void* aa[] = {&P, &rec, &ldr_a, &ni_a};
   HIPCHK(h, hipLaunchKernel(fs_inst_kernel(), dim3((unsigned)B), dim3(fs_inst_block()), aa, fs_inst_lds_bytes(L), st));
-  const int64_t total = (int64_t)B * P.ntiles;
-  const int64_t grid = ((total + 7) / 8) * 8;
+  // stream blocks: one FsBlock for a group of kGsGroup problems
+  const size_t lds = sizeof(double) * fs_region(L);
+  int32_t ng = (B + kGsGroup - 1) / kGsGroup;
+  const int64_t grid = ((int64_t)ng * P.ntiles + 7) / 8 * 8;   // the kernel's XCD-aware mapping needs whole rounds of 8
   if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
   const double* crec = rec;
-  void* ab[] = {&P, const_cast<double**>(&crec), &ldr_a, &ni_a};
-  HIPCHK(h, hipLaunchKernel(fs_stream_kernel(), dim3((unsigned)grid), dim3(kFsBlock), ab, sizeof(double) * fs_region(L), st));
+  void* ab[] = {&P, const_cast<double**>(&crec), &ldr_a, &ng};
+  HIPCHK(h, hipLaunchKernel(fs_stream_kernel(), dim3((unsigned)grid), dim3(kFsBlock), ab, lds, st));
   return TOWR_OK;
 }
 
@@ -413,16 +415,14 @@ size_t gs_rec_lds(const Layout& L) {
 }
 int gs_rec_threads(const Layout& L) {
   const int64_t Kd = gs_kd(L), Kr = L.gstream[GS_ROM] ? (int64_t)L.gs_inst[GS_ROM].size() : 0;
-  const int64_t ee0 = (Kd + 63) & ~63, r0 = (ee0 + L.rb.n_ee * Kd + 63) & ~63;
+  const int64_t ee0 = (Kd + 63) & ~63, r0 = (ee0 + 3 * L.rb.n_ee * Kd + 63) & ~63;
   const int64_t lanes = std::max<int64_t>(r0 + Kr, 4 * ((Kd + 63) & ~63));
   return (int)std::min<int64_t>(kGsRecMaxBlock, std::max<int64_t>(64, (lanes + 63) & ~63));
 }
 
 // The streaming RangeOfMotion / Dynamic path: the record kernel into the handle's scratch, then the
 // composer of each class (only: one class, for the per-class timings; -1 both) over its GsBlocks. A
-// composer block takes one GsBlock for a group of problems (b = g, g + ng, ...), the grid sized to one
-// round of resident blocks (its LDS and registers allow kGsResident per CU).
-constexpr int kGsResident = 6;   // 4-wave composer blocks per CU its registers allow (79 VGPRs)
+// composer block takes one GsBlock for a group of kGsGroup problems (b = g, g + ng, ...).
 int launch_gstream(towr_gpu_handle h, KParams& P, int only, hipStream_t st) {
   const Layout& L = h->L;
   const int B = P.B;
@@ -444,11 +444,8 @@ int launch_gstream(towr_gpu_handle h, KParams& P, int only, hipStream_t st) {
     P.gs_blk = h->d_gs_blk[cls];
     P.ntiles = (int32_t)L.gs_blocks[cls].size();
     const size_t lds = gs_stream_lds(L, cls);
-    const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(kGsResident, (int64_t)(160 * 1024) / (int64_t)lds));
-    const int64_t slots = per_cu * h->n_cu;
-    const int64_t ppb = std::max<int64_t>(1, ((int64_t)B * P.ntiles + slots - 1) / slots);   // problems per block
-    int32_t ng = (int32_t)((B + ppb - 1) / ppb);
-    const int64_t grid = (int64_t)ng * P.ntiles;
+    int32_t ng = (B + kGsGroup - 1) / kGsGroup;
+    const int64_t grid = ((int64_t)ng * P.ntiles + 7) / 8 * 8;   // the kernel's XCD-aware mapping needs whole rounds of 8
     if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
     const double* crec = h->d_gsrec + (cls == GS_DYN ? lr : 0);
     int64_t ldr = lr + ld;
@@ -917,7 +914,6 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
   h->device = device;
   auto bail = [&](int code) { std::string m = h->err; towr_gpu_destroy(h); fail(nullptr, code, m); return code; };
   if (hipSetDevice(device) != hipSuccess) { h->err = "hipSetDevice failed"; return bail(TOWR_ERR_HIP); }
-  if (hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || h->n_cu <= 0) h->n_cu = 256;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
     h->err = std::string("device is ") + prop.gcnArchName + ", this build targets gfx950 only";
@@ -939,7 +935,7 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
       (r = upload(h, &h->d_citems, L.cost_items)) || (r = upload(h, &h->d_cq, L.cost_q)) || (r = upload(h, &h->d_gtab, gait_blob(L))) ||
       (r = upload(h, &h->d_idir, L.idirect)) || (r = upload(h, &h->d_fsb, L.fs_blocks)) || (r = upload(h, &h->d_fs_t, L.fs_t)) ||
       (r = upload(h, &h->d_fs_tmpl, L.fs_tmpl)) || (r = upload(h, &h->d_fs_ws, L.fs_ws)) ||
-      (r = upload(h, &h->d_fs_iee, L.fs_iee)) || (r = upload(h, &h->d_fs_irow, L.fs_irow)) ||
+      (r = upload(h, &h->d_fs_iee, L.fs_iee)) || (r = upload(h, &h->d_fs_irow, L.fs_irow)) || (r = upload(h, &h->d_fs_iblk, L.fs_iblk)) ||
       (r = upload(h, &h->d_gs_geo, L.gs_geo)) || (r = upload(h, &h->d_gs_tmpl, L.gs_tmpl)) || (r = upload(h, &h->d_gs_pcode, L.gs_pcode)) ||
       (r = upload(h, &h->d_gs_blk[GS_ROM], L.gs_blocks[GS_ROM])) || (r = upload(h, &h->d_gs_blk[GS_DYN], L.gs_blocks[GS_DYN])) ||
       (r = upload(h, &h->d_gs_inst[GS_ROM], L.gs_inst[GS_ROM])) || (r = upload(h, &h->d_gs_inst[GS_DYN], L.gs_inst[GS_DYN])) ||
@@ -1060,7 +1056,7 @@ int towr_gpu_destroy(towr_gpu_handle h) {
                  h->d_pinfo, h->d_pcols, h->d_pact, h->d_sched, h->d_misc, h->d_misc_lds, h->d_eelin, h->d_gtab, h->d_idir, h->d_citems, h->d_cq, h->fuse[0].d_units, h->fuse[1].d_units,
                  h->d_bterrain, h->d_x, h->d_g, h->d_v, h->d_f, h->d_grad,
                  h->d_traj_pd, h->d_traj_n, h->d_traj_c0, h->d_traj_t, h->d_fsb, h->d_fs_t, h->d_fs_tmpl, h->d_fs_ws,
-                 h->d_fs_iee, h->d_fs_irow, h->d_fsrec, h->d_lin, h->d_soft_b, h->d_soft_rp, h->d_soft_col, h->d_sg, h->d_sv,
+                 h->d_fs_iee, h->d_fs_irow, h->d_fs_iblk, h->d_fsrec, h->d_lin, h->d_soft_b, h->d_soft_rp, h->d_soft_col, h->d_sg, h->d_sv,
                  h->single.d_units, h->d_gs_geo, h->d_gs_tmpl, h->d_gs_pcode, h->d_gs_blk[0], h->d_gs_blk[1], h->d_gs_inst[0],
                  h->d_gs_inst[1], h->d_gsrec, h->d_gs_segs, h->d_gs_tseg, h->d_gs_vmap, h->d_gs_ws, h->d_gs_blob};
   if (h->device >= 0) for (void* p : dev) if (p) (void)hipFree(p);
