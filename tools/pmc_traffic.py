@@ -34,6 +34,13 @@ def per_kernel(d, counter):
             acc[name].append(float(r["Counter_Value"]) * 1024.0)
         elif "towr_fdisc_inst_kernel" in k or "towr_fdisc_stream_kernel" in k:   # gait streaming FDISC
             acc["gait_fdisc_" + ("inst" if "inst" in k else "stream")].append(float(r["Counter_Value"]) * 1024.0)
+        elif "towr_gs_rec_kernel" in k:   # gait RangeOfMotion + Dynamic record kernel
+            acc["gait_gs_rec"].append(float(r["Counter_Value"]) * 1024.0)
+        elif "towr_gs_stream_kernel<" in k:   # <0> RangeOfMotion composer, <1> Dynamic composer
+            c = k.split("towr_gs_stream_kernel<")[1].split(">")[0].strip()
+            acc["gait_gs_stream_" + ("range_of_motion" if c == "0" else "dynamic")].append(float(r["Counter_Value"]) * 1024.0)
+        elif "towr_dyn_g1_kernel" in k:
+            acc["dyn_g1"].append(float(r["Counter_Value"]) * 1024.0)
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
 
