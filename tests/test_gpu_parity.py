@@ -331,6 +331,48 @@ def test_batch_device_gait_optimization():
     _batch_vs_single(F.anymal_trot(optimize_timings=True), "anymal_gaitopt_batch", B=64, optimize_timings=True)
 
 
+def test_batch_device_gait_two_chains():
+    """The phase-duration path at B >= kSplitBatch (64) runs two chains (FDISC records + compose on the side
+    stream, RangeOfMotion / Dynamic on the caller's), below it one serial chain (towr_gpu.hip
+    launch_stream_path). B = 601 (odd: a compose block's problem pair is ragged) against the same problems
+    as batches of 37 and 1 (37 < 64: the serial chain): bit-identical, nothing written past m / nnz, a
+    sample against the oracle."""
+    import torch
+    import bench
+    f = F.anymal_trot(optimize_timings=True)
+    desc = f.to_desc()
+    p = TowrGpuProblem(desc)
+    B = 601
+    Xh, terrains = bench.make_batch(p, B, first_id=7100, optimize_timings=True)
+    X = np.ascontiguousarray(Xh[0])
+    dev = torch.device("cuda:0")
+    ldg, ldv = p.m + 3, p.nnz + 5
+    Xd = torch.from_numpy(X).to(dev)
+    Gd = torch.full((B, ldg), np.nan, dtype=torch.float64, device=dev)
+    Vd = torch.full((B, ldv), np.nan, dtype=torch.float64, device=dev)
+    p.set_batch_terrain(terrains)
+    p.eval_batch_device(Xd, Gd, Vd)
+    torch.cuda.synchronize()
+    G, V = Gd.cpu().numpy(), Vd.cpu().numpy()
+    assert np.isnan(G[:, p.m:]).all() and np.isnan(V[:, p.nnz:]).all(), "write past m / nnz"
+    for s, e in [(k, min(B, k + 37)) for k in range(0, B, 37)] + [(300, 301)]:
+        g = torch.full((e - s, p.m), np.nan, dtype=torch.float64, device=dev)
+        v = torch.full((e - s, p.nnz), np.nan, dtype=torch.float64, device=dev)
+        p.set_batch_terrain(terrains[s:e])
+        p.eval_batch_device(Xd[s:e].contiguous(), g, v)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(G[s:e, :p.m], g.cpu().numpy(), err_msg=f"g of problems [{s}, {e})")
+        np.testing.assert_array_equal(V[s:e, :p.nnz], v.cpu().numpy(), err_msg=f"J of problems [{s}, {e})")
+    r, c = p.jac_structure()
+    for b in (0, 255, 256, 600):
+        d = f.to_desc()
+        d.terrain = terrains[b]
+        o = Oracle(d)
+        _, _, v_ref = o.eval_jac(X[b])
+        assert_close(o.eval_g(X[b]), G[b, :p.m], r, v_ref, V[b, :p.nnz], o.m, f"gait chunk problem {b}", cols_ref=c,
+                     floor_cols=residue_cols(d, o.n))
+
+
 def test_batch_device_rotvec():
     """RotVecConverter base orientation (ROTVEC kernels) as a randomised device batch."""
     f = F.anymal_trot()

@@ -1,5 +1,5 @@
 """Launch-path selection of the phase-duration-optimisation formulations (CPU, layout-only handles):
-the streaming record + compose path (gstream.hip, fstream.hip) must be the one that runs for every
+the streaming record + compose path (gstream.hip) must be the one that runs for every
 gait configuration whose rows it can express, so the parity tests on the GPU exercise it."""
 import os
 import subprocess

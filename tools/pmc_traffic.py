@@ -32,13 +32,12 @@ def per_kernel(d, counter):
             t = int(targs[0])
             name = ("gait_" if targs[2] == "true" else "") + ("rotvec_" if targs[3] == "true" else "") + NAMES[t]
             acc[name].append(float(r["Counter_Value"]) * 1024.0)
-        elif "towr_fdisc_inst_kernel" in k or "towr_fdisc_stream_kernel" in k:   # gait streaming FDISC
-            acc["gait_fdisc_" + ("inst" if "inst" in k else "stream")].append(float(r["Counter_Value"]) * 1024.0)
-        elif "towr_gs_rec_kernel" in k:   # gait RangeOfMotion + Dynamic record kernel
-            acc["gait_gs_rec"].append(float(r["Counter_Value"]) * 1024.0)
-        elif "towr_gs_stream_kernel<" in k:   # <0> RangeOfMotion composer, <1> Dynamic composer
-            c = k.split("towr_gs_stream_kernel<")[1].split(">")[0].strip()
-            acc["gait_gs_stream_" + ("range_of_motion" if c == "0" else "dynamic")].append(float(r["Counter_Value"]) * 1024.0)
+        elif "towr_gait_rec_kernel" in k:   # phase-duration path: the record launches (FDISC, RangeOfMotion / Dynamic)
+            acc["gait_records"].append(float(r["Counter_Value"]) * 1024.0)
+        elif "towr_gait_compose_kernel<" in k:   # <block, roles>: 1 FDISC, 2 RangeOfMotion, 4 Dynamic, 8 small kinds
+            roles = int(k.split("towr_gait_compose_kernel<")[1].split(">")[0].split(",")[1])
+            names = [n for bit, n in ((1, "fdisc"), (2, "range_of_motion"), (4, "dynamic"), (8, "small_kinds")) if roles & bit]
+            acc["gait_compose_" + "+".join(names)].append(float(r["Counter_Value"]) * 1024.0)
         elif "towr_dyn_g1_kernel" in k:
             acc["dyn_g1"].append(float(r["Counter_Value"]) * 1024.0)
     return {k: sum(v) / len(v) for k, v in acc.items()}

@@ -70,4 +70,6 @@ def empty():
 out["h2d_x_us"] = med(h2d)
 out["d2h_g_values_us"] = med(d2h)
 out["sync_only_us"] = med(empty)
+for k, name, nt, by in p.kernels():   # each launch class alone at B = 1, device outputs
+    out[f"class_{name}_B1_us"] = med(lambda: (p.eval_batch_device_kernel(k, Xd, Gd, Vd, s), s.synchronize()), reps=200)
 print(out)

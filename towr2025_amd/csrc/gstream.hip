@@ -8,9 +8,10 @@
 //            instant (Dynamic: one instant's base terms, one base-angular axis, or one endeffector)
 //            with engine_math.h's item code and stores what the instant's Jacobian entries are built
 //            from, field-major (a wave's stores coalesce);
-//   compose: one block per (problem, GsBlock) reads its instants' records, forms the active-window
-//            basis sums once per (instant, spline, dimension), then streams its whole CSR range with
-//            16-byte non-temporal stores, each unit written once, zeros included.
+//   compose: one block per (problem group, GsBlock) reads its instants' records, forms each value of
+//            an instant once, then streams its whole CSR range with 16-byte non-temporal stores, each
+//            unit written once, zeros included. The ForceConstraintDiscretized compose blocks
+//            (their records: fdisc_records) run in the same launch (towr_gait_compose_kernel).
 // Every entry is the tile path's own expression (eval_rom / eval_dyn, cited per case), so parity is
 // the tile path's parity.
 #include <hip/hip_runtime.h>
@@ -20,6 +21,7 @@
 #include "engine_math.h"
 #include "kernel_common.h"
 #include "layout.h"
+#include "tile_emit.h"
 
 namespace tg {
 namespace {
@@ -43,7 +45,56 @@ __device__ __forceinline__ void gs_window(const Ctx& c, int s, int poly, const d
 }
 
 // ------------------------------------------------------------------------------------------------
-// records
+// ForceConstraintDiscretized records (layout.h FsBlock, kFsRS). Every Jacobian row of the class is the
+// force set's full PhaseSpline pattern plus the schedule columns, ~90 % exact zeros whose positions move
+// with x. One lane per instant: fdisc_instant's result in the composer's form — the basis sums of the
+// kFsWin columns the force polynomial can touch (phase_basis_sum over the instant's window of the
+// template), the 5 pyramid rows b, d force / d schedule, the window start and dimension codes — goes to
+// the per-problem record array; the instant's g rows go straight out. Records are chunk-major per
+// FsBlock (field f of the block's instant kk at kFsRS t0 + f n + kk), so a compose block's prologue is
+// one contiguous copy.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ double fs_int(int v) { return __longlong_as_double((long long)v); }
+__device__ __forceinline__ void fdisc_records(const KParams& P, const Ctx& c, int b, double* rec, int64_t ldr, int32_t ni) {
+  double* Gb = P.G + (int64_t)b * P.ldg;
+  double* R = rec + (int64_t)b * ldr;
+  for (int k = threadIdx.x; k < ni; k += blockDim.x) {
+    FdiscInstant o;
+    fdisc_instant(c, P.fs_iee[k], P.fs_t[k], o);
+    const FsBlock fb = P.fsb[P.fs_iblk[k]];
+    const int kk = k - fb.t0, nb = fb.n_inst;
+    double* r = R + (int64_t)kFsRS * fb.t0 + kk;
+    auto put = [&](int f, double v) { r[f * nb] = v; };
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+      for (int e = 0; e < 3; ++e) put(kFsB + 3 * i + e, o.b[i][e]);
+#pragma unroll
+    for (int e = 0; e < 3; ++e) { put(kFsDx + e, o.Jf.dx[e]); put(kFsV + e, o.Jf.v[e]); }
+    put(kFsND + 2, fs_int(o.Jf.cur));
+    if (P.want_g) {
+      const int row = P.fs_irow[k];
+#pragma unroll
+      for (int i = 0; i < 5; ++i) __builtin_nontemporal_store(o.g[i], Gb + row + i);
+    }
+    const int poly = o.poly;
+    const int ws = P.fs_ws[2 * (fb.wsoff + poly)], wd = P.fs_ws[2 * (fb.wsoff + poly) + 1];
+    put(kFsND, fs_int(ws));
+    put(kFsND + 1, fs_int(wd));
+    double h0 = o.H[0], h1 = o.H[1], h2 = o.H[2], h3 = o.H[3];
+    asm volatile("" : "+v"(h0), "+v"(h1), "+v"(h2), "+v"(h3));
+    const int32_t* tm = P.fs_tmpl + fb.tmpl;
+#pragma unroll 4
+    for (int q = 0; q < kFsWin; ++q) {   // the window's basis sums (schedule entries: never read, 0)
+      const int pos = ws + q;
+      const int32_t te = pos < fb.L ? tm[pos] : -1;
+      put(q, te >= 0 ? phase_basis_sum(c.pcols[te & 0xFFFFFF], poly, h0, h1, h2, h3) : 0.0);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// RangeOfMotion / Dynamic records
 // ------------------------------------------------------------------------------------------------
 // One block per problem records both classes (layout.h, record format): the staging of x and the
 // PhaseSpline tables (gait_record_setup) is done once for RangeOfMotion and Dynamic. Lanes, whole
@@ -72,13 +123,8 @@ __device__ __forceinline__ double* gs_field(double* R, int RS, int k, const GsIn
 }
 
 template <bool ROTVEC>
-// 4 waves per SIMD (128 VGPRs, a few spilled): at the unconstrained 166 VGPRs a second 5-wave block did not
-// fit a CU (MI355X, ANYmal gait B = 1024: 122 us, 100 us at 4 waves per SIMD)
-__global__ void __launch_bounds__(kGsRecMaxBlock) __attribute__((amdgpu_waves_per_eu(4))) towr_gs_rec_kernel(KParams P, GsRecArgs A) {
+__device__ __forceinline__ void gs_records(const KParams& P, const GsRecArgs& A, Ctx c, int b, double* smem) {
   using State = typename DynState<ROTVEC>::type;
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int b = blockIdx.x;
-  Ctx c = gait_record_setup<0>(P, b, smem);   // blockDim.x threads (gs_rec_threads)
   c.rotvec = ROTVEC;
   State* S = reinterpret_cast<State*>(smem + A.st_off);   // one per Dynamic instant
   double* scr = smem + A.scr_off;
@@ -275,6 +321,23 @@ __global__ void __launch_bounds__(kGsRecMaxBlock) __attribute__((amdgpu_waves_pe
   }
 }
 
+// The record launch: per problem one block per role (RecArgs::roles, bit 0 the FDISC records, bit 1 the
+// RangeOfMotion / Dynamic records), each staging x and the PhaseSpline tables itself (gait_record_setup).
+// The two roles run as one launch at small batch sizes (B = 1: one launch boundary less) and as two
+// launches on two streams at large ones (towr_gpu.hip launch_stream_path).
+// 4 waves per SIMD (128 VGPRs, a few spilled): at the unconstrained 166 VGPRs a second 5-wave block did not
+// fit a CU (MI355X, ANYmal gait B = 1024: 122 us, 100 us at 4 waves per SIMD)
+template <bool ROTVEC>
+__global__ void __launch_bounds__(kGsRecMaxBlock) __attribute__((amdgpu_waves_per_eu(4))) towr_gait_rec_kernel(KParams P, RecArgs A) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int nr = A.roles == 3 ? 2 : 1;
+  const int b = (int)blockIdx.x / nr;
+  const int role = A.roles == 3 ? 1 + (int)(blockIdx.x % 2) : A.roles;   // 1 FDISC, 2 RangeOfMotion / Dynamic
+  const Ctx c = gait_record_setup<0>(P, b, smem);
+  if (role == 1) fdisc_records(P, c, b, A.frec, A.fldr, A.ni);
+  else gs_records<ROTVEC>(P, A.g, c, b, smem);
+}
+
 // ------------------------------------------------------------------------------------------------
 // composers
 // ------------------------------------------------------------------------------------------------
@@ -285,7 +348,7 @@ __device__ __forceinline__ double gs_sched_val(const double* dx, const double* v
   if (col < cur) return last ? -v[k] - dx[k] : -v[k];
   return 0.0;
 }
-// Per-class pieces of the composer (towr_gs_stream_kernel): an instant's record in LDS is its RS fields
+// Per-class pieces of the composer (gs_compose): an instant's record in LDS is its RS fields
 // (stride RS | 1, layout.h record format); ci = its int fields, field j at ci[2 j] (gs_int);
 //   poly(): the active polynomial of a PhaseSpline segment's spline at the instant;
 //   value(): value q of a segment at the instant (the tile path's expression for that entry).
@@ -360,18 +423,122 @@ struct DynCls {
 //      the value or 0.
 // LDS: [the geometry's blob (segments, value map, template, position -> segment, prefix codes, window
 // starts; layout.h gs_blob) | values | records (doubles) | wp (int2) | record ints | nph].
+// ForceConstraintDiscretized compose block: FsBlock jt for the problems g0, g0 + ng, ...
+// LDS: [per-instant records (stride kFsCS) | row window values (5 n x kFsWin) | row window starts (5 n)]
+constexpr int kFsUnits = 4;   // 16-byte units composed per lane before their stores
+template <int BLOCK>
+__device__ __forceinline__ void fdisc_compose(const KParams& P, const double* rec, int64_t ldr, int ng, int jt, int g0, double* smem) {
+  constexpr int kFsPre = (kFsInst * kFsRS + BLOCK - 1) / BLOCK;   // prefetched record doubles per thread
+  const FsBlock fb = P.fsb[jt];
+  const int tid = threadIdx.x, n = fb.n_inst, nr = 5 * n;
+  double* cd = smem;
+  double* rowv = cd + ((n * kFsCS + 1) & ~1);
+  int32_t* wsr = reinterpret_cast<int32_t*>(rowv + nr * kFsWin);
+  auto ci = [&](int k, int f) -> int { return *reinterpret_cast<const int32_t*>(cd + k * kFsCS + kFsND + f); };   // ws, wd, cur
+  // the chunk: element e = f * n + kk -> LDS kk * kFsCS + f
+  const int nch = n * kFsRS;
+  const int64_t chunk0 = (int64_t)kFsRS * fb.t0;
+  int dst[kFsPre];
+#pragma unroll
+  for (int q = 0; q < kFsPre; ++q) {
+    const int e = tid + q * BLOCK;
+    const int f = e / n, kk = e - f * n;
+    dst[q] = e >= nch ? -1 : kk * kFsCS + f;
+  }
+  double pre[kFsPre];
+  auto fetch = [&](int b) {
+    const double* src = rec + (int64_t)b * ldr + chunk0;
+#pragma unroll
+    for (int q = 0; q < kFsPre; ++q) pre[q] = dst[q] >= 0 ? src[tid + q * BLOCK] : 0.0;
+  };
+  const int Lr = fb.L, js0 = fb.js0, ns1 = fb.ns1;
+  const float invL = 1.0f / (float)Lr;   // exact row of element e < 2^20 for rows <= 4096 long (|err| << 0.5 / Lr)
+  // entry j of row r (instant k = r / 5, pyramid row i): eval_fdisc's value (see fdisc_sched_value / emit_dim)
+  auto entry = [&](int r, int j) -> double {
+    const unsigned js = (unsigned)(j - js0);
+    if (js < (unsigned)ns1) {   // schedule column js: sched_val per dimension, then the b-weighted sum
+      const int k = r / 5, i = r - 5 * k;
+      const double* d = cd + k * kFsCS;
+      const int cur = ci(k, 2), col = (int)js;
+      const bool last = cur == ns1;   // J.cur == J.n - 1
+      double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+      if (col == cur && !last) {
+        s0 = d[kFsDx + 0]; s1 = d[kFsDx + 1]; s2 = d[kFsDx + 2];
+      } else if (col < cur) {
+        const double v0 = d[kFsV + 0], v1 = d[kFsV + 1], v2 = d[kFsV + 2];
+        if (last) {
+          s0 = -v0 - d[kFsDx + 0]; s1 = -v1 - d[kFsDx + 1]; s2 = -v2 - d[kFsDx + 2];
+        } else {
+          s0 = -v0; s1 = -v1; s2 = -v2;
+        }
+      }
+      return d[kFsB + 3 * i] * s0 + d[kFsB + 3 * i + 1] * s1 + d[kFsB + 3 * i + 2] * s2;
+    }
+    const unsigned q = (unsigned)(j - wsr[r]);
+    return q < (unsigned)kFsWin ? rowv[r * kFsWin + q] : 0.0;
+  };
+  auto value = [&](int e) -> double {
+    const int r = (int)(((float)e + 0.5f) * invL);
+    return entry(r, e - r * Lr);
+  };
+  int b = g0;
+  fetch(b);
+  for (;;) {
+#pragma unroll
+    for (int q = 0; q < kFsPre; ++q)
+      if (dst[q] >= 0) cd[dst[q]] = pre[q];
+    __syncthreads();
+    for (int t = tid; t < nr * kFsWin; t += BLOCK) {   // window value q of row r: b[i][e(q)] * basis sum (emit_dim)
+      const int r = t / kFsWin, q = t - r * kFsWin;
+      const int k = r / 5, i = r - 5 * k;
+      const double v = cd[k * kFsCS + q];
+      const int ed = (ci(k, 1) >> (2 * q)) & 3;
+      rowv[t] = v == 0.0 ? 0.0 : cd[k * kFsCS + kFsB + 3 * i + ed] * v;
+    }
+    for (int t = tid; t < nr; t += BLOCK) wsr[t] = ci(t / 5, 0);
+    __syncthreads();
+    const int bn = b + ng;
+    if (bn < P.B) fetch(bn);   // in flight while this problem streams
+    {
+      double* out = P.V + (int64_t)b * P.ldv + fb.v0;
+      const int nv = fb.nv;
+      const int head = (reinterpret_cast<uintptr_t>(out) & 15) ? 1 : 0;
+      if (head && tid == 0) __builtin_nontemporal_store(value(0), out);
+      const int m2 = (nv - head) >> 1;
+      dbl2_t* d2 = reinterpret_cast<dbl2_t*>(out + head);
+      // kFsUnits units per lane composed into registers first, then stored together, so a lane keeps
+      // kFsUnits stores in flight instead of one store per LDS round trip
+      for (int u0 = tid; u0 < m2; u0 += BLOCK * kFsUnits) {
+        dbl2_t v[kFsUnits];
+#pragma unroll
+        for (int q = 0; q < kFsUnits; ++q) {
+          const int u = u0 + q * BLOCK;
+          const int e = head + 2 * u;
+          const int r = (int)(((float)e + 0.5f) * invL);
+          const int j = e - r * Lr;
+          v[q].x = u < m2 ? entry(r, j) : 0.0;
+          v[q].y = u < m2 ? (j + 1 < Lr ? entry(r, j + 1) : entry(r + 1, 0)) : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < kFsUnits; ++q)
+          if (u0 + q * BLOCK < m2) __builtin_nontemporal_store(v[q], d2 + u0 + q * BLOCK);
+      }
+      if (((nv - head) & 1) && tid == 0) __builtin_nontemporal_store(value(nv - 1), out + nv - 1);
+    }
+    if (bn >= P.B) break;
+    b = bn;
+    __syncthreads();   // this problem's records and row values read before the next deposit
+  }
+}
+
+
 constexpr int kGsUnits = 4;
-template <int CLS>
-__global__ void __launch_bounds__(kGsBlock, 1) towr_gs_stream_kernel(KParams P, const double* rec, int64_t ldr, int32_t ng) {
+template <int CLS, int BLOCK>
+__device__ __forceinline__ void gs_compose(const KParams& P, const GsBlock* blks, const double* rec, int64_t ldr, int ng, int j, int g0,
+                                           double* smem) {
   using C = typename std::conditional<CLS == GS_ROM, RomCls, DynCls>::type;
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  // XCD-aware: blocks are dealt round-robin over the 8 XCDs; XCD x takes the contiguous range
-  // [x per, (x + 1) per) of (group, block) pairs, so each XCD writes whole problems' CSR ranges
-  const int per = (int)((gridDim.x + 7) / 8);
-  const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
-  const int j = w % P.ntiles, g0 = w / P.ntiles;
-  if (g0 >= ng || g0 >= P.B) return;   // the grid is rounded up to a multiple of 8
-  const GsBlock bl = P.gs_blk[j];
+  constexpr int kGsPre = kGsChunkMax / BLOCK;   // prefetched record doubles per thread
+  const GsBlock bl = blks[j];
   const GsGeo g = P.gs_geo[bl.geo];
   const int E = P.rb.n_ee, n = bl.n_inst, tid = threadIdx.x;
   const int ND = gs_rec_nd(CLS, E), NI = gs_rec_ni(CLS, E), RS = ND + NI;
@@ -382,7 +549,7 @@ __global__ void __launch_bounds__(kGsBlock, 1) towr_gs_stream_kernel(KParams P, 
   double* cd = val + ((n * vt + 1) & ~1);
   int2* wp = reinterpret_cast<int2*>(cd + ((n * CS + 1) & ~1));
   int32_t* nph = reinterpret_cast<int32_t*>(wp + n * ns);
-  stage16<kGsBlock>(reinterpret_cast<uint4*>(blob), P.gs_blob + g.blob0, g.blob_n16);
+  stage16<BLOCK>(reinterpret_cast<uint4*>(blob), P.gs_blob + g.blob0, g.blob_n16);
   if (tid < E) nph[tid] = P.sched[tid].n_phases;
   const GsSeg* segs = reinterpret_cast<const GsSeg*>(blob);
   const uint32_t* vmap = reinterpret_cast<const uint32_t*>(blob + g.o_vmap);
@@ -396,7 +563,7 @@ __global__ void __launch_bounds__(kGsBlock, 1) towr_gs_stream_kernel(KParams P, 
   int dst[kGsPre];
 #pragma unroll
   for (int q = 0; q < kGsPre; ++q) {
-    const int e = tid + q * kGsBlock;
+    const int e = tid + q * BLOCK;
     const int f = e / n, kk = e - f * n;
     dst[q] = e >= nch ? -1 : kk * CS + f;
   }
@@ -404,7 +571,7 @@ __global__ void __launch_bounds__(kGsBlock, 1) towr_gs_stream_kernel(KParams P, 
   auto fetch = [&](int b) {
     const double* src = rec + (int64_t)b * ldr + chunk0;
 #pragma unroll
-    for (int q = 0; q < kGsPre; ++q) pre[q] = dst[q] >= 0 ? src[tid + q * kGsBlock] : 0.0;
+    for (int q = 0; q < kGsPre; ++q) pre[q] = dst[q] >= 0 ? src[tid + q * BLOCK] : 0.0;
   };
   auto deposit = [&]() {
 #pragma unroll
@@ -426,7 +593,7 @@ __global__ void __launch_bounds__(kGsBlock, 1) towr_gs_stream_kernel(KParams P, 
   for (;;) {
     deposit();
     __syncthreads();
-    for (int t = tid; t < n * ns; t += kGsBlock) {   // window starts and value bases
+    for (int t = tid; t < n * ns; t += BLOCK) {   // window starts and value bases
       const int kk = t / ns, sid = t - kk * ns;
       const GsSeg sg = segs[sid];
       int ws = 0;
@@ -434,7 +601,7 @@ __global__ void __launch_bounds__(kGsBlock, 1) towr_gs_stream_kernel(KParams P, 
       wp[t] = make_int2(sg.p0 + ws, ((int)sg.W << 16) | (kk * vt + sg.vbase));
     }
     __syncthreads();
-    for (int t = tid; t < n * vt; t += kGsBlock) {   // every value of every instant, once
+    for (int t = tid; t < n * vt; t += BLOCK) {   // every value of every instant, once
       const int kk = t / vt, v = t - kk * vt;
       const uint32_t vm = vmap[v];
       const int sid = (int)(vm >> 16), q = (int)(vm & 0xFFFF);
@@ -457,24 +624,56 @@ __global__ void __launch_bounds__(kGsBlock, 1) towr_gs_stream_kernel(KParams P, 
     if (head && tid == 0) __builtin_nontemporal_store(value(0), out);
     const int m2 = (nv - head) >> 1;
     dbl2_t* d2 = reinterpret_cast<dbl2_t*>(out + head);
-    for (int u0 = tid; u0 < m2; u0 += kGsBlock * kGsUnits) {
+    for (int u0 = tid; u0 < m2; u0 += BLOCK * kGsUnits) {
       dbl2_t v[kGsUnits];
 #pragma unroll
       for (int q = 0; q < kGsUnits; ++q) {
-        const int u = u0 + q * kGsBlock;
+        const int u = u0 + q * BLOCK;
         const int e = head + 2 * u;
         v[q].x = u < m2 ? value(e) : 0.0;
         v[q].y = u < m2 ? value(e + 1) : 0.0;
       }
 #pragma unroll
       for (int q = 0; q < kGsUnits; ++q)
-        if (u0 + q * kGsBlock < m2) __builtin_nontemporal_store(v[q], d2 + u0 + q * kGsBlock);
+        if (u0 + q * BLOCK < m2) __builtin_nontemporal_store(v[q], d2 + u0 + q * BLOCK);
     }
     if (((nv - head) & 1) && tid == 0) __builtin_nontemporal_store(value(nv - 1), out + nv - 1);
     if (bn >= P.B) break;
     b = bn;
     __syncthreads();   // this problem's wp / values / records read before the next deposit
   }
+}
+
+
+// The composer launch: every compose block of every problem in one grid. Per problem group the units are
+// [FDISC FsBlocks | RangeOfMotion GsBlocks | Dynamic GsBlocks] (A.nt), so the write-bound FDISC blocks
+// and the Dynamic blocks' longer value phases interleave on every CU, and one launch replaces three (at
+// B = 1 a launch boundary costs more than a compose block). XCD-aware: blocks are dealt round-robin over
+// the 8 XCDs; XCD x takes the contiguous range [x per, (x + 1) per) of (group, unit) pairs, so each XCD
+// writes whole problems' CSR ranges.
+template <int BLOCK, int MASK>   // MASK: the roles of this instantiation (bit 0 FDISC, 1 RangeOfMotion, 2 Dynamic, 3 small kinds)
+__global__ void __launch_bounds__(BLOCK, 1) towr_gait_compose_kernel(KParams P, ComposeArgs A) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int NT = A.nt[0] + A.nt[1] + A.nt[2] + A.nt[3];
+  const int per = (int)((gridDim.x + 7) / 8);
+  const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+  int j = w % NT;
+  const int g0 = w / NT;
+  if (g0 >= A.ng || g0 >= P.B) return;   // the grid is rounded up to a multiple of 8
+  if constexpr ((MASK & 1) != 0)
+    if (j < A.nt[0]) { fdisc_compose<BLOCK>(P, A.frec, A.fldr, A.ng, j, g0, smem); return; }
+  j -= A.nt[0];
+  if constexpr ((MASK & 2) != 0)
+    if (j < A.nt[1]) { gs_compose<GS_ROM, BLOCK>(P, A.blk[GS_ROM], A.grec, A.gldr, A.ng, j, g0, smem); return; }
+  j -= A.nt[1];
+  if constexpr ((MASK & 4) != 0)
+    if (j < A.nt[2]) { gs_compose<GS_DYN, BLOCK>(P, A.blk[GS_DYN], A.grec + A.gdyn_off, A.gldr, A.ng, j, g0, smem); return; }
+  j -= A.nt[2];
+  if constexpr ((MASK & 8) != 0)   // a small-kind group (tile_emit.h misc_body) of each of the block's problems
+    for (int b = g0; b < P.B; b += A.ng) {
+      misc_body<true, BLOCK>(P, smem, b, j, A.misc_x_off);
+      __syncthreads();
+    }
 }
 
 }  // namespace
@@ -493,11 +692,24 @@ int64_t gs_record_doubles(const Layout& L, int cls) {
   const int64_t K = (int64_t)L.gs_inst[cls].size();
   return ((int64_t)gs_rec_fields(cls, L.rb.n_ee) * K + 1) & ~(int64_t)1;
 }
-const void* gs_rec_kernel(bool rotvec) {
-  return rotvec ? reinterpret_cast<const void*>(&towr_gs_rec_kernel<true>) : reinterpret_cast<const void*>(&towr_gs_rec_kernel<false>);
+const void* gait_rec_kernel(bool rotvec) {
+  return rotvec ? reinterpret_cast<const void*>(&towr_gait_rec_kernel<true>) : reinterpret_cast<const void*>(&towr_gait_rec_kernel<false>);
 }
-const void* gs_stream_kernel(int cls) {
-  return cls == GS_ROM ? reinterpret_cast<const void*>(&towr_gs_stream_kernel<GS_ROM>) : reinterpret_cast<const void*>(&towr_gs_stream_kernel<GS_DYN>);
+const void* gait_compose_kernel(int mask) {
+  // the instantiations the host launches (towr_gpu.hip launch_stream_path): at small batch sizes every role
+  // in one launch; at large ones the FDISC chain beside the Dynamic and RangeOfMotion launches (one class
+  // alone: the per-class timings); block sizes: compose_block
+  switch (mask) {
+    case 1: return reinterpret_cast<const void*>(&towr_gait_compose_kernel<kComposeBlock, 1>);
+    case 2: return reinterpret_cast<const void*>(&towr_gait_compose_kernel<kComposeBlockRD, 2>);
+    case 4: return reinterpret_cast<const void*>(&towr_gait_compose_kernel<kComposeBlockRD, 4>);
+    case 6: return reinterpret_cast<const void*>(&towr_gait_compose_kernel<kComposeBlockRD, 6>);
+    case 7: return reinterpret_cast<const void*>(&towr_gait_compose_kernel<kComposeBlock, 7>);
+    default: return reinterpret_cast<const void*>(&towr_gait_compose_kernel<kComposeBlock, 15>);
+  }
+}
+size_t fs_compose_lds(const Layout& L) {   // records, row window values, row window starts
+  return sizeof(double) * ((size_t)(((kFsInst * kFsCS + 1) & ~1) + 5 * kFsInst * kFsWin + (5 * kFsInst + 1) / 2 + 1) & ~(size_t)1);
 }
 size_t gs_dyn_state_bytes(bool rotvec) { return rotvec ? dyn_state_bytes<true>() : dyn_state_bytes<false>(); }
 

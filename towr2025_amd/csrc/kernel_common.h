@@ -1,7 +1,7 @@
 // kernel_common.h — device-side definitions shared by the engine's translation units
-// (towr_gpu.hip: tile / small-kind / cost / trajectory kernels and the C-ABI; fstream.hip: the
-// streaming ForceConstraintDiscretized kernels): the launch parameter block and the staging and
-// copy-out helpers.
+// (tiles.hip: tile / small-kind / fused kernels; gstream.hip: the phase-duration path's record and
+// compose kernels; cost_traj.hip; towr_gpu.hip: the C-ABI): the launch parameter block and the staging
+// and copy-out helpers.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -208,8 +208,7 @@ __device__ __forceinline__ void stage_x(const KParams& P, const double* xg, doub
     stage16<BLOCK>(reinterpret_cast<uint4*>(ns), reinterpret_cast<const uint4*>(P.nodecol), (P.n_nodecol + 3) >> 2);
 }
 
-// Prologue of the per-problem record kernels under phase-duration optimisation (fstream.hip,
-// gstream.hip): x (+ zero slot), the node table, the PhaseSpline tables and the terrain staged in LDS
+// Prologue of the per-problem record kernel under phase-duration optimisation (gstream.hip): x (+ zero slot), the node table, the PhaseSpline tables and the terrain staged in LDS
 // ([x | node table | tables | timings | terrain], fs_inst_lds_bytes), then the x-dependent PhaseSpline
 // timings formed once per block (as tile_body does); returns the evaluation context over them.
 template <int BLOCK>

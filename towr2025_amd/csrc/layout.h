@@ -35,8 +35,11 @@ struct TileDesc {
 // The force entries polynomial p can make non-zero (its two nodes' variables) lie in the window
 // [fs_ws[2 (wsoff + p)], + kFsWin) of row positions (checked); schedule columns at [js0, js0 + ns1).
 constexpr int kFsInst = 16;   // measured on MI355X (ANYmal gait, B = 1024): 64 -> 0.501 ms, 32 -> 0.463, 16 -> 0.452, 8 -> 0.478
-constexpr int kFsBlock = 512;   // stream kernel threads (MI355X, ANYmal gait B = 1024: 256 -> 0.359 ms, 512 -> 0.333 at one problem per block)
 constexpr int kFsWin = 12;
+// FDISC record (gstream.hip fdisc_records -> the composer): Hv[kFsWin] | b[5][3] | Jf.dx[3] |
+// Jf.v[3] | ints ws, wd, cur (64-bit integer bit patterns)
+constexpr int kFsB = kFsWin, kFsDx = kFsWin + 15, kFsV = kFsWin + 18, kFsND = kFsWin + 21;
+constexpr int kFsRS = kFsND + 3, kFsCS = kFsRS | 1;   // record fields; LDS stride per instant
 struct FsBlock {
   int32_t ee, n_inst, t0, r0;   // endeffector, instants, first instant's time index (fs_t), first row
   int32_t v0, nv, L, tmpl;      // CSR range [v0, v0 + nv), row length, template offset (fs_tmpl)
@@ -63,7 +66,11 @@ struct FsBlock {
 enum GsClass { GS_ROM = 0, GS_DYN = 1, GS_COUNT = 2 };
 constexpr int kGsRowTypes = 6;
 constexpr int kGsAct = 4;
-constexpr int kGsBlock = 256;
+// The composer launch (gstream.hip towr_gait_compose_kernel): the ForceConstraintDiscretized,
+// RangeOfMotion and Dynamic compose blocks of every problem in one grid, kComposeBlock threads each.
+constexpr int kComposeBlock = 512;
+constexpr int kComposeBlockRD = 256;   // a launch without FDISC blocks
+inline int compose_block(int mask) { return (mask & 9) ? kComposeBlock : kComposeBlockRD; }
 constexpr int kGsInstRom = 16;   // instants per compose block
 constexpr int kGsInstDyn = 2;   // measured on MI355X (ANYmal gait, B = 1024, grouped composer): 2 -> 0.201 ms, 4 -> 0.230, 8 -> 0.219
 // A row type is cut into segments: its base prefix, each maximal run of template columns of one
@@ -88,7 +95,7 @@ struct GsGeo {
 struct GsBlock { int32_t geo, k0, n_inst, v0, nv, reserved[3]; };   // instants [k0, k0 + n_inst) of the geometry
 // a record lane's instant; kk / nb: its index in its GsBlock and the block's instants (the record chunk)
 struct GsInst { double t; int32_t seg, row0; int16_t ee, kk, nb, reserved; };
-// Records (gstream.hip towr_gs_rec_kernel): per instant RS fields, the composer's view of the instant —
+// Records (gstream.hip gs_records): per instant RS fields, the composer's view of the instant —
 // ND doubles then NI ints (stored as doubles) — so that a composer block's prologue is one contiguous
 // copy. The fields of the GsBlock of instants [k0, k0 + n) form one chunk at RS * k0 (class-global
 // instant index), field-major inside it (field f of instant k0 + kk at RS * k0 + f * n + kk).
@@ -106,8 +113,8 @@ TG_HD constexpr int gs_rec_ni(int cls, int E) { return cls == GS_ROM ? kRomNI : 
 TG_HD constexpr int gs_rec_fields(int cls, int E) { return gs_rec_nd(cls, E) + gs_rec_ni(cls, E); }
 constexpr int kGsGroup = 2;   // problems per composer block (gstream and fstream; 1 -> 0.333 ms, 2 -> 0.321, 8+ slower: a block
                               // waits for its stores to drain before the next problem's records land)
-constexpr int kGsPre = 8;   // a composer thread's prefetched record doubles: chunks of at most kGsBlock * kGsPre
-// the record kernel's arguments (towr_gs_rec_kernel)
+constexpr int kGsChunkMax = 2048;   // record doubles of a compose block (prefetched into registers: kGsChunkMax / kComposeBlock per thread)
+// the RangeOfMotion / Dynamic records' arguments (gs_records)
 struct GsRecArgs {
   double* rec;                 // per problem: RangeOfMotion records at 0, Dynamic records at dyn_off
   int64_t ldr, dyn_off;
@@ -264,22 +271,37 @@ TypeSpec type_spec(int type, int n_ee, bool gait, bool rotvec = false);
 // the k-th of n instances in a tile
 int type_lane(int type, int group, int k, int n, int n_ee, bool gait, int sub);
 
-// The streaming ForceConstraintDiscretized kernels (fstream.hip): their LDS, record size, entry points.
-size_t fs_region(const Layout& L);
-int64_t fs_record_doubles();
-const void* fs_inst_kernel();
-const void* fs_stream_kernel();
-int fs_inst_block();
+inline int64_t fs_record_doubles() { return kFsRS; }   // FDISC record doubles per instant
 
-// The streaming RangeOfMotion / Dynamic kernels (gstream.hip): compose LDS (bytes), record doubles
-// per problem of one class, entry points. The record kernel (both classes in one launch) uses
-// fs_inst_lds_bytes' LDS layout, then its Dynamic states and scratch (gs_rec_lds).
+// The streaming kernels (gstream.hip): compose LDS (bytes), record doubles per problem of one class,
+// entry points. The record kernel uses fs_inst_lds_bytes' LDS layout, then its Dynamic states and
+// scratch (gs_rec_lds).
 size_t gs_stream_lds(const Layout& L, int cls);
+size_t fs_compose_lds(const Layout& L);   // the ForceConstraintDiscretized compose block (bytes)
 int64_t gs_record_doubles(const Layout& L, int cls);
-const void* gs_rec_kernel(bool rotvec);
-const void* gs_stream_kernel(int cls);
+const void* gait_rec_kernel(bool rotvec);
+const void* gait_compose_kernel(int mask);   // roles: bit 0 FDISC, 1 RangeOfMotion, 2 Dynamic, 3 small kinds
+// the composer launch's arguments: the record arrays (per problem, leading dimensions) and, per
+// role (0 FDISC, 1 RangeOfMotion, 2 Dynamic, 3 small-kind groups), its blocks per problem group (0: not
+// in this launch)
+struct ComposeArgs {
+  const double* frec; int64_t fldr;
+  const double* grec; int64_t gldr, gdyn_off;
+  const GsBlock* blk[GS_COUNT];
+  int32_t nt[4];
+  int32_t ng;          // problem groups: a block composes problems g, g + ng, ... (kGsGroup per block)
+  int32_t misc_x_off;  // small kinds: the staged x's LDS offset (doubles)
+};
+// the record launch's arguments (towr_gait_rec_kernel): roles bit 0 the FDISC records (frec, fldr,
+// ni instants), bit 1 the RangeOfMotion / Dynamic records (g)
+struct RecArgs {
+  GsRecArgs g;
+  double* frec; int64_t fldr;
+  int32_t ni, roles;
+};
 size_t gs_dyn_state_bytes(bool rotvec);   // the record kernel's per-Dynamic-instant LDS state
 constexpr int kGsRecMaxBlock = 512;
+constexpr int kFsRecBlock = 512;   // the record launch's threads when it holds FDISC records
 // The frozen-pattern check (WatchItem): reference Jacobian entries at x outside the x0 pattern, evaluated
 // with the structure pass's arithmetic on the host
 int64_t pattern_outside_host(const Layout& L, const double* x, const towr_terrain_t& terrain);

@@ -609,8 +609,8 @@ bool build_gstream_class(Layout& L, int cls, const std::vector<BaseDec>& bdec, c
   int gmax[3] = {0, 0, 0}, nmax = 0;
   int cap = cls == GS_ROM ? kGsInstRom : kGsInstDyn;
   if (const char* e = std::getenv(cls == GS_ROM ? "TOWR_GS_ROM_INST" : "TOWR_GS_DYN_INST")) cap = std::max(1, std::min(64, std::atoi(e)));   // tuning (A/B)
-  cap = std::max(1, std::min(cap, kGsBlock * kGsPre / gs_rec_fields(cls, L.rb.n_ee)));   // a block's record chunk fits the prefetch
-  if (gs_rec_fields(cls, L.rb.n_ee) > kGsBlock * kGsPre) { why = "record larger than the composer's prefetch"; return false; }
+  cap = std::max(1, std::min(cap, kGsChunkMax / gs_rec_fields(cls, L.rb.n_ee)));   // a block's record chunk fits the prefetch
+  if (gs_rec_fields(cls, L.rb.n_ee) > kGsChunkMax) { why = "record larger than the composer's prefetch"; return false; }
   int tmax = 0, pmax = 0;
   for (const ConsInfo& cs : L.cons) {
     if (cs.kind != ctype || cs.rows == 0) continue;

@@ -1,5 +1,5 @@
 // towr_gpu.hip — the C-ABI (include/towr_gpu.h) and host side of the eval_g / eval_jac_g engine: handle,
-// device tables, launch sequencing, host-pointer entry points. The kernels live in tiles.hip, fstream.hip,
+// device tables, launch sequencing, host-pointer entry points. The kernels live in tiles.hip,
 // gstream.hip and cost_traj.hip.
 //
 // One fused launch evaluates, for a batch of B problems sharing one layout, every constraint value
@@ -231,9 +231,8 @@ std::vector<uint4> gait_blob(const Layout& L) {
   return b;
 }
 
-const void* kernel_for_class(int lc, bool gait, bool rotvec, bool fstream = false, int gcls = -1) {
-  if (lc == LC_FDISC && gait && fstream) return fs_stream_kernel();   // the stream kernel (B); A: fs_inst_kernel()
-  if (gcls >= 0) return gs_stream_kernel(gcls);                       // the composer; the record kernel: gs_rec_kernel
+const void* kernel_for_class(int lc, bool gait, bool rotvec, bool streamed = false) {
+  if (streamed) return gait_compose_kernel(15);   // the composer launch; the record kernel: gait_rec_kernel
   if (lc == LC_MISC) return misc_kernel_for(gait);
   return tile_kernel_for(class_type(lc), gait, rotvec);
 }
@@ -246,19 +245,27 @@ int gstream_cls(const Layout& L, int lc) {   // the streaming class of launch cl
   if (lc == LC_DYN && L.gstream[GS_DYN]) return GS_DYN;
   return -1;
 }
+bool streamed_class(const Layout& L, int lc) { return fstream_class(L, lc) || gstream_cls(L, lc) >= 0; }
+// LDS of the composer launch: its largest compose block
+size_t lds_bytes(const Layout& L, int lc);
+int class_units(const Layout& L, int lc);
+size_t compose_lds(const Layout& L, bool f = true, bool r = true, bool d = true, bool misc = true) {
+  size_t b = L.fstream && f ? fs_compose_lds(L) : 0;
+  if (L.gstream[GS_ROM] && r) b = std::max(b, gs_stream_lds(L, GS_ROM));
+  if (L.gstream[GS_DYN] && d) b = std::max(b, gs_stream_lds(L, GS_DYN));
+  if (misc && class_units(L, LC_MISC) > 0) b = std::max(b, lds_bytes(L, LC_MISC));   // small-kind groups (small batches)
+  return b;
+}
 size_t lds_region(const Layout& L, int lc) {
-  if (fstream_class(L, lc)) return fs_region(L);
-  if (gstream_cls(L, lc) >= 0) return gs_stream_lds(L, gstream_cls(L, lc)) / sizeof(double);
+  if (streamed_class(L, lc)) return compose_lds(L, true, true, true, false) / sizeof(double);
   return lc == LC_MISC ? (size_t)((L.misc_region + 1) & ~1) : (size_t)L.type_lds[class_type(lc)];
 }
 int class_block(const Layout& L, int lc) {
-  if (fstream_class(L, lc)) return kFsBlock;
-  if (gstream_cls(L, lc) >= 0) return kGsBlock;
+  if (streamed_class(L, lc)) return kComposeBlock;
   return lc == LC_MISC ? 64 * kMiscWaves : L.type_block[class_type(lc)];
 }
 size_t lds_bytes(const Layout& L, int lc) {
-  if (fstream_class(L, lc)) return sizeof(double) * fs_region(L);   // the stream kernel (B) stages no x
-  if (gstream_cls(L, lc) >= 0) return gs_stream_lds(L, gstream_cls(L, lc));
+  if (streamed_class(L, lc)) return compose_lds(L);   // the composer (its small-kind groups stage x)
   size_t d = lds_region(L, lc);
   d += (size_t)((L.n + 2) & ~1);                                                                  // x + zero slot
   if (lc == LC_MISC || stages_nodes(class_type(lc), L.gait)) d += (L.nodecol.size() + 3) / 4 * 2;  // node table (16-B units)
@@ -379,32 +386,7 @@ int launch_fused(towr_gpu_handle h, const towr_gpu_handle_s::FuseGroup& fg, int 
   return TOWR_OK;
 }
 
-// The streaming ForceConstraintDiscretized path: instant kernel (A) into the handle's record scratch,
-// then the stream kernel (B) over the FsBlocks. P comes from fill_common with ntiles = FsBlocks.
-int launch_fstream(towr_gpu_handle h, KParams& P, hipStream_t st) {
-  const Layout& L = h->L;
-  const int B = P.B;
-  const int32_t ni = (int32_t)L.fs_t.size();
-  const int64_t ldr = fs_record_doubles() * ni;
-  if (int rc = scratch_grow(h, &h->d_fsrec, &h->fsrec_cap, B, ldr)) return rc;
-  P.lds_x_off = 0;
-  double* rec = h->d_fsrec;
-  int64_t ldr_a = ldr;
-  int32_t ni_a = ni;
-  void* aa[] = {&P, &rec, &ldr_a, &ni_a};
-  HIPCHK(h, hipLaunchKernel(fs_inst_kernel(), dim3((unsigned)B), dim3(fs_inst_block()), aa, fs_inst_lds_bytes(L), st));
-  // stream blocks: one FsBlock for a group of kGsGroup problems
-  const size_t lds = sizeof(double) * fs_region(L);
-  int32_t ng = (B + kGsGroup - 1) / kGsGroup;
-  const int64_t grid = ((int64_t)ng * P.ntiles + 7) / 8 * 8;   // the kernel's XCD-aware mapping needs whole rounds of 8
-  if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
-  const double* crec = rec;
-  void* ab[] = {&P, const_cast<double**>(&crec), &ldr_a, &ng};
-  HIPCHK(h, hipLaunchKernel(fs_stream_kernel(), dim3((unsigned)grid), dim3(kFsBlock), ab, lds, st));
-  return TOWR_OK;
-}
-
-// The record kernel (both streaming classes, one block per problem): its LDS is the staging of
+// The record kernel (both RangeOfMotion / Dynamic, one block per problem): its LDS is the staging of
 // fs_inst_lds_bytes, one base-angular converter state per Dynamic instant, then the Dynamic scratch
 // (9 doubles per instant and per (endeffector, instant)); its lanes, whole waves per kind (gstream.hip).
 int64_t gs_kd(const Layout& L) { return L.gstream[GS_DYN] ? (int64_t)L.gs_inst[GS_DYN].size() : 0; }
@@ -420,38 +402,99 @@ int gs_rec_threads(const Layout& L) {
   return (int)std::min<int64_t>(kGsRecMaxBlock, std::max<int64_t>(64, (lanes + 63) & ~63));
 }
 
-// The streaming RangeOfMotion / Dynamic path: the record kernel into the handle's scratch, then the
-// composer of each class (only: one class, for the per-class timings; -1 both) over its GsBlocks. A
-// composer block takes one GsBlock for a group of kGsGroup problems (b = g, g + ng, ...).
-int launch_gstream(towr_gpu_handle h, KParams& P, int only, hipStream_t st) {
+// The streaming path under phase-duration optimisation (gstream.hip) for the streamed classes in
+// `mask` (bits LC_FDISC, LC_ROM, LC_DYN; LC_MISC: the small kinds may join the composer launch):
+//   records: the FDISC records and the RangeOfMotion / Dynamic records (towr_gait_rec_kernel, one block
+//            per problem and role) into the handle's record scratch; they write g;
+//   compose: the compose blocks of the classes (towr_gait_compose_kernel), each CSR range written once.
+// A batch of kSplitBatch problems or more runs as two chains: FDISC records + compose on the caller's
+// stream beside the RangeOfMotion / Dynamic records + the Dynamic and RangeOfMotion compose launches on the
+// side stream, so that the write-bound FDISC compose overlaps the latency-bound record work (MI355X, ANYmal
+// gait, B = 1024, one box: 0.600-0.608 ms per step; one chain 0.663, records in 256-problem chunks
+// pipelined against the compose 0.737, Dynamic + RangeOfMotion in one compose launch 0.640). The small
+// kinds then follow the shorter chain on the side stream (*forked: the caller launches them there and
+// joins). A smaller batch (B = 1: IPOPT's callbacks) is two launches on the caller's stream: both record
+// roles in one, every compose role and the small-kind groups in the other (*misc_done) — at B = 1 a
+// launch boundary or a cross-stream event costs more than any overlap gains (MI355X, ANYmal gait: 97 us
+// for the per-class chains, 70 us for four launches on one stream).
+constexpr int kSplitBatch = 64;
+bool compose_lds_attr(size_t lds) {   // every composer instantiation may take `lds` bytes of LDS
+  for (int m = 1; m < 16; ++m)
+    if (hipFuncSetAttribute(gait_compose_kernel(m), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return false;
+  return true;
+}
+int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t st, bool* forked, bool* misc_done) {
   const Layout& L = h->L;
   const int B = P.B;
+  const bool fs = L.fstream && ((mask >> LC_FDISC) & 1);
+  const bool gr = L.gstream[GS_ROM] && ((mask >> LC_ROM) & 1), gd = L.gstream[GS_DYN] && ((mask >> LC_DYN) & 1);
+  const int32_t ni = (int32_t)L.fs_t.size();
+  const int64_t fldr = fs_record_doubles() * ni;
   const int64_t lr = L.gstream[GS_ROM] ? gs_record_doubles(L, GS_ROM) : 0, ld = L.gstream[GS_DYN] ? gs_record_doubles(L, GS_DYN) : 0;
-  if (int rc = scratch_grow(h, &h->d_gsrec, &h->gsrec_cap, B, lr + ld)) return rc;
-  GsRecArgs A{};
-  A.rec = h->d_gsrec; A.ldr = lr + ld; A.dyn_off = lr;
+  if (fs)
+    if (int rc = scratch_grow(h, &h->d_fsrec, &h->fsrec_cap, B, fldr)) return rc;
+  if (gr || gd)
+    if (int rc = scratch_grow(h, &h->d_gsrec, &h->gsrec_cap, B, lr + ld)) return rc;
+  const bool split = fs && (gr || gd) && h->n_side > 0 && B >= kSplitBatch;
+  const bool misc = !split && ((mask >> LC_MISC) & 1) && class_units(L, LC_MISC) > 0;
+  const hipStream_t gst = split ? h->side[0] : st;   // the RangeOfMotion / Dynamic chain
+  if (split) {
+    HIPCHK(h, hipEventRecord(h->fork, st));
+    HIPCHK(h, hipStreamWaitEvent(gst, h->fork, 0));
+  }
+  RecArgs R{};
+  R.frec = h->d_fsrec; R.fldr = fldr; R.ni = ni;
+  R.g.rec = h->d_gsrec; R.g.ldr = lr + ld; R.g.dyn_off = lr;
   for (int c = 0; c < GS_COUNT; ++c) {
-    A.inst[c] = h->d_gs_inst[c];
-    A.K[c] = L.gstream[c] ? (int32_t)L.gs_inst[c].size() : 0;
+    R.g.inst[c] = h->d_gs_inst[c];
+    R.g.K[c] = L.gstream[c] ? (int32_t)L.gs_inst[c].size() : 0;
   }
-  A.st_off = (int32_t)(fs_inst_lds_bytes(L) / sizeof(double));
-  A.scr_off = A.st_off + (int32_t)(gs_kd(L) * gs_state_stride(L) / sizeof(double));
-  void* aa[] = {&P, &A};
-  HIPCHK(h, hipLaunchKernel(gs_rec_kernel(L.rotvec), dim3((unsigned)B), dim3((unsigned)gs_rec_threads(L)), aa, gs_rec_lds(L), st));
-  if (!P.want_jac) return TOWR_OK;   // the g rows are the record kernel's
-  for (int cls = GS_COUNT - 1; cls >= 0; --cls) {
-    if (!L.gstream[cls] || (only >= 0 && only != cls)) continue;
-    P.gs_blk = h->d_gs_blk[cls];
-    P.ntiles = (int32_t)L.gs_blocks[cls].size();
-    const size_t lds = gs_stream_lds(L, cls);
-    int32_t ng = (B + kGsGroup - 1) / kGsGroup;
-    const int64_t grid = ((int64_t)ng * P.ntiles + 7) / 8 * 8;   // the kernel's XCD-aware mapping needs whole rounds of 8
+  R.g.st_off = (int32_t)(fs_inst_lds_bytes(L) / sizeof(double));
+  R.g.scr_off = R.g.st_off + (int32_t)(gs_kd(L) * gs_state_stride(L) / sizeof(double));
+  // FDISC role: 512 threads (its instants); RangeOfMotion / Dynamic role: gs_rec_threads
+  auto records = [&](int roles, hipStream_t s) -> int {
+    R.roles = roles;
+    const int nr = roles == 3 ? 2 : 1;
+    const int threads = roles == 2 ? gs_rec_threads(L) : std::max(gs_rec_threads(L), kFsRecBlock);
+    void* aa[] = {&P, &R};
+    HIPCHK(h, hipLaunchKernel(gait_rec_kernel(L.rotvec), dim3((unsigned)(B * nr)), dim3((unsigned)threads), aa, gs_rec_lds(L), s));
+    return TOWR_OK;
+  };
+  ComposeArgs C{};
+  C.frec = h->d_fsrec; C.fldr = fldr;
+  C.grec = h->d_gsrec; C.gldr = lr + ld; C.gdyn_off = lr;
+  C.blk[GS_ROM] = h->d_gs_blk[GS_ROM]; C.blk[GS_DYN] = h->d_gs_blk[GS_DYN];
+  C.ng = (B + kGsGroup - 1) / kGsGroup;
+  C.misc_x_off = (int32_t)lds_region(L, LC_MISC);
+  auto compose = [&](bool f, bool r, bool d, bool m, hipStream_t s) -> int {
+    const bool j = P.want_jac != 0;   // without the Jacobian only the small kinds (their g rows)
+    C.nt[0] = f && j ? (int32_t)L.fs_blocks.size() : 0;
+    C.nt[1] = r && j ? (int32_t)L.gs_blocks[GS_ROM].size() : 0;
+    C.nt[2] = d && j ? (int32_t)L.gs_blocks[GS_DYN].size() : 0;
+    C.nt[3] = m ? class_units(L, LC_MISC) : 0;
+    const int64_t grid = ((int64_t)C.ng * (C.nt[0] + C.nt[1] + C.nt[2] + C.nt[3]) + 7) / 8 * 8;   // whole rounds of 8 (XCD-aware mapping)
+    if (grid == 0) return TOWR_OK;
     if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
-    const double* crec = h->d_gsrec + (cls == GS_DYN ? lr : 0);
-    int64_t ldr = lr + ld;
-    void* ab[] = {&P, const_cast<double**>(&crec), &ldr, &ng};
-    HIPCHK(h, hipLaunchKernel(gs_stream_kernel(cls), dim3((unsigned)grid), dim3(kGsBlock), ab, lds, st));
+    void* ab[] = {&P, &C};
+    // the launch's own roles: their instantiation (registers) and LDS; without FDISC or small kinds 256 threads
+    const int roles = (C.nt[0] ? 1 : 0) | (C.nt[1] ? 2 : 0) | (C.nt[2] ? 4 : 0) | (C.nt[3] ? 8 : 0);
+    HIPCHK(h, hipLaunchKernel(gait_compose_kernel(roles), dim3((unsigned)grid), dim3(compose_block(roles)), ab,
+                              compose_lds(L, C.nt[0] > 0, C.nt[1] > 0, C.nt[2] > 0, C.nt[3] > 0), s));
+    return TOWR_OK;
+  };
+  if (split) {
+    if (int rc = records(1, st)) return rc;
+    if (int rc = compose(true, false, false, false, st)) return rc;
+    if (int rc = records(2, gst)) return rc;
+    if (int rc = compose(false, false, gd, false, gst)) return rc;
+    if (int rc = compose(false, gr, false, false, gst)) return rc;
+  } else {
+    if (fs || gr || gd)
+      if (int rc = records((fs ? 1 : 0) | (gr || gd ? 2 : 0), st)) return rc;
+    if (int rc = compose(fs, gr, gd, misc, st)) return rc;
   }
+  *forked = split;   // the caller's other launches follow on the side stream, then it joins
+  *misc_done = misc;
   return TOWR_OK;
 }
 
@@ -484,27 +527,30 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
   for (int lc = 0; lc < LC_COUNT; ++lc)
     if (class_units(L, lc) > 0 && !((fused_mask >> lc) & 1) && (only_class < 0 || lc == only_class)) order[nk++] = lc;
   std::sort(order, order + nk, [&](int a, int b) { return class_bytes(L, a) > class_bytes(L, b); });
-  const int nside = (only_class < 0 && nk > 1) ? std::min(h->n_side, nk - 1) : 0;
+  std::stable_partition(order, order + nk, [](int lc) { return lc != LC_MISC; });   // the small kinds last
+  // (the streaming path forks its own side stream, see launch_stream_path; the other classes follow it on
+  // the caller's stream)
+  const int nside = (only_class < 0 && nk > 1 && !uses_scratch(L)) ? std::min(h->n_side, nk - 1) : 0;
   if (nside > 0) {
     HIPCHK(h, hipEventRecord(h->fork, s));
     for (int i = 0; i < nside; ++i) HIPCHK(h, hipStreamWaitEvent(h->side[i], h->fork, 0));
   }
-  bool gs_done = false;
+  bool stream_done = false, stream_forked = false, misc_done = false;
   for (int q = 0; q < nk; ++q) {
     const int lc = order[q];
+    if (lc == LC_MISC && misc_done) continue;   // in the streaming path's composer launch
     const int nt = class_units(L, lc);
-    const hipStream_t st = (nside > 0 && q % (nside + 1) != 0) ? h->side[q % (nside + 1) - 1] : s;
+    const hipStream_t st = stream_forked ? h->side[0] : (nside > 0 && q % (nside + 1) != 0) ? h->side[q % (nside + 1) - 1] : s;
     KParams P{};
     fill_common(h, P, B, X, ldx, G, ldg, V, ldv, want_g, want_jac, terrains, per_problem);
     P.ntiles = nt;
-    if (fstream_class(L, lc)) {
-      if (int rc = launch_fstream(h, P, st)) return rc;
-      continue;
-    }
-    if (gstream_cls(L, lc) >= 0) {   // both streaming classes at the first one (one record kernel)
-      if (only_class < 0 && gs_done) continue;
-      gs_done = true;
-      if (int rc = launch_gstream(h, P, only_class < 0 ? -1 : gstream_cls(L, lc), st)) return rc;
+    if (streamed_class(L, lc)) {   // every streamed class at the first one: its records and one composer launch
+      if (stream_done) continue;
+      stream_done = true;
+      uint32_t mask = 0;
+      for (int k = 0; k < nk; ++k)
+        if (streamed_class(L, order[k]) || order[k] == LC_MISC) mask |= 1u << order[k];   // (the small kinds are last)
+      if (int rc = launch_stream_path(h, P, mask, s, &stream_forked, &misc_done)) return rc;
       continue;
     }
     if (lc == LC_MISC) {
@@ -524,10 +570,10 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
     if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
     const int block = class_block(L, lc);
     void* args[] = {&P};
-    HIPCHK(h, hipLaunchKernel(kernel_for_class(lc, L.gait, L.rotvec, L.fstream, gstream_cls(L, lc)), dim3((unsigned)grid), dim3((unsigned)block), args,
+    HIPCHK(h, hipLaunchKernel(kernel_for_class(lc, L.gait, L.rotvec), dim3((unsigned)grid), dim3((unsigned)block), args,
                               lds_bytes(L, lc), st));
   }
-  for (int i = 0; i < nside; ++i) {
+  for (int i = 0; i < (stream_forked ? 1 : nside); ++i) {
     HIPCHK(h, hipEventRecord(h->join[i], h->side[i]));
     HIPCHK(h, hipStreamWaitEvent(s, h->join[i], 0));
   }
@@ -1021,20 +1067,18 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
     if (class_units(L, lc) == 0) continue;
     const size_t lds = lds_bytes(L, lc);
     if (lds > 160 * 1024) { h->err = "tile too large for LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
-    if (lds > 64 * 1024 && hipFuncSetAttribute(kernel_for_class(lc, L.gait, L.rotvec, L.fstream, gstream_cls(L, lc)), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+    if (lds > 64 * 1024 && (hipFuncSetAttribute(kernel_for_class(lc, L.gait, L.rotvec, streamed_class(L, lc)), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess ||
+                            (streamed_class(L, lc) && !compose_lds_attr(lds)))) {
       h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
     }
   }
   if (L.fstream || L.gstream[GS_ROM] || L.gstream[GS_DYN]) {   // the record kernels share fs_inst_lds_bytes' layout
     const size_t lds = fs_inst_lds_bytes(L);
     if (lds > 160 * 1024) { h->err = "problem too large for the streaming instant kernel's LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
-    const void* ks[] = {fs_inst_kernel(), gs_rec_kernel(L.rotvec)};
-    const size_t need[] = {lds, gs_rec_lds(L)};
-    for (int q = 0; q < 2; ++q) {
-      if (need[q] > 160 * 1024) { h->err = "problem too large for a record kernel's LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
-      if (need[q] > 64 * 1024 && hipFuncSetAttribute(ks[q], hipFuncAttributeMaxDynamicSharedMemorySize, (int)need[q]) != hipSuccess) {
-        h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
-      }
+    const size_t need = gs_rec_lds(L);
+    if (need > 160 * 1024) { h->err = "problem too large for the record kernel's LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
+    if (need > 64 * 1024 && hipFuncSetAttribute(gait_rec_kernel(L.rotvec), hipFuncAttributeMaxDynamicSharedMemorySize, (int)need) != hipSuccess) {
+      h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
     }
   }
   {
