@@ -1347,6 +1347,30 @@ TG_HD void dyn_rv_column(const DynRvState& S, double Mp[3], double Mv[3], double
   }
 }
 
+// The base-angular entries of a RotVec group-1 item from the instant's formed state: one column per
+// call (a RotVec g1 item carries its component in a1 = 1 + e, layout.hip; the device evaluates exactly
+// that column, a loop over three columns spilled to scratch), the host structure pass and emulation take
+// every column of an unsplit item in order. The fixed-gait device tile forms S once per instant in LDS
+// (tiles.hip tile_body) and calls this from each component lane.
+template <class Emit>
+TG_HD void dyn_rv_emit(const Ctx& c, const ItemDesc& it, const DynRvState& S, Emit& em) {
+  const int r0 = it.row0;
+  double Hp[4], Hv[4], Ha[4];
+  spline_basis(S.A, kPos, Hp); spline_basis(S.A, kVel, Hv); spline_basis(S.A, kAcc, Ha);
+  auto column = [&](auto ec) {   // ec: std::integral_constant (the device instantiates each column)
+    constexpr int e = decltype(ec)::value;
+    double Mp[3], Mv[3], Ma[3];
+    dyn_rv_column<e>(S, Mp, Mv, Ma);
+    for (int r = 0; r < 3; ++r)
+      for (int bb = 0; bb < 4; ++bb)
+        em(r0 + AX + r, basis_col(c, SP_BASE_ANG, S.A.poly, bb, e), Mp[r] * Hp[bb] + Mv[r] * Hv[bb] + Ma[r] * Ha[bb], true);
+  };
+  const int e_lo = it.a1 > 0 ? it.a1 - 1 : 0, e_hi = it.a1 > 0 ? it.a1 : 3;
+  if (e_lo <= 0 && 0 < e_hi) column(std::integral_constant<int, 0>{});
+  if (e_lo <= 1 && 1 < e_hi) column(std::integral_constant<int, 1>{});
+  if (e_lo <= 2 && 2 < e_hi) column(std::integral_constant<int, 2>{});
+}
+
 template <class Emit>
 TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
   if constexpr (emit_dyn_groups<Emit>::value == 1) { if (it.group == 1) return; }
@@ -1371,23 +1395,7 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
   if (it.group == 1 && c.rotvec) {
     DynRvState S;
     dyn_rv_state(c, t, S);
-    double Hp[4], Hv[4], Ha[4];
-    spline_basis(S.A, kPos, Hp); spline_basis(S.A, kVel, Hv); spline_basis(S.A, kAcc, Ha);
-    // one column per call: a RotVec g1 item carries its component in a1 (1 + e, layout.hip); the
-    // device evaluates exactly that column (a loop over three columns spilled to scratch), the host
-    // structure pass and emulation take every column of an unsplit item in order
-    auto column = [&](auto ec) {   // ec: std::integral_constant (the device instantiates each column)
-      constexpr int e = decltype(ec)::value;
-      double Mp[3], Mv[3], Ma[3];
-      dyn_rv_column<e>(S, Mp, Mv, Ma);
-      for (int r = 0; r < 3; ++r)
-        for (int bb = 0; bb < 4; ++bb)
-          em(r0 + AX + r, basis_col(c, SP_BASE_ANG, S.A.poly, bb, e), Mp[r] * Hp[bb] + Mv[r] * Hv[bb] + Ma[r] * Ha[bb], true);
-    };
-    const int e_lo = it.a1 > 0 ? it.a1 - 1 : 0, e_hi = it.a1 > 0 ? it.a1 : 3;
-    if (e_lo <= 0 && 0 < e_hi) column(std::integral_constant<int, 0>{});
-    if (e_lo <= 1 && 1 < e_hi) column(std::integral_constant<int, 1>{});
-    if (e_lo <= 2 && 2 < e_hi) column(std::integral_constant<int, 2>{});
+    dyn_rv_emit(c, it, S, em);
     return;
   }
   if (it.group == 1) {
@@ -1395,7 +1403,7 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
     dyn_euler_state(c, t, S);
     double Hp[4], Hv[4], Ha[4];
     spline_basis(S.A, kPos, Hp); spline_basis(S.A, kVel, Hv); spline_basis(S.A, kAcc, Ha);
-    // all three axes in one lane (242 VGPRs on the fixed-gait device tile); the host (structure pass,
+    // all three axes in one lane (236 VGPRs on the fixed-gait device tile); the host (structure pass,
     // emulation) takes the axes of an unsplit item (a1 = 0) in order
     auto axis = [&](const int e) {
       double Ap[3], Av[3], Aa[3];

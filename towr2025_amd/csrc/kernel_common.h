@@ -43,6 +43,7 @@ struct KParams {
   int32_t lds_rows_off;          // start of the g buffer in the dynamic LDS (doubles)
   int32_t lds_x_off;             // start of the staged x (+ zero slot) and node-column table
   int32_t lds_scr_off;           // DYN: per-instant endeffector sum terms (instants x n_ee x 6)
+  int32_t lds_rv_off;            // DYN, fixed gait, RotVec: per-instant converter states (DynRvState)
   int32_t n, n_pad, n_nodecol;
   int32_t want_g, want_jac, fdisc_motion;
   const int32_t* misc_tiles;      // merged small-kind launch: kMiscWaves tile ids per group

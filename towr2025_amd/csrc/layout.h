@@ -176,6 +176,7 @@ struct Layout {
   int32_t type_lds_rows_off[IT_COUNT] = {};   // start of the g buffer inside the type's LDS
   int32_t type_lds_dummy_off[IT_COUNT] = {};  // per-lane dummy slots for absent candidates
   int32_t dyn_scr_off = 0;                    // DYN LDS: endeffector sum terms after the g rows
+  int32_t dyn_rv_off = 0;                     // DYN LDS, fixed gait, RotVec: per-instant DynRvState after them
   // algorithmic bytes per problem of each type's launch: CSR values + g rows written, distinct
   // x columns read (= the columns of its Jacobian rows)
   int64_t type_bytes[IT_COUNT] = {};

@@ -1373,6 +1373,11 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
       if (t == IT_DYN) {   // + per-instant endeffector sum terms (dyn_g0_a)
         L.dyn_scr_off = L.type_lds[t];
         L.type_lds[t] += type_spec(IT_DYN, E, L.gait, L.rotvec).max_inst * E * 6;
+        if (L.rotvec && !L.gait) {   // + one converter state per instant (tile_body: formed once, read by the three component lanes)
+          L.type_lds[t] = (L.type_lds[t] + 1) & ~1;
+          L.dyn_rv_off = L.type_lds[t];
+          L.type_lds[t] += type_spec(IT_DYN, E, L.gait, L.rotvec).max_inst * (int32_t)((sizeof(DynRvState) + 15) / 16 * 2);
+        }
       }
     }
     L.type_tile0[IT_COUNT] = (int32_t)L.tiles.size();
@@ -1530,7 +1535,7 @@ TypeSpec type_spec(int type, int n_ee, bool gait, bool rotvec) {
   const int blk = tile_block(type, gait);
   switch (type) {
     case IT_DYN:   // waves: g0 | g1 | ee, ee (gait: rows); per-axis base-angular items: 3 g1 lanes per instant
-      if (rotvec)
+      if (rotvec)   // per-component base-angular items
         return {blk, std::max(1, gait ? std::min(64 / 3, 64 / E) : std::min(64, (blk - 64) / (3 + E)))};
       return {blk, std::max(1, std::min(64, gait ? 64 / E : 128 / E))};
     case IT_ROM: return {blk, gait ? 128 : 64};                                         // waves: g0 | g1 | g2 (gait: rows, 2 halves)

@@ -356,6 +356,7 @@ void fill_common(towr_gpu_handle h, KParams& P, int B, const double* X, int64_t 
   P.rb = L.rb;
   P.misc_tiles = h->d_misc; P.misc_lds = h->d_misc_lds;
   P.lds_scr_off = L.dyn_scr_off;
+  P.lds_rv_off = L.dyn_rv_off;
   const GaitTables gt = gait_tables(L);
   P.gtab = h->d_gtab;
   P.idir = h->d_idir;
@@ -844,7 +845,9 @@ int setup_fusion(towr_gpu_handle h, std::string& err) {
   // (tile_block), which the fused kernel's fixed 192 / 256-lane bodies do not cover
   if (L.gait) return TOWR_OK;
   const char* fz = std::getenv("TOWR_GPU_FUSE");
-  const std::string spec = fz ? fz : kDefaultFuse;
+  // RotVec: per-class launches (ANYmal, B = 4096, one box: 0.359-0.367 ms per step, "rf" 0.375: its
+  // RangeOfMotion tiles carry the Rodrigues / left-Jacobian chain and share the CUs worse)
+  const std::string spec = fz ? fz : L.rotvec ? "none" : kDefaultFuse;
   size_t p0 = 0;
   while (p0 <= spec.size() && h->n_fuse < towr_gpu_handle_s::kMaxFuse) {
     const size_t p1 = std::min(spec.find(',', p0), spec.size());
