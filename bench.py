@@ -303,6 +303,9 @@ def main():
     # stream; the roofline's kernel is the longest of the launches one step actually makes
     kernels = {}
     reps = max(5, args.steps // 2)
+    # the side legs (objective, phase-duration optimisation, RotVec): untimed warm-up calls, then at least
+    # 20 timed ones (a leg follows other work, and its first calls settle caches and clocks)
+    leg_warm, leg_reps = 20, max(20, args.steps // 2)
     step_ks = set(prob.step_launches())
     step_names = []
     for k, name, nt, by in prob.kernels():
@@ -357,15 +360,15 @@ def main():
         cprob.set_batch_terrain(terrains)
         Fo = torch.empty(B, dtype=torch.float64, device=dev)
         Go = torch.empty((B, (prob.n + 15) // 16 * 16), dtype=torch.float64, device=dev)
-        for i in range(2):
+        for i in range(leg_warm):
             cprob.eval_cost_batch_device(X[i % N_X], Fo, Go, stream)
         a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
-        for i in range(reps):
+        for i in range(leg_reps):
             cprob.eval_cost_batch_device(X[i % N_X], Fo, Go, stream)
         z.record(stream)
         torch.cuda.synchronize()
-        ms = a.elapsed_time(z) / reps
+        ms = a.elapsed_time(z) / leg_reps
         cbytes = 8 * (2 * prob.n + 1)
         out["objective"] = {"value": B / (ms * 1e-3), "unit": "eval_f+eval_grad_f calls/s", "ms_per_batch": ms,
                             "cost_terms": cdesc.n_costs, "bytes_per_call": cbytes,
@@ -382,15 +385,15 @@ def main():
         Xgd = [torch.from_numpy(Xg[k]).to(dev) for k in range(2)]
         Gg = torch.empty((Bg, (gprob.m + 15) // 16 * 16), dtype=torch.float64, device=dev)
         Vg = torch.empty((Bg, (gprob.nnz + 15) // 16 * 16), dtype=torch.float64, device=dev)
-        for i in range(2):
+        for i in range(leg_warm):
             gprob.eval_batch_device(Xgd[i % 2], Gg, Vg, stream=stream)
         a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
-        for i in range(reps):
+        for i in range(leg_reps):
             gprob.eval_batch_device(Xgd[i % 2], Gg, Vg, stream=stream)
         z.record(stream)
         torch.cuda.synchronize()
-        ms = a.elapsed_time(z) / reps
+        ms = a.elapsed_time(z) / leg_reps
         gb = gprob.algorithmic_bytes_per_call()
         out["gait_optimization"] = {"value": Bg / (ms * 1e-3), "unit": "calls/s", "ms_per_batch": ms, "problems": Bg,
                                     "n": gprob.n, "m": gprob.m, "nnz": gprob.nnz, "GB/s": Bg * gb / (ms * 1e-3) / 1e9,
@@ -406,15 +409,15 @@ def main():
         rprob.set_batch_terrain(terrains)
         Gr = torch.empty((B, (rprob.m + 15) // 16 * 16), dtype=torch.float64, device=dev)
         Vr = torch.empty((B, (rprob.nnz + 15) // 16 * 16), dtype=torch.float64, device=dev)
-        for i in range(2):
+        for i in range(leg_warm):
             rprob.eval_batch_device(X[i % N_X], Gr, Vr, stream=stream)
         a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
-        for i in range(reps):
+        for i in range(leg_reps):
             rprob.eval_batch_device(X[i % N_X], Gr, Vr, stream=stream)
         z.record(stream)
         torch.cuda.synchronize()
-        ms = a.elapsed_time(z) / reps
+        ms = a.elapsed_time(z) / leg_reps
         rb = rprob.algorithmic_bytes_per_call()
         out["rotvec"] = {"value": B / (ms * 1e-3), "unit": "calls/s", "ms_per_batch": ms, "problems": B,
                          "n": rprob.n, "m": rprob.m, "nnz": rprob.nnz, "GB/s": B * rb / (ms * 1e-3) / 1e9,
