@@ -408,7 +408,8 @@ int gs_rec_threads(const Layout& L) {
 //   records: the FDISC records and the RangeOfMotion / Dynamic records (towr_gait_rec_kernel, one block
 //            per problem and role) into the handle's record scratch; they write g;
 //   compose: the compose blocks of the classes (towr_gait_compose_kernel), each CSR range written once.
-// A batch of kSplitBatch problems or more runs as two chains: FDISC records + compose on the caller's
+// A batch of kSplitBatch problems or more runs as two chains (one after the other without a side stream,
+// TOWR_GPU_STREAMS=1): FDISC records + compose on the caller's
 // stream beside the RangeOfMotion / Dynamic records + the Dynamic and RangeOfMotion compose launches on the
 // side stream, so that the write-bound FDISC compose overlaps the latency-bound record work (MI355X, ANYmal
 // gait, B = 1024, one box: 0.600-0.608 ms per step; one chain 0.663, records in 256-problem chunks
@@ -436,8 +437,9 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
     if (int rc = scratch_grow(h, &h->d_fsrec, &h->fsrec_cap, B, fldr)) return rc;
   if (gr || gd)
     if (int rc = scratch_grow(h, &h->d_gsrec, &h->gsrec_cap, B, lr + ld)) return rc;
-  const bool split = fs && (gr || gd) && h->n_side > 0 && B >= kSplitBatch;
-  const bool misc = !split && ((mask >> LC_MISC) & 1) && class_units(L, LC_MISC) > 0;
+  const bool big = B >= kSplitBatch;
+  const bool split = fs && (gr || gd) && h->n_side > 0 && big;
+  const bool misc = !big && ((mask >> LC_MISC) & 1) && class_units(L, LC_MISC) > 0;
   const hipStream_t gst = split ? h->side[0] : st;   // the RangeOfMotion / Dynamic chain
   if (split) {
     HIPCHK(h, hipEventRecord(h->fork, st));
@@ -452,13 +454,16 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
   }
   R.g.st_off = (int32_t)(fs_inst_lds_bytes(L) / sizeof(double));
   R.g.scr_off = R.g.st_off + (int32_t)(gs_kd(L) * gs_state_stride(L) / sizeof(double));
-  // FDISC role: 512 threads (its instants); RangeOfMotion / Dynamic role: gs_rec_threads
+  // threads: the FDISC role alone one lane per instant (whole waves, up to kFsRecBlock) and its staging's
+  // LDS only; the RangeOfMotion / Dynamic role gs_rec_threads; both roles in one launch the larger
   auto records = [&](int roles, hipStream_t s) -> int {
     R.roles = roles;
     const int nr = roles == 3 ? 2 : 1;
-    const int threads = roles == 2 ? gs_rec_threads(L) : std::max(gs_rec_threads(L), kFsRecBlock);
+    const int fth = (int)std::min<int64_t>(kFsRecBlock, std::max<int64_t>(64, ((int64_t)ni + 63) & ~63));
+    const int threads = roles == 2 ? gs_rec_threads(L) : roles == 1 ? fth : std::max(gs_rec_threads(L), kFsRecBlock);
+    const size_t lds = roles == 1 ? fs_inst_lds_bytes(L) : gs_rec_lds(L);
     void* aa[] = {&P, &R};
-    HIPCHK(h, hipLaunchKernel(gait_rec_kernel(L.rotvec), dim3((unsigned)(B * nr)), dim3((unsigned)threads), aa, gs_rec_lds(L), s));
+    HIPCHK(h, hipLaunchKernel(gait_rec_kernel(L.rotvec), dim3((unsigned)(B * nr)), dim3((unsigned)threads), aa, lds, s));
     return TOWR_OK;
   };
   ComposeArgs C{};
@@ -483,12 +488,16 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
                               compose_lds(L, C.nt[0] > 0, C.nt[1] > 0, C.nt[2] > 0, C.nt[3] > 0), s));
     return TOWR_OK;
   };
-  if (split) {
-    if (int rc = records(1, st)) return rc;
-    if (int rc = compose(true, false, false, false, st)) return rc;
-    if (int rc = records(2, gst)) return rc;
-    if (int rc = compose(false, false, gd, false, gst)) return rc;
-    if (int rc = compose(false, gr, false, false, gst)) return rc;
+  if (big) {   // (without a side stream the two chains run one after the other on the caller's stream)
+    if (fs) {
+      if (int rc = records(1, st)) return rc;
+      if (int rc = compose(true, false, false, false, st)) return rc;
+    }
+    if (gr || gd) {
+      if (int rc = records(2, gst)) return rc;
+      if (int rc = compose(false, false, gd, false, gst)) return rc;
+      if (int rc = compose(false, gr, false, false, gst)) return rc;
+    }
   } else {
     if (fs || gr || gd)
       if (int rc = records((fs ? 1 : 0) | (gr || gd ? 2 : 0), st)) return rc;
