@@ -331,7 +331,7 @@ def test_batch_device_gait_optimization():
     _batch_vs_single(F.anymal_trot(optimize_timings=True), "anymal_gaitopt_batch", B=64, optimize_timings=True)
 
 
-def test_batch_device_gait_two_chains():
+def test_batch_device_gait_two_chains(monkeypatch):
     """The phase-duration path at B >= kSplitBatch (64) runs two chains (FDISC records + compose on the side
     stream, RangeOfMotion / Dynamic on the caller's), below it one serial chain (towr_gpu.hip
     launch_stream_path). B = 601 (odd: a compose block's problem pair is ragged) against the same problems
@@ -363,6 +363,17 @@ def test_batch_device_gait_two_chains():
         torch.cuda.synchronize()
         np.testing.assert_array_equal(G[s:e, :p.m], g.cpu().numpy(), err_msg=f"g of problems [{s}, {e})")
         np.testing.assert_array_equal(V[s:e, :p.nnz], v.cpu().numpy(), err_msg=f"J of problems [{s}, {e})")
+    # one launch stream (TOWR_GPU_STREAMS=1, read at handle creation): the two chains one after the other
+    monkeypatch.setenv("TOWR_GPU_STREAMS", "1")
+    q = TowrGpuProblem(desc)
+    q.set_batch_terrain(terrains)
+    g1 = torch.full((B, ldg), np.nan, dtype=torch.float64, device=dev)
+    v1 = torch.full((B, ldv), np.nan, dtype=torch.float64, device=dev)
+    q.eval_batch_device(Xd, g1, v1)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(g1.cpu().numpy(), G, err_msg="g: one stream vs two")
+    np.testing.assert_array_equal(v1.cpu().numpy(), V, err_msg="J: one stream vs two")
+    q.close()
     r, c = p.jac_structure()
     for b in (0, 255, 256, 600):
         d = f.to_desc()

@@ -325,17 +325,27 @@ __device__ __forceinline__ void gs_records(const KParams& P, const GsRecArgs& A,
 // RangeOfMotion / Dynamic records), each staging x and the PhaseSpline tables itself (gait_record_setup).
 // The two roles run as one launch at small batch sizes (B = 1: one launch boundary less) and as two
 // launches on two streams at large ones (towr_gpu.hip launch_stream_path).
-// 4 waves per SIMD (128 VGPRs, a few spilled): at the unconstrained 166 VGPRs a second 5-wave block did not
-// fit a CU (MI355X, ANYmal gait B = 1024: 122 us, 100 us at 4 waves per SIMD)
-template <bool ROTVEC>
+// Instantiated per role set (ROLES), so the FDISC-only launch keeps its own registers. With the
+// RangeOfMotion / Dynamic role: 4 waves per SIMD (128 VGPRs, a few spilled): at the unconstrained 166 VGPRs a
+// second 5-wave block did not fit a CU (MI355X, ANYmal gait B = 1024: 122 us, 100 us at 4 waves per SIMD)
+template <bool ROTVEC, int ROLES>
+__device__ __forceinline__ void rec_body(const KParams& P, const RecArgs& A, double* smem) {
+  const int nr = ROLES == 3 ? 2 : 1;
+  const int b = (int)blockIdx.x / nr;
+  const int role = ROLES == 3 ? 1 + (int)(blockIdx.x % 2) : ROLES;   // 1 FDISC, 2 RangeOfMotion / Dynamic
+  const Ctx c = gait_record_setup<0>(P, b, smem);
+  if constexpr ((ROLES & 1) != 0)
+    if (role == 1) { fdisc_records(P, c, b, A.frec, A.fldr, A.ni); return; }
+  if constexpr ((ROLES & 2) != 0) gs_records<ROTVEC>(P, A.g, c, b, smem);
+}
+template <bool ROTVEC, int ROLES>
 __global__ void __launch_bounds__(kGsRecMaxBlock) __attribute__((amdgpu_waves_per_eu(4))) towr_gait_rec_kernel(KParams P, RecArgs A) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int nr = A.roles == 3 ? 2 : 1;
-  const int b = (int)blockIdx.x / nr;
-  const int role = A.roles == 3 ? 1 + (int)(blockIdx.x % 2) : A.roles;   // 1 FDISC, 2 RangeOfMotion / Dynamic
-  const Ctx c = gait_record_setup<0>(P, b, smem);
-  if (role == 1) fdisc_records(P, c, b, A.frec, A.fldr, A.ni);
-  else gs_records<ROTVEC>(P, A.g, c, b, smem);
+  rec_body<ROTVEC, ROLES>(P, A, smem);
+}
+__global__ void __launch_bounds__(kGsRecMaxBlock) towr_gait_frec_kernel(KParams P, RecArgs A) {   // FDISC records only
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  rec_body<false, 1>(P, A, smem);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -692,8 +702,10 @@ int64_t gs_record_doubles(const Layout& L, int cls) {
   const int64_t K = (int64_t)L.gs_inst[cls].size();
   return ((int64_t)gs_rec_fields(cls, L.rb.n_ee) * K + 1) & ~(int64_t)1;
 }
-const void* gait_rec_kernel(bool rotvec) {
-  return rotvec ? reinterpret_cast<const void*>(&towr_gait_rec_kernel<true>) : reinterpret_cast<const void*>(&towr_gait_rec_kernel<false>);
+const void* gait_rec_kernel(bool rotvec, int roles) {
+  if (roles == 1) return reinterpret_cast<const void*>(&towr_gait_frec_kernel);
+  if (roles == 2) return rotvec ? reinterpret_cast<const void*>(&towr_gait_rec_kernel<true, 2>) : reinterpret_cast<const void*>(&towr_gait_rec_kernel<false, 2>);
+  return rotvec ? reinterpret_cast<const void*>(&towr_gait_rec_kernel<true, 3>) : reinterpret_cast<const void*>(&towr_gait_rec_kernel<false, 3>);
 }
 const void* gait_compose_kernel(int mask) {
   // the instantiations the host launches (towr_gpu.hip launch_stream_path): at small batch sizes every role

@@ -463,7 +463,7 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
     const int threads = roles == 2 ? gs_rec_threads(L) : roles == 1 ? fth : std::max(gs_rec_threads(L), kFsRecBlock);
     const size_t lds = roles == 1 ? fs_inst_lds_bytes(L) : gs_rec_lds(L);
     void* aa[] = {&P, &R};
-    HIPCHK(h, hipLaunchKernel(gait_rec_kernel(L.rotvec), dim3((unsigned)(B * nr)), dim3((unsigned)threads), aa, lds, s));
+    HIPCHK(h, hipLaunchKernel(gait_rec_kernel(L.rotvec, roles), dim3((unsigned)(B * nr)), dim3((unsigned)threads), aa, lds, s));
     return TOWR_OK;
   };
   ComposeArgs C{};
@@ -1089,7 +1089,9 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
     if (lds > 160 * 1024) { h->err = "problem too large for the streaming instant kernel's LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
     const size_t need = gs_rec_lds(L);
     if (need > 160 * 1024) { h->err = "problem too large for the record kernel's LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
-    if (need > 64 * 1024 && hipFuncSetAttribute(gait_rec_kernel(L.rotvec), hipFuncAttributeMaxDynamicSharedMemorySize, (int)need) != hipSuccess) {
+    if (need > 64 * 1024 && (hipFuncSetAttribute(gait_rec_kernel(L.rotvec, 1), hipFuncAttributeMaxDynamicSharedMemorySize, (int)need) != hipSuccess ||
+                             hipFuncSetAttribute(gait_rec_kernel(L.rotvec, 2), hipFuncAttributeMaxDynamicSharedMemorySize, (int)need) != hipSuccess ||
+                             hipFuncSetAttribute(gait_rec_kernel(L.rotvec, 3), hipFuncAttributeMaxDynamicSharedMemorySize, (int)need) != hipSuccess)) {
       h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
     }
   }
