@@ -32,7 +32,9 @@ def per_kernel(d, counter):
             t = int(targs[0])
             name = ("gait_" if targs[2] == "true" else "") + ("rotvec_" if targs[3] == "true" else "") + NAMES[t]
             acc[name].append(float(r["Counter_Value"]) * 1024.0)
-        elif "towr_gait_rec_kernel" in k:   # phase-duration path: the record launches (FDISC, RangeOfMotion / Dynamic)
+        elif "towr_gait_frec_kernel" in k:   # phase-duration path: the FDISC record launch
+            acc["gait_records_fdisc"].append(float(r["Counter_Value"]) * 1024.0)
+        elif "towr_gait_rec_kernel" in k:   # the RangeOfMotion / Dynamic record launch (<rotvec, roles>)
             acc["gait_records"].append(float(r["Counter_Value"]) * 1024.0)
         elif "towr_gait_compose_kernel<" in k:   # <block, roles>: 1 FDISC, 2 RangeOfMotion, 4 Dynamic, 8 small kinds
             roles = int(k.split("towr_gait_compose_kernel<")[1].split(">")[0].split(",")[1])
