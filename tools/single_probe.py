@@ -1,7 +1,7 @@
 """B = 1 latency breakdown (GPU box): towr_gpu_eval_g_jac with registered g / values, timed per call;
 then the same call's pieces in isolation on torch device buffers: the kernel alone (eval_batch_device,
 B = 1, synchronised), an 8.7 kB H2D, the g + values D2H into pinned memory.
-Usage: python tools/single_probe.py [gait]"""
+Usage: python tools/single_probe.py [gait] [--lib tools/build/libtowr_gpu_x.so]"""
 import sys
 import time
 
@@ -23,7 +23,10 @@ def med(f, reps=300):
     return float(np.median(ts) * 1e6)
 
 
-gait = len(sys.argv) > 1 and sys.argv[1] == "gait"
+gait = "gait" in sys.argv[1:]
+if "--lib" in sys.argv:   # an experiment / baseline build under tools/build
+    from towr2025_amd import _capi
+    _capi.load_library(sys.argv[sys.argv.index("--lib") + 1])
 p = TowrGpuProblem(F.anymal_trot(optimize_timings=gait).to_desc())
 x = p.initial_x()
 g, v = np.zeros(p.m), np.zeros(p.nnz)

@@ -123,7 +123,9 @@ __device__ __forceinline__ double* gs_field(double* R, int RS, int k, const GsIn
 }
 
 template <bool ROTVEC>
-__device__ __forceinline__ void gs_records(const KParams& P, const GsRecArgs& A, Ctx c, int b, double* smem) {
+// part: 0 every lane, 1 the Dynamic lanes only, 2 the RangeOfMotion lanes only (a small batch spreads the
+// role over two blocks)
+__device__ __forceinline__ void gs_records(const KParams& P, const GsRecArgs& A, Ctx c, int b, double* smem, int part = 0) {
   using State = typename DynState<ROTVEC>::type;
   c.rotvec = ROTVEC;
   State* S = reinterpret_cast<State*>(smem + A.st_off);   // one per Dynamic instant
@@ -135,7 +137,7 @@ __device__ __forceinline__ void gs_records(const KParams& P, const GsRecArgs& A,
   double* Gb = P.G + (int64_t)b * P.ldg;
   const int RSr = gs_rec_fields(GS_ROM, E), RSd = gs_rec_fields(GS_DYN, E), NDd = gs_rec_nd(GS_DYN, E);
   const int ee0 = (Kd + 63) & ~63, r0 = (ee0 + 3 * EK + 63) & ~63;
-  for (int i = tid; i < r0 + Kr; i += nthr) {
+  for (int i = (part == 2 ? r0 : 0) + tid; i < (part == 1 ? r0 : r0 + Kr); i += nthr) {
     if (i < Kd) {   // Dynamic instant
       const int k = i;
       const GsInst gi = A.inst[GS_DYN][k];
@@ -274,7 +276,7 @@ __device__ __forceinline__ void gs_records(const KParams& P, const GsRecArgs& A,
       put(kRomND + 4, gs_int(M.poly));
     }
   }
-  if (Kd == 0) return;
+  if (Kd == 0 || part == 2) return;
   __syncthreads();
   // phase 2: part 0-2 = base-angular axis e, part 3 = the endeffector sums and g rows; whole waves per part
   const int Kp = (Kd + 63) & ~63;
@@ -328,15 +330,16 @@ __device__ __forceinline__ void gs_records(const KParams& P, const GsRecArgs& A,
 // Instantiated per role set (ROLES), so the FDISC-only launch keeps its own registers. With the
 // RangeOfMotion / Dynamic role: 4 waves per SIMD (128 VGPRs, a few spilled): at the unconstrained 166 VGPRs a
 // second 5-wave block did not fit a CU (MI355X, ANYmal gait B = 1024: 122 us, 100 us at 4 waves per SIMD)
+// ROLES 7: three blocks per problem, FDISC | Dynamic lanes | RangeOfMotion lanes (small batches)
 template <bool ROTVEC, int ROLES>
 __device__ __forceinline__ void rec_body(const KParams& P, const RecArgs& A, double* smem) {
-  const int nr = ROLES == 3 ? 2 : 1;
-  const int b = (int)blockIdx.x / nr;
-  const int role = ROLES == 3 ? 1 + (int)(blockIdx.x % 2) : ROLES;   // 1 FDISC, 2 RangeOfMotion / Dynamic
+  const int nr = ROLES == 7 ? 3 : ROLES == 3 ? 2 : 1;
+  const int b = (int)blockIdx.x / nr, r = (int)blockIdx.x % nr;
+  const int role = nr > 1 ? 1 + (r > 0) : ROLES;   // 1 FDISC, 2 RangeOfMotion / Dynamic
   const Ctx c = gait_record_setup<0>(P, b, smem);
   if constexpr ((ROLES & 1) != 0)
     if (role == 1) { fdisc_records(P, c, b, A.frec, A.fldr, A.ni); return; }
-  if constexpr ((ROLES & 2) != 0) gs_records<ROTVEC>(P, A.g, c, b, smem);
+  if constexpr ((ROLES & 2) != 0) gs_records<ROTVEC>(P, A.g, c, b, smem, ROLES == 7 ? r : 0);
 }
 template <bool ROTVEC, int ROLES>
 __global__ void __launch_bounds__(kGsRecMaxBlock) __attribute__((amdgpu_waves_per_eu(4))) towr_gait_rec_kernel(KParams P, RecArgs A) {
@@ -705,7 +708,8 @@ int64_t gs_record_doubles(const Layout& L, int cls) {
 const void* gait_rec_kernel(bool rotvec, int roles) {
   if (roles == 1) return reinterpret_cast<const void*>(&towr_gait_frec_kernel);
   if (roles == 2) return rotvec ? reinterpret_cast<const void*>(&towr_gait_rec_kernel<true, 2>) : reinterpret_cast<const void*>(&towr_gait_rec_kernel<false, 2>);
-  return rotvec ? reinterpret_cast<const void*>(&towr_gait_rec_kernel<true, 3>) : reinterpret_cast<const void*>(&towr_gait_rec_kernel<false, 3>);
+  if (roles == 3) return rotvec ? reinterpret_cast<const void*>(&towr_gait_rec_kernel<true, 3>) : reinterpret_cast<const void*>(&towr_gait_rec_kernel<false, 3>);
+  return rotvec ? reinterpret_cast<const void*>(&towr_gait_rec_kernel<true, 7>) : reinterpret_cast<const void*>(&towr_gait_rec_kernel<false, 7>);
 }
 const void* gait_compose_kernel(int mask) {
   // the instantiations the host launches (towr_gpu.hip launch_stream_path): at small batch sizes every role

@@ -280,7 +280,7 @@ inline int64_t fs_record_doubles() { return kFsRS; }   // FDISC record doubles p
 size_t gs_stream_lds(const Layout& L, int cls);
 size_t fs_compose_lds(const Layout& L);   // the ForceConstraintDiscretized compose block (bytes)
 int64_t gs_record_doubles(const Layout& L, int cls);
-const void* gait_rec_kernel(bool rotvec, int roles);   // roles: 1 FDISC, 2 RangeOfMotion / Dynamic, 3 both
+const void* gait_rec_kernel(bool rotvec, int roles);   // roles: 1 FDISC, 2 RangeOfMotion / Dynamic, 3 both, 7 both in 3 blocks
 const void* gait_compose_kernel(int mask);   // roles: bit 0 FDISC, 1 RangeOfMotion, 2 Dynamic, 3 small kinds
 // the composer launch's arguments: the record arrays (per problem, leading dimensions) and, per
 // role (0 FDISC, 1 RangeOfMotion, 2 Dynamic, 3 small-kind groups), its blocks per problem group (0: not

@@ -458,7 +458,7 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
   // LDS only; the RangeOfMotion / Dynamic role gs_rec_threads; both roles in one launch the larger
   auto records = [&](int roles, hipStream_t s) -> int {
     R.roles = roles;
-    const int nr = roles == 3 ? 2 : 1;
+    const int nr = roles == 7 ? 3 : roles == 3 ? 2 : 1;
     const int fth = (int)std::min<int64_t>(kFsRecBlock, std::max<int64_t>(64, ((int64_t)ni + 63) & ~63));
     const int threads = roles == 2 ? gs_rec_threads(L) : roles == 1 ? fth : std::max(gs_rec_threads(L), kFsRecBlock);
     const size_t lds = roles == 1 ? fs_inst_lds_bytes(L) : gs_rec_lds(L);
@@ -499,8 +499,8 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
       if (int rc = compose(false, gr, false, false, gst)) return rc;
     }
   } else {
-    if (fs || gr || gd)
-      if (int rc = records((fs ? 1 : 0) | (gr || gd ? 2 : 0), st)) return rc;
+    if (fs || gr || gd)   // both RangeOfMotion and Dynamic: their lanes in two blocks (shorter chains per CU)
+      if (int rc = records(fs && gr && gd ? 7 : (fs ? 1 : 0) | (gr || gd ? 2 : 0), st)) return rc;
     if (int rc = compose(fs, gr, gd, misc, st)) return rc;
   }
   *forked = split;   // the caller's other launches follow on the side stream, then it joins
@@ -1091,7 +1091,8 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
     if (need > 160 * 1024) { h->err = "problem too large for the record kernel's LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
     if (need > 64 * 1024 && (hipFuncSetAttribute(gait_rec_kernel(L.rotvec, 1), hipFuncAttributeMaxDynamicSharedMemorySize, (int)need) != hipSuccess ||
                              hipFuncSetAttribute(gait_rec_kernel(L.rotvec, 2), hipFuncAttributeMaxDynamicSharedMemorySize, (int)need) != hipSuccess ||
-                             hipFuncSetAttribute(gait_rec_kernel(L.rotvec, 3), hipFuncAttributeMaxDynamicSharedMemorySize, (int)need) != hipSuccess)) {
+                             hipFuncSetAttribute(gait_rec_kernel(L.rotvec, 3), hipFuncAttributeMaxDynamicSharedMemorySize, (int)need) != hipSuccess ||
+                             hipFuncSetAttribute(gait_rec_kernel(L.rotvec, 7), hipFuncAttributeMaxDynamicSharedMemorySize, (int)need) != hipSuccess)) {
       h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
     }
   }
