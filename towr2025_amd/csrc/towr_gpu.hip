@@ -88,6 +88,7 @@ struct towr_gpu_handle_s {
   hipEvent_t scr_ev = nullptr;
   hipStream_t scr_stream = nullptr;
   bool scr_used = false;
+  bool sync_call = false;   // host_eval: the call synchronises its stream before returning (no event needed)
   // fusion groups (TOWR_GPU_FUSE, see towr_step_kernel): classes that run in one launch
   struct FuseGroup {
     uint32_t mask = 0;        // bit lc: launch class lc belongs to the group
@@ -181,6 +182,10 @@ int scratch_acquire(towr_gpu_handle h, hipStream_t s) {
   return TOWR_OK;
 }
 int scratch_release(towr_gpu_handle h, hipStream_t s) {
+  if (h->sync_call) {   // synchronised before the entry point returns: no later call needs to wait for it
+    h->scr_used = false;
+    return TOWR_OK;
+  }
   HIPCHK(h, hipEventRecord(h->scr_ev, s));
   h->scr_stream = s;
   h->scr_used = true;
@@ -795,12 +800,17 @@ int host_eval(towr_gpu_handle h, int B, const double* X, double* G, double* V, b
     if (!xd) { std::memcpy(h->h_x, X, xb); xd = h->hd_x; }
     double* gd = G ? device_view(h, G, gp) : nullptr;
     double* vd = V ? device_view(h, V, vp) : nullptr;
+    h->sync_call = true;   // (the scratch event: this call ends with a synchronisation below)
     const int rc = h->single.n_units > 0
                        ? launch_fused(h, h->single, 1, xd, L.n, gd ? gd : h->hd_g, L.m, vd ? vd : h->hd_v, L.nnz, G != nullptr,
                                       V != nullptr, h->stream, ter, per)
                        : launch(h, 1, xd, L.n, gd ? gd : h->hd_g, L.m, vd ? vd : h->hd_v, L.nnz, G != nullptr, V != nullptr, h->stream,
                                 ter, per, -1);
-    if (rc) return rc;
+    h->sync_call = false;
+    if (rc) {
+      (void)hipStreamSynchronize(h->stream);   // whatever was launched has finished before the scratch is reused
+      return rc;
+    }
     HIPCHK(h, hipStreamSynchronize(h->stream));
     if (G && !gd) std::memcpy(G, h->h_g, gp);
     if (V && !vd) par_copy(V, h->h_v, vp);
