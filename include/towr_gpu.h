@@ -294,9 +294,12 @@ int towr_gpu_set_batch_terrain(towr_gpu_handle h, int32_t B, const towr_terrain_
  * description's). These return how many entries the reference's Jacobian at x holds OUTSIDE that
  * frozen pattern (0 on terrains without curvature): entries the frozen structure cannot deliver. The
  * values on the frozen pattern are always the reference's, or 0.0 where the reference has no entry.
- * Evaluated on the host with the reference's own operations (the predicate is a floating-point tie),
- * so both are synchronous; the batch form copies X (device) to the host, uses the batch terrains like
- * eval_batch_device, and writes counts[B] in host memory. Layout-only handles answer the single form. */
+ * Both are HOST passes, not device kernels: the predicate is a floating-point tie (is a scale exactly
+ * 0.0?), so it is evaluated with the reference's own host operations (std::pow, no contraction). Both are
+ * synchronous. The batch form ("_device": X lives in HBM) copies X to the host on `stream`, waits for
+ * it, evaluates the B problems on up to 16 host threads with the batch terrains like eval_batch_device,
+ * and writes counts[B] in host memory (bench.py `pattern_watch` times it on a 4096-problem Gap batch).
+ * Layout-only handles answer the single form. */
 int towr_gpu_pattern_outside(towr_gpu_handle h, const double* x, int64_t* count);
 int towr_gpu_pattern_outside_batch_device(towr_gpu_handle h, int32_t B, const double* X, int64_t ldx,
                                           int32_t* counts, void* stream);

@@ -26,6 +26,8 @@ def config_descs():
         # Torque (discretized and node-based), TerrainHard, EELinear
         "biped_torque_hard_eelin": _with_next_tier(F.biped_walk()),
         "hopper_torque_node": _with_next_tier(F.monoped_hopper(), node_torque=True, eelin=False),
+        # the fork's hopper driver (hopper_example.cc:95-171): FiveStepStairs, Torque, phase-duration optimisation
+        "hopper_gait_torque": F.hopper_example_desc(),
         "anymal_gait_torque": _with_next_tier(F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.StairsID),
                                                             optimize_timings=True), hard=False),
         "hyq_gap_torque": _with_next_tier(_hyq_formulation(F.HeightMap.GapID)),
@@ -122,6 +124,7 @@ def cost_descs():
         "anymal_rotvec_costs": _with_costs(_rotvec(F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.StairsID),
                                                                  optimize_timings=True))).to_desc(),
         "monoped_backflip_rotvec": F.backflip_desc(),
+        "hopper_gait_torque": F.hopper_example_desc(),
         "anymal_slope_yaw_costs": _with_costs(F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.SlopeID),
                                                             goal=(1.8, 0.3, 0.0), goal_yaw=0.3)).to_desc(),
     }

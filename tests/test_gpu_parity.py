@@ -166,9 +166,12 @@ def test_fusion_groups(monkeypatch, spec, name):
 # Phase-duration optimisation: the streaming record + compose path (default) and the tile path it
 # replaced (TOWR_GPU_GAIT_TILES, read at handle creation) both against the oracle, and against each other;
 # one and two launch streams (TOWR_GPU_STREAMS: the record scratch is per class, the classes overlap)
-@pytest.mark.parametrize("name", ["anymal_stairs_gaitopt", "biped_gaitopt_rotvec", "anymal_gait_torque", "hyq_gap_gaitopt"])
+@pytest.mark.parametrize("name", ["anymal_stairs_gaitopt", "biped_gaitopt_rotvec", "anymal_gait_torque", "hyq_gap_gaitopt",
+                                  "hopper_gait_torque"])
 def test_gait_paths(monkeypatch, name):
+    from towr2025_amd import _capi as capi
     desc = CONFIGS[name]
+    torque = any(desc.constraints[i].kind == capi.C_TORQUE_DISCRETIZED for i in range(desc.n_constraints))
     o = Oracle(desc)
     x = _perturb(o.initial_x(), 91)
     r, c, _ = o.eval_jac(o.initial_x())   # the pattern is frozen at x0 (Gap: the reference's moves with x)
@@ -183,6 +186,8 @@ def test_gait_paths(monkeypatch, name):
                 monkeypatch.setenv(var, val)
         p = TowrGpuProblem(desc, device=0)
         assert p.kernel_path(0) == (0 if tiles else 1) and p.kernel_path(1) == (0 if tiles else 1)
+        if torque:   # TorqueConstraintDiscretized: record + compose except on curved terrain (data-dependent motion block)
+            assert p.kernel_path(3) == (0 if tiles or is_gap(desc) else 1)
         g, v = p.eval_g_jac(x)
         assert_close(o.eval_g(x), g, r, v_ref, v, o.m, f"{name} tiles={tiles} streams={streams}", cols_ref=c, floor_cols=fc)
         outs[(tiles, streams)] = (g, v)
@@ -332,8 +337,8 @@ def test_batch_device_gait_optimization():
 
 
 def test_batch_device_gait_two_chains(monkeypatch):
-    """The phase-duration path at B >= kSplitBatch (64) runs two chains (FDISC records + compose on the side
-    stream, RangeOfMotion / Dynamic on the caller's), below it one serial chain (towr_gpu.hip
+    """The phase-duration path at B >= kSplitBatch (64) runs two chains (FDISC records + compose on the caller's
+    stream, RangeOfMotion / Dynamic on the side stream), below it one serial chain (towr_gpu.hip
     launch_stream_path). B = 601 (odd: a compose block's problem pair is ragged) against the same problems
     as batches of 37 and 1 (37 < 64: the serial chain): bit-identical, nothing written past m / nnz, a
     sample against the oracle."""
@@ -382,6 +387,15 @@ def test_batch_device_gait_two_chains(monkeypatch):
         _, _, v_ref = o.eval_jac(X[b])
         assert_close(o.eval_g(X[b]), G[b, :p.m], r, v_ref, V[b, :p.nnz], o.m, f"gait chunk problem {b}", cols_ref=c,
                      floor_cols=residue_cols(d, o.n))
+
+
+def test_batch_device_gait_torque():
+    """ANYmal phase-duration optimisation + TorqueConstraintDiscretized (the TQDISC records beside FDISC's in
+    the FDISC chain, its compose blocks in the FDISC compose launch) as a randomised B = 64 device batch:
+    the two-chain path, every problem bit-identical to its B = 1 (single-chain) evaluation."""
+    f = F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.StairsID), optimize_timings=True)
+    f.params_.constraints_.append(F.Parameters.Torque)
+    _batch_vs_single(f, "anymal_gait_torque_batch", B=64, optimize_timings=True)
 
 
 def test_batch_device_rotvec():

@@ -13,6 +13,7 @@ from towr2025_amd import TowrGpuProblem
 CONFIGS = config_descs()
 GAIT = [n for n, d in CONFIGS.items() if d.optimize_timings]
 DYN, ROM, FDISC, TQDISC = 0, 1, 2, 3
+from towr2025_amd._capi import C_TORQUE_DISCRETIZED  # noqa: E402
 
 
 @pytest.mark.parametrize("name", GAIT)
@@ -22,6 +23,15 @@ def test_gait_classes_stream(name):
     assert p.kernel_path(ROM) == 1, "RangeOfMotion should run record + compose"
     gap = CONFIGS[name].terrain.id == 3   # Gap: curvature, FDISC's motion block is data-dependent
     assert p.kernel_path(FDISC) == (0 if gap else 1)
+    torque = any(CONFIGS[name].constraints[i].kind == C_TORQUE_DISCRETIZED for i in range(CONFIGS[name].n_constraints))
+    assert p.kernel_path(TQDISC) == (-1 if not torque else 0 if gap else 1), "TQDISC should run record + compose"
+
+
+def test_fork_hopper_driver_streams_every_class():
+    """The fork's hopper driver (hopper_example.cc: monoped, FiveStepStairs, Torque, phase-duration
+    optimisation): every heavy class on the record + compose path."""
+    p = TowrGpuProblem(CONFIGS["hopper_gait_torque"], device=-1)
+    assert [p.kernel_path(k) for k in (DYN, ROM, FDISC, TQDISC)] == [1, 1, 1, 1]
 
 
 @pytest.mark.parametrize("name", ["anymal_trot_2p4s", "biped_walk_2s", "anymal_trot_rotvec"])

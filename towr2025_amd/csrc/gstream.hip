@@ -93,6 +93,82 @@ __device__ __forceinline__ void fdisc_records(const KParams& P, const Ctx& c, in
   }
 }
 
+// an int field of a record: its 64-bit integer bit pattern (the composer reads the low dword in place)
+__device__ __forceinline__ double gs_int(int v) { return __longlong_as_double((long long)v); }
+// field f of class-global instant k of a record (layout.h: chunk-major, field-major in the chunk)
+__device__ __forceinline__ double* gs_field(double* R, int RS, int k, const GsInst& gi, int f) {
+  return R + (int64_t)RS * (k - gi.kk) + f * gi.nb + gi.kk;
+}
+
+// ------------------------------------------------------------------------------------------------
+// TorqueConstraintDiscretized records (layout.h record format, GS_TQ). Every row of the class is the torque
+// set's full PhaseSpline pattern (rows 2, 3 also the force set's) plus the schedule columns; on a terrain
+// without curvature the motion block is skipped (every scale is exactly 0.0,
+// torque_constraint_discretized.cc:57). One lane per instant: eval_tqdisc's quantities in the composer's
+// form — the terrain basis t1, t2, n, the force row scale b = -k mu n, d torque / d schedule and d force /
+// d schedule, the active-window basis sums of the torque and force polynomials — go to the record; the 4
+// g rows go straight out (:101-125).
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void tq_records(const KParams& P, const RecArgs& A, Ctx c, int b) {
+  constexpr int RS = kTqND + kTqNI;
+  const int K = A.g.K[GS_TQ];
+  const GsInst* inst = A.g.inst[GS_TQ];
+  double* Gb = P.G + (int64_t)b * P.ldg;
+  double* R = A.frec + (int64_t)b * A.fldr + A.tq_off;
+  const double mu = c.ter->friction_coeff;
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    const GsInst gi = inst[k];
+    c.row = gi.seg;
+    const int ee = gi.ee;
+    const double t = gi.t, kf = gi.p0;
+    SplinePt Pm, F, Tq;
+    spline_eval(c, sp_motion(ee), t, Pm);
+    spline_eval(c, sp_force(ee), t, F);
+    spline_eval(c, sp_torque(ee), t, Tq);
+    double n[3], t1[3], t2[3];
+    ter_nbasis(*c.ter, 0, Pm.p[0], Pm.p[1], n);
+    ter_nbasis(*c.ter, 1, Pm.p[0], Pm.p[1], t1);
+    ter_nbasis(*c.ter, 2, Pm.p[0], Pm.p[1], t2);
+    if (P.want_g) {   // eval_tqdisc's g rows
+      const double tau_n = dot3(Tq.p, n), tz_lim = kf * mu * dot3(F.p, n);
+      double* G = Gb + gi.row0;
+      __builtin_nontemporal_store(dot3(Tq.p, t1), G + 0);
+      __builtin_nontemporal_store(dot3(Tq.p, t2), G + 1);
+      __builtin_nontemporal_store(tau_n - tz_lim, G + 2);
+      __builtin_nontemporal_store(-tau_n - tz_lim, G + 3);
+    }
+    auto put = [&](int f, double v) { *gs_field(R, RS, k, gi, f) = v; };
+#pragma unroll
+    for (int e = 0; e < 3; ++e) { put(e, t1[e]); put(3 + e, t2[e]); put(6 + e, n[e]); put(9 + e, -kf * mu * n[e]); }
+    SchedJac Jt, Jf;   // the schedule rows (:210-234): torque and force linear forms (one phase index: one ee)
+    sched_jac(c, sp_torque(ee), t, Tq, Jt);
+    sched_jac(c, sp_force(ee), t, F, Jf);
+#pragma unroll
+    for (int e = 0; e < 3; ++e) { put(12 + e, Jt.dx[e]); put(15 + e, Jt.v[e]); put(18 + e, Jf.dx[e]); put(21 + e, Jf.v[e]); }
+    put(kTqND, gs_int(Jt.cur));
+    double H[4], sums[3][kGsAct];
+    int qa[3];
+    spline_basis(Tq, kPos, H);   // AccumulateLinearFormJacobian of the torque spline (:147-155)
+    gs_window(c, sp_torque(ee), Tq.poly, H, sums, qa);
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      put(kTqND + 1 + e, gs_int(qa[e]));
+#pragma unroll
+      for (int q = 0; q < kGsAct; ++q) put(24 + e * kGsAct + q, sums[e][q]);
+    }
+    spline_basis(F, kPos, H);    // ... of the force spline into the normal-torque rows (:158-163)
+    gs_window(c, sp_force(ee), F.poly, H, sums, qa);
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      put(kTqND + 4 + e, gs_int(qa[e]));
+#pragma unroll
+      for (int q = 0; q < kGsAct; ++q) put(36 + e * kGsAct + q, sums[e][q]);
+    }
+    put(kTqND + 7, gs_int(Tq.poly));
+    put(kTqND + 8, gs_int(F.poly));
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // RangeOfMotion / Dynamic records
 // ------------------------------------------------------------------------------------------------
@@ -115,12 +191,6 @@ struct DynState { using type = typename std::conditional<ROTVEC, DynRvState, Dyn
 template <bool ROTVEC>
 size_t dyn_state_bytes() { return sizeof(typename DynState<ROTVEC>::type); }
 
-// an int field of a record: its 64-bit integer bit pattern (the composer reads the low dword in place)
-__device__ __forceinline__ double gs_int(int v) { return __longlong_as_double((long long)v); }
-// field f of class-global instant k of a record (layout.h: chunk-major, field-major in the chunk)
-__device__ __forceinline__ double* gs_field(double* R, int RS, int k, const GsInst& gi, int f) {
-  return R + (int64_t)RS * (k - gi.kk) + f * gi.nb + gi.kk;
-}
 
 template <bool ROTVEC>
 // part: 0 every lane, 1 the Dynamic lanes only, 2 the RangeOfMotion lanes only (a small batch spreads the
@@ -323,30 +393,32 @@ __device__ __forceinline__ void gs_records(const KParams& P, const GsRecArgs& A,
   }
 }
 
-// The record launch: per problem one block per role (RecArgs::roles, bit 0 the FDISC records, bit 1 the
-// RangeOfMotion / Dynamic records), each staging x and the PhaseSpline tables itself (gait_record_setup).
-// The two roles run as one launch at small batch sizes (B = 1: one launch boundary less) and as two
-// launches on two streams at large ones (towr_gpu.hip launch_stream_path).
-// Instantiated per role set (ROLES), so the FDISC-only launch keeps its own registers. With the
-// RangeOfMotion / Dynamic role: 4 waves per SIMD (128 VGPRs, a few spilled): at the unconstrained 166 VGPRs a
-// second 5-wave block did not fit a CU (MI355X, ANYmal gait B = 1024: 122 us, 100 us at 4 waves per SIMD)
-// ROLES 7: three blocks per problem, FDISC | Dynamic lanes | RangeOfMotion lanes (small batches)
+// The record launch: per problem RecArgs::nparts blocks, block r doing part (parts >> 4 r) & 15
+// (layout.h RecPart): the FDISC records, the TorqueConstraintDiscretized records, or the RangeOfMotion /
+// Dynamic records (all lanes, or one class's lanes when a small batch spreads them over two blocks), each
+// block staging x and the PhaseSpline tables itself (gait_record_setup). towr_gpu.hip launch_stream_path
+// chooses the parts: at large batch sizes one launch per chain, at small ones (B = 1) every part in one.
+// Instantiated per role set (ROLES bit 0 the FDISC / TQDISC parts, bit 1 the RangeOfMotion / Dynamic parts),
+// so the FDISC-only launch keeps its own registers. With the RangeOfMotion / Dynamic role: 4 waves per SIMD
+// (128 VGPRs, a few spilled): at the unconstrained 166 VGPRs a second 5-wave block did not fit a CU (MI355X,
+// ANYmal gait B = 1024: 122 us, 100 us at 4 waves per SIMD)
 template <bool ROTVEC, int ROLES>
 __device__ __forceinline__ void rec_body(const KParams& P, const RecArgs& A, double* smem) {
-  const int nr = ROLES == 7 ? 3 : ROLES == 3 ? 2 : 1;
-  const int b = (int)blockIdx.x / nr, r = (int)blockIdx.x % nr;
-  const int role = nr > 1 ? 1 + (r > 0) : ROLES;   // 1 FDISC, 2 RangeOfMotion / Dynamic
+  const int np = A.nparts;
+  const int b = (int)blockIdx.x / np, part = (A.parts >> (4 * ((int)blockIdx.x % np))) & 15;
   const Ctx c = gait_record_setup<0>(P, b, smem);
-  if constexpr ((ROLES & 1) != 0)
-    if (role == 1) { fdisc_records(P, c, b, A.frec, A.fldr, A.ni); return; }
-  if constexpr ((ROLES & 2) != 0) gs_records<ROTVEC>(P, A.g, c, b, smem, ROLES == 7 ? r : 0);
+  if constexpr ((ROLES & 1) != 0) {
+    if (part == kRecFdisc) { fdisc_records(P, c, b, A.frec, A.fldr, A.ni); return; }
+    if (part == kRecTq) { tq_records(P, A, c, b); return; }
+  }
+  if constexpr ((ROLES & 2) != 0) gs_records<ROTVEC>(P, A.g, c, b, smem, part == kRecGsDyn ? 1 : part == kRecGsRom ? 2 : 0);
 }
 template <bool ROTVEC, int ROLES>
 __global__ void __launch_bounds__(kGsRecMaxBlock) __attribute__((amdgpu_waves_per_eu(4))) towr_gait_rec_kernel(KParams P, RecArgs A) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   rec_body<ROTVEC, ROLES>(P, A, smem);
 }
-__global__ void __launch_bounds__(kGsRecMaxBlock) towr_gait_frec_kernel(KParams P, RecArgs A) {   // FDISC records only
+__global__ void __launch_bounds__(kGsRecMaxBlock) towr_gait_frec_kernel(KParams P, RecArgs A) {   // FDISC / TQDISC records only
   extern __shared__ __attribute__((aligned(16))) double smem[];
   rec_body<false, 1>(P, A, smem);
 }
@@ -422,6 +494,32 @@ struct DynCls {
     // emit_dim scales: motion Cross(f)[r][e]; force Cross(rv)[r][e] (angular) or -1 (linear); torque -1
     const double sc = kind == 0 ? cross_el(de, r, e) : kind == 1 ? (r < 3 ? cross_el(de + 3, r, e) : -1.0) : -1.0;
     return sc * v;
+  }
+};
+
+// TorqueConstraintDiscretized rows r = 0..3 scale the torque window by tb[r] = t1, t2, n, -n and (rows 2,
+// 3) the force window by b = -k mu n; a schedule column is eval_tqdisc's sum of the two linear forms
+struct TqCls {
+  __device__ static int poly(const int32_t* ci, int kind, int) { return ci[2 * (kind == 2 ? 7 : 8)]; }
+  __device__ static double tb(const double* d, int r, int e) { return r == 3 ? -d[6 + e] : d[3 * r + e]; }
+  __device__ static double value(const KParams& P, const int32_t* tmpl, const GsSeg& sg, int pos, const double* d, const int32_t* ci,
+                                 const uint8_t*, int nph) {
+    const int r = sg.r;
+    const int32_t t = tmpl[sg.toff + pos];
+    if (sg.type == 2) {   // d / d schedule (torque_constraint_discretized.cc:210-234)
+      const int col = t & 0xFFFF, cur = ci[0];
+      double v = tb(d, r, 0) * gs_sched_val(d + 12, d + 15, cur, nph, 0, col) + tb(d, r, 1) * gs_sched_val(d + 12, d + 15, cur, nph, 1, col) +
+                 tb(d, r, 2) * gs_sched_val(d + 12, d + 15, cur, nph, 2, col);
+      if (r >= 2)
+        v += d[9] * gs_sched_val(d + 18, d + 21, cur, nph, 0, col) + d[10] * gs_sched_val(d + 18, d + 21, cur, nph, 1, col) +
+             d[11] * gs_sched_val(d + 18, d + 21, cur, nph, 2, col);
+      return v;
+    }
+    const int kind = sg.kind, e = (t >> 22) & 3, q = t & 0x3FFFFF;   // torque (kind 2) or force (1) PhaseCol
+    const unsigned rel = (unsigned)(q - ci[2 * (kind == 2 ? 1 + e : 4 + e)]);
+    if (rel >= (unsigned)kGsAct) return 0.0;
+    const double sum = d[(kind == 2 ? 24 : 36) + e * kGsAct + rel];
+    return (kind == 2 ? tb(d, r, e) : d[9 + e]) * sum;   // emit_dim: scale * basis sum
   }
 };
 
@@ -549,7 +647,7 @@ constexpr int kGsUnits = 4;
 template <int CLS, int BLOCK>
 __device__ __forceinline__ void gs_compose(const KParams& P, const GsBlock* blks, const double* rec, int64_t ldr, int ng, int j, int g0,
                                            double* smem) {
-  using C = typename std::conditional<CLS == GS_ROM, RomCls, DynCls>::type;
+  using C = typename std::conditional<CLS == GS_ROM, RomCls, typename std::conditional<CLS == GS_TQ, TqCls, DynCls>::type>::type;
   constexpr int kGsPre = kGsChunkMax / BLOCK;   // prefetched record doubles per thread
   const GsBlock bl = blks[j];
   const GsGeo g = P.gs_geo[bl.geo];
@@ -624,8 +722,8 @@ __device__ __forceinline__ void gs_compose(const KParams& P, const GsBlock* blks
       if (pos < sg.p0 + sg.len) {
         const double* d = cd + kk * CS;
         const int32_t* ci = reinterpret_cast<const int32_t*>(d + ND);
-        if constexpr (CLS == GS_ROM) x = C::value(P, tmpl, sg, pos, d, ci, pcl + kk * g.Psum, nph[g.ee]);
-        else x = C::value(P, tmpl, sg, pos, d, ci, pcl + kk * g.Psum, nph);
+        if constexpr (CLS == GS_DYN) x = C::value(P, tmpl, sg, pos, d, ci, pcl + kk * g.Psum, nph);
+        else x = C::value(P, tmpl, sg, pos, d, ci, pcl + kk * g.Psum, nph[g.ee]);
       }
       val[t] = x;
     }
@@ -659,15 +757,15 @@ __device__ __forceinline__ void gs_compose(const KParams& P, const GsBlock* blks
 
 
 // The composer launch: every compose block of every problem in one grid. Per problem group the units are
-// [FDISC FsBlocks | RangeOfMotion GsBlocks | Dynamic GsBlocks] (A.nt), so the write-bound FDISC blocks
-// and the Dynamic blocks' longer value phases interleave on every CU, and one launch replaces three (at
-// B = 1 a launch boundary costs more than a compose block). XCD-aware: blocks are dealt round-robin over
-// the 8 XCDs; XCD x takes the contiguous range [x per, (x + 1) per) of (group, unit) pairs, so each XCD
-// writes whole problems' CSR ranges.
-template <int BLOCK, int MASK>   // MASK: the roles of this instantiation (bit 0 FDISC, 1 RangeOfMotion, 2 Dynamic, 3 small kinds)
+// [FDISC FsBlocks | TQDISC GsBlocks | RangeOfMotion GsBlocks | Dynamic GsBlocks | small-kind groups] (A.nt),
+// so the write-bound FDISC blocks and the Dynamic blocks' longer value phases interleave on every CU, and one
+// launch replaces several (at B = 1 a launch boundary costs more than a compose block). XCD-aware: blocks
+// are dealt round-robin over the 8 XCDs; XCD x takes the contiguous range [x per, (x + 1) per) of (group,
+// unit) pairs, so each XCD writes whole problems' CSR ranges.
+template <int BLOCK, int MASK>   // MASK: the roles of this instantiation (bit 0 FDISC, 1 RangeOfMotion, 2 Dynamic, 3 small kinds, 4 TQDISC)
 __global__ void __launch_bounds__(BLOCK, 1) towr_gait_compose_kernel(KParams P, ComposeArgs A) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int NT = A.nt[0] + A.nt[1] + A.nt[2] + A.nt[3];
+  const int NT = A.nt[0] + A.nt[1] + A.nt[2] + A.nt[3] + A.nt[4];
   const int per = (int)((gridDim.x + 7) / 8);
   const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
   int j = w % NT;
@@ -676,6 +774,9 @@ __global__ void __launch_bounds__(BLOCK, 1) towr_gait_compose_kernel(KParams P, 
   if constexpr ((MASK & 1) != 0)
     if (j < A.nt[0]) { fdisc_compose<BLOCK>(P, A.frec, A.fldr, A.ng, j, g0, smem); return; }
   j -= A.nt[0];
+  if constexpr ((MASK & 16) != 0)
+    if (j < A.nt[4]) { gs_compose<GS_TQ, BLOCK>(P, A.blk[GS_TQ], A.frec + A.tq_off, A.fldr, A.ng, j, g0, smem); return; }
+  j -= A.nt[4];
   if constexpr ((MASK & 2) != 0)
     if (j < A.nt[1]) { gs_compose<GS_ROM, BLOCK>(P, A.blk[GS_ROM], A.grec, A.gldr, A.ng, j, g0, smem); return; }
   j -= A.nt[1];
@@ -708,20 +809,25 @@ int64_t gs_record_doubles(const Layout& L, int cls) {
 const void* gait_rec_kernel(bool rotvec, int roles) {
   if (roles == 1) return reinterpret_cast<const void*>(&towr_gait_frec_kernel);
   if (roles == 2) return rotvec ? reinterpret_cast<const void*>(&towr_gait_rec_kernel<true, 2>) : reinterpret_cast<const void*>(&towr_gait_rec_kernel<false, 2>);
-  if (roles == 3) return rotvec ? reinterpret_cast<const void*>(&towr_gait_rec_kernel<true, 3>) : reinterpret_cast<const void*>(&towr_gait_rec_kernel<false, 3>);
-  return rotvec ? reinterpret_cast<const void*>(&towr_gait_rec_kernel<true, 7>) : reinterpret_cast<const void*>(&towr_gait_rec_kernel<false, 7>);
+  return rotvec ? reinterpret_cast<const void*>(&towr_gait_rec_kernel<true, 3>) : reinterpret_cast<const void*>(&towr_gait_rec_kernel<false, 3>);
 }
+template <int MASK>
+const void* compose_fn() { return reinterpret_cast<const void*>(&towr_gait_compose_kernel<(MASK & 25) ? kComposeBlock : kComposeBlockRD, MASK>); }
 const void* gait_compose_kernel(int mask) {
-  // the instantiations the host launches (towr_gpu.hip launch_stream_path): at small batch sizes every role
-  // in one launch; at large ones the FDISC chain beside the Dynamic and RangeOfMotion launches (one class
-  // alone: the per-class timings); block sizes: compose_block
+  // the instantiations the host launches (towr_gpu.hip launch_stream_path, layout.h kComposeMasks): at small
+  // batch sizes every role in one launch; at large ones the FDISC (+ TQDISC) chain beside the Dynamic and
+  // RangeOfMotion launches (one class alone: the per-class timings); block sizes: compose_block
   switch (mask) {
-    case 1: return reinterpret_cast<const void*>(&towr_gait_compose_kernel<kComposeBlock, 1>);
-    case 2: return reinterpret_cast<const void*>(&towr_gait_compose_kernel<kComposeBlockRD, 2>);
-    case 4: return reinterpret_cast<const void*>(&towr_gait_compose_kernel<kComposeBlockRD, 4>);
-    case 6: return reinterpret_cast<const void*>(&towr_gait_compose_kernel<kComposeBlockRD, 6>);
-    case 7: return reinterpret_cast<const void*>(&towr_gait_compose_kernel<kComposeBlock, 7>);
-    default: return reinterpret_cast<const void*>(&towr_gait_compose_kernel<kComposeBlock, 15>);
+    case 1: return compose_fn<1>();
+    case 2: return compose_fn<2>();
+    case 4: return compose_fn<4>();
+    case 6: return compose_fn<6>();
+    case 7: return compose_fn<7>();
+    case 15: return compose_fn<15>();
+    case 16: return compose_fn<16>();
+    case 17: return compose_fn<17>();
+    case 23: return compose_fn<23>();
+    default: return compose_fn<31>();
   }
 }
 size_t fs_compose_lds(const Layout& L) {   // records, row window values, row window starts

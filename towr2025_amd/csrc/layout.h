@@ -36,6 +36,12 @@ struct TileDesc {
 // [fs_ws[2 (wsoff + p)], + kFsWin) of row positions (checked); schedule columns at [js0, js0 + ns1).
 constexpr int kFsInst = 16;   // measured on MI355X (ANYmal gait, B = 1024): 64 -> 0.501 ms, 32 -> 0.463, 16 -> 0.452, 8 -> 0.478
 constexpr int kFsWin = 12;
+// The composers (gstream.hip) find an entry's row (FsBlock) or instant (GsBlock) from its position e in the
+// block's CSR range as (int)((e + 0.5f) * (1.0f / L)). The float product is within 2^-23 relative of
+// (e + 0.5) / L, whose distance to the nearest integer is at least 0.5 / L; the result is exact while
+// (e / L) 2^-23 < 0.5 / L, i.e. for e < 2^22. The layout keeps every block range below half that bound
+// (build_fstream, build_gstream_class: fewer instants per block, or the tile path).
+constexpr int kFloatDivMax = 1 << 21;
 // FDISC record (gstream.hip fdisc_records -> the composer): Hv[kFsWin] | b[5][3] | Jf.dx[3] |
 // Jf.v[3] | ints ws, wd, cur (64-bit integer bit patterns)
 constexpr int kFsB = kFsWin, kFsDx = kFsWin + 15, kFsV = kFsWin + 18, kFsND = kFsWin + 21;
@@ -63,15 +69,16 @@ struct FsBlock {
 //   endeffector, 22-23 dimension, 0-21 PhaseCol index within that dimension's list.
 // A PhaseSpline column is non-zero only in its instant's active window, at most kGsAct PhaseCols per
 // dimension from the polynomial's first (pact); the composer's prologue forms their basis sums.
-enum GsClass { GS_ROM = 0, GS_DYN = 1, GS_COUNT = 2 };
+enum GsClass { GS_ROM = 0, GS_DYN = 1, GS_TQ = 2, GS_COUNT = 3 };   // GS_TQ: TorqueConstraintDiscretized (no base prefix)
 constexpr int kGsRowTypes = 6;
 constexpr int kGsAct = 4;
 // The composer launch (gstream.hip towr_gait_compose_kernel): the ForceConstraintDiscretized,
 // RangeOfMotion and Dynamic compose blocks of every problem in one grid, kComposeBlock threads each.
 constexpr int kComposeBlock = 512;
 constexpr int kComposeBlockRD = 256;   // a launch without FDISC blocks
-inline int compose_block(int mask) { return (mask & 9) ? kComposeBlock : kComposeBlockRD; }
+inline int compose_block(int mask) { return (mask & 25) ? kComposeBlock : kComposeBlockRD; }
 constexpr int kGsInstRom = 16;   // instants per compose block
+constexpr int kGsInstTq = 16;
 constexpr int kGsInstDyn = 2;   // measured on MI355X (ANYmal gait, B = 1024, grouped composer): 2 -> 0.201 ms, 4 -> 0.230, 8 -> 0.219
 // A row type is cut into segments: its base prefix, each maximal run of template columns of one
 // (spline kind, endeffector) or of one endeffector's schedule. Per instant a segment owns W values
@@ -94,7 +101,8 @@ struct GsGeo {
 };
 struct GsBlock { int32_t geo, k0, n_inst, v0, nv, reserved[3]; };   // instants [k0, k0 + n_inst) of the geometry
 // a record lane's instant; kk / nb: its index in its GsBlock and the block's instants (the record chunk)
-struct GsInst { double t; int32_t seg, row0; int16_t ee, kk, nb, reserved; };
+// p0: TorqueConstraintDiscretized's k_friction (ItemDesc::p0)
+struct GsInst { double t; int32_t seg, row0; int16_t ee, kk, nb, reserved; double p0; };
 // Records (gstream.hip gs_records): per instant RS fields, the composer's view of the instant —
 // ND doubles then NI ints (stored as doubles) — so that a composer block's prologue is one contiguous
 // copy. The fields of the GsBlock of instants [k0, k0 + n) form one chunk at RS * k0 (class-global
@@ -104,12 +112,17 @@ struct GsInst { double t; int32_t seg, row0; int16_t ee, kk, nb, reserved; };
 //   Dynamic:       fs[3] | Lp[3] | HpL[4] | HaL[4] | A[axis][p v a][r] (27) | HpA HvA HaA (12), then per
 //                  endeffector Fp[3] | rv[3] | Jf.dx v[6] | Jx.dx v[6] | sums[kind][dim][4] (36);
 //                  ints per endeffector curF | curX | qa[kind][dim] (9) | poly[kind] (3)
+//   TorqueConstraintDiscretized: t1[3] | t2[3] | n[3] | b[3] (= -k mu n) | Jt.dx v[6] | Jf.dx v[6] |
+//                  torque sums[dim][4] (12) | force sums[dim][4] (12); ints cur | qaT[3] | qaF[3] | polyT | polyF
+//                  (torque_constraint_discretized.cc:139-235 without the motion block: a terrain
+//                  without curvature, where every motion scale is exactly 0.0 and the block is skipped, :57)
 // (kind 0 motion, 1 force, 2 torque; sums / qa: the active-window basis sums of the PhaseSpline, the
 // first active PhaseCol of each dimension and the basis sums of up to kGsAct PhaseCols from it)
 constexpr int kRomND = 44, kRomNI = 5;
 constexpr int kDynBaseND = 53, kDynEeND = 54, kDynEeNI = 14;
-TG_HD constexpr int gs_rec_nd(int cls, int E) { return cls == GS_ROM ? kRomND : kDynBaseND + kDynEeND * E; }
-TG_HD constexpr int gs_rec_ni(int cls, int E) { return cls == GS_ROM ? kRomNI : kDynEeNI * E; }
+constexpr int kTqND = 48, kTqNI = 9;
+TG_HD constexpr int gs_rec_nd(int cls, int E) { return cls == GS_ROM ? kRomND : cls == GS_TQ ? kTqND : kDynBaseND + kDynEeND * E; }
+TG_HD constexpr int gs_rec_ni(int cls, int E) { return cls == GS_ROM ? kRomNI : cls == GS_TQ ? kTqNI : kDynEeNI * E; }
 TG_HD constexpr int gs_rec_fields(int cls, int E) { return gs_rec_nd(cls, E) + gs_rec_ni(cls, E); }
 constexpr int kGsGroup = 2;   // problems per composer block (gstream and fstream; 1 -> 0.333 ms, 2 -> 0.321, 8+ slower: a block
                               // waits for its stores to drain before the next problem's records land)
@@ -280,25 +293,29 @@ inline int64_t fs_record_doubles() { return kFsRS; }   // FDISC record doubles p
 size_t gs_stream_lds(const Layout& L, int cls);
 size_t fs_compose_lds(const Layout& L);   // the ForceConstraintDiscretized compose block (bytes)
 int64_t gs_record_doubles(const Layout& L, int cls);
-const void* gait_rec_kernel(bool rotvec, int roles);   // roles: 1 FDISC, 2 RangeOfMotion / Dynamic, 3 both, 7 both in 3 blocks
-const void* gait_compose_kernel(int mask);   // roles: bit 0 FDISC, 1 RangeOfMotion, 2 Dynamic, 3 small kinds
-// the composer launch's arguments: the record arrays (per problem, leading dimensions) and, per
-// role (0 FDISC, 1 RangeOfMotion, 2 Dynamic, 3 small-kind groups), its blocks per problem group (0: not
-// in this launch)
+const void* gait_rec_kernel(bool rotvec, int roles);   // instantiation: bit 0 the FDISC / TQDISC parts, bit 1 the RangeOfMotion / Dynamic parts
+const void* gait_compose_kernel(int mask);   // roles: bit 0 FDISC, 1 RangeOfMotion, 2 Dynamic, 3 small kinds, 4 TQDISC
+constexpr int kComposeMasks[] = {1, 2, 4, 6, 7, 15, 16, 17, 23, 31};   // the instantiated role sets
+// the composer launch's arguments: the record arrays (per problem, leading dimensions; the
+// TorqueConstraintDiscretized records sit in the FDISC record array at tq_off) and, per role (0 FDISC,
+// 1 RangeOfMotion, 2 Dynamic, 3 small-kind groups, 4 TorqueConstraintDiscretized), its blocks per problem
+// group (0: not in this launch). A problem group's units: [FDISC | TQDISC | RangeOfMotion | Dynamic | small kinds]
 struct ComposeArgs {
-  const double* frec; int64_t fldr;
+  const double* frec; int64_t fldr, tq_off;
   const double* grec; int64_t gldr, gdyn_off;
   const GsBlock* blk[GS_COUNT];
-  int32_t nt[4];
+  int32_t nt[5];
   int32_t ng;          // problem groups: a block composes problems g, g + ng, ... (kGsGroup per block)
   int32_t misc_x_off;  // small kinds: the staged x's LDS offset (doubles)
 };
-// the record launch's arguments (towr_gait_rec_kernel): roles bit 0 the FDISC records (frec, fldr,
-// ni instants), bit 1 the RangeOfMotion / Dynamic records (g)
+// the record launch's arguments (towr_gait_rec_kernel): nparts blocks per problem, block r doing part
+// (parts >> 4 r) & 15 (RecPart); the FDISC records (frec, fldr, ni instants) and the
+// TorqueConstraintDiscretized records (frec + tq_off, g.inst[GS_TQ]) share one array per problem
+enum RecPart { kRecFdisc = 1, kRecTq = 2, kRecGs = 3, kRecGsDyn = 4, kRecGsRom = 5 };
 struct RecArgs {
   GsRecArgs g;
-  double* frec; int64_t fldr;
-  int32_t ni, roles;
+  double* frec; int64_t fldr, tq_off;
+  int32_t ni, nparts, parts, reserved;
 };
 size_t gs_dyn_state_bytes(bool rotvec);   // the record kernel's per-Dynamic-instant LDS state
 constexpr int kGsRecMaxBlock = 512;

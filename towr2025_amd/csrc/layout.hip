@@ -562,7 +562,10 @@ int build_fstream(Layout& L, std::string& err) {
     for (const ItemDesc& it : L.items)
       if (it.type == IT_FDISC && it.row0 >= r0 && it.row0 < r0 + nrow) its[(it.row0 - r0) / 5] = it.t;
     for (double t : its) if (t < 0) { err = "internal: ForceConstraintDiscretized instant missing"; return TOWR_ERR_INVALID; }
-    const int cap = kFsInst;   // instants per block (the stream kernel's LDS records)
+    // instants per block (the stream kernel's LDS records); the composer finds an entry's row by a float
+    // division of its position, exact while the block's range stays below kFloatDivMax (layout.h)
+    if (5 * L0 >= kFloatDivMax) return TOWR_OK;
+    const int cap = std::max(1, std::min(kFsInst, (int)((kFloatDivMax - 1) / (5 * L0))));
     const int nb = (K + cap - 1) / cap;
     for (int q = 0; q < nb; ++q) {
       const int a = (int)((int64_t)q * K / nb), b = (int)((int64_t)(q + 1) * K / nb);
@@ -570,6 +573,7 @@ int build_fstream(Layout& L, std::string& err) {
       fb.ee = ee; fb.n_inst = b - a; fb.t0 = (int32_t)ts.size() + a; fb.r0 = r0 + 5 * a;
       fb.v0 = (int32_t)L.row_ptr[r0 + 5 * a]; fb.nv = (int32_t)(L.row_ptr[r0 + 5 * b] - L.row_ptr[r0 + 5 * a]);
       fb.L = (int32_t)L0; fb.tmpl = toff; fb.js0 = js0 < 0 ? (int32_t)L0 : js0; fb.ns1 = nsch; fb.wsoff = wsoff;
+      if (fb.nv >= kFloatDivMax) { err = "internal: FsBlock past the float-division bound"; return TOWR_ERR_INVALID; }
       blocks.push_back(fb);
     }
     ts.insert(ts.end(), its.begin(), its.end());
@@ -594,9 +598,12 @@ struct PhaseDec { int8_t kind = -1, ee = 0, dim = 0; int32_t q = 0; };     // Ph
 bool build_gstream_class(Layout& L, int cls, const std::vector<BaseDec>& bdec, const std::vector<PhaseDec>& pdec,
                          const std::vector<int>& sdec_ee, const std::vector<int>& sdec_j, std::string& why) {
   const int nspl = (int)L.spl.size();
-  const int ctype = cls == GS_ROM ? TOWR_C_RANGE_OF_MOTION : TOWR_C_DYNAMIC;
-  const int itype = cls == GS_ROM ? IT_ROM : IT_DYN;
-  const int R = cls == GS_ROM ? 3 : 6;
+  const int ctype = cls == GS_ROM ? TOWR_C_RANGE_OF_MOTION : cls == GS_TQ ? TOWR_C_TORQUE_DISCRETIZED : TOWR_C_DYNAMIC;
+  const int itype = cls == GS_ROM ? IT_ROM : cls == GS_TQ ? IT_TQDISC : IT_DYN;
+  const int R = cls == GS_ROM ? 3 : cls == GS_TQ ? 4 : 6;
+  const bool per_ee = cls != GS_DYN;   // one endeffector's constraint (RangeOfMotion, TQDISC)
+  // TQDISC on curved terrain adds its motion block only where a scale is non-zero (:57): data-dependent, tiles
+  if (cls == GS_TQ && L.fdisc_motion) { why = "motion block on curved terrain"; return false; }
   std::vector<GsGeo> geos;
   std::vector<GsBlock> blocks;
   std::vector<GsInst> insts;
@@ -607,8 +614,7 @@ bool build_gstream_class(Layout& L, int cls, const std::vector<BaseDec>& bdec, c
   std::vector<uint32_t> vmap;
   std::vector<int16_t> wsv;
   int gmax[3] = {0, 0, 0}, nmax = 0;
-  int cap = cls == GS_ROM ? kGsInstRom : kGsInstDyn;
-  if (const char* e = std::getenv(cls == GS_ROM ? "TOWR_GS_ROM_INST" : "TOWR_GS_DYN_INST")) cap = std::max(1, std::min(64, std::atoi(e)));   // tuning (A/B)
+  int cap = cls == GS_ROM ? kGsInstRom : cls == GS_TQ ? kGsInstTq : kGsInstDyn;
   cap = std::max(1, std::min(cap, kGsChunkMax / gs_rec_fields(cls, L.rb.n_ee)));   // a block's record chunk fits the prefetch
   if (gs_rec_fields(cls, L.rb.n_ee) > kGsChunkMax) { why = "record larger than the composer's prefetch"; return false; }
   int tmax = 0, pmax = 0;
@@ -616,14 +622,14 @@ bool build_gstream_class(Layout& L, int cls, const std::vector<BaseDec>& bdec, c
     if (cs.kind != ctype || cs.rows == 0) continue;
     const int K = cs.rows / R;
     GsGeo g{};
-    g.cls = cls; g.ee = cls == GS_ROM ? cs.ee : -1; g.nrt = R; g.r0 = cs.row0;
+    g.cls = cls; g.ee = per_ee ? cs.ee : -1; g.nrt = R; g.r0 = cs.row0;
     g.rec0 = (int32_t)insts.size();
     // the instants: time and segment row from the items of the set
-    std::vector<GsInst> its((size_t)K, GsInst{-1.0, -1, 0, 0, 0, 0, 0});
+    std::vector<GsInst> its((size_t)K, GsInst{-1.0, -1, 0, 0, 0, 0, 0, 0.0});
     for (const ItemDesc& it : L.items)
       if (it.type == itype && it.row0 >= cs.row0 && it.row0 < cs.row0 + cs.rows) {
         GsInst& q = its[(it.row0 - cs.row0) / R];
-        q.t = it.t; q.seg = it.seg; q.ee = (int16_t)(cls == GS_ROM ? cs.ee : 0); q.row0 = it.row0;
+        q.t = it.t; q.seg = it.seg; q.ee = (int16_t)(per_ee ? cs.ee : 0); q.row0 = it.row0; q.p0 = it.p0;
       }
     for (const GsInst& q : its) if (q.seg < 0) { why = "instant without items"; return false; }
     const int toff = (int)tmpl.size();
@@ -643,18 +649,22 @@ bool build_gstream_class(Layout& L, int cls, const std::vector<BaseDec>& bdec, c
       for (int64_t j = P; j < len; ++j) {
         const int32_t col = L.col[b0 + j];
         if (sdec_ee[col] >= 0) {
-          if (cls == GS_ROM && sdec_ee[col] != cs.ee) { why = "schedule of another endeffector"; return false; }
+          if (per_ee && sdec_ee[col] != cs.ee) { why = "schedule of another endeffector"; return false; }
           tmpl.push_back((int32_t)(0x80000000u | ((uint32_t)sdec_ee[col] << 16) | (uint32_t)sdec_j[col]));
           continue;
         }
         const PhaseDec& d = pdec[col];
-        if (d.kind < 0 || (cls == GS_ROM && (d.kind != 0 || d.ee != cs.ee))) { why = "a column the template cannot express"; return false; }
+        const bool ok = d.kind >= 0 && (cls == GS_DYN || (d.ee == cs.ee && (cls == GS_ROM ? d.kind == 0 : d.kind == 1 || d.kind == 2)));
+        if (!ok) { why = "a column the template cannot express"; return false; }
         tmpl.push_back((int32_t)(((uint32_t)d.kind << 28) | ((uint32_t)d.ee << 25) | ((uint32_t)d.dim << 22) | (uint32_t)d.q));
       }
       Lsum += (int)len; Psum += P;
       tmax = std::max(tmax, (int)tmpl.size() - toff);
     }
     g.Li = Lsum; g.Psum = Psum; g.pc0 = (int32_t)pcode.size(); g.K = K;
+    // instants per compose block: the composer finds an entry's instant by a float division of its position,
+    // exact while the block's range stays below kFloatDivMax (layout.h)
+    const int capg = std::max(1, std::min(cap, (kFloatDivMax - 1) / std::max(1, Lsum)));
     {   // segments (layout.h GsSeg), the position -> segment map, the value map, window starts
       g.seg0 = (int32_t)(L.gs_segs.size() + segs.size());
       g.ts0 = (int32_t)(L.gs_tseg.size() + tseg.size());
@@ -714,7 +724,9 @@ bool build_gstream_class(Layout& L, int cls, const std::vector<BaseDec>& bdec, c
       std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return rank(segs[a]) < rank(segs[b]); });
       vbase = 0;
       for (int q : order) { segs[q].vbase = (int16_t)vbase; vbase += segs[q].W; }
-      if (g.ns > 255 || vbase > 4096 || Lsum > 65535 || (int64_t)vbase * cap > 65535) { why = "segment tables exceed their encodings"; return false; }
+      // encodings: GsSeg::p0 / len / W / vbase are int16 positions within an instant (Lsum), the composer's
+      // value index kk vt + vbase and the window width share one int (16 bits each), segment ids are bytes
+      if (g.ns > 255 || vbase > 4096 || Lsum > INT16_MAX || (int64_t)vbase * capg > 65535) { why = "segment tables exceed their encodings"; return false; }
       for (int sg : order)
         for (int q = 0; q < segs[sg].W; ++q) vmap.push_back((uint32_t)((sg - s0) << 16 | q));
       tseg.insert(tseg.end(), ts.begin(), ts.end());
@@ -733,7 +745,7 @@ bool build_gstream_class(Layout& L, int cls, const std::vector<BaseDec>& bdec, c
         }
       }
     }
-    const int nb = (K + cap - 1) / cap;
+    const int nb = (K + capg - 1) / capg;
     for (int q = 0; q < nb; ++q) {
       const int a = (int)((int64_t)q * K / nb), b = (int)((int64_t)(q + 1) * K / nb);
       GsBlock bl{};
@@ -741,6 +753,7 @@ bool build_gstream_class(Layout& L, int cls, const std::vector<BaseDec>& bdec, c
       nmax = std::max(nmax, b - a);
       bl.v0 = (int32_t)L.row_ptr[cs.row0 + R * a]; bl.nv = (int32_t)(L.row_ptr[cs.row0 + R * b] - L.row_ptr[cs.row0 + R * a]);
       if ((int64_t)bl.nv != (int64_t)(b - a) * Lsum) { why = "internal: block range"; return false; }
+      if (bl.nv >= kFloatDivMax) { why = "internal: compose block past the float-division bound"; return false; }
       for (int k = a; k < b; ++k) { its[k].kk = (int16_t)(k - a); its[k].nb = (int16_t)(b - a); }
       blocks.push_back(bl);
     }
@@ -840,7 +853,7 @@ int build_gstream(Layout& L, std::string& err) {
     std::memcpy(b.data() + o_vmap, L.gs_vmap.data() + g.vm0, 4 * (size_t)g.vt);
     std::memcpy(b.data() + o_tmpl, L.gs_tmpl.data() + g.T[0], 4 * (size_t)ntl);
     std::memcpy(b.data() + o_tseg, L.gs_tseg.data() + g.ts0, (size_t)g.Li);
-    std::memcpy(b.data() + o_pcode, L.gs_pcode.data() + g.pc0, (size_t)g.K * g.Psum);
+    if (g.K * g.Psum > 0) std::memcpy(b.data() + o_pcode, L.gs_pcode.data() + g.pc0, (size_t)g.K * g.Psum);   // TQDISC: no prefix
     if (nws > ws0) std::memcpy(b.data() + o_ws, L.gs_ws.data() + ws0, 2 * (size_t)(nws - ws0));
     g.blob0 = (int32_t)L.gs_blob.size();
     g.blob_n16 = (int32_t)(end / 16);

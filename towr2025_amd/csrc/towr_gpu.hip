@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <initializer_list>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -248,16 +249,18 @@ bool fstream_class(const Layout& L, int lc) { return lc == LC_FDISC && L.fstream
 int gstream_cls(const Layout& L, int lc) {   // the streaming class of launch class lc, or -1
   if (lc == LC_ROM && L.gstream[GS_ROM]) return GS_ROM;
   if (lc == LC_DYN && L.gstream[GS_DYN]) return GS_DYN;
+  if (lc == LC_TQDISC && L.gstream[GS_TQ]) return GS_TQ;
   return -1;
 }
 bool streamed_class(const Layout& L, int lc) { return fstream_class(L, lc) || gstream_cls(L, lc) >= 0; }
 // LDS of the composer launch: its largest compose block
 size_t lds_bytes(const Layout& L, int lc);
 int class_units(const Layout& L, int lc);
-size_t compose_lds(const Layout& L, bool f = true, bool r = true, bool d = true, bool misc = true) {
+size_t compose_lds(const Layout& L, bool f = true, bool r = true, bool d = true, bool misc = true, bool t = true) {
   size_t b = L.fstream && f ? fs_compose_lds(L) : 0;
   if (L.gstream[GS_ROM] && r) b = std::max(b, gs_stream_lds(L, GS_ROM));
   if (L.gstream[GS_DYN] && d) b = std::max(b, gs_stream_lds(L, GS_DYN));
+  if (L.gstream[GS_TQ] && t) b = std::max(b, gs_stream_lds(L, GS_TQ));
   if (misc && class_units(L, LC_MISC) > 0) b = std::max(b, lds_bytes(L, LC_MISC));   // small-kind groups (small batches)
   return b;
 }
@@ -401,49 +404,52 @@ size_t gs_rec_lds(const Layout& L) {
   const size_t Kd = (size_t)gs_kd(L);
   return fs_inst_lds_bytes(L) + Kd * gs_state_stride(L) + sizeof(double) * 9 * Kd * (1 + (size_t)L.rb.n_ee);
 }
-int gs_rec_threads(const Layout& L) {
-  const int64_t Kd = gs_kd(L), Kr = L.gstream[GS_ROM] ? (int64_t)L.gs_inst[GS_ROM].size() : 0;
+int gs_rec_threads(const Layout& L, int64_t Kd, int64_t Kr) {   // the record lanes of Kd Dynamic and Kr RangeOfMotion instants
   const int64_t ee0 = (Kd + 63) & ~63, r0 = (ee0 + 3 * L.rb.n_ee * Kd + 63) & ~63;
   const int64_t lanes = std::max<int64_t>(r0 + Kr, 4 * ((Kd + 63) & ~63));
   return (int)std::min<int64_t>(kGsRecMaxBlock, std::max<int64_t>(64, (lanes + 63) & ~63));
 }
 
 // The streaming path under phase-duration optimisation (gstream.hip) for the streamed classes in
-// `mask` (bits LC_FDISC, LC_ROM, LC_DYN; LC_MISC: the small kinds may join the composer launch):
-//   records: the FDISC records and the RangeOfMotion / Dynamic records (towr_gait_rec_kernel, one block
-//            per problem and role) into the handle's record scratch; they write g;
+// `mask` (bits LC_FDISC, LC_TQDISC, LC_ROM, LC_DYN; LC_MISC: the small kinds may join the composer launch):
+//   records: the FDISC / TQDISC records and the RangeOfMotion / Dynamic records (towr_gait_rec_kernel, one
+//            block per problem and record part, RecPart) into the handle's record scratch; they write g;
 //   compose: the compose blocks of the classes (towr_gait_compose_kernel), each CSR range written once.
+// Only the classes in `mask` are recorded (a single-class launch records nothing else).
 // A batch of kSplitBatch problems or more runs as two chains (one after the other without a side stream,
-// TOWR_GPU_STREAMS=1): FDISC records + compose on the caller's
-// stream beside the RangeOfMotion / Dynamic records + the Dynamic and RangeOfMotion compose launches on the
-// side stream, so that the write-bound FDISC compose overlaps the latency-bound record work (MI355X, ANYmal
-// gait, B = 1024, one box: 0.600-0.608 ms per step; one chain 0.663, records in 256-problem chunks
-// pipelined against the compose 0.737, Dynamic + RangeOfMotion in one compose launch 0.640). The small
-// kinds then follow the shorter chain on the side stream (*forked: the caller launches them there and
-// joins). A smaller batch (B = 1: IPOPT's callbacks) is two launches on the caller's stream: both record
-// roles in one, every compose role and the small-kind groups in the other (*misc_done) — at B = 1 a
-// launch boundary or a cross-stream event costs more than any overlap gains (MI355X, ANYmal gait: 97 us
-// for the per-class chains, 70 us for four launches on one stream).
+// TOWR_GPU_STREAMS=1): FDISC + TQDISC records + their compose launch on the caller's stream beside the
+// RangeOfMotion / Dynamic records + the Dynamic and RangeOfMotion compose launches on the side stream, so that
+// the write-bound FDISC compose overlaps the latency-bound record work (MI355X, ANYmal gait, B = 1024, one
+// box: 0.600-0.608 ms per step; one chain 0.663, records in 256-problem chunks pipelined against the compose
+// 0.737, Dynamic + RangeOfMotion in one compose launch 0.640). The small kinds then follow the shorter chain
+// on the side stream (*forked: the caller launches them there and joins). A smaller batch (B = 1: IPOPT's
+// callbacks) is two launches on the caller's stream: every record part in one, every compose role and the
+// small-kind groups in the other (*misc_done) — at B = 1 a launch boundary or a cross-stream event costs
+// more than any overlap gains (MI355X, ANYmal gait: 97 us for the per-class chains, 70 us for four launches
+// on one stream).
 constexpr int kSplitBatch = 64;
 bool compose_lds_attr(size_t lds) {   // every composer instantiation may take `lds` bytes of LDS
-  for (int m = 1; m < 16; ++m)
+  for (int m = 1; m < 32; ++m)
     if (hipFuncSetAttribute(gait_compose_kernel(m), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return false;
   return true;
 }
+// per-problem record doubles: [FDISC instants | TQDISC records] and [RangeOfMotion | Dynamic]
+int64_t fs_rec_doubles(const Layout& L) { return fs_record_doubles() * (int64_t)L.fs_t.size(); }
+int64_t frec_ld(const Layout& L) { return fs_rec_doubles(L) + (L.gstream[GS_TQ] ? gs_record_doubles(L, GS_TQ) : 0); }
 int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t st, bool* forked, bool* misc_done) {
   const Layout& L = h->L;
   const int B = P.B;
-  const bool fs = L.fstream && ((mask >> LC_FDISC) & 1);
+  const bool fs = L.fstream && ((mask >> LC_FDISC) & 1), tq = L.gstream[GS_TQ] && ((mask >> LC_TQDISC) & 1);
   const bool gr = L.gstream[GS_ROM] && ((mask >> LC_ROM) & 1), gd = L.gstream[GS_DYN] && ((mask >> LC_DYN) & 1);
   const int32_t ni = (int32_t)L.fs_t.size();
-  const int64_t fldr = fs_record_doubles() * ni;
+  const int64_t fldr = frec_ld(L), tq_off = fs_rec_doubles(L);
   const int64_t lr = L.gstream[GS_ROM] ? gs_record_doubles(L, GS_ROM) : 0, ld = L.gstream[GS_DYN] ? gs_record_doubles(L, GS_DYN) : 0;
-  if (fs)
+  if (fs || tq)
     if (int rc = scratch_grow(h, &h->d_fsrec, &h->fsrec_cap, B, fldr)) return rc;
   if (gr || gd)
     if (int rc = scratch_grow(h, &h->d_gsrec, &h->gsrec_cap, B, lr + ld)) return rc;
   const bool big = B >= kSplitBatch;
-  const bool split = fs && (gr || gd) && h->n_side > 0 && big;
+  const bool split = (fs || tq) && (gr || gd) && h->n_side > 0 && big;
   const bool misc = !big && ((mask >> LC_MISC) & 1) && class_units(L, LC_MISC) > 0;
   const hipStream_t gst = split ? h->side[0] : st;   // the RangeOfMotion / Dynamic chain
   if (split) {
@@ -451,69 +457,79 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
     HIPCHK(h, hipStreamWaitEvent(gst, h->fork, 0));
   }
   RecArgs R{};
-  R.frec = h->d_fsrec; R.fldr = fldr; R.ni = ni;
+  R.frec = h->d_fsrec; R.fldr = fldr; R.tq_off = tq_off; R.ni = fs ? ni : 0;
   R.g.rec = h->d_gsrec; R.g.ldr = lr + ld; R.g.dyn_off = lr;
-  for (int c = 0; c < GS_COUNT; ++c) {
-    R.g.inst[c] = h->d_gs_inst[c];
-    R.g.K[c] = L.gstream[c] ? (int32_t)L.gs_inst[c].size() : 0;
-  }
+  for (int c = 0; c < GS_COUNT; ++c) R.g.inst[c] = h->d_gs_inst[c];
+  R.g.K[GS_ROM] = gr ? (int32_t)L.gs_inst[GS_ROM].size() : 0;
+  R.g.K[GS_DYN] = gd ? (int32_t)L.gs_inst[GS_DYN].size() : 0;
+  R.g.K[GS_TQ] = tq ? (int32_t)L.gs_inst[GS_TQ].size() : 0;
   R.g.st_off = (int32_t)(fs_inst_lds_bytes(L) / sizeof(double));
   R.g.scr_off = R.g.st_off + (int32_t)(gs_kd(L) * gs_state_stride(L) / sizeof(double));
-  // threads: the FDISC role alone one lane per instant (whole waves, up to kFsRecBlock) and its staging's
-  // LDS only; the RangeOfMotion / Dynamic role gs_rec_threads; both roles in one launch the larger
-  auto records = [&](int roles, hipStream_t s) -> int {
-    R.roles = roles;
-    const int nr = roles == 7 ? 3 : roles == 3 ? 2 : 1;
-    const int fth = (int)std::min<int64_t>(kFsRecBlock, std::max<int64_t>(64, ((int64_t)ni + 63) & ~63));
-    const int threads = roles == 2 ? gs_rec_threads(L) : roles == 1 ? fth : std::max(gs_rec_threads(L), kFsRecBlock);
-    const size_t lds = roles == 1 ? fs_inst_lds_bytes(L) : gs_rec_lds(L);
+  // one block per (problem, part); threads: the parts' lanes in whole waves (FDISC / TQDISC one per instant,
+  // the RangeOfMotion / Dynamic parts gs_rec_threads), at most kGsRecMaxBlock; LDS: the staging
+  // (fs_inst_lds_bytes), with a RangeOfMotion / Dynamic part also its states and scratch (gs_rec_lds)
+  auto records = [&](std::initializer_list<int> parts, hipStream_t s) -> int {
+    R.nparts = 0; R.parts = 0;
+    int roles = 0;
+    int64_t lanes = 64;
+    for (int p : parts) {
+      if (p == 0) continue;
+      R.parts |= p << (4 * R.nparts++);
+      roles |= p == kRecFdisc || p == kRecTq ? 1 : 2;
+      lanes = std::max<int64_t>(lanes, p == kRecFdisc ? R.ni : p == kRecTq ? R.g.K[GS_TQ] : gs_rec_threads(L, R.g.K[GS_DYN], R.g.K[GS_ROM]));
+    }
+    if (R.nparts == 0) return TOWR_OK;
+    const int threads = (int)std::min<int64_t>(kGsRecMaxBlock, (lanes + 63) & ~63);
+    const size_t lds = (roles & 2) ? gs_rec_lds(L) : fs_inst_lds_bytes(L);
     void* aa[] = {&P, &R};
-    HIPCHK(h, hipLaunchKernel(gait_rec_kernel(L.rotvec, roles), dim3((unsigned)(B * nr)), dim3((unsigned)threads), aa, lds, s));
+    HIPCHK(h, hipLaunchKernel(gait_rec_kernel(L.rotvec, roles), dim3((unsigned)(B * R.nparts)), dim3((unsigned)threads), aa, lds, s));
     return TOWR_OK;
   };
   ComposeArgs C{};
-  C.frec = h->d_fsrec; C.fldr = fldr;
+  C.frec = h->d_fsrec; C.fldr = fldr; C.tq_off = tq_off;
   C.grec = h->d_gsrec; C.gldr = lr + ld; C.gdyn_off = lr;
-  C.blk[GS_ROM] = h->d_gs_blk[GS_ROM]; C.blk[GS_DYN] = h->d_gs_blk[GS_DYN];
+  for (int c = 0; c < GS_COUNT; ++c) C.blk[c] = h->d_gs_blk[c];
   C.ng = (B + kGsGroup - 1) / kGsGroup;
   C.misc_x_off = (int32_t)lds_region(L, LC_MISC);
-  auto compose = [&](bool f, bool r, bool d, bool m, hipStream_t s) -> int {
+  auto compose = [&](bool f, bool t, bool r, bool d, bool m, hipStream_t s) -> int {
     const bool j = P.want_jac != 0;   // without the Jacobian only the small kinds (their g rows)
     C.nt[0] = f && j ? (int32_t)L.fs_blocks.size() : 0;
     C.nt[1] = r && j ? (int32_t)L.gs_blocks[GS_ROM].size() : 0;
     C.nt[2] = d && j ? (int32_t)L.gs_blocks[GS_DYN].size() : 0;
     C.nt[3] = m ? class_units(L, LC_MISC) : 0;
-    const int64_t grid = ((int64_t)C.ng * (C.nt[0] + C.nt[1] + C.nt[2] + C.nt[3]) + 7) / 8 * 8;   // whole rounds of 8 (XCD-aware mapping)
+    C.nt[4] = t && j ? (int32_t)L.gs_blocks[GS_TQ].size() : 0;
+    const int64_t units = (int64_t)C.nt[0] + C.nt[1] + C.nt[2] + C.nt[3] + C.nt[4];
+    const int64_t grid = ((int64_t)C.ng * units + 7) / 8 * 8;   // whole rounds of 8 (XCD-aware mapping)
     if (grid == 0) return TOWR_OK;
     if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
     void* ab[] = {&P, &C};
-    // the launch's own roles: their instantiation (registers) and LDS; without FDISC or small kinds 256 threads
-    const int roles = (C.nt[0] ? 1 : 0) | (C.nt[1] ? 2 : 0) | (C.nt[2] ? 4 : 0) | (C.nt[3] ? 8 : 0);
+    // the launch's own roles: their instantiation (registers) and LDS; without FDISC, TQDISC or small kinds 256 threads
+    const int roles = (C.nt[0] ? 1 : 0) | (C.nt[1] ? 2 : 0) | (C.nt[2] ? 4 : 0) | (C.nt[3] ? 8 : 0) | (C.nt[4] ? 16 : 0);
     HIPCHK(h, hipLaunchKernel(gait_compose_kernel(roles), dim3((unsigned)grid), dim3(compose_block(roles)), ab,
-                              compose_lds(L, C.nt[0] > 0, C.nt[1] > 0, C.nt[2] > 0, C.nt[3] > 0), s));
+                              compose_lds(L, C.nt[0] > 0, C.nt[1] > 0, C.nt[2] > 0, C.nt[3] > 0, C.nt[4] > 0), s));
     return TOWR_OK;
   };
   if (big) {   // (without a side stream the two chains run one after the other on the caller's stream)
-    if (fs) {
-      if (int rc = records(1, st)) return rc;
-      if (int rc = compose(true, false, false, false, st)) return rc;
+    if (fs || tq) {
+      if (int rc = records({fs ? kRecFdisc : 0, tq ? kRecTq : 0}, st)) return rc;
+      if (int rc = compose(fs, tq, false, false, false, st)) return rc;
     }
     if (gr || gd) {
-      if (int rc = records(2, gst)) return rc;
-      if (int rc = compose(false, false, gd, false, gst)) return rc;
-      if (int rc = compose(false, gr, false, false, gst)) return rc;
+      if (int rc = records({kRecGs}, gst)) return rc;
+      if (int rc = compose(false, false, false, gd, false, gst)) return rc;
+      if (int rc = compose(false, false, gr, false, false, gst)) return rc;
     }
-  } else {
-    if (fs || gr || gd)   // both RangeOfMotion and Dynamic: their lanes in two blocks (shorter chains per CU)
-      if (int rc = records(fs && gr && gd ? 7 : (fs ? 1 : 0) | (gr || gd ? 2 : 0), st)) return rc;
-    if (int rc = compose(fs, gr, gd, misc, st)) return rc;
+  } else {   // every record part in one launch (RangeOfMotion and Dynamic in two blocks beside FDISC: shorter chains per CU)
+    const bool two = gr && gd && (fs || tq);
+    if (int rc = records({fs ? kRecFdisc : 0, tq ? kRecTq : 0, two ? kRecGsDyn : (gr || gd) ? kRecGs : 0, two ? kRecGsRom : 0}, st)) return rc;
+    if (int rc = compose(fs, tq, gr, gd, misc, st)) return rc;
   }
   *forked = split;   // the caller's other launches follow on the side stream, then it joins
   *misc_done = misc;
   return TOWR_OK;
 }
 
-bool uses_scratch(const Layout& L) { return L.fstream || L.gstream[GS_ROM] || L.gstream[GS_DYN]; }
+bool uses_scratch(const Layout& L) { return L.fstream || L.gstream[GS_ROM] || L.gstream[GS_DYN] || L.gstream[GS_TQ]; }
 
 int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, int64_t ldg, double* V, int64_t ldv,
                    int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem, int only_class);
@@ -523,7 +539,14 @@ int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, in
   const bool scr = uses_scratch(h->L);
   if (scr)
     if (int rc = scratch_acquire(h, s)) return rc;
-  if (int rc = launch_classes(h, B, X, ldx, G, ldg, V, ldv, want_g, want_jac, s, terrains, per_problem, only_class)) return rc;
+  if (int rc = launch_classes(h, B, X, ldx, G, ldg, V, ldv, want_g, want_jac, s, terrains, per_problem, only_class)) {
+    // a failure after the streaming path forked its side stream: join every side stream into s and still
+    // order the scratch, so that later calls (and scratch_grow's hipFree) wait for the kernels already queued
+    for (int i = 0; i < h->n_side; ++i)
+      if (hipEventRecord(h->join[i], h->side[i]) == hipSuccess) (void)hipStreamWaitEvent(s, h->join[i], 0);
+    if (scr) (void)scratch_release(h, s);
+    return rc;
+  }
   return scr ? scratch_release(h, s) : TOWR_OK;
 }
 
@@ -1006,6 +1029,7 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
       (r = upload(h, &h->d_fs_iee, L.fs_iee)) || (r = upload(h, &h->d_fs_irow, L.fs_irow)) || (r = upload(h, &h->d_fs_iblk, L.fs_iblk)) ||
       (r = upload(h, &h->d_gs_geo, L.gs_geo)) || (r = upload(h, &h->d_gs_tmpl, L.gs_tmpl)) || (r = upload(h, &h->d_gs_pcode, L.gs_pcode)) ||
       (r = upload(h, &h->d_gs_blk[GS_ROM], L.gs_blocks[GS_ROM])) || (r = upload(h, &h->d_gs_blk[GS_DYN], L.gs_blocks[GS_DYN])) ||
+      (r = upload(h, &h->d_gs_blk[GS_TQ], L.gs_blocks[GS_TQ])) || (r = upload(h, &h->d_gs_inst[GS_TQ], L.gs_inst[GS_TQ])) ||
       (r = upload(h, &h->d_gs_inst[GS_ROM], L.gs_inst[GS_ROM])) || (r = upload(h, &h->d_gs_inst[GS_DYN], L.gs_inst[GS_DYN])) ||
       (r = upload(h, &h->d_gs_segs, L.gs_segs)) || (r = upload(h, &h->d_gs_tseg, L.gs_tseg)) || (r = upload(h, &h->d_gs_vmap, L.gs_vmap)) ||
       (r = upload(h, &h->d_gs_ws, L.gs_ws)) || (r = upload(h, &h->d_gs_blob, L.gs_blob)))
@@ -1060,7 +1084,7 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
     // streams gave 0.524, 0.521, 0.550 ms per step — every kind already fills the CUs' LDS, so kinds
     // cannot co-reside. Under phase-duration optimisation (streaming FDISC) two streams: the write-bound
     // FDISC stream kernel runs beside the latency-bound Dynamic tiles.
-    const int want = ns ? std::atoi(ns) - 1 : (h->L.gait && h->L.fstream ? 1 : 0);
+    const int want = ns ? std::atoi(ns) - 1 : (h->L.gait && (h->L.fstream || h->L.gstream[GS_TQ]) ? 1 : 0);
     h->n_side = std::max(0, std::min(towr_gpu_handle_s::kMaxSide, want));
     if (h->n_side > 0 && hipEventCreateWithFlags(&h->fork, hipEventDisableTiming) != hipSuccess) { h->err = "hipEventCreate failed"; return bail(TOWR_ERR_HIP); }
     for (int i = 0; i < h->n_side; ++i)
@@ -1094,15 +1118,14 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
       h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
     }
   }
-  if (L.fstream || L.gstream[GS_ROM] || L.gstream[GS_DYN]) {   // the record kernels share fs_inst_lds_bytes' layout
+  if (uses_scratch(L)) {   // the record kernels share fs_inst_lds_bytes' layout
     const size_t lds = fs_inst_lds_bytes(L);
     if (lds > 160 * 1024) { h->err = "problem too large for the streaming instant kernel's LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
     const size_t need = gs_rec_lds(L);
     if (need > 160 * 1024) { h->err = "problem too large for the record kernel's LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
     if (need > 64 * 1024 && (hipFuncSetAttribute(gait_rec_kernel(L.rotvec, 1), hipFuncAttributeMaxDynamicSharedMemorySize, (int)need) != hipSuccess ||
                              hipFuncSetAttribute(gait_rec_kernel(L.rotvec, 2), hipFuncAttributeMaxDynamicSharedMemorySize, (int)need) != hipSuccess ||
-                             hipFuncSetAttribute(gait_rec_kernel(L.rotvec, 3), hipFuncAttributeMaxDynamicSharedMemorySize, (int)need) != hipSuccess ||
-                             hipFuncSetAttribute(gait_rec_kernel(L.rotvec, 7), hipFuncAttributeMaxDynamicSharedMemorySize, (int)need) != hipSuccess)) {
+                             hipFuncSetAttribute(gait_rec_kernel(L.rotvec, 3), hipFuncAttributeMaxDynamicSharedMemorySize, (int)need) != hipSuccess)) {
       h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
     }
   }
@@ -1126,8 +1149,8 @@ int towr_gpu_destroy(towr_gpu_handle h) {
                  h->d_bterrain, h->d_x, h->d_g, h->d_v, h->d_f, h->d_grad,
                  h->d_traj_pd, h->d_traj_n, h->d_traj_c0, h->d_traj_t, h->d_fsb, h->d_fs_t, h->d_fs_tmpl, h->d_fs_ws,
                  h->d_fs_iee, h->d_fs_irow, h->d_fs_iblk, h->d_fsrec, h->d_lin, h->d_soft_b, h->d_soft_rp, h->d_soft_col, h->d_sg, h->d_sv,
-                 h->single.d_units, h->d_gs_geo, h->d_gs_tmpl, h->d_gs_pcode, h->d_gs_blk[0], h->d_gs_blk[1], h->d_gs_inst[0],
-                 h->d_gs_inst[1], h->d_gsrec, h->d_gs_segs, h->d_gs_tseg, h->d_gs_vmap, h->d_gs_ws, h->d_gs_blob};
+                 h->single.d_units, h->d_gs_geo, h->d_gs_tmpl, h->d_gs_pcode, h->d_gs_blk[0], h->d_gs_blk[1], h->d_gs_blk[2],
+                 h->d_gs_inst[0], h->d_gs_inst[1], h->d_gs_inst[2], h->d_gsrec, h->d_gs_segs, h->d_gs_tseg, h->d_gs_vmap, h->d_gs_ws, h->d_gs_blob};
   if (h->device >= 0) for (void* p : dev) if (p) (void)hipFree(p);
   void* host[] = {h->h_x, h->h_g, h->h_v};
   for (void* p : host) if (p) (void)hipHostFree(p);

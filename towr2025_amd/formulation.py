@@ -712,6 +712,34 @@ def monoped_hopper() -> NlpFormulation:
     return f
 
 
+def hopper_example():
+    """The fork's own hopper driver exactly as towr/test/hopper_example.cc:95-171 builds it: monoped on the
+    FiveStepStairs terrain (:53-86), its 13 phase durations, Parameters::Torque added to the default
+    constraints (:145), costs ForcesCost 1e-9 and EEMotionCost 1e-4 (:147-148), OptimizePhaseDurations
+    (:150), then NodeCosts 1e-4 on the base-linear and base-angular position and velocity nodes of every
+    dimension, added after GetCosts (:163-168). The stance-position bounds (:114-122) are variable bounds,
+    not evaluation inputs. Returns (formulation, cost terms in ifopt AddCostSet order)."""
+    f = monoped_hopper()
+    f.terrain_ = HeightMap.MakeTerrain(HeightMap.StepsID)
+    P = f.params_
+    P.constraints_.append(Parameters.Torque)
+    P.costs_ = [(Parameters.ForcesCostID, 1e-9), (Parameters.EEMotionCostID, 1e-4)]
+    P.OptimizePhaseDurations()
+    # final base: z = 0.6 + FiveStepStairs().GetHeight(0, 0) (:131), 0.6 in front of the stairs
+    f.final_base_ = BaseState(lin_p=(0.0, 0.0, 0.6 + f.terrain_.GetHeight(0.0, 0.0)))
+    costs = f.cost_terms()
+    for dim in range(3):
+        for var in (capi.VAR_BASE_LIN, capi.VAR_BASE_ANG):
+            costs.append(dict(kind=capi.COST_NODE, weight=1e-4, ip=[var, 0, dim]))
+            costs.append(dict(kind=capi.COST_NODE, weight=1e-4, ip=[var, 1, dim]))
+    return f, costs
+
+
+def hopper_example_desc() -> capi.ProblemDesc:
+    f, costs = hopper_example()
+    return f.to_desc(costs=costs)
+
+
 def procedural_monoped():
     """towr/test/procedural_example.cc:54-242: manual variable order and constraint list, node-based
     ForceConstraint, plain linear initialisation. Returns (formulation, varsets, constraints, goal)."""
