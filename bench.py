@@ -193,6 +193,28 @@ def single_leg(desc, name, note, device, reps=300, cpu=True, sigma=0.02):
     return out
 
 
+def pattern_watch(Xd, B, device, reps=3):
+    """towr_gpu_pattern_outside_batch_device on B ANYmal problems with randomised Gap terrains (the curved
+    terrain whose reference pattern moves with x): a synchronous host pass — X copied to the host, the
+    watched instants evaluated on up to 16 host threads with the reference's operations (include/towr_gpu.h)."""
+    from towr2025_amd import TowrGpuProblem
+    from towr2025_amd import formulation as F
+    p = TowrGpuProblem(F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.GapID)).to_desc(), device=device)
+    rng = np.random.default_rng(SEED)
+    p.set_batch_terrain([F.HeightMap(F.HeightMap.GapID, (rng.uniform(0.9, 1.1), rng.uniform(0.45, 0.55),
+                                                         rng.uniform(1.2, 1.6))).to_c() for _ in range(B)])
+    counts = np.zeros(B, dtype=np.int32)
+    p.pattern_outside_batch(Xd, counts)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        p.pattern_outside_batch(Xd, counts)
+    ms = (time.perf_counter() - t0) / reps * 1e3
+    p.close()
+    return {"ms_per_batch": ms, "problems": B, "value": B / (ms * 1e-3), "unit": "problems/s",
+            "entries_outside_total": int(counts.sum()),
+            "note": "host pass (D2H of X, up to 16 host threads), ANYmal on randomised Gap terrains, the headline's x"}
+
+
 def host_batch(prob, Xh, reps=3):
     """PCIe-inclusive rate of towr_gpu_eval_batch (host X, G, V; the caller's G / V reused across
     calls): through the pinned staging, and with G / V registered (in-place DMA)."""
@@ -375,55 +397,56 @@ def main():
                             "GB/s": B * cbytes / (ms * 1e-3) / 1e9,
                             "note": "ANYmal trot + Forces/EEMotion/Energy/AngularMomentum/EEBasePos costs, same batch"}
         cprob.close()
-    if rank == 0 and not args.no_gait:
-        # BASELINE configs[3]'s formulation (phase-duration optimisation: PhaseSplines with x-dependent
-        # durations, schedule Jacobian columns) on a batch of the same randomised instances
-        gprob = TowrGpuProblem(F.anymal_trot(optimize_timings=True).to_desc(), device=local)
-        Bg = min(B, 1024)
-        Xg, gter = make_batch(gprob, Bg, first_id=shard_first_id(rank, Bg), optimize_timings=True)
-        gprob.set_batch_terrain(gter)
-        Xgd = [torch.from_numpy(Xg[k]).to(dev) for k in range(2)]
-        Gg = torch.empty((Bg, (gprob.m + 15) // 16 * 16), dtype=torch.float64, device=dev)
-        Vg = torch.empty((Bg, (gprob.nnz + 15) // 16 * 16), dtype=torch.float64, device=dev)
+    def batch_leg(lprob, Xl, Bl, ter):
+        """ms per eval_batch_device of Bl problems (leg_warm untimed calls, then leg_reps timed ones, HIP
+        events on the launch stream), cycling over the x sets Xl (device tensors)."""
+        lprob.set_batch_terrain(ter)
+        Gl = torch.empty((Bl, (lprob.m + 15) // 16 * 16), dtype=torch.float64, device=dev)
+        Vl = torch.empty((Bl, (lprob.nnz + 15) // 16 * 16), dtype=torch.float64, device=dev)
         for i in range(leg_warm):
-            gprob.eval_batch_device(Xgd[i % 2], Gg, Vg, stream=stream)
+            lprob.eval_batch_device(Xl[i % len(Xl)], Gl, Vl, stream=stream)
         a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
         for i in range(leg_reps):
-            gprob.eval_batch_device(Xgd[i % 2], Gg, Vg, stream=stream)
+            lprob.eval_batch_device(Xl[i % len(Xl)], Gl, Vl, stream=stream)
         z.record(stream)
         torch.cuda.synchronize()
         ms = a.elapsed_time(z) / leg_reps
-        gb = gprob.algorithmic_bytes_per_call()
-        out["gait_optimization"] = {"value": Bg / (ms * 1e-3), "unit": "calls/s", "ms_per_batch": ms, "problems": Bg,
-                                    "n": gprob.n, "m": gprob.m, "nnz": gprob.nnz, "GB/s": Bg * gb / (ms * 1e-3) / 1e9,
-                                    "note": "BASELINE configs[3] formulation (ANYmal, phase-duration optimisation), "
-                                            "randomised Flat/Stairs instances, durations +-3 %"}
-        gprob.close()
+        lb = lprob.algorithmic_bytes_per_call()
+        return {"value": Bl / (ms * 1e-3), "unit": "calls/s", "ms_per_batch": ms, "problems": Bl,
+                "n": lprob.n, "m": lprob.m, "nnz": lprob.nnz, "GB/s": Bl * lb / (ms * 1e-3) / 1e9}
+
+    if rank == 0 and not args.no_gait:
+        # BASELINE configs[3]'s formulation (phase-duration optimisation: PhaseSplines with x-dependent
+        # durations, schedule Jacobian columns) on a batch of the same randomised instances
+        Bg = min(B, 1024)
+        for key, f, note in (
+                ("gait_optimization", F.anymal_trot(optimize_timings=True),
+                 "BASELINE configs[3] formulation (ANYmal, phase-duration optimisation), randomised Flat/Stairs "
+                 "instances, durations +-3 %"),
+                ("gait_torque", F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.StairsID), optimize_timings=True),
+                 "the same + Parameters::Torque (TorqueConstraintDiscretized per foot, dt 0.02, on the record + "
+                 "compose path), the formulation class of the fork's hopper driver (hopper_example.cc:145-150)")):
+            if key == "gait_torque":
+                f.params_.constraints_.append(F.Parameters.Torque)
+            gprob = TowrGpuProblem(f.to_desc(), device=local)
+            Xg, gter = make_batch(gprob, Bg, first_id=shard_first_id(rank, Bg), optimize_timings=True)
+            out[key] = batch_leg(gprob, [torch.from_numpy(Xg[k]).to(dev) for k in range(2)], Bg, gter)
+            out[key]["note"] = note
+            gprob.close()
     if rank == 0 and not args.no_gait:
         # RotVecConverter base orientation (Parameters::RotationVector, SURVEY §8(f) rank 3) on the same
         # randomised instances: the headline formulation with the rotation-vector base parameterisation
         fr = F.anymal_trot()
         fr.params_.angular_rep_ = 1
         rprob = TowrGpuProblem(fr.to_desc(), device=local)
-        rprob.set_batch_terrain(terrains)
-        Gr = torch.empty((B, (rprob.m + 15) // 16 * 16), dtype=torch.float64, device=dev)
-        Vr = torch.empty((B, (rprob.nnz + 15) // 16 * 16), dtype=torch.float64, device=dev)
-        for i in range(leg_warm):
-            rprob.eval_batch_device(X[i % N_X], Gr, Vr, stream=stream)
-        a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        for i in range(leg_reps):
-            rprob.eval_batch_device(X[i % N_X], Gr, Vr, stream=stream)
-        z.record(stream)
-        torch.cuda.synchronize()
-        ms = a.elapsed_time(z) / leg_reps
-        rb = rprob.algorithmic_bytes_per_call()
-        out["rotvec"] = {"value": B / (ms * 1e-3), "unit": "calls/s", "ms_per_batch": ms, "problems": B,
-                         "n": rprob.n, "m": rprob.m, "nnz": rprob.nnz, "GB/s": B * rb / (ms * 1e-3) / 1e9,
-                         "note": "ANYmal trot with the RotVecConverter base orientation (angular_rep = 1), the "
-                                 "headline's randomised instances and x"}
+        out["rotvec"] = batch_leg(rprob, [X[k] for k in range(N_X)], B, terrains)
+        out["rotvec"]["note"] = ("ANYmal trot with the RotVecConverter base orientation (angular_rep = 1), the "
+                                 "headline's randomised instances and x")
         rprob.close()
+    if rank == 0 and not args.no_gait:
+        # the frozen-pattern check (towr_gpu_pattern_outside_batch_device, a host pass) on a Gap batch
+        out["pattern_watch"] = pattern_watch(X[0], B, local)
     if rank == 0 and not args.no_host:
         # PCIe-inclusive rate through the host-buffer entry point (towr_gpu_eval_batch: H2D of X,
         # chunked launches, D2H of G and V overlapping the next chunk) — reported beside, never as `value`
@@ -453,6 +476,9 @@ def main():
             F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.StairsID), optimize_timings=True).to_desc(),
             "BASELINE configs[3]: ANYmal on stairs, phase-duration optimisation",
             "B = 1 through host pointers, registered outputs", local, cpu=cpu)
+        out["single_call_hopper_gait"] = single_leg(
+            F.hopper_example_desc(), "the fork's hopper driver (hopper_example.cc:95-171): monoped, FiveStepStairs, "
+            "Torque, phase-duration optimisation", "B = 1 through host pointers, registered outputs", local, cpu=cpu)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if distributed:

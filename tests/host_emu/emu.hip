@@ -1,6 +1,7 @@
 // TEST INFRASTRUCTURE ONLY — host emulation of towr_eval_kernel's per-item loop, used by the
 // CPU test suite to check engine_math.h values against the oracle before GPU runs. It is built
 // into tests/host_emu/build/libemu.so and is never linked into or loaded by the product.
+#include "../../towr2025_amd/csrc/gs_cls.h"
 #include "../../towr2025_amd/csrc/layout.h"
 
 #include <cmath>
@@ -83,6 +84,31 @@ extern "C" int emu_eval_ex(const towr_problem_desc_t* d, int n_data, const towr_
       }
     }
   }
+  if (L.gstream[GS_TQ]) {   // the streaming TorqueConstraintDiscretized composition (gstream.hip tq_records + gs_compose)
+    c.pact = L.pact.data();
+    constexpr int RS = kTqND + kTqNI;
+    for (const GsBlock& bl : L.gs_blocks[GS_TQ]) {
+      const GsGeo& gg = L.gs_geo[bl.geo];
+      std::vector<double> rec((size_t)bl.n_inst * RS);
+      for (int kk = 0; kk < bl.n_inst; ++kk) {   // the record lanes
+        const GsInst& gi = L.gs_inst[GS_TQ][gg.rec0 + bl.k0 + kk];
+        c.seg = L.segs.data() + (size_t)gi.seg * L.spl.size();
+        double gq[4];
+        tq_record(c, gi, [&](int f, double val) { rec[(size_t)kk * RS + f] = val; }, gq);
+        for (int i = 0; i < 4; ++i) g[gi.row0 + i] = gq[i];
+      }
+      for (int e = 0; e < bl.nv; ++e) {   // every entry of the block's range: segment, window, value or 0
+        const int kk = e / gg.Li, rr = e - kk * gg.Li;
+        const GsSeg& sg = L.gs_segs[gg.seg0 + L.gs_tseg[gg.ts0 + rr]];
+        const double* d = rec.data() + (size_t)kk * RS;
+        const int32_t* ci = reinterpret_cast<const int32_t*>(d + kTqND);
+        const int ws = sg.type == 1 ? L.gs_ws[sg.wsoff + TqCls::poly(ci, sg.kind, sg.ee)] : 0;
+        const int q = rr - (sg.p0 + ws);
+        v[bl.v0 + e] = q >= 0 && q < sg.W && rr < sg.p0 + sg.len
+                           ? TqCls::value(L.rb, L.gs_tmpl.data(), sg, rr, d, ci, nullptr, L.sched[gg.ee].n_phases) : 0.0;
+      }
+    }
+  }
   return 0;
 }
 extern "C" int emu_eval(const towr_problem_desc_t* d, const double* x, double* g, double* v, char* err, int errlen) {
@@ -119,8 +145,9 @@ extern "C" int emu_cost(const towr_problem_desc_t* d, const double* x, double* f
 extern "C" int emu_stats(const towr_problem_desc_t* d) {
   Layout L; std::string e;
   if (build_layout(*d, L, e)) return -1;
-  std::printf("fstream %d blocks %zu tmpl_max %d | gstream rom %d (%zu blocks) dyn %d (%zu blocks)\n", (int)L.fstream, L.fs_blocks.size(),
-              L.fs_tmpl_max, (int)L.gstream[GS_ROM], L.gs_blocks[GS_ROM].size(), (int)L.gstream[GS_DYN], L.gs_blocks[GS_DYN].size());
+  std::printf("fstream %d blocks %zu tmpl_max %d | gstream rom %d (%zu blocks) dyn %d (%zu blocks) tq %d (%zu blocks)\n", (int)L.fstream,
+              L.fs_blocks.size(), L.fs_tmpl_max, (int)L.gstream[GS_ROM], L.gs_blocks[GS_ROM].size(), (int)L.gstream[GS_DYN],
+              L.gs_blocks[GS_DYN].size(), (int)L.gstream[GS_TQ], L.gs_blocks[GS_TQ].size());
   std::printf("n %d m %d nnz %lld nodecol %zu | gait tables: spl %zu pinfo %zu pcols %zu pact %zu sched %zu\n", L.n, L.m,
               (long long)L.nnz, L.nodecol.size(), L.spl.size(), L.pinfo.size(), L.pcols.size(), L.pact.size(), L.sched.size());
   {
@@ -134,7 +161,7 @@ extern "C" int emu_stats(const towr_problem_desc_t* d) {
                 sizeof(PolyPhase) * L.pinfo.size(), sizeof(int32_t) * L.pact.size(), sizeof(PhaseCol) * L.pcols.size(),
                 8 * (2 * L.pinfo.size() + L.sched.size() * phs), sizeof(DynEulerState), sizeof(DynRvState));
   }
-  for (int cls = 0; cls < 2; ++cls) {
+  for (int cls = 0; cls < GS_COUNT; ++cls) {
     if (!L.gstream[cls]) continue;
     long nv = 0; int maxnv = 0;
     for (const GsBlock& bl : L.gs_blocks[cls]) { nv += bl.nv; maxnv = std::max(maxnv, bl.nv); }

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--rotvec", action="store_true")
     ap.add_argument("--no-gait", action="store_true", help="the headline formulation (fixed phase durations)")
     ap.add_argument("--only", default=None, help="comma-separated part names: time only these, no whole step")
+    ap.add_argument("--torque", action="store_true", help="ANYmal on stairs + Parameters::Torque (bench.py gait_torque)")
     args = ap.parse_args()
     import torch
     from towr2025_amd import _capi as capi
@@ -28,7 +29,10 @@ def main():
     from towr2025_amd import TowrGpuProblem
     from towr2025_amd import formulation as F
     import bench
-    f = F.anymal_trot(optimize_timings=not args.no_gait)
+    f = F.anymal_trot(optimize_timings=not args.no_gait,
+                      terrain=F.HeightMap.MakeTerrain(F.HeightMap.StairsID) if args.torque else None)
+    if args.torque:
+        f.params_.constraints_.append(F.Parameters.Torque)
     if args.rotvec:
         f.params_.angular_rep_ = 1
     p = TowrGpuProblem(f.to_desc(), device=0)

@@ -515,7 +515,11 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
       if (int rc = compose(fs, tq, false, false, false, st)) return rc;
     }
     if (gr || gd) {
+#ifdef TOWR_EXP_RECSPLIT
+      if (int rc = records({gd ? kRecGsDyn : 0, gr ? kRecGsRom : 0}, gst)) return rc;
+#else
       if (int rc = records({kRecGs}, gst)) return rc;
+#endif
       if (int rc = compose(false, false, false, gd, false, gst)) return rc;
       if (int rc = compose(false, false, gr, false, false, gst)) return rc;
     }
