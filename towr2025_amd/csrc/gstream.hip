@@ -39,41 +39,47 @@ namespace {
 // one contiguous copy.
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ double fs_int(int v) { return __longlong_as_double((long long)v); }
+// FDISC instant k (fs_t order) of the problem in c: its record fields through put(field, value) and its 5 g
+// rows (when wanted) straight to Gb
+template <class Put>
+__device__ __forceinline__ void fdisc_record(const KParams& P, const Ctx& c, int k, double* Gb, Put&& put) {
+  FdiscInstant o;
+  fdisc_instant(c, P.fs_iee[k], P.fs_t[k], o);
+  const FsBlock fb = P.fsb[P.fs_iblk[k]];
+#pragma unroll
+  for (int i = 0; i < 5; ++i)
+#pragma unroll
+    for (int e = 0; e < 3; ++e) put(kFsB + 3 * i + e, o.b[i][e]);
+#pragma unroll
+  for (int e = 0; e < 3; ++e) { put(kFsDx + e, o.Jf.dx[e]); put(kFsV + e, o.Jf.v[e]); }
+  put(kFsND + 2, fs_int(o.Jf.cur));
+  if (P.want_g) {
+    const int row = P.fs_irow[k];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) __builtin_nontemporal_store(o.g[i], Gb + row + i);
+  }
+  const int poly = o.poly;
+  const int ws = P.fs_ws[2 * (fb.wsoff + poly)], wd = P.fs_ws[2 * (fb.wsoff + poly) + 1];
+  put(kFsND, fs_int(ws));
+  put(kFsND + 1, fs_int(wd));
+  double h0 = o.H[0], h1 = o.H[1], h2 = o.H[2], h3 = o.H[3];
+  asm volatile("" : "+v"(h0), "+v"(h1), "+v"(h2), "+v"(h3));
+  const int32_t* tm = P.fs_tmpl + fb.tmpl;
+#pragma unroll 4
+  for (int q = 0; q < kFsWin; ++q) {   // the window's basis sums (schedule entries: never read, 0)
+    const int pos = ws + q;
+    const int32_t te = pos < fb.L ? tm[pos] : -1;
+    put(q, te >= 0 ? phase_basis_sum(c.pcols[te & 0xFFFFFF], poly, h0, h1, h2, h3) : 0.0);
+  }
+}
 __device__ __forceinline__ void fdisc_records(const KParams& P, const Ctx& c, int b, double* rec, int64_t ldr, int32_t ni) {
   double* Gb = P.G + (int64_t)b * P.ldg;
   double* R = rec + (int64_t)b * ldr;
   for (int k = threadIdx.x; k < ni; k += blockDim.x) {
-    FdiscInstant o;
-    fdisc_instant(c, P.fs_iee[k], P.fs_t[k], o);
     const FsBlock fb = P.fsb[P.fs_iblk[k]];
     const int kk = k - fb.t0, nb = fb.n_inst;
     double* r = R + (int64_t)kFsRS * fb.t0 + kk;
-    auto put = [&](int f, double v) { r[f * nb] = v; };
-#pragma unroll
-    for (int i = 0; i < 5; ++i)
-#pragma unroll
-      for (int e = 0; e < 3; ++e) put(kFsB + 3 * i + e, o.b[i][e]);
-#pragma unroll
-    for (int e = 0; e < 3; ++e) { put(kFsDx + e, o.Jf.dx[e]); put(kFsV + e, o.Jf.v[e]); }
-    put(kFsND + 2, fs_int(o.Jf.cur));
-    if (P.want_g) {
-      const int row = P.fs_irow[k];
-#pragma unroll
-      for (int i = 0; i < 5; ++i) __builtin_nontemporal_store(o.g[i], Gb + row + i);
-    }
-    const int poly = o.poly;
-    const int ws = P.fs_ws[2 * (fb.wsoff + poly)], wd = P.fs_ws[2 * (fb.wsoff + poly) + 1];
-    put(kFsND, fs_int(ws));
-    put(kFsND + 1, fs_int(wd));
-    double h0 = o.H[0], h1 = o.H[1], h2 = o.H[2], h3 = o.H[3];
-    asm volatile("" : "+v"(h0), "+v"(h1), "+v"(h2), "+v"(h3));
-    const int32_t* tm = P.fs_tmpl + fb.tmpl;
-#pragma unroll 4
-    for (int q = 0; q < kFsWin; ++q) {   // the window's basis sums (schedule entries: never read, 0)
-      const int pos = ws + q;
-      const int32_t te = pos < fb.L ? tm[pos] : -1;
-      put(q, te >= 0 ? phase_basis_sum(c.pcols[te & 0xFFFFFF], poly, h0, h1, h2, h3) : 0.0);
-    }
+    fdisc_record(P, c, k, Gb, [&](int f, double v) { r[f * nb] = v; });
   }
 }
 
@@ -388,6 +394,17 @@ __device__ __forceinline__ void fdisc_compose(const KParams& P, const double* re
   double* rowv = cd + ((n * kFsCS + 1) & ~1);
   int32_t* wsr = reinterpret_cast<int32_t*>(rowv + nr * kFsWin);
   auto ci = [&](int k, int f) -> int { return *reinterpret_cast<const int32_t*>(cd + k * kFsCS + kFsND + f); };   // ws, wd, cur
+#ifdef TOWR_EXP_FSFOLD
+  // the block forms its instants' records itself (fdisc_record) from its problem's x staged here; the
+  // PhaseSpline tables and the node table are read from global memory (L2)
+  double* xs = rowv + nr * kFsWin + ((((nr + 1) / 2) + 1) & ~1);
+  Ctx c{};
+  c.seg = nullptr; c.sg = P.sg; c.row = -1;
+  c.x = xs; c.nodecol = P.nodecol; c.dur = P.dur;
+  c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
+  c.gait = true; c.rotvec = false; c.eelin = P.eelin; c.lin = P.lin; c.dyn_scratch = nullptr;
+  c.spl = P.spl; c.sched = P.sched; c.pinfo = P.pinfo; c.pact = P.pact; c.pcols = P.pcols;
+#endif
   // the chunk: element e = f * n + kk -> LDS kk * kFsCS + f
   const int nch = n * kFsRS;
   const int64_t chunk0 = (int64_t)kFsRS * fb.t0;
@@ -405,7 +422,7 @@ __device__ __forceinline__ void fdisc_compose(const KParams& P, const double* re
     for (int q = 0; q < kFsPre; ++q) pre[q] = dst[q] >= 0 ? src[tid + q * BLOCK] : 0.0;
   };
   const int Lr = fb.L, js0 = fb.js0, ns1 = fb.ns1;
-  const float invL = 1.0f / (float)Lr;   // exact row of element e < 2^20 for rows <= 4096 long (|err| << 0.5 / Lr)
+  const float invL = 1.0f / (float)Lr;   // exact row for block ranges below kFloatDivMax (layout.h, checked by build_fstream)
   // entry j of row r (instant k = r / 5, pyramid row i): eval_fdisc's value (see fdisc_sched_value / emit_dim)
   auto entry = [&](int r, int j) -> double {
     const unsigned js = (unsigned)(j - js0);
@@ -435,11 +452,23 @@ __device__ __forceinline__ void fdisc_compose(const KParams& P, const double* re
     return entry(r, e - r * Lr);
   };
   int b = g0;
+#ifndef TOWR_EXP_FSFOLD
   fetch(b);
+#endif
   for (;;) {
+#ifdef TOWR_EXP_FSFOLD
+    (void)rec; (void)ldr;
+    stage_x<BLOCK, false>(P, P.X + (int64_t)b * P.ldx, xs, nullptr);
+    __syncthreads();
+    if (tid < n) {
+      c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
+      fdisc_record(P, c, fb.t0 + tid, P.G + (int64_t)b * P.ldg, [&](int f, double v) { cd[tid * kFsCS + f] = v; });
+    }
+#else
 #pragma unroll
     for (int q = 0; q < kFsPre; ++q)
       if (dst[q] >= 0) cd[dst[q]] = pre[q];
+#endif
     __syncthreads();
     for (int t = tid; t < nr * kFsWin; t += BLOCK) {   // window value q of row r: b[i][e(q)] * basis sum (emit_dim)
       const int r = t / kFsWin, q = t - r * kFsWin;
@@ -451,7 +480,9 @@ __device__ __forceinline__ void fdisc_compose(const KParams& P, const double* re
     for (int t = tid; t < nr; t += BLOCK) wsr[t] = ci(t / 5, 0);
     __syncthreads();
     const int bn = b + ng;
+#ifndef TOWR_EXP_FSFOLD
     if (bn < P.B) fetch(bn);   // in flight while this problem streams
+#endif
     {
       double* out = P.V + (int64_t)b * P.ldv + fb.v0;
       const int nv = fb.nv;
@@ -534,7 +565,7 @@ __device__ __forceinline__ void gs_compose(const KParams& P, const GsBlock* blks
   const int Li = g.Li;
   const float invLi = 1.0f / (float)Li;
   auto value = [&](int e) -> double {
-    const int kk = (int)(((float)e + 0.5f) * invLi);   // exact for block ranges < 2^20
+    const int kk = (int)(((float)e + 0.5f) * invLi);   // exact below kFloatDivMax (layout.h, checked by build_gstream_class)
     const int rr = e - kk * Li;
     const int2 p = wp[kk * ns + tsg[rr]];
     const unsigned q = (unsigned)(rr - p.x);
@@ -673,7 +704,11 @@ const void* gait_compose_kernel(int mask) {
   }
 }
 size_t fs_compose_lds(const Layout& L) {   // records, row window values, row window starts
+#ifdef TOWR_EXP_FSFOLD
+  return sizeof(double) * ((size_t)((kFsInst * kFsCS + 1) & ~1) + 5 * kFsInst * kFsWin + ((((5 * kFsInst + 1) / 2) + 1) & ~1) + ((L.n + 2) & ~1));
+#else
   return sizeof(double) * ((size_t)(((kFsInst * kFsCS + 1) & ~1) + 5 * kFsInst * kFsWin + (5 * kFsInst + 1) / 2 + 1) & ~(size_t)1);
+#endif
 }
 size_t gs_dyn_state_bytes(bool rotvec) { return rotvec ? dyn_state_bytes<true>() : dyn_state_bytes<false>(); }
 

@@ -43,7 +43,9 @@ struct KParams {
   int32_t lds_rows_off;          // start of the g buffer in the dynamic LDS (doubles)
   int32_t lds_x_off;             // start of the staged x (+ zero slot) and node-column table
   int32_t lds_scr_off;           // DYN: per-instant endeffector sum terms (instants x n_ee x 6)
-  int32_t lds_rv_off;            // DYN, fixed gait, RotVec: per-instant converter states (DynRvState)
+  double* rvc;                   // DYN, fixed gait, RotVec: the pre-pass's base-angular coefficients (kRvCoef per instant)
+  const RvInst* rvi;             // ... and its instants (n_rvi per problem)
+  int32_t n_rvi;
   int32_t n, n_pad, n_nodecol;
   int32_t want_g, want_jac, fdisc_motion;
   const int32_t* misc_tiles;      // merged small-kind launch: kMiscWaves tile ids per group
@@ -257,6 +259,8 @@ const void* misc_kernel_for(bool gait);
 const void* step_kernel_for(bool gait, bool rotvec, int kblock);
 const void* cost_kernel_for(bool gait, bool grad, bool rotvec);
 const void* traj_kernel_for(bool gait);
+const void* rv_coef_kernel();
+constexpr int kRvCoefBlock = 256;   // the RotVec coefficient pre-pass: 4 waves, one component each
 constexpr int kCostBlock = 256;   // objective kernel: one block per problem
 constexpr int kTrajBlock = 64;    // trajectory kernel: one block per (problem, 64 sample times)
 

@@ -149,6 +149,10 @@ struct WatchItem {
   int32_t cnt[2];         // entries of a block of dimension 0 / 1 (the motion spline's Jacobian row)
 };
 
+// a Dynamic instant of the RotVec coefficient pre-pass (fixed gait): its time and segment-table row
+struct RvInst { double t; int32_t seg, reserved; };
+constexpr int kRvCoef = 27;   // coefficients per instant: per component e, Mp[3] | Mv[3] | Ma[3] (dyn_rv_column)
+
 struct VarSetInfo { int kind, ee, col0, n; };
 struct ConsInfo { int kind, ee, row0, rows; };
 
@@ -189,7 +193,9 @@ struct Layout {
   int32_t type_lds_rows_off[IT_COUNT] = {};   // start of the g buffer inside the type's LDS
   int32_t type_lds_dummy_off[IT_COUNT] = {};  // per-lane dummy slots for absent candidates
   int32_t dyn_scr_off = 0;                    // DYN LDS: endeffector sum terms after the g rows
-  int32_t dyn_rv_off = 0;                     // DYN LDS, fixed gait, RotVec: per-instant DynRvState after them
+  // fixed gait, RotVec: the Dynamic instants whose base-angular coefficients the pre-pass forms
+  // (tiles.hip towr_rv_coef_kernel; a RotVec group-1 item's a0 indexes them)
+  std::vector<RvInst> rv_inst;
   // algorithmic bytes per problem of each type's launch: CSR values + g rows written, distinct
   // x columns read (= the columns of its Jacobian rows)
   int64_t type_bytes[IT_COUNT] = {};

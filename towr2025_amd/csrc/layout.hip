@@ -1192,6 +1192,21 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
     }
   }
 
+  // ---- fixed gait, RotVec: the Dynamic instants of the base-angular coefficient pre-pass (tiles.hip
+  // towr_rv_coef_kernel); the three component items of an instant (a1 = 1, 2, 3, consecutive) get its index in a0
+  L.rv_inst.clear();
+  if (L.rotvec && !L.gait)
+    for (ItemDesc& it : L.items) {
+      if (it.type != IT_DYN || it.group != 1 || it.a1 <= 0) continue;
+      if (it.a1 == 1) {
+        for (int bb = 0; bb < 4; ++bb)   // the pre-pass reads x in global memory: no constant node values
+          for (int e = 0; e < 3; ++e)
+            if (L.segs[(size_t)it.seg * L.spl.size() + SP_BASE_ANG].col[bb][e] >= L.n) { err = "internal: constant base-angular node value"; return TOWR_ERR_INVALID; }
+        L.rv_inst.push_back(RvInst{it.t, it.seg, 0});
+      }
+      it.a0 = (int32_t)L.rv_inst.size() - 1;
+    }
+
   // ---- cost terms (their sample times append rows to the segment table)
   if (int rc = build_costs(d, base_d, L, err)) return rc;
 
@@ -1386,11 +1401,6 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
       if (t == IT_DYN) {   // + per-instant endeffector sum terms (dyn_g0_a)
         L.dyn_scr_off = L.type_lds[t];
         L.type_lds[t] += type_spec(IT_DYN, E, L.gait, L.rotvec).max_inst * E * 6;
-        if (L.rotvec && !L.gait) {   // + one converter state per instant (tile_body: formed once, read by the three component lanes)
-          L.type_lds[t] = (L.type_lds[t] + 1) & ~1;
-          L.dyn_rv_off = L.type_lds[t];
-          L.type_lds[t] += type_spec(IT_DYN, E, L.gait, L.rotvec).max_inst * (int32_t)((sizeof(DynRvState) + 15) / 16 * 2);
-        }
       }
     }
     L.type_tile0[IT_COUNT] = (int32_t)L.tiles.size();

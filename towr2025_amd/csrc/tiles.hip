@@ -112,7 +112,7 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
     it = ItemDesc{}; it.type = IT_NONE; it.slot = 0;
   }
   // GAIT: direct HBM emission into the zero-filled V (see TileEmit)
-  // fixed gait, RotVec Dynamic: eval_dyn never takes group 1 (the LDS state path below, kStateLds)
+  // fixed gait, RotVec Dynamic: eval_dyn never takes group 1 (the pre-pass coefficients, kRvPre)
   TileEmit<TBLOCK, slot_depth(TYPE), GAIT, gait_slot_pre(TYPE), (TYPE == IT_DYN && ROTVEC && !GAIT) ? 1 : 0> em(
       P.slots + it.slot, GAIT ? Vb + T.v0 : smem, GAIT ? Gb : smem + lds_rows_off - T.r0);
   if constexpr (GAIT) {
@@ -182,19 +182,14 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
     }
   }
   DynG0 g0;   // DYN group 0 between its two phases
-  // fixed gait, RotVec: the base-angular converter state of each instant is formed once, in LDS, by its
-  // component-0 lane before the phase barrier; the three component lanes form their columns after it
-  // (RotVec Dynamic, ANYmal, B = 4096: 0.143 -> 0.131 ms, no scratch; the same for the Euler block, with
-  // per-axis items, measured 0.062 -> 0.088 ms: its state is cheap, and the axis columns then wait
-  // behind the barrier instead of running beside the endeffector lanes)
-  constexpr bool kStateLds = TYPE == IT_DYN && ROTVEC && !GAIT;
-  DynRvState* sts = reinterpret_cast<DynRvState*>(smem + P.lds_rv_off);
-  const bool st_lane = kStateLds && it.type == TYPE && it.group == 1;   // (RotVec group-1 items are per component, a1 > 0)
+  // fixed gait, RotVec: the base-angular coefficients of each (instant, component) come from the pre-pass
+  // (towr_rv_coef_kernel, launched before this kernel); the component lanes only form and emit their 12 entries
+  constexpr bool kRvPre = TYPE == IT_DYN && ROTVEC && !GAIT;
   if (it.type == TYPE) {
     if constexpr (TYPE == IT_DYN) {
       if (it.group == 0) dyn_g0_a(c, it, em, g0);
-      else if (st_lane) {
-        if (it.a1 == 1) dyn_rv_state(c, it.t, sts[it.a2]);
+      else if (kRvPre && it.group == 1) {
+        if (P.want_jac) dyn_rv_emit_pre(c, it, P.rvc + (int64_t)b * P.n_rvi + it.a0, (int64_t)P.B * P.n_rvi, em);
       }
       else eval_dyn(c, it, em);   // group 1 and the endeffector groups (these deposit their sum terms)
     } else {
@@ -215,10 +210,6 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
       for (int ee = 0; ee < P.rb.n_ee; ++ee)
         for (int e = 0; e < 3; ++e) { ts[e] += d[ee * 6 + e]; fs[e] += d[ee * 6 + 3 + e]; }
       dyn_g0_b(c, it, emb, g0, fs, ts);
-    }
-    if (st_lane) {
-      dyn_rv_emit(c, it, sts[it.a2], em);
-      em.flush();
     }
   }
   __syncthreads();
@@ -288,6 +279,39 @@ __global__ void __launch_bounds__(KBLOCK, (KBLOCK == 256 ? 2 : 1)) towr_step_ker
   }
 }
 
+// The base-angular coefficients of the fixed-gait RotVec Dynamic block (dyn_rv_state + dyn_rv_column<e>,
+// rotvec_converter.cc:148-561 through dynamic_constraint.cc:124-166) for every (problem, instant, component),
+// before the Dynamic launch. In the tile, one lane per instant formed the converter state and three lanes its
+// columns after a barrier: the block's life was that chain at 2 waves per SIMD (242 VGPRs). Here one lane per
+// (problem, instant, component) at full occupancy; waves are component-uniform (wave w: component w % 3, 64
+// consecutive (problem, instant) pairs), and the coefficients are stored field-major (field f of component
+// e at (9 e + f) B K + b K + q), so both this kernel's stores and the tile's loads coalesce.
+__global__ void __launch_bounds__(kRvCoefBlock) towr_rv_coef_kernel(KParams P) {
+  const int K = P.n_rvi;
+  const int64_t pairs = (int64_t)P.B * K, chunks = (pairs + 63) / 64;
+  const int64_t w = (int64_t)blockIdx.x * (kRvCoefBlock / 64) + threadIdx.x / 64;
+  if (w >= 3 * chunks) return;
+  const int e = (int)(w % 3);
+  const int64_t pr = (w / 3) * 64 + (threadIdx.x & 63);
+  if (pr >= pairs) return;
+  const int b = (int)(pr / K), q = (int)(pr - (int64_t)b * K);
+  const RvInst ri = P.rvi[q];
+  Ctx c{};
+  c.seg = nullptr; c.sg = P.sg; c.row = ri.seg;
+  c.x = P.X + (int64_t)b * P.ldx;   // base-angular node values only: never a constant node (layout.hip checks)
+  c.nodecol = P.nodecol; c.spl = P.spl; c.dur = P.dur; c.ter = P.terrains;
+  c.rb = P.rb; c.gait = false; c.rotvec = true;
+  DynRvState S;
+  dyn_rv_state(c, ri.t, S);
+  double M[9];
+  if (e == 0) dyn_rv_column<0>(S, M, M + 3, M + 6);
+  else if (e == 1) dyn_rv_column<1>(S, M, M + 3, M + 6);
+  else dyn_rv_column<2>(S, M, M + 3, M + 6);
+  double* o = P.rvc + (int64_t)9 * e * pairs + pr;
+#pragma unroll
+  for (int f = 0; f < 9; ++f) __builtin_nontemporal_store(M[f], o + f * pairs);
+}
+
 template <bool GAIT, bool ROTVEC>
 const void* kernel_for_mode(int type) {
   switch (type) {
@@ -315,6 +339,7 @@ const void* tile_kernel_for(int type, bool gait, bool rotvec) {
   if (gait) return rotvec ? kernel_for_mode<true, true>(type) : kernel_for_mode<true, false>(type);
   return rotvec ? kernel_for_mode<false, true>(type) : kernel_for_mode<false, false>(type);
 }
+const void* rv_coef_kernel() { return reinterpret_cast<const void*>(&towr_rv_coef_kernel); }
 const void* misc_kernel_for(bool gait) {
   return gait ? reinterpret_cast<const void*>(&towr_misc_kernel<true>) : reinterpret_cast<const void*>(&towr_misc_kernel<false>);
 }

@@ -81,6 +81,9 @@ struct towr_gpu_handle_s {
   uint4* d_gs_blob = nullptr;
   GsBlock* d_gs_blk[GS_COUNT] = {};
   GsInst* d_gs_inst[GS_COUNT] = {};
+  double* d_rvc = nullptr;     // fixed gait, RotVec: the Dynamic base-angular coefficients of the pre-pass (scratch)
+  int64_t rvc_cap = 0;
+  RvInst* d_rvi = nullptr;
   double* d_gsrec = nullptr;   // their records, both classes (scratch, grown on demand)
   int64_t gsrec_cap = 0;
   // The scratch above (and the soft child's g / values, d_sg / d_sv) is shared by every call on the
@@ -364,7 +367,7 @@ void fill_common(towr_gpu_handle h, KParams& P, int B, const double* X, int64_t 
   P.rb = L.rb;
   P.misc_tiles = h->d_misc; P.misc_lds = h->d_misc_lds;
   P.lds_scr_off = L.dyn_scr_off;
-  P.lds_rv_off = L.dyn_rv_off;
+  P.rvc = h->d_rvc; P.rvi = h->d_rvi; P.n_rvi = (int32_t)L.rv_inst.size();
   const GaitTables gt = gait_tables(L);
   P.gtab = h->d_gtab;
   P.idir = h->d_idir;
@@ -379,10 +382,31 @@ void fill_common(towr_gpu_handle h, KParams& P, int B, const double* X, int64_t 
   P.gs_segs = h->d_gs_segs; P.gs_tseg = h->d_gs_tseg; P.gs_vmap = h->d_gs_vmap; P.gs_ws = h->d_gs_ws; P.gs_blob = h->d_gs_blob;
 }
 
+// Fixed gait, RotVec: the pre-pass of the Dynamic base-angular coefficients (tiles.hip towr_rv_coef_kernel)
+// into the handle's scratch, on the stream of the Dynamic launch that follows it (every launch holding the
+// Dynamic class: its tile kernel, a fusion group, the single-problem group). Only with the Jacobian.
+int launch_rv_prepass(towr_gpu_handle h, int B, const double* X, int64_t ldx, int want_jac, hipStream_t s) {
+  const Layout& L = h->L;
+  const int64_t K = (int64_t)L.rv_inst.size();
+  if (K == 0 || !want_jac || B <= 0) return TOWR_OK;
+  if (int rc = scratch_grow(h, &h->d_rvc, &h->rvc_cap, B, kRvCoef * K)) return rc;
+  KParams P{};
+  P.X = X; P.ldx = ldx; P.B = B;
+  P.nodecol = h->d_nodecol; P.spl = h->d_spl; P.dur = h->d_dur; P.sg = h->sg; P.terrains = h->d_terrain;
+  P.rb = L.rb; P.rvc = h->d_rvc; P.rvi = h->d_rvi; P.n_rvi = (int32_t)K;
+  const int64_t waves = 3 * (((int64_t)B * K + 63) / 64), grid = (waves + kRvCoefBlock / 64 - 1) / (kRvCoefBlock / 64);
+  if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
+  void* args[] = {&P};
+  HIPCHK(h, hipLaunchKernel(rv_coef_kernel(), dim3((unsigned)grid), dim3(kRvCoefBlock), args, 0, s));
+  return TOWR_OK;
+}
+
 int launch_fused(towr_gpu_handle h, const towr_gpu_handle_s::FuseGroup& fg, int B, const double* X, int64_t ldx, double* G,
                  int64_t ldg, double* V, int64_t ldv, int want_g, int want_jac, hipStream_t s,
                  const towr_terrain_t* terrains, int per_problem) {
   const Layout& L = h->L;
+  if ((fg.mask >> LC_DYN) & 1)
+    if (int rc = launch_rv_prepass(h, B, X, ldx, want_jac, s)) return rc;
   KParams P{};
   fill_common(h, P, B, X, ldx, G, ldg, V, ldv, want_g, want_jac, terrains, per_problem);
   P.units = fg.d_units; P.n_units = fg.n_units;
@@ -509,9 +533,14 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
                               compose_lds(L, C.nt[0] > 0, C.nt[1] > 0, C.nt[2] > 0, C.nt[3] > 0, C.nt[4] > 0), s));
     return TOWR_OK;
   };
+#ifdef TOWR_EXP_FSFOLD
+  const int fpart = fs && !P.want_jac ? kRecFdisc : 0;   // with the Jacobian the FDISC compose blocks form their records
+#else
+  const int fpart = fs ? kRecFdisc : 0;
+#endif
   if (big) {   // (without a side stream the two chains run one after the other on the caller's stream)
     if (fs || tq) {
-      if (int rc = records({fs ? kRecFdisc : 0, tq ? kRecTq : 0}, st)) return rc;
+      if (int rc = records({fpart, tq ? kRecTq : 0}, st)) return rc;
       if (int rc = compose(fs, tq, false, false, false, st)) return rc;
     }
     if (gr || gd) {
@@ -525,7 +554,7 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
     }
   } else {   // every record part in one launch (RangeOfMotion and Dynamic in two blocks beside FDISC: shorter chains per CU)
     const bool two = gr && gd && (fs || tq);
-    if (int rc = records({fs ? kRecFdisc : 0, tq ? kRecTq : 0, two ? kRecGsDyn : (gr || gd) ? kRecGs : 0, two ? kRecGsRom : 0}, st)) return rc;
+    if (int rc = records({fpart, tq ? kRecTq : 0, two ? kRecGsDyn : (gr || gd) ? kRecGs : 0, two ? kRecGsRom : 0}, st)) return rc;
     if (int rc = compose(fs, tq, gr, gd, misc, st)) return rc;
   }
   *forked = split;   // the caller's other launches follow on the side stream, then it joins
@@ -533,7 +562,7 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
   return TOWR_OK;
 }
 
-bool uses_scratch(const Layout& L) { return L.fstream || L.gstream[GS_ROM] || L.gstream[GS_DYN] || L.gstream[GS_TQ]; }
+bool uses_scratch(const Layout& L) { return L.fstream || L.gstream[GS_ROM] || L.gstream[GS_DYN] || L.gstream[GS_TQ] || !L.rv_inst.empty(); }
 
 int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, int64_t ldg, double* V, int64_t ldv,
                    int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem, int only_class);
@@ -610,6 +639,10 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
     const int64_t total = (int64_t)B * nt;
     const int64_t grid = ((total + 7) / 8) * 8;
     if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
+    if (lc == LC_DYN) {
+      if (int rc = launch_rv_prepass(h, B, X, ldx, want_jac, st)) return rc;
+      P.rvc = h->d_rvc;   // (grown by the pre-pass)
+    }
     const int block = class_block(L, lc);
     void* args[] = {&P};
     HIPCHK(h, hipLaunchKernel(kernel_for_class(lc, L.gait, L.rotvec), dim3((unsigned)grid), dim3((unsigned)block), args,
@@ -828,11 +861,15 @@ int host_eval(towr_gpu_handle h, int B, const double* X, double* G, double* V, b
     double* gd = G ? device_view(h, G, gp) : nullptr;
     double* vd = V ? device_view(h, V, vp) : nullptr;
     h->sync_call = true;   // (the scratch event: this call ends with a synchronisation below)
+    const bool scr = uses_scratch(L);
+    if (scr && h->single.n_units > 0)
+      if (int rc = scratch_acquire(h, h->stream)) { h->sync_call = false; return rc; }
     const int rc = h->single.n_units > 0
                        ? launch_fused(h, h->single, 1, xd, L.n, gd ? gd : h->hd_g, L.m, vd ? vd : h->hd_v, L.nnz, G != nullptr,
                                       V != nullptr, h->stream, ter, per)
                        : launch(h, 1, xd, L.n, gd ? gd : h->hd_g, L.m, vd ? vd : h->hd_v, L.nnz, G != nullptr, V != nullptr, h->stream,
                                 ter, per, -1);
+    if (scr && h->single.n_units > 0) (void)scratch_release(h, h->stream);
     h->sync_call = false;
     if (rc) {
       (void)hipStreamSynchronize(h->stream);   // whatever was launched has finished before the scratch is reused
@@ -1035,7 +1072,7 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
       (r = upload(h, &h->d_gs_blk[GS_ROM], L.gs_blocks[GS_ROM])) || (r = upload(h, &h->d_gs_blk[GS_DYN], L.gs_blocks[GS_DYN])) ||
       (r = upload(h, &h->d_gs_blk[GS_TQ], L.gs_blocks[GS_TQ])) || (r = upload(h, &h->d_gs_inst[GS_TQ], L.gs_inst[GS_TQ])) ||
       (r = upload(h, &h->d_gs_inst[GS_ROM], L.gs_inst[GS_ROM])) || (r = upload(h, &h->d_gs_inst[GS_DYN], L.gs_inst[GS_DYN])) ||
-      (r = upload(h, &h->d_gs_segs, L.gs_segs)) || (r = upload(h, &h->d_gs_tseg, L.gs_tseg)) || (r = upload(h, &h->d_gs_vmap, L.gs_vmap)) ||
+      (r = upload(h, &h->d_rvi, L.rv_inst)) || (r = upload(h, &h->d_gs_segs, L.gs_segs)) || (r = upload(h, &h->d_gs_tseg, L.gs_tseg)) || (r = upload(h, &h->d_gs_vmap, L.gs_vmap)) ||
       (r = upload(h, &h->d_gs_ws, L.gs_ws)) || (r = upload(h, &h->d_gs_blob, L.gs_blob)))
     return bail(r);
   if (hipEventCreateWithFlags(&h->scr_ev, hipEventDisableTiming) != hipSuccess) { h->err = "hipEventCreate failed"; return bail(TOWR_ERR_HIP); }
@@ -1154,7 +1191,7 @@ int towr_gpu_destroy(towr_gpu_handle h) {
                  h->d_traj_pd, h->d_traj_n, h->d_traj_c0, h->d_traj_t, h->d_fsb, h->d_fs_t, h->d_fs_tmpl, h->d_fs_ws,
                  h->d_fs_iee, h->d_fs_irow, h->d_fs_iblk, h->d_fsrec, h->d_lin, h->d_soft_b, h->d_soft_rp, h->d_soft_col, h->d_sg, h->d_sv,
                  h->single.d_units, h->d_gs_geo, h->d_gs_tmpl, h->d_gs_pcode, h->d_gs_blk[0], h->d_gs_blk[1], h->d_gs_blk[2],
-                 h->d_gs_inst[0], h->d_gs_inst[1], h->d_gs_inst[2], h->d_gsrec, h->d_gs_segs, h->d_gs_tseg, h->d_gs_vmap, h->d_gs_ws, h->d_gs_blob};
+                 h->d_gs_inst[0], h->d_gs_inst[1], h->d_gs_inst[2], h->d_gsrec, h->d_rvc, h->d_rvi, h->d_gs_segs, h->d_gs_tseg, h->d_gs_vmap, h->d_gs_ws, h->d_gs_blob};
   if (h->device >= 0) for (void* p : dev) if (p) (void)hipFree(p);
   void* host[] = {h->h_x, h->h_g, h->h_v};
   for (void* p : host) if (p) (void)hipHostFree(p);
