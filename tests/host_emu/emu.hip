@@ -141,6 +141,26 @@ extern "C" int emu_cost(const towr_problem_desc_t* d, const double* x, double* f
   return 0;
 }
 
+// The composers' encoding bounds over every streamed block (layout.h kFloatDivMax, GsSeg int16 positions):
+// out[0..2] per GsClass: streamed (0/1); out[3..5]: its largest positions per instant (Lsum, GsGeo::Li);
+// out[6]: the largest CSR range of any FsBlock or GsBlock; out[7]: FDISC streamed
+extern "C" int emu_stream_limits(const towr_problem_desc_t* d, int64_t* out) {
+  Layout L; std::string e;
+  if (build_layout(*d, L, e)) return -1;
+  int64_t nv = 0;
+  for (int c = 0; c < GS_COUNT; ++c) {
+    out[c] = L.gstream[c];
+    int64_t li = 0;
+    for (const GsGeo& g : L.gs_geo) if (g.cls == c) li = std::max<int64_t>(li, g.Li);
+    out[3 + c] = li;
+    for (const GsBlock& bl : L.gs_blocks[c]) nv = std::max<int64_t>(nv, bl.nv);
+  }
+  for (const FsBlock& fb : L.fs_blocks) nv = std::max<int64_t>(nv, fb.nv);
+  out[6] = nv;
+  out[7] = L.fstream;
+  return 0;
+}
+
 // layout statistics per item type (tiles, lanes used, candidates per wave, values per tile)
 extern "C" int emu_stats(const towr_problem_desc_t* d) {
   Layout L; std::string e;

@@ -50,3 +50,46 @@ def test_tile_path_switch():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = subprocess.check_output([sys.executable, "-c", code], env=env, cwd=root, text=True)
     assert out.split() == ["0", "0"]
+
+
+def _limits(desc):
+    import ctypes as C
+    import numpy as np
+    lib = C.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "host_emu", "build", "libemu.so"))
+    out = np.zeros(8, dtype=np.int64)
+    assert lib.emu_stream_limits(C.byref(desc), out.ctypes.data_as(C.POINTER(C.c_int64))) == 0
+    return out
+
+
+K_FLOAT_DIV_MAX = 1 << 21   # layout.h kFloatDivMax: the composers' float row division is exact below it
+INT16_MAX = 32767           # GsSeg positions within an instant are int16
+
+
+@pytest.mark.parametrize("name", GAIT)
+def test_stream_blocks_within_encoding_bounds(name):
+    """Every streamed block of the gait configurations stays inside the composers' proven ranges."""
+    lim = _limits(CONFIGS[name])
+    assert lim[6] < K_FLOAT_DIV_MAX
+    for c in range(3):
+        if lim[c]:
+            assert lim[3 + c] <= INT16_MAX
+
+
+def test_long_horizon_falls_back_past_the_encodings():
+    """A long-horizon gait formulation (ANYmal, 47 phases per foot, 12 polynomials per phase): Dynamic's rows
+    hold more positions per instant than GsSeg's int16 encodes, so Dynamic keeps the tile path (no silent
+    wrap), while RangeOfMotion and FDISC still stream, inside their bounds."""
+    from towr2025_amd import formulation as F
+    f = F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.StairsID), optimize_timings=True)
+    for ee in range(4):
+        f.params_.ee_phase_durations_[ee] = [0.2] * 47
+        f.params_.ee_in_contact_at_start_[ee] = True
+    P = f.params_
+    P.force_polynomials_per_stance_phase_ = P.torque_polynomials_per_stance_phase_ = P.ee_polynomials_per_swing_phase_ = 12
+    d = f.to_desc()
+    lim = _limits(d)
+    assert lim[1] == 0, "Dynamic past the int16 positions must keep the tile path"
+    assert lim[0] == 1 and lim[7] == 1
+    assert lim[3] <= INT16_MAX and lim[6] < K_FLOAT_DIV_MAX
+    p = TowrGpuProblem(d, device=-1)
+    assert [p.kernel_path(k) for k in (DYN, ROM, FDISC)] == [0, 1, 1]
