@@ -394,17 +394,6 @@ __device__ __forceinline__ void fdisc_compose(const KParams& P, const double* re
   double* rowv = cd + ((n * kFsCS + 1) & ~1);
   int32_t* wsr = reinterpret_cast<int32_t*>(rowv + nr * kFsWin);
   auto ci = [&](int k, int f) -> int { return *reinterpret_cast<const int32_t*>(cd + k * kFsCS + kFsND + f); };   // ws, wd, cur
-#ifdef TOWR_EXP_FSFOLD
-  // the block forms its instants' records itself (fdisc_record) from its problem's x staged here; the
-  // PhaseSpline tables and the node table are read from global memory (L2)
-  double* xs = rowv + nr * kFsWin + ((((nr + 1) / 2) + 1) & ~1);
-  Ctx c{};
-  c.seg = nullptr; c.sg = P.sg; c.row = -1;
-  c.x = xs; c.nodecol = P.nodecol; c.dur = P.dur;
-  c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
-  c.gait = true; c.rotvec = false; c.eelin = P.eelin; c.lin = P.lin; c.dyn_scratch = nullptr;
-  c.spl = P.spl; c.sched = P.sched; c.pinfo = P.pinfo; c.pact = P.pact; c.pcols = P.pcols;
-#endif
   // the chunk: element e = f * n + kk -> LDS kk * kFsCS + f
   const int nch = n * kFsRS;
   const int64_t chunk0 = (int64_t)kFsRS * fb.t0;
@@ -452,23 +441,13 @@ __device__ __forceinline__ void fdisc_compose(const KParams& P, const double* re
     return entry(r, e - r * Lr);
   };
   int b = g0;
-#ifndef TOWR_EXP_FSFOLD
+  // (the compose block forming its instants' records itself from x and the PhaseSpline tables in global
+  // memory, instead of reading them: FDISC 0.42 -> 2.7 ms per 1024 problems, the dependent table loads)
   fetch(b);
-#endif
   for (;;) {
-#ifdef TOWR_EXP_FSFOLD
-    (void)rec; (void)ldr;
-    stage_x<BLOCK, false>(P, P.X + (int64_t)b * P.ldx, xs, nullptr);
-    __syncthreads();
-    if (tid < n) {
-      c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
-      fdisc_record(P, c, fb.t0 + tid, P.G + (int64_t)b * P.ldg, [&](int f, double v) { cd[tid * kFsCS + f] = v; });
-    }
-#else
 #pragma unroll
     for (int q = 0; q < kFsPre; ++q)
       if (dst[q] >= 0) cd[dst[q]] = pre[q];
-#endif
     __syncthreads();
     for (int t = tid; t < nr * kFsWin; t += BLOCK) {   // window value q of row r: b[i][e(q)] * basis sum (emit_dim)
       const int r = t / kFsWin, q = t - r * kFsWin;
@@ -480,9 +459,7 @@ __device__ __forceinline__ void fdisc_compose(const KParams& P, const double* re
     for (int t = tid; t < nr; t += BLOCK) wsr[t] = ci(t / 5, 0);
     __syncthreads();
     const int bn = b + ng;
-#ifndef TOWR_EXP_FSFOLD
     if (bn < P.B) fetch(bn);   // in flight while this problem streams
-#endif
     {
       double* out = P.V + (int64_t)b * P.ldv + fb.v0;
       const int nv = fb.nv;
@@ -704,11 +681,7 @@ const void* gait_compose_kernel(int mask) {
   }
 }
 size_t fs_compose_lds(const Layout& L) {   // records, row window values, row window starts
-#ifdef TOWR_EXP_FSFOLD
-  return sizeof(double) * ((size_t)((kFsInst * kFsCS + 1) & ~1) + 5 * kFsInst * kFsWin + ((((5 * kFsInst + 1) / 2) + 1) & ~1) + ((L.n + 2) & ~1));
-#else
   return sizeof(double) * ((size_t)(((kFsInst * kFsCS + 1) & ~1) + 5 * kFsInst * kFsWin + (5 * kFsInst + 1) / 2 + 1) & ~(size_t)1);
-#endif
 }
 size_t gs_dyn_state_bytes(bool rotvec) { return rotvec ? dyn_state_bytes<true>() : dyn_state_bytes<false>(); }
 

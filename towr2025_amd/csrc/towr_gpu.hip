@@ -496,15 +496,17 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
     R.nparts = 0; R.parts = 0;
     int roles = 0;
     int64_t lanes = 64;
+    bool dyn = false;   // a part with Dynamic lanes: the converter states and sums in LDS (gs_rec_lds)
     for (int p : parts) {
       if (p == 0) continue;
       R.parts |= p << (4 * R.nparts++);
       roles |= p == kRecFdisc || p == kRecTq ? 1 : 2;
+      dyn = dyn || ((p == kRecGs || p == kRecGsDyn) && R.g.K[GS_DYN] > 0);
       lanes = std::max<int64_t>(lanes, p == kRecFdisc ? R.ni : p == kRecTq ? R.g.K[GS_TQ] : gs_rec_threads(L, R.g.K[GS_DYN], R.g.K[GS_ROM]));
     }
     if (R.nparts == 0) return TOWR_OK;
     const int threads = (int)std::min<int64_t>(kGsRecMaxBlock, (lanes + 63) & ~63);
-    const size_t lds = (roles & 2) ? gs_rec_lds(L) : fs_inst_lds_bytes(L);
+    const size_t lds = dyn ? gs_rec_lds(L) : fs_inst_lds_bytes(L);
     void* aa[] = {&P, &R};
     HIPCHK(h, hipLaunchKernel(gait_rec_kernel(L.rotvec, roles), dim3((unsigned)(B * R.nparts)), dim3((unsigned)threads), aa, lds, s));
     return TOWR_OK;
@@ -533,22 +535,16 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
                               compose_lds(L, C.nt[0] > 0, C.nt[1] > 0, C.nt[2] > 0, C.nt[3] > 0, C.nt[4] > 0), s));
     return TOWR_OK;
   };
-#ifdef TOWR_EXP_FSFOLD
-  const int fpart = fs && !P.want_jac ? kRecFdisc : 0;   // with the Jacobian the FDISC compose blocks form their records
-#else
   const int fpart = fs ? kRecFdisc : 0;
-#endif
   if (big) {   // (without a side stream the two chains run one after the other on the caller's stream)
     if (fs || tq) {
       if (int rc = records({fpart, tq ? kRecTq : 0}, st)) return rc;
       if (int rc = compose(fs, tq, false, false, false, st)) return rc;
     }
     if (gr || gd) {
-#ifdef TOWR_EXP_RECSPLIT
-      if (int rc = records({gd ? kRecGsDyn : 0, gr ? kRecGsRom : 0}, gst)) return rc;
-#else
+      // one block per problem: two blocks (Dynamic | RangeOfMotion lanes) in one launch or in two launches
+      // measured slower (ANYmal gait, B = 1024, one box: 0.676 / 0.675 vs 0.645 / 0.660 ms per step)
       if (int rc = records({kRecGs}, gst)) return rc;
-#endif
       if (int rc = compose(false, false, false, gd, false, gst)) return rc;
       if (int rc = compose(false, false, gr, false, false, gst)) return rc;
     }
