@@ -105,7 +105,7 @@ extern "C" int emu_eval_ex(const towr_problem_desc_t* d, int n_data, const towr_
         const int ws = sg.type == 1 ? L.gs_ws[sg.wsoff + TqCls::poly(ci, sg.kind, sg.ee)] : 0;
         const int q = rr - (sg.p0 + ws);
         v[bl.v0 + e] = q >= 0 && q < sg.W && rr < sg.p0 + sg.len
-                           ? TqCls::value(GsTabs{L.rb.m, L.spl.data(), L.pcols.data()}, L.gs_tmpl.data(), sg, rr, d, ci, nullptr, L.sched[gg.ee].n_phases) : 0.0;
+                           ? TqCls::value(L.rb, L.gs_tmpl.data(), sg, rr, d, ci, nullptr, L.sched[gg.ee].n_phases) : 0.0;
       }
     }
   }

@@ -12,24 +12,23 @@ namespace tg {
 // an int field of a record: its 64-bit integer bit pattern (the composer reads the low dword in place)
 TG_HD double gs_int(int v) { return __builtin_bit_cast(double, (long long)v); }
 
-// The first active PhaseCol of each dimension of one PhaseSpline's polynomial (Ctx::pact), qa[e] (1 << 24:
-// none); the composer forms a window entry's basis sum from it (gs_sum)
-TG_HD void gs_qa(const Ctx& c, int s, int poly, int qa[3]) {
+// The active-window basis sums of one PhaseSpline at one instant, from the block's PhaseSpline tables
+// (Ctx: SplineMeta, pact, PhaseCol in LDS): sums[e][q] = emit_dim's basis sum of the dimension's PhaseCol
+// qa[e] + q (phase_basis_sum), qa[e] = the polynomial's first active PhaseCol (1 << 24: none)
+TG_HD void gs_window(const Ctx& c, int s, int poly, const double H[4], double sums[3][kGsAct], int qa[3]) {
   const SplineMeta& m = c.spl[s];
+  double h0 = H[0], h1 = H[1], h2 = H[2], h3 = H[3];
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(h0), "+v"(h1), "+v"(h2), "+v"(h3));   // opaque: no runtime-indexed H (scratch)
+#endif
 #pragma unroll
   for (int e = 0; e < 3; ++e) {
     const int32_t* w = c.pact + m.pact_off + 2 * (e * m.n_polys + poly);
-    qa[e] = w[1] >= w[0] ? w[0] : (1 << 24);
+    const int a = w[0], z = w[1];
+    qa[e] = z >= a ? a : (1 << 24);
+#pragma unroll
+    for (int q = 0; q < kGsAct; ++q) sums[e][q] = a + q <= z ? phase_basis_sum(c.pcols[m.pcol_off[e] + a + q], poly, h0, h1, h2, h3) : 0.0;
   }
-}
-// The batch-shared tables a composer's value phase reads (global memory: L2-resident on the device)
-struct GsTabs { double m; const SplineMeta* spl; const PhaseCol* pcols; };
-// A window entry of spline s: dimension e, PhaseCol q (within the dimension's list, the template's code), the
-// active polynomial poly with position basis H, qa = its first active PhaseCol: emit_dim's basis sum
-// (phase_basis_sum, 0 outside the active polynomial's kGsAct-wide window)
-TG_HD double gs_sum(const GsTabs& T, int s, int e, int q, int qa, int poly, const double* H) {
-  if ((unsigned)(q - qa) >= (unsigned)kGsAct) return 0.0;
-  return phase_basis_sum(T.pcols[T.spl[s].pcol_off[e] + q], poly, H[0], H[1], H[2], H[3]);
 }
 
 // SchedJac's sched_val from a record in LDS (dx, v) with the instant's phase and the ee's phase count
@@ -45,7 +44,7 @@ TG_HD double gs_sched_val(const double* dx, const double* v, int cur, int n, int
 //   value(): value q of a segment at the instant (the tile path's expression for that entry).
 struct RomCls {
   TG_HD static int poly(const int32_t* ci, int, int) { return ci[8]; }
-  TG_HD static double value(const GsTabs& T, const int32_t* tmpl, const GsSeg& sg, int pos, const double* d, const int32_t* ci,
+  TG_HD static double value(const RobotC& rb, const int32_t* tmpl, const GsSeg& sg, int pos, const double* d, const int32_t* ci,
                                  const uint8_t* pcl, int nph) {
     const int r = sg.r;
     if (sg.type == 0) {   // base prefix (eval_rom groups 0 and 1)
@@ -61,21 +60,21 @@ struct RomCls {
              d[6 + r] * gs_sched_val(d + 26, d + 29, cur, nph, 2, col);
     }
     const int e = (t >> 22) & 3, q = t & 0x3FFFFF;   // motion PhaseCol: R[e][r] * basis sum (emit_dim)
-    if ((unsigned)(q - ci[2 + 2 * e]) >= (unsigned)kGsAct) return 0.0;   // outside the window: a structural 0
-    return d[3 * e + r] * gs_sum(T, sp_motion(sg.ee), e, q, ci[2 + 2 * e], ci[8], d + 32);
+    const unsigned rel = (unsigned)(q - ci[2 + 2 * e]);
+    return rel < (unsigned)kGsAct ? d[3 * e + r] * d[32 + e * kGsAct + rel] : 0.0;
   }
 };
 
 struct DynCls {
   TG_HD static int poly(const int32_t* ci, int kind, int ee) { return ci[2 * (ee * kDynEeNI + 11 + kind)]; }
-  TG_HD static double value(const GsTabs& T, const int32_t* tmpl, const GsSeg& sg, int pos, const double* d, const int32_t* ci,
+  TG_HD static double value(const RobotC& rb, const int32_t* tmpl, const GsSeg& sg, int pos, const double* d, const int32_t* ci,
                                  const uint8_t* pcl, const int32_t* nph) {
     const int r = sg.r;
     if (sg.type == 0) {   // base prefix
       const int code = pcl[sg.toff + pos];
       const int e = (code >> 2) & 3, bb = code & 3;
       if ((code >> 4) == 0)   // base-linear: -Cross(sum f)[r][e] Hp (dyn_g0_b), m Ha (dyn_g0_a)
-        return r < 3 ? -cross_el(d, r, e) * d[6 + bb] : T.m * d[10 + bb];
+        return r < 3 ? -cross_el(d, r, e) * d[6 + bb] : rb.m * d[10 + bb];
       // base-angular: Ap[r] Hp + Av[r] Hv + Aa[r] Ha of axis e (eval_dyn group 1)
       return d[14 + 9 * e + r] * d[41 + bb] + d[14 + 9 * e + 3 + r] * d[45 + bb] + d[14 + 9 * e + 6 + r] * d[49 + bb];
     }
@@ -94,9 +93,9 @@ struct DynCls {
       return a + bq;
     }
     const int kind = sg.kind, e = (t >> 22) & 3, q = t & 0x3FFFFF;
-    const int qa = ii[2 * (2 + 3 * kind + e)];
-    if ((unsigned)(q - qa) >= (unsigned)kGsAct) return 0.0;
-    const double v = gs_sum(T, kind == 0 ? sp_motion(ee) : kind == 1 ? sp_force(ee) : sp_torque(ee), e, q, qa, ii[2 * (11 + kind)], de + 18 + 4 * kind);
+    const unsigned rel = (unsigned)(q - ii[2 * (2 + 3 * kind + e)]);
+    if (rel >= (unsigned)kGsAct) return 0.0;
+    const double v = de[18 + (kind * 3 + e) * kGsAct + rel];
     // emit_dim scales: motion Cross(f)[r][e]; force Cross(rv)[r][e] (angular) or -1 (linear); torque -1
     const double sc = kind == 0 ? cross_el(de, r, e) : kind == 1 ? (r < 3 ? cross_el(de + 3, r, e) : -1.0) : -1.0;
     return sc * v;
@@ -108,8 +107,9 @@ struct DynCls {
 struct TqCls {
   TG_HD static int poly(const int32_t* ci, int kind, int) { return ci[2 * (kind == 2 ? 7 : 8)]; }
   TG_HD static double tb(const double* d, int r, int e) { return r == 3 ? -d[6 + e] : d[3 * r + e]; }
-  TG_HD static double value(const GsTabs& T, const int32_t* tmpl, const GsSeg& sg, int pos, const double* d, const int32_t* ci,
+  TG_HD static double value(const RobotC& rb, const int32_t* tmpl, const GsSeg& sg, int pos, const double* d, const int32_t* ci,
                                  const uint8_t*, int nph) {
+    (void)rb;
     const int r = sg.r;
     const int32_t t = tmpl[sg.toff + pos];
     if (sg.type == 2) {   // d / d schedule (torque_constraint_discretized.cc:210-234)
@@ -122,9 +122,9 @@ struct TqCls {
       return v;
     }
     const int kind = sg.kind, e = (t >> 22) & 3, q = t & 0x3FFFFF;   // torque (kind 2) or force (1) PhaseCol
-    const int qa = ci[2 * (kind == 2 ? 1 + e : 4 + e)];
-    if ((unsigned)(q - qa) >= (unsigned)kGsAct) return 0.0;
-    const double sum = gs_sum(T, kind == 2 ? sp_torque(sg.ee) : sp_force(sg.ee), e, q, qa, ci[2 * (kind == 2 ? 7 : 8)], d + (kind == 2 ? 24 : 28));
+    const unsigned rel = (unsigned)(q - ci[2 * (kind == 2 ? 1 + e : 4 + e)]);
+    if (rel >= (unsigned)kGsAct) return 0.0;
+    const double sum = d[(kind == 2 ? 24 : 36) + e * kGsAct + rel];
     return (kind == 2 ? tb(d, r, e) : d[9 + e]) * sum;   // emit_dim: scale * basis sum
   }
 };
@@ -157,20 +157,24 @@ TG_HD void tq_record(const Ctx& c, const GsInst& gi, Put&& put, double g[4]) {
 #pragma unroll
   for (int e = 0; e < 3; ++e) { put(12 + e, Jt.dx[e]); put(15 + e, Jt.v[e]); put(18 + e, Jf.dx[e]); put(21 + e, Jf.v[e]); }
   put(kTqND, gs_int(Jt.cur));
-  double H[4];
+  double H[4], sums[3][kGsAct];
   int qa[3];
   spline_basis(Tq, kPos, H);   // AccumulateLinearFormJacobian of the torque spline (:147-155)
-  gs_qa(c, sp_torque(ee), Tq.poly, qa);
+  gs_window(c, sp_torque(ee), Tq.poly, H, sums, qa);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) put(24 + q, H[q]);
+  for (int e = 0; e < 3; ++e) {
+    put(kTqND + 1 + e, gs_int(qa[e]));
 #pragma unroll
-  for (int e = 0; e < 3; ++e) put(kTqND + 1 + e, gs_int(qa[e]));
+    for (int q = 0; q < kGsAct; ++q) put(24 + e * kGsAct + q, sums[e][q]);
+  }
   spline_basis(F, kPos, H);    // ... of the force spline into the normal-torque rows (:158-163)
-  gs_qa(c, sp_force(ee), F.poly, qa);
+  gs_window(c, sp_force(ee), F.poly, H, sums, qa);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) put(28 + q, H[q]);
+  for (int e = 0; e < 3; ++e) {
+    put(kTqND + 4 + e, gs_int(qa[e]));
 #pragma unroll
-  for (int e = 0; e < 3; ++e) put(kTqND + 4 + e, gs_int(qa[e]));
+    for (int q = 0; q < kGsAct; ++q) put(36 + e * kGsAct + q, sums[e][q]);
+  }
   put(kTqND + 7, gs_int(Tq.poly));
   put(kTqND + 8, gs_int(F.poly));
 }

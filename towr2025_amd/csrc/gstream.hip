@@ -31,11 +31,12 @@ namespace {
 // ------------------------------------------------------------------------------------------------
 // ForceConstraintDiscretized records (layout.h FsBlock, kFsRS). Every Jacobian row of the class is the
 // force set's full PhaseSpline pattern plus the schedule columns, ~90 % exact zeros whose positions move
-// with x. One lane per instant: fdisc_instant's result in the composer's form — the force polynomial's
-// position basis, the terrain basis at the foot, d force / d schedule, the window start, dimension codes and
-// polynomial — goes to the per-problem record array (the composer forms the pyramid rows and the window's
-// basis sums); the instant's g rows go straight out. Records are chunk-major per FsBlock (field f of the
-// block's instant kk at kFsRS t0 + f n + kk), so a compose block's prologue is one contiguous copy.
+// with x. One lane per instant: fdisc_instant's result in the composer's form — the basis sums of the
+// kFsWin columns the force polynomial can touch (phase_basis_sum over the instant's window of the
+// template), the 5 pyramid rows b, d force / d schedule, the window start and dimension codes — goes to
+// the per-problem record array; the instant's g rows go straight out. Records are chunk-major per
+// FsBlock (field f of the block's instant kk at kFsRS t0 + f n + kk), so a compose block's prologue is
+// one contiguous copy.
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ double fs_int(int v) { return __longlong_as_double((long long)v); }
 // FDISC instant k (fs_t order) of the problem in c: its record fields (layout.h kFsRS) through put(field,
@@ -84,7 +85,7 @@ __device__ __forceinline__ double* gs_field(double* R, int RS, int k, const GsIn
 // without curvature the motion block is skipped (every scale is exactly 0.0,
 // torque_constraint_discretized.cc:57). One lane per instant: eval_tqdisc's quantities in the composer's
 // form — the terrain basis t1, t2, n, the force row scale b = -k mu n, d torque / d schedule and d force /
-// d schedule, the torque and force polynomials' position bases and first active PhaseCols — go to the record; the 4
+// d schedule, the active-window basis sums of the torque and force polynomials — go to the record; the 4
 // g rows go straight out (:101-125).
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ void tq_records(const KParams& P, const RecArgs& A, Ctx c, int b) {
@@ -114,7 +115,7 @@ __device__ __forceinline__ void tq_records(const KParams& P, const RecArgs& A, C
 //                            dyn_rv_state) into LDS; the base-linear and base-angular bases; ab, La, Lp
 //                            to the scratch;
 //   [ee0, ee0 + 3 E Kd)      Dynamic (spline kind, endeffector, instant): the motion / force / torque
-//                            PhaseSpline, its basis and first active PhaseCols, schedule Jacobian; F, Tq, M to the
+//                            PhaseSpline, its active-window sums and schedule Jacobian; F, Tq, M to the
 //                            scratch (one chain per lane: the three splines no longer run in series);
 //   [r0, r0 + Kr)            RangeOfMotion instant (range_of_motion_constraint.cc:72-131, eval_rom); its
 //                            3 g rows go straight out;
@@ -192,16 +193,18 @@ __device__ __forceinline__ void gs_records(const KParams& P, const GsRecArgs& A,
       for (int e = 0; e < 3; ++e) sk[e] = Sp.p[e];
       const int fd = kDynBaseND + kDynEeND * ee, fi = NDd + kDynEeNI * ee;
       auto put = [&](int f, double v) { *gs_field(Rd, RSd, k, gi, f) = v; };
-      {   // the active polynomial: its position basis and first active PhaseCols (the composer forms the sums)
-        double H[4];
+      {   // the active window's basis sums
+        double H[4], sums[3][kGsAct];
         int qa[3];
         spline_basis(Sp, kPos, H);
-        gs_qa(c, sp, Sp.poly, qa);
+        gs_window(c, sp, Sp.poly, H, sums, qa);
         put(fi + 11 + kind, gs_int(Sp.poly));
 #pragma unroll
-        for (int q = 0; q < 4; ++q) put(fd + 18 + 4 * kind + q, H[q]);
+        for (int e = 0; e < 3; ++e) {
+          put(fi + 2 + 3 * kind + e, gs_int(qa[e]));
 #pragma unroll
-        for (int e = 0; e < 3; ++e) put(fi + 2 + 3 * kind + e, gs_int(qa[e]));
+          for (int q = 0; q < kGsAct; ++q) put(fd + 18 + (3 * kind + e) * kGsAct + q, sums[e][q]);
+        }
       }
       if (kind < 2) {   // force and ee-position schedule terms (dynamic_constraint.cc:116-122; no torque term)
         SchedJac J;
@@ -261,12 +264,15 @@ __device__ __forceinline__ void gs_records(const KParams& P, const GsRecArgs& A,
       for (int bb = 0; bb < 4; ++bb) put(22 + bb, H[bb]);
       spline_basis(M, kPos, H);
       {
+        double sums[3][kGsAct];
         int qa[3];
-        gs_qa(c, sp_motion(gi.ee), M.poly, qa);
+        gs_window(c, sp_motion(gi.ee), M.poly, H, sums, qa);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) put(32 + q, H[q]);
+        for (int e = 0; e < 3; ++e) {
+          put(kRomND + 1 + e, gs_int(qa[e]));
 #pragma unroll
-        for (int e = 0; e < 3; ++e) put(kRomND + 1 + e, gs_int(qa[e]));
+          for (int qq = 0; qq < kGsAct; ++qq) put(32 + e * kGsAct + qq, sums[e][qq]);
+        }
       }
       SchedJac Jx;
       sched_jac(c, sp_motion(gi.ee), t, M, Jx);   // b_R_w * d pos / d schedule (:123-130)
@@ -545,7 +551,6 @@ __device__ __forceinline__ void gs_compose(const KParams& P, const GsBlock* blks
     return q < (unsigned)(p.y >> 16) ? val[(p.y & 0xFFFF) + q] : 0.0;
   };
   const int nv = bl.nv;
-  const GsTabs T{P.rb.m, P.spl, P.pcols};   // the window entries' PhaseCols (batch-shared, L2)
   int b = g0;
   fetch(b);
   for (;;) {
@@ -569,8 +574,8 @@ __device__ __forceinline__ void gs_compose(const KParams& P, const GsBlock* blks
       if (pos < sg.p0 + sg.len) {
         const double* d = cd + kk * CS;
         const int32_t* ci = reinterpret_cast<const int32_t*>(d + ND);
-        if constexpr (CLS == GS_DYN) x = C::value(T, tmpl, sg, pos, d, ci, pcl + kk * g.Psum, nph);
-        else x = C::value(T, tmpl, sg, pos, d, ci, pcl + kk * g.Psum, nph[g.ee]);
+        if constexpr (CLS == GS_DYN) x = C::value(P.rb, tmpl, sg, pos, d, ci, pcl + kk * g.Psum, nph);
+        else x = C::value(P.rb, tmpl, sg, pos, d, ci, pcl + kk * g.Psum, nph[g.ee]);
       }
       val[t] = x;
     }

@@ -111,23 +111,20 @@ struct GsInst { double t; int32_t seg, row0; int16_t ee, kk, nb, reserved; doubl
 // ND doubles then NI ints (stored as doubles) — so that a composer block's prologue is one contiguous
 // copy. The fields of the GsBlock of instants [k0, k0 + n) form one chunk at RS * k0 (class-global
 // instant index), field-major inside it (field f of instant k0 + kk at RS * k0 + f * n + kk).
-//   RangeOfMotion: R[9] | HL[4] | Ag[axis][r] (9) | HA[4] | Jx.dx[3] v[3] | HM[4];
+//   RangeOfMotion: R[9] | HL[4] | Ag[axis][r] (9) | HA[4] | Jx.dx[3] v[3] | sums[dim][4] (12);
 //                  ints cur | qa[dim] (3) | poly
 //   Dynamic:       fs[3] | Lp[3] | HpL[4] | HaL[4] | A[axis][p v a][r] (27) | HpA HvA HaA (12), then per
-//                  endeffector Fp[3] | rv[3] | Jf.dx v[6] | Jx.dx v[6] | H[kind][4] (12);
+//                  endeffector Fp[3] | rv[3] | Jf.dx v[6] | Jx.dx v[6] | sums[kind][dim][4] (36);
 //                  ints per endeffector curF | curX | qa[kind][dim] (9) | poly[kind] (3)
 //   TorqueConstraintDiscretized: t1[3] | t2[3] | n[3] | b[3] (= -k mu n) | Jt.dx v[6] | Jf.dx v[6] |
-//                  HT[4] | HF[4]; ints cur | qaT[3] | qaF[3] | polyT | polyF
-// (H*: the position basis of a PhaseSpline's active polynomial at the instant; qa: the first PhaseCol of each
-// dimension that polynomial touches, layout Ctx::pact. The composer forms a window entry's basis sum itself,
-// phase_basis_sum over the entry's PhaseCol: records 49 -> 41, 325 -> 229 (ANYmal) and 57 -> 41 doubles.)
+//                  torque sums[dim][4] (12) | force sums[dim][4] (12); ints cur | qaT[3] | qaF[3] | polyT | polyF
 //                  (torque_constraint_discretized.cc:139-235 without the motion block: a terrain
 //                  without curvature, where every motion scale is exactly 0.0 and the block is skipped, :57)
 // (kind 0 motion, 1 force, 2 torque; sums / qa: the active-window basis sums of the PhaseSpline, the
 // first active PhaseCol of each dimension and the basis sums of up to kGsAct PhaseCols from it)
-constexpr int kRomND = 36, kRomNI = 5;
-constexpr int kDynBaseND = 53, kDynEeND = 30, kDynEeNI = 14;
-constexpr int kTqND = 32, kTqNI = 9;
+constexpr int kRomND = 44, kRomNI = 5;
+constexpr int kDynBaseND = 53, kDynEeND = 54, kDynEeNI = 14;
+constexpr int kTqND = 48, kTqNI = 9;
 TG_HD constexpr int gs_rec_nd(int cls, int E) { return cls == GS_ROM ? kRomND : cls == GS_TQ ? kTqND : kDynBaseND + kDynEeND * E; }
 TG_HD constexpr int gs_rec_ni(int cls, int E) { return cls == GS_ROM ? kRomNI : cls == GS_TQ ? kTqNI : kDynEeNI * E; }
 TG_HD constexpr int gs_rec_fields(int cls, int E) { return gs_rec_nd(cls, E) + gs_rec_ni(cls, E); }
