@@ -1117,11 +1117,6 @@ TG_HD void pyramid(const double n[3], const double t1[3], const double t2[3], do
     b[3][q] = t2[q] - mu * n[q]; b[4][q] = t2[q] + mu * n[q];
   }
 }
-// element (i, q) of pyramid's rows from nb = (n, t1, t2): the same operation as pyramid's
-TG_HD double pyramid_el(const double nb[9], double mu, int i, int q) {
-  const double n = nb[q];
-  return i == 0 ? n : i == 1 ? nb[3 + q] - mu * n : i == 2 ? nb[3 + q] + mu * n : i == 3 ? nb[6 + q] - mu * n : nb[6 + q] + mu * n;
-}
 TG_HD double dot3(const double a[3], const double b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 
 // ----------------------------------------------------------------------------------------------

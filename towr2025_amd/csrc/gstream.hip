@@ -39,29 +39,38 @@ namespace {
 // one contiguous copy.
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ double fs_int(int v) { return __longlong_as_double((long long)v); }
-// FDISC instant k (fs_t order) of the problem in c: its record fields (layout.h kFsRS) through put(field,
-// value) and its 5 g rows (when wanted) straight to Gb
+// FDISC instant k (fs_t order) of the problem in c: its record fields through put(field, value) and its 5 g
+// rows (when wanted) straight to Gb
 template <class Put>
 __device__ __forceinline__ void fdisc_record(const KParams& P, const Ctx& c, int k, double* Gb, Put&& put) {
   FdiscInstant o;
   fdisc_instant(c, P.fs_iee[k], P.fs_t[k], o);
   const FsBlock fb = P.fsb[P.fs_iblk[k]];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) put(kFsH + q, o.H[q]);
+  for (int i = 0; i < 5; ++i)
 #pragma unroll
-  for (int q = 0; q < 9; ++q) put(kFsNb + q, o.nb[q / 3][q % 3]);
+    for (int e = 0; e < 3; ++e) put(kFsB + 3 * i + e, o.b[i][e]);
 #pragma unroll
   for (int e = 0; e < 3; ++e) { put(kFsDx + e, o.Jf.dx[e]); put(kFsV + e, o.Jf.v[e]); }
+  put(kFsND + 2, fs_int(o.Jf.cur));
   if (P.want_g) {
     const int row = P.fs_irow[k];
 #pragma unroll
     for (int i = 0; i < 5; ++i) __builtin_nontemporal_store(o.g[i], Gb + row + i);
   }
   const int poly = o.poly;
-  put(kFsND, fs_int(P.fs_ws[2 * (fb.wsoff + poly)]));
-  put(kFsND + 1, fs_int(P.fs_ws[2 * (fb.wsoff + poly) + 1]));
-  put(kFsND + 2, fs_int(o.Jf.cur));
-  put(kFsND + 3, fs_int(poly));
+  const int ws = P.fs_ws[2 * (fb.wsoff + poly)], wd = P.fs_ws[2 * (fb.wsoff + poly) + 1];
+  put(kFsND, fs_int(ws));
+  put(kFsND + 1, fs_int(wd));
+  double h0 = o.H[0], h1 = o.H[1], h2 = o.H[2], h3 = o.H[3];
+  asm volatile("" : "+v"(h0), "+v"(h1), "+v"(h2), "+v"(h3));
+  const int32_t* tm = P.fs_tmpl + fb.tmpl;
+#pragma unroll 4
+  for (int q = 0; q < kFsWin; ++q) {   // the window's basis sums (schedule entries: never read, 0)
+    const int pos = ws + q;
+    const int32_t te = pos < fb.L ? tm[pos] : -1;
+    put(q, te >= 0 ? phase_basis_sum(c.pcols[te & 0xFFFFFF], poly, h0, h1, h2, h3) : 0.0);
+  }
 }
 __device__ __forceinline__ void fdisc_records(const KParams& P, const Ctx& c, int b, double* rec, int64_t ldr, int32_t ni) {
   double* Gb = P.G + (int64_t)b * P.ldg;
@@ -384,8 +393,7 @@ __device__ __forceinline__ void fdisc_compose(const KParams& P, const double* re
   double* cd = smem;
   double* rowv = cd + ((n * kFsCS + 1) & ~1);
   int32_t* wsr = reinterpret_cast<int32_t*>(rowv + nr * kFsWin);
-  auto ci = [&](int k, int f) -> int { return *reinterpret_cast<const int32_t*>(cd + k * kFsCS + kFsND + f); };   // ws, wd, cur, poly
-  const int32_t* tmpl = P.fs_tmpl + fb.tmpl;
+  auto ci = [&](int k, int f) -> int { return *reinterpret_cast<const int32_t*>(cd + k * kFsCS + kFsND + f); };   // ws, wd, cur
   // the chunk: element e = f * n + kk -> LDS kk * kFsCS + f
   const int nch = n * kFsRS;
   const int64_t chunk0 = (int64_t)kFsRS * fb.t0;
@@ -441,22 +449,12 @@ __device__ __forceinline__ void fdisc_compose(const KParams& P, const double* re
     for (int q = 0; q < kFsPre; ++q)
       if (dst[q] >= 0) cd[dst[q]] = pre[q];
     __syncthreads();
-    // window value q of row r: b[i][e(q)] * the basis sum of the window's column q (emit_dim; the template and
-    // PhaseCol tables are batch-shared, L2-resident), and the instants' pyramid rows b for the schedule entries
-    const double mu = P.terrains[P.terrain_per_problem ? b : 0].friction_coeff;
-    for (int t = tid; t < nr * kFsWin; t += BLOCK) {
+    for (int t = tid; t < nr * kFsWin; t += BLOCK) {   // window value q of row r: b[i][e(q)] * basis sum (emit_dim)
       const int r = t / kFsWin, q = t - r * kFsWin;
       const int k = r / 5, i = r - 5 * k;
-      const double* d = cd + k * kFsCS;
-      const int pos = ci(k, 0) + q;
-      const int32_t te = pos < Lr ? tmpl[pos] : -1;
-      const double v = te >= 0 ? phase_basis_sum(P.pcols[te & 0xFFFFFF], ci(k, 3), d[kFsH], d[kFsH + 1], d[kFsH + 2], d[kFsH + 3]) : 0.0;
+      const double v = cd[k * kFsCS + q];
       const int ed = (ci(k, 1) >> (2 * q)) & 3;
-      rowv[t] = v == 0.0 ? 0.0 : pyramid_el(d + kFsNb, mu, i, ed) * v;
-    }
-    for (int t = tid; t < 15 * n; t += BLOCK) {
-      const int k = t / 15, j = t - 15 * k;
-      cd[k * kFsCS + kFsB + j] = pyramid_el(cd + k * kFsCS + kFsNb, mu, j / 3, j % 3);
+      rowv[t] = v == 0.0 ? 0.0 : cd[k * kFsCS + kFsB + 3 * i + ed] * v;
     }
     for (int t = tid; t < nr; t += BLOCK) wsr[t] = ci(t / 5, 0);
     __syncthreads();

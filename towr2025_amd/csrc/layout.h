@@ -42,14 +42,10 @@ constexpr int kFsWin = 12;
 // (e / L) 2^-23 < 0.5 / L, i.e. for e < 2^22. The layout keeps every block range below half that bound
 // (build_fstream, build_gstream_class: fewer instants per block, or the tile path).
 constexpr int kFloatDivMax = 1 << 21;
-// FDISC record (gstream.hip fdisc_records -> the composer): H[4] (the force polynomial's position basis) |
-// nb[9] (the terrain basis n, t1, t2 at the foot) | Jf.dx[3] | Jf.v[3] | ints ws, wd, cur, poly (64-bit
-// integer bit patterns). The composer forms the pyramid rows b[5][3] (from nb and the problem's mu) and the
-// window's basis sums (phase_basis_sum over the template) itself: 23 doubles per instant instead of 36.
-constexpr int kFsH = 0, kFsNb = 4, kFsDx = 13, kFsV = 16, kFsND = 19;
-constexpr int kFsRS = kFsND + 4;             // record fields
-constexpr int kFsB = kFsRS;                  // the composer's LDS: b[5][3] after the record fields
-constexpr int kFsCS = (kFsB + 15) | 1;       // LDS stride per instant
+// FDISC record (gstream.hip fdisc_records -> the composer): Hv[kFsWin] | b[5][3] | Jf.dx[3] |
+// Jf.v[3] | ints ws, wd, cur (64-bit integer bit patterns)
+constexpr int kFsB = kFsWin, kFsDx = kFsWin + 15, kFsV = kFsWin + 18, kFsND = kFsWin + 21;
+constexpr int kFsRS = kFsND + 3, kFsCS = kFsRS | 1;   // record fields; LDS stride per instant
 struct FsBlock {
   int32_t ee, n_inst, t0, r0;   // endeffector, instants, first instant's time index (fs_t), first row
   int32_t v0, nv, L, tmpl;      // CSR range [v0, v0 + nv), row length, template offset (fs_tmpl)

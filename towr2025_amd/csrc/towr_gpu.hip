@@ -583,16 +583,6 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
                    int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem, int only_class) {
   const Layout& L = h->L;
   uint32_t fused_mask = 0;
-#ifdef TOWR_EXP_MISCFORK
-  bool misc_side = only_class < 0 && !L.gait && h->n_side > 0 && class_units(L, LC_MISC) > 0 && !uses_scratch(L);
-  for (int g = 0; g < h->n_fuse; ++g) misc_side = misc_side && !((h->fuse[g].mask >> LC_MISC) & 1);
-  if (misc_side) {
-    HIPCHK(h, hipEventRecord(h->fork, s));
-    HIPCHK(h, hipStreamWaitEvent(h->side[0], h->fork, 0));
-  }
-#else
-  const bool misc_side = false;
-#endif
   if (only_class < 0)
     for (int g = 0; g < h->n_fuse; ++g) {
       if (int rc = launch_fused(h, h->fuse[g], B, X, ldx, G, ldg, V, ldv, want_g, want_jac, s, terrains, per_problem)) return rc;
@@ -607,7 +597,7 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
   std::stable_partition(order, order + nk, [](int lc) { return lc != LC_MISC; });   // the small kinds last
   // (the streaming path forks its own side stream, see launch_stream_path; the other classes follow it on
   // the caller's stream)
-  const int nside = (only_class < 0 && nk > 1 && !uses_scratch(L) && !misc_side) ? std::min(h->n_side, nk - 1) : 0;
+  const int nside = (only_class < 0 && nk > 1 && !uses_scratch(L)) ? std::min(h->n_side, nk - 1) : 0;
   if (nside > 0) {
     HIPCHK(h, hipEventRecord(h->fork, s));
     for (int i = 0; i < nside; ++i) HIPCHK(h, hipStreamWaitEvent(h->side[i], h->fork, 0));
@@ -617,8 +607,7 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
     const int lc = order[q];
     if (lc == LC_MISC && misc_done) continue;   // in the streaming path's composer launch
     const int nt = class_units(L, lc);
-    const hipStream_t st = stream_forked || (misc_side && lc == LC_MISC) ? h->side[0]
-                                                                         : (nside > 0 && q % (nside + 1) != 0) ? h->side[q % (nside + 1) - 1] : s;
+    const hipStream_t st = stream_forked ? h->side[0] : (nside > 0 && q % (nside + 1) != 0) ? h->side[q % (nside + 1) - 1] : s;
     KParams P{};
     fill_common(h, P, B, X, ldx, G, ldg, V, ldv, want_g, want_jac, terrains, per_problem);
     P.ntiles = nt;
@@ -655,7 +644,7 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
     HIPCHK(h, hipLaunchKernel(kernel_for_class(lc, L.gait, L.rotvec), dim3((unsigned)grid), dim3((unsigned)block), args,
                               lds_bytes(L, lc), st));
   }
-  for (int i = 0; i < (stream_forked || misc_side ? 1 : nside); ++i) {
+  for (int i = 0; i < (stream_forked ? 1 : nside); ++i) {
     HIPCHK(h, hipEventRecord(h->join[i], h->side[i]));
     HIPCHK(h, hipStreamWaitEvent(s, h->join[i], 0));
   }
@@ -1132,11 +1121,7 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
     // streams gave 0.524, 0.521, 0.550 ms per step — every kind already fills the CUs' LDS, so kinds
     // cannot co-reside. Under phase-duration optimisation (streaming FDISC) two streams: the write-bound
     // FDISC stream kernel runs beside the latency-bound Dynamic tiles.
-#ifdef TOWR_EXP_MISCFORK
-    const int want = ns ? std::atoi(ns) - 1 : 1;
-#else
     const int want = ns ? std::atoi(ns) - 1 : (h->L.gait && (h->L.fstream || h->L.gstream[GS_TQ]) ? 1 : 0);
-#endif
     h->n_side = std::max(0, std::min(towr_gpu_handle_s::kMaxSide, want));
     if (h->n_side > 0 && hipEventCreateWithFlags(&h->fork, hipEventDisableTiming) != hipSuccess) { h->err = "hipEventCreate failed"; return bail(TOWR_ERR_HIP); }
     for (int i = 0; i < h->n_side; ++i)
