@@ -17,7 +17,7 @@ for i in 1 2; do
   done
 done
 for i in 1 2; do
-  for LIB in "" tools/build/libtowr_gpu_miscfork.so tools/build/libtowr_gpu_eulerpre.so tools/build/libtowr_gpu_r03.so; do
+  for LIB in "" tools/build/libtowr_gpu_miscfork.so tools/build/libtowr_gpu_r03.so; do
     timeout -k 10 200 python tools/gait_ab.py --reps 100 --no-gait --batch 4096 ${LIB:+--lib $LIB} >> gpurun_out/${TAG}_ab.log 2>&1 || exit $?
   done
 done

@@ -397,7 +397,7 @@ int launch_rv_prepass(towr_gpu_handle h, int B, const double* X, int64_t ldx, in
   const int64_t waves = 3 * (((int64_t)B * K + 63) / 64), grid = (waves + kRvCoefBlock / 64 - 1) / (kRvCoefBlock / 64);
   if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
   void* args[] = {&P};
-  HIPCHK(h, hipLaunchKernel(rv_coef_kernel(L.rotvec), dim3((unsigned)grid), dim3(kRvCoefBlock), args, 0, s));
+  HIPCHK(h, hipLaunchKernel(rv_coef_kernel(), dim3((unsigned)grid), dim3(kRvCoefBlock), args, 0, s));
   return TOWR_OK;
 }
 
