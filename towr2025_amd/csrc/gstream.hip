@@ -343,8 +343,9 @@ __device__ __forceinline__ void gs_records(const KParams& P, const GsRecArgs& A,
 // Dynamic records (all lanes, or one class's lanes when a small batch spreads them over two blocks), each
 // block staging x and the PhaseSpline tables itself (gait_record_setup). towr_gpu.hip launch_stream_path
 // chooses the parts: at large batch sizes one launch per chain, at small ones (B = 1) every part in one.
-// Instantiated per role set (ROLES bit 0 the FDISC / TQDISC parts, bit 1 the RangeOfMotion / Dynamic parts),
-// so the FDISC-only launch keeps its own registers. With the RangeOfMotion / Dynamic role: 4 waves per SIMD
+// Instantiated per role set (ROLES bit 0 the FDISC part, bit 1 the RangeOfMotion / Dynamic parts, bit 2 the
+// TQDISC part), so a launch carries only its parts' registers: the FDISC records alone 110 VGPRs (4 waves per
+// SIMD), with the TQDISC code 170 (2 waves per SIMD; ANYmal gait, B = 1024: FDISC 0.389 -> 0.419 ms). With the RangeOfMotion / Dynamic role: 4 waves per SIMD
 // (128 VGPRs, a few spilled): at the unconstrained 166 VGPRs a second 5-wave block did not fit a CU (MI355X,
 // ANYmal gait B = 1024: 122 us, 100 us at 4 waves per SIMD)
 template <bool ROTVEC, int ROLES>
@@ -352,10 +353,10 @@ __device__ __forceinline__ void rec_body(const KParams& P, const RecArgs& A, dou
   const int np = A.nparts;
   const int b = (int)blockIdx.x / np, part = (A.parts >> (4 * ((int)blockIdx.x % np))) & 15;
   const Ctx c = gait_record_setup<0>(P, b, smem);
-  if constexpr ((ROLES & 1) != 0) {
+  if constexpr ((ROLES & 1) != 0)
     if (part == kRecFdisc) { fdisc_records(P, c, b, A.frec, A.fldr, A.ni); return; }
+  if constexpr ((ROLES & 4) != 0)
     if (part == kRecTq) { tq_records(P, A, c, b); return; }
-  }
   if constexpr ((ROLES & 2) != 0) gs_records<ROTVEC>(P, A.g, c, b, smem, part == kRecGsDyn ? 1 : part == kRecGsRom ? 2 : 0);
 }
 template <bool ROTVEC, int ROLES>
@@ -363,9 +364,14 @@ __global__ void __launch_bounds__(kGsRecMaxBlock) __attribute__((amdgpu_waves_pe
   extern __shared__ __attribute__((aligned(16))) double smem[];
   rec_body<ROTVEC, ROLES>(P, A, smem);
 }
-__global__ void __launch_bounds__(kGsRecMaxBlock) towr_gait_frec_kernel(KParams P, RecArgs A) {   // FDISC / TQDISC records only
+template <int ROLES>   // FDISC and / or TQDISC records only
+#ifdef TOWR_EXP_TQW2
+__global__ void __launch_bounds__(kGsRecMaxBlock) towr_gait_frec_kernel(KParams P, RecArgs A) {
+#else
+__global__ void __launch_bounds__(kGsRecMaxBlock) __attribute__((amdgpu_waves_per_eu(4))) towr_gait_frec_kernel(KParams P, RecArgs A) {
+#endif
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  rec_body<false, 1>(P, A, smem);
+  rec_body<false, ROLES>(P, A, smem);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -656,10 +662,13 @@ int64_t gs_record_doubles(const Layout& L, int cls) {
   const int64_t K = (int64_t)L.gs_inst[cls].size();
   return ((int64_t)gs_rec_fields(cls, L.rb.n_ee) * K + 1) & ~(int64_t)1;
 }
-const void* gait_rec_kernel(bool rotvec, int roles) {
-  if (roles == 1) return reinterpret_cast<const void*>(&towr_gait_frec_kernel);
+const void* gait_rec_kernel(bool rotvec, int roles) {   // roles: bit 0 FDISC, 1 RangeOfMotion / Dynamic, 2 TQDISC
+  if ((roles & 2) == 0)
+    return roles == 1 ? reinterpret_cast<const void*>(&towr_gait_frec_kernel<1>) : roles == 4 ? reinterpret_cast<const void*>(&towr_gait_frec_kernel<4>)
+                      : reinterpret_cast<const void*>(&towr_gait_frec_kernel<5>);
   if (roles == 2) return rotvec ? reinterpret_cast<const void*>(&towr_gait_rec_kernel<true, 2>) : reinterpret_cast<const void*>(&towr_gait_rec_kernel<false, 2>);
-  return rotvec ? reinterpret_cast<const void*>(&towr_gait_rec_kernel<true, 3>) : reinterpret_cast<const void*>(&towr_gait_rec_kernel<false, 3>);
+  if (roles == 3) return rotvec ? reinterpret_cast<const void*>(&towr_gait_rec_kernel<true, 3>) : reinterpret_cast<const void*>(&towr_gait_rec_kernel<false, 3>);
+  return rotvec ? reinterpret_cast<const void*>(&towr_gait_rec_kernel<true, 7>) : reinterpret_cast<const void*>(&towr_gait_rec_kernel<false, 7>);
 }
 template <int MASK>
 const void* compose_fn() { return reinterpret_cast<const void*>(&towr_gait_compose_kernel<(MASK & 25) ? kComposeBlock : kComposeBlockRD, MASK>); }

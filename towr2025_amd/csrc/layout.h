@@ -299,7 +299,7 @@ inline int64_t fs_record_doubles() { return kFsRS; }   // FDISC record doubles p
 size_t gs_stream_lds(const Layout& L, int cls);
 size_t fs_compose_lds(const Layout& L);   // the ForceConstraintDiscretized compose block (bytes)
 int64_t gs_record_doubles(const Layout& L, int cls);
-const void* gait_rec_kernel(bool rotvec, int roles);   // instantiation: bit 0 the FDISC / TQDISC parts, bit 1 the RangeOfMotion / Dynamic parts
+const void* gait_rec_kernel(bool rotvec, int roles);   // instantiation: bit 0 the FDISC part, 1 the RangeOfMotion / Dynamic parts, 2 the TQDISC part
 const void* gait_compose_kernel(int mask);   // roles: bit 0 FDISC, 1 RangeOfMotion, 2 Dynamic, 3 small kinds, 4 TQDISC
 constexpr int kComposeMasks[] = {1, 2, 4, 6, 7, 15, 16, 17, 23, 31};   // the instantiated role sets
 // the composer launch's arguments: the record arrays (per problem, leading dimensions; the

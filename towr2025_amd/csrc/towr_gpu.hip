@@ -500,7 +500,7 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
     for (int p : parts) {
       if (p == 0) continue;
       R.parts |= p << (4 * R.nparts++);
-      roles |= p == kRecFdisc || p == kRecTq ? 1 : 2;
+      roles |= p == kRecFdisc ? 1 : p == kRecTq ? 4 : 2;
       dyn = dyn || ((p == kRecGs || p == kRecGsDyn) && R.g.K[GS_DYN] > 0);
       lanes = std::max<int64_t>(lanes, p == kRecFdisc ? R.ni : p == kRecTq ? R.g.K[GS_TQ] : gs_rec_threads(L, R.g.K[GS_DYN], R.g.K[GS_ROM]));
     }
@@ -1160,9 +1160,10 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
     if (lds > 160 * 1024) { h->err = "problem too large for the streaming instant kernel's LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
     const size_t need = gs_rec_lds(L);
     if (need > 160 * 1024) { h->err = "problem too large for the record kernel's LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
-    if (need > 64 * 1024 && (hipFuncSetAttribute(gait_rec_kernel(L.rotvec, 1), hipFuncAttributeMaxDynamicSharedMemorySize, (int)need) != hipSuccess ||
-                             hipFuncSetAttribute(gait_rec_kernel(L.rotvec, 2), hipFuncAttributeMaxDynamicSharedMemorySize, (int)need) != hipSuccess ||
-                             hipFuncSetAttribute(gait_rec_kernel(L.rotvec, 3), hipFuncAttributeMaxDynamicSharedMemorySize, (int)need) != hipSuccess)) {
+    bool ok = true;
+    for (int roles = 1; roles < 8 && need > 64 * 1024; ++roles)
+      ok = ok && hipFuncSetAttribute(gait_rec_kernel(L.rotvec, roles), hipFuncAttributeMaxDynamicSharedMemorySize, (int)need) == hipSuccess;
+    if (!ok) {
       h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
     }
   }
