@@ -475,10 +475,16 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
   const bool big = B >= kSplitBatch;
   const bool split = (fs || tq) && (gr || gd) && h->n_side > 0 && big;
   const bool misc = !big && ((mask >> LC_MISC) & 1) && class_units(L, LC_MISC) > 0;
-  const hipStream_t gst = split ? h->side[0] : st;   // the RangeOfMotion / Dynamic chain
+  // two chains: the FDISC / TQDISC chain (the longer one, and its compose cannot start before its records) on
+  // the high-priority side stream 0, the RangeOfMotion / Dynamic chain and what follows on the caller's stream.
+  // At equal priority the FDISC record blocks waited for CU slots behind the other chain's blocks: the record
+  // launch took 299 us instead of 75 us (rocprofv3 kernel trace, ANYmal gait, B = 1024) and the FDISC compose
+  // started only after the other chain had finished.
+  const hipStream_t fst = split ? h->side[0] : st;   // the FDISC / TQDISC chain
+  const hipStream_t gst = st;                        // the RangeOfMotion / Dynamic chain
   if (split) {
     HIPCHK(h, hipEventRecord(h->fork, st));
-    HIPCHK(h, hipStreamWaitEvent(gst, h->fork, 0));
+    HIPCHK(h, hipStreamWaitEvent(fst, h->fork, 0));
   }
   RecArgs R{};
   R.frec = h->d_fsrec; R.fldr = fldr; R.tq_off = tq_off; R.ni = fs ? ni : 0;
@@ -538,8 +544,8 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
   const int fpart = fs ? kRecFdisc : 0;
   if (big) {   // (without a side stream the two chains run one after the other on the caller's stream)
     if (fs || tq) {
-      if (int rc = records({fpart, tq ? kRecTq : 0}, st)) return rc;
-      if (int rc = compose(fs, tq, false, false, false, st)) return rc;
+      if (int rc = records({fpart, tq ? kRecTq : 0}, fst)) return rc;
+      if (int rc = compose(fs, tq, false, false, false, fst)) return rc;
     }
     if (gr || gd) {
       // one block per problem: two blocks (Dynamic | RangeOfMotion lanes) in one launch or in two launches
@@ -553,7 +559,7 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
     if (int rc = records({fpart, tq ? kRecTq : 0, two ? kRecGsDyn : (gr || gd) ? kRecGs : 0, two ? kRecGsRom : 0}, st)) return rc;
     if (int rc = compose(fs, tq, gr, gd, misc, st)) return rc;
   }
-  *forked = split;   // the caller's other launches follow on the side stream, then it joins
+  *forked = split;   // the caller joins side stream 0 after its other launches (which follow on its own stream)
   *misc_done = misc;
   return TOWR_OK;
 }
@@ -607,7 +613,7 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
     const int lc = order[q];
     if (lc == LC_MISC && misc_done) continue;   // in the streaming path's composer launch
     const int nt = class_units(L, lc);
-    const hipStream_t st = stream_forked ? h->side[0] : (nside > 0 && q % (nside + 1) != 0) ? h->side[q % (nside + 1) - 1] : s;
+    const hipStream_t st = stream_forked ? s : (nside > 0 && q % (nside + 1) != 0) ? h->side[q % (nside + 1) - 1] : s;
     KParams P{};
     fill_common(h, P, B, X, ldx, G, ldg, V, ldv, want_g, want_jac, terrains, per_problem);
     P.ntiles = nt;
@@ -1124,8 +1130,15 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
     const int want = ns ? std::atoi(ns) - 1 : (h->L.gait && (h->L.fstream || h->L.gstream[GS_TQ]) ? 1 : 0);
     h->n_side = std::max(0, std::min(towr_gpu_handle_s::kMaxSide, want));
     if (h->n_side > 0 && hipEventCreateWithFlags(&h->fork, hipEventDisableTiming) != hipSuccess) { h->err = "hipEventCreate failed"; return bail(TOWR_ERR_HIP); }
+    // side stream 0 at the device's greatest priority: the streaming path runs its critical chain there (the
+    // FDISC records, whose blocks must not wait behind the other chain's, see launch_stream_path)
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = least = 0;
+#ifdef TOWR_EXP_NOPRIO
+    greatest = least;
+#endif
     for (int i = 0; i < h->n_side; ++i)
-      if (hipStreamCreateWithFlags(&h->side[i], hipStreamNonBlocking) != hipSuccess ||
+      if (hipStreamCreateWithPriority(&h->side[i], hipStreamNonBlocking, i == 0 ? greatest : least) != hipSuccess ||
           hipEventCreateWithFlags(&h->join[i], hipEventDisableTiming) != hipSuccess) {
         h->err = "side stream creation failed"; return bail(TOWR_ERR_HIP);
       }
