@@ -72,10 +72,10 @@ __device__ __forceinline__ void fdisc_record(const KParams& P, const Ctx& c, int
     put(q, te >= 0 ? phase_basis_sum(c.pcols[te & 0xFFFFFF], poly, h0, h1, h2, h3) : 0.0);
   }
 }
-__device__ __forceinline__ void fdisc_records(const KParams& P, const Ctx& c, int b, double* rec, int64_t ldr, int32_t ni) {
+__device__ __forceinline__ void fdisc_records(const KParams& P, const Ctx& c, int b, double* rec, int64_t ldr, int32_t k0, int32_t k1) {
   double* Gb = P.G + (int64_t)b * P.ldg;
   double* R = rec + (int64_t)b * ldr;
-  for (int k = threadIdx.x; k < ni; k += blockDim.x) {
+  for (int k = k0 + threadIdx.x; k < k1; k += blockDim.x) {
     const FsBlock fb = P.fsb[P.fs_iblk[k]];
     const int kk = k - fb.t0, nb = fb.n_inst;
     double* r = R + (int64_t)kFsRS * fb.t0 + kk;
@@ -354,7 +354,11 @@ __device__ __forceinline__ void rec_body(const KParams& P, const RecArgs& A, dou
   const int b = (int)blockIdx.x / np, part = (A.parts >> (4 * ((int)blockIdx.x % np))) & 15;
   const Ctx c = gait_record_setup<0>(P, b, smem);
   if constexpr ((ROLES & 1) != 0)
-    if (part == kRecFdisc) { fdisc_records(P, c, b, A.frec, A.fldr, A.ni); return; }
+    if (part == kRecFdisc || part == kRecFdiscLo || part == kRecFdiscHi) {
+      const int h = (A.ni + 1) / 2;
+      fdisc_records(P, c, b, A.frec, A.fldr, part == kRecFdiscHi ? h : 0, part == kRecFdiscLo ? h : A.ni);
+      return;
+    }
   if constexpr ((ROLES & 4) != 0)
     if (part == kRecTq) { tq_records(P, A, c, b); return; }
   if constexpr ((ROLES & 2) != 0) gs_records<ROTVEC>(P, A.g, c, b, smem, part == kRecGsDyn ? 1 : part == kRecGsRom ? 2 : 0);

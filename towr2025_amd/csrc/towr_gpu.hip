@@ -482,9 +482,18 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
   // started only after the other chain had finished.
   const hipStream_t fst = split ? h->side[0] : st;   // the FDISC / TQDISC chain
   const hipStream_t gst = st;                        // the RangeOfMotion / Dynamic chain
+  // with a second side stream, TQDISC (records + compose) is a third chain: its compose is as long as FDISC's
+  // (ANYmal gait + Torque, B = 1024: 1.7 GB vs 1.46 GB of values), and behind FDISC's in one chain it was the step
+#ifdef TOWR_EXP_TQ2CHAIN
+  const bool tq3 = false;
+#else
+  const bool tq3 = split && tq && fs && h->n_side > 1;
+#endif
+  const hipStream_t tst = tq3 ? h->side[1] : fst;
   if (split) {
     HIPCHK(h, hipEventRecord(h->fork, st));
     HIPCHK(h, hipStreamWaitEvent(fst, h->fork, 0));
+    if (tq3) HIPCHK(h, hipStreamWaitEvent(tst, h->fork, 0));
   }
   RecArgs R{};
   R.frec = h->d_fsrec; R.fldr = fldr; R.tq_off = tq_off; R.ni = fs ? ni : 0;
@@ -506,9 +515,11 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
     for (int p : parts) {
       if (p == 0) continue;
       R.parts |= p << (4 * R.nparts++);
-      roles |= p == kRecFdisc ? 1 : p == kRecTq ? 4 : 2;
+      const bool fp = p == kRecFdisc || p == kRecFdiscLo || p == kRecFdiscHi;
+      roles |= fp ? 1 : p == kRecTq ? 4 : 2;
       dyn = dyn || ((p == kRecGs || p == kRecGsDyn) && R.g.K[GS_DYN] > 0);
-      lanes = std::max<int64_t>(lanes, p == kRecFdisc ? R.ni : p == kRecTq ? R.g.K[GS_TQ] : gs_rec_threads(L, R.g.K[GS_DYN], R.g.K[GS_ROM]));
+      lanes = std::max<int64_t>(lanes, p == kRecFdisc ? R.ni : fp ? (R.ni + 1) / 2 : p == kRecTq ? R.g.K[GS_TQ]
+                                                                                     : gs_rec_threads(L, R.g.K[GS_DYN], R.g.K[GS_ROM]));
     }
     if (R.nparts == 0) return TOWR_OK;
     const int threads = (int)std::min<int64_t>(kGsRecMaxBlock, (lanes + 63) & ~63);
@@ -543,9 +554,18 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
   };
   const int fpart = fs ? kRecFdisc : 0;
   if (big) {   // (without a side stream the two chains run one after the other on the caller's stream)
-    if (fs || tq) {
-      if (int rc = records({fpart, tq ? kRecTq : 0}, fst)) return rc;
-      if (int rc = compose(fs, tq, false, false, false, fst)) return rc;
+    if (tq3) {
+      if (int rc = records({kRecTq}, tst)) return rc;
+      if (int rc = compose(false, true, false, false, false, tst)) return rc;
+    }
+    const bool tqf = tq && !tq3;   // TQDISC in the FDISC chain
+    if (fs || tqf) {
+#ifdef TOWR_EXP_FSPLIT
+      if (int rc = records({fs ? kRecFdiscLo : 0, fs ? kRecFdiscHi : 0, tqf ? kRecTq : 0}, fst)) return rc;
+#else
+      if (int rc = records({fpart, tqf ? kRecTq : 0}, fst)) return rc;
+#endif
+      if (int rc = compose(fs, tqf, false, false, false, fst)) return rc;
     }
     if (gr || gd) {
       // one block per problem: two blocks (Dynamic | RangeOfMotion lanes) in one launch or in two launches
@@ -559,7 +579,7 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
     if (int rc = records({fpart, tq ? kRecTq : 0, two ? kRecGsDyn : (gr || gd) ? kRecGs : 0, two ? kRecGsRom : 0}, st)) return rc;
     if (int rc = compose(fs, tq, gr, gd, misc, st)) return rc;
   }
-  *forked = split;   // the caller joins side stream 0 after its other launches (which follow on its own stream)
+  *forked = split;   // the caller joins side stream 0 (and 1) after its other launches (which follow on its own stream)
   *misc_done = misc;
   return TOWR_OK;
 }
@@ -650,7 +670,7 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
     HIPCHK(h, hipLaunchKernel(kernel_for_class(lc, L.gait, L.rotvec), dim3((unsigned)grid), dim3((unsigned)block), args,
                               lds_bytes(L, lc), st));
   }
-  for (int i = 0; i < (stream_forked ? 1 : nside); ++i) {
+  for (int i = 0; i < (stream_forked ? std::min(h->n_side, 2) : nside); ++i) {
     HIPCHK(h, hipEventRecord(h->join[i], h->side[i]));
     HIPCHK(h, hipStreamWaitEvent(s, h->join[i], 0));
   }
@@ -1127,7 +1147,7 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
     // streams gave 0.524, 0.521, 0.550 ms per step — every kind already fills the CUs' LDS, so kinds
     // cannot co-reside. Under phase-duration optimisation (streaming FDISC) two streams: the write-bound
     // FDISC stream kernel runs beside the latency-bound Dynamic tiles.
-    const int want = ns ? std::atoi(ns) - 1 : (h->L.gait && (h->L.fstream || h->L.gstream[GS_TQ]) ? 1 : 0);
+    const int want = ns ? std::atoi(ns) - 1 : (h->L.gait && (h->L.fstream || h->L.gstream[GS_TQ]) ? (h->L.gstream[GS_TQ] ? 2 : 1) : 0);
     h->n_side = std::max(0, std::min(towr_gpu_handle_s::kMaxSide, want));
     if (h->n_side > 0 && hipEventCreateWithFlags(&h->fork, hipEventDisableTiming) != hipSuccess) { h->err = "hipEventCreate failed"; return bail(TOWR_ERR_HIP); }
     // side stream 0 at the device's greatest priority: the streaming path runs its critical chain there (the
