@@ -32,14 +32,17 @@ def per_kernel(d, counter):
             t = int(targs[0])
             name = ("gait_" if targs[2] == "true" else "") + ("rotvec_" if targs[3] == "true" else "") + NAMES[t]
             acc[name].append(float(r["Counter_Value"]) * 1024.0)
-        elif "towr_gait_frec_kernel" in k:   # phase-duration path: the FDISC record launch
-            acc["gait_records_fdisc"].append(float(r["Counter_Value"]) * 1024.0)
+        elif "towr_gait_frec_kernel" in k:   # phase-duration path: the FDISC (1) / TQDISC (4) / both (5) record launch
+            roles = int(k.split("towr_gait_frec_kernel<")[1].split(">")[0]) if "towr_gait_frec_kernel<" in k else 1
+            acc["gait_records_" + {1: "fdisc", 4: "tqdisc", 5: "fdisc+tqdisc"}[roles]].append(float(r["Counter_Value"]) * 1024.0)
         elif "towr_gait_rec_kernel" in k:   # the RangeOfMotion / Dynamic record launch (<rotvec, roles>)
             acc["gait_records"].append(float(r["Counter_Value"]) * 1024.0)
         elif "towr_gait_compose_kernel<" in k:   # <block, roles>: 1 FDISC, 2 RangeOfMotion, 4 Dynamic, 8 small kinds
             roles = int(k.split("towr_gait_compose_kernel<")[1].split(">")[0].split(",")[1])
-            names = [n for bit, n in ((1, "fdisc"), (2, "range_of_motion"), (4, "dynamic"), (8, "small_kinds")) if roles & bit]
+            names = [n for bit, n in ((1, "fdisc"), (16, "tqdisc"), (2, "range_of_motion"), (4, "dynamic"), (8, "small_kinds")) if roles & bit]
             acc["gait_compose_" + "+".join(names)].append(float(r["Counter_Value"]) * 1024.0)
+        elif "towr_rv_coef_kernel" in k:   # the RotVec base-angular coefficient pre-pass
+            acc["rotvec_coef"].append(float(r["Counter_Value"]) * 1024.0)
         elif "towr_dyn_g1_kernel" in k:
             acc["dyn_g1"].append(float(r["Counter_Value"]) * 1024.0)
     return {k: sum(v) / len(v) for k, v in acc.items()}

@@ -354,11 +354,7 @@ __device__ __forceinline__ void rec_body(const KParams& P, const RecArgs& A, dou
   const int b = (int)blockIdx.x / np, part = (A.parts >> (4 * ((int)blockIdx.x % np))) & 15;
   const Ctx c = gait_record_setup<0>(P, b, smem);
   if constexpr ((ROLES & 1) != 0)
-    if (part == kRecFdisc || part == kRecFdiscLo || part == kRecFdiscHi) {
-      const int h = (A.ni + 1) / 2;
-      fdisc_records(P, c, b, A.frec, A.fldr, part == kRecFdiscHi ? h : 0, part == kRecFdiscLo ? h : A.ni);
-      return;
-    }
+    if (part == kRecFdisc) { fdisc_records(P, c, b, A.frec, A.fldr, 0, A.ni); return; }
   if constexpr ((ROLES & 4) != 0)
     if (part == kRecTq) { tq_records(P, A, c, b); return; }
   if constexpr ((ROLES & 2) != 0) gs_records<ROTVEC>(P, A.g, c, b, smem, part == kRecGsDyn ? 1 : part == kRecGsRom ? 2 : 0);

@@ -317,7 +317,7 @@ struct ComposeArgs {
 // the record launch's arguments (towr_gait_rec_kernel): nparts blocks per problem, block r doing part
 // (parts >> 4 r) & 15 (RecPart); the FDISC records (frec, fldr, ni instants) and the
 // TorqueConstraintDiscretized records (frec + tq_off, g.inst[GS_TQ]) share one array per problem
-enum RecPart { kRecFdisc = 1, kRecTq = 2, kRecGs = 3, kRecGsDyn = 4, kRecGsRom = 5, kRecFdiscLo = 6, kRecFdiscHi = 7 };   // Lo / Hi: the first / second half of the FDISC instants
+enum RecPart { kRecFdisc = 1, kRecTq = 2, kRecGs = 3, kRecGsDyn = 4, kRecGsRom = 5 };
 struct RecArgs {
   GsRecArgs g;
   double* frec; int64_t fldr, tq_off;

@@ -480,19 +480,22 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
   // At equal priority the FDISC record blocks waited for CU slots behind the other chain's blocks: the record
   // launch took 299 us instead of 75 us (rocprofv3 kernel trace, ANYmal gait, B = 1024) and the FDISC compose
   // started only after the other chain had finished.
+#ifdef TOWR_EXP_OLDCHAIN
+  const hipStream_t fst = st;
+  const hipStream_t gst = split ? h->side[0] : st;
+#else
   const hipStream_t fst = split ? h->side[0] : st;   // the FDISC / TQDISC chain
   const hipStream_t gst = st;                        // the RangeOfMotion / Dynamic chain
+#endif
   // with a second side stream, TQDISC (records + compose) is a third chain: its compose is as long as FDISC's
   // (ANYmal gait + Torque, B = 1024: 1.7 GB vs 1.46 GB of values), and behind FDISC's in one chain it was the step
-#ifdef TOWR_EXP_TQ2CHAIN
-  const bool tq3 = false;
-#else
+  // (measured: ANYmal gait + Torque, B = 1024, one box: 1.206 ms per step with three chains, 1.233 with TQDISC
+  // behind FDISC in one chain)
   const bool tq3 = split && tq && fs && h->n_side > 1;
-#endif
   const hipStream_t tst = tq3 ? h->side[1] : fst;
   if (split) {
     HIPCHK(h, hipEventRecord(h->fork, st));
-    HIPCHK(h, hipStreamWaitEvent(fst, h->fork, 0));
+    HIPCHK(h, hipStreamWaitEvent(fst == st ? gst : fst, h->fork, 0));
     if (tq3) HIPCHK(h, hipStreamWaitEvent(tst, h->fork, 0));
   }
   RecArgs R{};
@@ -515,11 +518,9 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
     for (int p : parts) {
       if (p == 0) continue;
       R.parts |= p << (4 * R.nparts++);
-      const bool fp = p == kRecFdisc || p == kRecFdiscLo || p == kRecFdiscHi;
-      roles |= fp ? 1 : p == kRecTq ? 4 : 2;
+      roles |= p == kRecFdisc ? 1 : p == kRecTq ? 4 : 2;
       dyn = dyn || ((p == kRecGs || p == kRecGsDyn) && R.g.K[GS_DYN] > 0);
-      lanes = std::max<int64_t>(lanes, p == kRecFdisc ? R.ni : fp ? (R.ni + 1) / 2 : p == kRecTq ? R.g.K[GS_TQ]
-                                                                                     : gs_rec_threads(L, R.g.K[GS_DYN], R.g.K[GS_ROM]));
+      lanes = std::max<int64_t>(lanes, p == kRecFdisc ? R.ni : p == kRecTq ? R.g.K[GS_TQ] : gs_rec_threads(L, R.g.K[GS_DYN], R.g.K[GS_ROM]));
     }
     if (R.nparts == 0) return TOWR_OK;
     const int threads = (int)std::min<int64_t>(kGsRecMaxBlock, (lanes + 63) & ~63);
@@ -560,11 +561,8 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
     }
     const bool tqf = tq && !tq3;   // TQDISC in the FDISC chain
     if (fs || tqf) {
-#ifdef TOWR_EXP_FSPLIT
-      if (int rc = records({fs ? kRecFdiscLo : 0, fs ? kRecFdiscHi : 0, tqf ? kRecTq : 0}, fst)) return rc;
-#else
+      // (the FDISC records in two blocks per problem, each half the instants: 0.638 vs 0.629 ms, not kept)
       if (int rc = records({fpart, tqf ? kRecTq : 0}, fst)) return rc;
-#endif
       if (int rc = compose(fs, tqf, false, false, false, fst)) return rc;
     }
     if (gr || gd) {
