@@ -64,8 +64,8 @@ struct TileEmit {
     }
   }
   bool gon = true;         // DIRECT: g requested
-  __device__ __forceinline__ void g(int row, double v) {
-    if (!DIRECT) gout[row] = v;
+  __device__ __forceinline__ void g(int row, double v) {   // (fixed-gait Dynamic: g straight to HBM, gon = g requested)
+    if (!DIRECT) { if (gon) gout[row] = v; }
     else if (gon && want(row)) gout[row] = v;
   }
   // GAIT outputs are zero-filled before the evaluation (tile_body / misc_body), so candidates whose

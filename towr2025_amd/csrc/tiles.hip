@@ -113,8 +113,12 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
   }
   // GAIT: direct HBM emission into the zero-filled V (see TileEmit)
   // fixed gait, RotVec Dynamic: eval_dyn never takes group 1 (the pre-pass coefficients, kRvPre)
+  // fixed-gait Dynamic writes its g rows (group 0, phase B: 6 complete rows per instant, after every load) straight to
+  // HBM: without the LDS rows the block fits three per CU at <= 168 VGPRs (layout.hip, the Dynamic LDS)
+  constexpr bool kGDirect = TYPE == IT_DYN && !GAIT;
   TileEmit<TBLOCK, slot_depth(TYPE), GAIT, gait_slot_pre(TYPE), (TYPE == IT_DYN && ROTVEC && !GAIT) ? 1 : 0> em(
-      P.slots + it.slot, GAIT ? Vb + T.v0 : smem, GAIT ? Gb : smem + lds_rows_off - T.r0);
+      P.slots + it.slot, GAIT ? Vb + T.v0 : smem, GAIT || kGDirect ? Gb : smem + lds_rows_off - T.r0);
+  if constexpr (kGDirect) em.gon = P.want_g != 0;
   if constexpr (GAIT) {
     if (it.rsel > 0) { em.flo = it.row0 + rsel_first(it.rsel); em.fcnt = rsel_count(it.rsel); }
     em.nvals = P.want_jac ? T.v1 - T.v0 : 0;
@@ -200,7 +204,8 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
   if constexpr (TYPE == IT_DYN) {   // phase B of group 0: the endeffector sums from LDS
     const bool g0lane = it.type == TYPE && it.group == 0;
     TileEmitPre<TBLOCK, kDynG0PhaseA, GAIT> emb(P.slots + it.slot, GAIT ? Vb + T.v0 : smem,
-                                                GAIT ? Gb : smem + lds_rows_off - T.r0, g0lane);
+                                                GAIT || kGDirect ? Gb : smem + lds_rows_off - T.r0, g0lane);
+    if constexpr (kGDirect) emb.gon = P.want_g != 0;
     emb.nvals = P.want_jac ? T.v1 - T.v0 : 0;
     emb.gon = P.want_g != 0;
     __syncthreads();
@@ -215,7 +220,7 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
   __syncthreads();
   if constexpr (!GAIT) {
     if (P.want_jac) copy_out(smem, Vb + T.v0, T.v1 - T.v0, threadIdx.x, KBLOCK);
-    if (P.want_g)
+    if (P.want_g && !kGDirect)
       for (int i = threadIdx.x; i < T.r1 - T.r0; i += KBLOCK) __builtin_nontemporal_store(smem[lds_rows_off + i], Gb + T.r0 + i);
   }
 }
@@ -223,7 +228,11 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
 template <int TYPE, int BLOCK, bool GAIT, bool ROTVEC>
 // second argument: minimum waves per SIMD. Dynamic: 2 (fixed gait: 256 lanes, 2 blocks per CU; gait: the
 // 512-lane row-split block, <= 256 VGPRs)
+#ifdef TOWR_EXP_DYN3
+__global__ void __launch_bounds__(BLOCK, TYPE == IT_DYN && !GAIT ? 3 : TYPE == IT_DYN ? 2 : 1) towr_tile_kernel(KParams P) {
+#else
 __global__ void __launch_bounds__(BLOCK, TYPE == IT_DYN ? 2 : 1) towr_tile_kernel(KParams P) {
+#endif
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int total = P.B * P.ntiles;
   const int per = (total + 7) / 8;

@@ -1148,15 +1148,13 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
     const int want = ns ? std::atoi(ns) - 1 : (h->L.gait && (h->L.fstream || h->L.gstream[GS_TQ]) ? (h->L.gstream[GS_TQ] ? 2 : 1) : 0);
     h->n_side = std::max(0, std::min(towr_gpu_handle_s::kMaxSide, want));
     if (h->n_side > 0 && hipEventCreateWithFlags(&h->fork, hipEventDisableTiming) != hipSuccess) { h->err = "hipEventCreate failed"; return bail(TOWR_ERR_HIP); }
-    // side stream 0 at the device's greatest priority: the streaming path runs its critical chain there (the
-    // FDISC records, whose blocks must not wait behind the other chain's, see launch_stream_path)
+    // side streams at the device's greatest priority: the streaming path runs its critical chains there (the
+    // FDISC / TQDISC records, whose blocks must not wait behind the other chain's, see launch_stream_path;
+    // ANYmal gait + Torque, B = 1024: the TQDISC records on a low-priority stream took 730 us instead of ~50)
     int least = 0, greatest = 0;
     if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = least = 0;
-#ifdef TOWR_EXP_NOPRIO
-    greatest = least;
-#endif
     for (int i = 0; i < h->n_side; ++i)
-      if (hipStreamCreateWithPriority(&h->side[i], hipStreamNonBlocking, i == 0 ? greatest : least) != hipSuccess ||
+      if (hipStreamCreateWithPriority(&h->side[i], hipStreamNonBlocking, greatest) != hipSuccess ||
           hipEventCreateWithFlags(&h->join[i], hipEventDisableTiming) != hipSuccess) {
         h->err = "side stream creation failed"; return bail(TOWR_ERR_HIP);
       }
