@@ -25,11 +25,7 @@
 namespace tg {
 
 enum { kPos = 0, kVel = 1, kAcc = 2 };
-#ifdef TOWR_EXP_EULERSPLIT
-constexpr bool kEulerAxisItems = true;    // experiment: fixed-gait Euler base-angular block as one item per axis
-#else
-constexpr bool kEulerAxisItems = false;
-#endif
+
 enum { X = 0, Y = 1, Z = 2 };
 enum { AX = 0, AY = 1, AZ = 2, LX = 3, LY = 4, LZ = 5 };
 
@@ -1435,8 +1431,7 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
     };
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
-    for (int e = 0; e < 3; ++e)
-      if (!kEulerAxisItems || it.a1 == 0 || it.a1 == 1 + e) axis(e);
+    for (int e = 0; e < 3; ++e) axis(e);
 #else
     for (int e = 0; e < 3; ++e)
       if (it.a1 == 0 || it.a1 == 1 + e) axis(e);

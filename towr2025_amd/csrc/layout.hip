@@ -1028,7 +1028,7 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
         auto ts = dts_of(c.T, c.dt);
         for (int k = 0; k < (int)ts.size(); ++k, ++inst)
           for (int g = 0; g < 2 + E; ++g) {
-            if (g == 1 && (L.rotvec || (kEulerAxisItems && !L.gait))) {   // RotVec base-angular block: one item per rotation-vector component
+            if (g == 1 && L.rotvec) {   // RotVec base-angular block: one item per rotation-vector component
               for (int ax = 0; ax < 3; ++ax) add(IT_DYN, g, 0, k, row + 6 * k, ts[k], 0, 1 + ax, 0.0);
             } else {
               add(IT_DYN, g, 0, k, row + 6 * k, ts[k], 0, 0, 0.0);
@@ -1364,7 +1364,7 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
             // the endeffector groups after the three axis groups (one wave may hold the last axis and
             // the first endeffectors); two tiles with whole waves per group measured slower (0.078 vs
             // 0.063 ms: twice the x staging and block overhead)
-            if (type == IT_DYN && !L.gait && it.group >= 2 && (L.rotvec || kEulerAxisItems))
+            if (type == IT_DYN && !L.gait && it.group >= 2 && L.rotvec)
               lane = 64 + 3 * (b - a) + (it.group - 2) * (b - a) + (k - a);
             if (lane < 0 || lane >= sp.block || lanes[lane].type != IT_NONE) { err = "internal: lane assignment"; return TOWR_ERR_INVALID; }
             lanes[lane] = it;
@@ -1561,7 +1561,7 @@ TypeSpec type_spec(int type, int n_ee, bool gait, bool rotvec) {
   const int blk = tile_block(type, gait);
   switch (type) {
     case IT_DYN:   // waves: g0 | g1 | ee, ee (gait: rows); per-axis base-angular items: 3 g1 lanes per instant
-      if (rotvec || (kEulerAxisItems && !gait))   // per-component base-angular items
+      if (rotvec)   // per-component base-angular items
         return {blk, std::max(1, gait ? std::min(64 / 3, 64 / E) : std::min(64, (blk - 64) / (3 + E)))};
       return {blk, std::max(1, std::min(64, gait ? 64 / E : 128 / E))};
     case IT_ROM: return {blk, gait ? 128 : 64};                                         // waves: g0 | g1 | g2 (gait: rows, 2 halves)

@@ -227,12 +227,10 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
 
 template <int TYPE, int BLOCK, bool GAIT, bool ROTVEC>
 // second argument: minimum waves per SIMD. Dynamic: 2 (fixed gait: 256 lanes, 2 blocks per CU; gait: the
-// 512-lane row-split block, <= 256 VGPRs)
-#ifdef TOWR_EXP_DYN3
-__global__ void __launch_bounds__(BLOCK, TYPE == IT_DYN && !GAIT ? 3 : TYPE == IT_DYN ? 2 : 1) towr_tile_kernel(KParams P) {
-#else
-__global__ void __launch_bounds__(BLOCK, TYPE == IT_DYN ? 2 : 1) towr_tile_kernel(KParams P) {
-#endif
+// 512-lane row-split block, <= 256 VGPRs). Fixed-gait RotVec Dynamic: 3 (<= 168 VGPRs, a 44-byte spill; with
+// the g rows out of LDS three blocks fit a CU: 0.097 -> 0.093 ms per 4096 problems incl. the pre-pass, RotVec step
+// 0.325 -> 0.320 ms; the Euler tile at 3 spills 324 bytes per lane and slows 0.061 -> 0.076 ms)
+__global__ void __launch_bounds__(BLOCK, TYPE == IT_DYN && !GAIT && ROTVEC ? 3 : TYPE == IT_DYN ? 2 : 1) towr_tile_kernel(KParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int total = P.B * P.ntiles;
   const int per = (total + 7) / 8;
