@@ -1374,22 +1374,18 @@ TG_HD void dyn_rv_emit(const Ctx& c, const ItemDesc& it, const DynRvState& S, Em
 
 // The same entries from precomputed coefficients (the device's RotVec pre-pass, tiles.hip towr_rv_coef_kernel):
 // coef[(9 e + f) stride] = field f (Mp[3] | Mv[3] | Ma[3]) of the item's component e = a1 - 1
-// (rotvec false: an unsplit Euler item, all three axes in order, as eval_dyn's group 1)
 template <class Emit>
-TG_HD void dyn_rv_emit_pre(const Ctx& c, const ItemDesc& it, const double* coef, int64_t stride, Emit& em, bool rotvec = true) {
-  const int r0 = it.row0;
+TG_HD void dyn_rv_emit_pre(const Ctx& c, const ItemDesc& it, const double* coef, int64_t stride, Emit& em) {
+  const int r0 = it.row0, e = it.a1 - 1;
   SplinePt A;
   spline_eval(c, SP_BASE_ANG, it.t, A);
   double Hp[4], Hv[4], Ha[4];
   spline_basis(A, kPos, Hp); spline_basis(A, kVel, Hv); spline_basis(A, kAcc, Ha);
-  const int e0 = rotvec ? it.a1 - 1 : 0, e1 = rotvec ? it.a1 : 3;
-  for (int e = e0; e < e1; ++e) {
-    double M[9];
-    for (int f = 0; f < 9; ++f) M[f] = coef[(9 * e + f) * stride];
-    for (int r = 0; r < 3; ++r)
-      for (int bb = 0; bb < 4; ++bb)
-        em(r0 + AX + r, basis_col(c, SP_BASE_ANG, A.poly, bb, e), M[r] * Hp[bb] + M[3 + r] * Hv[bb] + M[6 + r] * Ha[bb], true);
-  }
+  double M[9];
+  for (int f = 0; f < 9; ++f) M[f] = coef[(9 * e + f) * stride];
+  for (int r = 0; r < 3; ++r)
+    for (int bb = 0; bb < 4; ++bb)
+      em(r0 + AX + r, basis_col(c, SP_BASE_ANG, A.poly, bb, e), M[r] * Hp[bb] + M[3 + r] * Hv[bb] + M[6 + r] * Ha[bb], true);
 }
 
 template <class Emit>

@@ -259,7 +259,7 @@ const void* misc_kernel_for(bool gait);
 const void* step_kernel_for(bool gait, bool rotvec, int kblock);
 const void* cost_kernel_for(bool gait, bool grad, bool rotvec);
 const void* traj_kernel_for(bool gait);
-const void* rv_coef_kernel(bool rotvec);
+const void* rv_coef_kernel();
 constexpr int kRvCoefBlock = 256;   // the RotVec coefficient pre-pass: 4 waves, one component each
 constexpr int kCostBlock = 256;   // objective kernel: one block per problem
 constexpr int kTrajBlock = 64;    // trajectory kernel: one block per (problem, 64 sample times)

@@ -1195,15 +1195,10 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
   // ---- fixed gait, RotVec: the Dynamic instants of the base-angular coefficient pre-pass (tiles.hip
   // towr_rv_coef_kernel); the three component items of an instant (a1 = 1, 2, 3, consecutive) get its index in a0
   L.rv_inst.clear();
-#ifdef TOWR_EXP_EULERPRE
-  const bool bang_pre = !L.gait;   // experiment: the Euler block's coefficients from the pre-pass too
-#else
-  const bool bang_pre = L.rotvec && !L.gait;
-#endif
-  if (bang_pre)
+  if (L.rotvec && !L.gait)
     for (ItemDesc& it : L.items) {
-      if (it.type != IT_DYN || it.group != 1 || (L.rotvec && it.a1 <= 0)) continue;
-      if (it.a1 <= 1) {
+      if (it.type != IT_DYN || it.group != 1 || it.a1 <= 0) continue;
+      if (it.a1 == 1) {
         for (int bb = 0; bb < 4; ++bb)   // the pre-pass reads x in global memory: no constant node values
           for (int e = 0; e < 3; ++e)
             if (L.segs[(size_t)it.seg * L.spl.size() + SP_BASE_ANG].col[bb][e] >= L.n) { err = "internal: constant base-angular node value"; return TOWR_ERR_INVALID; }

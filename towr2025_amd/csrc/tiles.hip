@@ -188,16 +188,12 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
   DynG0 g0;   // DYN group 0 between its two phases
   // fixed gait, RotVec: the base-angular coefficients of each (instant, component) come from the pre-pass
   // (towr_rv_coef_kernel, launched before this kernel); the component lanes only form and emit their 12 entries
-#ifdef TOWR_EXP_EULERPRE
-  constexpr bool kRvPre = TYPE == IT_DYN && !GAIT;
-#else
   constexpr bool kRvPre = TYPE == IT_DYN && ROTVEC && !GAIT;
-#endif
   if (it.type == TYPE) {
     if constexpr (TYPE == IT_DYN) {
       if (it.group == 0) dyn_g0_a(c, it, em, g0);
       else if (kRvPre && it.group == 1) {
-        if (P.want_jac) dyn_rv_emit_pre(c, it, P.rvc + (int64_t)b * P.n_rvi + it.a0, (int64_t)P.B * P.n_rvi, em, ROTVEC);
+        if (P.want_jac) dyn_rv_emit_pre(c, it, P.rvc + (int64_t)b * P.n_rvi + it.a0, (int64_t)P.B * P.n_rvi, em);
       }
       else eval_dyn(c, it, em);   // group 1 and the endeffector groups (these deposit their sum terms)
     } else {
@@ -297,7 +293,6 @@ __global__ void __launch_bounds__(KBLOCK, (KBLOCK == 256 ? 2 : 1)) towr_step_ker
 // (problem, instant, component) at full occupancy; waves are component-uniform (wave w: component w % 3, 64
 // consecutive (problem, instant) pairs), and the coefficients are stored field-major (field f of component
 // e at (9 e + f) B K + b K + q), so both this kernel's stores and the tile's loads coalesce.
-template <bool ROTVEC>
 __global__ void __launch_bounds__(kRvCoefBlock) towr_rv_coef_kernel(KParams P) {
   const int K = P.n_rvi;
   const int64_t pairs = (int64_t)P.B * K, chunks = (pairs + 63) / 64;
@@ -312,19 +307,13 @@ __global__ void __launch_bounds__(kRvCoefBlock) towr_rv_coef_kernel(KParams P) {
   c.seg = nullptr; c.sg = P.sg; c.row = ri.seg;
   c.x = P.X + (int64_t)b * P.ldx;   // base-angular node values only: never a constant node (layout.hip checks)
   c.nodecol = P.nodecol; c.spl = P.spl; c.dur = P.dur; c.ter = P.terrains;
-  c.rb = P.rb; c.gait = false; c.rotvec = ROTVEC;
+  c.rb = P.rb; c.gait = false; c.rotvec = true;
+  DynRvState S;
+  dyn_rv_state(c, ri.t, S);
   double M[9];
-  if constexpr (ROTVEC) {
-    DynRvState S;
-    dyn_rv_state(c, ri.t, S);
-    if (e == 0) dyn_rv_column<0>(S, M, M + 3, M + 6);
-    else if (e == 1) dyn_rv_column<1>(S, M, M + 3, M + 6);
-    else dyn_rv_column<2>(S, M, M + 3, M + 6);
-  } else {   // (experiment: the Euler block's axis coefficients)
-    DynEulerState S;
-    dyn_euler_state(c, ri.t, S);
-    dyn_euler_axis(c, S, e, M, M + 3, M + 6);
-  }
+  if (e == 0) dyn_rv_column<0>(S, M, M + 3, M + 6);
+  else if (e == 1) dyn_rv_column<1>(S, M, M + 3, M + 6);
+  else dyn_rv_column<2>(S, M, M + 3, M + 6);
   double* o = P.rvc + (int64_t)9 * e * pairs + pr;
 #pragma unroll
   for (int f = 0; f < 9; ++f) __builtin_nontemporal_store(M[f], o + f * pairs);
@@ -357,9 +346,7 @@ const void* tile_kernel_for(int type, bool gait, bool rotvec) {
   if (gait) return rotvec ? kernel_for_mode<true, true>(type) : kernel_for_mode<true, false>(type);
   return rotvec ? kernel_for_mode<false, true>(type) : kernel_for_mode<false, false>(type);
 }
-const void* rv_coef_kernel(bool rotvec) {
-  return rotvec ? reinterpret_cast<const void*>(&towr_rv_coef_kernel<true>) : reinterpret_cast<const void*>(&towr_rv_coef_kernel<false>);
-}
+const void* rv_coef_kernel() { return reinterpret_cast<const void*>(&towr_rv_coef_kernel); }
 const void* misc_kernel_for(bool gait) {
   return gait ? reinterpret_cast<const void*>(&towr_misc_kernel<true>) : reinterpret_cast<const void*>(&towr_misc_kernel<false>);
 }

@@ -397,7 +397,7 @@ int launch_rv_prepass(towr_gpu_handle h, int B, const double* X, int64_t ldx, in
   const int64_t waves = 3 * (((int64_t)B * K + 63) / 64), grid = (waves + kRvCoefBlock / 64 - 1) / (kRvCoefBlock / 64);
   if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
   void* args[] = {&P};
-  HIPCHK(h, hipLaunchKernel(rv_coef_kernel(L.rotvec), dim3((unsigned)grid), dim3(kRvCoefBlock), args, 0, s));
+  HIPCHK(h, hipLaunchKernel(rv_coef_kernel(), dim3((unsigned)grid), dim3(kRvCoefBlock), args, 0, s));
   return TOWR_OK;
 }
 
@@ -607,20 +607,6 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
                    int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem, int only_class) {
   const Layout& L = h->L;
   uint32_t fused_mask = 0;
-  bool rv_async = false;   // the base-angular pre-pass runs on side stream 0 beside the fused launch
-#ifdef TOWR_EXP_EULERPRE
-  {
-    bool dyn_fused = false;
-    for (int g = 0; g < h->n_fuse; ++g) dyn_fused = dyn_fused || ((h->fuse[g].mask >> LC_DYN) & 1);
-    if (only_class < 0 && !L.gait && !L.rv_inst.empty() && want_jac && h->n_side > 0 && !dyn_fused && class_units(L, LC_DYN) > 0) {
-      HIPCHK(h, hipEventRecord(h->fork, s));
-      HIPCHK(h, hipStreamWaitEvent(h->side[0], h->fork, 0));
-      if (int rc = launch_rv_prepass(h, B, X, ldx, want_jac, h->side[0])) return rc;
-      HIPCHK(h, hipEventRecord(h->join[0], h->side[0]));
-      rv_async = true;
-    }
-  }
-#endif
   if (only_class < 0)
     for (int g = 0; g < h->n_fuse; ++g) {
       if (int rc = launch_fused(h, h->fuse[g], B, X, ldx, G, ldg, V, ldv, want_g, want_jac, s, terrains, per_problem)) return rc;
@@ -674,8 +660,7 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
     const int64_t grid = ((total + 7) / 8) * 8;
     if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
     if (lc == LC_DYN) {
-      if (rv_async) HIPCHK(h, hipStreamWaitEvent(st, h->join[0], 0));
-      else if (int rc = launch_rv_prepass(h, B, X, ldx, want_jac, st)) return rc;
+      if (int rc = launch_rv_prepass(h, B, X, ldx, want_jac, st)) return rc;
       P.rvc = h->d_rvc;   // (grown by the pre-pass)
     }
     const int block = class_block(L, lc);
@@ -1160,10 +1145,7 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
     // streams gave 0.524, 0.521, 0.550 ms per step — every kind already fills the CUs' LDS, so kinds
     // cannot co-reside. Under phase-duration optimisation (streaming FDISC) two streams: the write-bound
     // FDISC stream kernel runs beside the latency-bound Dynamic tiles.
-    int want = ns ? std::atoi(ns) - 1 : (h->L.gait && (h->L.fstream || h->L.gstream[GS_TQ]) ? (h->L.gstream[GS_TQ] ? 2 : 1) : 0);
-#ifdef TOWR_EXP_EULERPRE
-    if (!ns && !h->L.gait && !h->L.rv_inst.empty()) want = 1;
-#endif
+    const int want = ns ? std::atoi(ns) - 1 : (h->L.gait && (h->L.fstream || h->L.gstream[GS_TQ]) ? (h->L.gstream[GS_TQ] ? 2 : 1) : 0);
     h->n_side = std::max(0, std::min(towr_gpu_handle_s::kMaxSide, want));
     if (h->n_side > 0 && hipEventCreateWithFlags(&h->fork, hipEventDisableTiming) != hipSuccess) { h->err = "hipEventCreate failed"; return bail(TOWR_ERR_HIP); }
     // side streams at the device's greatest priority: the streaming path runs its critical chains there (the
