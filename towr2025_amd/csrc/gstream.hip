@@ -365,11 +365,7 @@ __global__ void __launch_bounds__(kGsRecMaxBlock) __attribute__((amdgpu_waves_pe
   rec_body<ROTVEC, ROLES>(P, A, smem);
 }
 template <int ROLES>   // FDISC and / or TQDISC records only
-#ifdef TOWR_EXP_TQW2
-__global__ void __launch_bounds__(kGsRecMaxBlock) towr_gait_frec_kernel(KParams P, RecArgs A) {
-#else
 __global__ void __launch_bounds__(kGsRecMaxBlock) __attribute__((amdgpu_waves_per_eu(4))) towr_gait_frec_kernel(KParams P, RecArgs A) {
-#endif
   extern __shared__ __attribute__((aligned(16))) double smem[];
   rec_body<false, ROLES>(P, A, smem);
 }

@@ -441,13 +441,13 @@ int gs_rec_threads(const Layout& L, int64_t Kd, int64_t Kr) {   // the record la
 //   compose: the compose blocks of the classes (towr_gait_compose_kernel), each CSR range written once.
 // Only the classes in `mask` are recorded (a single-class launch records nothing else).
 // A batch of kSplitBatch problems or more runs as two chains (one after the other without a side stream,
-// TOWR_GPU_STREAMS=1): FDISC + TQDISC records + their compose launch on the caller's stream beside the
-// RangeOfMotion / Dynamic records + the Dynamic and RangeOfMotion compose launches on the side stream, so that
-// the write-bound FDISC compose overlaps the latency-bound record work (MI355X, ANYmal gait, B = 1024, one
-// box: 0.600-0.608 ms per step; one chain 0.663, records in 256-problem chunks pipelined against the compose
-// 0.737, Dynamic + RangeOfMotion in one compose launch 0.640). The small kinds then follow the shorter chain
-// on the side stream (*forked: the caller launches them there and joins). A smaller batch (B = 1: IPOPT's
-// callbacks) is two launches on the caller's stream: every record part in one, every compose role and the
+// TOWR_GPU_STREAMS=1): FDISC + TQDISC records + their compose launch on the high-priority side stream 0 beside
+// the RangeOfMotion / Dynamic records + the Dynamic and RangeOfMotion compose launches on the caller's stream, so
+// that the write-bound FDISC compose overlaps the latency-bound record work (MI355X, ANYmal gait, B = 1024, one
+// box, round 3: 0.600-0.608 ms per step; one chain 0.663, records in 256-problem chunks pipelined against the
+// compose 0.737, Dynamic + RangeOfMotion in one compose launch 0.640). With TQDISC and a second side stream it is
+// a third chain (below). The caller joins the side streams after its other launches (*forked). A smaller
+// batch (B = 1: IPOPT's callbacks) is two launches on the caller's stream: every record part in one, every compose role and the
 // small-kind groups in the other (*misc_done) — at B = 1 a launch boundary or a cross-stream event costs
 // more than any overlap gains (MI355X, ANYmal gait: 97 us for the per-class chains, 70 us for four launches
 // on one stream).
@@ -480,13 +480,8 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
   // At equal priority the FDISC record blocks waited for CU slots behind the other chain's blocks: the record
   // launch took 299 us instead of 75 us (rocprofv3 kernel trace, ANYmal gait, B = 1024) and the FDISC compose
   // started only after the other chain had finished.
-#ifdef TOWR_EXP_OLDCHAIN
-  const hipStream_t fst = st;
-  const hipStream_t gst = split ? h->side[0] : st;
-#else
   const hipStream_t fst = split ? h->side[0] : st;   // the FDISC / TQDISC chain
   const hipStream_t gst = st;                        // the RangeOfMotion / Dynamic chain
-#endif
   // with a second side stream, TQDISC (records + compose) is a third chain: its compose is as long as FDISC's
   // (ANYmal gait + Torque, B = 1024: 1.7 GB vs 1.46 GB of values), and behind FDISC's in one chain it was the step
   // (measured: ANYmal gait + Torque, B = 1024, one box: 1.206 ms per step with three chains, 1.233 with TQDISC
@@ -495,7 +490,7 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
   const hipStream_t tst = tq3 ? h->side[1] : fst;
   if (split) {
     HIPCHK(h, hipEventRecord(h->fork, st));
-    HIPCHK(h, hipStreamWaitEvent(fst == st ? gst : fst, h->fork, 0));
+    HIPCHK(h, hipStreamWaitEvent(fst, h->fork, 0));
     if (tq3) HIPCHK(h, hipStreamWaitEvent(tst, h->fork, 0));
   }
   RecArgs R{};
