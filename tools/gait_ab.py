@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--no-gait", action="store_true", help="the headline formulation (fixed phase durations)")
     ap.add_argument("--only", default=None, help="comma-separated part names: time only these, no whole step")
     ap.add_argument("--torque", action="store_true", help="ANYmal on stairs + Parameters::Torque (bench.py gait_torque)")
+    ap.add_argument("--step-only", action="store_true", help="only the whole step (no per-kernel times)")
     args = ap.parse_args()
     import torch
     from towr2025_amd import _capi as capi
@@ -48,7 +49,7 @@ def main():
     for _ in range(0 if only else 30):
         p.eval_batch_device(X, G, V)
     out = {}
-    for k, name, nt, by in p.kernels():
+    for k, name, nt, by in ([] if args.step_only else p.kernels()):
         if only and name not in only:
             continue
         for _ in range(3):
