@@ -602,22 +602,30 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
                    int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem, int only_class) {
   const Layout& L = h->L;
   uint32_t fused_mask = 0;
+  // a batch with fusion groups: the other classes on the side streams beside the fused launches (forked before
+  // them: the fused launch on the caller's stream, Dynamic then the small kinds on side stream 0); at small B the
+  // fork and join cost more than the overlap gains
+  const bool overlap = only_class < 0 && h->n_side > 0 && h->n_fuse > 0 && !uses_scratch(L) && B >= kSplitBatch;
+  if (overlap) {
+    HIPCHK(h, hipEventRecord(h->fork, s));
+    for (int i = 0; i < h->n_side; ++i) HIPCHK(h, hipStreamWaitEvent(h->side[i], h->fork, 0));
+  }
   if (only_class < 0)
     for (int g = 0; g < h->n_fuse; ++g) {
       if (int rc = launch_fused(h, h->fuse[g], B, X, ldx, G, ldg, V, ldv, want_g, want_jac, s, terrains, per_problem)) return rc;
       fused_mask |= h->fuse[g].mask;
     }
-  // The launch classes are independent (disjoint rows and CSR ranges): optionally fork them onto the
-  // handle's side streams (TOWR_GPU_STREAMS) and join back into the caller's stream. Heaviest first.
+  // The launch classes are independent (disjoint rows and CSR ranges): they may run on the handle's side
+  // streams (above, or TOWR_GPU_STREAMS without fusion groups) and join back into the caller's stream. Heaviest first.
   int order[LC_COUNT], nk = 0;
   for (int lc = 0; lc < LC_COUNT; ++lc)
     if (class_units(L, lc) > 0 && !((fused_mask >> lc) & 1) && (only_class < 0 || lc == only_class)) order[nk++] = lc;
   std::sort(order, order + nk, [&](int a, int b) { return class_bytes(L, a) > class_bytes(L, b); });
   std::stable_partition(order, order + nk, [](int lc) { return lc != LC_MISC; });   // the small kinds last
   // (the streaming path forks its own side stream, see launch_stream_path; the other classes follow it on
-  // the caller's stream)
-  const int nside = (only_class < 0 && nk > 1 && !uses_scratch(L)) ? std::min(h->n_side, nk - 1) : 0;
-  if (nside > 0) {
+  // the caller's stream; a small batch with fusion groups runs serially)
+  const int nside = overlap ? h->n_side : (only_class < 0 && nk > 1 && !uses_scratch(L) && h->n_fuse == 0) ? std::min(h->n_side, nk - 1) : 0;
+  if (nside > 0 && !overlap) {
     HIPCHK(h, hipEventRecord(h->fork, s));
     for (int i = 0; i < nside; ++i) HIPCHK(h, hipStreamWaitEvent(h->side[i], h->fork, 0));
   }
@@ -626,7 +634,7 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
     const int lc = order[q];
     if (lc == LC_MISC && misc_done) continue;   // in the streaming path's composer launch
     const int nt = class_units(L, lc);
-    const hipStream_t st = stream_forked ? s : (nside > 0 && q % (nside + 1) != 0) ? h->side[q % (nside + 1) - 1] : s;
+    const hipStream_t st = stream_forked ? s : overlap ? h->side[q % nside] : (nside > 0 && q % (nside + 1) != 0) ? h->side[q % (nside + 1) - 1] : s;
     KParams P{};
     fill_common(h, P, B, X, ldx, G, ldg, V, ldv, want_g, want_jac, terrains, per_problem);
     P.ntiles = nt;
@@ -1136,11 +1144,15 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
   }
   {
     const char* ns = std::getenv("TOWR_GPU_STREAMS");
-    // Default with fixed phase durations: serial launches. Measured on MI355X (ANYmal, B = 4096): 1, 2, 4
-    // streams gave 0.524, 0.521, 0.550 ms per step — every kind already fills the CUs' LDS, so kinds
-    // cannot co-reside. Under phase-duration optimisation (streaming FDISC) two streams: the write-bound
-    // FDISC stream kernel runs beside the latency-bound Dynamic tiles.
-    const int want = ns ? std::atoi(ns) - 1 : (h->L.gait && (h->L.fstream || h->L.gstream[GS_TQ]) ? (h->L.gstream[GS_TQ] ? 2 : 1) : 0);
+    // Fixed phase durations with a fusion group: one side stream, on which the other classes (Dynamic, then the
+    // small kinds) run beside the fused launch (launch_classes; ANYmal, B = 4096, one box: 0.2450 vs 0.2514 ms
+    // per step serial; Dynamic and the small kinds on two side streams 0.2547, the small kinds after the fused
+    // launch 0.2500). Without a fusion group (RotVec): serial launches (1, 2, 4 streams in round 1: 0.524, 0.521,
+    // 0.550 ms; RotVec with the classes beside each other: no change). Under phase-duration optimisation (the
+    // streaming path) one or two side streams: the write-bound compose launches run beside the latency-bound
+    // record work (launch_stream_path).
+    const bool streamed = h->L.gait && (h->L.fstream || h->L.gstream[GS_TQ]);
+    const int want = ns ? std::atoi(ns) - 1 : streamed ? (h->L.gstream[GS_TQ] ? 2 : 1) : h->n_fuse > 0 ? 1 : 0;
     h->n_side = std::max(0, std::min(towr_gpu_handle_s::kMaxSide, want));
     if (h->n_side > 0 && hipEventCreateWithFlags(&h->fork, hipEventDisableTiming) != hipSuccess) { h->err = "hipEventCreate failed"; return bail(TOWR_ERR_HIP); }
     // side streams at the device's greatest priority: the streaming path runs its critical chains there (the
