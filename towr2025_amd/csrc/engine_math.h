@@ -1523,18 +1523,24 @@ TG_HD void eval_rom(const Ctx& c, const ItemDesc& it, Emit& em) {
   spline_eval(c, sp_motion(ee), t, P);
   double R[3][3];
   Trig q{};
-  if (c.rotvec) rv_rodrigues(A.p, R);
+  double th = 0.0;
+  RvCoeffs cf{};
+  if (c.rotvec) { th = rv_norm(A.p); cf = rv_coeffs(th); rv_rodrigues_c(A.p, th, cf, R); }
   else { q = trig(A.p); euler_R(q, R); }
   const double rW[3] = {P.p[0] - L.p[0], P.p[1] - L.p[1], P.p[2] - L.p[2]};
   double H[4];
   if (it.group == 1 && c.rotvec) {
-    // DerivOfRotVecMult(t, r_W, inverse = true) of the RotVecConverter: R^T [r_W]x J_L, full pattern
+    // DerivOfRotVecMult(t, r_W, inverse = true) of the RotVecConverter: R^T [r_W]x J_L, full pattern (the
+    // trigonometry shared with R; unrolled like the Euler branch below, so the slot-group loads are hoisted)
     double JL[3][3], Am[3][3];
-    rv_left_jac(A.p, JL);
+    rv_left_jac_c(A.p, th, cf, JL);
     rv_rotvec_mult(R, JL, rW, true, Am);
     spline_basis(A, kPos, H);
+#pragma unroll
     for (int e = 0; e < 3; ++e)
+#pragma unroll
       for (int r = 0; r < 3; ++r)
+#pragma unroll
         for (int bb = 0; bb < 4; ++bb) em(r0 + r, basis_col(c, SP_BASE_ANG, A.poly, bb, e), Am[r][e] * H[bb], true);
     return;
   }
