@@ -45,10 +45,20 @@ extern "C" int emu_eval_ex(const towr_problem_desc_t* d, int n_data, const towr_
   c.ter = &L.terrain; c.rb = L.rb; c.fdisc_motion = L.fdisc_motion;
   c.gait = L.gait; c.pinfo = L.pinfo.data(); c.pcols = L.pcols.data(); c.sched = L.sched.data();
   c.eelin = L.eelin.data(); c.lin = L.lin.data(); c.rotvec = L.rotvec;
+  // the small kinds see x as the kernel stages it (Layout::misc_xspan): every column outside the spans is NaN,
+  // so an item reading an unstaged column fails the comparison with the oracle
+  std::vector<double> xm;
+  if (!L.misc_xspan.empty()) {
+    xm.assign((size_t)L.n, std::nan(""));
+    for (size_t k = 0; k + 1 < L.misc_xspan.size(); k += 2)
+      for (int32_t u = L.misc_xspan[k]; u < L.misc_xspan[k] + L.misc_xspan[k + 1]; ++u)
+        for (int j = 2 * u; j < 2 * u + 2 && j < L.n; ++j) xm[(size_t)j] = x[j];
+  }
   for (const TileDesc& td : L.tiles)
     for (int l = td.i0; l < td.i1; ++l) {
       const ItemDesc& it = L.items[l];
       if (it.type == IT_NONE) continue;
+      c.x = is_misc_kind(it.type) && !xm.empty() ? xm.data() : x;
       AccEmit em{L.slot_groups.data() + it.slot, td.i1 - td.i0, v + td.v0, g, td.v1 - td.v0,
                  it.rsel > 0 ? it.row0 + rsel_first(it.rsel) : 0, it.rsel > 0 ? rsel_count(it.rsel) : 0,
                  L.idirect.empty() ? ItemDirect{} : L.idirect[l]};
@@ -56,6 +66,7 @@ extern "C" int emu_eval_ex(const towr_problem_desc_t* d, int n_data, const towr_
       eval_item(c, it, em);
       em.flush();
     }
+  c.x = x;
   if (L.fstream) {   // the kernel's streaming ForceConstraintDiscretized composition (fdisc_stream_body)
     c.pact = L.pact.data();
     for (const FsBlock& fb : L.fs_blocks) {
@@ -158,6 +169,18 @@ extern "C" int emu_stream_limits(const towr_problem_desc_t* d, int64_t* out) {
   for (const FsBlock& fb : L.fs_blocks) nv = std::max<int64_t>(nv, fb.nv);
   out[6] = nv;
   out[7] = L.fstream;
+  return 0;
+}
+
+// the small kinds' staged x (Layout::misc_xspan): out = {spans, 16-byte units staged, units of all of x}
+extern "C" int emu_misc_xspan(const towr_problem_desc_t* d, int64_t* out) {
+  Layout L; std::string e;
+  if (build_layout(*d, L, e)) return -1;
+  int64_t units = 0;
+  for (size_t k = 1; k < L.misc_xspan.size(); k += 2) units += L.misc_xspan[k];
+  out[0] = (int64_t)L.misc_xspan.size() / 2;
+  out[1] = units;
+  out[2] = (L.n + 1) / 2;
   return 0;
 }
 

@@ -50,6 +50,8 @@ struct KParams {
   int32_t want_g, want_jac, fdisc_motion;
   const int32_t* misc_tiles;      // merged small-kind launch: kMiscWaves tile ids per group
   const int32_t* misc_lds;        // per (group, wave): LDS offset, g-row offset
+  const int32_t* xspan;           // the small kinds' x spans (Layout::misc_xspan), n_xspan pairs; 0 = all of x
+  int32_t n_xspan;
   RobotC rb;
   const UnitDesc* units;          // fused launch: a problem's units (UnitDesc), n_units per problem
   int32_t n_units;
@@ -209,6 +211,27 @@ __device__ __forceinline__ void stage_x(const KParams& P, const double* xg, doub
   if (threadIdx.x == 0) xs[P.n] = 0.0;
   if constexpr (NODES)
     stage16<BLOCK>(reinterpret_cast<uint4*>(ns), reinterpret_cast<const uint4*>(P.nodecol), (P.n_nodecol + 3) >> 2);
+}
+
+// stage_x over the 16-byte spans of x in P.xspan (Layout::misc_xspan) when there are any: the small kinds read
+// only the base and foot-motion nodes, about half of x (with the zero slot and the node table)
+template <int BLOCK>
+__device__ __forceinline__ void stage_x_spans(const KParams& P, const double* xg, double* xs, int32_t* ns) {
+  if (P.n_xspan == 0 || (reinterpret_cast<uintptr_t>(xg) & 15) != 0) {
+    stage_x<BLOCK, true>(P, xg, xs, ns);
+    return;
+  }
+  for (int k = 0; k < P.n_xspan; ++k) {
+    const int a = P.xspan[2 * k], len = P.xspan[2 * k + 1];
+    if (2 * (a + len) <= P.n) {
+      stage16<BLOCK>(reinterpret_cast<uint4*>(xs) + a, reinterpret_cast<const uint4*>(xg) + a, len);
+    } else {   // the last unit of an odd n: its first double only
+      stage16<BLOCK>(reinterpret_cast<uint4*>(xs) + a, reinterpret_cast<const uint4*>(xg) + a, len - 1);
+      if (threadIdx.x == 0) xs[P.n - 1] = xg[P.n - 1];
+    }
+  }
+  if (threadIdx.x == 0) xs[P.n] = 0.0;
+  stage16<BLOCK>(reinterpret_cast<uint4*>(ns), reinterpret_cast<const uint4*>(P.nodecol), (P.n_nodecol + 3) >> 2);
 }
 
 // Prologue of the per-problem record kernel under phase-duration optimisation (gstream.hip): x (+ zero slot), the node table, the PhaseSpline tables and the terrain staged in LDS

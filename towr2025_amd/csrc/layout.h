@@ -202,6 +202,7 @@ struct Layout {
   // small kinds (is_misc_kind) run in one launch: kMiscWaves tiles per block, one per wave
   std::vector<int32_t> misc_tiles;   // groups of kMiscWaves tile indices (-1 = empty wave)
   std::vector<int32_t> misc_lds;     // per (group, wave): LDS offset of the wave's tile, its g-row offset (doubles)
+  std::vector<int32_t> misc_xspan;   // x spans the small-kind blocks stage: (first 16-B unit, units) pairs; empty = all of x
   int32_t misc_region = 0;           // LDS of the largest group (doubles)
   int64_t misc_bytes = 0;
   // streaming ForceConstraintDiscretized (FsBlock): enabled under phase-duration optimisation on

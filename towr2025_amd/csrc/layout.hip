@@ -883,6 +883,7 @@ towr_problem_desc_t soft_desc(const towr_problem_desc_t& d, const Layout& L) {
   return s;
 }
 
+void build_misc_xspan(Layout& L);
 int build_layout(const towr_problem_desc_t& d, Layout& L, std::string& err) { return build_layout_ex(d, 0, nullptr, L, err); }
 
 int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t* data, Layout& L, std::string& err) {
@@ -1541,8 +1542,54 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
       for (uint8_t u : used) nx += u;
       L.misc_bytes = 8 * (nv + nr + nx);
     }
+    build_misc_xspan(L);
   }
   return TOWR_OK;
+}
+
+// The 16-byte spans of x the small-kind launch stages (fixed phase durations): the node columns of every
+// spline its items read (eval_height / eval_swing: the foot's motion nodes; eval_bmot, base height: the base
+// nodes; eval_sacc: spline it.ee; eval_fnode: the foot's force and motion nodes), merged into runs of 16-byte
+// units. Empty (the whole x) when an item kind reads anything else, or under phase-duration optimisation.
+void build_misc_xspan(Layout& L) {
+  L.misc_xspan.clear();
+  if (L.gait || L.misc_tiles.empty()) return;
+  std::vector<uint8_t> need((size_t)(L.n + 1) / 2, 0);
+  bool all = false;
+  auto spline = [&](int s) {
+    if (s < 0 || s >= (int)L.spl.size()) { all = true; return; }
+    const SplineMeta& m = L.spl[(size_t)s];
+    for (int64_t k = (int64_t)m.node_off * 6; k < (int64_t)(m.node_off + m.n_polys + 1) * 6; ++k) {
+      if (k >= (int64_t)L.nodecol.size()) { all = true; return; }
+      const int32_t c = L.nodecol[(size_t)k];
+      if (c >= 0 && c < L.n) need[(size_t)c / 2] = 1;
+    }
+  };
+  for (int32_t ti : L.misc_tiles) {
+    if (ti < 0) continue;
+    const TileDesc& td = L.tiles[(size_t)ti];
+    for (int32_t i = td.i0; i < td.i1 && !all; ++i) {
+      const ItemDesc& it = L.items[(size_t)i];
+      switch (it.type) {
+        case IT_NONE: break;
+        case IT_TERR: case IT_SWING: spline(sp_motion(it.ee)); break;
+        case IT_BHGT: spline(SP_BASE_LIN); break;
+        case IT_BMOT: spline(SP_BASE_LIN); spline(SP_BASE_ANG); break;
+        case IT_SACC: spline(it.ee); break;
+        case IT_FNODE: spline(sp_force(it.ee)); spline(sp_motion(it.ee)); break;
+        default: all = true; break;
+      }
+    }
+    if (all) return;
+  }
+  for (size_t u = 0; u < need.size();) {
+    if (!need[u]) { ++u; continue; }
+    size_t v = u;
+    while (v < need.size() && need[v]) ++v;
+    L.misc_xspan.push_back((int32_t)u);
+    L.misc_xspan.push_back((int32_t)(v - u));
+    u = v;
+  }
 }
 
 int split_rows(int type, int group, bool gait) {

@@ -156,7 +156,8 @@ __device__ __forceinline__ void misc_body(const KParams& P, double* smem, int b,
   int32_t* ns = reinterpret_cast<int32_t*>(smem + lds_x_off + P.n_pad);
   if constexpr (GAIT)   // sparse PhaseSpline emission: each wave zero-fills its own tile
     if (ti >= 0) zero_lds(wl, T.v1 - T.v0, lane, 64);
-  stage_x<BLOCK, true>(P, P.X + (int64_t)b * P.ldx, xs, ns);
+  if constexpr (GAIT) stage_x<BLOCK, true>(P, P.X + (int64_t)b * P.ldx, xs, ns);
+  else stage_x_spans<BLOCK>(P, P.X + (int64_t)b * P.ldx, xs, ns);
   __syncthreads();
   if (it.type != IT_NONE) {
     Ctx c;

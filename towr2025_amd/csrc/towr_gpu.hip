@@ -56,6 +56,7 @@ struct towr_gpu_handle_s {
   SchedInfo* d_sched = nullptr;
   int32_t* d_misc = nullptr;
   int32_t* d_misc_lds = nullptr;
+  int32_t* d_xspan = nullptr;
   EELinDef* d_eelin = nullptr;
   LinNz* d_lin = nullptr;
   uint4* d_gtab = nullptr;     // GAIT: PhaseSpline tables blob (GaitTables)
@@ -366,6 +367,7 @@ void fill_common(towr_gpu_handle h, KParams& P, int B, const double* X, int64_t 
   P.want_g = want_g; P.want_jac = want_jac; P.fdisc_motion = L.fdisc_motion;
   P.rb = L.rb;
   P.misc_tiles = h->d_misc; P.misc_lds = h->d_misc_lds;
+  P.xspan = h->d_xspan; P.n_xspan = (int32_t)(L.misc_xspan.size() / 2);
   P.lds_scr_off = L.dyn_scr_off;
   P.rvc = h->d_rvc; P.rvi = h->d_rvi; P.n_rvi = (int32_t)L.rv_inst.size();
   const GaitTables gt = gait_tables(L);
@@ -1085,7 +1087,7 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
       (r = upload(h, &h->d_tiles, L.tiles)) || (r = upload(h, &h->d_nodecol, nodecol16)) ||
       (r = upload(h, &h->d_spl, L.spl)) || (r = upload(h, &h->d_dur, L.dur)) || (r = upload(h, &h->d_terrain, ter)) ||
       (r = upload(h, &h->d_pinfo, L.pinfo)) || (r = upload(h, &h->d_pcols, L.pcols)) || (r = upload(h, &h->d_pact, L.pact)) || (r = upload(h, &h->d_sched, L.sched)) ||
-      (r = upload(h, &h->d_misc, L.misc_tiles)) || (r = upload(h, &h->d_misc_lds, L.misc_lds)) || (r = upload(h, &h->d_eelin, L.eelin)) ||
+      (r = upload(h, &h->d_misc, L.misc_tiles)) || (r = upload(h, &h->d_misc_lds, L.misc_lds)) || (r = upload(h, &h->d_xspan, L.misc_xspan)) || (r = upload(h, &h->d_eelin, L.eelin)) ||
       (r = upload(h, &h->d_lin, L.lin)) ||
       (r = upload(h, &h->d_citems, L.cost_items)) || (r = upload(h, &h->d_cq, L.cost_q)) || (r = upload(h, &h->d_gtab, gait_blob(L))) ||
       (r = upload(h, &h->d_idir, L.idirect)) || (r = upload(h, &h->d_fsb, L.fs_blocks)) || (r = upload(h, &h->d_fs_t, L.fs_t)) ||
@@ -1219,7 +1221,7 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
 int towr_gpu_destroy(towr_gpu_handle h) {
   if (!h) return TOWR_OK;
   void* dev[] = {h->d_items, h->d_slots, h->d_tiles, h->d_nodecol, h->d_spl, h->d_dur, h->d_segs, h->d_terrain,
-                 h->d_pinfo, h->d_pcols, h->d_pact, h->d_sched, h->d_misc, h->d_misc_lds, h->d_eelin, h->d_gtab, h->d_idir, h->d_citems, h->d_cq, h->fuse[0].d_units, h->fuse[1].d_units,
+                 h->d_pinfo, h->d_pcols, h->d_pact, h->d_sched, h->d_misc, h->d_misc_lds, h->d_xspan, h->d_eelin, h->d_gtab, h->d_idir, h->d_citems, h->d_cq, h->fuse[0].d_units, h->fuse[1].d_units,
                  h->d_bterrain, h->d_x, h->d_g, h->d_v, h->d_f, h->d_grad,
                  h->d_traj_pd, h->d_traj_n, h->d_traj_c0, h->d_traj_t, h->d_fsb, h->d_fs_t, h->d_fs_tmpl, h->d_fs_ws,
                  h->d_fs_iee, h->d_fs_irow, h->d_fs_iblk, h->d_fsrec, h->d_lin, h->d_soft_b, h->d_soft_rp, h->d_soft_col, h->d_sg, h->d_sv,
