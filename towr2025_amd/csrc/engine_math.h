@@ -961,9 +961,11 @@ TG_HD void rv_rotvec_mult_col(const double R[3][3], const double JL[3][3], const
 // GetAngularAccelerationInWorld, :118-138)
 TG_HD void rv_state(const SplinePt& A, double R[3][3], double w[3], double wd[3]) {
   double JL[3][3], JLd[3][3], a[3], b[3];
-  rv_rodrigues(A.p, R);
-  rv_left_jac(A.p, JL);
-  rv_left_jac_dot(A.p, A.v, JLd);
+  const double theta = rv_norm(A.p);
+  const RvCoeffs cf = rv_coeffs(theta);   // the trigonometry once for the three converter quantities
+  rv_rodrigues_c(A.p, theta, cf, R);
+  rv_left_jac_c(A.p, theta, cf, JL);
+  rv_left_jac_dot_c(A.p, A.v, theta, cf, JLd);
   mat3_vec(JL, A.v, w);
   mat3_vec(JLd, A.v, a); mat3_vec(JL, A.a, b);
   for (int k = 0; k < 3; ++k) wd[k] = a[k] + b[k];
@@ -1134,28 +1136,39 @@ TG_HD double dot3(const double a[3], const double b[3]) { return a[0] * b[0] + a
 struct DynG0 { double ab[3], La[3], Lp[3], Hp[4], Ha[4]; int poly; };
 constexpr int kDynG0PhaseA = 12;   // candidates of dyn_g0_a (base-linear acceleration block)
 constexpr int kDynG0Cand = 36;     // + dyn_g0_b's 24 (the base-linear block of the angular rows)
-template <class Emit>
-TG_HD void dyn_g0_a(const Ctx& c, const ItemDesc& it, Emit& em, DynG0& st) {
-  const double t = it.t;
-  const int r0 = it.row0;
-  SplinePt L; spline_eval(c, SP_BASE_LIN, t, L);
-  SplinePt A; spline_eval(c, SP_BASE_ANG, t, A);
-  double R[3][3], w[3], wd[3];
-  if (c.rotvec) rv_state(A, R, w, wd);
-  else {
-    const Trig q = trig(A.p);
-    euler_R(q, R);
-    euler_w_wd(q, A.v, A.a, w, wd);
-  }
-  // I_w = R I_b R^T
+// I_w wd + w x (I_w w), I_w = R I_b R^T (the angular rows' base terms)
+TG_HD void dyn_base_ab(const RobotC& rb, const double R[3][3], const double w[3], const double wd[3], double ab[3]) {
   double RI[3][3], Iw[3][3];
   for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) RI[i][j] = R[i][0] * c.rb.Ib[0 * 3 + j] + R[i][1] * c.rb.Ib[1 * 3 + j] + R[i][2] * c.rb.Ib[2 * 3 + j];
+    for (int j = 0; j < 3; ++j) RI[i][j] = R[i][0] * rb.Ib[0 * 3 + j] + R[i][1] * rb.Ib[1 * 3 + j] + R[i][2] * rb.Ib[2 * 3 + j];
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) Iw[i][j] = RI[i][0] * R[j][0] + RI[i][1] * R[j][1] + RI[i][2] * R[j][2];
   double a[3], Iww[3], b[3];
   mat3_vec(Iw, wd, a); mat3_vec(Iw, w, Iww); cross3(w, Iww, b);
-  for (int e = 0; e < 3; ++e) { st.ab[e] = a[e] + b[e]; st.La[e] = L.a[e]; st.Lp[e] = L.p[e]; }
+  for (int e = 0; e < 3; ++e) ab[e] = a[e] + b[e];
+}
+// PRE (fixed gait, RotVec, device): the base terms ab come from the coefficient pre-pass (tiles.hip
+// towr_rv_coef_kernel, fields kRvAb.. of the instant it.a0, field stride `stride`), so the lane forms no
+// converter state
+template <bool PRE = false, class Emit>
+TG_HD void dyn_g0_a(const Ctx& c, const ItemDesc& it, Emit& em, DynG0& st, const double* pre = nullptr, int64_t stride = 0) {
+  const double t = it.t;
+  const int r0 = it.row0;
+  SplinePt L; spline_eval(c, SP_BASE_LIN, t, L);
+  if constexpr (PRE) {
+    for (int e = 0; e < 3; ++e) st.ab[e] = pre[e * stride];
+  } else {
+    SplinePt A; spline_eval(c, SP_BASE_ANG, t, A);
+    double R[3][3], w[3], wd[3];
+    if (c.rotvec) rv_state(A, R, w, wd);
+    else {
+      const Trig q = trig(A.p);
+      euler_R(q, R);
+      euler_w_wd(q, A.v, A.a, w, wd);
+    }
+    dyn_base_ab(c.rb, R, w, wd, st.ab);
+  }
+  for (int e = 0; e < 3; ++e) { st.La[e] = L.a[e]; st.Lp[e] = L.p[e]; }
   st.poly = L.poly;
   spline_basis(L, kPos, st.Hp); spline_basis(L, kAcc, st.Ha);
   for (int e = 0; e < 3; ++e)

@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <unordered_map>
 
 namespace tg {
 namespace {
@@ -1207,6 +1208,17 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
       }
       it.a0 = (int32_t)L.rv_inst.size() - 1;
     }
+  if (!L.rv_inst.empty()) {   // the group-0 lane of each instant: the same index (its base terms, kRvAb)
+    std::unordered_map<int32_t, int32_t> at;   // first row of the instant -> pre-pass instant
+    for (const ItemDesc& it : L.items)
+      if (it.type == IT_DYN && it.group == 1 && it.a1 > 0) at[it.row0] = it.a0;
+    for (ItemDesc& it : L.items)
+      if (it.type == IT_DYN && it.group == 0) {
+        const auto f = at.find(it.row0);
+        if (f == at.end()) { err = "internal: a RotVec Dynamic instant without pre-pass coefficients"; return TOWR_ERR_INVALID; }
+        it.a0 = f->second;
+      }
+  }
 
   // ---- cost terms (their sample times append rows to the segment table)
   if (int rc = build_costs(d, base_d, L, err)) return rc;

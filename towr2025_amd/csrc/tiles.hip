@@ -191,7 +191,10 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
   constexpr bool kRvPre = TYPE == IT_DYN && ROTVEC && !GAIT;
   if (it.type == TYPE) {
     if constexpr (TYPE == IT_DYN) {
-      if (it.group == 0) dyn_g0_a(c, it, em, g0);
+      if (it.group == 0) {
+        if constexpr (kRvPre) dyn_g0_a<true>(c, it, em, g0, P.rvc + (int64_t)kRvAb * P.B * P.n_rvi + (int64_t)b * P.n_rvi + it.a0, (int64_t)P.B * P.n_rvi);
+        else dyn_g0_a(c, it, em, g0);
+      }
       else if (kRvPre && it.group == 1) {
         if (P.want_jac) dyn_rv_emit_pre(c, it, P.rvc + (int64_t)b * P.n_rvi + it.a0, (int64_t)P.B * P.n_rvi, em);
       }
@@ -286,7 +289,7 @@ __global__ void __launch_bounds__(KBLOCK, (KBLOCK == 256 ? 2 : 1)) towr_step_ker
   }
 }
 
-// The base-angular coefficients of the fixed-gait RotVec Dynamic block (dyn_rv_state + dyn_rv_column<e>,
+// The base-angular coefficients (and the base terms ab of the angular rows) of the fixed-gait RotVec Dynamic block (dyn_rv_state + dyn_rv_column<e>,
 // rotvec_converter.cc:148-561 through dynamic_constraint.cc:124-166) for every (problem, instant, component),
 // before the Dynamic launch. In the tile, one lane per instant formed the converter state and three lanes its
 // columns after a barrier: the block's life was that chain at 2 waves per SIMD (242 VGPRs). Here one lane per
@@ -310,6 +313,14 @@ __global__ void __launch_bounds__(kRvCoefBlock) towr_rv_coef_kernel(KParams P) {
   c.rb = P.rb; c.gait = false; c.rotvec = true;
   DynRvState S;
   dyn_rv_state(c, ri.t, S);
+  if (e == 0) {   // the instant's base terms for its group-0 lane (also without the Jacobian: the g rows need them)
+    double ab[3];
+    dyn_base_ab(c.rb, S.R, S.w, S.wd, ab);
+    double* o = P.rvc + (int64_t)kRvAb * pairs + pr;
+#pragma unroll
+    for (int f = 0; f < 3; ++f) __builtin_nontemporal_store(ab[f], o + f * pairs);
+  }
+  if (!P.want_jac) return;
   double M[9];
   if (e == 0) dyn_rv_column<0>(S, M, M + 3, M + 6);
   else if (e == 1) dyn_rv_column<1>(S, M, M + 3, M + 6);

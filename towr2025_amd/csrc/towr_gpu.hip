@@ -386,16 +386,17 @@ void fill_common(towr_gpu_handle h, KParams& P, int B, const double* X, int64_t 
 
 // Fixed gait, RotVec: the pre-pass of the Dynamic base-angular coefficients (tiles.hip towr_rv_coef_kernel)
 // into the handle's scratch, on the stream of the Dynamic launch that follows it (every launch holding the
-// Dynamic class: its tile kernel, a fusion group, the single-problem group). Only with the Jacobian.
+// Dynamic class: its tile kernel, a fusion group, the single-problem group). Without the Jacobian only the
+// base terms of the g rows (kRvAb).
 int launch_rv_prepass(towr_gpu_handle h, int B, const double* X, int64_t ldx, int want_jac, hipStream_t s) {
   const Layout& L = h->L;
   const int64_t K = (int64_t)L.rv_inst.size();
-  if (K == 0 || !want_jac || B <= 0) return TOWR_OK;
+  if (K == 0 || B <= 0) return TOWR_OK;
   if (int rc = scratch_grow(h, &h->d_rvc, &h->rvc_cap, B, kRvCoef * K)) return rc;
   KParams P{};
   P.X = X; P.ldx = ldx; P.B = B;
   P.nodecol = h->d_nodecol; P.spl = h->d_spl; P.dur = h->d_dur; P.sg = h->sg; P.terrains = h->d_terrain;
-  P.rb = L.rb; P.rvc = h->d_rvc; P.rvi = h->d_rvi; P.n_rvi = (int32_t)K;
+  P.rb = L.rb; P.rvc = h->d_rvc; P.rvi = h->d_rvi; P.n_rvi = (int32_t)K; P.want_jac = want_jac;
   const int64_t waves = 3 * (((int64_t)B * K + 63) / 64), grid = (waves + kRvCoefBlock / 64 - 1) / (kRvCoefBlock / 64);
   if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
   void* args[] = {&P};
