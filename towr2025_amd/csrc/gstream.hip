@@ -65,9 +65,8 @@ __device__ __forceinline__ void fdisc_record(const KParams& P, const Ctx& c, int
   double h0 = o.H[0], h1 = o.H[1], h2 = o.H[2], h3 = o.H[3];
   asm volatile("" : "+v"(h0), "+v"(h1), "+v"(h2), "+v"(h3));
   const int32_t* tm = P.fs_tmpl + fb.tmpl;
-#pragma unroll
-  for (int q = 0; q < kFsWin; ++q) {   // the window's basis sums (schedule entries: never read, 0); unrolled: the
-                                       // template loads of the whole window issue together
+#pragma unroll 4
+  for (int q = 0; q < kFsWin; ++q) {   // the window's basis sums (schedule entries: never read, 0)
     const int pos = ws + q;
     const int32_t te = pos < fb.L ? tm[pos] : -1;
     put(q, te >= 0 ? phase_basis_sum(c.pcols[te & 0xFFFFFF], poly, h0, h1, h2, h3) : 0.0);
