@@ -493,3 +493,36 @@ def test_host_batch_chunks_and_registered_buffers():
     r, c, v_ref = o.eval_jac(xs[2])
     assert_close(o.eval_g(xs[2]), g, r, v_ref, v, o.m, "registered single call")
     q.close()   # destroy unregisters
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["anymal_trot_2p4s", "anymal_trot_rotvec"])
+def test_batch_device_g_or_jac_only(name):
+    """g alone and the Jacobian alone over a batch of 80 (B >= 64: Dynamic and the small kinds beside the fused
+    launch for the Euler layout; for RotVec the coefficient pre-pass runs without the Jacobian too, for the base
+    terms the g rows need): each equals the full call's output bit for bit and leaves the other output untouched."""
+    import torch
+    desc = CONFIGS[name]
+    o = Oracle(desc)
+    p = TowrGpuProblem(desc)
+    B = 80
+    X = np.stack([_perturb(o.initial_x(), 900 + b) for b in range(B)])
+    ldv = (p.nnz + 15) // 16 * 16
+    dev = torch.device("cuda:0")
+    Xd = torch.from_numpy(X).to(dev)
+
+    def run(want_g, want_jac):
+        Gd = torch.full((B, p.m), np.nan, dtype=torch.float64, device=dev)
+        Vd = torch.full((B, ldv), np.nan, dtype=torch.float64, device=dev)
+        p.eval_batch_device(Xd, Gd, Vd, want_g=want_g, want_jac=want_jac)
+        torch.cuda.synchronize()
+        return Gd.cpu().numpy(), Vd.cpu().numpy()[:, :p.nnz]
+
+    G, V = run(True, True)
+    for b in (0, B - 1):
+        r, _, v_ref = o.eval_jac(X[b])
+        assert_close(o.eval_g(X[b]), G[b], r, v_ref, V[b], o.m, f"{name} full batch {b}")
+    Gg, Vg = run(True, False)
+    assert np.array_equal(Gg, G) and np.isnan(Vg).all()
+    Gj, Vj = run(False, True)
+    assert np.array_equal(Vj, V) and np.isnan(Gj).all()
