@@ -40,8 +40,8 @@ struct TileEmitPre {   // four groups: candidates J0 - J0 % 8 .. + 31
       q2 = s[((J0 >> 3) + 2) * BLOCK]; q3 = s[((J0 >> 3) + 3) * BLOCK];
     }
   }
-  __device__ __forceinline__ void g(int row, double v) {
-    if (!DIRECT || gon) gout[row] = v;
+  __device__ __forceinline__ void g(int row, double v) {   // gon: g requested (LDS rows: always on)
+    if (gon) gout[row] = v;
   }
   __device__ __forceinline__ void operator()(int, int, double v, bool) {
     const int k = (j >> 3) - (J0 >> 3);
