@@ -1525,58 +1525,28 @@ TG_HD void eval_dyn(const Ctx& c, const ItemDesc& it, Emit& em) {
 }
 
 
-constexpr int kRvRom = 18;   // per RangeOfMotion instant of the RotVec pre-pass: R (9, row-major) | J_L (9)
-// The RotVec base orientation of a RangeOfMotion instant in the pre-pass's form (tiles.hip towr_rv_coef_kernel):
-// R then J_L, row-major, kRvRom doubles, with the expressions eval_rom uses
-TG_HD void rom_rv_pre(const Ctx& c, double t, double out[kRvRom]) {
-  SplinePt A;
-  spline_eval(c, SP_BASE_ANG, t, A);
-  const double th = rv_norm(A.p);
-  const RvCoeffs cf = rv_coeffs(th);
-  double R[3][3], JL[3][3];
-  rv_rodrigues_c(A.p, th, cf, R);
-  rv_left_jac_c(A.p, th, cf, JL);
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) { out[3 * i + j] = R[i][j]; out[9 + 3 * i + j] = JL[i][j]; }
-}
-
-// RangeOfMotionConstraint instant (range_of_motion_constraint.cc:72-131). PRE (fixed gait, RotVec, device): R and
-// J_L come from the pre-pass (rom_rv_pre, field f at pre[f stride]) instead of the lane's own converter chain.
-template <bool PRE = false, class Emit>
-TG_HD void eval_rom(const Ctx& c, const ItemDesc& it, Emit& em, const double* pre = nullptr, int64_t stride = 0) {
+// RangeOfMotionConstraint instant (range_of_motion_constraint.cc:72-131)
+template <class Emit>
+TG_HD void eval_rom(const Ctx& c, const ItemDesc& it, Emit& em) {
   const double t = it.t;
   const int r0 = it.row0, ee = it.ee;
   SplinePt L, A, P;
   spline_eval(c, SP_BASE_LIN, t, L);
-  if (!PRE || it.group == 1) spline_eval(c, SP_BASE_ANG, t, A);   // (PRE: only the base-angular lanes' basis)
+  spline_eval(c, SP_BASE_ANG, t, A);
   spline_eval(c, sp_motion(ee), t, P);
   double R[3][3];
   Trig q{};
   double th = 0.0;
   RvCoeffs cf{};
-  if constexpr (PRE) {
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) R[i][j] = pre[(3 * i + j) * stride];
-  } else {
-    if (c.rotvec) { th = rv_norm(A.p); cf = rv_coeffs(th); rv_rodrigues_c(A.p, th, cf, R); }
-    else { q = trig(A.p); euler_R(q, R); }
-  }
+  if (c.rotvec) { th = rv_norm(A.p); cf = rv_coeffs(th); rv_rodrigues_c(A.p, th, cf, R); }
+  else { q = trig(A.p); euler_R(q, R); }
   const double rW[3] = {P.p[0] - L.p[0], P.p[1] - L.p[1], P.p[2] - L.p[2]};
   double H[4];
-  if (it.group == 1 && (PRE || c.rotvec)) {
+  if (it.group == 1 && c.rotvec) {
     // DerivOfRotVecMult(t, r_W, inverse = true) of the RotVecConverter: R^T [r_W]x J_L, full pattern (the
     // trigonometry shared with R; unrolled like the Euler branch below, so the slot-group loads are hoisted)
     double JL[3][3], Am[3][3];
-    if constexpr (PRE) {
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) JL[i][j] = pre[(9 + 3 * i + j) * stride];
-    } else {
-      rv_left_jac_c(A.p, th, cf, JL);
-    }
+    rv_left_jac_c(A.p, th, cf, JL);
     rv_rotvec_mult(R, JL, rW, true, Am);
     spline_basis(A, kPos, H);
 #pragma unroll

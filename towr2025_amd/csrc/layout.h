@@ -150,7 +150,7 @@ struct WatchItem {
 };
 
 // a Dynamic instant of the RotVec coefficient pre-pass (fixed gait): its time and segment-table row
-struct RvInst { double t; int32_t seg, kind; };   // kind 0: a Dynamic instant, 1: a RangeOfMotion instant (kRvRom fields)
+struct RvInst { double t; int32_t seg, reserved; };
 constexpr int kRvCoef = 30;   // per instant: per component e, Mp[3] | Mv[3] | Ma[3] (dyn_rv_column); then the base terms ab[3]
 constexpr int kRvAb = 27;     // (dyn_base_ab, read by the instant's group-0 lane)
 

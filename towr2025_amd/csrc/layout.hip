@@ -1208,21 +1208,6 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
       }
       it.a0 = (int32_t)L.rv_inst.size() - 1;
     }
-  if (L.rotvec && !L.gait) {   // the RangeOfMotion instants (R and J_L, kRvRom), one per sample time
-    std::map<double, int32_t> at;
-    for (ItemDesc& it : L.items) {
-      if (it.type != IT_ROM) continue;
-      auto f = at.find(it.t);
-      if (f == at.end()) {
-        for (int bb = 0; bb < 4; ++bb)
-          for (int e = 0; e < 3; ++e)
-            if (L.segs[(size_t)it.seg * L.spl.size() + SP_BASE_ANG].col[bb][e] >= L.n) { err = "internal: constant base-angular node value"; return TOWR_ERR_INVALID; }
-        f = at.emplace(it.t, (int32_t)L.rv_inst.size()).first;
-        L.rv_inst.push_back(RvInst{it.t, it.seg, 1});
-      }
-      it.a0 = f->second;
-    }
-  }
   if (!L.rv_inst.empty()) {   // the group-0 lane of each instant: the same index (its base terms, kRvAb)
     std::unordered_map<int32_t, int32_t> at;   // first row of the instant -> pre-pass instant
     for (const ItemDesc& it : L.items)

@@ -199,8 +199,6 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
         if (P.want_jac) dyn_rv_emit_pre(c, it, P.rvc + (int64_t)b * P.n_rvi + it.a0, (int64_t)P.B * P.n_rvi, em);
       }
       else eval_dyn(c, it, em);   // group 1 and the endeffector groups (these deposit their sum terms)
-    } else if constexpr (TYPE == IT_ROM && ROTVEC && !GAIT) {   // R and J_L from the pre-pass
-      eval_rom<true>(c, it, em, P.rvc + (int64_t)b * P.n_rvi + it.a0, (int64_t)P.B * P.n_rvi);
     } else {
       eval_typed<TYPE>(c, it, em);
     }
@@ -313,15 +311,6 @@ __global__ void __launch_bounds__(kRvCoefBlock) towr_rv_coef_kernel(KParams P) {
   c.x = P.X + (int64_t)b * P.ldx;   // base-angular node values only: never a constant node (layout.hip checks)
   c.nodecol = P.nodecol; c.spl = P.spl; c.dur = P.dur; c.ter = P.terrains;
   c.rb = P.rb; c.gait = false; c.rotvec = true;
-  if (ri.kind == 1) {   // a RangeOfMotion instant: R and J_L (also without the Jacobian: the g rows need R)
-    if (e != 0) return;
-    double o[kRvRom];
-    rom_rv_pre(c, ri.t, o);
-    double* d = P.rvc + pr;
-#pragma unroll
-    for (int f = 0; f < kRvRom; ++f) __builtin_nontemporal_store(o[f], d + f * pairs);
-    return;
-  }
   DynRvState S;
   dyn_rv_state(c, ri.t, S);
   if (e == 0) {   // the instant's base terms for its group-0 lane (also without the Jacobian: the g rows need them)

@@ -384,9 +384,9 @@ void fill_common(towr_gpu_handle h, KParams& P, int B, const double* X, int64_t 
   P.gs_segs = h->d_gs_segs; P.gs_tseg = h->d_gs_tseg; P.gs_vmap = h->d_gs_vmap; P.gs_ws = h->d_gs_ws; P.gs_blob = h->d_gs_blob;
 }
 
-// Fixed gait, RotVec: the pre-pass of the Dynamic base-angular coefficients and base terms and of the
-// RangeOfMotion instants' R and J_L (tiles.hip towr_rv_coef_kernel) into the handle's scratch, on the caller's
-// stream before the launches that read it (launch_classes, before any fork; the single-problem group). Without the Jacobian only the
+// Fixed gait, RotVec: the pre-pass of the Dynamic base-angular coefficients (tiles.hip towr_rv_coef_kernel)
+// into the handle's scratch, on the stream of the Dynamic launch that follows it (every launch holding the
+// Dynamic class: its tile kernel, a fusion group, the single-problem group). Without the Jacobian only the
 // base terms of the g rows (kRvAb).
 int launch_rv_prepass(towr_gpu_handle h, int B, const double* X, int64_t ldx, int want_jac, hipStream_t s) {
   const Layout& L = h->L;
@@ -404,13 +404,11 @@ int launch_rv_prepass(towr_gpu_handle h, int B, const double* X, int64_t ldx, in
   return TOWR_OK;
 }
 
-// prepass: launch the RotVec pre-pass first when the group holds Dynamic or RangeOfMotion (launch_classes runs it
-// once for all its launches and passes false)
 int launch_fused(towr_gpu_handle h, const towr_gpu_handle_s::FuseGroup& fg, int B, const double* X, int64_t ldx, double* G,
                  int64_t ldg, double* V, int64_t ldv, int want_g, int want_jac, hipStream_t s,
-                 const towr_terrain_t* terrains, int per_problem, bool prepass = true) {
+                 const towr_terrain_t* terrains, int per_problem) {
   const Layout& L = h->L;
-  if (prepass && (fg.mask & ((1u << LC_DYN) | (1u << LC_ROM))))
+  if ((fg.mask >> LC_DYN) & 1)
     if (int rc = launch_rv_prepass(h, B, X, ldx, want_jac, s)) return rc;
   KParams P{};
   fill_common(h, P, B, X, ldx, G, ldg, V, ldv, want_g, want_jac, terrains, per_problem);
@@ -607,9 +605,6 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
                    int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem, int only_class) {
   const Layout& L = h->L;
   uint32_t fused_mask = 0;
-  // fixed gait, RotVec: the pre-pass before every launch (and before any fork) when Dynamic or RangeOfMotion runs
-  if (only_class < 0 || only_class == LC_DYN || only_class == LC_ROM)
-    if (int rc = launch_rv_prepass(h, B, X, ldx, want_jac, s)) return rc;
   // a batch with fusion groups: the other classes on the side streams beside the fused launches (forked before
   // them: the fused launch on the caller's stream, Dynamic then the small kinds on side stream 0); at small B the
   // fork and join cost more than the overlap gains
@@ -620,7 +615,7 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
   }
   if (only_class < 0)
     for (int g = 0; g < h->n_fuse; ++g) {
-      if (int rc = launch_fused(h, h->fuse[g], B, X, ldx, G, ldg, V, ldv, want_g, want_jac, s, terrains, per_problem, false)) return rc;
+      if (int rc = launch_fused(h, h->fuse[g], B, X, ldx, G, ldg, V, ldv, want_g, want_jac, s, terrains, per_problem)) return rc;
       fused_mask |= h->fuse[g].mask;
     }
   // The launch classes are independent (disjoint rows and CSR ranges): they may run on the handle's side
@@ -670,6 +665,10 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
     const int64_t total = (int64_t)B * nt;
     const int64_t grid = ((total + 7) / 8) * 8;
     if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
+    if (lc == LC_DYN) {
+      if (int rc = launch_rv_prepass(h, B, X, ldx, want_jac, st)) return rc;
+      P.rvc = h->d_rvc;   // (grown by the pre-pass)
+    }
     const int block = class_block(L, lc);
     void* args[] = {&P};
     HIPCHK(h, hipLaunchKernel(kernel_for_class(lc, L.gait, L.rotvec), dim3((unsigned)grid), dim3((unsigned)block), args,
