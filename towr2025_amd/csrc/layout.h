@@ -153,6 +153,10 @@ struct WatchItem {
 struct RvInst { double t; int32_t seg, reserved; };
 constexpr int kRvCoef = 30;   // per instant: per component e, Mp[3] | Mv[3] | Ma[3] (dyn_rv_column); then the base terms ab[3]
 constexpr int kRvAb = 27;     // (dyn_base_ab, read by the instant's group-0 lane)
+// Scratch layout of the pre-pass: blocks of 64 (problem, instant) pairs pr = b K + q, field-major inside a block, so
+// a wave's store of one field is 512 contiguous bytes and the kRvCoef fields of one pair sit in one 15 kB block
+// (field-major over the whole batch put them 1.8 MB apart at B = 4096); field f of pair pr at rv_at(pr) + 64 f
+__host__ __device__ constexpr int64_t rv_at(int64_t pr) { return (pr >> 6) * (int64_t)kRvCoef * 64 + (pr & 63); }
 
 struct VarSetInfo { int kind, ee, col0, n; };
 struct ConsInfo { int kind, ee, row0, rows; };

@@ -192,11 +192,11 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
   if (it.type == TYPE) {
     if constexpr (TYPE == IT_DYN) {
       if (it.group == 0) {
-        if constexpr (kRvPre) dyn_g0_a<true>(c, it, em, g0, P.rvc + (int64_t)kRvAb * P.B * P.n_rvi + (int64_t)b * P.n_rvi + it.a0, (int64_t)P.B * P.n_rvi);
+        if constexpr (kRvPre) dyn_g0_a<true>(c, it, em, g0, P.rvc + rv_at((int64_t)b * P.n_rvi + it.a0) + 64 * kRvAb, 64);
         else dyn_g0_a(c, it, em, g0);
       }
       else if (kRvPre && it.group == 1) {
-        if (P.want_jac) dyn_rv_emit_pre(c, it, P.rvc + (int64_t)b * P.n_rvi + it.a0, (int64_t)P.B * P.n_rvi, em);
+        if (P.want_jac) dyn_rv_emit_pre(c, it, P.rvc + rv_at((int64_t)b * P.n_rvi + it.a0), 64, em);
       }
       else eval_dyn(c, it, em);   // group 1 and the endeffector groups (these deposit their sum terms)
     } else {
@@ -294,8 +294,8 @@ __global__ void __launch_bounds__(KBLOCK, (KBLOCK == 256 ? 2 : 1)) towr_step_ker
 // before the Dynamic launch. In the tile, one lane per instant formed the converter state and three lanes its
 // columns after a barrier: the block's life was that chain at 2 waves per SIMD (242 VGPRs). Here one lane per
 // (problem, instant, component) at full occupancy; waves are component-uniform (wave w: component w % 3, 64
-// consecutive (problem, instant) pairs), and the coefficients are stored field-major (field f of component
-// e at (9 e + f) B K + b K + q), so both this kernel's stores and the tile's loads coalesce.
+// consecutive (problem, instant) pairs), and the coefficients are stored in blocks of 64 pairs, field-major in a
+// block (layout.h rv_at), so both this kernel's stores and the tile's loads coalesce.
 __global__ void __launch_bounds__(kRvCoefBlock) towr_rv_coef_kernel(KParams P) {
   const int K = P.n_rvi;
   const int64_t pairs = (int64_t)P.B * K, chunks = (pairs + 63) / 64;
@@ -316,18 +316,18 @@ __global__ void __launch_bounds__(kRvCoefBlock) towr_rv_coef_kernel(KParams P) {
   if (e == 0) {   // the instant's base terms for its group-0 lane (also without the Jacobian: the g rows need them)
     double ab[3];
     dyn_base_ab(c.rb, S.R, S.w, S.wd, ab);
-    double* o = P.rvc + (int64_t)kRvAb * pairs + pr;
+    double* o = P.rvc + rv_at(pr) + 64 * kRvAb;
 #pragma unroll
-    for (int f = 0; f < 3; ++f) __builtin_nontemporal_store(ab[f], o + f * pairs);
+    for (int f = 0; f < 3; ++f) __builtin_nontemporal_store(ab[f], o + 64 * f);
   }
   if (!P.want_jac) return;
   double M[9];
   if (e == 0) dyn_rv_column<0>(S, M, M + 3, M + 6);
   else if (e == 1) dyn_rv_column<1>(S, M, M + 3, M + 6);
   else dyn_rv_column<2>(S, M, M + 3, M + 6);
-  double* o = P.rvc + (int64_t)9 * e * pairs + pr;
+  double* o = P.rvc + rv_at(pr) + 64 * 9 * e;
 #pragma unroll
-  for (int f = 0; f < 9; ++f) __builtin_nontemporal_store(M[f], o + f * pairs);
+  for (int f = 0; f < 9; ++f) __builtin_nontemporal_store(M[f], o + 64 * f);
 }
 
 template <bool GAIT, bool ROTVEC>

@@ -392,7 +392,7 @@ int launch_rv_prepass(towr_gpu_handle h, int B, const double* X, int64_t ldx, in
   const Layout& L = h->L;
   const int64_t K = (int64_t)L.rv_inst.size();
   if (K == 0 || B <= 0) return TOWR_OK;
-  if (int rc = scratch_grow(h, &h->d_rvc, &h->rvc_cap, B, kRvCoef * K)) return rc;
+  if (int rc = scratch_grow(h, &h->d_rvc, &h->rvc_cap, B + 64, kRvCoef * K)) return rc;   // whole 64-pair blocks (rv_at)
   KParams P{};
   P.X = X; P.ldx = ldx; P.B = B;
   P.nodecol = h->d_nodecol; P.spl = h->d_spl; P.dur = h->d_dur; P.sg = h->sg; P.terrains = h->d_terrain;
