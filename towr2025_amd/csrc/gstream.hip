@@ -365,6 +365,8 @@ __global__ void __launch_bounds__(kGsRecMaxBlock) __attribute__((amdgpu_waves_pe
   rec_body<ROTVEC, ROLES>(P, A, smem);
 }
 template <int ROLES>   // FDISC and / or TQDISC records only
+// (5 or 6 waves per SIMD: 96 / 80 VGPRs with 48 / 120 bytes of spill, gait step 0.645-0.651 / 0.665-0.667 vs
+// 0.630-0.631 ms; with Torque 1.24 / 1.30-1.31 vs 1.21)
 __global__ void __launch_bounds__(kGsRecMaxBlock) __attribute__((amdgpu_waves_per_eu(4))) towr_gait_frec_kernel(KParams P, RecArgs A) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   rec_body<false, ROLES>(P, A, smem);
