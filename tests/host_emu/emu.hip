@@ -188,6 +188,8 @@ extern "C" int emu_misc_xspan(const towr_problem_desc_t* d, int64_t* out) {
 extern "C" int emu_stats(const towr_problem_desc_t* d) {
   Layout L; std::string e;
   if (build_layout(*d, L, e)) return -1;
+  std::printf("fs tables: fs_t %zu fs_tmpl %zu fs_ws %zu fs_blocks %zu (bytes %zu)\n", L.fs_t.size(), L.fs_tmpl.size(), L.fs_ws.size(),
+              L.fs_blocks.size(), 8 * L.fs_t.size() + 4 * L.fs_tmpl.size() + 4 * L.fs_ws.size() + sizeof(FsBlock) * L.fs_blocks.size() + 12 * L.fs_t.size());
   std::printf("fstream %d blocks %zu tmpl_max %d | gstream rom %d (%zu blocks) dyn %d (%zu blocks) tq %d (%zu blocks)\n", (int)L.fstream,
               L.fs_blocks.size(), L.fs_tmpl_max, (int)L.gstream[GS_ROM], L.gs_blocks[GS_ROM].size(), (int)L.gstream[GS_DYN],
               L.gs_blocks[GS_DYN].size(), (int)L.gstream[GS_TQ], L.gs_blocks[GS_TQ].size());

@@ -41,11 +41,13 @@ namespace {
 __device__ __forceinline__ double fs_int(int v) { return __longlong_as_double((long long)v); }
 // FDISC instant k (fs_t order) of the problem in c: its record fields through put(field, value) and its 5 g
 // rows (when wanted) straight to Gb
+// the FDISC tables a record lane reads after its instant: in LDS (staged by towr_gait_frec_kernel) or global memory
+struct FsTabs { const FsBlock* fsb; const int32_t* ws; const int32_t* tmpl; };
 template <class Put>
-__device__ __forceinline__ void fdisc_record(const KParams& P, const Ctx& c, int k, double* Gb, Put&& put) {
+__device__ __forceinline__ void fdisc_record(const KParams& P, const FsTabs& T, const Ctx& c, int k, double* Gb, Put&& put) {
   FdiscInstant o;
   fdisc_instant(c, P.fs_iee[k], P.fs_t[k], o);
-  const FsBlock fb = P.fsb[P.fs_iblk[k]];
+  const FsBlock fb = T.fsb[P.fs_iblk[k]];
 #pragma unroll
   for (int i = 0; i < 5; ++i)
 #pragma unroll
@@ -59,12 +61,12 @@ __device__ __forceinline__ void fdisc_record(const KParams& P, const Ctx& c, int
     for (int i = 0; i < 5; ++i) __builtin_nontemporal_store(o.g[i], Gb + row + i);
   }
   const int poly = o.poly;
-  const int ws = P.fs_ws[2 * (fb.wsoff + poly)], wd = P.fs_ws[2 * (fb.wsoff + poly) + 1];
+  const int ws = T.ws[2 * (fb.wsoff + poly)], wd = T.ws[2 * (fb.wsoff + poly) + 1];
   put(kFsND, fs_int(ws));
   put(kFsND + 1, fs_int(wd));
   double h0 = o.H[0], h1 = o.H[1], h2 = o.H[2], h3 = o.H[3];
   asm volatile("" : "+v"(h0), "+v"(h1), "+v"(h2), "+v"(h3));
-  const int32_t* tm = P.fs_tmpl + fb.tmpl;
+  const int32_t* tm = T.tmpl + fb.tmpl;
 #pragma unroll 4
   for (int q = 0; q < kFsWin; ++q) {   // the window's basis sums (schedule entries: never read, 0)
     const int pos = ws + q;
@@ -72,14 +74,15 @@ __device__ __forceinline__ void fdisc_record(const KParams& P, const Ctx& c, int
     put(q, te >= 0 ? phase_basis_sum(c.pcols[te & 0xFFFFFF], poly, h0, h1, h2, h3) : 0.0);
   }
 }
-__device__ __forceinline__ void fdisc_records(const KParams& P, const Ctx& c, int b, double* rec, int64_t ldr, int32_t k0, int32_t k1) {
+__device__ __forceinline__ void fdisc_records(const KParams& P, const FsTabs& T, const Ctx& c, int b, double* rec, int64_t ldr, int32_t k0,
+                                              int32_t k1) {
   double* Gb = P.G + (int64_t)b * P.ldg;
   double* R = rec + (int64_t)b * ldr;
   for (int k = k0 + threadIdx.x; k < k1; k += blockDim.x) {
-    const FsBlock fb = P.fsb[P.fs_iblk[k]];
+    const FsBlock fb = T.fsb[P.fs_iblk[k]];
     const int kk = k - fb.t0, nb = fb.n_inst;
     double* r = R + (int64_t)kFsRS * fb.t0 + kk;
-    fdisc_record(P, c, k, Gb, [&](int f, double v) { r[f * nb] = v; });
+    fdisc_record(P, T, c, k, Gb, [&](int f, double v) { r[f * nb] = v; });
   }
 }
 
@@ -352,9 +355,21 @@ template <bool ROTVEC, int ROLES>
 __device__ __forceinline__ void rec_body(const KParams& P, const RecArgs& A, double* smem) {
   const int np = A.nparts;
   const int b = (int)blockIdx.x / np, part = (A.parts >> (4 * ((int)blockIdx.x % np))) & 15;
+  FsTabs T{P.fsb, P.fs_ws, P.fs_tmpl};
+  if constexpr ((ROLES & 1) != 0) {
+    if (A.fs_lds > 0) {   // the FDISC tables to LDS beside the staging (gait_record_setup's barrier covers them)
+      int32_t* d = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(smem) + A.fs_lds);
+      const int32_t* sb = reinterpret_cast<const int32_t*>(P.fsb);
+      for (int i = threadIdx.x; i < A.fs_nb + A.fs_nws + A.fs_ntm; i += blockDim.x)
+        d[i] = i < A.fs_nb ? sb[i] : i < A.fs_nb + A.fs_nws ? P.fs_ws[i - A.fs_nb] : P.fs_tmpl[i - A.fs_nb - A.fs_nws];
+      T.fsb = reinterpret_cast<const FsBlock*>(d);
+      T.ws = d + A.fs_nb;
+      T.tmpl = d + A.fs_nb + A.fs_nws;
+    }
+  }
   const Ctx c = gait_record_setup<0>(P, b, smem);
   if constexpr ((ROLES & 1) != 0)
-    if (part == kRecFdisc) { fdisc_records(P, c, b, A.frec, A.fldr, 0, A.ni); return; }
+    if (part == kRecFdisc) { fdisc_records(P, T, c, b, A.frec, A.fldr, 0, A.ni); return; }
   if constexpr ((ROLES & 4) != 0)
     if (part == kRecTq) { tq_records(P, A, c, b); return; }
   if constexpr ((ROLES & 2) != 0) gs_records<ROTVEC>(P, A.g, c, b, smem, part == kRecGsDyn ? 1 : part == kRecGsRom ? 2 : 0);

@@ -51,6 +51,7 @@ struct FsBlock {
   int32_t v0, nv, L, tmpl;      // CSR range [v0, v0 + nv), row length, template offset (fs_tmpl)
   int32_t js0, ns1, wsoff, reserved;
 };
+static_assert(sizeof(FsBlock) % 4 == 0, "FsBlock is staged to LDS as int32 words");
 
 // Streaming RangeOfMotion and Dynamic under phase-duration optimisation (gstream.hip), the FsBlock
 // scheme generalised to rows whose columns differ by row type. Two launches per class:
@@ -327,7 +328,10 @@ enum RecPart { kRecFdisc = 1, kRecTq = 2, kRecGs = 3, kRecGsDyn = 4, kRecGsRom =
 struct RecArgs {
   GsRecArgs g;
   double* frec; int64_t fldr, tq_off;
-  int32_t ni, nparts, parts, reserved;
+  int32_t ni, nparts, parts;
+  // the FDISC launch (gstream.hip towr_gait_frec_kernel): byte offset in LDS of the staged FsBlock / window /
+  // template tables (0: the lanes read them in global memory), and their sizes in int32 words
+  int32_t fs_lds, fs_nb, fs_nws, fs_ntm;
 };
 size_t gs_dyn_state_bytes(bool rotvec);   // the record kernel's per-Dynamic-instant LDS state
 constexpr int kGsRecMaxBlock = 512;

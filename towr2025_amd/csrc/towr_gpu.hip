@@ -522,7 +522,17 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
     }
     if (R.nparts == 0) return TOWR_OK;
     const int threads = (int)std::min<int64_t>(kGsRecMaxBlock, (lanes + 63) & ~63);
-    const size_t lds = dyn ? gs_rec_lds(L) : fs_inst_lds_bytes(L);
+    size_t lds = dyn ? gs_rec_lds(L) : fs_inst_lds_bytes(L);
+    // the FDISC launch (no RangeOfMotion / Dynamic part) stages the FDISC tables after its staging region, so its
+    // lanes' table reads after the instant (block, window start, template) are LDS reads
+    R.fs_lds = 0;
+    if ((roles & 1) && !(roles & 2)) {
+      R.fs_lds = (int32_t)((lds + 15) & ~(size_t)15);
+      R.fs_nb = (int32_t)(L.fs_blocks.size() * (sizeof(FsBlock) / 4));
+      R.fs_nws = (int32_t)L.fs_ws.size();
+      R.fs_ntm = (int32_t)L.fs_tmpl.size();
+      lds = (size_t)R.fs_lds + 4 * (size_t)(R.fs_nb + R.fs_nws + R.fs_ntm);
+    }
     void* aa[] = {&P, &R};
     HIPCHK(h, hipLaunchKernel(gait_rec_kernel(L.rotvec, roles), dim3((unsigned)(B * R.nparts)), dim3((unsigned)threads), aa, lds, s));
     return TOWR_OK;
