@@ -234,6 +234,61 @@ __device__ __forceinline__ void stage_x_spans(const KParams& P, const double* xg
   stage16<BLOCK>(reinterpret_cast<uint4*>(ns), reinterpret_cast<const uint4*>(P.nodecol), (P.n_nodecol + 3) >> 2);
 }
 
+// The x-dependent PhaseSpline timings of one problem (phase_spline_timings / phase_end_timings: pdur, pend per
+// polynomial, phend per (endeffector, phase)) by the whole block: (1) each endeffector's last phase duration,
+// parked in its phend slot; (2) one thread per polynomial forms its duration (the divisions in parallel);
+// (3) one thread per spline / endeffector forms the running sums in the reference's order. Every value is the
+// one thread-per-spline loop's (same operations, same order); with one thread per spline the prologue took ~4 us
+// of a ~30 us record block (MI355X, ANYmal gait, per-block timestamps).
+__device__ __forceinline__ void phase_timings_block(const Ctx& c, const KParams& P, double* tm) {
+  double* pdur = tm;
+  double* pend = tm + P.n_pinfo;
+  double* phend = tm + 2 * P.n_pinfo;
+  const int tid = threadIdx.x, nspl = P.n_spl, nee = P.rb.n_ee;
+  if (tid < nee) {
+    const SchedInfo si = c.sched[tid];
+    if (si.col0 >= 0) phend[tid * P.ph_stride + si.n_phases - 1] = last_phase_duration(c, si);
+  }
+  __syncthreads();
+  for (int i = tid; i < P.n_pinfo; i += blockDim.x) {
+    int s = 0;
+    for (int q = 0; q < nspl; ++q) {
+      const SplineMeta& m = c.spl[q];
+      if (m.ee >= 0 && i >= m.pinfo_off && i < m.pinfo_off + m.n_polys) s = q;
+    }
+    const SplineMeta m = c.spl[s];
+    const SchedInfo si = c.sched[m.ee];
+    if (i >= m.pinfo_off && i < m.pinfo_off + m.n_polys && m.ee >= 0) {
+      const double last = si.col0 >= 0 ? phend[m.ee * P.ph_stride + si.n_phases - 1] : last_phase_duration(c, si);
+      pdur[i] = phase_poly_duration(c, m, si, last, i - m.pinfo_off);
+    }
+  }
+  __syncthreads();
+  if (tid < nspl) {
+    const SplineMeta m = c.spl[tid];
+    if (m.ee >= 0) {
+      double t = 0.0;
+      for (int i = 0; i < m.n_polys; ++i) {
+        t += pdur[m.pinfo_off + i];
+        pend[m.pinfo_off + i] = t;
+      }
+    }
+  } else if (tid < nspl + nee) {
+    const int ee = tid - nspl;
+    const SchedInfo si = c.sched[ee];
+    if (si.col0 >= 0) {
+      double* ph = phend + ee * P.ph_stride;
+      const double last = ph[si.n_phases - 1];
+      double acc = 0.0;
+      for (int k = 0; k < si.n_phases; ++k) {
+        acc += phase_duration(c, si, last, k);
+        ph[k] = acc;
+      }
+    }
+  }
+  __syncthreads();
+}
+
 // Prologue of the per-problem record kernel under phase-duration optimisation (gstream.hip): x (+ zero slot), the node table, the PhaseSpline tables and the terrain staged in LDS
 // ([x | node table | tables | timings | terrain], fs_inst_lds_bytes), then the x-dependent PhaseSpline
 // timings formed once per block (as tile_body does); returns the evaluation context over them.
@@ -264,13 +319,7 @@ __device__ __forceinline__ Ctx gait_record_setup(const KParams& P, int b, double
   c.rotvec = false;
   c.dyn_scratch = nullptr;
   double* tmg = reinterpret_cast<double*>(gt + 16 * P.gt_n16);
-  const int nspl = P.n_spl, nee = P.rb.n_ee;
-  if (tid < nspl) {
-    if (c.spl[tid].ee >= 0) phase_spline_timings(c, tid, tmg, tmg + P.n_pinfo);
-  } else if (tid < nspl + nee) {
-    if (c.sched[tid - nspl].col0 >= 0) phase_end_timings(c, tid - nspl, tmg + 2 * P.n_pinfo + (tid - nspl) * P.ph_stride);
-  }
-  __syncthreads();
+  phase_timings_block(c, P, tmg);
   c.pdur = tmg; c.pend = tmg + P.n_pinfo; c.phend = tmg + 2 * P.n_pinfo; c.ph_stride = P.ph_stride;
   return c;
 }

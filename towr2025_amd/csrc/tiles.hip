@@ -161,16 +161,10 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
   c.rotvec = ROTVEC;
   c.dyn_scratch = TYPE == IT_DYN ? smem + P.lds_scr_off : nullptr;
   if constexpr (GAIT) {
-    // the x-dependent PhaseSpline timings once per block (one thread per spline / endeffector)
-    // instead of a division-carrying scan per lane and spline evaluation
+    // the x-dependent PhaseSpline timings once per block (phase_timings_block) instead of a
+    // division-carrying scan per lane and spline evaluation
     double* tm = reinterpret_cast<double*>(gt + 16 * P.gt_n16);
-    const int tid = threadIdx.x, nspl = P.n_spl, nee = P.rb.n_ee;
-    if (tid < nspl) {
-      if (c.spl[tid].ee >= 0) phase_spline_timings(c, tid, tm, tm + P.n_pinfo);
-    } else if (tid < nspl + nee) {
-      if (c.sched[tid - nspl].col0 >= 0) phase_end_timings(c, tid - nspl, tm + 2 * P.n_pinfo + (tid - nspl) * P.ph_stride);
-    }
-    __syncthreads();
+    phase_timings_block(c, P, tm);
     c.pdur = tm; c.pend = tm + P.n_pinfo; c.phend = tm + 2 * P.n_pinfo; c.ph_stride = P.ph_stride;
     c.ter = ters;   // LDS copy: no global load in the evaluation waits behind the zero-fill stores
     if constexpr (kWaveZero) {
