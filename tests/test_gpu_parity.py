@@ -526,3 +526,10 @@ def test_batch_device_g_or_jac_only(name):
     assert np.array_equal(Gg, G) and np.isnan(Vg).all()
     Gj, Vj = run(False, True)
     assert np.array_equal(Vj, V) and np.isnan(Gj).all()
+    # the output that is not wanted may be NULL
+    Gd = torch.full((B, p.m), np.nan, dtype=torch.float64, device=dev)
+    Vd = torch.full((B, ldv), np.nan, dtype=torch.float64, device=dev)
+    p.eval_batch_device(Xd, Gd, None, want_g=True, want_jac=False)
+    p.eval_batch_device(Xd, None, Vd, want_g=False, want_jac=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(Gd.cpu().numpy(), G) and np.array_equal(Vd.cpu().numpy()[:, :p.nnz], V)

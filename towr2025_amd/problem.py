@@ -244,9 +244,11 @@ class TowrGpuProblem:
         self._check_batch(X, G, V, want_g, want_jac)
         if stream is None:
             stream = torch.cuda.current_stream(X.device)
+        def ptr(t):   # an output that is not wanted may be None (NULL: the C-ABI never touches it)
+            return (C.c_void_p(None), 0) if t is None else (C.c_void_p(t.data_ptr()), t.stride(0))
+        (gp, ldg), (vp, ldv) = ptr(G), ptr(V)
         self._check(self._lib.towr_gpu_eval_batch_device(
-            self._h, B, C.c_void_p(X.data_ptr()), X.stride(0),
-            C.c_void_p(G.data_ptr()), G.stride(0), C.c_void_p(V.data_ptr()), V.stride(0),
+            self._h, B, C.c_void_p(X.data_ptr()), X.stride(0), gp, ldg, vp, ldv,
             int(want_g), int(want_jac), C.c_void_p(stream.cuda_stream)))
 
     def _check_batch(self, X, G, V, want_g=True, want_jac=True):
