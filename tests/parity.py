@@ -104,11 +104,11 @@ def check_values(g_ref, g, rows_ref, v_ref, v, m, cols_ref=None, floor_cols=None
     mag_v = np.maximum(np.abs(v_ref), np.abs(v))
     err_v = np.abs(v_ref - v)
     tol_v = REL * mag_v + floor_v
-    bad_v = np.flatnonzero(err_v > tol_v)
+    bad_v = np.flatnonzero(~(err_v <= tol_v))   # (a NaN on either side is a mismatch)
     mag_g = np.maximum(np.abs(g_ref), np.abs(g))
     err_g = np.abs(g_ref - g)
     tol_g = REL * mag_g + floor
-    bad_g = np.flatnonzero(err_g > tol_g)
+    bad_g = np.flatnonzero(~(err_g <= tol_g))
     big_v = mag_v > floor_v
     big_g = mag_g > floor
     stats = {
@@ -145,7 +145,7 @@ def assert_cost_close(f_ref, f, g_ref, g, what=""):
         f"{what}: f ref {f_ref!r} got {f!r}"
     scale = max(1.0, float(np.max(np.abs(g_ref))) if len(g_ref) else 1.0)
     tol = REL * np.maximum(np.abs(g_ref), np.abs(g)) + ABS * scale
-    bad = np.flatnonzero(np.abs(g_ref - g) > tol)
+    bad = np.flatnonzero(~(np.abs(g_ref - g) <= tol))   # (NaN: a mismatch)
     if len(bad):
         j = bad[np.argmax(np.abs(g_ref[bad] - g[bad]))]
         raise AssertionError(f"{what}: {len(bad)} gradient mismatches, largest at {j}: ref {g_ref[j]!r} got {g[j]!r}")
