@@ -16,6 +16,7 @@ def config_descs():
         "anymal_slope_yaw": F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.SlopeID),
                                           goal=(1.8, 0.3, 0.0), goal_yaw=0.3).to_desc(),
         "hyq_chimney": _hyq(F.HeightMap.ChimneyID),
+        "hyq_chimney_lr": _hyq(F.HeightMap.ChimneyLRID),                          # height_map_examples.cc:186-211
         "hyq_gap": _hyq(F.HeightMap.GapID),
         "anymal_block_baserom": _anymal_baserom(),
         # configs[3]: ANYmal on stairs with phase-duration (gait) optimisation
@@ -231,3 +232,15 @@ def ext_cases():
                                     (capi.DATA_SOFT_BOUNDS, 0, _soft_bounds(nfd, 23)),
                                     (capi.DATA_SOFT_BOUNDS, 1, _soft_bounds(4, 24))])
     return out
+
+
+def anymal_long_gait(n_phases=17, phase=0.2):
+    """ANYmal on stairs with phase-duration optimisation over a longer horizon (n_phases phases of `phase` s per
+    foot, every foot in contact at the start and the end). At 17 phases the FDISC record launch's LDS (staging +
+    its FsBlock / window / template tables, towr_gpu.hip rec_launch_lds) is past 64 kB."""
+    f = F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.StairsID), optimize_timings=True,
+                      total_duration=phase * n_phases)
+    for ee in range(4):
+        f.params_.ee_phase_durations_[ee] = [phase] * n_phases
+        f.params_.ee_in_contact_at_start_[ee] = True
+    return f.to_desc()

@@ -85,6 +85,13 @@ def residue_cols(desc, n, data=None):
     return ResidueMask(sched, motion, rows)
 
 
+def _within(a, b, err, tol):
+    """Entries inside the tolerance. A NaN on either side is a mismatch (err <= tol is False for it), and so is an
+    infinity facing a finite value: its tolerance REL * inf is itself infinite, so err <= tol alone would pass it.
+    Identical values (the same infinity included) always match."""
+    return (a == b) | ((err <= tol) & np.isfinite(a) & np.isfinite(b))
+
+
 def check_values(g_ref, g, rows_ref, v_ref, v, m, cols_ref=None, floor_cols=None):
     """Indices of g and J entries outside the tolerance, and a summary dict:
     max_rel = largest |a-b| / max(|a|,|b|) over entries above their floor; worst = largest
@@ -104,11 +111,11 @@ def check_values(g_ref, g, rows_ref, v_ref, v, m, cols_ref=None, floor_cols=None
     mag_v = np.maximum(np.abs(v_ref), np.abs(v))
     err_v = np.abs(v_ref - v)
     tol_v = REL * mag_v + floor_v
-    bad_v = np.flatnonzero(~(err_v <= tol_v))   # (a NaN on either side is a mismatch)
+    bad_v = np.flatnonzero(~_within(v_ref, v, err_v, tol_v))
     mag_g = np.maximum(np.abs(g_ref), np.abs(g))
     err_g = np.abs(g_ref - g)
     tol_g = REL * mag_g + floor
-    bad_g = np.flatnonzero(~(err_g <= tol_g))
+    bad_g = np.flatnonzero(~_within(g_ref, g, err_g, tol_g))
     big_v = mag_v > floor_v
     big_g = mag_g > floor
     stats = {
@@ -141,11 +148,12 @@ def assert_cost_close(f_ref, f, g_ref, g, what=""):
     """Objective and dense gradient: the value tolerance above with the floor 1e-12 * max(1, |f|) for f
     and 1e-12 * max(1, max |grad|) for the gradient (its entries are sums over many samples whose
     order differs: the device accumulates them with atomics)."""
-    assert abs(f - f_ref) <= REL * max(abs(f), abs(f_ref)) + ABS * max(1.0, abs(f_ref)), \
+    assert bool(_within(np.float64(f_ref), np.float64(f), abs(f - f_ref), REL * max(abs(f), abs(f_ref)) + ABS * max(1.0, abs(f_ref)))), \
         f"{what}: f ref {f_ref!r} got {f!r}"
-    scale = max(1.0, float(np.max(np.abs(g_ref))) if len(g_ref) else 1.0)
+    fin = np.abs(g_ref)[np.isfinite(g_ref)]
+    scale = max(1.0, float(np.max(fin)) if len(fin) else 1.0)
     tol = REL * np.maximum(np.abs(g_ref), np.abs(g)) + ABS * scale
-    bad = np.flatnonzero(~(np.abs(g_ref - g) <= tol))   # (NaN: a mismatch)
+    bad = np.flatnonzero(~_within(g_ref, g, np.abs(g_ref - g), tol))
     if len(bad):
         j = bad[np.argmax(np.abs(g_ref[bad] - g[bad]))]
         raise AssertionError(f"{what}: {len(bad)} gradient mismatches, largest at {j}: ref {g_ref[j]!r} got {g[j]!r}")

@@ -197,6 +197,42 @@ def test_gait_paths(monkeypatch, name):
         np.testing.assert_array_equal(outs[k][1], outs[(None, None)][1])
 
 
+@pytest.mark.parametrize("tiles", [None, "1"])
+def test_long_gait_record_lds_past_64k(monkeypatch, tiles):
+    """A longer gait horizon (tests/configs.py anymal_long_gait: 17 phases per foot) whose FDISC record launch needs
+    more than 64 kB of LDS for its staging and FsBlock / window / template tables. With RangeOfMotion / Dynamic on
+    the tile path (TOWR_GPU_GAIT_TILES) no record launch has a Dynamic part, so the FDISC launch's LDS alone sets
+    the kernel's dynamic-LDS attribute (towr_gpu.hip rec_launch_lds, used at creation and at the launch); the
+    default path streams every class. Both against the oracle, single call and a B = 70 batch."""
+    import torch
+    from tests.configs import anymal_long_gait
+    if tiles is None:
+        monkeypatch.delenv("TOWR_GPU_GAIT_TILES", raising=False)
+    else:
+        monkeypatch.setenv("TOWR_GPU_GAIT_TILES", tiles)
+    desc = anymal_long_gait()
+    o = Oracle(desc)
+    p = TowrGpuProblem(desc, device=0)
+    assert p.kernel_path(2) == 1 and p.kernel_path(0) == (0 if tiles else 1)
+    x0 = o.initial_x()
+    r, c, _ = o.eval_jac(x0)
+    fc = residue_cols(desc, o.n)
+    x = _perturb(x0, 1717, 0.02)
+    g, v = p.eval_g_jac(x)
+    assert_close(o.eval_g(x), g, r, o.eval_jac(x)[2], v, o.m, f"long gait tiles={tiles}", cols_ref=c, floor_cols=fc)
+    B = 70
+    X = np.stack([_perturb(x0, 1800 + b, 0.02) for b in range(B)])
+    dev = torch.device("cuda:0")
+    Gd = torch.full((B, p.m), np.nan, dtype=torch.float64, device=dev)
+    Vd = torch.full((B, p.nnz), np.nan, dtype=torch.float64, device=dev)
+    p.eval_batch_device(torch.from_numpy(X).to(dev), Gd, Vd)
+    torch.cuda.synchronize()
+    G, V = Gd.cpu().numpy(), Vd.cpu().numpy()
+    for b in (0, 41, B - 1):
+        assert_close(o.eval_g(X[b]), G[b], r, o.eval_jac(X[b])[2], V[b], o.m, f"long gait batch {b} tiles={tiles}",
+                     cols_ref=c, floor_cols=fc)
+
+
 @pytest.mark.parametrize("name", ["hyq_gap", "hyq_gap_gaitopt"])
 def test_gap_batch(name):
     """Gap batches (one handle, per-problem Gap terrains): every problem's values on the frozen pattern are
@@ -337,9 +373,9 @@ def test_batch_device_gait_optimization():
 
 
 def test_batch_device_gait_two_chains(monkeypatch):
-    """The phase-duration path at B >= kSplitBatch (64) runs two chains (FDISC records + compose on the caller's
-    stream, RangeOfMotion / Dynamic on the side stream), below it one serial chain (towr_gpu.hip
-    launch_stream_path). B = 601 (odd: a compose block's problem pair is ragged) against the same problems
+    """The phase-duration path at B >= kSplitBatch (64) runs two chains (FDISC records + compose on the
+    high-priority side stream 0, RangeOfMotion / Dynamic records + composes on the caller's stream), below it one
+    serial chain (towr_gpu.hip launch_stream_path). B = 601 (odd: a compose block's problem pair is ragged) against the same problems
     as batches of 37 and 1 (37 < 64: the serial chain): bit-identical, nothing written past m / nnz, a
     sample against the oracle."""
     import torch
@@ -389,13 +425,22 @@ def test_batch_device_gait_two_chains(monkeypatch):
                      floor_cols=residue_cols(d, o.n))
 
 
-def test_batch_device_gait_torque():
-    """ANYmal phase-duration optimisation + TorqueConstraintDiscretized (the TQDISC records beside FDISC's in
-    the FDISC chain, its compose blocks in the FDISC compose launch) as a randomised B = 64 device batch:
-    the two-chain path, every problem bit-identical to its B = 1 (single-chain) evaluation."""
+@pytest.mark.parametrize("streams", [None, "1", "2"])
+def test_batch_device_gait_torque(monkeypatch, streams):
+    """ANYmal phase-duration optimisation + TorqueConstraintDiscretized as a randomised B = 64 device batch, every
+    problem bit-identical to its B = 1 (single-chain) evaluation, on each big-batch launch arrangement of
+    launch_stream_path (TOWR_GPU_STREAMS, read at handle creation):
+      * default (two side streams): TQDISC records + compose as a third chain (`tq3`);
+      * "2" (one side stream): the TQDISC records in the FDISC record launch (towr_gait_frec_kernel<5>) and its
+        compose blocks in the FDISC compose launch (mask 17) on side stream 0 (`tqf`);
+      * "1" (no side stream): the same chains one after the other on the caller's stream."""
+    if streams is None:
+        monkeypatch.delenv("TOWR_GPU_STREAMS", raising=False)
+    else:
+        monkeypatch.setenv("TOWR_GPU_STREAMS", streams)
     f = F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.StairsID), optimize_timings=True)
     f.params_.constraints_.append(F.Parameters.Torque)
-    _batch_vs_single(f, "anymal_gait_torque_batch", B=64, optimize_timings=True)
+    _batch_vs_single(f, f"anymal_gait_torque_batch streams={streams}", B=64, optimize_timings=True)
 
 
 def test_batch_device_rotvec():

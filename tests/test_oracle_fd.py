@@ -38,7 +38,7 @@ def _fd_check(desc, x, h_rel=1e-6, tol=2e-5, skip_cols=None, skip_rows=None):
 
 
 @pytest.mark.parametrize("name", ["monoped_procedural", "biped_walk_2s", "anymal_trot_2p4s",
-                                  "hopper_five_steps", "hyq_chimney", "anymal_slope_yaw", "anymal_block_baserom"])
+                                  "hopper_five_steps", "hyq_chimney", "hyq_chimney_lr", "anymal_slope_yaw", "anymal_block_baserom"])
 def test_fd_consistency(name):
     desc = CONFIGS[name]
     o = Oracle(desc)

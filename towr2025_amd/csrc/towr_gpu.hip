@@ -165,6 +165,26 @@ int fail(towr_gpu_handle h, int code, const std::string& msg) {
     if (e_ != hipSuccess) return fail((h), TOWR_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
   } while (0)
 
+// Every kernel launch of the engine. With TOWR_GPU_LAUNCH_LOG set (read once), the first launch of each (kernel, block,
+// dynamic LDS) is written to stderr as "towr-launch <symbol> block <threads> lds <bytes> grid <blocks>": the dynamic
+// LDS is a host-side choice the code object does not record, so tools/kernel_resources.py joins these lines with the
+// code objects' register / scratch metadata into profiles/kernel_resources.txt (occupancy per launch).
+hipError_t launch_kernel(const void* fn, dim3 grid, dim3 block, void** args, size_t lds, hipStream_t s) {
+  static const bool log = std::getenv("TOWR_GPU_LAUNCH_LOG") != nullptr;
+  if (log) {
+    static std::mutex mu;
+    static std::vector<std::pair<const void*, std::pair<unsigned, size_t>>> seen;
+    std::lock_guard<std::mutex> lk(mu);
+    const auto key = std::make_pair(fn, std::make_pair(block.x, lds));
+    if (std::find(seen.begin(), seen.end(), key) == seen.end()) {
+      seen.push_back(key);
+      const char* nm = hipKernelNameRefByPtr(fn, s);
+      std::fprintf(stderr, "towr-launch %s block %u lds %zu grid %u\n", nm ? nm : "?", block.x, lds, grid.x);
+    }
+  }
+  return hipLaunchKernel(fn, grid, block, args, lds, s);
+}
+
 template <class T>
 int upload(towr_gpu_handle h, T** dst, const std::vector<T>& src) {
   const size_t bytes = sizeof(T) * (src.empty() ? 1 : src.size());
@@ -400,7 +420,7 @@ int launch_rv_prepass(towr_gpu_handle h, int B, const double* X, int64_t ldx, in
   const int64_t waves = 3 * (((int64_t)B * K + 63) / 64), grid = (waves + kRvCoefBlock / 64 - 1) / (kRvCoefBlock / 64);
   if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
   void* args[] = {&P};
-  HIPCHK(h, hipLaunchKernel(rv_coef_kernel(), dim3((unsigned)grid), dim3(kRvCoefBlock), args, 0, s));
+  HIPCHK(h, launch_kernel(rv_coef_kernel(), dim3((unsigned)grid), dim3(kRvCoefBlock), args, 0, s));
   return TOWR_OK;
 }
 
@@ -417,7 +437,7 @@ int launch_fused(towr_gpu_handle h, const towr_gpu_handle_s::FuseGroup& fg, int 
   const int64_t grid = ((total + 7) / 8) * 8;
   if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
   void* args[] = {&P};
-  HIPCHK(h, hipLaunchKernel(step_kernel_for(L.gait, L.rotvec, fg.kblock), dim3((unsigned)grid), dim3((unsigned)fg.kblock),
+  HIPCHK(h, launch_kernel(step_kernel_for(L.gait, L.rotvec, fg.kblock), dim3((unsigned)grid), dim3((unsigned)fg.kblock),
                             args, fg.lds, s));
   return TOWR_OK;
 }
@@ -430,6 +450,21 @@ size_t gs_state_stride(const Layout& L) { return (gs_dyn_state_bytes(L.rotvec) +
 size_t gs_rec_lds(const Layout& L) {
   const size_t Kd = (size_t)gs_kd(L);
   return fs_inst_lds_bytes(L) + Kd * gs_state_stride(L) + sizeof(double) * 9 * Kd * (1 + (size_t)L.rb.n_ee);
+}
+// LDS of one record launch (bytes), used at the launch and at handle creation: the staging (fs_inst_lds_bytes), with
+// a Dynamic part also its states and scratch (gs_rec_lds). A launch with the FDISC part and no RangeOfMotion /
+// Dynamic part stages the FDISC tables (FsBlock, window, template) after that region when they fit in 160 kB
+// (*fs_lds: their byte offset), else its lanes read them in global memory (*fs_lds = 0).
+constexpr size_t kLdsMax = 160 * 1024;
+size_t rec_launch_lds(const Layout& L, bool dyn, bool fdisc_only, int32_t* fs_lds) {
+  const size_t base = dyn ? gs_rec_lds(L) : fs_inst_lds_bytes(L);
+  if (fs_lds) *fs_lds = 0;
+  if (!fdisc_only) return base;
+  const size_t off = (base + 15) & ~(size_t)15;
+  const size_t tabs = 4 * (L.fs_blocks.size() * (sizeof(FsBlock) / 4) + L.fs_ws.size() + L.fs_tmpl.size());
+  if (off + tabs > kLdsMax) return base;
+  if (fs_lds) *fs_lds = (int32_t)off;
+  return off + tabs;
 }
 int gs_rec_threads(const Layout& L, int64_t Kd, int64_t Kr) {   // the record lanes of Kd Dynamic and Kr RangeOfMotion instants
   const int64_t ee0 = (Kd + 63) & ~63, r0 = (ee0 + 3 * L.rb.n_ee * Kd + 63) & ~63;
@@ -522,19 +557,14 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
     }
     if (R.nparts == 0) return TOWR_OK;
     const int threads = (int)std::min<int64_t>(kGsRecMaxBlock, (lanes + 63) & ~63);
-    size_t lds = dyn ? gs_rec_lds(L) : fs_inst_lds_bytes(L);
-    // the FDISC launch (no RangeOfMotion / Dynamic part) stages the FDISC tables after its staging region, so its
-    // lanes' table reads after the instant (block, window start, template) are LDS reads
-    R.fs_lds = 0;
-    if ((roles & 1) && !(roles & 2)) {
-      R.fs_lds = (int32_t)((lds + 15) & ~(size_t)15);
-      R.fs_nb = (int32_t)(L.fs_blocks.size() * (sizeof(FsBlock) / 4));
-      R.fs_nws = (int32_t)L.fs_ws.size();
-      R.fs_ntm = (int32_t)L.fs_tmpl.size();
-      lds = (size_t)R.fs_lds + 4 * (size_t)(R.fs_nb + R.fs_nws + R.fs_ntm);
-    }
+    // the FDISC launch (no RangeOfMotion / Dynamic part) stages the FDISC tables after its staging region when they
+    // fit, so its lanes' table reads after the instant (block, window start, template) are LDS reads
+    const size_t lds = rec_launch_lds(L, dyn, (roles & 1) && !(roles & 2), &R.fs_lds);
+    R.fs_nb = (int32_t)(L.fs_blocks.size() * (sizeof(FsBlock) / 4));
+    R.fs_nws = (int32_t)L.fs_ws.size();
+    R.fs_ntm = (int32_t)L.fs_tmpl.size();
     void* aa[] = {&P, &R};
-    HIPCHK(h, hipLaunchKernel(gait_rec_kernel(L.rotvec, roles), dim3((unsigned)(B * R.nparts)), dim3((unsigned)threads), aa, lds, s));
+    HIPCHK(h, launch_kernel(gait_rec_kernel(L.rotvec, roles), dim3((unsigned)(B * R.nparts)), dim3((unsigned)threads), aa, lds, s));
     return TOWR_OK;
   };
   ComposeArgs C{};
@@ -557,7 +587,7 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
     void* ab[] = {&P, &C};
     // the launch's own roles: their instantiation (registers) and LDS; without FDISC, TQDISC or small kinds 256 threads
     const int roles = (C.nt[0] ? 1 : 0) | (C.nt[1] ? 2 : 0) | (C.nt[2] ? 4 : 0) | (C.nt[3] ? 8 : 0) | (C.nt[4] ? 16 : 0);
-    HIPCHK(h, hipLaunchKernel(gait_compose_kernel(roles), dim3((unsigned)grid), dim3(compose_block(roles)), ab,
+    HIPCHK(h, launch_kernel(gait_compose_kernel(roles), dim3((unsigned)grid), dim3(compose_block(roles)), ab,
                               compose_lds(L, C.nt[0] > 0, C.nt[1] > 0, C.nt[2] > 0, C.nt[3] > 0, C.nt[4] > 0), s));
     return TOWR_OK;
   };
@@ -681,7 +711,7 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
     }
     const int block = class_block(L, lc);
     void* args[] = {&P};
-    HIPCHK(h, hipLaunchKernel(kernel_for_class(lc, L.gait, L.rotvec), dim3((unsigned)grid), dim3((unsigned)block), args,
+    HIPCHK(h, launch_kernel(kernel_for_class(lc, L.gait, L.rotvec), dim3((unsigned)grid), dim3((unsigned)block), args,
                               lds_bytes(L, lc), st));
   }
   for (int i = 0; i < (stream_forked ? std::min(h->n_side, 2) : nside); ++i) {
@@ -735,7 +765,7 @@ int launch_cost(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* 
   P.lds_red_off = (int32_t)cost_red_off(L);
   P.F = F; P.GR = GR; P.ldgr = ldgr;
   void* args[] = {&P};
-  HIPCHK(h, hipLaunchKernel(cost_kernel_for(L.gait, GR != nullptr, L.rotvec), dim3((unsigned)B), dim3(kCostBlock), args,
+  HIPCHK(h, launch_kernel(cost_kernel_for(L.gait, GR != nullptr, L.rotvec), dim3((unsigned)B), dim3(kCostBlock), args,
                             cost_lds_bytes(L), s));
   return h->soft ? scratch_release(h, s) : TOWR_OK;
 }
@@ -781,7 +811,7 @@ int launch_traj(towr_gpu_handle h, int B, const double* X, int64_t ldx, double d
   if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
   const double* tp = h->d_traj_t;
   void* args[] = {&P, &tp, const_cast<int*>(&ns), &ph, &OUT, &ldo, const_cast<int32_t*>(&xoff)};
-  HIPCHK(h, hipLaunchKernel(traj_kernel_for(L.gait), dim3((unsigned)grid), dim3(kTrajBlock), args, lds, s));
+  HIPCHK(h, launch_kernel(traj_kernel_for(L.gait), dim3((unsigned)grid), dim3(kTrajBlock), args, lds, s));
   return TOWR_OK;
 }
 
@@ -1204,11 +1234,13 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
       h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
     }
   }
-  if (uses_scratch(L)) {   // the record kernels share fs_inst_lds_bytes' layout
+  if (L.fstream || L.gstream[GS_ROM] || L.gstream[GS_DYN] || L.gstream[GS_TQ]) {   // the record kernels share fs_inst_lds_bytes' layout
+    // (fixed-gait RotVec also uses scratch, for its coefficient pre-pass, but launches no record kernel)
     const size_t lds = fs_inst_lds_bytes(L);
-    if (lds > 160 * 1024) { h->err = "problem too large for the streaming instant kernel's LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
-    const size_t need = gs_rec_lds(L);
-    if (need > 160 * 1024) { h->err = "problem too large for the record kernel's LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
+    if (lds > kLdsMax) { h->err = "problem too large for the streaming instant kernel's LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
+    // every record launch's LDS (rec_launch_lds): a Dynamic part, or the FDISC part with its staged tables
+    const size_t need = std::max(rec_launch_lds(L, true, false, nullptr), rec_launch_lds(L, false, true, nullptr));
+    if (need > kLdsMax) { h->err = "problem too large for the record kernel's LDS"; return bail(TOWR_ERR_UNSUPPORTED); }
     bool ok = true;
     for (int roles = 1; roles < 8 && need > 64 * 1024; ++roles)
       ok = ok && hipFuncSetAttribute(gait_rec_kernel(L.rotvec, roles), hipFuncAttributeMaxDynamicSharedMemorySize, (int)need) == hipSuccess;
