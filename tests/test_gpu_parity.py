@@ -405,16 +405,18 @@ def test_batch_device_gait_two_chains(monkeypatch):
         np.testing.assert_array_equal(G[s:e, :p.m], g.cpu().numpy(), err_msg=f"g of problems [{s}, {e})")
         np.testing.assert_array_equal(V[s:e, :p.nnz], v.cpu().numpy(), err_msg=f"J of problems [{s}, {e})")
     # one launch stream (TOWR_GPU_STREAMS=1, read at handle creation): the two chains one after the other
-    monkeypatch.setenv("TOWR_GPU_STREAMS", "1")
-    q = TowrGpuProblem(desc)
-    q.set_batch_terrain(terrains)
-    g1 = torch.full((B, ldg), np.nan, dtype=torch.float64, device=dev)
-    v1 = torch.full((B, ldv), np.nan, dtype=torch.float64, device=dev)
-    q.eval_batch_device(Xd, g1, v1)
-    torch.cuda.synchronize()
-    np.testing.assert_array_equal(g1.cpu().numpy(), G, err_msg="g: one stream vs two")
-    np.testing.assert_array_equal(v1.cpu().numpy(), V, err_msg="J: one stream vs two")
-    q.close()
+    for var, val in (("TOWR_GPU_STREAMS", "1"),):
+        monkeypatch.setenv(var, val)
+        q = TowrGpuProblem(desc)
+        monkeypatch.delenv(var)
+        q.set_batch_terrain(terrains)
+        g1 = torch.full((B, ldg), np.nan, dtype=torch.float64, device=dev)
+        v1 = torch.full((B, ldv), np.nan, dtype=torch.float64, device=dev)
+        q.eval_batch_device(Xd, g1, v1)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(g1.cpu().numpy(), G, err_msg=f"g: {var}={val} vs the default")
+        np.testing.assert_array_equal(v1.cpu().numpy(), V, err_msg=f"J: {var}={val} vs the default")
+        q.close()
     r, c = p.jac_structure()
     for b in (0, 255, 256, 600):
         d = f.to_desc()

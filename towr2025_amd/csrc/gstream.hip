@@ -369,10 +369,11 @@ __device__ __forceinline__ void rec_body(const KParams& P, const RecArgs& A, dou
   }
   const Ctx c = gait_record_setup<0>(P, b, smem);
   if constexpr ((ROLES & 1) != 0)
-    if (part == kRecFdisc) { fdisc_records(P, T, c, b, A.frec, A.fldr, 0, A.ni); return; }
+    if (part == kRecFdisc) { fdisc_records(P, T, c, b, A.frec, A.fldr, 0, A.ni); TG_STAMP(P, 3); return; }
   if constexpr ((ROLES & 4) != 0)
-    if (part == kRecTq) { tq_records(P, A, c, b); return; }
+    if (part == kRecTq) { tq_records(P, A, c, b); TG_STAMP(P, 3); return; }
   if constexpr ((ROLES & 2) != 0) gs_records<ROTVEC>(P, A.g, c, b, smem, part == kRecGsDyn ? 1 : part == kRecGsRom ? 2 : 0);
+  TG_STAMP(P, 3);
 }
 template <bool ROTVEC, int ROLES>
 __global__ void __launch_bounds__(kGsRecMaxBlock) __attribute__((amdgpu_waves_per_eu(4))) towr_gait_rec_kernel(KParams P, RecArgs A) {
@@ -462,12 +463,15 @@ __device__ __forceinline__ void fdisc_compose(const KParams& P, const double* re
   int b = g0;
   // (the compose block forming its instants' records itself from x and the PhaseSpline tables in global
   // memory, instead of reading them: FDISC 0.42 -> 2.7 ms per 1024 problems, the dependent table loads)
+  TG_STAMP(P, 0);
   fetch(b);
+  int it = 0;
   for (;;) {
 #pragma unroll
     for (int q = 0; q < kFsPre; ++q)
       if (dst[q] >= 0) cd[dst[q]] = pre[q];
     __syncthreads();
+    if (it == 0) TG_STAMP(P, 1);
     for (int t = tid; t < nr * kFsWin; t += BLOCK) {   // window value q of row r: b[i][e(q)] * basis sum (emit_dim)
       const int r = t / kFsWin, q = t - r * kFsWin;
       const int k = r / 5, i = r - 5 * k;
@@ -477,6 +481,7 @@ __device__ __forceinline__ void fdisc_compose(const KParams& P, const double* re
     }
     for (int t = tid; t < nr; t += BLOCK) wsr[t] = ci(t / 5, 0);
     __syncthreads();
+    if (it == 0) TG_STAMP(P, 2);
     const int bn = b + ng;
     if (bn < P.B) fetch(bn);   // in flight while this problem streams
     {
@@ -505,10 +510,13 @@ __device__ __forceinline__ void fdisc_compose(const KParams& P, const double* re
       }
       if (((nv - head) & 1) && tid == 0) __builtin_nontemporal_store(value(nv - 1), out + nv - 1);
     }
+    if (it == 0) TG_STAMP(P, 3);
+    ++it;
     if (bn >= P.B) break;
     b = bn;
     __syncthreads();   // this problem's records and row values read before the next deposit
   }
+  TG_STAMP(P, 4);
 }
 
 

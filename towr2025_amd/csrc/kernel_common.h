@@ -84,7 +84,22 @@ struct KParams {
   const int32_t* s_col;
   const double* s_b;
   int32_t s_m;
+  // experiment build only (-DTOWR_STAMPS, tools/stamps.py): per-block timestamp slots of this launch, or null
+  unsigned long long* stamps;
 };
+
+// In-kernel phase timestamps of the experiment build (make variant VFLAGS=-DTOWR_STAMPS): lane 0 of each wave
+// stores the 100 MHz real-time counter into slot k of its wave (64 slots per block: 8 waves x 8 phases); the
+// product build compiles them out.
+#ifdef TOWR_STAMPS
+#define TG_STAMP(P, k)                                                                                              \
+  do {                                                                                                              \
+    if ((P).stamps && (threadIdx.x & 63) == 0 && threadIdx.x < 512)                                                 \
+      (P).stamps[(size_t)blockIdx.x * 64 + (threadIdx.x >> 6) * 8 + (k)] = __builtin_amdgcn_s_memrealtime();        \
+  } while (0)
+#else
+#define TG_STAMP(P, k) do { } while (0)
+#endif
 
 // global -> LDS copy of n16 16-byte units: each thread issues up to K independent loads before its
 // first LDS write, so the staging costs one memory latency rather than one per loop trip
@@ -300,6 +315,7 @@ __device__ __forceinline__ Ctx gait_record_setup(const KParams& P, int b, double
   char* gt = reinterpret_cast<char*>(xs + P.n_pad + ((P.n_nodecol + 3) >> 2) * 2);
   towr_terrain_t* ters = reinterpret_cast<towr_terrain_t*>(gt + 16 * P.gt_n16 + 8 * P.gt_ntime);
   const int tid = threadIdx.x;
+  TG_STAMP(P, 0);
   stage_x<BLOCK, true>(P, xg, xs, ns);
   stage16<BLOCK>(reinterpret_cast<uint4*>(gt), P.gtab, P.gt_n16);
   if (tid < (int)(sizeof(towr_terrain_t) / 8))
@@ -319,7 +335,9 @@ __device__ __forceinline__ Ctx gait_record_setup(const KParams& P, int b, double
   c.rotvec = false;
   c.dyn_scratch = nullptr;
   double* tmg = reinterpret_cast<double*>(gt + 16 * P.gt_n16);
+  TG_STAMP(P, 1);
   phase_timings_block(c, P, tmg);
+  TG_STAMP(P, 2);
   c.pdur = tmg; c.pend = tmg + P.n_pinfo; c.phend = tmg + 2 * P.n_pinfo; c.ph_stride = P.ph_stride;
   return c;
 }

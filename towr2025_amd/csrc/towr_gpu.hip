@@ -169,7 +169,22 @@ int fail(towr_gpu_handle h, int code, const std::string& msg) {
 // dynamic LDS) is written to stderr as "towr-launch <symbol> block <threads> lds <bytes> grid <blocks>": the dynamic
 // LDS is a host-side choice the code object does not record, so tools/kernel_resources.py joins these lines with the
 // code objects' register / scratch metadata into profiles/kernel_resources.txt (occupancy per launch).
+#ifdef TOWR_STAMPS
+// experiment build (tools/stamps.py): launch i after towr_gpu_debug_stamps(buf) stores its TG_STAMP slots in region i
+// of buf (kStampRegion slots each, kStampRegions regions); the kernel of each region is kept for the tool
+constexpr size_t kStampRegion = size_t(1) << 20;
+constexpr int kStampRegions = 16;
+unsigned long long* g_stamps = nullptr;
+int g_stamp_n = 0;
+const void* g_stamp_fn[kStampRegions];
+#endif
 hipError_t launch_kernel(const void* fn, dim3 grid, dim3 block, void** args, size_t lds, hipStream_t s) {
+#ifdef TOWR_STAMPS
+  if (g_stamps && g_stamp_n < kStampRegions && (size_t)grid.x * 64 <= kStampRegion) {
+    static_cast<KParams*>(args[0])->stamps = g_stamps + kStampRegion * g_stamp_n;   // every kernel's first argument
+    g_stamp_fn[g_stamp_n++] = fn;
+  }
+#endif
   static const bool log = std::getenv("TOWR_GPU_LAUNCH_LOG") != nullptr;
   if (log) {
     static std::mutex mu;
@@ -1052,6 +1067,13 @@ int setup_fusion(towr_gpu_handle h, std::string& err) {
 // C-ABI
 // =================================================================================================
 extern "C" {
+
+#ifdef TOWR_STAMPS
+// experiment build: device buffer of kStampRegions x kStampRegion slots for the TG_STAMP timestamps (null: off);
+// resets the launch count. towr_gpu_debug_stamp_kernel(i): the kernel symbol of region i (null past the last)
+int towr_gpu_debug_stamps(void* buf) { g_stamps = static_cast<unsigned long long*>(buf); if (buf) g_stamp_n = 0; return TOWR_OK; }
+const char* towr_gpu_debug_stamp_kernel(int i) { return i < g_stamp_n ? hipKernelNameRefByPtr(g_stamp_fn[i], nullptr) : nullptr; }
+#endif
 
 int towr_gpu_abi_version(void) { return TOWR_GPU_ABI_VERSION; }
 

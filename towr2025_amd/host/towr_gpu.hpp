@@ -8,9 +8,9 @@
 // NlpCallbacks  the IPOPT TNLP callback subset of ifopt's IpoptAdapter for the hot path
 //            (get_nlp_info / eval_f / eval_grad_f / eval_g / eval_jac_g) with Ipopt's argument
 //            meaning: eval_jac_g with
-//            values == nullptr fills the structure, otherwise the values. Unlike ifopt (which
-//            ignores new_x and re-evaluates every set), g and J are produced by one fused launch per
-//            new x and J is served from that launch when IPOPT asks for it at the same x.
+//            values == nullptr fills the structure, otherwise the values, written by the device straight
+//            into IPOPT's (page-locked) array; eval_g evaluates g alone unless the Jacobian came first at
+//            that x (see the class comment).
 //
 // Error behaviour: construction failures throw std::runtime_error (the reference's
 // NlpFormulation throws at setup, nlp_formulation.cc:396, 477-481); the callbacks return false on
@@ -93,17 +93,29 @@ class Engine {
 
 // The eval_f / eval_grad_f / eval_g / eval_jac_g callbacks of an IPOPT TNLP (Index = int,
 // Number = double), as ifopt's IpoptAdapter implements them for towr, served by the engine.
+//
+// Zero-copy Jacobian. eval_jac_g evaluates the values straight into IPOPT's own `values` array: the array is
+// page-locked for the engine (towr_gpu_register_host) the first time it is seen, and the engine's B = 1 launch
+// writes every value into it over PCIe, so no copy of the nnz values happens on the host (ifopt's IpoptAdapter
+// copies its sparse matrix there, ipopt_adapter.cc; at nnz = 241,250 that copy took longer than the evaluation).
+// IPOPT's TNLPAdapter passes the same array on every call (its jac_g_ member, allocated once), so registration
+// happens once per solve; when a different pointer arrives, the old one is unregistered and the new one
+// registered. If registration fails (the range overlaps one already registered, or the array is too short to
+// matter) the values go through the page-locked cache and a copy, as before.
+// eval_g evaluates g alone (into the page-locked g cache, then m doubles to IPOPT's g), unless eval_jac_g came first
+// at this x: then one launch formed both and eval_g serves the cached g. The Jacobian is written only when IPOPT asks
+// for it, so IPOPT's array never holds values of an x it did not request (its adapter reuses the array without
+// re-asking when the x tag it last evaluated matches).
+// finalize_solution (or the destructor) unregisters IPOPT's array.
 class NlpCallbacks {
  public:
-  // The g / values cache lives in page-locked memory, so every fused evaluation DMAs straight into it
-  // (a layout-only engine refuses the registration; the cache then stays pageable).
   // Lifetime: the Engine must outlive these callbacks (declare the Engine first): the destructor
-  // unregisters the cache through the Engine's handle.
-  explicit NlpCallbacks(Engine& e) : e_(e), g_(e.GetNumberOfConstraints()), v_(e.GetNumberOfJacobianNonzeros()) {
+  // unregisters through the Engine's handle.
+  explicit NlpCallbacks(Engine& e) : e_(e), g_(e.GetNumberOfConstraints()) {
     pin_g_ = !g_.empty() && e_.RegisterHost(g_.data(), g_.size() * sizeof(double)) == TOWR_OK;
-    pin_v_ = !v_.empty() && e_.RegisterHost(v_.data(), v_.size() * sizeof(double)) == TOWR_OK;
   }
   ~NlpCallbacks() {
+    ReleaseValues();
     if (pin_g_) e_.UnregisterHost(g_.data());
     if (pin_v_) e_.UnregisterHost(v_.data());
   }
@@ -131,7 +143,11 @@ class NlpCallbacks {
   }
   bool eval_g(int n, const double* x, bool new_x, int m, double* g) {
     if (n != e_.GetNumberOfOptimizationVariables() || m != e_.GetNumberOfConstraints()) return false;
-    if (!Update(x, new_x)) return false;
+    NewX(new_x);
+    if (!g_valid_) {   // g alone (the Jacobian is evaluated when IPOPT asks for it)
+      try { e_.EvalConstraints(x, g_.data()); } catch (const std::exception&) { return false; }
+      g_valid_ = true;
+    }
     for (int i = 0; i < m; ++i) g[i] = g_[i];
     return true;
   }
@@ -143,26 +159,52 @@ class NlpCallbacks {
       try { e_.GetJacobianStructure(iRow, jCol); } catch (const std::exception&) { return false; }
       return true;
     }
-    if (!Update(x, new_x)) return false;
-    for (int k = 0; k < nele_jac; ++k) values[k] = v_[k];
+    NewX(new_x);
+    double* dst = Values(values, nele_jac);   // IPOPT's array when registered, else the page-locked cache
+    try {
+      if (g_valid_) e_.EvalNonzerosOfJacobian(x, dst);
+      else e_.EvalConstraintsAndJacobian(x, g_.data(), dst);   // first callback at this x: g comes along
+    } catch (const std::exception&) { g_valid_ = false; return false; }
+    g_valid_ = true;
+    if (dst != values)
+      for (int k = 0; k < nele_jac; ++k) values[k] = dst[k];
     return true;
   }
+  // TNLP::finalize_solution: the solve is over, IPOPT's array is released
+  void finalize_solution() { ReleaseValues(); }
+
+  // introspection for tests: whether the last eval_jac_g wrote IPOPT's array directly, registrations so far
+  bool values_zero_copy() const { return reg_ != nullptr; }
+  int values_registrations() const { return n_reg_; }
 
  private:
-  // IPOPT's new_x == true on the first callback at a new x (whichever it is) invalidates the cache
-  void NewX(bool new_x) { if (new_x) valid_ = false; }
-  // one fused launch per new x; IPOPT's new_x == false promises the x of the previous call
-  bool Update(const double* x, bool new_x) {
-    NewX(new_x);
-    if (valid_) return true;
-    try { e_.EvalConstraintsAndJacobian(x, g_.data(), v_.data()); } catch (const std::exception&) { valid_ = false; return false; }
-    valid_ = true;
-    return true;
+  // IPOPT's new_x == true on the first callback at a new x (whichever it is) invalidates the cached g
+  void NewX(bool new_x) { if (new_x) g_valid_ = false; }
+  double* Values(double* values, int nele) {
+    if (values == reg_) return values;
+    ReleaseValues();
+    if (nele > 0 && e_.RegisterHost(values, (size_t)nele * sizeof(double)) == TOWR_OK) {
+      reg_ = values;
+      ++n_reg_;
+      return values;
+    }
+    if (v_.size() != (size_t)nele) {   // fallback: the page-locked cache and a copy
+      if (pin_v_) e_.UnregisterHost(v_.data());
+      v_.assign((size_t)nele, 0.0);
+      pin_v_ = nele > 0 && e_.RegisterHost(v_.data(), v_.size() * sizeof(double)) == TOWR_OK;
+    }
+    return v_.data();
+  }
+  void ReleaseValues() {
+    if (reg_) e_.UnregisterHost(reg_);
+    reg_ = nullptr;
   }
   Engine& e_;
   std::vector<double> g_, v_;
   bool pin_g_ = false, pin_v_ = false;
-  bool valid_ = false;
+  bool g_valid_ = false;
+  double* reg_ = nullptr;   // IPOPT's values array, registered
+  int n_reg_ = 0;
 };
 
 // The CSV text of SaveTrajectoryToCSV (towr/src/utils/save_data.cpp:9-130): the reference's header,

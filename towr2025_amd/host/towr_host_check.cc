@@ -6,7 +6,16 @@
 // and dumps everything to a binary file:
 //   desc bytes | n m (int32) nnz (int64) | x0[n] | iRow[nnz] jCol[nnz] | (device >= 0) g[m] values[nnz] f grad[n]
 // and (device >= 0) the trajectory of x0 sampled at 0.01 s as SaveTrajectoryToCSV writes it, to <out.bin>.csv
-// usage: towr_host_check <anymal|anymal_costs|anymal_rotvec|biped|biped_next|hopper> <out.bin> [device (default -1: layout only)]
+// usage: towr_host_check <anymal|anymal_costs|anymal_rotvec|anymal_gait|biped|biped_next|hopper> <out.bin> [device (default -1: layout only)]
+//        towr_host_check <cfg> --zerocopy [device] [timed iterations]
+//   the zero-copy Jacobian of NlpCallbacks (towr_gpu.hpp) against the engine's own evaluation, bit for bit: IPOPT's
+//   values array stable across calls (TNLPAdapter's jac_g_), g before J and J before g, a values array that moves
+//   between calls, and the array after finalize_solution; then per-iteration timings (eval_g + eval_jac_g through the
+//   callbacks, and eval_jac_g alone) against the cached path (one fused evaluation into the page-locked cache + the
+//   nnz-value copy into IPOPT's array). Prints one line "zerocopy ok ..." or fails with a message.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -17,11 +26,95 @@
 
 using namespace towr_gpu;
 
+namespace {
+
+double median(std::vector<double> v) {
+  std::sort(v.begin(), v.end());
+  return v.empty() ? 0.0 : v[v.size() / 2];
+}
+
+int zerocopy_check(const towr_problem_desc_t& d, int device, int iters) {
+  Engine e(d, device);
+  const int n = e.GetNumberOfOptimizationVariables(), m = e.GetNumberOfConstraints();
+  const int nnz = (int)e.GetNumberOfJacobianNonzeros();
+  const std::vector<double> x0 = e.GetVariableValues();
+  std::vector<std::vector<double>> xs;
+  for (int k = 0; k < 3; ++k) {   // x0 and two deterministic perturbations
+    std::vector<double> x = x0;
+    for (int i = 0; i < n; ++i) x[i] += 0.01 * k * std::sin(0.37 * i + k);
+    xs.push_back(x);
+  }
+  std::vector<std::vector<double>> gr(3, std::vector<double>(m)), vr(3, std::vector<double>(nnz));
+  for (int k = 0; k < 3; ++k) e.EvalConstraintsAndJacobian(xs[k].data(), gr[k].data(), vr[k].data());   // the engine's own (staged) evaluation
+  auto same = [&](const std::vector<double>& a, const std::vector<double>& b, const char* what, int k) {
+    if (std::memcmp(a.data(), b.data(), a.size() * sizeof(double)) != 0) {
+      std::fprintf(stderr, "zerocopy: %s differs at x %d\n", what, k);
+      return false;
+    }
+    return true;
+  };
+  NlpCallbacks nlp(e);
+  std::vector<double> g(m), jac_g(nnz);   // IPOPT's TNLPAdapter arrays: allocated once per solve
+  for (int rep = 0; rep < 2; ++rep)
+    for (int k = 0; k < 3; ++k) {
+      std::fill(jac_g.begin(), jac_g.end(), NAN);
+      bool ok;
+      if (rep == 0) ok = nlp.eval_g(n, xs[k].data(), true, m, g.data()) && nlp.eval_jac_g(n, xs[k].data(), false, m, nnz, nullptr, nullptr, jac_g.data());
+      else ok = nlp.eval_jac_g(n, xs[k].data(), true, m, nnz, nullptr, nullptr, jac_g.data()) && nlp.eval_g(n, xs[k].data(), false, m, g.data());
+      if (!ok) { std::fprintf(stderr, "zerocopy: callback failed: %s\n", towr_gpu_last_error(e.handle())); return 1; }
+      if (!same(g, gr[k], rep ? "g (J first)" : "g", k) || !same(jac_g, vr[k], rep ? "values (J first)" : "values", k)) return 1;
+      if (!nlp.values_zero_copy()) { std::fprintf(stderr, "zerocopy: IPOPT's array was not registered\n"); return 1; }
+    }
+  if (nlp.values_registrations() != 1) { std::fprintf(stderr, "zerocopy: %d registrations of a stable array\n", nlp.values_registrations()); return 1; }
+  for (int k = 0; k < 3; ++k) {   // a values array that moves between calls
+    std::vector<double> moved(nnz, NAN);
+    if (!nlp.eval_g(n, xs[k].data(), true, m, g.data()) || !nlp.eval_jac_g(n, xs[k].data(), false, m, nnz, nullptr, nullptr, moved.data())) return 1;
+    if (!same(moved, vr[k], "values (moved array)", k)) return 1;
+    nlp.finalize_solution();   // (the vector is freed next: release its registration first)
+  }
+  if (nlp.values_registrations() != 4) { std::fprintf(stderr, "zerocopy: %d registrations, expected 4\n", nlp.values_registrations()); return 1; }
+  // timings: IPOPT's per-iteration pair through the callbacks, against the cached path of round 4 (one fused
+  // evaluation into page-locked g / values caches, then both copied into IPOPT's arrays)
+  using clk = std::chrono::steady_clock;
+  auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+  std::vector<double> t_pair, t_jac, t_old, t_oldjac;
+  std::vector<double> cg(m), cv(nnz);
+  const bool pg = e.RegisterHost(cg.data(), cg.size() * sizeof(double)) == TOWR_OK;
+  const bool pv = e.RegisterHost(cv.data(), cv.size() * sizeof(double)) == TOWR_OK;
+  for (int it = 0; it < iters + 10; ++it) {
+    const double* x = xs[it % 3].data();
+    auto t0 = clk::now();
+    nlp.eval_g(n, x, true, m, g.data());
+    auto t1 = clk::now();
+    nlp.eval_jac_g(n, x, false, m, nnz, nullptr, nullptr, jac_g.data());
+    auto t2 = clk::now();
+    e.EvalConstraintsAndJacobian(x, cg.data(), cv.data());
+    std::copy(cg.begin(), cg.end(), g.begin());
+    auto t3 = clk::now();
+    std::copy(cv.begin(), cv.end(), jac_g.begin());
+    auto t4 = clk::now();
+    if (it >= 10) { t_pair.push_back(us(t0, t2)); t_jac.push_back(us(t1, t2)); t_old.push_back(us(t2, t4)); t_oldjac.push_back(us(t3, t4)); }
+  }
+  if (pg) e.UnregisterHost(cg.data());
+  if (pv) e.UnregisterHost(cv.data());
+  std::printf("zerocopy ok n=%d m=%d nnz=%d iters=%d pair_us %.1f jac_us %.1f cached_pair_us %.1f cached_copy_us %.1f\n", n, m, nnz,
+              iters, median(t_pair), median(t_jac), median(t_old), median(t_oldjac));
+  return 0;
+}
+
+}  // namespace
+
 int main(int argc, char** argv) {
   if (argc < 3) { std::fprintf(stderr, "usage: %s <anymal|biped|hopper> <out.bin> [device]\n", argv[0]); return 2; }
   const std::string cfg = argv[1];
   const int device = argc > 3 ? std::atoi(argv[3]) : -1;
-  NlpFormulation f = (cfg == "anymal" || cfg == "anymal_costs" || cfg == "anymal_rotvec") ? AnymalTrot() : (cfg == "biped" || cfg == "biped_next") ? BipedWalk() : MonopedHopper();
+  const bool zc = std::string(argv[2]) == "--zerocopy";
+  NlpFormulation f = (cfg == "anymal" || cfg == "anymal_costs" || cfg == "anymal_rotvec" || cfg == "anymal_gait") ? AnymalTrot()
+                     : (cfg == "biped" || cfg == "biped_next") ? BipedWalk() : MonopedHopper();
+  if (cfg == "anymal_gait") {   // BASELINE configs[3]: stairs, phase-duration optimisation
+    f.terrain_ = HeightMap::MakeTerrain(HeightMap::StairsID);
+    f.params_.OptimizePhaseDurations();
+  }
   if (cfg == "biped_next") {   // SURVEY §8(f) kinds: Torque, TerrainHard, EELinear (tests/configs.py)
     f.params_.constraints_.push_back(Parameters::Torque);
     f.params_.constraints_.push_back(Parameters::TerrainHard);
@@ -40,6 +133,7 @@ int main(int argc, char** argv) {
   }
   try {
     const towr_problem_desc_t d = f.MakeDesc();
+    if (zc) return zerocopy_check(d, device < 0 ? 0 : device, argc > 4 ? std::atoi(argv[4]) : 200);
     Engine e(d, device);
     NlpCallbacks nlp(e);
     int n = 0, m = 0, nnz = 0;
