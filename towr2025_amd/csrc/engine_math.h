@@ -70,7 +70,7 @@ struct SplineMeta {
 };
 
 // phase of a polynomial (NodesVariablesPhaseBased::PolyInfo, nodes_variables_phase_based.cc:39-59)
-struct PolyPhase { int16_t phase, poly_in_phase, n_in_phase, reserved; };
+struct PolyPhase { int16_t phase, poly_in_phase, n_in_phase, spl; };   // spl: the spline whose polynomial it is
 
 // one column of a PhaseSpline's full Jacobian pattern in one dimension: the optimisation variable
 // and the (1 or 2) node values it sets (a stance variable sets two nodes)
@@ -355,21 +355,58 @@ TG_HD void phase_end_timings(const Ctx& c, int ee, double* phend) {
     phend[ph] = acc;
   }
 }
+// Spline::GetSegmentID + GetLocalTime (spline.cc:48-78) over precomputed polynomial durations d[np] and their running
+// sums e[np] (Ctx::pdur / pend): the first polynomial whose end is at or past tg - eps (else the last), and tg minus
+// the durations before it, subtracted in order. The operands are loaded 8 at a time ahead of the comparisons / the
+// dependent subtractions (one LDS round trip per 8 polynomials instead of one per polynomial).
+TG_HD void locate_poly(const double* d, const double* e, int np, double tg, int& poly, double& tl, double& T) {
+  const double eps = 1e-10, thr = tg - eps;
+  int id = np - 1;
+  for (int i0 = 0; i0 < np; i0 += 8) {
+    double v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = i0 + k < np ? e[i0 + k] : 0.0;
+    int f = -1;
+#pragma unroll
+    for (int k = 7; k >= 0; --k)
+      if (i0 + k < np && v[k] >= thr) f = k;   // the first entry of the group at or past tg - eps
+    if (f >= 0) { id = i0 + f; break; }
+  }
+  double l = tg;
+  for (int i0 = 0; i0 < id; i0 += 8) {
+    double v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = i0 + k < id ? d[i0 + k] : 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (i0 + k < id) l -= v[k];
+  }
+  poly = id;
+  tl = l;
+  T = d[id];
+}
+// PhaseDurations' GetSegmentID over the running sums of phase durations pe[n] (Ctx::phend): the first phase whose end
+// is at or past t - eps, else the last (loaded 8 at a time, as locate_poly)
+TG_HD int phase_cur(const double* pe, int n, double t) {
+  const double eps = 1e-10, thr = t - eps;
+  for (int p0 = 0; p0 < n; p0 += 8) {
+    double v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = p0 + k < n ? pe[p0 + k] : 0.0;
+    int f = -1;
+#pragma unroll
+    for (int k = 7; k >= 0; --k)
+      if (p0 + k < n && v[k] >= thr) f = k;
+    if (f >= 0) return p0 + f;
+  }
+  return n - 1;
+}
+
 // Spline::GetLocalTime (spline.cc:48-78) over the x-dependent durations of a PhaseSpline
 TG_HD void phase_spline_locate(const Ctx& c, int s, double tg, SplinePt& o) {
   if (c.pdur) {   // the block's precomputed durations and running sums (see Ctx::pdur)
-    const int off = c.spl[s].pinfo_off, np = c.spl[s].n_polys;
-    const double* d = c.pdur + off;
-    const double* e = c.pend + off;
-    const double eps = 1e-10;
-    int id = np - 1;
-    for (int i = 0; i < np; ++i)
-      if (e[i] >= tg - eps) { id = i; break; }
-    double l = tg;
-    for (int i = 0; i < id; ++i) l -= d[i];
-    o.poly = id;
-    o.tl = l;
-    o.T = d[id];
+    const int off = c.spl[s].pinfo_off;
+    locate_poly(c.pdur + off, c.pend + off, c.spl[s].n_polys, tg, o.poly, o.tl, o.T);
     return;
   }
   const SplineMeta m = c.spl[s];
@@ -545,28 +582,31 @@ TG_HD void emit_dim(const Ctx& c, Emit& em, int row, int s, const SplinePt& P, c
 // (phase_spline.cc:67-93) with PhaseDurations::GetJacobianOfPos (phase_durations.cc:126-154).
 // J[k][col] over the endeffector's n_phases - 1 schedule variables is dense (sparseView(1, -1)).
 struct SchedJac { int cur, n, col0; double dx[3], v[3]; };
-TG_HD void sched_jac(const Ctx& c, int s, double t, const SplinePt& P, SchedJac& J) {
+// one dimension of J.dx: CubicHermitePolynomial::GetDerivativeOfPosWrtDuration (polynomial.cc:236-257) of the polynomial
+// with node values x0, v0, x1, v1, duration T, local time tl, minus the polynomial's share of the velocity vk
+// (phase_spline.cc:67-93: inner = 1 / polynomials in the phase, prev = the polynomial's index in the phase)
+TG_HD double sched_dx_dim(double x0, double v0, double x1, double v1, double T, double tl, double vk, const PolyPhase& pp) {
 #pragma clang fp contract(off)
+  const double inner = 1. / pp.n_in_phase, prev = pp.poly_in_phase;
+  const double t2 = cpow(tl, 2), t3 = cpow(tl, 3), T2 = cpow(T, 2), T3 = cpow(T, 3), T4 = cpow(T, 4);
+  const double dxdT = (t3 * (v0 + v1)) / T3 - (t2 * (2 * v0 + v1)) / T2 - (3 * t3 * (2 * x0 - 2 * x1 + T * v0 + T * v1)) / T4 +
+                      (2 * t2 * (3 * x0 - 3 * x1 + 2 * T * v0 + T * v1)) / T3;
+  return inner * (dxdT - prev * vk);
+}
+TG_HD void sched_jac(const Ctx& c, int s, double t, const SplinePt& P, SchedJac& J) {
   const SplineMeta m = c.spl[s];
   const SchedInfo si = c.sched[m.ee];
   const PolyPhase pp = c.pinfo[m.pinfo_off + P.poly];
-  const double inner = 1. / pp.n_in_phase, prev = pp.poly_in_phase;
-  const double T = P.T, tl = P.tl, t2 = cpow(tl, 2), t3 = cpow(tl, 3), T2 = cpow(T, 2), T3 = cpow(T, 3), T4 = cpow(T, 4);
   for (int k = 0; k < 3; ++k) {
-    // CubicHermitePolynomial::GetDerivativeOfPosWrtDuration (polynomial.cc:236-257)
     const double x0 = xval(c, node_col(c, s, P.poly, kPos, k)), v0 = xval(c, node_col(c, s, P.poly, kVel, k));
     const double x1 = xval(c, node_col(c, s, P.poly + 1, kPos, k)), v1 = xval(c, node_col(c, s, P.poly + 1, kVel, k));
-    const double dxdT = (t3 * (v0 + v1)) / T3 - (t2 * (2 * v0 + v1)) / T2 - (3 * t3 * (2 * x0 - 2 * x1 + T * v0 + T * v1)) / T4 +
-                        (2 * t2 * (3 * x0 - 3 * x1 + 2 * T * v0 + T * v1)) / T3;
-    J.dx[k] = inner * (dxdT - prev * P.v[k]);
+    J.dx[k] = sched_dx_dim(x0, v0, x1, v1, P.T, P.tl, P.v[k], pp);
     J.v[k] = P.v[k];
   }
   const double eps = 1e-10;   // GetSegmentID over the phases
   J.cur = si.n_phases - 1;
-  if (c.phend) {
-    const double* pe = c.phend + m.ee * c.ph_stride;
-    for (int ph = 0; ph < si.n_phases; ++ph)
-      if (pe[ph] >= t - eps) { J.cur = ph; break; }
+  if (c.phend) {   // the block's running sums
+    J.cur = phase_cur(c.phend + m.ee * c.ph_stride, si.n_phases, t);
   } else {
     const double last = last_phase_duration(c, si);
     double acc = 0.0;

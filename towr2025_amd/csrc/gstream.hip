@@ -405,33 +405,32 @@ __global__ void __launch_bounds__(kGsRecMaxBlock) __attribute__((amdgpu_waves_pe
 // ForceConstraintDiscretized compose block: FsBlock jt for the problems g0, g0 + ng, ...
 // LDS: [per-instant records (stride kFsCS) | row window values (5 n x kFsWin) | row window starts (5 n)]
 constexpr int kFsUnits = 4;   // 16-byte units composed per lane before their stores
+// The row window values and starts of an FsBlock's rows from its instants' records in LDS (cd: instant kk's record at
+// kk * kFsCS): window value q of row r = b[i][e(q)] * basis sum q (emit_dim; 0.0 where the sum is exactly 0)
 template <int BLOCK>
-__device__ __forceinline__ void fdisc_compose(const KParams& P, const double* rec, int64_t ldr, int ng, int jt, int g0, double* smem) {
-  constexpr int kFsPre = (kFsInst * kFsRS + BLOCK - 1) / BLOCK;   // prefetched record doubles per thread
-  const FsBlock fb = P.fsb[jt];
-  const int tid = threadIdx.x, n = fb.n_inst, nr = 5 * n;
-  double* cd = smem;
-  double* rowv = cd + ((n * kFsCS + 1) & ~1);
-  int32_t* wsr = reinterpret_cast<int32_t*>(rowv + nr * kFsWin);
+__device__ __forceinline__ void fs_rows(const FsBlock& fb, const double* cd, double* rowv, int32_t* wsr) {
+  const int tid = threadIdx.x, nr = 5 * fb.n_inst;
   auto ci = [&](int k, int f) -> int { return *reinterpret_cast<const int32_t*>(cd + k * kFsCS + kFsND + f); };   // ws, wd, cur
-  // the chunk: element e = f * n + kk -> LDS kk * kFsCS + f
-  const int nch = n * kFsRS;
-  const int64_t chunk0 = (int64_t)kFsRS * fb.t0;
-  int dst[kFsPre];
-#pragma unroll
-  for (int q = 0; q < kFsPre; ++q) {
-    const int e = tid + q * BLOCK;
-    const int f = e / n, kk = e - f * n;
-    dst[q] = e >= nch ? -1 : kk * kFsCS + f;
+  for (int t = tid; t < nr * kFsWin; t += BLOCK) {
+    const int r = t / kFsWin, q = t - r * kFsWin;
+    const int k = r / 5, i = r - 5 * k;
+    const double v = cd[k * kFsCS + q];
+    const int ed = (ci(k, 1) >> (2 * q)) & 3;
+    rowv[t] = v == 0.0 ? 0.0 : cd[k * kFsCS + kFsB + 3 * i + ed] * v;
   }
-  double pre[kFsPre];
-  auto fetch = [&](int b) {
-    const double* src = rec + (int64_t)b * ldr + chunk0;
-#pragma unroll
-    for (int q = 0; q < kFsPre; ++q) pre[q] = dst[q] >= 0 ? src[tid + q * BLOCK] : 0.0;
-  };
+  for (int t = tid; t < nr; t += BLOCK) wsr[t] = ci(t / 5, 0);
+}
+// The FsBlock's CSR range [v0, v0 + nv) of problem b with 16-byte non-temporal stores, UNITS units composed per lane
+// before their stores (UNITS stores in flight instead of one per LDS round trip); every entry one lookup: a schedule
+// column from the instant's d force / d schedule and pyramid row (eval_fdisc's arithmetic, see fdisc_sched_value), a
+// force column from the row's window, else 0
+template <int BLOCK, int UNITS>
+__device__ __forceinline__ void fs_stream(const KParams& P, const FsBlock& fb, int b, const double* cd, const double* rowv,
+                                          const int32_t* wsr) {
+  const int tid = threadIdx.x;
   const int Lr = fb.L, js0 = fb.js0, ns1 = fb.ns1;
   const float invL = 1.0f / (float)Lr;   // exact row for block ranges below kFloatDivMax (layout.h, checked by build_fstream)
+  auto ci = [&](int k, int f) -> int { return *reinterpret_cast<const int32_t*>(cd + k * kFsCS + kFsND + f); };
   // entry j of row r (instant k = r / 5, pyramid row i): eval_fdisc's value (see fdisc_sched_value / emit_dim)
   auto entry = [&](int r, int j) -> double {
     const unsigned js = (unsigned)(j - js0);
@@ -460,9 +459,58 @@ __device__ __forceinline__ void fdisc_compose(const KParams& P, const double* re
     const int r = (int)(((float)e + 0.5f) * invL);
     return entry(r, e - r * Lr);
   };
+  double* out = P.V + (int64_t)b * P.ldv + fb.v0;
+  const int nv = fb.nv;
+  const int head = (reinterpret_cast<uintptr_t>(out) & 15) ? 1 : 0;
+  if (head && tid == 0) __builtin_nontemporal_store(value(0), out);
+  const int m2 = (nv - head) >> 1;
+  dbl2_t* d2 = reinterpret_cast<dbl2_t*>(out + head);
+  for (int u0 = tid; u0 < m2; u0 += BLOCK * UNITS) {
+    dbl2_t v[UNITS];
+#pragma unroll
+    for (int q = 0; q < UNITS; ++q) {
+      const int u = u0 + q * BLOCK;
+      const int e = head + 2 * u;
+      const int r = (int)(((float)e + 0.5f) * invL);
+      const int j = e - r * Lr;
+      v[q].x = u < m2 ? entry(r, j) : 0.0;
+      v[q].y = u < m2 ? (j + 1 < Lr ? entry(r, j + 1) : entry(r + 1, 0)) : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < UNITS; ++q)
+      if (u0 + q * BLOCK < m2) __builtin_nontemporal_store(v[q], d2 + u0 + q * BLOCK);
+  }
+  if (((nv - head) & 1) && tid == 0) __builtin_nontemporal_store(value(nv - 1), out + nv - 1);
+}
+
+template <int BLOCK>
+__device__ __forceinline__ void fdisc_compose(const KParams& P, const double* rec, int64_t ldr, int ng, int jt, int g0, double* smem) {
+  constexpr int kFsPre = (kFsInst * kFsRS + BLOCK - 1) / BLOCK;   // prefetched record doubles per thread
+  const FsBlock fb = P.fsb[jt];
+  const int tid = threadIdx.x, n = fb.n_inst, nr = 5 * n;
+  double* cd = smem;
+  double* rowv = cd + ((n * kFsCS + 1) & ~1);
+  int32_t* wsr = reinterpret_cast<int32_t*>(rowv + nr * kFsWin);
+  // the chunk: element e = f * n + kk -> LDS kk * kFsCS + f
+  const int nch = n * kFsRS;
+  const int64_t chunk0 = (int64_t)kFsRS * fb.t0;
+  int dst[kFsPre];
+#pragma unroll
+  for (int q = 0; q < kFsPre; ++q) {
+    const int e = tid + q * BLOCK;
+    const int f = e / n, kk = e - f * n;
+    dst[q] = e >= nch ? -1 : kk * kFsCS + f;
+  }
+  double pre[kFsPre];
+  auto fetch = [&](int b) {
+    const double* src = rec + (int64_t)b * ldr + chunk0;
+#pragma unroll
+    for (int q = 0; q < kFsPre; ++q) pre[q] = dst[q] >= 0 ? src[tid + q * BLOCK] : 0.0;
+  };
   int b = g0;
   // (the compose block forming its instants' records itself from x and the PhaseSpline tables in global
-  // memory, instead of reading them: FDISC 0.42 -> 2.7 ms per 1024 problems, the dependent table loads)
+  // memory, instead of reading them: FDISC 0.42 -> 2.7 ms per 1024 problems, the dependent table loads;
+  // forming them from tables staged in LDS is towr_fdisc_fused_kernel)
   TG_STAMP(P, 0);
   fetch(b);
   int it = 0;
@@ -472,44 +520,12 @@ __device__ __forceinline__ void fdisc_compose(const KParams& P, const double* re
       if (dst[q] >= 0) cd[dst[q]] = pre[q];
     __syncthreads();
     if (it == 0) TG_STAMP(P, 1);
-    for (int t = tid; t < nr * kFsWin; t += BLOCK) {   // window value q of row r: b[i][e(q)] * basis sum (emit_dim)
-      const int r = t / kFsWin, q = t - r * kFsWin;
-      const int k = r / 5, i = r - 5 * k;
-      const double v = cd[k * kFsCS + q];
-      const int ed = (ci(k, 1) >> (2 * q)) & 3;
-      rowv[t] = v == 0.0 ? 0.0 : cd[k * kFsCS + kFsB + 3 * i + ed] * v;
-    }
-    for (int t = tid; t < nr; t += BLOCK) wsr[t] = ci(t / 5, 0);
+    fs_rows<BLOCK>(fb, cd, rowv, wsr);
     __syncthreads();
     if (it == 0) TG_STAMP(P, 2);
     const int bn = b + ng;
     if (bn < P.B) fetch(bn);   // in flight while this problem streams
-    {
-      double* out = P.V + (int64_t)b * P.ldv + fb.v0;
-      const int nv = fb.nv;
-      const int head = (reinterpret_cast<uintptr_t>(out) & 15) ? 1 : 0;
-      if (head && tid == 0) __builtin_nontemporal_store(value(0), out);
-      const int m2 = (nv - head) >> 1;
-      dbl2_t* d2 = reinterpret_cast<dbl2_t*>(out + head);
-      // kFsUnits units per lane composed into registers first, then stored together, so a lane keeps
-      // kFsUnits stores in flight instead of one store per LDS round trip
-      for (int u0 = tid; u0 < m2; u0 += BLOCK * kFsUnits) {
-        dbl2_t v[kFsUnits];
-#pragma unroll
-        for (int q = 0; q < kFsUnits; ++q) {
-          const int u = u0 + q * BLOCK;
-          const int e = head + 2 * u;
-          const int r = (int)(((float)e + 0.5f) * invL);
-          const int j = e - r * Lr;
-          v[q].x = u < m2 ? entry(r, j) : 0.0;
-          v[q].y = u < m2 ? (j + 1 < Lr ? entry(r, j + 1) : entry(r + 1, 0)) : 0.0;
-        }
-#pragma unroll
-        for (int q = 0; q < kFsUnits; ++q)
-          if (u0 + q * BLOCK < m2) __builtin_nontemporal_store(v[q], d2 + u0 + q * BLOCK);
-      }
-      if (((nv - head) & 1) && tid == 0) __builtin_nontemporal_store(value(nv - 1), out + nv - 1);
-    }
+    fs_stream<BLOCK, kFsUnits>(P, fb, b, cd, rowv, wsr);
     if (it == 0) TG_STAMP(P, 3);
     ++it;
     if (bn >= P.B) break;
@@ -519,6 +535,180 @@ __device__ __forceinline__ void fdisc_compose(const KParams& P, const double* re
   TG_STAMP(P, 4);
 }
 
+// ------------------------------------------------------------------------------------------------
+// The fused ForceConstraintDiscretized kernel (layout.h FfGeo): one block per (problem, FsBlock) forms its instants'
+// records in LDS and streams the block's CSR range, so the FDISC records never go through HBM and no record launch
+// precedes the composition. The block stages its constraint's blob (the two splines' PolyPhases, the force PhaseCols,
+// the template and window table) and gathers the local x (the motion and force splines' node values, the schedule
+// variables), forms the two splines' polynomial durations and running sums and the phase ends (the same operations as
+// phase_timings_block), then kFfLanes lanes per instant evaluate fdisc_record's quantities in four stages with the
+// same functions (locate_poly / phase_cur, poly_state_dim per dimension, hermite_dpos, sched_dx_dim per dimension,
+// ter_nbasis + pyramid, phase_basis_sum per window position, dot3 per g row), so every value is the record kernel's.
+// ------------------------------------------------------------------------------------------------
+constexpr int kFfEx = 40;        // per-instant exchange slots (doubles) between the record stages
+constexpr int kFfUnits = 8;      // 16-byte units per lane in flight while streaming
+enum { kXfT = 0, kXfTl, kXfPoly, kXmT, kXmTl, kXmPoly, kXcur, kXws, kXwd, kXFp, kXFv = kXFp + 3, kXMp = kXFv + 3,
+       kXH = kXMp + 2, kXb = kXH + 4 };
+static_assert(kXb + 15 <= kFfEx, "exchange slots");
+
+__global__ void __launch_bounds__(kFfBlock) towr_fdisc_fused_kernel(KParams P, FfArgs A) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  constexpr int BLOCK = kFfBlock;
+  const int NFS = A.nfs;
+  const int per = (int)((gridDim.x + 7) / 8);   // XCD-aware: a problem's FsBlocks on one XCD (its x from that L2)
+  const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+  const int b = w / NFS, jt = w - b * NFS;
+  if (b >= P.B) return;   // (the grid is rounded up to a multiple of 8)
+  const FsBlock fb = P.fsb[jt];
+  const FfGeo g = A.geo[fb.ff];
+  char* base = reinterpret_cast<char*>(smem);
+  int32_t* blob = reinterpret_cast<int32_t*>(base);
+  double* lx = reinterpret_cast<double*>(base + A.o_lx);
+  double* pdm = reinterpret_cast<double*>(base + A.o_tm);
+  double* pem = pdm + A.np_max;
+  double* pdf = pem + A.np_max;
+  double* pef = pdf + A.np_max;
+  double* phe = pef + A.np_max;
+  double* ex = reinterpret_cast<double*>(base + A.o_ex);
+  double* cd = reinterpret_cast<double*>(base + A.o_cd);
+  double* rowv = reinterpret_cast<double*>(base + A.o_rowv);
+  int32_t* wsr = reinterpret_cast<int32_t*>(base + A.o_wsr);
+  towr_terrain_t* ter = reinterpret_cast<towr_terrain_t*>(base + A.o_ter);
+  const int tid = threadIdx.x, kk = tid / kFfLanes, sub = tid - kk * kFfLanes;
+  const bool inst = kk < fb.n_inst;
+  const double t = inst ? P.fs_t[fb.t0 + kk] : 0.0;
+  TG_STAMP(P, 0);
+  // stage: the blob and the terrain, then the local x
+  stage16<BLOCK>(reinterpret_cast<uint4*>(blob), A.blob + g.blob0, g.blob_n16);
+  if (tid < (int)(sizeof(towr_terrain_t) / 8))
+    reinterpret_cast<double*>(ter)[tid] = reinterpret_cast<const double*>(P.terrains + (P.terrain_per_problem ? b : 0))[tid];
+  __syncthreads();
+  {
+    const double* xg = P.X + (int64_t)b * P.ldx;
+    const int32_t* gat = blob + g.o_gather;
+    for (int j = tid; j < g.nx; j += BLOCK) {
+      const int col = gat[j];
+      lx[j] = col >= 0 ? xg[col] : 0.0;
+    }
+  }
+  __syncthreads();
+  TG_STAMP(P, 1);
+  // the two splines' polynomial durations, their running sums and the phase ends (phase_timings_block's operations)
+  const PolyPhase* pim = reinterpret_cast<const PolyPhase*>(blob + g.o_pinfo);
+  const PolyPhase* pif = pim + g.np_m;
+  const double* sx = lx + 6 * (g.nm + g.nf);   // the schedule variables
+  const int nph = g.n_ph;
+  auto last_phase = [&]() { double sum = 0.0; for (int i = 0; i < nph - 1; ++i) sum += sx[i]; return g.t_total - sum; };
+  auto phase_dur = [&](int ph, double last) { return ph < nph - 1 ? sx[ph] : last; };
+  if (tid < g.np_m + g.np_f) {
+    const double last = last_phase();
+    const bool f = tid >= g.np_m;
+    const PolyPhase pp = f ? pif[tid - g.np_m] : pim[tid];
+    (f ? pdf[tid - g.np_m] : pdm[tid]) = phase_dur(pp.phase, last) / pp.n_in_phase;
+  }
+  __syncthreads();
+  auto running = [](const double* d, double* out, int n) {
+    double acc = 0.0;
+    for (int i0 = 0; i0 < n; i0 += 8) {
+      double v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = i0 + k < n ? d[i0 + k] : 0.0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (i0 + k < n) { acc += v[k]; out[i0 + k] = acc; }
+    }
+  };
+  if (tid == 0) running(pdm, pem, g.np_m);
+  else if (tid == 64) running(pdf, pef, g.np_f);
+  else if (tid == 128) {
+    const double last = last_phase();
+    double acc = 0.0;
+    for (int ph = 0; ph < nph; ++ph) { acc += phase_dur(ph, last); phe[ph] = acc; }
+  }
+  __syncthreads();
+  TG_STAMP(P, 2);
+  double* X = ex + kk * kFfEx;
+  auto iput = [](double* d, int v) { *d = __longlong_as_double((long long)v); };
+  auto iget = [](const double* d) { return (int)__double_as_longlong(*d); };
+  // stage 1: the active polynomials (force, motion) and the phase (fdisc_instant's spline_eval / sched_jac scans)
+  if (inst && sub < 3) {
+    if (sub < 2) {
+      int poly; double tl, T;
+      if (sub == 0) locate_poly(pdf, pef, g.np_f, t, poly, tl, T);
+      else locate_poly(pdm, pem, g.np_m, t, poly, tl, T);
+      const int o = sub == 0 ? kXfT : kXmT;
+      X[o] = T; X[o + 1] = tl; iput(X + o + 2, poly);
+    } else {
+      iput(X + kXcur, phase_cur(phe, nph, t));
+    }
+  }
+  __syncthreads();
+  const double* nvm = lx;                  // motion node values: node j at nvm[6 j + 3 deriv + dim]
+  const double* nvf = lx + 6 * g.nm;       // force node values
+  // stage 2: the splines' states per dimension (poly_state_dim), the force basis (hermite_dpos), the window (fs_ws)
+  if (inst && sub < 7) {
+    if (sub < 5) {
+      const bool f = sub < 3;
+      const int e = f ? sub : sub - 3, o = f ? kXfT : kXmT;
+      const int poly = iget(X + o + 2);
+      const double* nv = f ? nvf : nvm;
+      double pp, vv, aa;
+      poly_state_dim(nv[6 * poly + e], nv[6 * poly + 3 + e], nv[6 * poly + 6 + e], nv[6 * poly + 9 + e], X[o], X[o + 1], pp, vv, aa);
+      if (f) { X[kXFp + e] = pp; X[kXFv + e] = vv; }
+      else X[kXMp + e] = pp;
+    } else if (sub == 5) {
+      double H[4];
+      hermite_dpos(X[kXfT], X[kXfTl], H);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) X[kXH + q] = H[q];
+    } else {
+      const int32_t* ws = blob + g.o_ws + 2 * iget(X + kXfPoly);
+      iput(X + kXws, ws[0]);
+      iput(X + kXwd, ws[1]);
+    }
+  }
+  __syncthreads();
+  // stage 3: the record fields (fdisc_record): d force / d schedule per dimension, the pyramid rows, the window sums
+  double* R = cd + kk * kFsCS;
+  if (inst) {
+    const int poly = iget(X + kXfPoly);
+    if (sub < 3) {
+      const int k = sub;
+      R[kFsDx + k] = sched_dx_dim(nvf[6 * poly + k], nvf[6 * poly + 3 + k], nvf[6 * poly + 6 + k], nvf[6 * poly + 9 + k], X[kXfT], X[kXfTl],
+                                  X[kXFv + k], pif[poly]);
+      R[kFsV + k] = X[kXFv + k];
+      if (k == 0) { R[kFsND] = X[kXws]; R[kFsND + 1] = X[kXwd]; R[kFsND + 2] = X[kXcur]; }
+    } else if (sub == 3) {
+      double nb[3][3], bb[5][3];
+      ter_nbasis(*ter, 0, X[kXMp], X[kXMp + 1], nb[0]);
+      ter_nbasis(*ter, 1, X[kXMp], X[kXMp + 1], nb[1]);
+      ter_nbasis(*ter, 2, X[kXMp], X[kXMp + 1], nb[2]);
+      pyramid(nb[0], nb[1], nb[2], ter->friction_coeff, bb);
+#pragma unroll
+      for (int i = 0; i < 5; ++i)
+#pragma unroll
+        for (int e = 0; e < 3; ++e) { R[kFsB + 3 * i + e] = bb[i][e]; X[kXb + 3 * i + e] = bb[i][e]; }
+    } else {   // window position q (emit_dim's basis sum of the template column there; 0 past the row)
+      const int q = sub - 4, pos = iget(X + kXws) + q;
+      const int32_t te = pos < g.L ? blob[g.o_tmpl + pos] : -1;
+      double h0 = X[kXH], h1 = X[kXH + 1], h2 = X[kXH + 2], h3 = X[kXH + 3];
+      const PhaseCol* pc = reinterpret_cast<const PhaseCol*>(blob + g.o_pcols);
+      R[q] = te >= 0 ? phase_basis_sum(pc[te & 0xFFFFFF], poly, h0, h1, h2, h3) : 0.0;
+    }
+  }
+  __syncthreads();
+  // the instant's 5 g rows (fdisc_instant: F . b_i)
+  if (inst && sub < 5 && P.want_g) {
+    const double Fp[3] = {X[kXFp], X[kXFp + 1], X[kXFp + 2]}, bi[3] = {X[kXb + 3 * sub], X[kXb + 3 * sub + 1], X[kXb + 3 * sub + 2]};
+    __builtin_nontemporal_store(dot3(Fp, bi), P.G + (int64_t)b * P.ldg + fb.r0 + 5 * kk + sub);
+  }
+  TG_STAMP(P, 3);
+  if (!P.want_jac) return;
+  fs_rows<BLOCK>(fb, cd, rowv, wsr);
+  __syncthreads();
+  fs_stream<BLOCK, kFfUnits>(P, fb, b, cd, rowv, wsr);
+  TG_STAMP(P, 4);
+}
 
 constexpr int kGsUnits = 4;
 template <int CLS, int BLOCK>
@@ -709,6 +899,26 @@ const void* gait_compose_kernel(int mask) {
     case 23: return compose_fn<23>();
     default: return compose_fn<31>();
   }
+}
+const void* fdisc_fused_kernel() { return reinterpret_cast<const void*>(&towr_fdisc_fused_kernel); }
+// the fused kernel's LDS layout (bytes): [blob | local x | timings | exchange | records | row windows | window starts |
+// terrain]; offsets into A, returns the total
+size_t ff_lds(const Layout& L, FfArgs* A) {
+  auto a16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+  size_t o = a16(16 * (size_t)L.ff_blob_max16);
+  const size_t o_lx = o; o = a16(o + 8 * (size_t)(L.ff_nx_max + 1));
+  const size_t o_tm = o; o = a16(o + 8 * (size_t)(4 * L.ff_np_max + L.ff_ph_max));
+  const size_t o_ex = o; o = a16(o + 8 * (size_t)kFsInst * kFfEx);
+  const size_t o_cd = o; o = a16(o + 8 * (size_t)kFsInst * kFsCS);
+  const size_t o_rowv = o; o = a16(o + 8 * (size_t)5 * kFsInst * kFsWin);
+  const size_t o_wsr = o; o = a16(o + 4 * (size_t)5 * kFsInst);
+  const size_t o_ter = o; o = a16(o + sizeof(towr_terrain_t));
+  if (A) {
+    A->np_max = L.ff_np_max; A->ph_max = L.ff_ph_max;
+    A->o_lx = (int32_t)o_lx; A->o_tm = (int32_t)o_tm; A->o_ex = (int32_t)o_ex; A->o_cd = (int32_t)o_cd;
+    A->o_rowv = (int32_t)o_rowv; A->o_wsr = (int32_t)o_wsr; A->o_ter = (int32_t)o_ter;
+  }
+  return o;
 }
 size_t fs_compose_lds(const Layout& L) {   // records, row window values, row window starts
   return sizeof(double) * ((size_t)(((kFsInst * kFsCS + 1) & ~1) + 5 * kFsInst * kFsWin + (5 * kFsInst + 1) / 2 + 1) & ~(size_t)1);

@@ -251,10 +251,11 @@ __device__ __forceinline__ void stage_x_spans(const KParams& P, const double* xg
 
 // The x-dependent PhaseSpline timings of one problem (phase_spline_timings / phase_end_timings: pdur, pend per
 // polynomial, phend per (endeffector, phase)) by the whole block: (1) each endeffector's last phase duration,
-// parked in its phend slot; (2) one thread per polynomial forms its duration (the divisions in parallel);
-// (3) one thread per spline / endeffector forms the running sums in the reference's order. Every value is the
-// one thread-per-spline loop's (same operations, same order); with one thread per spline the prologue took ~4 us
-// of a ~30 us record block (MI355X, ANYmal gait, per-block timestamps).
+// parked in its phend slot; (2) one thread per polynomial forms its duration (the divisions in parallel; the entry's
+// spline from PolyPhase::spl); (3) one thread per spline / endeffector forms the running sums in the reference's order,
+// its operands loaded 8 at a time ahead of the dependent additions. Every value is the one thread-per-spline loop's
+// (same operations, same order). MI355X, ANYmal gait, B = 1024 (tools/stamps.py): this prologue took 5.3 us of a
+// 27 us record block with a per-entry scan over the splines and one LDS round trip per running-sum step.
 __device__ __forceinline__ void phase_timings_block(const Ctx& c, const KParams& P, double* tm) {
   double* pdur = tm;
   double* pend = tm + P.n_pinfo;
@@ -266,38 +267,41 @@ __device__ __forceinline__ void phase_timings_block(const Ctx& c, const KParams&
   }
   __syncthreads();
   for (int i = tid; i < P.n_pinfo; i += blockDim.x) {
-    int s = 0;
-    for (int q = 0; q < nspl; ++q) {
-      const SplineMeta& m = c.spl[q];
-      if (m.ee >= 0 && i >= m.pinfo_off && i < m.pinfo_off + m.n_polys) s = q;
-    }
-    const SplineMeta m = c.spl[s];
+    const SplineMeta m = c.spl[c.pinfo[i].spl];
     const SchedInfo si = c.sched[m.ee];
-    if (i >= m.pinfo_off && i < m.pinfo_off + m.n_polys && m.ee >= 0) {
-      const double last = si.col0 >= 0 ? phend[m.ee * P.ph_stride + si.n_phases - 1] : last_phase_duration(c, si);
-      pdur[i] = phase_poly_duration(c, m, si, last, i - m.pinfo_off);
-    }
+    const double last = si.col0 >= 0 ? phend[m.ee * P.ph_stride + si.n_phases - 1] : last_phase_duration(c, si);
+    pdur[i] = phase_poly_duration(c, m, si, last, i - m.pinfo_off);
   }
   __syncthreads();
+  // running sums t += d[i] in order; the loads of a group of 8 issue together
+  auto running = [](const double* d, double* out, int n, double t) {
+    for (int i0 = 0; i0 < n; i0 += 8) {
+      double v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = i0 + k < n ? d[i0 + k] : 0.0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (i0 + k < n) { t += v[k]; out[i0 + k] = t; }
+    }
+  };
   if (tid < nspl) {
     const SplineMeta m = c.spl[tid];
-    if (m.ee >= 0) {
-      double t = 0.0;
-      for (int i = 0; i < m.n_polys; ++i) {
-        t += pdur[m.pinfo_off + i];
-        pend[m.pinfo_off + i] = t;
-      }
-    }
+    if (m.ee >= 0) running(pdur + m.pinfo_off, pend + m.pinfo_off, m.n_polys, 0.0);
   } else if (tid < nspl + nee) {
     const int ee = tid - nspl;
     const SchedInfo si = c.sched[ee];
     if (si.col0 >= 0) {
+      // phase_duration: the schedule variables x[col0 ..], then the last phase (parked in ph[n - 1] by step 1)
       double* ph = phend + ee * P.ph_stride;
       const double last = ph[si.n_phases - 1];
       double acc = 0.0;
-      for (int k = 0; k < si.n_phases; ++k) {
-        acc += phase_duration(c, si, last, k);
-        ph[k] = acc;
+      for (int k0 = 0; k0 < si.n_phases; k0 += 8) {
+        double v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = k0 + k < si.n_phases ? phase_duration(c, si, last, k0 + k) : 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (k0 + k < si.n_phases) { acc += v[k]; ph[k0 + k] = acc; }
       }
     }
   }

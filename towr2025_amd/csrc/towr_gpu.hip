@@ -64,6 +64,9 @@ struct towr_gpu_handle_s {
   CostItem* d_citems = nullptr;
   double* d_cq = nullptr;
   FsBlock* d_fsb = nullptr;    // streaming ForceConstraintDiscretized tables (layout.h FsBlock)
+  FfGeo* d_ff_geo = nullptr;   // the fused FDISC kernel's per-constraint tables (layout.h FfGeo)
+  uint4* d_ff_blob = nullptr;
+  bool ff = false;             // the big-batch FDISC chain is the fused kernel (TOWR_GPU_FDISC_FUSED=0: records + compose)
   double* d_fs_t = nullptr;
   int32_t* d_fs_tmpl = nullptr;
   int32_t* d_fs_ws = nullptr;
@@ -121,6 +124,7 @@ struct towr_gpu_handle_s {
   int n_side = 0;
   hipStream_t side[kMaxSide] = {};
   hipEvent_t fork = nullptr, join[kMaxSide] = {};
+  bool rv_overlap = false;   // RotVec without fusion groups: Dynamic and the small kinds on side stream 0 (launch_classes)
   towr_terrain_t* d_terrain = nullptr;      // base terrain (1 entry)
   towr_terrain_t* d_bterrain = nullptr;     // per-problem batch terrains
   int32_t bterrain_n = 0;
@@ -607,13 +611,30 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
     return TOWR_OK;
   };
   const int fpart = fs ? kRecFdisc : 0;
+  // the fused FDISC kernel (h->ff): records formed in LDS by the blocks that compose them
+  auto fused = [&](hipStream_t s) -> int {
+    FfArgs A{};
+    const size_t lds = ff_lds(L, &A);
+    A.geo = h->d_ff_geo; A.blob = h->d_ff_blob; A.nfs = (int32_t)L.fs_blocks.size();
+    const int64_t grid = ((int64_t)P.B * A.nfs + 7) / 8 * 8;   // whole rounds of 8 (XCD-aware mapping)
+    if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
+    void* a[] = {&P, &A};
+    HIPCHK(h, launch_kernel(fdisc_fused_kernel(), dim3((unsigned)grid), dim3(kFfBlock), a, lds, s));
+    return TOWR_OK;
+  };
   if (big) {   // (without a side stream the two chains run one after the other on the caller's stream)
     if (tq3) {
       if (int rc = records({kRecTq}, tst)) return rc;
       if (int rc = compose(false, true, false, false, false, tst)) return rc;
     }
     const bool tqf = tq && !tq3;   // TQDISC in the FDISC chain
-    if (fs || tqf) {
+    if (fs && h->ff) {
+      if (int rc = fused(fst)) return rc;
+      if (tqf) {
+        if (int rc = records({kRecTq}, fst)) return rc;
+        if (int rc = compose(false, true, false, false, false, fst)) return rc;
+      }
+    } else if (fs || tqf) {
       // (the FDISC records in two blocks per problem, each half the instants: 0.638 vs 0.629 ms, not kept)
       if (int rc = records({fpart, tqf ? kRecTq : 0}, fst)) return rc;
       if (int rc = compose(fs, tqf, false, false, false, fst)) return rc;
@@ -635,7 +656,8 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
   return TOWR_OK;
 }
 
-bool uses_scratch(const Layout& L) { return L.fstream || L.gstream[GS_ROM] || L.gstream[GS_DYN] || L.gstream[GS_TQ] || !L.rv_inst.empty(); }
+bool gait_streamed(const Layout& L) { return L.fstream || L.gstream[GS_ROM] || L.gstream[GS_DYN] || L.gstream[GS_TQ]; }
+bool uses_scratch(const Layout& L) { return gait_streamed(L) || !L.rv_inst.empty(); }
 
 int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, int64_t ldg, double* V, int64_t ldv,
                    int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem, int only_class);
@@ -663,7 +685,10 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
   // a batch with fusion groups: the other classes on the side streams beside the fused launches (forked before
   // them: the fused launch on the caller's stream, Dynamic then the small kinds on side stream 0); at small B the
   // fork and join cost more than the overlap gains
-  const bool overlap = only_class < 0 && h->n_side > 0 && h->n_fuse > 0 && !uses_scratch(L) && B >= kSplitBatch;
+  // RotVec layouts (per-class launches, no fusion group): RangeOfMotion and FDISC on the caller's stream, the coefficient
+  // pre-pass, Dynamic and the small kinds on side stream 0 beside them (h->rv_overlap)
+  const bool rv_side = h->rv_overlap && h->n_fuse == 0;
+  const bool overlap = only_class < 0 && h->n_side > 0 && (h->n_fuse > 0 || rv_side) && !gait_streamed(L) && B >= kSplitBatch;
   if (overlap) {
     HIPCHK(h, hipEventRecord(h->fork, s));
     for (int i = 0; i < h->n_side; ++i) HIPCHK(h, hipStreamWaitEvent(h->side[i], h->fork, 0));
@@ -692,7 +717,9 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
     const int lc = order[q];
     if (lc == LC_MISC && misc_done) continue;   // in the streaming path's composer launch
     const int nt = class_units(L, lc);
-    const hipStream_t st = stream_forked ? s : overlap ? h->side[q % nside] : (nside > 0 && q % (nside + 1) != 0) ? h->side[q % (nside + 1) - 1] : s;
+    const hipStream_t st = stream_forked ? s
+                         : overlap ? ((rv_side && lc != LC_DYN && lc != LC_MISC) ? s : h->side[q % nside])
+                         : (nside > 0 && q % (nside + 1) != 0) ? h->side[q % (nside + 1) - 1] : s;
     KParams P{};
     fill_common(h, P, B, X, ldx, G, ldg, V, ldv, want_g, want_jac, terrains, per_problem);
     P.ntiles = nt;
@@ -1155,6 +1182,7 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
       (r = upload(h, &h->d_citems, L.cost_items)) || (r = upload(h, &h->d_cq, L.cost_q)) || (r = upload(h, &h->d_gtab, gait_blob(L))) ||
       (r = upload(h, &h->d_idir, L.idirect)) || (r = upload(h, &h->d_fsb, L.fs_blocks)) || (r = upload(h, &h->d_fs_t, L.fs_t)) ||
       (r = upload(h, &h->d_fs_tmpl, L.fs_tmpl)) || (r = upload(h, &h->d_fs_ws, L.fs_ws)) ||
+      (r = upload(h, &h->d_ff_geo, L.ff_geo)) || (r = upload(h, &h->d_ff_blob, L.ff_blob)) ||
       (r = upload(h, &h->d_fs_iee, L.fs_iee)) || (r = upload(h, &h->d_fs_irow, L.fs_irow)) || (r = upload(h, &h->d_fs_iblk, L.fs_iblk)) ||
       (r = upload(h, &h->d_gs_geo, L.gs_geo)) || (r = upload(h, &h->d_gs_tmpl, L.gs_tmpl)) || (r = upload(h, &h->d_gs_pcode, L.gs_pcode)) ||
       (r = upload(h, &h->d_gs_blk[GS_ROM], L.gs_blocks[GS_ROM])) || (r = upload(h, &h->d_gs_blk[GS_DYN], L.gs_blocks[GS_DYN])) ||
@@ -1217,7 +1245,9 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
     // streaming path) one or two side streams: the write-bound compose launches run beside the latency-bound
     // record work (launch_stream_path).
     const bool streamed = h->L.gait && (h->L.fstream || h->L.gstream[GS_TQ]);
-    const int want = ns ? std::atoi(ns) - 1 : streamed ? (h->L.gstream[GS_TQ] ? 2 : 1) : h->n_fuse > 0 ? 1 : 0;
+    const char* rvo = std::getenv("TOWR_GPU_ROTVEC_OVERLAP");
+    h->rv_overlap = h->L.rotvec && !(rvo && std::strcmp(rvo, "0") == 0);
+    const int want = ns ? std::atoi(ns) - 1 : streamed ? (h->L.gstream[GS_TQ] ? 2 : 1) : (h->n_fuse > 0 || h->rv_overlap) ? 1 : 0;
     h->n_side = std::max(0, std::min(towr_gpu_handle_s::kMaxSide, want));
     if (h->n_side > 0 && hipEventCreateWithFlags(&h->fork, hipEventDisableTiming) != hipSuccess) { h->err = "hipEventCreate failed"; return bail(TOWR_ERR_HIP); }
     // side streams at the device's greatest priority: the streaming path runs its critical chains there (the
@@ -1256,6 +1286,14 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
       h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
     }
   }
+  {
+    const char* ffe = std::getenv("TOWR_GPU_FDISC_FUSED");
+    h->ff = L.fstream && !L.ff_geo.empty() && !(ffe && std::strcmp(ffe, "0") == 0) && ff_lds(L, nullptr) <= kLdsMax;
+    if (h->ff && ff_lds(L, nullptr) > 64 * 1024 &&
+        hipFuncSetAttribute(fdisc_fused_kernel(), hipFuncAttributeMaxDynamicSharedMemorySize, (int)ff_lds(L, nullptr)) != hipSuccess) {
+      h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
+    }
+  }
   if (L.fstream || L.gstream[GS_ROM] || L.gstream[GS_DYN] || L.gstream[GS_TQ]) {   // the record kernels share fs_inst_lds_bytes' layout
     // (fixed-gait RotVec also uses scratch, for its coefficient pre-pass, but launches no record kernel)
     const size_t lds = fs_inst_lds_bytes(L);
@@ -1288,7 +1326,7 @@ int towr_gpu_destroy(towr_gpu_handle h) {
   void* dev[] = {h->d_items, h->d_slots, h->d_tiles, h->d_nodecol, h->d_spl, h->d_dur, h->d_segs, h->d_terrain,
                  h->d_pinfo, h->d_pcols, h->d_pact, h->d_sched, h->d_misc, h->d_misc_lds, h->d_xspan, h->d_eelin, h->d_gtab, h->d_idir, h->d_citems, h->d_cq, h->fuse[0].d_units, h->fuse[1].d_units,
                  h->d_bterrain, h->d_x, h->d_g, h->d_v, h->d_f, h->d_grad,
-                 h->d_traj_pd, h->d_traj_n, h->d_traj_c0, h->d_traj_t, h->d_fsb, h->d_fs_t, h->d_fs_tmpl, h->d_fs_ws,
+                 h->d_traj_pd, h->d_traj_n, h->d_traj_c0, h->d_traj_t, h->d_fsb, h->d_fs_t, h->d_fs_tmpl, h->d_fs_ws, h->d_ff_geo, h->d_ff_blob,
                  h->d_fs_iee, h->d_fs_irow, h->d_fs_iblk, h->d_fsrec, h->d_lin, h->d_soft_b, h->d_soft_rp, h->d_soft_col, h->d_sg, h->d_sv,
                  h->single.d_units, h->d_gs_geo, h->d_gs_tmpl, h->d_gs_pcode, h->d_gs_blk[0], h->d_gs_blk[1], h->d_gs_blk[2],
                  h->d_gs_inst[0], h->d_gs_inst[1], h->d_gs_inst[2], h->d_gsrec, h->d_rvc, h->d_rvi, h->d_gs_segs, h->d_gs_tseg, h->d_gs_vmap, h->d_gs_ws, h->d_gs_blob};
