@@ -545,11 +545,7 @@ __device__ __forceinline__ void fdisc_compose(const KParams& P, const double* re
 // same functions (locate_poly / phase_cur, poly_state_dim per dimension, hermite_dpos, sched_dx_dim per dimension,
 // ter_nbasis + pyramid, phase_basis_sum per window position, dot3 per g row), so every value is the record kernel's.
 // ------------------------------------------------------------------------------------------------
-constexpr int kFfEx = 40;        // per-instant exchange slots (doubles) between the record stages
 constexpr int kFfUnits = 8;      // 16-byte units per lane in flight while streaming
-enum { kXfT = 0, kXfTl, kXfPoly, kXmT, kXmTl, kXmPoly, kXcur, kXws, kXwd, kXFp, kXFv = kXFp + 3, kXMp = kXFv + 3,
-       kXH = kXMp + 2, kXb = kXH + 4 };
-static_assert(kXb + 15 <= kFfEx, "exchange slots");
 
 __global__ void __launch_bounds__(kFfBlock) towr_fdisc_fused_kernel(KParams P, FfArgs A) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -560,33 +556,37 @@ __global__ void __launch_bounds__(kFfBlock) towr_fdisc_fused_kernel(KParams P, F
   const int b = w / NFS, jt = w - b * NFS;
   if (b >= P.B) return;   // (the grid is rounded up to a multiple of 8)
   const FsBlock fb = P.fsb[jt];
-  const FfGeo g = A.geo[fb.ff];
   char* base = reinterpret_cast<char*>(smem);
+  FfView v;
+  v.g = A.geo[fb.ff];
   int32_t* blob = reinterpret_cast<int32_t*>(base);
   double* lx = reinterpret_cast<double*>(base + A.o_lx);
-  double* pdm = reinterpret_cast<double*>(base + A.o_tm);
-  double* pem = pdm + A.np_max;
-  double* pdf = pem + A.np_max;
-  double* pef = pdf + A.np_max;
-  double* phe = pef + A.np_max;
+  v.blob = blob;
+  v.lx = lx;
+  v.pdm = reinterpret_cast<double*>(base + A.o_tm);
+  v.pem = v.pdm + A.np_max;
+  v.pdf = v.pem + A.np_max;
+  v.pef = v.pdf + A.np_max;
+  v.phe = v.pef + A.np_max;
+  towr_terrain_t* ter = reinterpret_cast<towr_terrain_t*>(base + A.o_ter);
+  v.ter = ter;
   double* ex = reinterpret_cast<double*>(base + A.o_ex);
   double* cd = reinterpret_cast<double*>(base + A.o_cd);
   double* rowv = reinterpret_cast<double*>(base + A.o_rowv);
   int32_t* wsr = reinterpret_cast<int32_t*>(base + A.o_wsr);
-  towr_terrain_t* ter = reinterpret_cast<towr_terrain_t*>(base + A.o_ter);
   const int tid = threadIdx.x, kk = tid / kFfLanes, sub = tid - kk * kFfLanes;
   const bool inst = kk < fb.n_inst;
   const double t = inst ? P.fs_t[fb.t0 + kk] : 0.0;
   TG_STAMP(P, 0);
-  // stage: the blob and the terrain, then the local x
-  stage16<BLOCK>(reinterpret_cast<uint4*>(blob), A.blob + g.blob0, g.blob_n16);
+  // stage the blob and the terrain, then gather the local x
+  stage16<BLOCK>(reinterpret_cast<uint4*>(blob), A.blob + v.g.blob0, v.g.blob_n16);
   if (tid < (int)(sizeof(towr_terrain_t) / 8))
     reinterpret_cast<double*>(ter)[tid] = reinterpret_cast<const double*>(P.terrains + (P.terrain_per_problem ? b : 0))[tid];
   __syncthreads();
   {
     const double* xg = P.X + (int64_t)b * P.ldx;
-    const int32_t* gat = blob + g.o_gather;
-    for (int j = tid; j < g.nx; j += BLOCK) {
+    const int32_t* gat = blob + v.g.o_gather;
+    for (int j = tid; j < v.g.nx; j += BLOCK) {
       const int col = gat[j];
       lx[j] = col >= 0 ? xg[col] : 0.0;
     }
@@ -594,114 +594,20 @@ __global__ void __launch_bounds__(kFfBlock) towr_fdisc_fused_kernel(KParams P, F
   __syncthreads();
   TG_STAMP(P, 1);
   // the two splines' polynomial durations, their running sums and the phase ends (phase_timings_block's operations)
-  const PolyPhase* pim = reinterpret_cast<const PolyPhase*>(blob + g.o_pinfo);
-  const PolyPhase* pif = pim + g.np_m;
-  const double* sx = lx + 6 * (g.nm + g.nf);   // the schedule variables
-  const int nph = g.n_ph;
-  auto last_phase = [&]() { double sum = 0.0; for (int i = 0; i < nph - 1; ++i) sum += sx[i]; return g.t_total - sum; };
-  auto phase_dur = [&](int ph, double last) { return ph < nph - 1 ? sx[ph] : last; };
-  if (tid < g.np_m + g.np_f) {
-    const double last = last_phase();
-    const bool f = tid >= g.np_m;
-    const PolyPhase pp = f ? pif[tid - g.np_m] : pim[tid];
-    (f ? pdf[tid - g.np_m] : pdm[tid]) = phase_dur(pp.phase, last) / pp.n_in_phase;
-  }
+  if (tid < v.g.np_m + v.g.np_f) ff_pdur(v, tid);
   __syncthreads();
-  auto running = [](const double* d, double* out, int n) {
-    double acc = 0.0;
-    for (int i0 = 0; i0 < n; i0 += 8) {
-      double v[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = i0 + k < n ? d[i0 + k] : 0.0;
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (i0 + k < n) { acc += v[k]; out[i0 + k] = acc; }
-    }
-  };
-  if (tid == 0) running(pdm, pem, g.np_m);
-  else if (tid == 64) running(pdf, pef, g.np_f);
-  else if (tid == 128) {
-    const double last = last_phase();
-    double acc = 0.0;
-    for (int ph = 0; ph < nph; ++ph) { acc += phase_dur(ph, last); phe[ph] = acc; }
-  }
+  if ((tid & 63) == 0 && tid < 192) ff_sums(v, tid >> 6);   // one wave each
   __syncthreads();
   TG_STAMP(P, 2);
   double* X = ex + kk * kFfEx;
-  auto iput = [](double* d, int v) { *d = __longlong_as_double((long long)v); };
-  auto iget = [](const double* d) { return (int)__double_as_longlong(*d); };
-  // stage 1: the active polynomials (force, motion) and the phase (fdisc_instant's spline_eval / sched_jac scans)
-  if (inst && sub < 3) {
-    if (sub < 2) {
-      int poly; double tl, T;
-      if (sub == 0) locate_poly(pdf, pef, g.np_f, t, poly, tl, T);
-      else locate_poly(pdm, pem, g.np_m, t, poly, tl, T);
-      const int o = sub == 0 ? kXfT : kXmT;
-      X[o] = T; X[o + 1] = tl; iput(X + o + 2, poly);
-    } else {
-      iput(X + kXcur, phase_cur(phe, nph, t));
-    }
-  }
-  __syncthreads();
-  const double* nvm = lx;                  // motion node values: node j at nvm[6 j + 3 deriv + dim]
-  const double* nvf = lx + 6 * g.nm;       // force node values
-  // stage 2: the splines' states per dimension (poly_state_dim), the force basis (hermite_dpos), the window (fs_ws)
-  if (inst && sub < 7) {
-    if (sub < 5) {
-      const bool f = sub < 3;
-      const int e = f ? sub : sub - 3, o = f ? kXfT : kXmT;
-      const int poly = iget(X + o + 2);
-      const double* nv = f ? nvf : nvm;
-      double pp, vv, aa;
-      poly_state_dim(nv[6 * poly + e], nv[6 * poly + 3 + e], nv[6 * poly + 6 + e], nv[6 * poly + 9 + e], X[o], X[o + 1], pp, vv, aa);
-      if (f) { X[kXFp + e] = pp; X[kXFv + e] = vv; }
-      else X[kXMp + e] = pp;
-    } else if (sub == 5) {
-      double H[4];
-      hermite_dpos(X[kXfT], X[kXfTl], H);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) X[kXH + q] = H[q];
-    } else {
-      const int32_t* ws = blob + g.o_ws + 2 * iget(X + kXfPoly);
-      iput(X + kXws, ws[0]);
-      iput(X + kXwd, ws[1]);
-    }
-  }
-  __syncthreads();
-  // stage 3: the record fields (fdisc_record): d force / d schedule per dimension, the pyramid rows, the window sums
   double* R = cd + kk * kFsCS;
-  if (inst) {
-    const int poly = iget(X + kXfPoly);
-    if (sub < 3) {
-      const int k = sub;
-      R[kFsDx + k] = sched_dx_dim(nvf[6 * poly + k], nvf[6 * poly + 3 + k], nvf[6 * poly + 6 + k], nvf[6 * poly + 9 + k], X[kXfT], X[kXfTl],
-                                  X[kXFv + k], pif[poly]);
-      R[kFsV + k] = X[kXFv + k];
-      if (k == 0) { R[kFsND] = X[kXws]; R[kFsND + 1] = X[kXwd]; R[kFsND + 2] = X[kXcur]; }
-    } else if (sub == 3) {
-      double nb[3][3], bb[5][3];
-      ter_nbasis(*ter, 0, X[kXMp], X[kXMp + 1], nb[0]);
-      ter_nbasis(*ter, 1, X[kXMp], X[kXMp + 1], nb[1]);
-      ter_nbasis(*ter, 2, X[kXMp], X[kXMp + 1], nb[2]);
-      pyramid(nb[0], nb[1], nb[2], ter->friction_coeff, bb);
-#pragma unroll
-      for (int i = 0; i < 5; ++i)
-#pragma unroll
-        for (int e = 0; e < 3; ++e) { R[kFsB + 3 * i + e] = bb[i][e]; X[kXb + 3 * i + e] = bb[i][e]; }
-    } else {   // window position q (emit_dim's basis sum of the template column there; 0 past the row)
-      const int q = sub - 4, pos = iget(X + kXws) + q;
-      const int32_t te = pos < g.L ? blob[g.o_tmpl + pos] : -1;
-      double h0 = X[kXH], h1 = X[kXH + 1], h2 = X[kXH + 2], h3 = X[kXH + 3];
-      const PhaseCol* pc = reinterpret_cast<const PhaseCol*>(blob + g.o_pcols);
-      R[q] = te >= 0 ? phase_basis_sum(pc[te & 0xFFFFFF], poly, h0, h1, h2, h3) : 0.0;
-    }
-  }
+  if (inst && sub < 3) ff_stage1(v, t, sub, X);
   __syncthreads();
-  // the instant's 5 g rows (fdisc_instant: F . b_i)
-  if (inst && sub < 5 && P.want_g) {
-    const double Fp[3] = {X[kXFp], X[kXFp + 1], X[kXFp + 2]}, bi[3] = {X[kXb + 3 * sub], X[kXb + 3 * sub + 1], X[kXb + 3 * sub + 2]};
-    __builtin_nontemporal_store(dot3(Fp, bi), P.G + (int64_t)b * P.ldg + fb.r0 + 5 * kk + sub);
-  }
+  if (inst && sub < 7) ff_stage2(v, sub, X);
+  __syncthreads();
+  if (inst) ff_stage3(v, sub, X, R);
+  __syncthreads();
+  if (inst && sub < 5 && P.want_g) __builtin_nontemporal_store(ff_g(X, sub), P.G + (int64_t)b * P.ldg + fb.r0 + 5 * kk + sub);
   TG_STAMP(P, 3);
   if (!P.want_jac) return;
   fs_rows<BLOCK>(fb, cd, rowv, wsr);
