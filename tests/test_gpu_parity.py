@@ -373,9 +373,9 @@ def test_batch_device_gait_optimization():
 
 
 def test_batch_device_gait_two_chains(monkeypatch):
-    """The phase-duration path at B >= kSplitBatch (64) runs two chains (FDISC: the fused kernel, on the
-    high-priority side stream 0; RangeOfMotion / Dynamic records + composes on the caller's stream), below it one
-    serial chain of record and compose launches (towr_gpu.hip launch_stream_path). B = 601 (odd: a compose block's problem pair is ragged) against the same problems
+    """The phase-duration path at B >= kSplitBatch (64) runs two chains (FDISC records + compose on the
+    high-priority side stream 0, RangeOfMotion / Dynamic records + composes on the caller's stream), below it one
+    serial chain (towr_gpu.hip launch_stream_path). B = 601 (odd: a compose block's problem pair is ragged) against the same problems
     as batches of 37 and 1 (37 < 64: the serial chain): bit-identical, nothing written past m / nnz, a
     sample against the oracle."""
     import torch
@@ -405,9 +405,9 @@ def test_batch_device_gait_two_chains(monkeypatch):
         np.testing.assert_array_equal(G[s:e, :p.m], g.cpu().numpy(), err_msg=f"g of problems [{s}, {e})")
         np.testing.assert_array_equal(V[s:e, :p.nnz], v.cpu().numpy(), err_msg=f"J of problems [{s}, {e})")
     # one launch stream (TOWR_GPU_STREAMS=1, read at handle creation): the two chains one after the other
-    # and the FDISC chain as records + compose instead of the fused kernel (TOWR_GPU_FDISC_FUSED=0); the batches of
-    # 37 above run below kSplitBatch, on the records + compose path, so they pin the fused kernel too
-    for var, val in (("TOWR_GPU_STREAMS", "1"), ("TOWR_GPU_FDISC_FUSED", "0")):
+    # and the FDISC chain as the fused kernel (TOWR_GPU_FDISC_FUSED=1, gstream.hip towr_fdisc_fused_kernel) instead of
+    # records + compose
+    for var, val in (("TOWR_GPU_STREAMS", "1"), ("TOWR_GPU_FDISC_FUSED", "1")):
         monkeypatch.setenv(var, val)
         q = TowrGpuProblem(desc)
         monkeypatch.delenv(var)

@@ -12,7 +12,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-REGION, NREG = 1 << 20, 16
+REGION, NREG = 1 << 21, 12
 TICK_US = 0.01   # s_memrealtime: 100 MHz
 
 
@@ -62,7 +62,11 @@ def main():
         names.append(n.decode().replace("void tg::(anonymous namespace)::", "").split("(")[0])
     lib.towr_gpu_debug_stamps(None)
     S = buf.cpu().numpy().reshape(NREG, -1, 8, 8)   # region, block, wave, phase
-    t0 = min(int(S[i][S[i] > 0].min()) for i in range(len(names)) if (S[i] > 0).any())
+    starts = [int(S[i][S[i] > 0].min()) for i in range(len(names)) if (S[i] > 0).any()]
+    if not starts:
+        print("no stamps recorded (launches: %s)" % names)
+        return
+    t0 = min(starts)
     for i, nm in enumerate(names):
         R = S[i]
         used = (R[:, :, :] > 0).any(axis=(1, 2))

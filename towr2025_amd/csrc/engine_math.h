@@ -250,6 +250,10 @@ TG_HD int basis_col(const Ctx& c, int s, int poly, int b, int e) {
 // formulas cancel (polynomial state, d pos / d duration), so that the engine reproduces them.
 TG_HD double cpow(double x, int k) {
 #if defined(__HIP_DEVICE_COMPILE__)
+  // no contraction: the double-double steps are exact only as written (p + e with p = hi * x contracted to
+  // fma(hi, x, e) changes the result, and whether the compiler contracts it depended on the kernel cpow was inlined
+  // into: the fused FDISC kernel and the record kernel gave force velocities 1 ulp apart)
+#pragma clang fp contract(off)
   if (k == 0) return 1.0;
   double hi = x, lo = 0.0;
   for (int i = 1; i < k; ++i) {

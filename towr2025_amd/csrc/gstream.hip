@@ -427,12 +427,17 @@ __device__ __forceinline__ void fs_rows(const FsBlock& fb, const double* cd, dou
 template <int BLOCK, int UNITS>
 __device__ __forceinline__ void fs_stream(const KParams& P, const FsBlock& fb, int b, const double* cd, const double* rowv,
                                           const int32_t* wsr) {
+  // no contraction: a schedule entry is a sum of three products that cancels to a rounding residue where the force is
+  // flat, and the fused / record + compose instantiations must form it with the same operations (with contraction the
+  // compiler fused different products in the two kernels: 391 of 241,250 residues differed by up to 3e-13)
+#pragma clang fp contract(off)
   const int tid = threadIdx.x;
   const int Lr = fb.L, js0 = fb.js0, ns1 = fb.ns1;
   const float invL = 1.0f / (float)Lr;   // exact row for block ranges below kFloatDivMax (layout.h, checked by build_fstream)
   auto ci = [&](int k, int f) -> int { return *reinterpret_cast<const int32_t*>(cd + k * kFsCS + kFsND + f); };
   // entry j of row r (instant k = r / 5, pyramid row i): eval_fdisc's value (see fdisc_sched_value / emit_dim)
   auto entry = [&](int r, int j) -> double {
+#pragma clang fp contract(off)   // (lambda bodies: the enclosing function's pragma is not relied on)
     const unsigned js = (unsigned)(j - js0);
     if (js < (unsigned)ns1) {   // schedule column js: sched_val per dimension, then the b-weighted sum
       const int k = r / 5, i = r - 5 * k;

@@ -176,8 +176,8 @@ int fail(towr_gpu_handle h, int code, const std::string& msg) {
 #ifdef TOWR_STAMPS
 // experiment build (tools/stamps.py): launch i after towr_gpu_debug_stamps(buf) stores its TG_STAMP slots in region i
 // of buf (kStampRegion slots each, kStampRegions regions); the kernel of each region is kept for the tool
-constexpr size_t kStampRegion = size_t(1) << 20;
-constexpr int kStampRegions = 16;
+constexpr size_t kStampRegion = size_t(1) << 21;
+constexpr int kStampRegions = 12;
 unsigned long long* g_stamps = nullptr;
 int g_stamp_n = 0;
 const void* g_stamp_fn[kStampRegions];
@@ -1255,6 +1255,8 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
     // ANYmal gait + Torque, B = 1024: the TQDISC records on a low-priority stream took 730 us instead of ~50)
     int least = 0, greatest = 0;
     if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = least = 0;
+    // (round 5, ANYmal gait, B = 1024, one box: side streams at the default priority 0.6225-0.6335 vs 0.6263-0.6371 ms
+    // per step, + Torque 1.216-1.219 vs 1.209-1.211: noise without Torque, the greatest priority kept)
     for (int i = 0; i < h->n_side; ++i)
       if (hipStreamCreateWithPriority(&h->side[i], hipStreamNonBlocking, greatest) != hipSuccess ||
           hipEventCreateWithFlags(&h->join[i], hipEventDisableTiming) != hipSuccess) {
@@ -1288,7 +1290,7 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
   }
   {
     const char* ffe = std::getenv("TOWR_GPU_FDISC_FUSED");
-    h->ff = L.fstream && !L.ff_geo.empty() && !(ffe && std::strcmp(ffe, "0") == 0) && ff_lds(L, nullptr) <= kLdsMax;
+    h->ff = L.fstream && !L.ff_geo.empty() && ffe && std::strcmp(ffe, "1") == 0 && ff_lds(L, nullptr) <= kLdsMax;
     if (h->ff && ff_lds(L, nullptr) > 64 * 1024 &&
         hipFuncSetAttribute(fdisc_fused_kernel(), hipFuncAttributeMaxDynamicSharedMemorySize, (int)ff_lds(L, nullptr)) != hipSuccess) {
       h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
