@@ -80,13 +80,14 @@ def main():
         last = np.nanmax(rel.reshape(len(R), -1), axis=1)
         print(f"{nm}: {len(R)} blocks, first start {np.nanmin(start):.1f} us, last end {np.nanmax(last):.1f} us, "
               f"block life median {np.nanmedian(last - start):.1f} p90 {np.nanpercentile(last - start, 90):.1f} us")
-        k_max = max(k for k in range(8) if not np.isnan(rel[:, :, k]).all())
-        for k in range(1, k_max + 1):
-            # phase k: from the slowest wave's stamp k-1 to the slowest wave's stamp k
-            a = np.nanmax(rel[:, :, k - 1], axis=1)
-            b = np.nanmax(rel[:, :, k], axis=1)
+        ks = [k for k in range(8) if not np.isnan(rel[:, :, k]).all()]
+        # phases between consecutive stamps in time order (the slowest wave's stamps, median over blocks)
+        ks.sort(key=lambda k: np.nanmedian(np.nanmax(rel[:, :, k], axis=1)))
+        for k0, k1 in zip(ks, ks[1:]):
+            a = np.nanmax(rel[:, :, k0], axis=1)
+            b = np.nanmax(rel[:, :, k1], axis=1)
             d = b - a
-            print(f"    phase {k - 1}->{k}: median {np.nanmedian(d):7.2f} us  p90 {np.nanpercentile(d, 90):7.2f} us")
+            print(f"    phase {k0}->{k1}: median {np.nanmedian(d):7.2f} us  p90 {np.nanpercentile(d, 90):7.2f} us")
         # start histogram: how many blocks start in each 20 us window
         h, e = np.histogram(start, bins=np.arange(0, np.nanmax(last) + 20, 20))
         print("    starts per 20 us: " + " ".join(str(x) for x in h))

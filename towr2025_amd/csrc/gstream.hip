@@ -45,9 +45,12 @@ __device__ __forceinline__ double fs_int(int v) { return __longlong_as_double((l
 struct FsTabs { const FsBlock* fsb; const int32_t* ws; const int32_t* tmpl; };
 template <class Put>
 __device__ __forceinline__ void fdisc_record(const KParams& P, const FsTabs& T, const Ctx& c, int k, double* Gb, Put&& put) {
+  // every global load of the lane before its first store: a load issued after stores waits for them (vmcnt)
+  const int row = P.want_g ? P.fs_irow[k] : 0;
+  const FsBlock fb = T.fsb[P.fs_iblk[k]];
   FdiscInstant o;
   fdisc_instant(c, P.fs_iee[k], P.fs_t[k], o);
-  const FsBlock fb = T.fsb[P.fs_iblk[k]];
+  TG_STAMP(P, 4);
 #pragma unroll
   for (int i = 0; i < 5; ++i)
 #pragma unroll
@@ -55,11 +58,10 @@ __device__ __forceinline__ void fdisc_record(const KParams& P, const FsTabs& T, 
 #pragma unroll
   for (int e = 0; e < 3; ++e) { put(kFsDx + e, o.Jf.dx[e]); put(kFsV + e, o.Jf.v[e]); }
   put(kFsND + 2, fs_int(o.Jf.cur));
-  if (P.want_g) {
-    const int row = P.fs_irow[k];
+  if (P.want_g)
 #pragma unroll
     for (int i = 0; i < 5; ++i) __builtin_nontemporal_store(o.g[i], Gb + row + i);
-  }
+  TG_STAMP(P, 5);
   const int poly = o.poly;
   const int ws = T.ws[2 * (fb.wsoff + poly)], wd = T.ws[2 * (fb.wsoff + poly) + 1];
   put(kFsND, fs_int(ws));
@@ -73,6 +75,7 @@ __device__ __forceinline__ void fdisc_record(const KParams& P, const FsTabs& T, 
     const int32_t te = pos < fb.L ? tm[pos] : -1;
     put(q, te >= 0 ? phase_basis_sum(c.pcols[te & 0xFFFFFF], poly, h0, h1, h2, h3) : 0.0);
   }
+  TG_STAMP(P, 6);
 }
 __device__ __forceinline__ void fdisc_records(const KParams& P, const FsTabs& T, const Ctx& c, int b, double* rec, int64_t ldr, int32_t k0,
                                               int32_t k1) {
@@ -165,6 +168,14 @@ __device__ __forceinline__ void gs_records(const KParams& P, const GsRecArgs& A,
       else dyn_euler_state(c, gi.t, st);
       SplinePt L;
       spline_eval(c, SP_BASE_LIN, gi.t, L);
+      // the five bases (segment-table loads) before the lane's first record store: a load issued after stores waits
+      // for them (vmcnt counts stores)
+      double HLp[4], HLa[4], HAp[4], HAv[4], HAa[4];
+      spline_basis(L, kPos, HLp);
+      spline_basis(L, kAcc, HLa);
+      spline_basis(st.A, kPos, HAp);
+      spline_basis(st.A, kVel, HAv);
+      spline_basis(st.A, kAcc, HAa);
       double a[3], bb3[3];   // dyn_g0_a: ab = I_w wd + w x (I_w w)
       mat3_vec(st.Iw, st.wd, a);
       cross3(st.w, st.Iww, bb3);
@@ -174,22 +185,8 @@ __device__ __forceinline__ void gs_records(const KParams& P, const GsRecArgs& A,
       auto put = [&](int f, double v) { *gs_field(Rd, RSd, k, gi, f) = v; };
 #pragma unroll
       for (int e = 0; e < 3; ++e) put(3 + e, L.p[e]);
-      double H[4];
-      spline_basis(L, kPos, H);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) put(6 + q, H[q]);
-      spline_basis(L, kAcc, H);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) put(10 + q, H[q]);
-      spline_basis(st.A, kPos, H);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) put(41 + q, H[q]);
-      spline_basis(st.A, kVel, H);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) put(45 + q, H[q]);
-      spline_basis(st.A, kAcc, H);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) put(49 + q, H[q]);
+      for (int q = 0; q < 4; ++q) { put(6 + q, HLp[q]); put(10 + q, HLa[q]); put(41 + q, HAp[q]); put(45 + q, HAv[q]); put(49 + q, HAa[q]); }
     } else if (i >= ee0 && i < ee0 + 3 * EK) {   // Dynamic (spline kind, endeffector ee, instant k)
       const int idx = i - ee0;
       const int kind = idx / EK, rem = idx - kind * EK;   // kind 0 motion, 1 force, 2 torque
@@ -238,6 +235,9 @@ __device__ __forceinline__ void gs_records(const KParams& P, const GsRecArgs& A,
       spline_eval(c, SP_BASE_LIN, t, L);
       spline_eval(c, SP_BASE_ANG, t, Ab);
       spline_eval(c, sp_motion(gi.ee), t, M);
+      double HL[4], HA[4];   // (segment-table loads before the lane's first store, as the Dynamic lanes)
+      spline_basis(L, kPos, HL);
+      spline_basis(Ab, kPos, HA);
       double R[3][3];
       Trig q{};
       if constexpr (ROTVEC) rv_rodrigues(Ab.p, R);
@@ -250,10 +250,8 @@ __device__ __forceinline__ void gs_records(const KParams& P, const GsRecArgs& A,
       for (int j = 0; j < 3; ++j)
 #pragma unroll
         for (int l = 0; l < 3; ++l) put(3 * j + l, R[j][l]);
-      double H[4];
-      spline_basis(L, kPos, H);
 #pragma unroll
-      for (int bb = 0; bb < 4; ++bb) put(9 + bb, H[bb]);
+      for (int bb = 0; bb < 4; ++bb) put(9 + bb, HL[bb]);
       // base-angular coefficients Ag[e][r]: the entry at (axis e, basis b) of row r is Ag[e][r] HA[b]
       if constexpr (ROTVEC) {   // DerivOfRotVecMult(t, r_W, inverse = true): R^T [r_W]x J_L
         double JL[3][3], Am[3][3];
@@ -271,9 +269,9 @@ __device__ __forceinline__ void gs_records(const KParams& P, const GsRecArgs& A,
           for (int rr = 0; rr < 3; ++rr) put(13 + 3 * e + rr, rW[0] * dR[0][rr] + rW[1] * dR[1][rr] + rW[2] * dR[2][rr]);
         }
       }
-      spline_basis(Ab, kPos, H);
 #pragma unroll
-      for (int bb = 0; bb < 4; ++bb) put(22 + bb, H[bb]);
+      for (int bb = 0; bb < 4; ++bb) put(22 + bb, HA[bb]);
+      double H[4];
       spline_basis(M, kPos, H);
       {
         double sums[3][kGsAct];
@@ -355,21 +353,25 @@ template <bool ROTVEC, int ROLES>
 __device__ __forceinline__ void rec_body(const KParams& P, const RecArgs& A, double* smem) {
   const int np = A.nparts;
   const int b = (int)blockIdx.x / np, part = (A.parts >> (4 * ((int)blockIdx.x % np))) & 15;
-  FsTabs T{P.fsb, P.fs_ws, P.fs_tmpl};
+  int32_t* d = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(smem) + A.fs_lds);
   if constexpr ((ROLES & 1) != 0) {
     if (A.fs_lds > 0) {   // the FDISC tables to LDS beside the staging (gait_record_setup's barrier covers them)
-      int32_t* d = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(smem) + A.fs_lds);
       const int32_t* sb = reinterpret_cast<const int32_t*>(P.fsb);
       for (int i = threadIdx.x; i < A.fs_nb + A.fs_nws + A.fs_ntm; i += blockDim.x)
         d[i] = i < A.fs_nb ? sb[i] : i < A.fs_nb + A.fs_nws ? P.fs_ws[i - A.fs_nb] : P.fs_tmpl[i - A.fs_nb - A.fs_nws];
-      T.fsb = reinterpret_cast<const FsBlock*>(d);
-      T.ws = d + A.fs_nb;
-      T.tmpl = d + A.fs_nb + A.fs_nws;
     }
   }
   const Ctx c = gait_record_setup<0>(P, b, smem);
   if constexpr ((ROLES & 1) != 0)
-    if (part == kRecFdisc) { fdisc_records(P, T, c, b, A.frec, A.fldr, 0, A.ni); TG_STAMP(P, 3); return; }
+    if (part == kRecFdisc) {
+      // two instances, so that every table pointer has one address space: a pointer that may be LDS or global is a
+      // flat one, and a flat load waits for the lane's earlier record stores too (vmcnt counts stores): the 12 window
+      // loads after the record stores then took ~6 of a ~24 us record block (MI355X, ANYmal gait, tools/stamps.py)
+      if (A.fs_lds > 0) fdisc_records(P, FsTabs{reinterpret_cast<const FsBlock*>(d), d + A.fs_nb, d + A.fs_nb + A.fs_nws}, c, b, A.frec, A.fldr, 0, A.ni);
+      else fdisc_records(P, FsTabs{P.fsb, P.fs_ws, P.fs_tmpl}, c, b, A.frec, A.fldr, 0, A.ni);
+      TG_STAMP(P, 3);
+      return;
+    }
   if constexpr ((ROLES & 4) != 0)
     if (part == kRecTq) { tq_records(P, A, c, b); TG_STAMP(P, 3); return; }
   if constexpr ((ROLES & 2) != 0) gs_records<ROTVEC>(P, A.g, c, b, smem, part == kRecGsDyn ? 1 : part == kRecGsRom ? 2 : 0);
