@@ -406,7 +406,19 @@ __global__ void __launch_bounds__(kGsRecMaxBlock) __attribute__((amdgpu_waves_pe
 // starts; layout.h gs_blob) | values | records (doubles) | wp (int2) | record ints | nph].
 // ForceConstraintDiscretized compose block: FsBlock jt for the problems g0, g0 + ng, ...
 // LDS: [per-instant records (stride kFsCS) | row window values (5 n x kFsWin) | row window starts (5 n)]
-constexpr int kFsUnits = 4;   // 16-byte units composed per lane before their stores
+// 16-byte units composed per lane before their stores (experiment builds: -DTOWR_FS_UNITS / -DTOWR_GS_UNITS). One unit
+// per lane: the composers then leave CU time and memory slots to the launches beside them. MI355X, ANYmal gait, B = 1024,
+// same box, 4 runs each (gpurun_out/r05q_ab.log), (FDISC units, GsBlock units) -> step ms, + Torque ms:
+// (4, 4) 0.624-0.638, 1.208-1.211; (2, 2) 0.612-0.620, 1.178-1.180; (1, 2) 0.614-0.616, 1.181-1.186;
+// (1, 1) 0.606-0.618, 1.162-1.167; (8, 8) 0.715-0.719, 1.310-1.316 (r05o). The FDISC compose alone is slower with fewer
+// units (0.383 -> 0.397 ms at 2), the overlapped step faster.
+#ifndef TOWR_FS_UNITS
+#define TOWR_FS_UNITS 1
+#endif
+#ifndef TOWR_GS_UNITS
+#define TOWR_GS_UNITS 1
+#endif
+constexpr int kFsUnits = TOWR_FS_UNITS;
 // The row window values and starts of an FsBlock's rows from its instants' records in LDS (cd: instant kk's record at
 // kk * kFsCS): window value q of row r = b[i][e(q)] * basis sum q (emit_dim; 0.0 where the sum is exactly 0)
 template <int BLOCK>
@@ -623,7 +635,7 @@ __global__ void __launch_bounds__(kFfBlock) towr_fdisc_fused_kernel(KParams P, F
   TG_STAMP(P, 4);
 }
 
-constexpr int kGsUnits = 4;
+constexpr int kGsUnits = TOWR_GS_UNITS;
 template <int CLS, int BLOCK>
 __device__ __forceinline__ void gs_compose(const KParams& P, const GsBlock* blks, const double* rec, int64_t ldr, int ng, int j, int g0,
                                            double* smem) {
