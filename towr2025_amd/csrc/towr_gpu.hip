@@ -182,6 +182,7 @@ unsigned long long* g_stamps = nullptr;
 int g_stamp_n = 0;
 const void* g_stamp_fn[kStampRegions];
 #endif
+bool launch_log_on() { static const bool log = std::getenv("TOWR_GPU_LAUNCH_LOG") != nullptr; return log; }
 hipError_t launch_kernel(const void* fn, dim3 grid, dim3 block, void** args, size_t lds, hipStream_t s) {
 #ifdef TOWR_STAMPS
   if (g_stamps && g_stamp_n < kStampRegions && (size_t)grid.x * 64 <= kStampRegion) {
@@ -189,8 +190,7 @@ hipError_t launch_kernel(const void* fn, dim3 grid, dim3 block, void** args, siz
     g_stamp_fn[g_stamp_n++] = fn;
   }
 #endif
-  static const bool log = std::getenv("TOWR_GPU_LAUNCH_LOG") != nullptr;
-  if (log) {
+  if (launch_log_on()) {
     static std::mutex mu;
     static std::vector<std::pair<const void*, std::pair<unsigned, size_t>>> seen;
     std::lock_guard<std::mutex> lk(mu);
@@ -537,6 +537,10 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
   // At equal priority the FDISC record blocks waited for CU slots behind the other chain's blocks: the record
   // launch took 299 us instead of 75 us (rocprofv3 kernel trace, ANYmal gait, B = 1024) and the FDISC compose
   // started only after the other chain had finished.
+  // (round 5: the chains swapped, FDISC on the caller's stream so that the step's last launch and the next step's first
+  // share a stream, the RangeOfMotion / Dynamic chain on side 0 at the default / least priority (HIP range 1 .. -1):
+  // ANYmal gait, B = 1024, one box, 4 runs: 0.623-0.648 / 0.656-0.659 vs 0.611-0.614 ms, + Torque 1.227-1.233 /
+  // 1.223-1.227 vs 1.163-1.171; gpurun_out/r05r_ab.log)
   const hipStream_t fst = split ? h->side[0] : st;   // the FDISC / TQDISC chain
   const hipStream_t gst = st;                        // the RangeOfMotion / Dynamic chain
   // with a second side stream, TQDISC (records + compose) is a third chain: its compose is as long as FDISC's
