@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--only", default=None, help="comma-separated part names: time only these, no whole step")
     ap.add_argument("--torque", action="store_true", help="ANYmal on stairs + Parameters::Torque (bench.py gait_torque)")
     ap.add_argument("--step-only", action="store_true", help="only the whole step (no per-kernel times)")
+    ap.add_argument("--settle-ms", type=float, default=300.0, help="untimed steps before timing (clock ramp)")
     args = ap.parse_args()
     import torch
     from towr2025_amd import _capi as capi
@@ -48,6 +49,12 @@ def main():
     only = args.only.split(",") if args.only else None
     for _ in range(0 if only else 30):
         p.eval_batch_device(X, G, V)
+    import time
+    t0 = time.perf_counter()   # untimed steps until the clocks have ramped (bench.py --settle-ms)
+    while time.perf_counter() - t0 < args.settle_ms * 1e-3:
+        for _ in range(10):
+            p.eval_batch_device(X, G, V)
+        torch.cuda.synchronize()
     out = {}
     for k, name, nt, by in ([] if args.step_only else p.kernels()):
         if only and name not in only:

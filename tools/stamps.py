@@ -1,7 +1,7 @@
 """In-kernel phase timestamps of the experiment build (make -C towr2025_amd/csrc variant VNAME=stamps
 VFLAGS=-DTOWR_STAMPS): one gait step (bench.py's gait_optimization workload) with every launch's TG_STAMP slots
 (kernel_common.h) collected, then per launch: blocks, span, and the median / p90 of each phase per block.
-usage: python tools/stamps.py [--lib tools/build/libtowr_gpu_stamps.so] [--batch 1024] [--torque] [--only KERNEL]
+usage: python tools/stamps.py [--lib tools/build/libtowr_gpu_stamps.so] [--batch 1024] [--torque | --fixed] [--only KERNEL]
 A measurement tool, not part of the product."""
 import argparse
 import ctypes as C
@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--lib", default="tools/build/libtowr_gpu_stamps.so")
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--torque", action="store_true")
+    ap.add_argument("--fixed", action="store_true", help="the headline formulation (fixed phase durations, B = 4096 default)")
     ap.add_argument("--only", type=int, default=-1, help="launch class index (towr_gpu_eval_batch_device_kernel)")
     ap.add_argument("--steps", type=int, default=20, help="untimed steps before the stamped one")
     args = ap.parse_args()
@@ -31,12 +32,12 @@ def main():
     from towr2025_amd import TowrGpuProblem
     from towr2025_amd import formulation as F
     import bench
-    f = F.anymal_trot(optimize_timings=True, terrain=F.HeightMap.MakeTerrain(F.HeightMap.StairsID) if args.torque else None)
+    f = F.anymal_trot(optimize_timings=not args.fixed, terrain=F.HeightMap.MakeTerrain(F.HeightMap.StairsID) if args.torque else None)
     if args.torque:
         f.params_.constraints_.append(F.Parameters.Torque)
     p = TowrGpuProblem(f.to_desc(), device=0)
-    B = args.batch
-    Xh, ter = bench.make_batch(p, B, 0, optimize_timings=True)
+    B = args.batch if not (args.fixed and args.batch == 1024) else 4096
+    Xh, ter = bench.make_batch(p, B, 0, optimize_timings=not args.fixed)
     p.set_batch_terrain(ter)
     dev = torch.device("cuda", 0)
     X = torch.from_numpy(np.ascontiguousarray(Xh[0])).to(dev)

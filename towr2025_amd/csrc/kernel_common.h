@@ -50,6 +50,8 @@ struct KParams {
   int32_t want_g, want_jac, fdisc_motion;
   const int32_t* misc_tiles;      // merged small-kind launch: kMiscWaves tile ids per group
   const int32_t* misc_lds;        // per (group, wave): LDS offset, g-row offset
+  const MiscWave* misc_wave;      // per (group, wave): the tile's ranges and LDS offsets (layout.h MiscWave)
+  const ItemDesc* misc_items;     // per (group, wave, lane): the tile's items
   const int32_t* xspan;           // the small kinds' x spans (Layout::misc_xspan), n_xspan pairs; 0 = all of x
   int32_t n_xspan;
   RobotC rb;
@@ -236,6 +238,55 @@ __device__ __forceinline__ void stage_x_spans(const KParams& P, const double* xg
     stage_x<BLOCK, true>(P, xg, xs, ns);
     return;
   }
+  // one pass when the spans' 16-byte units fit 3 per thread: every thread's units of the spans' concatenation and of
+  // the node table in flight together, then their LDS stores (one memory latency; span by span it was one per span:
+  // tools/stamps.py, MI355X, ANYmal, B = 4096: 2.8-3.6 us of a 5.8-6.6 us block). The unit holding x[n - 1] of an odd
+  // n is one double (thread 0).
+  const int nx = P.n >> 1, tid = (int)threadIdx.x;
+  int u0 = -1, u1 = -1, u2 = -1, acc = 0;
+  bool tail = false;
+  for (int k = 0; k < P.n_xspan; ++k) {
+    const int a = P.xspan[2 * k], l = P.xspan[2 * k + 1];
+    tail = tail || 2 * (a + l) > P.n;
+    const int len = min(l, nx - a);
+    if (len <= 0) continue;
+    const int j0 = tid - acc;
+    if ((unsigned)j0 < (unsigned)len) u0 = a + j0;
+    if ((unsigned)(j0 + BLOCK) < (unsigned)len) u1 = a + j0 + BLOCK;
+    if ((unsigned)(j0 + 2 * BLOCK) < (unsigned)len) u2 = a + j0 + 2 * BLOCK;
+    acc += len;
+  }
+  const int nn = (P.n_nodecol + 3) >> 2;
+#ifdef TOWR_SPAN_SERIAL   // experiment build: span by span (the round-4 staging)
+  acc = 3 * BLOCK + 1;
+#endif
+  if (acc <= 3 * BLOCK) {
+    const u32x4_t* sx = reinterpret_cast<const u32x4_t*>(xg);
+    const u32x4_t* sn = reinterpret_cast<const u32x4_t*>(P.nodecol);
+    u32x4_t x0 = {}, x1 = {}, x2 = {}, n0 = {}, n1 = {}, n2 = {};
+    double xt = 0.0;
+    if (u0 >= 0) x0 = sx[u0];
+    if (u1 >= 0) x1 = sx[u1];
+    if (u2 >= 0) x2 = sx[u2];
+    if (tail && tid == 0) xt = xg[P.n - 1];
+    if (tid < nn) n0 = sn[tid];
+    if (tid + BLOCK < nn) n1 = sn[tid + BLOCK];
+    if (tid + 2 * BLOCK < nn) n2 = sn[tid + 2 * BLOCK];
+    u32x4_t* dx = reinterpret_cast<u32x4_t*>(xs);
+    u32x4_t* dn = reinterpret_cast<u32x4_t*>(ns);
+    if (u0 >= 0) dx[u0] = x0;
+    if (u1 >= 0) dx[u1] = x1;
+    if (u2 >= 0) dx[u2] = x2;
+    if (tid == 0) {
+      if (tail) xs[P.n - 1] = xt;
+      xs[P.n] = 0.0;
+    }
+    if (tid < nn) dn[tid] = n0;
+    if (tid + BLOCK < nn) dn[tid + BLOCK] = n1;
+    if (tid + 2 * BLOCK < nn) dn[tid + 2 * BLOCK] = n2;
+    if (nn > 3 * BLOCK) stage16<BLOCK>(reinterpret_cast<uint4*>(ns) + 3 * BLOCK, reinterpret_cast<const uint4*>(P.nodecol) + 3 * BLOCK, nn - 3 * BLOCK);
+    return;
+  }
   for (int k = 0; k < P.n_xspan; ++k) {
     const int a = P.xspan[2 * k], len = P.xspan[2 * k + 1];
     if (2 * (a + len) <= P.n) {
@@ -246,7 +297,7 @@ __device__ __forceinline__ void stage_x_spans(const KParams& P, const double* xg
     }
   }
   if (threadIdx.x == 0) xs[P.n] = 0.0;
-  stage16<BLOCK>(reinterpret_cast<uint4*>(ns), reinterpret_cast<const uint4*>(P.nodecol), (P.n_nodecol + 3) >> 2);
+  stage16<BLOCK>(reinterpret_cast<uint4*>(ns), reinterpret_cast<const uint4*>(P.nodecol), nn);
 }
 
 // The x-dependent PhaseSpline timings of one problem (phase_spline_timings / phase_end_timings: pdur, pend per

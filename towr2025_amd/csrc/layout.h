@@ -25,6 +25,13 @@ struct TileDesc {
   int32_t type, reserved;
 };
 
+// Wave w of small-kind group g (Layout::misc_tiles / misc_lds) as the device reads it: its tile's rows and values and
+// its LDS offsets (ti -1: an empty wave), beside a copy of the tile's 64 items per (g, w) (towr_gpu.hip), so a block's
+// descriptors are one load level instead of three (group -> tile -> items; tile_emit.h misc_body)
+struct MiscWave {
+  int32_t ti, r0, r1, v0, v1, wl_off, rows_off, reserved;
+};
+
 // Streaming composition of ForceConstraintDiscretized under phase-duration optimisation on a terrain
 // without curvature (towr_gpu.hip fdisc_stream_body). One block per (problem, FsBlock) evaluates up to
 // kFsInst instants once each (fdisc_instant), then writes the block's whole CSR range [v0, v0 + nv)

@@ -139,17 +139,22 @@ template <bool GAIT, int BLOCK = 64 * kMiscWaves>
 __device__ __forceinline__ void misc_body(const KParams& P, double* smem, int b, int group, int lds_x_off) {
   static_assert(BLOCK >= 64 * kMiscWaves, "a small-kind group needs a wave per tile");
   const int wave = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
-  const int ti = wave < kMiscWaves ? P.misc_tiles[group * kMiscWaves + wave] : -1;
-  TileDesc T{};
+  TG_STAMP(P, 0);
+  // the wave's descriptor and the lane's item: one load level, issued with the x staging (the chain group -> tile ->
+  // items was three: tools/stamps.py, MI355X, ANYmal, B = 4096: 3.5 us to the staging barrier of a 6.6 us block)
+  const int gw = group * kMiscWaves + wave;
+  MiscWave T{};
+  T.ti = -1;
   ItemDesc it{};
   it.type = IT_NONE;
   it.slot = 0;
-  if (ti >= 0) {
-    T = P.tiles[ti];
-    it = P.items[T.i0 + lane];
+  if (wave < kMiscWaves) {
+    T = P.misc_wave[gw];
+    it = P.misc_items[gw * 64 + lane];
   }
-  const int32_t wl_off = ti >= 0 ? P.misc_lds[2 * (group * kMiscWaves + wave)] : 0;
-  const int32_t rows_off = ti >= 0 ? P.misc_lds[2 * (group * kMiscWaves + wave) + 1] : 0;
+  const int ti = T.ti;
+  const int32_t wl_off = ti >= 0 ? T.wl_off : 0;
+  const int32_t rows_off = ti >= 0 ? T.rows_off : 0;
   double* wl = smem + wl_off;
   TileEmit<64, 3> em(P.slots + it.slot, wl, wl + rows_off - T.r0);
   double* xs = smem + lds_x_off;
@@ -159,6 +164,7 @@ __device__ __forceinline__ void misc_body(const KParams& P, double* smem, int b,
   if constexpr (GAIT) stage_x<BLOCK, true>(P, P.X + (int64_t)b * P.ldx, xs, ns);
   else stage_x_spans<BLOCK>(P, P.X + (int64_t)b * P.ldx, xs, ns);
   __syncthreads();
+  TG_STAMP(P, 1);
   if (it.type != IT_NONE) {
     Ctx c;
     c.seg = nullptr; c.sg = P.sg; c.row = it.seg;
@@ -184,12 +190,14 @@ __device__ __forceinline__ void misc_body(const KParams& P, double* smem, int b,
     }
   }
   __syncthreads();
+  TG_STAMP(P, 2);
   if (ti < 0) return;
   double* Vb = P.V + (int64_t)b * P.ldv;
   double* Gb = P.G + (int64_t)b * P.ldg;
   if (P.want_jac) copy_out(wl, Vb + T.v0, T.v1 - T.v0, lane, 64);
   if (P.want_g)
     for (int i = lane; i < T.r1 - T.r0; i += 64) __builtin_nontemporal_store(wl[rows_off + i], Gb + T.r0 + i);
+  TG_STAMP(P, 3);
 }
 
 }  // namespace

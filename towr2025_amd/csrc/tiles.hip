@@ -96,6 +96,7 @@ __device__ __forceinline__ void eval_typed(const Ctx& c, const ItemDesc& it, Emi
 // whose extra wave only helps stage x and copy out.
 template <int TYPE, int TBLOCK, int KBLOCK, bool GAIT, bool ROTVEC>
 __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b, int tile, int lds_x_off, int lds_rows_off) {
+  TG_STAMP(P, 0);
   const TileDesc T = P.tiles[tile];
   double* Vb = P.V + (int64_t)b * P.ldv;
   double* Gb = P.G + (int64_t)b * P.ldg;
@@ -145,6 +146,7 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
     if constexpr (!kWaveZero) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
+  TG_STAMP(P, 1);
   Ctx c;
   c.seg = nullptr; c.sg = P.sg; c.row = it.seg;
   c.x = xs; c.nodecol = ns; c.spl = P.spl; c.dur = P.dur;
@@ -198,6 +200,7 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
     }
     em.flush();
   }
+  TG_STAMP(P, 2);
   if constexpr (TYPE == IT_DYN) {   // phase B of group 0: the endeffector sums from LDS
     const bool g0lane = it.type == TYPE && it.group == 0;
     TileEmitPre<TBLOCK, kDynG0PhaseA, GAIT> emb(P.slots + it.slot, GAIT ? Vb + T.v0 : smem,
@@ -215,11 +218,13 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
     }
   }
   __syncthreads();
+  TG_STAMP(P, 3);
   if constexpr (!GAIT) {
     if (P.want_jac) copy_out(smem, Vb + T.v0, T.v1 - T.v0, threadIdx.x, KBLOCK);
     if (P.want_g && !kGDirect)
       for (int i = threadIdx.x; i < T.r1 - T.r0; i += KBLOCK) __builtin_nontemporal_store(smem[lds_rows_off + i], Gb + T.r0 + i);
   }
+  TG_STAMP(P, 4);
 }
 
 template <int TYPE, int BLOCK, bool GAIT, bool ROTVEC>
