@@ -12,7 +12,12 @@
 namespace tg {
 
 // one unit of the fused launch: a tile of a tile class, or a small-kind group (LC_MISC)
-struct UnitDesc { int32_t lc, tile, lds_x_off, lds_rows_off; };
+// a fused launch's unit: its class, tile (with a copy of the tile's descriptor, so a block's first load level holds it)
+// and LDS offsets
+struct UnitDesc {
+  int32_t lc, tile, lds_x_off, lds_rows_off;
+  TileDesc t;
+};
 
 struct KParams {
   const double* X; int64_t ldx;

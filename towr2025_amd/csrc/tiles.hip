@@ -95,9 +95,9 @@ __device__ __forceinline__ void eval_typed(const Ctx& c, const ItemDesc& it, Emi
 // launch's block size (>= TBLOCK): in the fused launch a 192-lane tile runs in a 256-thread block,
 // whose extra wave only helps stage x and copy out.
 template <int TYPE, int TBLOCK, int KBLOCK, bool GAIT, bool ROTVEC>
-__device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b, int tile, int lds_x_off, int lds_rows_off) {
+// (T by value: a reference into global memory is reloaded after the tile's stores, and on gfx950 such a load waits for them)
+__device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b, const TileDesc T, int lds_x_off, int lds_rows_off) {
   TG_STAMP(P, 0);
-  const TileDesc T = P.tiles[tile];
   double* Vb = P.V + (int64_t)b * P.ldv;
   double* Gb = P.G + (int64_t)b * P.ldg;
   const double* xg = P.X + (int64_t)b * P.ldx;
@@ -107,6 +107,8 @@ __device__ __forceinline__ void tile_body(const KParams& P, double* smem, int b,
   XStage<KBLOCK, stages_nodes(TYPE, GAIT)> xst;
   if constexpr (early_stage(TYPE)) xst.issue(P, xg);
   ItemDesc it;
+  // (the slot address from the tile descriptor, base + lane, instead of the item: no gain, MI355X, ANYmal, B = 4096,
+  // one box: 0.2381-0.2394 vs 0.2381-0.2389 ms per step; for the small kinds 25.8 vs 23.2 us)
   if (KBLOCK == TBLOCK || (int)threadIdx.x < TBLOCK) {
     it = P.items[T.i0 + threadIdx.x];
   } else {
@@ -239,7 +241,7 @@ __global__ void __launch_bounds__(BLOCK, TYPE == IT_DYN && !GAIT && ROTVEC ? 3 :
   // XCD-aware mapping: work ids w and w+1 (tiles of one problem) share blockIdx % 8
   const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
   if (w >= total) return;
-  tile_body<TYPE, BLOCK, BLOCK, GAIT, ROTVEC>(P, smem, w / P.ntiles, P.tile0 + w % P.ntiles, P.lds_x_off, P.lds_rows_off);
+  tile_body<TYPE, BLOCK, BLOCK, GAIT, ROTVEC>(P, smem, w / P.ntiles, P.tiles[P.tile0 + w % P.ntiles], P.lds_x_off, P.lds_rows_off);
 }
 
 
@@ -274,12 +276,12 @@ __global__ void __launch_bounds__(KBLOCK, (KBLOCK == 256 ? 2 : 1)) towr_step_ker
   const int b = w / P.n_units;
   const UnitDesc u = P.units[w % P.n_units];
   switch (u.lc) {
-    case LC_ROM: tile_body<IT_ROM, 192, KBLOCK, GAIT, ROTVEC>(P, smem, b, u.tile, u.lds_x_off, u.lds_rows_off); break;
-    case LC_FDISC: tile_body<IT_FDISC, 192, KBLOCK, GAIT, false>(P, smem, b, u.tile, u.lds_x_off, u.lds_rows_off); break;
-    case LC_TQDISC: tile_body<IT_TQDISC, 192, KBLOCK, GAIT, false>(P, smem, b, u.tile, u.lds_x_off, u.lds_rows_off); break;
+    case LC_ROM: tile_body<IT_ROM, 192, KBLOCK, GAIT, ROTVEC>(P, smem, b, u.t, u.lds_x_off, u.lds_rows_off); break;
+    case LC_FDISC: tile_body<IT_FDISC, 192, KBLOCK, GAIT, false>(P, smem, b, u.t, u.lds_x_off, u.lds_rows_off); break;
+    case LC_TQDISC: tile_body<IT_TQDISC, 192, KBLOCK, GAIT, false>(P, smem, b, u.t, u.lds_x_off, u.lds_rows_off); break;
     default:
       if constexpr (KBLOCK == 256) {
-        if (u.lc == LC_DYN) tile_body<IT_DYN, 256, KBLOCK, GAIT, ROTVEC>(P, smem, b, u.tile, u.lds_x_off, u.lds_rows_off);
+        if (u.lc == LC_DYN) tile_body<IT_DYN, 256, KBLOCK, GAIT, ROTVEC>(P, smem, b, u.t, u.lds_x_off, u.lds_rows_off);
         else misc_body<GAIT, KBLOCK>(P, smem, b, u.tile, u.lds_x_off);
       } else if constexpr (KBLOCK >= 64 * kMiscWaves) {
         if (u.lc == LC_MISC) misc_body<GAIT, KBLOCK>(P, smem, b, u.tile, u.lds_x_off);

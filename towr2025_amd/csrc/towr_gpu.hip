@@ -387,6 +387,7 @@ std::vector<UnitDesc> fused_units(const Layout& L, uint32_t mask) {
       d.tile = lc == LC_MISC ? k : L.type_tile0[class_type(lc)] + k;
       d.lds_x_off = (int32_t)lds_region(L, lc);
       d.lds_rows_off = lc == LC_MISC ? 0 : L.type_lds_rows_off[class_type(lc)];   // small kinds: misc_lds
+      if (lc != LC_MISC) d.t = L.tiles[d.tile];
       u.push_back(d);
       any = true;
     }
