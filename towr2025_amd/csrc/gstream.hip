@@ -492,12 +492,20 @@ __device__ __forceinline__ void fs_stream(const KParams& P, const FsBlock& fb, i
       const int e = head + 2 * u;
       const int r = (int)(((float)e + 0.5f) * invL);
       const int j = e - r * Lr;
+#ifdef TOWR_FS_PURE   // experiment build: the stream without the entries' arithmetic (bandwidth of the store pattern)
+      v[q].x = (double)r; v[q].y = (double)j;
+#else
       v[q].x = u < m2 ? entry(r, j) : 0.0;
       v[q].y = u < m2 ? (j + 1 < Lr ? entry(r, j + 1) : entry(r + 1, 0)) : 0.0;
+#endif
     }
 #pragma unroll
     for (int q = 0; q < UNITS; ++q)
+#ifdef TOWR_FS_PLAIN
+      if (u0 + q * BLOCK < m2) d2[u0 + q * BLOCK] = v[q];
+#else
       if (u0 + q * BLOCK < m2) __builtin_nontemporal_store(v[q], d2 + u0 + q * BLOCK);
+#endif
   }
   if (((nv - head) & 1) && tid == 0) __builtin_nontemporal_store(value(nv - 1), out + nv - 1);
 }

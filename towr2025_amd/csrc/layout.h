@@ -102,8 +102,17 @@ constexpr int kGsRowTypes = 6;
 constexpr int kGsAct = 4;
 // The composer launch (gstream.hip towr_gait_compose_kernel): the ForceConstraintDiscretized,
 // RangeOfMotion and Dynamic compose blocks of every problem in one grid, kComposeBlock threads each.
-constexpr int kComposeBlock = 512;
-constexpr int kComposeBlockRD = 256;   // a launch without FDISC blocks
+// (experiment builds: -DTOWR_COMPOSE_BLOCK / -DTOWR_COMPOSE_BLOCK_RD. Round 5, ANYmal gait, B = 1024, one box, ms per step
+// gait / + Torque: 512 / 256 0.606-0.619 / 1.163-1.174; FDISC composer 1024: 0.624-0.635 / 1.29; 256: 0.667-0.682 / 1.28;
+// RangeOfMotion / Dynamic composer 512: 0.660-0.664 / 1.23; 128: 0.654-0.659 / 1.19)
+#ifndef TOWR_COMPOSE_BLOCK
+#define TOWR_COMPOSE_BLOCK 512
+#endif
+#ifndef TOWR_COMPOSE_BLOCK_RD
+#define TOWR_COMPOSE_BLOCK_RD 256
+#endif
+constexpr int kComposeBlock = TOWR_COMPOSE_BLOCK;
+constexpr int kComposeBlockRD = TOWR_COMPOSE_BLOCK_RD;   // a launch without FDISC blocks
 inline int compose_block(int mask) { return (mask & 25) ? kComposeBlock : kComposeBlockRD; }
 constexpr int kGsInstRom = 16;   // instants per compose block
 constexpr int kGsInstTq = 16;
