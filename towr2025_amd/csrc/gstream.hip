@@ -484,11 +484,11 @@ __device__ __forceinline__ void fs_stream(const KParams& P, const FsBlock& fb, i
   if (head && tid == 0) __builtin_nontemporal_store(value(0), out);
   const int m2 = (nv - head) >> 1;
   dbl2_t* d2 = reinterpret_cast<dbl2_t*>(out + head);
-  for (int u0 = tid; u0 < m2; u0 += BLOCK * UNITS) {
+  for (int u0 = tid - trip_skew<0>(d2); u0 < m2; u0 += BLOCK * UNITS) {
     dbl2_t v[UNITS];
 #pragma unroll
     for (int q = 0; q < UNITS; ++q) {
-      const int u = u0 + q * BLOCK;
+      const int u = max(u0 + q * BLOCK, 0);
       const int e = head + 2 * u;
       const int r = (int)(((float)e + 0.5f) * invL);
       const int j = e - r * Lr;
@@ -502,9 +502,9 @@ __device__ __forceinline__ void fs_stream(const KParams& P, const FsBlock& fb, i
 #pragma unroll
     for (int q = 0; q < UNITS; ++q)
 #ifdef TOWR_FS_PLAIN
-      if (u0 + q * BLOCK < m2) d2[u0 + q * BLOCK] = v[q];
+      if ((unsigned)(u0 + q * BLOCK) < (unsigned)m2) d2[u0 + q * BLOCK] = v[q];
 #else
-      if (u0 + q * BLOCK < m2) __builtin_nontemporal_store(v[q], d2 + u0 + q * BLOCK);
+      if ((unsigned)(u0 + q * BLOCK) < (unsigned)m2) __builtin_nontemporal_store(v[q], d2 + u0 + q * BLOCK);
 #endif
   }
   if (((nv - head) & 1) && tid == 0) __builtin_nontemporal_store(value(nv - 1), out + nv - 1);
@@ -735,18 +735,18 @@ __device__ __forceinline__ void gs_compose(const KParams& P, const GsBlock* blks
     if (head && tid == 0) __builtin_nontemporal_store(value(0), out);
     const int m2 = (nv - head) >> 1;
     dbl2_t* d2 = reinterpret_cast<dbl2_t*>(out + head);
-    for (int u0 = tid; u0 < m2; u0 += BLOCK * kGsUnits) {
+    for (int u0 = tid - (CLS == GS_TQ ? trip_skew<3>(d2) : trip_skew<1>(d2)); u0 < m2; u0 += BLOCK * kGsUnits) {
       dbl2_t v[kGsUnits];
 #pragma unroll
       for (int q = 0; q < kGsUnits; ++q) {
         const int u = u0 + q * BLOCK;
-        const int e = head + 2 * u;
-        v[q].x = u < m2 ? value(e) : 0.0;
-        v[q].y = u < m2 ? value(e + 1) : 0.0;
+        const int e = head + 2 * max(u, 0);
+        v[q].x = (unsigned)u < (unsigned)m2 ? value(e) : 0.0;
+        v[q].y = (unsigned)u < (unsigned)m2 ? value(e + 1) : 0.0;
       }
 #pragma unroll
       for (int q = 0; q < kGsUnits; ++q)
-        if (u0 + q * BLOCK < m2) __builtin_nontemporal_store(v[q], d2 + u0 + q * BLOCK);
+        if ((unsigned)(u0 + q * BLOCK) < (unsigned)m2) __builtin_nontemporal_store(v[q], d2 + u0 + q * BLOCK);
     }
     if (((nv - head) & 1) && tid == 0) __builtin_nontemporal_store(value(nv - 1), out + nv - 1);
     if (bn >= P.B) break;

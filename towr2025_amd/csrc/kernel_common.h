@@ -132,6 +132,22 @@ __device__ __forceinline__ void stage16(uint4* __restrict__ dst, const uint4* __
 // streamed (never re-read by the kernel); plain stores cost ~25 % more kernel time on MI355X
 // (ANYmal, B = 4096: 0.532 -> 0.444 ms per step with non-temporal stores).
 typedef double dbl2_t __attribute__((ext_vector_type(2)));
+// 16-byte units of a destination before its next 1 KB boundary: a stream loop whose lanes start at unit -skew (skipping
+// the negative units) issues every wave's 64 x 16-byte store on one whole 1 KB of HBM. TOWR_ALIGN_TRIPS: the loops that
+// align (bit 0 the FDISC composer, 1 the RangeOfMotion / Dynamic / TQDISC composer, 2 the tile copy-out, 3 the TQDISC
+// composer). tools/stride_probe.hip, the FDISC composer's pattern as pure stores: 4.2 -> 5.4 TB/s. In the kernels
+// (MI355X, ANYmal gait, B = 1024, one box, 3 runs, ms per step gait / + Torque): none 0.613-0.622 / 1.168-1.169; the
+// FDISC composer 0.591-0.605 / 1.163-1.167; the other composers 0.616-0.621 / 1.159-1.163; both 0.596-0.616 /
+// 1.195-1.196; every loop incl. the tile copy-out: the headline step 0.2355-0.2364 -> 0.2399-0.2408 ms (B = 4096).
+#ifndef TOWR_ALIGN_TRIPS
+#define TOWR_ALIGN_TRIPS 1
+#endif
+template <int LOOP>
+__device__ __forceinline__ int trip_skew(const void* d2) {
+  if constexpr (((TOWR_ALIGN_TRIPS >> LOOP) & 1) != 0) return (int)((reinterpret_cast<uintptr_t>(d2) & 1023) >> 4);
+  (void)d2;
+  return 0;
+}
 __device__ __forceinline__ void copy_out(const double* __restrict__ src, double* __restrict__ dst, int n,
                                          int tid, int nthr) {
   if (n <= 0) return;
@@ -139,7 +155,9 @@ __device__ __forceinline__ void copy_out(const double* __restrict__ src, double*
   if (head && tid == 0) __builtin_nontemporal_store(src[0], dst);
   const int m = (n - head) >> 1;
   dbl2_t* d2 = reinterpret_cast<dbl2_t*>(dst + head);
-  for (int i = tid; i < m; i += nthr) {
+  const int k = trip_skew<2>(d2);
+  for (int i = tid - k; i < m; i += nthr) {
+    if (i < 0) continue;
     dbl2_t v;
     v.x = src[head + 2 * i];
     v.y = src[head + 2 * i + 1];
