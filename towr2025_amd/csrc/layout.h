@@ -161,7 +161,10 @@ constexpr int kTqND = 48, kTqNI = 9;
 TG_HD constexpr int gs_rec_nd(int cls, int E) { return cls == GS_ROM ? kRomND : cls == GS_TQ ? kTqND : kDynBaseND + kDynEeND * E; }
 TG_HD constexpr int gs_rec_ni(int cls, int E) { return cls == GS_ROM ? kRomNI : cls == GS_TQ ? kTqNI : kDynEeNI * E; }
 TG_HD constexpr int gs_rec_fields(int cls, int E) { return gs_rec_nd(cls, E) + gs_rec_ni(cls, E); }
-constexpr int kGsGroup = 2;   // problems per composer block (gstream and fstream; 1 -> 0.333 ms, 2 -> 0.321, 8+ slower: a block
+#ifndef TOWR_GS_GROUP   // (experiment builds: -DTOWR_GS_GROUP)
+#define TOWR_GS_GROUP 2
+#endif
+constexpr int kGsGroup = TOWR_GS_GROUP;   // problems per composer block (gstream and fstream; 1 -> 0.333 ms, 2 -> 0.321, 8+ slower: a block
                               // waits for its stores to drain before the next problem's records land)
 constexpr int kGsChunkMax = 2048;   // record doubles of a compose block (prefetched into registers: kGsChunkMax / kComposeBlock per thread)
 // the RangeOfMotion / Dynamic records' arguments (gs_records)
