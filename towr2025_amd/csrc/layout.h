@@ -161,7 +161,8 @@ constexpr int kTqND = 48, kTqNI = 9;
 TG_HD constexpr int gs_rec_nd(int cls, int E) { return cls == GS_ROM ? kRomND : cls == GS_TQ ? kTqND : kDynBaseND + kDynEeND * E; }
 TG_HD constexpr int gs_rec_ni(int cls, int E) { return cls == GS_ROM ? kRomNI : cls == GS_TQ ? kTqNI : kDynEeNI * E; }
 TG_HD constexpr int gs_rec_fields(int cls, int E) { return gs_rec_nd(cls, E) + gs_rec_ni(cls, E); }
-#ifndef TOWR_GS_GROUP   // (experiment builds: -DTOWR_GS_GROUP)
+#ifndef TOWR_GS_GROUP   // (experiment builds: -DTOWR_GS_GROUP; round 5, one box, gait / + Torque / headline ms: 2 0.592-0.595 /
+                        // 1.161-1.165 / 0.2365-0.2375; 1 0.620-0.629 / 1.276; 4 0.589-0.599 / 1.160-1.166 / 0.2364-0.2372)
 #define TOWR_GS_GROUP 2
 #endif
 constexpr int kGsGroup = TOWR_GS_GROUP;   // problems per composer block (gstream and fstream; 1 -> 0.333 ms, 2 -> 0.321, 8+ slower: a block
