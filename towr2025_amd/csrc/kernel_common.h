@@ -280,9 +280,8 @@ __device__ __forceinline__ void stage_x_spans(const KParams& P, const double* xg
     acc += len;
   }
   const int nn = (P.n_nodecol + 3) >> 2;
-#ifdef TOWR_SPAN_SERIAL   // experiment build: span by span (the round-4 staging)
-  acc = 3 * BLOCK + 1;
-#endif
+  // (a host-built table of every thread's units instead of the walk over the span list: 23.9 vs 23.2 us per 4096
+  // problems, not kept)
   if (acc <= 3 * BLOCK) {
     const u32x4_t* sx = reinterpret_cast<const u32x4_t*>(xg);
     const u32x4_t* sn = reinterpret_cast<const u32x4_t*>(P.nodecol);
