@@ -700,10 +700,13 @@ __device__ __forceinline__ void gs_compose(const KParams& P, const GsBlock* blks
   };
   const int nv = bl.nv;
   int b = g0;
+  TG_STAMP(P, 0);
   fetch(b);
+  int it = 0;
   for (;;) {
     deposit();
     __syncthreads();
+    if (it == 0) TG_STAMP(P, 1);
     for (int t = tid; t < n * ns; t += BLOCK) {   // window starts and value bases
       const int kk = t / ns, sid = t - kk * ns;
       const GsSeg sg = segs[sid];
@@ -712,6 +715,7 @@ __device__ __forceinline__ void gs_compose(const KParams& P, const GsBlock* blks
       wp[t] = make_int2(sg.p0 + ws, ((int)sg.W << 16) | (kk * vt + sg.vbase));
     }
     __syncthreads();
+    if (it == 0) TG_STAMP(P, 2);
     for (int t = tid; t < n * vt; t += BLOCK) {   // every value of every instant, once
       const int kk = t / vt, v = t - kk * vt;
       const uint32_t vm = vmap[v];
@@ -728,6 +732,7 @@ __device__ __forceinline__ void gs_compose(const KParams& P, const GsBlock* blks
       val[t] = x;
     }
     __syncthreads();
+    if (it == 0) TG_STAMP(P, 3);
     const int bn = b + ng;
     if (bn < P.B) fetch(bn);   // in flight while this problem streams
     double* out = P.V + (int64_t)b * P.ldv + bl.v0;
@@ -749,10 +754,13 @@ __device__ __forceinline__ void gs_compose(const KParams& P, const GsBlock* blks
         if ((unsigned)(u0 + q * BLOCK) < (unsigned)m2) __builtin_nontemporal_store(v[q], d2 + u0 + q * BLOCK);
     }
     if (((nv - head) & 1) && tid == 0) __builtin_nontemporal_store(value(nv - 1), out + nv - 1);
+    if (it == 0) TG_STAMP(P, 4);
+    ++it;
     if (bn >= P.B) break;
     b = bn;
     __syncthreads();   // this problem's wp / values / records read before the next deposit
   }
+  TG_STAMP(P, 5);
 }
 
 
