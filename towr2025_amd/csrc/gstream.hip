@@ -716,6 +716,9 @@ __device__ __forceinline__ void gs_compose(const KParams& P, const GsBlock* blks
     }
     __syncthreads();
     if (it == 0) TG_STAMP(P, 2);
+    // (2 or 4 values per thread formed before their LDS stores, so that their load chains overlap: the value phase is
+    // 3.6 / 5.6 of a 15 / 19 us Dynamic / RangeOfMotion block (tools/stamps.py), but the gait step measured 0.595-0.603
+    // vs 0.594-0.607 ms and + Torque 1.19-1.20 vs 1.16 ms: not kept)
     for (int t = tid; t < n * vt; t += BLOCK) {   // every value of every instant, once
       const int kk = t / vt, v = t - kk * vt;
       const uint32_t vm = vmap[v];
