@@ -512,6 +512,13 @@ int gs_rec_threads(const Layout& L, int64_t Kd, int64_t Kr) {   // the record la
 // more than any overlap gains (MI355X, ANYmal gait: 97 us for the per-class chains, 70 us for four launches
 // on one stream).
 constexpr int kSplitBatch = 64;
+#ifndef TOWR_FS_GROUP   // (experiment builds: -DTOWR_FS_GROUP / -DTOWR_TQ_GROUP)
+#define TOWR_FS_GROUP 4
+#endif
+#ifndef TOWR_TQ_GROUP
+#define TOWR_TQ_GROUP kGsGroup
+#endif
+constexpr int kFsGroup = TOWR_FS_GROUP, kTqGroup = TOWR_TQ_GROUP;
 bool compose_lds_attr(size_t lds) {   // every composer instantiation may take `lds` bytes of LDS
   for (int m = 1; m < 32; ++m)
     if (hipFuncSetAttribute(gait_compose_kernel(m), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return false;
@@ -606,6 +613,14 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
     C.nt[2] = d && j ? (int32_t)L.gs_blocks[GS_DYN].size() : 0;
     C.nt[3] = m ? class_units(L, LC_MISC) : 0;
     C.nt[4] = t && j ? (int32_t)L.gs_blocks[GS_TQ].size() : 0;
+    // problems per block: kGsGroup; a launch of FDISC blocks only: kFsGroup (the next problem's records prefetched while
+    // one streams, so a block with more problems keeps its trips going longer; MI355X, ANYmal gait, B = 1024, one box,
+    // 3 runs, gait / + Torque ms: 2 0.596-0.598 / 1.163-1.167; 4 0.587-0.592 / 1.146-1.149; 8 0.585-0.593 / 1.151-1.157)
+    // and of TQDISC blocks only: kTqGroup (4: + Torque 1.161-1.163 vs 1.145-1.150; 1: 1.185-1.193)
+    const bool fonly = C.nt[0] > 0 && C.nt[1] + C.nt[2] + C.nt[3] + C.nt[4] == 0;
+    const bool tonly = C.nt[4] > 0 && C.nt[0] + C.nt[1] + C.nt[2] + C.nt[3] == 0;
+    const int grp = fonly ? kFsGroup : tonly ? kTqGroup : kGsGroup;
+    C.ng = (B + grp - 1) / grp;
     const int64_t units = (int64_t)C.nt[0] + C.nt[1] + C.nt[2] + C.nt[3] + C.nt[4];
     const int64_t grid = ((int64_t)C.ng * units + 7) / 8 * 8;   // whole rounds of 8 (XCD-aware mapping)
     if (grid == 0) return TOWR_OK;
