@@ -41,7 +41,13 @@ struct MiscWave {
 //   >= 0: force column, PhaseCol index (bits 0-23) and dimension (bits 24-25); < 0: schedule column.
 // The force entries polynomial p can make non-zero (its two nodes' variables) lie in the window
 // [fs_ws[2 (wsoff + p)], + kFsWin) of row positions (checked); schedule columns at [js0, js0 + ns1).
-constexpr int kFsInst = 16;   // measured on MI355X (ANYmal gait, B = 1024): 64 -> 0.501 ms, 32 -> 0.463, 16 -> 0.452, 8 -> 0.478
+#ifndef TOWR_FS_INST   // (experiment builds: -DTOWR_FS_INST)
+#define TOWR_FS_INST 16
+#endif
+// measured on MI355X (ANYmal gait, B = 1024): 64 -> 0.501 ms, 32 -> 0.463, 16 -> 0.452, 8 -> 0.478 (round 3); with the
+// round-5 composer (1 KB-aligned trips, 4 problems per block), step gait / + Torque: 16 0.584-0.593 / 1.144-1.152,
+// 32 0.570-0.591 / 1.153-1.159, 8 0.638-0.650 / 1.203-1.205
+constexpr int kFsInst = TOWR_FS_INST;
 constexpr int kFsWin = 12;
 // The composers (gstream.hip) find an entry's row (FsBlock) or instant (GsBlock) from its position e in the
 // block's CSR range as (int)((e + 0.5f) * (1.0f / L)). The float product is within 2^-23 relative of
