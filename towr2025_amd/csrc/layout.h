@@ -168,7 +168,9 @@ TG_HD constexpr int gs_rec_nd(int cls, int E) { return cls == GS_ROM ? kRomND : 
 TG_HD constexpr int gs_rec_ni(int cls, int E) { return cls == GS_ROM ? kRomNI : cls == GS_TQ ? kTqNI : kDynEeNI * E; }
 TG_HD constexpr int gs_rec_fields(int cls, int E) { return gs_rec_nd(cls, E) + gs_rec_ni(cls, E); }
 #ifndef TOWR_GS_GROUP   // (experiment builds: -DTOWR_GS_GROUP; round 5, one box, gait / + Torque / headline ms: 2 0.592-0.595 /
-                        // 1.161-1.165 / 0.2365-0.2375; 1 0.620-0.629 / 1.276; 4 0.589-0.599 / 1.160-1.166 / 0.2364-0.2372)
+                        // 1.161-1.165 / 0.2365-0.2375; 1 0.620-0.629 / 1.276; 4 0.589-0.599 / 1.160-1.166 / 0.2364-0.2372;
+                        // with the FDISC composer at 4 (towr_gpu.hip kFsGroup), the others at 4: 0.589-0.594 / 1.146-1.150
+                        // vs 0.584-0.599 / 1.141-1.144, at 1: 0.600-0.601 / 1.160-1.166)
 #define TOWR_GS_GROUP 2
 #endif
 constexpr int kGsGroup = TOWR_GS_GROUP;   // problems per composer block (gstream and fstream; 1 -> 0.333 ms, 2 -> 0.321, 8+ slower: a block
