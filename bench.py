@@ -253,7 +253,13 @@ def main():
     ap.add_argument("--no-host", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
     ap.add_argument("--no-gait", action="store_true", help="skip the phase-duration optimisation figure")
     ap.add_argument("--tiles-per-block", type=int, default=0)
+    ap.add_argument("--legs", default=None, help="A/B runs: comma-separated side legs to measure (objective, "
+                                                 "gait_optimization, gait_torque, rotvec, pattern_watch); default all")
     args = ap.parse_args()
+    legs = set(args.legs.split(",")) if args.legs else None
+
+    def want(leg):
+        return legs is None or leg in legs
 
     import torch
     import torch.distributed as dist
@@ -374,7 +380,7 @@ def main():
                 out["roofline"]["traffic_source"] = rec.get("source")
         except Exception:
             pass
-    if rank == 0:
+    if rank == 0 and want("objective"):
         # the objective callbacks on the same batch: every cost kind of
         # NlpFormulation::GetCosts on this formulation; one eval_f + eval_grad_f per problem
         cdesc = F.with_costs(F.anymal_trot()).to_desc()
@@ -427,6 +433,8 @@ def main():
                 ("gait_torque", F.anymal_trot(terrain=F.HeightMap.MakeTerrain(F.HeightMap.StairsID), optimize_timings=True),
                  "the same + Parameters::Torque (TorqueConstraintDiscretized per foot, dt 0.02, on the record + "
                  "compose path), the formulation class of the fork's hopper driver (hopper_example.cc:145-150)")):
+            if not want(key):
+                continue
             if key == "gait_torque":
                 f.params_.constraints_.append(F.Parameters.Torque)
             gprob = TowrGpuProblem(f.to_desc(), device=local)
@@ -434,7 +442,7 @@ def main():
             out[key] = batch_leg(gprob, [torch.from_numpy(Xg[k]).to(dev) for k in range(2)], Bg, gter)
             out[key]["note"] = note
             gprob.close()
-    if rank == 0 and not args.no_gait:
+    if rank == 0 and not args.no_gait and want("rotvec"):
         # RotVecConverter base orientation (Parameters::RotationVector) on the same
         # randomised instances: the headline formulation with the rotation-vector base parameterisation
         fr = F.anymal_trot()
@@ -444,7 +452,7 @@ def main():
         out["rotvec"]["note"] = ("ANYmal trot with the RotVecConverter base orientation (angular_rep = 1), the "
                                  "headline's randomised instances and x")
         rprob.close()
-    if rank == 0 and not args.no_gait:
+    if rank == 0 and not args.no_gait and want("pattern_watch"):
         # the frozen-pattern check (towr_gpu_pattern_outside_batch_device, a host pass) on a Gap batch
         out["pattern_watch"] = pattern_watch(X[0], B, local)
     if rank == 0 and not args.no_host:

@@ -202,6 +202,81 @@ extern "C" int emu_cost(const towr_problem_desc_t* d, const double* x, double* f
   return 0;
 }
 
+// The objective kernel's deterministic gradient (cost_traj.hip) on the host, with its own emitters:
+// acc 1 = the slot path (returns 1 when the layout has no slots), 2 = the fixed-point limb path.
+extern "C" int emu_cost_acc(const towr_problem_desc_t* d, const double* x, int acc, double* f, double* grad) {
+  Layout L; std::string e;
+  if (build_layout(*d, L, e)) return -1;
+  if (acc == 1 && L.cost_nslot == 0) return 1;
+  Ctx c{};
+  c.x = x; c.nodecol = L.nodecol.data(); c.spl = L.spl.data(); c.dur = L.dur.data();
+  c.ter = &L.terrain; c.rb = L.rb; c.fdisc_motion = L.fdisc_motion;
+  c.gait = L.gait; c.pinfo = L.pinfo.data(); c.pcols = L.pcols.data(); c.pact = L.pact.data(); c.sched = L.sched.data();
+  c.eelin = L.eelin.data(); c.rotvec = L.rotvec; c.cq = L.cost_q.data();
+  const int n_pad = (L.n + 2) & ~1;
+  std::vector<double> cs((size_t)std::max(1, L.cost_nslot), std::nan(""));
+  std::vector<unsigned long long> lacc(3 * (size_t)n_pad, 0);
+  int bad = 0;
+  double fs = 0.0;
+  for (const CostItem& it : L.cost_items) {
+    c.seg = it.seg >= 0 ? L.segs.data() + (size_t)it.seg * L.spl.size() : nullptr;
+    if (acc == 1) {
+      CostSlotEmit em{cs.data() + it.cslot, L.n};
+      eval_cost_item(c, it, em);
+      if (em.cs != cs.data() + it.cslot + it.cn) return 2;   // the host pass's slot count disagrees
+      fs += em.f;
+    } else {
+      CostLimbEmit em{lacc.data(), n_pad, &bad};
+      eval_cost_item(c, it, em);
+      fs += em.f;
+    }
+  }
+  for (int j = 0; j < L.n; ++j) {
+    if (acc == 1) {
+      double s = 0.0;
+      for (int k = L.cost_cptr[j]; k < L.cost_cptr[j + 1]; ++k) s += cs[L.cost_cslot[k]];
+      grad[j] = s;
+    } else {
+      grad[j] = bad ? std::nan("") : limb_value((long long)lacc[j], (long long)lacc[n_pad + j], (long long)lacc[2 * n_pad + j]);
+    }
+  }
+  *f = fs;
+  return 0;
+}
+
+namespace {
+struct CountEmit {
+  static constexpr bool kSparse = true;
+  double f = 0.0; long emits = 0, pres = 0; std::vector<int>* colcnt;
+  void skip(int) {}
+  void operator()(int, int col, double, bool p) { ++emits; if (p && col >= 0) { ++pres; ++(*colcnt)[col]; } }
+};
+}
+// cost work statistics at x (experiment aid): items per type, emissions, contributions per column
+extern "C" int emu_cost_stats(const towr_problem_desc_t* d, const double* x) {
+  Layout L; std::string e;
+  if (build_layout(*d, L, e)) return -1;
+  std::vector<int> colcnt(L.n + 1, 0);
+  Ctx c{};
+  c.x = x; c.nodecol = L.nodecol.data(); c.spl = L.spl.data(); c.dur = L.dur.data();
+  c.ter = &L.terrain; c.rb = L.rb; c.fdisc_motion = L.fdisc_motion;
+  c.gait = L.gait; c.pinfo = L.pinfo.data(); c.pcols = L.pcols.data(); c.pact = L.pact.data(); c.sched = L.sched.data();
+  c.eelin = L.eelin.data(); c.rotvec = L.rotvec; c.cq = L.cost_q.data();
+  long n_t[CT_COUNT] = {}, em_t[CT_COUNT] = {}, pr_t[CT_COUNT] = {}, mx_t[CT_COUNT] = {};
+  for (const CostItem& it : L.cost_items) {
+    c.seg = it.seg >= 0 ? L.segs.data() + (size_t)it.seg * L.spl.size() : nullptr;
+    CountEmit em{}; em.colcnt = &colcnt;
+    eval_cost_item(c, it, em);
+    n_t[it.type]++; em_t[it.type] += em.emits; pr_t[it.type] += em.pres; mx_t[it.type] = std::max(mx_t[it.type], em.emits);
+  }
+  for (int t = 0; t < CT_COUNT; ++t)
+    if (n_t[t]) std::printf("cost type %d: items %ld emits %ld present %ld max/item %ld\n", t, n_t[t], em_t[t], pr_t[t], mx_t[t]);
+  int touched = 0, mx = 0; long tot = 0;
+  for (int j = 0; j < L.n; ++j) if (colcnt[j]) { ++touched; mx = std::max(mx, colcnt[j]); tot += colcnt[j]; }
+  std::printf("n %d touched %d contributions %ld max/col %d\n", L.n, touched, tot, mx);
+  return 0;
+}
+
 // The composers' encoding bounds over every streamed block (layout.h kFloatDivMax, GsSeg int16 positions):
 // out[0..2] per GsClass: streamed (0/1); out[3..5]: its largest positions per instant (Lsum, GsGeo::Li);
 // out[6]: the largest CSR range of any FsBlock or GsBlock; out[7]: FDISC streamed

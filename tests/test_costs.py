@@ -96,6 +96,7 @@ def emu():
         subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "host_emu")])
     L = C.CDLL(lib)
     L.emu_cost.argtypes = [C.POINTER(capi.ProblemDesc), D, D, D, C.c_char_p, C.c_int]
+    L.emu_cost_acc.argtypes = [C.POINTER(capi.ProblemDesc), D, C.c_int, D, D]
     return L
 
 
@@ -111,6 +112,64 @@ def test_emulated_costs_match_oracle(emu, name):
         err = C.create_string_buffer(256)
         assert emu.emu_cost(C.byref(desc), x.ctypes.data_as(D), C.byref(f), g.ctypes.data_as(D), err, 256) == 0, err.value
         assert_cost_close(o.eval_f(x), f.value, o.eval_grad_f(x), g, f"{name} seed {seed}")
+
+
+@pytest.mark.parametrize("name", sorted(COSTS))
+def test_deterministic_gradient_paths_match_oracle(emu, name):
+    """The objective kernel's two deterministic gradient accumulations (cost_traj.hip), run on the host with
+    the kernel's own emitters: per-entry slots summed per column in the host's fixed order (fixed phase
+    durations) and exact fixed-point limbs (phase-duration optimisation; any layout). Both match the oracle;
+    the slot path must exist for every fixed-duration config here (ANYmal: 5,976 slots < kCostSlotMax)."""
+    desc = COSTS[name]
+    o = Oracle(desc)
+    for seed in (0, 1):
+        x = o.initial_x()
+        if seed:
+            x = x + 0.05 * np.random.default_rng(seed).standard_normal(o.n)
+        f_ref, g_ref = o.eval_f(x), o.eval_grad_f(x)
+        got = {}
+        for acc in (1, 2):
+            f, g = C.c_double(), np.zeros(o.n)
+            rc = emu.emu_cost_acc(C.byref(desc), x.ctypes.data_as(D), acc, C.byref(f), g.ctypes.data_as(D))
+            if acc == 1 and desc.optimize_timings:
+                assert rc == 1   # phase-duration optimisation has no slots: the limbs run
+                continue
+            assert rc == 0, f"acc {acc}: rc {rc}"
+            assert_cost_close(f_ref, f.value, g_ref, g, f"{name} seed {seed} acc {acc}")
+            got[acc] = g
+        if len(got) == 2:   # the two accumulations agree to rounding
+            np.testing.assert_allclose(got[1], got[2], rtol=1e-12, atol=1e-15 * max(1.0, np.abs(g_ref).max()))
+
+
+def test_limb_accumulation_is_order_independent():
+    """The limb encoding of cost_traj.hip's phase-duration path: random entries over a wide magnitude range,
+    added in two different orders, give the same limbs, hence the same bits; the value is the exact sum to
+    within the 2^-60 resolution per entry."""
+    rng = np.random.default_rng(11)
+    v = rng.standard_normal(500) * 10.0 ** rng.integers(-14, 12, 500)
+    v[::7] *= -1
+
+    def limbs(vals):
+        acc = [0, 0, 0]
+        for x in vals:
+            bits = int(np.float64(x).view(np.uint64))
+            ex = (bits >> 52) & 0x7FF
+            m = (bits & ((1 << 52) - 1)) | (1 << 52)
+            sh = ex - 1075 + 60
+            parts = []
+            for k in range(3):
+                s = sh - 42 * k
+                parts.append(0 if (s >= 42 or s <= -64) else (((m << s) if s >= 0 else (m >> -s)) & ((1 << 42) - 1)))
+            if bits >> 63:
+                parts = [-q for q in parts]
+            acc = [a + q for a, q in zip(acc, parts)]
+        return acc
+
+    a, b = limbs(v), limbs(v[::-1])
+    assert a == b
+    exact = sum(int(round(x * 2.0 ** 60)) for x in v)   # python ints: the exact fixed-point sum (to rounding per entry)
+    got = a[0] + (a[1] << 42) + (a[2] << 84)
+    assert abs(got - exact) <= len(v)
 
 
 def _create_layout(desc):

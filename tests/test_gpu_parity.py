@@ -148,6 +148,35 @@ def test_costs_batch_device_matches_single():
     assert np.all(np.isnan(Gh[:, o.n:]))   # nothing written past n
 
 
+@pytest.mark.parametrize("name", ["anymal_all_costs", "anymal_stairs_gaitopt_costs", "anymal_rotvec_costs",
+                                  "biped_energy_angmom"])
+def test_costs_gradient_bit_reproducible(name):
+    """The objective and gradient do not depend on scheduling: 512 copies of one x in a batch (blocks on
+    every CU at once) and a second call give identical bits in every row (cost_traj.hip: slots summed in
+    a fixed order, or exact fixed-point limbs), and the single-problem entry point gives the same bits."""
+    import torch
+    desc = COSTS[name]
+    o = Oracle(desc)
+    p = TowrGpuProblem(desc, device=0)
+    x = _perturb(o.initial_x(), 4242, 0.03)
+    B = 512
+    Xd = torch.from_numpy(np.tile(x, (B, 1))).cuda()
+    runs = []
+    for _ in range(2):
+        Fd = torch.zeros(B, dtype=torch.float64, device="cuda")
+        Gd = torch.zeros((B, o.n), dtype=torch.float64, device="cuda")
+        p.eval_cost_batch_device(Xd, Fd, Gd)
+        torch.cuda.synchronize()
+        runs.append((Fd.cpu().numpy(), Gd.cpu().numpy()))
+    for Fh, Gh in runs:
+        assert (Fh == Fh[0]).all()
+        assert (Gh.view(np.uint64) == Gh[0].view(np.uint64)).all(), f"rows differ: {np.unique(np.nonzero(Gh != Gh[0])[0])[:8]}"
+    np.testing.assert_array_equal(runs[0][1].view(np.uint64), runs[1][1].view(np.uint64))
+    g1 = p.eval_grad_f(x)
+    np.testing.assert_array_equal(g1.view(np.uint64), runs[0][1][0].view(np.uint64))
+    assert_cost_close(o.eval_f(x), runs[0][0][0], o.eval_grad_f(x), runs[0][1][0], name)
+
+
 # every launch arrangement (TOWR_GPU_FUSE) on configurations covering all launch classes: the
 # default fusion group, per-class launches, and the fused groups measured slower (kept selectable)
 @pytest.mark.parametrize("spec", ["none", "rf,dm", "drftm", "rftm,d"])

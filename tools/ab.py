@@ -1,7 +1,8 @@
-"""A/B of engine builds / environment switches on one GPU box: alternating bench runs, 3 rounds.
+"""A/B of engine builds / environment switches on one GPU box: alternating runs of bench.py itself (the driver's
+program: its x sets, leg order and reps), 3 rounds. The default arguments are the driver's flags.
 A measurement tool, not part of the product.
 usage: python tools/ab.py TAG "name:VAR=v,VAR2=v2" "name2:TOWR_GPU_LIB=tools/build/libtowr_gpu_x.so" ...
-       [--args "--steps 200 --warmup 20 --no-cpu --no-host --no-gait"] [--rounds 3]"""
+       [--args "--steps 20 --warmup 5 --no-cpu --no-host --legs objective,gait_optimization"] [--rounds 3]"""
 import argparse
 import json
 import os
@@ -9,13 +10,15 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LEGS = ("objective", "gait_optimization", "gait_torque", "rotvec")
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
     ap.add_argument("cfgs", nargs="+")
-    ap.add_argument("--args", default="--steps 200 --warmup 20 --no-cpu --no-host --no-gait")
+    ap.add_argument("--args", default="--steps 20 --warmup 5 --no-cpu --no-host "
+                                      "--legs objective,gait_optimization,gait_torque,rotvec")
     ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
@@ -37,14 +40,19 @@ def main():
             line = [l for l in open(log) if l.startswith("{")][-1]
             j = json.loads(line)
             ks = j["roofline"]["kernels"]
-            res.setdefault(name, []).append((j["ms_per_step"], {k: v["ms"] for k, v in ks.items()},
-                                             j.get("gait_optimization", {}).get("ms_per_batch")))
+            legs = {k: j[k]["ms_per_batch"] for k in LEGS if k in j}
+            res.setdefault(name, []).append((j["ms_per_step"], {k: v["ms"] for k, v in ks.items()}, legs))
             print(f"{name:12s} r{r} step {j['ms_per_step']:.4f} ms  " +
                   "  ".join(f"{k} {v['ms']:.4f}" for k, v in ks.items()) +
-                  (f"  gait {res[name][-1][2]:.4f}" if res[name][-1][2] else ""), flush=True)
+                  "".join(f"  {k} {v:.4f}" for k, v in legs.items()), flush=True)
     for name, v in res.items():
         steps = sorted(s for s, _, _ in v)
-        print(f"== {name}: step min {steps[0]:.4f} median {steps[len(steps) // 2]:.4f} ms")
+        line = f"== {name}: step {steps[0]:.4f}-{steps[-1]:.4f} ms"
+        for k in LEGS:
+            xs = sorted(l[k] for _, _, l in v if k in l)
+            if xs:
+                line += f" | {k} {xs[0]:.4f}-{xs[-1]:.4f}"
+        print(line, flush=True)
 
 
 if __name__ == "__main__":

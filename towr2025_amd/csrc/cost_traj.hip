@@ -10,37 +10,47 @@
 namespace tg {
 namespace {
 
-// Objective and gradient (IpoptAdapter::eval_f / eval_grad_f): one block per problem. The block
-// stages x and the node table in LDS and keeps the problem's dense gradient there; lanes take the
-// cost work items round-robin (grouped by kind, so waves mostly run one path) and add their
-// gradient entries with LDS atomics (ds_add_f64); f is reduced over the block. The gradient then
-// leaves with 16-byte non-temporal stores. The gradient's summation order is not fixed (atomics),
-// so it is reproducible to rounding only; f's order is fixed.
-template <bool GRAD>
-struct CostEmit {
-  double* grad;   // LDS; the dump slot at index n absorbs constant node values
-  double f = 0.0;
-  static constexpr bool kSparse = true;   // zero gradient contributions need no atomic
-  __device__ __forceinline__ void skip(int) {}
-  __device__ __forceinline__ void operator()(int, int col, double v, bool pres) {
-    if constexpr (GRAD)
-      if (pres && v != 0.0) atomicAdd(grad + col, v);
-  }
-};
+// Objective and gradient (IpoptAdapter::eval_f / eval_grad_f): one block per problem. The block stages x
+// and the node table in LDS; lanes take the cost work items round-robin (grouped by kind, so waves mostly
+// run one path). f is reduced over the block in a fixed order. The gradient is deterministic: every call
+// on the same x gives the same bits, whatever the scheduling of the block's waves.
+//   ACC = kAccSlots (fixed phase durations): an item writes its present entries to its own LDS slots
+//     (CostItem::cslot, Layout::cost_nslot), then one lane per column sums the column's slots in the host's
+//     fixed order (Layout::cost_cptr / cost_cslot, staged in LDS with x). Plain LDS stores and loads.
+//   ACC = kAccLimbs (phase-duration optimisation: the PhaseSpline windows a sample touches move with x):
+//     each entry is added as an exact fixed-point number v * 2^60 in three signed 42-bit limbs with
+//     64-bit integer LDS atomics. Integer addition is associative, so the sums are order-independent;
+//     a column's value is formed from its limbs once. Resolution 2^-60 (8.7e-19, far below the parity
+//     floor of 1e-12); |v| >= 2^65 or a NaN / inf entry makes the whole gradient NaN.
+//   ACC = kAccNone: f only.
+// SoftConstraint terms add J^T (g - b) per column from the soft child's CSR values, in row order
+// (towr_gpu.hip's column lists of the soft pattern).
+enum { kAccNone = 0, kAccSlots = 1, kAccLimbs = 2 };
 
-template <bool GAIT, bool GRAD, bool ROTVEC>
+template <int ACC, bool GAIT, bool ROTVEC>
 __global__ void __launch_bounds__(kCostBlock, 1) towr_cost_kernel(KParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int b = blockIdx.x;
-  double* gs = smem;                       // [n_pad] gradient (+ dump slot at n)
-  double* xs = smem + P.n_pad;             // [n_pad] x (+ zero slot at n)
-  int32_t* ns = reinterpret_cast<int32_t*>(smem + 2 * P.n_pad);
-  double* red = smem + P.lds_red_off;     // [kCostBlock / 64] per-wave partial objectives
+  double* xs = smem + P.lds_x_off;         // [n_pad] x (+ zero slot at n), then the node table
+  int32_t* ns = reinterpret_cast<int32_t*>(xs + P.n_pad);
+  double* red = smem + P.lds_red_off;      // [kCostBlock / 64] per-wave partial objectives
+  double* cs = smem;                       // kAccSlots: [cost_nslot] contributions
+  unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);   // kAccLimbs: [3][n_pad]
+  int* bad = reinterpret_cast<int*>(red + kCostBlock / 64);
+  // kAccSlots: the slot tables after the node table (16-byte units: cost_cslot, then cost_cptr)
+  uint16_t* cslot = reinterpret_cast<uint16_t*>(xs + P.n_pad + ((P.n_nodecol + 3) >> 2) * 2);
+  const int n16s = (P.c_nslot + 7) >> 3;
+  int32_t* cptr = reinterpret_cast<int32_t*>(cslot + 8 * n16s);
+  if constexpr (ACC == kAccSlots) {
+    stage16<kCostBlock>(reinterpret_cast<uint4*>(cslot), reinterpret_cast<const uint4*>(P.c_cslot), n16s);
+    stage16<kCostBlock>(reinterpret_cast<uint4*>(cptr), reinterpret_cast<const uint4*>(P.c_cptr), (P.n + 4) >> 2);
+  }
   stage_x<kCostBlock, true>(P, P.X + (int64_t)b * P.ldx, xs, ns);
-  if constexpr (GRAD)
-    for (int i = threadIdx.x; i < P.n_pad; i += kCostBlock) gs[i] = 0.0;
+  if constexpr (ACC == kAccLimbs) {
+    for (int i = threadIdx.x; i < 3 * P.n_pad; i += kCostBlock) acc[i] = 0;
+    if (threadIdx.x == 0) *bad = 0;
+  }
   __syncthreads();
-  CostEmit<GRAD> em{gs};
   Ctx c;
   c.x = xs; c.nodecol = ns; c.spl = P.spl; c.dur = P.dur;
   c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
@@ -49,29 +59,31 @@ __global__ void __launch_bounds__(kCostBlock, 1) towr_cost_kernel(KParams P) {
   c.rotvec = ROTVEC;
   c.dyn_scratch = nullptr;
   c.cq = P.cq;
+  double f = 0.0;
   for (int i = threadIdx.x; i < P.n_citems; i += kCostBlock) {
     const CostItem it = P.citems[i];
     c.seg = nullptr; c.sg = P.sg; c.row = it.seg;
-    eval_cost_item(c, it, em);
-  }
-  // SoftConstraint terms (soft_constraint.cc:52-69): 0.5 (g - b)^T (g - b) and J^T (g - b) over the
-  // wrapped sets' rows, from the soft child's g and CSR values of this problem (one row per lane)
-  if (P.s_m > 0) {
-    const double* sg = P.sG + (int64_t)b * P.s_ldg;
-    for (int r = threadIdx.x; r < P.s_m; r += kCostBlock) {
-      const double d = sg[r] - P.s_b[r];
-      em.f += (0.5 * d) * d;
-      if constexpr (GRAD) {
-        const double* sv = P.sV + (int64_t)b * P.s_ldv;
-        for (int k = P.s_rp[r]; k < P.s_rp[r + 1]; ++k) {
-          const double v = sv[k] * d;
-          if (v != 0.0) atomicAdd(gs + P.s_col[k], v);
-        }
-      }
+    if constexpr (ACC == kAccSlots) {
+      CostSlotEmit em{cs + it.cslot, P.n};
+      eval_cost_item(c, it, em);
+      f += em.f;
+    } else if constexpr (ACC == kAccLimbs) {
+      CostLimbEmit em{acc, P.n_pad, bad};
+      eval_cost_item(c, it, em);
+      f += em.f;
+    } else {
+      CostFEmit em;
+      eval_cost_item(c, it, em);
+      f += em.f;
     }
   }
+  // SoftConstraint terms (soft_constraint.cc:52-69): 0.5 (g - b)^T (g - b); the gradient J^T (g - b) below
+  const double* sgp = P.sG + (int64_t)b * P.s_ldg;
+  for (int r = threadIdx.x; r < P.s_m; r += kCostBlock) {
+    const double d = sgp[r] - P.s_b[r];
+    f += (0.5 * d) * d;
+  }
   // f: wave butterfly, then the waves' partials in order
-  double f = em.f;
   for (int o = 32; o > 0; o >>= 1) f += __shfl_xor(f, o, 64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = f;
   __syncthreads();
@@ -80,7 +92,33 @@ __global__ void __launch_bounds__(kCostBlock, 1) towr_cost_kernel(KParams P) {
     for (int w = 0; w < kCostBlock / 64; ++w) s += red[w];
     P.F[b] = s;
   }
-  if constexpr (GRAD) copy_out(gs, P.GR + (int64_t)b * P.ldgr, P.n, threadIdx.x, kCostBlock);
+  if constexpr (ACC != kAccNone) {
+    double* gr = P.GR + (int64_t)b * P.ldgr;
+    const double* sv = P.sV + (int64_t)b * P.s_ldv;
+    const bool nan_all = ACC == kAccLimbs && *bad != 0;
+    for (int j = threadIdx.x; j < P.n; j += kCostBlock) {
+      double s = 0.0;
+      if constexpr (ACC == kAccSlots) {
+        const int k1 = cptr[j + 1];
+        int k = cptr[j];
+        for (; k + 4 <= k1; k += 4) {   // the slot ids of 4 entries in flight together; the sum stays in order
+          const int i0 = cslot[k], i1 = cslot[k + 1], i2 = cslot[k + 2], i3 = cslot[k + 3];
+          const double a0 = cs[i0], a1 = cs[i1], a2 = cs[i2], a3 = cs[i3];
+          s += a0; s += a1; s += a2; s += a3;
+        }
+        for (; k < k1; ++k) s += cs[cslot[k]];
+      } else {
+        s = limb_value((long long)acc[j], (long long)acc[P.n_pad + j], (long long)acc[2 * P.n_pad + j]);
+        if (nan_all) s = __builtin_nan("");
+      }
+      if (P.s_m > 0)   // the soft child's column j, its rows in order
+        for (int k = P.s_cptr[j]; k < P.s_cptr[j + 1]; ++k) {
+          const int2 e = P.s_cent[k];   // (CSR index, row)
+          s += sv[e.x] * (sgp[e.y] - P.s_b[e.y]);
+        }
+      __builtin_nontemporal_store(s, gr + j);
+    }
+  }
 }
 // Trajectory export (SaveTrajectoryToCSV): one 64-lane block per (problem, 64 sample times). Each
 // lane evaluates its sample's row into an LDS buffer kept column-major with an odd stride (writes and
@@ -118,14 +156,16 @@ __global__ void __launch_bounds__(kTrajBlock, 1) towr_traj_kernel(KParams P, con
 
 }  // namespace
 
-template <bool GAIT, bool GRAD>
+template <int ACC, bool GAIT>
 const void* cost_kernel_rv(bool rotvec) {
-  return rotvec ? reinterpret_cast<const void*>(&towr_cost_kernel<GAIT, GRAD, true>)
-                : reinterpret_cast<const void*>(&towr_cost_kernel<GAIT, GRAD, false>);
+  return rotvec ? reinterpret_cast<const void*>(&towr_cost_kernel<ACC, GAIT, true>)
+                : reinterpret_cast<const void*>(&towr_cost_kernel<ACC, GAIT, false>);
 }
-const void* cost_kernel_for(bool gait, bool grad, bool rotvec) {
-  if (gait) return grad ? cost_kernel_rv<true, true>(rotvec) : cost_kernel_rv<true, false>(rotvec);
-  return grad ? cost_kernel_rv<false, true>(rotvec) : cost_kernel_rv<false, false>(rotvec);
+// acc: 0 f only, 1 gradient through slots (fixed phase durations only), 2 gradient through limbs
+const void* cost_kernel_for(bool gait, int acc, bool rotvec) {
+  if (gait) return acc ? cost_kernel_rv<kAccLimbs, true>(rotvec) : cost_kernel_rv<kAccNone, true>(rotvec);
+  return acc == 1 ? cost_kernel_rv<kAccSlots, false>(rotvec) : acc == 2 ? cost_kernel_rv<kAccLimbs, false>(rotvec)
+                  : cost_kernel_rv<kAccNone, false>(rotvec);
 }
 
 const void* traj_kernel_for(bool gait) {

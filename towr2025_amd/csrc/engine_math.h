@@ -2058,7 +2058,8 @@ struct CostItem {
                                    // test under gait optimisation); CT_ENERGYQ: a0 = Gram matrix index (Ctx::cq);
                                    // CT_BHC: a0 = contact-at-start bits, a1 = contact bits at t (fixed gait) or -1
   double t, w, wdt, tw;            // sample time, weight, weight * dt, EnergyCost torque weight
-  double p[3], pad;                // CT_EEBP: reference ee position in base frame
+  double p[3];                     // CT_EEBP: reference ee position in base frame
+  int32_t cslot, cn;               // gradient contribution slots [cslot, cslot + cn) (Layout::cost_nslot > 0)
 };
 
 // NodeCost (node_cost.cc:55-79): sum over nodes of w * value^2; d/dx_i = sum over the node values
@@ -2306,6 +2307,71 @@ TG_HD void eval_cost_item(const Ctx& c, const CostItem& it, Emit& em) {
     case CT_BHC: cost_bhc(c, it, em); break;
   }
 }
+
+// Gradient emitters of the objective kernel (cost_traj.hip), single-source so that the host emulation
+// (tests/host_emu) runs the kernel's exact accumulation. Both give the same bits on every call.
+// CostSlotEmit (fixed phase durations): an item's present entries (a variable's column: not a constant
+// node value, which is -1 on the host and the zero slot n on the device) go to consecutive slots from
+// CostItem::cslot, in emission order (layout.hip build_cost_slots enumerates the same entries).
+struct CostSlotEmit {
+  double* cs;
+  int n;
+  double f = 0.0;
+  static constexpr bool kSparse = true;
+  TG_HD void skip(int) {}
+  TG_HD void operator()(int, int col, double v, bool pres) {
+    if (pres && col >= 0 && col < n) *cs++ = v;
+  }
+};
+struct CostFEmit {   // f only
+  double f = 0.0;
+  static constexpr bool kSparse = true;
+  TG_HD void skip(int) {}
+  TG_HD void operator()(int, int, double, bool) {}
+};
+// CostLimbEmit (phase-duration optimisation): an entry v is added as the exact fixed-point integer
+// v * 2^60 split into three signed 42-bit limbs, accumulator k of column j at acc[k * n_pad + j]
+// (64-bit integer atomics on the device). Integer sums do not depend on the order of the additions.
+// Entries below 2^-60 in magnitude are truncated (the parity floor is 1e-12); a NaN, an infinity or
+// |v| >= 2^65 sets *bad (the kernel then returns a NaN gradient). Exact while a column has fewer than
+// 2^11 entries (its limb sums stay below 2^53 and convert to double exactly).
+constexpr unsigned long long kLimbMask = (1ull << 42) - 1;
+TG_HD long long limb_of(unsigned long long m, int s) {   // bits [0, 42) of m * 2^s
+  if (s >= 42 || s <= -64) return 0;
+  return (long long)((s >= 0 ? (m << s) : (m >> -s)) & kLimbMask);
+}
+TG_HD double limb_value(long long l0, long long l1, long long l2) {
+  return ((double)l2 * 0x1p24 + (double)l1 * 0x1p-18) + (double)l0 * 0x1p-60;
+}
+struct CostLimbEmit {
+  unsigned long long* acc;
+  int n_pad;
+  int* bad;
+  double f = 0.0;
+  static constexpr bool kSparse = true;   // zero entries need no addition
+  TG_HD void skip(int) {}
+  TG_HD void operator()(int, int col, double v, bool pres) {
+    if (!pres || v == 0.0 || col < 0) return;
+    unsigned long long bits;
+    __builtin_memcpy(&bits, &v, sizeof bits);
+    const int ex = (int)((bits >> 52) & 0x7ff);
+    if (ex == 0) return;                                        // subnormal: below the resolution
+    const int sh = ex - 1075 + 60;                              // v * 2^60 = m * 2^sh
+    if (ex == 0x7ff || sh > 126 - 53) { *bad = 1; return; }     // NaN / inf / |v| >= 2^65
+    const unsigned long long m = (bits & ((1ull << 52) - 1)) | (1ull << 52);
+    long long l0 = limb_of(m, sh), l1 = limb_of(m, sh - 42), l2 = limb_of(m, sh - 84);
+    if (bits >> 63) { l0 = -l0; l1 = -l1; l2 = -l2; }
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (l0) atomicAdd(acc + col, (unsigned long long)l0);
+    if (l1) atomicAdd(acc + n_pad + col, (unsigned long long)l1);
+    if (l2) atomicAdd(acc + 2 * n_pad + col, (unsigned long long)l2);
+#else
+    acc[col] += (unsigned long long)l0;
+    acc[n_pad + col] += (unsigned long long)l1;
+    acc[2 * n_pad + col] += (unsigned long long)l2;
+#endif
+  }
+};
 
 // ----------------------------------------------------------------------------------------------
 // Trajectory export (SaveTrajectoryToCSV, towr/src/utils/save_data.cpp:9-130): one row per sample

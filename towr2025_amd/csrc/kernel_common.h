@@ -81,16 +81,19 @@ struct KParams {
   const CostItem* citems;         // cost launch: work items, objective and gradient outputs
   const double* cq;               // cost launch: CT_ENERGYQ Gram matrices
   int32_t n_citems, lds_red_off;
+  const int32_t* c_cptr;          // cost launch, slot gradient (Layout::cost_cptr / cost_cslot, padded to 16 bytes)
+  const uint16_t* c_cslot;
+  int32_t c_nslot;
   double* F;
   double* GR; int64_t ldgr;
   // cost launch, SoftConstraint terms: the soft child's g (and CSR values) of this batch, its CSR
   // pattern, b = the bounds' mid-points; s_m = 0 without soft terms
   const double* sG; int64_t s_ldg;
   const double* sV; int64_t s_ldv;
-  const int32_t* s_rp;
-  const int32_t* s_col;
   const double* s_b;
   int32_t s_m;
+  const int32_t* s_cptr;          // the soft pattern by column: entries s_cent[s_cptr[j] .. s_cptr[j + 1]) =
+  const int2* s_cent;             // (CSR index, row), rows ascending
   // experiment build only (-DTOWR_STAMPS, tools/stamps.py): per-block timestamp slots of this launch, or null
   unsigned long long* stamps;
 };
@@ -424,7 +427,7 @@ __device__ __forceinline__ Ctx gait_record_setup(const KParams& P, int b, double
 const void* tile_kernel_for(int type, bool gait, bool rotvec);
 const void* misc_kernel_for(bool gait);
 const void* step_kernel_for(bool gait, bool rotvec, int kblock);
-const void* cost_kernel_for(bool gait, bool grad, bool rotvec);
+const void* cost_kernel_for(bool gait, int acc, bool rotvec);   // acc: 0 f only, 1 slots, 2 limbs
 const void* traj_kernel_for(bool gait);
 const void* rv_coef_kernel();
 constexpr int kRvCoefBlock = 256;   // the RotVec coefficient pre-pass: 4 waves, one component each

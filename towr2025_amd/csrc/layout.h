@@ -295,12 +295,21 @@ struct Layout {
   std::vector<CostItem> cost_items;
   std::vector<double> cost_q;        // CT_ENERGYQ Gram matrices, 16 doubles per item (CostItem::q)
   int32_t cost_type0[CT_COUNT + 1] = {};
+  // Deterministic gradient (fixed phase durations): every present gradient entry of every cost item has an
+  // LDS contribution slot (layout.hip build_cost_slots): entry k of item i goes to slot CostItem::cslot + k,
+  // and column j sums its slots cost_cslot[cost_cptr[j] .. cost_cptr[j + 1]) in that order.
+  // cost_nslot (slots incl. padding) = 0: fixed-point limbs instead (phase-duration optimisation, where the
+  // PhaseSpline windows move with x, or more slots than kCostSlotMax).
+  int32_t cost_nslot = 0;
+  std::vector<int32_t> cost_cptr;
+  std::vector<uint16_t> cost_cslot;
   // SoftConstraint terms (TOWR_COST_SOFT), in cost order: the cost index and the wrapped constraint.
   // The wrapped sets are evaluated by a second layout (the handle's soft child) whose constraint
   // list is exactly these sets in this order (soft_desc).
   std::vector<std::pair<int32_t, int32_t>> soft;
 };
 
+constexpr int kCostSlotMax = 8192;   // contribution slots of the cost kernel's LDS (64 KB)
 constexpr int kMiscWaves = 4;   // one-wave small-kind tiles per group (block)
 constexpr int kSlotSpare = 4;   // spare slot groups per lane: the kernels prefetch up to this many ahead
 constexpr bool is_misc_kind(int t) { return t != IT_DYN && t != IT_ROM && t != IT_FDISC && t != IT_TQDISC; }

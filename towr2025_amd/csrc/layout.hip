@@ -455,6 +455,48 @@ Ctx host_ctx(const Layout& L, const double* x, const towr_terrain_t& ter) {
   cx.eelin = L.eelin.data(); cx.lin = L.lin.data(); cx.rotvec = L.rotvec;
   return cx;
 }
+// Deterministic gradient slots (Layout::cost_nslot): with fixed phase durations every cost item's gradient
+// entries go to columns that do not depend on x, so the host enumerates them once. An entry is present when
+// its column is a variable (a constant node value has none). Item i writes its k-th present entry to slot
+// CostItem::cslot + k (plain LDS stores, no address load; an item's range is padded to an odd length, so the
+// lanes of a wave running items of one kind store to distinct LDS banks). Column j's slots, ascending, are
+// cost_cslot[cost_cptr[j] .. cost_cptr[j + 1]), and one lane sums them in that order. No atomics: the same
+// bits on every call.
+namespace {
+struct CostSlotPass {
+  std::vector<int32_t>* cols;
+  double f = 0.0;
+  void operator()(int, int col, double, bool pres) { if (pres && col >= 0) cols->push_back(col); }
+};
+}
+void build_cost_slots(Layout& L) {
+  L.cost_nslot = 0; L.cost_cptr.clear(); L.cost_cslot.clear();
+  if (L.gait || L.cost_items.empty()) return;   // PhaseSpline windows move with x: fixed-point limbs instead
+  Ctx cx = host_ctx(L, L.x0.data(), L.terrain);
+  cx.cq = L.cost_q.data();
+  std::vector<int32_t> cols;
+  for (CostItem& it : L.cost_items) {
+    cx.seg = it.seg >= 0 ? L.segs.data() + (size_t)it.seg * L.spl.size() : nullptr;
+    const size_t c0 = cols.size();
+    CostSlotPass em{&cols};
+    eval_cost_item(cx, it, em);
+    it.cslot = (int32_t)c0; it.cn = (int32_t)(cols.size() - c0);
+    if (!(it.cn & 1)) cols.push_back(-1);   // odd stride between the slot ranges of like items
+  }
+  if (cols.empty() || cols.size() > (size_t)kCostSlotMax) {   // too many for the LDS budget: limbs
+    for (CostItem& it : L.cost_items) it.cslot = it.cn = 0;
+    return;
+  }
+  L.cost_cptr.assign(L.n + 1, 0);
+  for (int32_t c : cols) if (c >= 0) ++L.cost_cptr[c + 1];
+  for (int j = 0; j < L.n; ++j) L.cost_cptr[j + 1] += L.cost_cptr[j];
+  L.cost_cslot.resize(L.cost_cptr[L.n]);
+  std::vector<int32_t> fill(L.cost_cptr.begin(), L.cost_cptr.end() - 1);
+  for (size_t k = 0; k < cols.size(); ++k)
+    if (cols[k] >= 0) L.cost_cslot[fill[cols[k]]++] = (uint16_t)k;   // ascending per column
+  L.cost_nslot = (int32_t)cols.size();
+}
+
 // presence bits (dim * rows + row) of a watched instant's motion blocks at cx.x: the scales eval_fdisc /
 // eval_tqdisc emit with, exactly as the structure pass evaluates them
 int watch_presence(const Layout& L, Ctx& cx, const WatchItem& w) {
@@ -1304,6 +1346,8 @@ int build_layout_ex(const towr_problem_desc_t& d, int n_data, const towr_data_t*
     }
     item_cand_begin[L.items.size()] = (int32_t)crow.size();
   }
+
+  build_cost_slots(L);
 
   // ---- pattern watch: x0 presence of the data-dependent motion blocks (curved terrain)
   L.watch.clear();

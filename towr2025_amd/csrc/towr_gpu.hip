@@ -148,8 +148,10 @@ struct towr_gpu_handle_s {
   towr_gpu_handle_s* soft = nullptr;
   std::vector<double> soft_b;
   double* d_soft_b = nullptr;
-  int32_t* d_soft_rp = nullptr;
-  int32_t* d_soft_col = nullptr;
+  int32_t* d_soft_cptr = nullptr;   // the soft pattern by column (KParams::s_cptr / s_cent)
+  int2* d_soft_cent = nullptr;
+  int32_t* d_c_cptr = nullptr;      // the cost gradient's slot lists (Layout::cost_cptr / cost_cslot)
+  uint16_t* d_c_cslot = nullptr;
   double *d_sg = nullptr, *d_sv = nullptr;
   int64_t soft_cap_g = 0, soft_cap_v = 0;   // problems the scratch holds
 };
@@ -212,6 +214,21 @@ int upload(towr_gpu_handle h, T** dst, const std::vector<T>& src) {
   HIPCHK(h, hipMalloc(reinterpret_cast<void**>(dst), bytes));
   if (!src.empty()) HIPCHK(h, hipMemcpy(*dst, src.data(), sizeof(T) * src.size(), hipMemcpyHostToDevice));
   return TOWR_OK;
+}
+
+// a copy padded to whole 16-byte units (k elements), for a kernel that stages it with 16-byte loads
+template <class T>
+std::vector<T> padded(const std::vector<T>& v, size_t k) {
+  std::vector<T> out(v);
+  out.resize((v.size() + k - 1) / k * k, T{});
+  return out;
+}
+
+// the cost kernel's slot-id table as it stages it: cost_nslot entries (padding included) in 16-byte units
+std::vector<uint16_t> cost_slot_table(const Layout& L) {
+  std::vector<uint16_t> t(L.cost_cslot);
+  t.resize(std::max(t.size(), (size_t)L.cost_nslot), 0);
+  return padded(t, 8);
 }
 
 // every evaluation entry point: refuse layout-only handles, make the handle's device current
@@ -787,9 +804,19 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
   return TOWR_OK;
 }
 
-// LDS of the cost launch: [gradient + dump slot | x + zero slot | node table | wave partials]
-size_t cost_red_off(const Layout& L) { return 2 * (size_t)((L.n + 2) & ~1) + (L.nodecol.size() + 3) / 4 * 2; }
-size_t cost_lds_bytes(const Layout& L) { return sizeof(double) * (cost_red_off(L) + kCostBlock / 64); }
+// LDS of the cost launch (doubles): [accumulators | x + zero slot | node table | wave partials, error flag].
+// The accumulators (cost_traj.hip): acc 1 = one slot per present gradient entry (Layout::cost_nslot), acc 2 =
+// three 64-bit limbs per column, acc 0 (f only) = none.
+int cost_acc(const Layout& L, bool grad) { return !grad ? 0 : L.cost_nslot > 0 ? 1 : 2; }
+size_t cost_x_off(const Layout& L, int acc) {
+  const size_t n_pad = (size_t)((L.n + 2) & ~1);
+  return acc == 1 ? (size_t)((L.cost_nslot + 1) & ~1) : acc == 2 ? 3 * n_pad : 0;
+}
+size_t cost_red_off(const Layout& L, int acc) {   // ... after x and the node table: acc 1's slot tables (16-byte units)
+  const size_t tabs = acc == 1 ? 2 * ((size_t)(L.cost_nslot + 7) / 8 + (size_t)(L.n + 4) / 4) : 0;
+  return cost_x_off(L, acc) + (size_t)((L.n + 2) & ~1) + (L.nodecol.size() + 3) / 4 * 2 + tabs;
+}
+size_t cost_lds_bytes(const Layout& L, int acc) { return sizeof(double) * (cost_red_off(L, acc) + kCostBlock / 64 + 2); }
 
 int launch(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* G, int64_t ldg, double* V, int64_t ldv,
            int want_g, int want_jac, hipStream_t s, const towr_terrain_t* terrains, int per_problem, int only_class);
@@ -806,7 +833,7 @@ int launch_soft(towr_gpu_handle h, int B, const double* X, int64_t ldx, bool gra
   if (int rc = launch(c, B, X, ldx, h->d_sg, ms, grad ? h->d_sv : nullptr, nzs, 1, grad ? 1 : 0, s, terrains, per_problem, -1))
     return fail(h, rc, "SoftConstraint sets: " + c->err);
   P.sG = h->d_sg; P.s_ldg = ms; P.sV = h->d_sv; P.s_ldv = nzs;
-  P.s_rp = h->d_soft_rp; P.s_col = h->d_soft_col; P.s_b = h->d_soft_b; P.s_m = c->L.m;
+  P.s_cptr = h->d_soft_cptr; P.s_cent = h->d_soft_cent; P.s_b = h->d_soft_b; P.s_m = c->L.m;
   return TOWR_OK;
 }
 
@@ -828,11 +855,14 @@ int launch_cost(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* 
   P.n = L.n; P.n_pad = (L.n + 2) & ~1; P.n_nodecol = (int32_t)L.nodecol.size();
   P.fdisc_motion = L.fdisc_motion; P.rb = L.rb;
   P.citems = h->d_citems; P.n_citems = (int32_t)L.cost_items.size(); P.cq = h->d_cq;
-  P.lds_red_off = (int32_t)cost_red_off(L);
+  const int acc = cost_acc(L, GR != nullptr);
+  P.lds_x_off = (int32_t)cost_x_off(L, acc);
+  P.lds_red_off = (int32_t)cost_red_off(L, acc);
+  P.c_cptr = h->d_c_cptr; P.c_cslot = h->d_c_cslot; P.c_nslot = L.cost_nslot;
   P.F = F; P.GR = GR; P.ldgr = ldgr;
   void* args[] = {&P};
-  HIPCHK(h, launch_kernel(cost_kernel_for(L.gait, GR != nullptr, L.rotvec), dim3((unsigned)B), dim3(kCostBlock), args,
-                            cost_lds_bytes(L), s));
+  HIPCHK(h, launch_kernel(cost_kernel_for(L.gait, acc, L.rotvec), dim3((unsigned)B), dim3(kCostBlock), args,
+                            cost_lds_bytes(L, acc), s));
   return h->soft ? scratch_release(h, s) : TOWR_OK;
 }
 
@@ -1222,7 +1252,8 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
       (r = upload(h, &h->d_pinfo, L.pinfo)) || (r = upload(h, &h->d_pcols, L.pcols)) || (r = upload(h, &h->d_pact, L.pact)) || (r = upload(h, &h->d_sched, L.sched)) ||
       (r = upload(h, &h->d_misc, L.misc_tiles)) || (r = upload(h, &h->d_misc_lds, L.misc_lds)) || (r = upload(h, &h->d_xspan, L.misc_xspan)) || (r = upload(h, &h->d_eelin, L.eelin)) ||
       (r = upload(h, &h->d_lin, L.lin)) ||
-      (r = upload(h, &h->d_citems, L.cost_items)) || (r = upload(h, &h->d_cq, L.cost_q)) || (r = upload(h, &h->d_gtab, gait_blob(L))) ||
+      (r = upload(h, &h->d_citems, L.cost_items)) || (r = upload(h, &h->d_cq, L.cost_q)) ||
+      (r = upload(h, &h->d_c_cptr, padded(L.cost_cptr, 4))) || (r = upload(h, &h->d_c_cslot, cost_slot_table(L))) || (r = upload(h, &h->d_gtab, gait_blob(L))) ||
       (r = upload(h, &h->d_idir, L.idirect)) || (r = upload(h, &h->d_fsb, L.fs_blocks)) || (r = upload(h, &h->d_fs_t, L.fs_t)) ||
       (r = upload(h, &h->d_fs_tmpl, L.fs_tmpl)) || (r = upload(h, &h->d_fs_ws, L.fs_ws)) ||
       (r = upload(h, &h->d_ff_geo, L.ff_geo)) || (r = upload(h, &h->d_ff_blob, L.ff_blob)) ||
@@ -1245,10 +1276,16 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
     }
     if ((r = upload(h, &h->d_traj_pd, pd)) || (r = upload(h, &h->d_traj_n, pn)) || (r = upload(h, &h->d_traj_c0, pc))) return bail(r);
   }
-  if (h->soft) {   // the soft child's pattern (int32 row pointers: its nnz is small) and b
+  if (h->soft) {   // the soft child's pattern by column, rows ascending (int32: its nnz is small), and b
     const Layout& C = h->soft->L;
-    std::vector<int32_t> rp(C.row_ptr.begin(), C.row_ptr.end());
-    if ((r = upload(h, &h->d_soft_rp, rp)) || (r = upload(h, &h->d_soft_col, C.col)) || (r = upload(h, &h->d_soft_b, h->soft_b))) return bail(r);
+    std::vector<int32_t> cptr(L.n + 1, 0);
+    for (int32_t c : C.col) ++cptr[c + 1];
+    for (int j = 0; j < L.n; ++j) cptr[j + 1] += cptr[j];
+    std::vector<int2> cent(C.col.size());
+    std::vector<int32_t> fill(cptr.begin(), cptr.end() - 1);
+    for (int row = 0; row < C.m; ++row)
+      for (int64_t k = C.row_ptr[row]; k < C.row_ptr[row + 1]; ++k) cent[fill[C.col[k]]++] = make_int2((int)k, row);
+    if ((r = upload(h, &h->d_soft_cptr, cptr)) || (r = upload(h, &h->d_soft_cent, cent)) || (r = upload(h, &h->d_soft_b, h->soft_b))) return bail(r);
   }
   {   // segment table in 32-row blocks (see SegSoA)
     const int nspl = (int)L.spl.size();
@@ -1354,13 +1391,14 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
     }
   }
   {
-    const size_t lds = cost_lds_bytes(L);
-    if (lds > 160 * 1024) { h->err = "problem too large for the cost kernel's LDS gradient"; return bail(TOWR_ERR_UNSUPPORTED); }
-    if (lds > 64 * 1024)
-      for (int g = 0; g < 2; ++g)
-        if (hipFuncSetAttribute(cost_kernel_for(L.gait, g != 0, L.rotvec), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
-          h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
-        }
+    for (int g = 0; g < 2; ++g) {
+      const int acc = cost_acc(L, g != 0);
+      const size_t lds = cost_lds_bytes(L, acc);
+      if (lds > 160 * 1024) { h->err = "problem too large for the cost kernel's LDS gradient"; return bail(TOWR_ERR_UNSUPPORTED); }
+      if (lds > 64 * 1024 && hipFuncSetAttribute(cost_kernel_for(L.gait, acc, L.rotvec), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+        h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
+      }
+    }
   }
   *out = h;
   return TOWR_OK;
@@ -1372,7 +1410,7 @@ int towr_gpu_destroy(towr_gpu_handle h) {
                  h->d_pinfo, h->d_pcols, h->d_pact, h->d_sched, h->d_misc, h->d_misc_lds, h->d_misc_wave, h->d_misc_items, h->d_xspan, h->d_eelin, h->d_gtab, h->d_idir, h->d_citems, h->d_cq, h->fuse[0].d_units, h->fuse[1].d_units,
                  h->d_bterrain, h->d_x, h->d_g, h->d_v, h->d_f, h->d_grad,
                  h->d_traj_pd, h->d_traj_n, h->d_traj_c0, h->d_traj_t, h->d_fsb, h->d_fs_t, h->d_fs_tmpl, h->d_fs_ws, h->d_ff_geo, h->d_ff_blob,
-                 h->d_fs_iee, h->d_fs_irow, h->d_fs_iblk, h->d_fsrec, h->d_lin, h->d_soft_b, h->d_soft_rp, h->d_soft_col, h->d_sg, h->d_sv,
+                 h->d_fs_iee, h->d_fs_irow, h->d_fs_iblk, h->d_fsrec, h->d_lin, h->d_soft_b, h->d_soft_cptr, h->d_soft_cent, h->d_c_cptr, h->d_c_cslot, h->d_sg, h->d_sv,
                  h->single.d_units, h->d_gs_geo, h->d_gs_tmpl, h->d_gs_pcode, h->d_gs_blk[0], h->d_gs_blk[1], h->d_gs_blk[2],
                  h->d_gs_inst[0], h->d_gs_inst[1], h->d_gs_inst[2], h->d_gsrec, h->d_rvc, h->d_rvi, h->d_gs_segs, h->d_gs_tseg, h->d_gs_vmap, h->d_gs_ws, h->d_gs_blob};
   if (h->device >= 0) for (void* p : dev) if (p) (void)hipFree(p);
