@@ -375,7 +375,7 @@ def main():
             with open(pmc) as fh:
                 rec = json.load(fh)
             k = rec.get("kernels", {}).get(dom)
-            if rec.get("problems_per_launch") == B and k:
+            if k and k.get("problems_per_launch", rec.get("problems_per_launch")) == B:
                 out["roofline"]["traffic"] = k["hbm_bytes_per_launch"]
                 out["roofline"]["traffic_source"] = rec.get("source")
         except Exception:

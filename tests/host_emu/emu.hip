@@ -122,56 +122,6 @@ extern "C" int emu_eval_ex(const towr_problem_desc_t* d, int n_data, const towr_
   }
   return 0;
 }
-// The fused FDISC kernel's stages (gs_cls.h ff_pdur / ff_sums / ff_stage1-3 / ff_g over the layout's FfGeo blobs, as
-// towr_fdisc_fused_kernel runs them, sub-lanes in order) against fdisc_instant (the record kernel's quantities): every
-// record field and g row of every FsBlock instant, bit for bit. Returns the mismatches (-1: no fused layout);
-// *checked = the values compared.
-extern "C" int64_t emu_ff_check(const towr_problem_desc_t* d, const double* x, int64_t* checked) {
-  Layout L; std::string e;
-  if (build_layout(*d, L, e) || !L.fstream || L.ff_geo.empty()) return -1;
-  Ctx c{};
-  c.x = x; c.nodecol = L.nodecol.data(); c.spl = L.spl.data(); c.dur = L.dur.data();
-  c.ter = &L.terrain; c.rb = L.rb; c.fdisc_motion = L.fdisc_motion;
-  c.gait = L.gait; c.pinfo = L.pinfo.data(); c.pcols = L.pcols.data(); c.sched = L.sched.data(); c.pact = L.pact.data();
-  int64_t bad = 0, n = 0;
-  auto cmp = [&](double a, double b) { ++n; if (std::memcmp(&a, &b, sizeof(double)) != 0) ++bad; };
-  for (const FsBlock& fb : L.fs_blocks) {
-    const FfGeo& g = L.ff_geo[fb.ff];
-    std::vector<int32_t> blob((size_t)g.blob_n16 * 4);
-    std::memcpy(blob.data(), L.ff_blob.data() + g.blob0, blob.size() * sizeof(int32_t));
-    std::vector<double> lx((size_t)g.nx), tm((size_t)(4 * L.ff_np_max + L.ff_ph_max));
-    for (int j = 0; j < g.nx; ++j) { const int col = blob[(size_t)g.o_gather + j]; lx[j] = col >= 0 ? x[col] : 0.0; }
-    FfView v;
-    v.g = g; v.blob = blob.data(); v.lx = lx.data(); v.ter = &L.terrain;
-    v.pdm = tm.data(); v.pem = v.pdm + L.ff_np_max; v.pdf = v.pem + L.ff_np_max; v.pef = v.pdf + L.ff_np_max; v.phe = v.pef + L.ff_np_max;
-    for (int i = 0; i < g.np_m + g.np_f; ++i) ff_pdur(v, i);
-    for (int w = 0; w < 3; ++w) ff_sums(v, w);
-    for (int kk = 0; kk < fb.n_inst; ++kk) {
-      const double t = L.fs_t[fb.t0 + kk];
-      double X[kFfEx], R[kFsCS];
-      for (int sub = 0; sub < 3; ++sub) ff_stage1(v, t, sub, X);
-      for (int sub = 0; sub < 7; ++sub) ff_stage2(v, sub, X);
-      for (int sub = 0; sub < kFfLanes; ++sub) ff_stage3(v, sub, X, R);
-      FdiscInstant o;
-      c.seg = nullptr;
-      fdisc_instant(c, fb.ee, t, o);
-      const int ws = L.fs_ws[2 * (fb.wsoff + o.poly)], wd = L.fs_ws[2 * (fb.wsoff + o.poly) + 1];
-      for (int q = 0; q < kFsWin; ++q) {   // fdisc_record's window sums
-        const int pos = ws + q;
-        const int32_t te = pos < fb.L ? L.fs_tmpl[fb.tmpl + pos] : -1;
-        cmp(R[q], te >= 0 ? phase_basis_sum(L.pcols[te & 0xFFFFFF], o.poly, o.H[0], o.H[1], o.H[2], o.H[3]) : 0.0);
-      }
-      for (int i = 0; i < 5; ++i)
-        for (int k = 0; k < 3; ++k) cmp(R[kFsB + 3 * i + k], o.b[i][k]);
-      for (int k = 0; k < 3; ++k) { cmp(R[kFsDx + k], o.Jf.dx[k]); cmp(R[kFsV + k], o.Jf.v[k]); }
-      cmp(R[kFsND], gs_int(ws)); cmp(R[kFsND + 1], gs_int(wd)); cmp(R[kFsND + 2], gs_int(o.Jf.cur));
-      for (int i = 0; i < 5; ++i) cmp(ff_g(X, i), o.g[i]);
-    }
-  }
-  if (checked) *checked = n;
-  return bad;
-}
-
 extern "C" int emu_eval(const towr_problem_desc_t* d, const double* x, double* g, double* v, char* err, int errlen) {
   return emu_eval_ex(d, 0, nullptr, x, g, v, err, errlen);
 }
@@ -221,9 +171,9 @@ extern "C" int emu_cost_acc(const towr_problem_desc_t* d, const double* x, int a
   for (const CostItem& it : L.cost_items) {
     c.seg = it.seg >= 0 ? L.segs.data() + (size_t)it.seg * L.spl.size() : nullptr;
     if (acc == 1) {
-      CostSlotEmit em{cs.data() + it.cslot, L.n};
+      CostSlotEmit em{cs.data(), L.cost_cslot.data() + it.cslot, L.n};
       eval_cost_item(c, it, em);
-      if (em.cs != cs.data() + it.cslot + it.cn) return 2;   // the host pass's slot count disagrees
+      if (em.slot != L.cost_cslot.data() + it.cslot + it.cn) return 2;   // the host pass's slot count disagrees
       fs += em.f;
     } else {
       CostLimbEmit em{lacc.data(), n_pad, &bad};
@@ -234,7 +184,7 @@ extern "C" int emu_cost_acc(const towr_problem_desc_t* d, const double* x, int a
   for (int j = 0; j < L.n; ++j) {
     if (acc == 1) {
       double s = 0.0;
-      for (int k = L.cost_cptr[j]; k < L.cost_cptr[j + 1]; ++k) s += cs[L.cost_cslot[k]];
+      for (int k = L.cost_cptr[j]; k < L.cost_cptr[j + 1]; ++k) s += cs[k];
       grad[j] = s;
     } else {
       grad[j] = bad ? std::nan("") : limb_value((long long)lacc[j], (long long)lacc[n_pad + j], (long long)lacc[2 * n_pad + j]);

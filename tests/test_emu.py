@@ -61,25 +61,3 @@ def test_small_kinds_stage_part_of_x(emu, name):
     assert emu.emu_misc_xspan(C.byref(desc), out) == 0
     spans, units, total = out[0], out[1], out[2]
     assert 0 < spans and 0 < units < 0.8 * total, (spans, units, total)
-
-
-GAIT_FLAT = ["anymal_stairs_gaitopt", "biped_walk_gaitopt", "anymal_gait_torque", "hopper_gait_torque", "biped_gaitopt_rotvec"]
-
-
-@pytest.mark.parametrize("name", GAIT_FLAT)
-def test_fused_fdisc_stages_match_records(emu, name):
-    """The fused FDISC kernel's stages (gs_cls.h ff_*: the constraint blob, the local x, the split record evaluation),
-    run on the host as towr_fdisc_fused_kernel runs them, give every record field and g row of fdisc_instant (the
-    record kernel's quantities) bit for bit, at x0 and at perturbed x."""
-    import ctypes as C
-    from oracle.oracle import Oracle
-    desc = CONFIGS[name]
-    o = Oracle(desc)
-    x0 = o.initial_x()
-    emu.emu_ff_check.restype = C.c_int64
-    for seed in (0, 1, 2):
-        x = x0 if seed == 0 else x0 + 0.03 * np.random.default_rng(5000 + seed).standard_normal(o.n)
-        x = np.ascontiguousarray(x)
-        n = C.c_int64(0)
-        bad = emu.emu_ff_check(C.byref(desc), x.ctypes.data_as(C.POINTER(C.c_double)), C.byref(n))
-        assert bad == 0 and n.value > 0, f"{name} seed {seed}: {bad} of {n.value} fused record values differ"

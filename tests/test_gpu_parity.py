@@ -434,9 +434,7 @@ def test_batch_device_gait_two_chains(monkeypatch):
         np.testing.assert_array_equal(G[s:e, :p.m], g.cpu().numpy(), err_msg=f"g of problems [{s}, {e})")
         np.testing.assert_array_equal(V[s:e, :p.nnz], v.cpu().numpy(), err_msg=f"J of problems [{s}, {e})")
     # one launch stream (TOWR_GPU_STREAMS=1, read at handle creation): the two chains one after the other
-    # and the FDISC chain as the fused kernel (TOWR_GPU_FDISC_FUSED=1, gstream.hip towr_fdisc_fused_kernel) instead of
-    # records + compose
-    for var, val in (("TOWR_GPU_STREAMS", "1"), ("TOWR_GPU_FDISC_FUSED", "1")):
+    for var, val in (("TOWR_GPU_STREAMS", "1"),):
         monkeypatch.setenv(var, val)
         q = TowrGpuProblem(desc)
         monkeypatch.delenv(var)
@@ -476,11 +474,18 @@ def test_batch_device_gait_torque(monkeypatch, streams):
     _batch_vs_single(f, f"anymal_gait_torque_batch streams={streams}", B=64, optimize_timings=True)
 
 
-def test_batch_device_rotvec():
-    """RotVecConverter base orientation (ROTVEC kernels) as a randomised device batch."""
+@pytest.mark.parametrize("streams", [None, "1"])
+def test_batch_device_rotvec(monkeypatch, streams):
+    """RotVecConverter base orientation (ROTVEC kernels) as a randomised device batch, every problem bit-identical to
+    its B = 1 evaluation: by default the coefficient pre-pass, Dynamic and the small kinds on side stream 0 beside
+    RangeOfMotion and FDISC; TOWR_GPU_STREAMS=1 (read at handle creation): every launch on the caller's stream."""
+    if streams is None:
+        monkeypatch.delenv("TOWR_GPU_STREAMS", raising=False)
+    else:
+        monkeypatch.setenv("TOWR_GPU_STREAMS", streams)
     f = F.anymal_trot()
     f.params_.angular_rep_ = 1
-    _batch_vs_single(f, "anymal_rotvec_batch", B=64)
+    _batch_vs_single(f, f"anymal_rotvec_batch streams={streams}", B=64)
 
 
 def test_batch_terrain_count_must_match():

@@ -14,9 +14,10 @@ namespace {
 // and the node table in LDS; lanes take the cost work items round-robin (grouped by kind, so waves mostly
 // run one path). f is reduced over the block in a fixed order. The gradient is deterministic: every call
 // on the same x gives the same bits, whatever the scheduling of the block's waves.
-//   ACC = kAccSlots (fixed phase durations): an item writes its present entries to its own LDS slots
-//     (CostItem::cslot, Layout::cost_nslot), then one lane per column sums the column's slots in the host's
-//     fixed order (Layout::cost_cptr / cost_cslot, staged in LDS with x). Plain LDS stores and loads.
+//   ACC = kAccSlots (fixed phase durations): an item writes each present entry to its slot, the slots ordered
+//     by column (Layout::cost_cslot, CostItem::cslot), then one lane per column sums the column's slots
+//     [cost_cptr[j], cost_cptr[j + 1]) in order. Both tables are staged in LDS once per block: plain LDS
+//     stores and loads, no atomics.
 //   ACC = kAccLimbs (phase-duration optimisation: the PhaseSpline windows a sample touches move with x):
 //     each entry is added as an exact fixed-point number v * 2^60 in three signed 42-bit limbs with
 //     64-bit integer LDS atomics. Integer addition is associative, so the sums are order-independent;
@@ -27,10 +28,12 @@ namespace {
 // (towr_gpu.hip's column lists of the soft pattern).
 enum { kAccNone = 0, kAccSlots = 1, kAccLimbs = 2 };
 
+// Blocks are persistent (the host launches as many as fit the device at once, cost_grid): a block stages the
+// node table and the slot tables once, then takes problems blockIdx.x, + gridDim.x, ...; the next problem's x
+// is in flight (XStage registers) while the block evaluates the current one, and goes to LDS after it.
 template <int ACC, bool GAIT, bool ROTVEC>
 __global__ void __launch_bounds__(kCostBlock, 1) towr_cost_kernel(KParams P) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int b = blockIdx.x;
   double* xs = smem + P.lds_x_off;         // [n_pad] x (+ zero slot at n), then the node table
   int32_t* ns = reinterpret_cast<int32_t*>(xs + P.n_pad);
   double* red = smem + P.lds_red_off;      // [kCostBlock / 64] per-wave partial objectives
@@ -40,84 +43,94 @@ __global__ void __launch_bounds__(kCostBlock, 1) towr_cost_kernel(KParams P) {
   // kAccSlots: the slot tables after the node table (16-byte units: cost_cslot, then cost_cptr)
   uint16_t* cslot = reinterpret_cast<uint16_t*>(xs + P.n_pad + ((P.n_nodecol + 3) >> 2) * 2);
   const int n16s = (P.c_nslot + 7) >> 3;
-  int32_t* cptr = reinterpret_cast<int32_t*>(cslot + 8 * n16s);
+  uint16_t* cptr = cslot + 8 * n16s;
   if constexpr (ACC == kAccSlots) {
     stage16<kCostBlock>(reinterpret_cast<uint4*>(cslot), reinterpret_cast<const uint4*>(P.c_cslot), n16s);
-    stage16<kCostBlock>(reinterpret_cast<uint4*>(cptr), reinterpret_cast<const uint4*>(P.c_cptr), (P.n + 4) >> 2);
+    stage16<kCostBlock>(reinterpret_cast<uint4*>(cptr), reinterpret_cast<const uint4*>(P.c_cptr), (P.n + 8) >> 3);
   }
+  int b = blockIdx.x;
+  const int G = gridDim.x;
   stage_x<kCostBlock, true>(P, P.X + (int64_t)b * P.ldx, xs, ns);
-  if constexpr (ACC == kAccLimbs) {
-    for (int i = threadIdx.x; i < 3 * P.n_pad; i += kCostBlock) acc[i] = 0;
-    if (threadIdx.x == 0) *bad = 0;
-  }
-  __syncthreads();
   Ctx c;
   c.x = xs; c.nodecol = ns; c.spl = P.spl; c.dur = P.dur;
-  c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
   c.rb = P.rb; c.fdisc_motion = P.fdisc_motion;
   c.gait = GAIT; c.pinfo = P.pinfo; c.pcols = P.pcols; c.pact = P.pact; c.sched = P.sched; c.eelin = P.eelin; c.lin = P.lin;
   c.rotvec = ROTVEC;
   c.dyn_scratch = nullptr;
   c.cq = P.cq;
-  double f = 0.0;
-  for (int i = threadIdx.x; i < P.n_citems; i += kCostBlock) {
-    const CostItem it = P.citems[i];
-    c.seg = nullptr; c.sg = P.sg; c.row = it.seg;
-    if constexpr (ACC == kAccSlots) {
-      CostSlotEmit em{cs + it.cslot, P.n};
-      eval_cost_item(c, it, em);
-      f += em.f;
-    } else if constexpr (ACC == kAccLimbs) {
-      CostLimbEmit em{acc, P.n_pad, bad};
-      eval_cost_item(c, it, em);
-      f += em.f;
-    } else {
-      CostFEmit em;
-      eval_cost_item(c, it, em);
-      f += em.f;
+  XStage<kCostBlock, false> next;
+  for (; b < P.B; b += G) {   // the same trip count for every thread of the block
+    if constexpr (ACC == kAccLimbs) {
+      for (int i = threadIdx.x; i < 3 * P.n_pad; i += kCostBlock) acc[i] = 0;
+      if (threadIdx.x == 0) *bad = 0;
     }
-  }
-  // SoftConstraint terms (soft_constraint.cc:52-69): 0.5 (g - b)^T (g - b); the gradient J^T (g - b) below
-  const double* sgp = P.sG + (int64_t)b * P.s_ldg;
-  for (int r = threadIdx.x; r < P.s_m; r += kCostBlock) {
-    const double d = sgp[r] - P.s_b[r];
-    f += (0.5 * d) * d;
-  }
-  // f: wave butterfly, then the waves' partials in order
-  for (int o = 32; o > 0; o >>= 1) f += __shfl_xor(f, o, 64);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = f;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double s = 0.0;
-    for (int w = 0; w < kCostBlock / 64; ++w) s += red[w];
-    P.F[b] = s;
-  }
-  if constexpr (ACC != kAccNone) {
-    double* gr = P.GR + (int64_t)b * P.ldgr;
-    const double* sv = P.sV + (int64_t)b * P.s_ldv;
-    const bool nan_all = ACC == kAccLimbs && *bad != 0;
-    for (int j = threadIdx.x; j < P.n; j += kCostBlock) {
-      double s = 0.0;
+    __syncthreads();   // x (and the tables, the cleared limbs) in LDS
+    const int bn = b + G;
+    if (bn < P.B) next.issue(P, P.X + (int64_t)bn * P.ldx);
+    c.ter = P.terrains + (P.terrain_per_problem ? b : 0);
+    double f = 0.0;
+    for (int i = threadIdx.x; i < P.n_citems; i += kCostBlock) {
+      const CostItem it = P.citems[i];
+      c.seg = nullptr; c.sg = P.sg; c.row = it.seg;
       if constexpr (ACC == kAccSlots) {
-        const int k1 = cptr[j + 1];
-        int k = cptr[j];
-        for (; k + 4 <= k1; k += 4) {   // the slot ids of 4 entries in flight together; the sum stays in order
-          const int i0 = cslot[k], i1 = cslot[k + 1], i2 = cslot[k + 2], i3 = cslot[k + 3];
-          const double a0 = cs[i0], a1 = cs[i1], a2 = cs[i2], a3 = cs[i3];
-          s += a0; s += a1; s += a2; s += a3;
-        }
-        for (; k < k1; ++k) s += cs[cslot[k]];
+        CostSlotEmit em{cs, cslot + it.cslot, P.n};
+        eval_cost_item(c, it, em);
+        f += em.f;
+      } else if constexpr (ACC == kAccLimbs) {
+        CostLimbEmit em{acc, P.n_pad, bad};
+        eval_cost_item(c, it, em);
+        f += em.f;
       } else {
-        s = limb_value((long long)acc[j], (long long)acc[P.n_pad + j], (long long)acc[2 * P.n_pad + j]);
-        if (nan_all) s = __builtin_nan("");
+        CostFEmit em;
+        eval_cost_item(c, it, em);
+        f += em.f;
       }
-      if (P.s_m > 0)   // the soft child's column j, its rows in order
-        for (int k = P.s_cptr[j]; k < P.s_cptr[j + 1]; ++k) {
-          const int2 e = P.s_cent[k];   // (CSR index, row)
-          s += sv[e.x] * (sgp[e.y] - P.s_b[e.y]);
-        }
-      __builtin_nontemporal_store(s, gr + j);
     }
+    // SoftConstraint terms (soft_constraint.cc:52-69): 0.5 (g - b)^T (g - b); the gradient J^T (g - b) below
+    const double* sgp = P.sG + (int64_t)b * P.s_ldg;
+    for (int r = threadIdx.x; r < P.s_m; r += kCostBlock) {
+      const double d = sgp[r] - P.s_b[r];
+      f += (0.5 * d) * d;
+    }
+    // f: wave butterfly, then the waves' partials in order
+    for (int o = 32; o > 0; o >>= 1) f += __shfl_xor(f, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = f;
+    __syncthreads();   // partials, and every gradient entry, in LDS
+    if (threadIdx.x == 0) {
+      double sf = 0.0;
+      for (int w = 0; w < kCostBlock / 64; ++w) sf += red[w];
+      P.F[b] = sf;
+    }
+    if constexpr (ACC != kAccNone) {
+      double* gr = P.GR + (int64_t)b * P.ldgr;
+      const double* sv = P.sV + (int64_t)b * P.s_ldv;
+      const bool nan_all = ACC == kAccLimbs && *bad != 0;
+      for (int j = threadIdx.x; j < P.n; j += kCostBlock) {
+        double s = 0.0;
+        if constexpr (ACC == kAccSlots) {
+          // (round 6, ANYmal + every cost kind, B = 4096, one box: 0.1306 ms per batch; slots in item order with the
+          // column reading its slot ids 0.1324; the item's slot ids from global memory instead of LDS 0.1554)
+          const int k1 = cptr[j + 1];
+          int k = cptr[j];
+          for (; k + 4 <= k1; k += 4) {   // 4 loads in flight together; the sum stays in order
+            const double a0 = cs[k], a1 = cs[k + 1], a2 = cs[k + 2], a3 = cs[k + 3];
+            s += a0; s += a1; s += a2; s += a3;
+          }
+          for (; k < k1; ++k) s += cs[k];
+        } else {
+          s = limb_value((long long)acc[j], (long long)acc[P.n_pad + j], (long long)acc[2 * P.n_pad + j]);
+          if (nan_all) s = __builtin_nan("");
+        }
+        if (P.s_m > 0)   // the soft child's column j, its rows in order
+          for (int k = P.s_cptr[j]; k < P.s_cptr[j + 1]; ++k) {
+            const int2 e = P.s_cent[k];   // (CSR index, row)
+            s += sv[e.x] * (sgp[e.y] - P.s_b[e.y]);
+          }
+        __builtin_nontemporal_store(s, gr + j);
+      }
+    }
+    __syncthreads();   // every lane is done with this problem's x, slots and partials
+    if (bn < P.B) next.commit(P, P.X + (int64_t)bn * P.ldx, xs, ns);
   }
 }
 // Trajectory export (SaveTrajectoryToCSV): one 64-lane block per (problem, 64 sample times). Each

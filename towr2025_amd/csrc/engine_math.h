@@ -2311,16 +2311,18 @@ TG_HD void eval_cost_item(const Ctx& c, const CostItem& it, Emit& em) {
 // Gradient emitters of the objective kernel (cost_traj.hip), single-source so that the host emulation
 // (tests/host_emu) runs the kernel's exact accumulation. Both give the same bits on every call.
 // CostSlotEmit (fixed phase durations): an item's present entries (a variable's column: not a constant
-// node value, which is -1 on the host and the zero slot n on the device) go to consecutive slots from
-// CostItem::cslot, in emission order (layout.hip build_cost_slots enumerates the same entries).
+// node value, which is -1 on the host and the zero slot n on the device) go, in emission order, to the
+// slots slot[0], slot[1], ... of its range of Layout::cost_cslot (layout.hip build_cost_slots enumerates the
+// same entries).
 struct CostSlotEmit {
   double* cs;
+  const uint16_t* slot;
   int n;
   double f = 0.0;
   static constexpr bool kSparse = true;
   TG_HD void skip(int) {}
   TG_HD void operator()(int, int col, double v, bool pres) {
-    if (pres && col >= 0 && col < n) *cs++ = v;
+    if (pres && col >= 0 && col < n) cs[*slot++] = v;
   }
 };
 struct CostFEmit {   // f only

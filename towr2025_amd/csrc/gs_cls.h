@@ -179,130 +179,4 @@ TG_HD void tq_record(const Ctx& c, const GsInst& gi, Put&& put, double g[4]) {
   put(kTqND + 8, gs_int(F.poly));
 }
 
-// ------------------------------------------------------------------------------------------------
-// The fused ForceConstraintDiscretized kernel's stages (gstream.hip towr_fdisc_fused_kernel), single-source so that
-// the host emulation (tests/host_emu emu_ff_check) runs exactly them. A view of one (problem, constraint): its blob
-// (layout.h FfGeo), the local x (motion node values, force node values, schedule variables) and the timings.
-// Every quantity is formed by the function the record kernel uses for it (fdisc_instant / fdisc_record), split
-// over kFfLanes lanes per instant (sub).
-// ------------------------------------------------------------------------------------------------
-enum { kXfT = 0, kXfTl, kXfPoly, kXmT, kXmTl, kXmPoly, kXcur, kXws, kXwd, kXFp, kXFv = kXFp + 3, kXMp = kXFv + 3,
-       kXH = kXMp + 2, kXb = kXH + 4, kFfEx = kXb + 16 };   // per-instant exchange slots (doubles) between the stages
-TG_HD int gs_iget(double d) { return (int)__builtin_bit_cast(long long, d); }
-struct FfView {
-  FfGeo g;
-  const int32_t* blob;
-  const double* lx;          // local x: motion node values (node j at 6 j + 3 deriv + dim), force node values, schedule
-  double *pdm, *pem, *pdf, *pef, *phe;   // polynomial durations and running sums (motion, force), phase ends
-  const towr_terrain_t* ter;
-  TG_HD const PolyPhase* pim() const { return reinterpret_cast<const PolyPhase*>(blob + g.o_pinfo); }
-  TG_HD const PolyPhase* pif() const { return pim() + g.np_m; }
-  TG_HD const double* sx() const { return lx + 6 * (g.nm + g.nf); }
-  TG_HD const double* nvm() const { return lx; }
-  TG_HD const double* nvf() const { return lx + 6 * g.nm; }
-  // PhaseDurations (phase_durations.cc:79-100): the last phase is the total minus the others (last_phase_duration)
-  TG_HD double last_phase() const {
-    double sum = 0.0;
-    for (int i = 0; i < g.n_ph - 1; ++i) sum += sx()[i];
-    return g.t_total - sum;
-  }
-  TG_HD double phase_dur(int ph, double last) const { return ph < g.n_ph - 1 ? sx()[ph] : last; }
-};
-// timings, step 1: polynomial duration i of the motion (i < np_m) or force spline (phase_poly_duration)
-TG_HD void ff_pdur(const FfView& v, int i) {
-  const double last = v.last_phase();
-  const bool f = i >= v.g.np_m;
-  const PolyPhase pp = f ? v.pif()[i - v.g.np_m] : v.pim()[i];
-  (f ? v.pdf[i - v.g.np_m] : v.pdm[i]) = v.phase_dur(pp.phase, last) / pp.n_in_phase;
-}
-// timings, step 2 (which 0: motion running sums, 1: force, 2: phase ends), in the reference's order
-TG_HD void ff_sums(const FfView& v, int which) {
-  if (which == 2) {
-    const double last = v.last_phase();
-    double acc = 0.0;
-    for (int ph = 0; ph < v.g.n_ph; ++ph) { acc += v.phase_dur(ph, last); v.phe[ph] = acc; }
-    return;
-  }
-  const double* d = which ? v.pdf : v.pdm;
-  double* out = which ? v.pef : v.pem;
-  const int n = which ? v.g.np_f : v.g.np_m;
-  double acc = 0.0;
-  for (int i0 = 0; i0 < n; i0 += 8) {   // (operands loaded 8 at a time ahead of the dependent additions)
-    double x[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) x[k] = i0 + k < n ? d[i0 + k] : 0.0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (i0 + k < n) { acc += x[k]; out[i0 + k] = acc; }
-  }
-}
-// stage 1 (sub 0: force, 1: motion, 2: phase): the active polynomials and phase at time t
-TG_HD void ff_stage1(const FfView& v, double t, int sub, double* X) {
-  if (sub < 2) {
-    int poly; double tl, T;
-    if (sub == 0) locate_poly(v.pdf, v.pef, v.g.np_f, t, poly, tl, T);
-    else locate_poly(v.pdm, v.pem, v.g.np_m, t, poly, tl, T);
-    const int o = sub == 0 ? kXfT : kXmT;
-    X[o] = T; X[o + 1] = tl; X[o + 2] = gs_int(poly);
-  } else if (sub == 2) {
-    X[kXcur] = gs_int(phase_cur(v.phe, v.g.n_ph, t));
-  }
-}
-// stage 2 (sub 0-2: force dimension, 3-4: motion x / y, 5: the force basis, 6: the window): poly_state_dim, hermite_dpos
-TG_HD void ff_stage2(const FfView& v, int sub, double* X) {
-  if (sub < 5) {
-    const bool f = sub < 3;
-    const int e = f ? sub : sub - 3, o = f ? kXfT : kXmT;
-    const int poly = gs_iget(X[o + 2]);
-    const double* nv = f ? v.nvf() : v.nvm();
-    double pp, vv, aa;
-    poly_state_dim(nv[6 * poly + e], nv[6 * poly + 3 + e], nv[6 * poly + 6 + e], nv[6 * poly + 9 + e], X[o], X[o + 1], pp, vv, aa);
-    if (f) { X[kXFp + e] = pp; X[kXFv + e] = vv; }
-    else X[kXMp + e] = pp;
-  } else if (sub == 5) {
-    double H[4];
-    hermite_dpos(X[kXfT], X[kXfTl], H);
-    for (int q = 0; q < 4; ++q) X[kXH + q] = H[q];
-  } else if (sub == 6) {
-    const int32_t* ws = v.blob + v.g.o_ws + 2 * gs_iget(X[kXfPoly]);
-    X[kXws] = gs_int(ws[0]);
-    X[kXwd] = gs_int(ws[1]);
-  }
-}
-// stage 3 (sub 0-2: d force / d schedule dimension, 3: the pyramid rows, 4-15: window position sub - 4): the record
-// fields (fdisc_record's layout: window sums | b | Jf.dx | Jf.v | ws, wd, cur); the rows b also to the exchange
-TG_HD void ff_stage3(const FfView& v, int sub, double* X, double* R) {
-  const int poly = gs_iget(X[kXfPoly]);
-  if (sub < 3) {
-    const int k = sub;
-    const double* nv = v.nvf();
-    R[kFsDx + k] = sched_dx_dim(nv[6 * poly + k], nv[6 * poly + 3 + k], nv[6 * poly + 6 + k], nv[6 * poly + 9 + k], X[kXfT], X[kXfTl],
-                                X[kXFv + k], v.pif()[poly]);
-    R[kFsV + k] = X[kXFv + k];
-    if (k == 0) { R[kFsND] = X[kXws]; R[kFsND + 1] = X[kXwd]; R[kFsND + 2] = X[kXcur]; }
-  } else if (sub == 3) {
-    double nb[3][3], bb[5][3];
-    ter_nbasis(*v.ter, 0, X[kXMp], X[kXMp + 1], nb[0]);
-    ter_nbasis(*v.ter, 1, X[kXMp], X[kXMp + 1], nb[1]);
-    ter_nbasis(*v.ter, 2, X[kXMp], X[kXMp + 1], nb[2]);
-    pyramid(nb[0], nb[1], nb[2], v.ter->friction_coeff, bb);
-    for (int i = 0; i < 5; ++i)
-      for (int e = 0; e < 3; ++e) { R[kFsB + 3 * i + e] = bb[i][e]; X[kXb + 3 * i + e] = bb[i][e]; }
-  } else if (sub < 4 + kFsWin) {   // emit_dim's basis sum of the template column at window position q (0 past the row)
-    const int q = sub - 4, pos = gs_iget(X[kXws]) + q;
-    const int32_t te = pos < v.g.L ? v.blob[v.g.o_tmpl + pos] : -1;
-    double h0 = X[kXH], h1 = X[kXH + 1], h2 = X[kXH + 2], h3 = X[kXH + 3];
-#if defined(__HIP_DEVICE_COMPILE__)
-    asm volatile("" : "+v"(h0), "+v"(h1), "+v"(h2), "+v"(h3));
-#endif
-    const PhaseCol* pc = reinterpret_cast<const PhaseCol*>(v.blob + v.g.o_pcols);
-    R[q] = te >= 0 ? phase_basis_sum(pc[te & 0xFFFFFF], poly, h0, h1, h2, h3) : 0.0;
-  }
-}
-// g row i of the instant (fdisc_instant: F . b_i)
-TG_HD double ff_g(const double* X, int i) {
-  const double Fp[3] = {X[kXFp], X[kXFp + 1], X[kXFp + 2]}, bi[3] = {X[kXb + 3 * i], X[kXb + 3 * i + 1], X[kXb + 3 * i + 2]};
-  return dot3(Fp, bi);
-}
-
 }  // namespace tg

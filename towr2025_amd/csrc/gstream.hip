@@ -537,7 +537,7 @@ __device__ __forceinline__ void fdisc_compose(const KParams& P, const double* re
   int b = g0;
   // (the compose block forming its instants' records itself from x and the PhaseSpline tables in global
   // memory, instead of reading them: FDISC 0.42 -> 2.7 ms per 1024 problems, the dependent table loads;
-  // forming them from tables staged in LDS is towr_fdisc_fused_kernel)
+  // from tables staged in LDS, a fused kernel of round 5: 0.76 vs 0.63 ms per gait step)
   TG_STAMP(P, 0);
   fetch(b);
   int it = 0;
@@ -559,87 +559,6 @@ __device__ __forceinline__ void fdisc_compose(const KParams& P, const double* re
     b = bn;
     __syncthreads();   // this problem's records and row values read before the next deposit
   }
-  TG_STAMP(P, 4);
-}
-
-// ------------------------------------------------------------------------------------------------
-// The fused ForceConstraintDiscretized kernel (layout.h FfGeo): one block per (problem, FsBlock) forms its instants'
-// records in LDS and streams the block's CSR range, so the FDISC records never go through HBM and no record launch
-// precedes the composition. The block stages its constraint's blob (the two splines' PolyPhases, the force PhaseCols,
-// the template and window table) and gathers the local x (the motion and force splines' node values, the schedule
-// variables), forms the two splines' polynomial durations and running sums and the phase ends (the same operations as
-// phase_timings_block), then kFfLanes lanes per instant evaluate fdisc_record's quantities in four stages with the
-// same functions (locate_poly / phase_cur, poly_state_dim per dimension, hermite_dpos, sched_dx_dim per dimension,
-// ter_nbasis + pyramid, phase_basis_sum per window position, dot3 per g row), so every value is the record kernel's.
-// ------------------------------------------------------------------------------------------------
-constexpr int kFfUnits = 8;      // 16-byte units per lane in flight while streaming
-
-__global__ void __launch_bounds__(kFfBlock) towr_fdisc_fused_kernel(KParams P, FfArgs A) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  constexpr int BLOCK = kFfBlock;
-  const int NFS = A.nfs;
-  const int per = (int)((gridDim.x + 7) / 8);   // XCD-aware: a problem's FsBlocks on one XCD (its x from that L2)
-  const int w = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
-  const int b = w / NFS, jt = w - b * NFS;
-  if (b >= P.B) return;   // (the grid is rounded up to a multiple of 8)
-  const FsBlock fb = P.fsb[jt];
-  char* base = reinterpret_cast<char*>(smem);
-  FfView v;
-  v.g = A.geo[fb.ff];
-  int32_t* blob = reinterpret_cast<int32_t*>(base);
-  double* lx = reinterpret_cast<double*>(base + A.o_lx);
-  v.blob = blob;
-  v.lx = lx;
-  v.pdm = reinterpret_cast<double*>(base + A.o_tm);
-  v.pem = v.pdm + A.np_max;
-  v.pdf = v.pem + A.np_max;
-  v.pef = v.pdf + A.np_max;
-  v.phe = v.pef + A.np_max;
-  towr_terrain_t* ter = reinterpret_cast<towr_terrain_t*>(base + A.o_ter);
-  v.ter = ter;
-  double* ex = reinterpret_cast<double*>(base + A.o_ex);
-  double* cd = reinterpret_cast<double*>(base + A.o_cd);
-  double* rowv = reinterpret_cast<double*>(base + A.o_rowv);
-  int32_t* wsr = reinterpret_cast<int32_t*>(base + A.o_wsr);
-  const int tid = threadIdx.x, kk = tid / kFfLanes, sub = tid - kk * kFfLanes;
-  const bool inst = kk < fb.n_inst;
-  const double t = inst ? P.fs_t[fb.t0 + kk] : 0.0;
-  TG_STAMP(P, 0);
-  // stage the blob and the terrain, then gather the local x
-  stage16<BLOCK>(reinterpret_cast<uint4*>(blob), A.blob + v.g.blob0, v.g.blob_n16);
-  if (tid < (int)(sizeof(towr_terrain_t) / 8))
-    reinterpret_cast<double*>(ter)[tid] = reinterpret_cast<const double*>(P.terrains + (P.terrain_per_problem ? b : 0))[tid];
-  __syncthreads();
-  {
-    const double* xg = P.X + (int64_t)b * P.ldx;
-    const int32_t* gat = blob + v.g.o_gather;
-    for (int j = tid; j < v.g.nx; j += BLOCK) {
-      const int col = gat[j];
-      lx[j] = col >= 0 ? xg[col] : 0.0;
-    }
-  }
-  __syncthreads();
-  TG_STAMP(P, 1);
-  // the two splines' polynomial durations, their running sums and the phase ends (phase_timings_block's operations)
-  if (tid < v.g.np_m + v.g.np_f) ff_pdur(v, tid);
-  __syncthreads();
-  if ((tid & 63) == 0 && tid < 192) ff_sums(v, tid >> 6);   // one wave each
-  __syncthreads();
-  TG_STAMP(P, 2);
-  double* X = ex + kk * kFfEx;
-  double* R = cd + kk * kFsCS;
-  if (inst && sub < 3) ff_stage1(v, t, sub, X);
-  __syncthreads();
-  if (inst && sub < 7) ff_stage2(v, sub, X);
-  __syncthreads();
-  if (inst) ff_stage3(v, sub, X, R);
-  __syncthreads();
-  if (inst && sub < 5 && P.want_g) __builtin_nontemporal_store(ff_g(X, sub), P.G + (int64_t)b * P.ldg + fb.r0 + 5 * kk + sub);
-  TG_STAMP(P, 3);
-  if (!P.want_jac) return;
-  fs_rows<BLOCK>(fb, cd, rowv, wsr);
-  __syncthreads();
-  fs_stream<BLOCK, kFfUnits>(P, fb, b, cd, rowv, wsr);
   TG_STAMP(P, 4);
 }
 
@@ -843,26 +762,6 @@ const void* gait_compose_kernel(int mask) {
     case 23: return compose_fn<23>();
     default: return compose_fn<31>();
   }
-}
-const void* fdisc_fused_kernel() { return reinterpret_cast<const void*>(&towr_fdisc_fused_kernel); }
-// the fused kernel's LDS layout (bytes): [blob | local x | timings | exchange | records | row windows | window starts |
-// terrain]; offsets into A, returns the total
-size_t ff_lds(const Layout& L, FfArgs* A) {
-  auto a16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
-  size_t o = a16(16 * (size_t)L.ff_blob_max16);
-  const size_t o_lx = o; o = a16(o + 8 * (size_t)(L.ff_nx_max + 1));
-  const size_t o_tm = o; o = a16(o + 8 * (size_t)(4 * L.ff_np_max + L.ff_ph_max));
-  const size_t o_ex = o; o = a16(o + 8 * (size_t)kFsInst * kFfEx);
-  const size_t o_cd = o; o = a16(o + 8 * (size_t)kFsInst * kFsCS);
-  const size_t o_rowv = o; o = a16(o + 8 * (size_t)5 * kFsInst * kFsWin);
-  const size_t o_wsr = o; o = a16(o + 4 * (size_t)5 * kFsInst);
-  const size_t o_ter = o; o = a16(o + sizeof(towr_terrain_t));
-  if (A) {
-    A->np_max = L.ff_np_max; A->ph_max = L.ff_ph_max;
-    A->o_lx = (int32_t)o_lx; A->o_tm = (int32_t)o_tm; A->o_ex = (int32_t)o_ex; A->o_cd = (int32_t)o_cd;
-    A->o_rowv = (int32_t)o_rowv; A->o_wsr = (int32_t)o_wsr; A->o_ter = (int32_t)o_ter;
-  }
-  return o;
 }
 size_t fs_compose_lds(const Layout& L) {   // records, row window values, row window starts
   return sizeof(double) * ((size_t)(((kFsInst * kFsCS + 1) & ~1) + 5 * kFsInst * kFsWin + (5 * kFsInst + 1) / 2 + 1) & ~(size_t)1);

@@ -81,7 +81,7 @@ struct KParams {
   const CostItem* citems;         // cost launch: work items, objective and gradient outputs
   const double* cq;               // cost launch: CT_ENERGYQ Gram matrices
   int32_t n_citems, lds_red_off;
-  const int32_t* c_cptr;          // cost launch, slot gradient (Layout::cost_cptr / cost_cslot, padded to 16 bytes)
+  const uint16_t* c_cptr;         // cost launch, slot gradient (Layout::cost_cptr / cost_cslot, padded to 16 bytes)
   const uint16_t* c_cslot;
   int32_t c_nslot;
   double* F;
@@ -431,7 +431,13 @@ const void* cost_kernel_for(bool gait, int acc, bool rotvec);   // acc: 0 f only
 const void* traj_kernel_for(bool gait);
 const void* rv_coef_kernel();
 constexpr int kRvCoefBlock = 256;   // the RotVec coefficient pre-pass: 4 waves, one component each
-constexpr int kCostBlock = 256;   // objective kernel: one block per problem
+// objective kernel: persistent blocks, one problem at a time per block. 512 threads: one block per CU (8 waves, the
+// 2 per SIMD its registers allow) with the CU's whole LDS for the slot gradient (ANYmal + every cost kind: 84 kB, more
+// than half a CU's 160 kB, so 256-thread blocks ran one per CU: 0.207 ms per 4096 problems)
+#ifndef TOWR_COST_BLOCK   // (experiment builds: -DTOWR_COST_BLOCK=256)
+#define TOWR_COST_BLOCK 256
+#endif
+constexpr int kCostBlock = TOWR_COST_BLOCK;
 constexpr int kTrajBlock = 64;    // trajectory kernel: one block per (problem, 64 sample times)
 
 // The heavy kinds read spline nodes through the segment records; with phase-duration optimisation

@@ -62,28 +62,8 @@ constexpr int kFsRS = kFsND + 3, kFsCS = kFsRS | 1;   // record fields; LDS stri
 struct FsBlock {
   int32_t ee, n_inst, t0, r0;   // endeffector, instants, first instant's time index (fs_t), first row
   int32_t v0, nv, L, tmpl;      // CSR range [v0, v0 + nv), row length, template offset (fs_tmpl)
-  int32_t js0, ns1, wsoff, ff;  // ff: the constraint's FfGeo (the fused kernel)
+  int32_t js0, ns1, wsoff, pad;
 };
-// The fused ForceConstraintDiscretized kernel (gstream.hip towr_fdisc_fused_kernel): one block per (problem, FsBlock)
-// forms its instants' records in LDS, kFfLanes lanes per instant, and streams the block's CSR range; no record
-// scratch in HBM, no separate record launch. What its instants read is one blob per constraint, rebased to it
-// (Layout::ff_blob, int32 words, sections 16-byte aligned):
-//   pinfo   PolyPhase of the motion spline's then the force spline's polynomials;
-//   pcols   the force spline's PhaseCols, dimensions consecutive (local index = global - SplineMeta::pcol_off[0]);
-//   gather  the local x: per node of the motion then the force spline its 6 values (deriv, dim), then the
-//           endeffector's schedule variables; the global column (-1: a constant 0.0 node value);
-//   tmpl    the constraint's template (FsBlock::tmpl) with PhaseCol indices rebased to pcols;
-//   ws      window start and dimension codes of each force polynomial (fs_ws at FsBlock::wsoff).
-struct FfGeo {
-  int32_t blob0, blob_n16;      // the blob in Layout::ff_blob (16-byte units)
-  int32_t nm, nf;               // nodes of the motion / force spline
-  int32_t np_m, np_f;           // their polynomials (PolyPhase entries)
-  int32_t n_ph, nx;             // phases of the endeffector; local x values (6 nm + 6 nf + n_ph - 1)
-  int32_t o_pinfo, o_pcols, o_gather, o_tmpl, o_ws, L;   // word offsets of the sections; template length
-  double t_total;               // the endeffector's total duration (SchedInfo::t_total)
-};
-constexpr int kFfLanes = 16;     // lanes per instant of the fused kernel's record stages
-constexpr int kFfBlock = kFfLanes * kFsInst;
 static_assert(sizeof(FsBlock) % 4 == 0, "FsBlock is staged to LDS as int32 words");
 
 // Streaming RangeOfMotion and Dynamic under phase-duration optimisation (gstream.hip), the FsBlock
@@ -268,9 +248,6 @@ struct Layout {
   std::vector<int32_t> fs_ws;        // per (constraint, force polynomial): window start, window dimension codes
   std::vector<int32_t> fs_iee, fs_irow, fs_iblk;   // per instant (fs_t order): endeffector, first row, FsBlock
   int32_t fs_tmpl_max = 0;
-  std::vector<FfGeo> ff_geo;         // the fused kernel (FfGeo): per constraint, and the blobs
-  std::vector<uint4> ff_blob;
-  int32_t ff_blob_max16 = 0, ff_nx_max = 0, ff_np_max = 0, ff_ph_max = 0;
   // streaming RangeOfMotion / Dynamic (GsGeo): per class enabled when every constraint of the class fits
   bool gstream[GS_COUNT] = {};
   std::vector<GsGeo> gs_geo;
@@ -296,12 +273,12 @@ struct Layout {
   std::vector<double> cost_q;        // CT_ENERGYQ Gram matrices, 16 doubles per item (CostItem::q)
   int32_t cost_type0[CT_COUNT + 1] = {};
   // Deterministic gradient (fixed phase durations): every present gradient entry of every cost item has an
-  // LDS contribution slot (layout.hip build_cost_slots): entry k of item i goes to slot CostItem::cslot + k,
-  // and column j sums its slots cost_cslot[cost_cptr[j] .. cost_cptr[j + 1]) in that order.
-  // cost_nslot (slots incl. padding) = 0: fixed-point limbs instead (phase-duration optimisation, where the
-  // PhaseSpline windows move with x, or more slots than kCostSlotMax).
+  // LDS contribution slot, ordered by column (layout.hip build_cost_slots): entry k of item i goes to slot
+  // cost_cslot[CostItem::cslot + k], and column j sums slots [cost_cptr[j], cost_cptr[j + 1]) in order.
+  // cost_nslot = 0: fixed-point limbs instead (phase-duration optimisation, where the PhaseSpline windows
+  // move with x, or more slots than kCostSlotMax).
   int32_t cost_nslot = 0;
-  std::vector<int32_t> cost_cptr;
+  std::vector<uint16_t> cost_cptr;
   std::vector<uint16_t> cost_cslot;
   // SoftConstraint terms (TOWR_COST_SOFT), in cost order: the cost index and the wrapped constraint.
   // The wrapped sets are evaluated by a second layout (the handle's soft child) whose constraint
@@ -309,7 +286,10 @@ struct Layout {
   std::vector<std::pair<int32_t, int32_t>> soft;
 };
 
-constexpr int kCostSlotMax = 8192;   // contribution slots of the cost kernel's LDS (64 KB)
+#ifndef TOWR_COST_SLOT_MAX   // (experiment builds: -DTOWR_COST_SLOT_MAX=0, the limbs everywhere)
+#define TOWR_COST_SLOT_MAX 8192
+#endif
+constexpr int kCostSlotMax = TOWR_COST_SLOT_MAX;   // contribution slots of the cost kernel's LDS (64 KB)
 constexpr int kMiscWaves = 4;   // one-wave small-kind tiles per group (block)
 constexpr int kSlotSpare = 4;   // spare slot groups per lane: the kernels prefetch up to this many ahead
 constexpr bool is_misc_kind(int t) { return t != IT_DYN && t != IT_ROM && t != IT_FDISC && t != IT_TQDISC; }
@@ -394,16 +374,6 @@ struct RecArgs {
   int32_t fs_lds, fs_nb, fs_nws, fs_ntm;
 };
 size_t gs_dyn_state_bytes(bool rotvec);   // the record kernel's per-Dynamic-instant LDS state
-// the fused FDISC kernel's arguments (gstream.hip towr_fdisc_fused_kernel, layout.h FfGeo)
-struct FfArgs {
-  const FfGeo* geo;
-  const uint4* blob;
-  int32_t nfs;                                   // FsBlocks per problem
-  int32_t np_max, ph_max;                        // the largest spline (polynomials) and phase count of any constraint
-  int32_t o_lx, o_tm, o_ex, o_cd, o_rowv, o_wsr, o_ter;   // LDS byte offsets (ff_lds)
-};
-const void* fdisc_fused_kernel();
-size_t ff_lds(const Layout& L, FfArgs* A);   // the fused kernel's LDS bytes (and the offsets into A)
 constexpr int kGsRecMaxBlock = 512;
 constexpr int kFsRecBlock = 512;   // the record launch's threads when it holds FDISC records
 // The frozen-pattern check (WatchItem): reference Jacobian entries at x outside the x0 pattern, evaluated

@@ -457,11 +457,10 @@ Ctx host_ctx(const Layout& L, const double* x, const towr_terrain_t& ter) {
 }
 // Deterministic gradient slots (Layout::cost_nslot): with fixed phase durations every cost item's gradient
 // entries go to columns that do not depend on x, so the host enumerates them once. An entry is present when
-// its column is a variable (a constant node value has none). Item i writes its k-th present entry to slot
-// CostItem::cslot + k (plain LDS stores, no address load; an item's range is padded to an odd length, so the
-// lanes of a wave running items of one kind store to distinct LDS banks). Column j's slots, ascending, are
-// cost_cslot[cost_cptr[j] .. cost_cptr[j + 1]), and one lane sums them in that order. No atomics: the same
-// bits on every call.
+// its column is a variable (a constant node value has none). The slots are ordered by column, and within a
+// column by item and emission order: entry k of item i (its k-th present entry) goes to slot
+// cost_cslot[CostItem::cslot + k], column j owns slots [cost_cptr[j], cost_cptr[j + 1]), and one lane sums
+// them in that order. No atomics: the same bits on every call.
 namespace {
 struct CostSlotPass {
   std::vector<int32_t>* cols;
@@ -481,19 +480,18 @@ void build_cost_slots(Layout& L) {
     CostSlotPass em{&cols};
     eval_cost_item(cx, it, em);
     it.cslot = (int32_t)c0; it.cn = (int32_t)(cols.size() - c0);
-    if (!(it.cn & 1)) cols.push_back(-1);   // odd stride between the slot ranges of like items
   }
   if (cols.empty() || cols.size() > (size_t)kCostSlotMax) {   // too many for the LDS budget: limbs
     for (CostItem& it : L.cost_items) it.cslot = it.cn = 0;
     return;
   }
-  L.cost_cptr.assign(L.n + 1, 0);
-  for (int32_t c : cols) if (c >= 0) ++L.cost_cptr[c + 1];
-  for (int j = 0; j < L.n; ++j) L.cost_cptr[j + 1] += L.cost_cptr[j];
-  L.cost_cslot.resize(L.cost_cptr[L.n]);
-  std::vector<int32_t> fill(L.cost_cptr.begin(), L.cost_cptr.end() - 1);
-  for (size_t k = 0; k < cols.size(); ++k)
-    if (cols[k] >= 0) L.cost_cslot[fill[cols[k]]++] = (uint16_t)k;   // ascending per column
+  std::vector<int32_t> cptr(L.n + 1, 0);
+  for (int32_t c : cols) ++cptr[c + 1];
+  for (int j = 0; j < L.n; ++j) cptr[j + 1] += cptr[j];
+  L.cost_cptr.assign(cptr.begin(), cptr.end());   // (below 2^16: kCostSlotMax)
+  L.cost_cslot.resize(cols.size());
+  std::vector<int32_t> fill(cptr.begin(), cptr.end() - 1);
+  for (size_t k = 0; k < cols.size(); ++k) L.cost_cslot[k] = (uint16_t)fill[cols[k]]++;   // ascending per column
   L.cost_nslot = (int32_t)cols.size();
 }
 
@@ -535,66 +533,6 @@ int64_t pattern_outside_host(const Layout& L, const double* x, const towr_terrai
 // in chunks of <= kFsInst, provided every row of the constraint holds the same column list, each column
 // is a force-set PhaseSpline column or a schedule column of the constraint's endeffector, and each force
 // polynomial's columns fit a kFsWin window of the row. Otherwise the tile path stays.
-// The fused FDISC kernel's per-constraint blobs (layout.h FfGeo), one per template (the FsBlocks of a constraint
-// share it). A constraint the blob cannot express (the motion or force spline not a PhaseSpline of the endeffector,
-// the force spline's PhaseCols not consecutive over the dimensions) leaves the fused kernel off (ff_geo empty).
-void build_ffused(Layout& L) {
-  L.ff_geo.clear(); L.ff_blob.clear();
-  L.ff_blob_max16 = L.ff_nx_max = L.ff_np_max = L.ff_ph_max = 0;
-  std::map<int32_t, int32_t> by_tmpl;
-  auto off = [&]() { L.ff_geo.clear(); L.ff_blob.clear(); };
-  for (FsBlock& fb : L.fs_blocks) {
-    const auto it = by_tmpl.find(fb.tmpl);
-    if (it != by_tmpl.end()) { fb.ff = it->second; continue; }
-    const int ee = fb.ee;
-    const SplineMeta& mm = L.spl[sp_motion(ee)];
-    const SplineMeta& mf = L.spl[sp_force(ee)];
-    const SchedInfo& si = L.sched[ee];
-    if (mm.ee != ee || mf.ee != ee || si.col0 < 0) { off(); return; }
-    FfGeo g{};
-    g.nm = mm.n_polys + 1; g.nf = mf.n_polys + 1;
-    g.np_m = mm.n_polys; g.np_f = mf.n_polys;
-    g.n_ph = si.n_phases; g.nx = 6 * (g.nm + g.nf) + si.n_phases - 1;
-    g.L = fb.L; g.t_total = si.t_total;
-    std::vector<int32_t> w;   // the blob, int32 words
-    auto align4 = [&]() { while (w.size() % 4) w.push_back(0); };
-    auto push = [&](const void* p, size_t bytes) { const size_t n0 = w.size(); w.resize(n0 + bytes / 4); std::memcpy(w.data() + n0, p, bytes); };
-    g.o_pinfo = (int32_t)w.size();
-    push(L.pinfo.data() + mm.pinfo_off, sizeof(PolyPhase) * mm.n_polys);
-    push(L.pinfo.data() + mf.pinfo_off, sizeof(PolyPhase) * mf.n_polys);
-    align4();
-    g.o_pcols = (int32_t)w.size();
-    const int pc0 = mf.pcol_off[0];
-    if (mf.pcol_off[1] != pc0 + mf.pcol_n[0] || mf.pcol_off[2] != mf.pcol_off[1] + mf.pcol_n[1]) { off(); return; }
-    push(L.pcols.data() + pc0, sizeof(PhaseCol) * (mf.pcol_n[0] + mf.pcol_n[1] + mf.pcol_n[2]));
-    align4();
-    g.o_gather = (int32_t)w.size();
-    push(L.nodecol.data() + (size_t)mm.node_off * 6, sizeof(int32_t) * 6 * g.nm);
-    push(L.nodecol.data() + (size_t)mf.node_off * 6, sizeof(int32_t) * 6 * g.nf);
-    for (int ph = 0; ph < si.n_phases - 1; ++ph) w.push_back(si.col0 + ph);
-    align4();
-    g.o_tmpl = (int32_t)w.size();
-    for (int j = 0; j < fb.L; ++j) {
-      const int32_t te = L.fs_tmpl[(size_t)fb.tmpl + j];
-      w.push_back(te < 0 ? te : (((te & 0xFFFFFF) - pc0) | (te & ~0xFFFFFF)));
-    }
-    align4();
-    g.o_ws = (int32_t)w.size();
-    push(L.fs_ws.data() + 2 * (size_t)fb.wsoff, sizeof(int32_t) * 2 * mf.n_polys);
-    align4();
-    g.blob0 = (int32_t)L.ff_blob.size();
-    g.blob_n16 = (int32_t)(w.size() / 4);
-    for (size_t q = 0; q < w.size(); q += 4) L.ff_blob.push_back(uint4{(uint32_t)w[q], (uint32_t)w[q + 1], (uint32_t)w[q + 2], (uint32_t)w[q + 3]});
-    L.ff_blob_max16 = std::max(L.ff_blob_max16, g.blob_n16);
-    L.ff_nx_max = std::max(L.ff_nx_max, g.nx);
-    L.ff_np_max = std::max({L.ff_np_max, g.np_m, g.np_f});
-    L.ff_ph_max = std::max(L.ff_ph_max, g.n_ph);
-    fb.ff = (int32_t)L.ff_geo.size();
-    by_tmpl[fb.tmpl] = fb.ff;
-    L.ff_geo.push_back(g);
-  }
-}
-
 int build_fstream(Layout& L, std::string& err) {
   L.fstream = false;
   L.fs_blocks.clear(); L.fs_t.clear(); L.fs_tmpl.clear(); L.fs_ws.clear(); L.fs_iee.clear(); L.fs_irow.clear(); L.fs_iblk.clear(); L.fs_tmpl_max = 0;
@@ -689,7 +627,6 @@ int build_fstream(Layout& L, std::string& err) {
   L.fs_iblk.assign(L.fs_t.size(), 0);
   for (size_t q = 0; q < L.fs_blocks.size(); ++q)
     for (int k = 0; k < L.fs_blocks[q].n_inst; ++k) L.fs_iblk[(size_t)L.fs_blocks[q].t0 + k] = (int32_t)q;
-  build_ffused(L);
   return TOWR_OK;
 }
 

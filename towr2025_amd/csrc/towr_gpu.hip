@@ -66,9 +66,6 @@ struct towr_gpu_handle_s {
   CostItem* d_citems = nullptr;
   double* d_cq = nullptr;
   FsBlock* d_fsb = nullptr;    // streaming ForceConstraintDiscretized tables (layout.h FsBlock)
-  FfGeo* d_ff_geo = nullptr;   // the fused FDISC kernel's per-constraint tables (layout.h FfGeo)
-  uint4* d_ff_blob = nullptr;
-  bool ff = false;             // the big-batch FDISC chain is the fused kernel (TOWR_GPU_FDISC_FUSED=0: records + compose)
   double* d_fs_t = nullptr;
   int32_t* d_fs_tmpl = nullptr;
   int32_t* d_fs_ws = nullptr;
@@ -150,8 +147,9 @@ struct towr_gpu_handle_s {
   double* d_soft_b = nullptr;
   int32_t* d_soft_cptr = nullptr;   // the soft pattern by column (KParams::s_cptr / s_cent)
   int2* d_soft_cent = nullptr;
-  int32_t* d_c_cptr = nullptr;      // the cost gradient's slot lists (Layout::cost_cptr / cost_cslot)
+  uint16_t* d_c_cptr = nullptr;     // the cost gradient's slot lists (Layout::cost_cptr / cost_cslot)
   uint16_t* d_c_cslot = nullptr;
+  int cost_grid[3] = {1, 1, 1};     // the cost kernel's persistent grid per accumulation (launch_cost)
   double *d_sg = nullptr, *d_sv = nullptr;
   int64_t soft_cap_g = 0, soft_cap_v = 0;   // problems the scratch holds
 };
@@ -576,6 +574,11 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
   // behind FDISC in one chain)
   const bool tq3 = split && tq && fs && h->n_side > 1;
   const hipStream_t tst = tq3 ? h->side[1] : fst;
+  // (round 6, ANYmal gait, B = 1024, one box, 3 runs each: a second side stream for the non-Torque gait, carrying the
+  // small kinds beside the records, or the RangeOfMotion composer beside the Dynamic composer, or the RangeOfMotion /
+  // Dynamic records at the greatest priority: 0.590-0.613 ms per step, all within the product's 0.589-0.606. The kernel
+  // trace shows why: the RangeOfMotion / Dynamic records finish at 144 us in one step and at 413 us in the next, behind
+  // the FDISC composer's blocks, and the composers that follow are bandwidth-bound together whichever way they overlap.)
   if (split) {
     HIPCHK(h, hipEventRecord(h->fork, st));
     HIPCHK(h, hipStreamWaitEvent(fst, h->fork, 0));
@@ -650,30 +653,13 @@ int launch_stream_path(towr_gpu_handle h, KParams P, uint32_t mask, hipStream_t 
     return TOWR_OK;
   };
   const int fpart = fs ? kRecFdisc : 0;
-  // the fused FDISC kernel (h->ff): records formed in LDS by the blocks that compose them
-  auto fused = [&](hipStream_t s) -> int {
-    FfArgs A{};
-    const size_t lds = ff_lds(L, &A);
-    A.geo = h->d_ff_geo; A.blob = h->d_ff_blob; A.nfs = (int32_t)L.fs_blocks.size();
-    const int64_t grid = ((int64_t)P.B * A.nfs + 7) / 8 * 8;   // whole rounds of 8 (XCD-aware mapping)
-    if (grid > INT32_MAX) return fail(h, TOWR_ERR_INVALID, "batch too large");
-    void* a[] = {&P, &A};
-    HIPCHK(h, launch_kernel(fdisc_fused_kernel(), dim3((unsigned)grid), dim3(kFfBlock), a, lds, s));
-    return TOWR_OK;
-  };
   if (big) {   // (without a side stream the two chains run one after the other on the caller's stream)
     if (tq3) {
       if (int rc = records({kRecTq}, tst)) return rc;
       if (int rc = compose(false, true, false, false, false, tst)) return rc;
     }
     const bool tqf = tq && !tq3;   // TQDISC in the FDISC chain
-    if (fs && h->ff) {
-      if (int rc = fused(fst)) return rc;
-      if (tqf) {
-        if (int rc = records({kRecTq}, fst)) return rc;
-        if (int rc = compose(false, true, false, false, false, fst)) return rc;
-      }
-    } else if (fs || tqf) {
+    if (fs || tqf) {
       // (the FDISC records in two blocks per problem, each half the instants: 0.638 vs 0.629 ms, not kept)
       if (int rc = records({fpart, tqf ? kRecTq : 0}, fst)) return rc;
       if (int rc = compose(fs, tqf, false, false, false, fst)) return rc;
@@ -754,25 +740,12 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
     for (int i = 0; i < nside; ++i) HIPCHK(h, hipStreamWaitEvent(h->side[i], h->fork, 0));
   }
   bool stream_done = false, stream_forked = false, misc_done = false;
-  for (int q = 0; q < nk; ++q) {
-    const int lc = order[q];
-    if (lc == LC_MISC && misc_done) continue;   // in the streaming path's composer launch
-    const int nt = class_units(L, lc);
-    const hipStream_t st = stream_forked ? s
-                         : overlap ? ((rv_side && lc != LC_DYN && lc != LC_MISC) ? s : h->side[q % nside])
-                         : (nside > 0 && q % (nside + 1) != 0) ? h->side[q % (nside + 1) - 1] : s;
+  // one launch of a class that is not streamed (a tile class or the small kinds) on stream st
+  auto launch_one = [&](int lc, hipStream_t st) -> int {
     KParams P{};
     fill_common(h, P, B, X, ldx, G, ldg, V, ldv, want_g, want_jac, terrains, per_problem);
+    const int nt = class_units(L, lc);
     P.ntiles = nt;
-    if (streamed_class(L, lc)) {   // every streamed class at the first one: its records and one composer launch
-      if (stream_done) continue;
-      stream_done = true;
-      uint32_t mask = 0;
-      for (int k = 0; k < nk; ++k)
-        if (streamed_class(L, order[k]) || order[k] == LC_MISC) mask |= 1u << order[k];   // (the small kinds are last)
-      if (int rc = launch_stream_path(h, P, mask, s, &stream_forked, &misc_done)) return rc;
-      continue;
-    }
     if (lc == LC_MISC) {
       P.tile0 = 0;
       P.misc_tiles = h->d_misc; P.misc_lds = h->d_misc_lds; P.misc_wave = h->d_misc_wave; P.misc_items = h->d_misc_items;
@@ -796,6 +769,27 @@ int launch_classes(towr_gpu_handle h, int B, const double* X, int64_t ldx, doubl
     void* args[] = {&P};
     HIPCHK(h, launch_kernel(kernel_for_class(lc, L.gait, L.rotvec), dim3((unsigned)grid), dim3((unsigned)block), args,
                               lds_bytes(L, lc), st));
+    return TOWR_OK;
+  };
+  for (int q = 0; q < nk; ++q) {
+    const int lc = order[q];
+    if (lc == LC_MISC && misc_done) continue;   // in the streaming path's composer launch
+    const hipStream_t st = stream_forked ? s
+                         : overlap ? ((rv_side && lc != LC_DYN && lc != LC_MISC) ? s : h->side[q % nside])
+                         : (nside > 0 && q % (nside + 1) != 0) ? h->side[q % (nside + 1) - 1] : s;
+    if (streamed_class(L, lc)) {   // every streamed class at the first one: its records and one composer launch
+      if (stream_done) continue;
+      stream_done = true;
+      uint32_t mask = 0;
+      for (int k = 0; k < nk; ++k)
+        if (streamed_class(L, order[k]) || order[k] == LC_MISC) mask |= 1u << order[k];   // (the small kinds are last)
+      KParams P{};
+      fill_common(h, P, B, X, ldx, G, ldg, V, ldv, want_g, want_jac, terrains, per_problem);
+      P.ntiles = class_units(L, lc);
+      if (int rc = launch_stream_path(h, P, mask, s, &stream_forked, &misc_done)) return rc;
+      continue;
+    }
+    if (int rc = launch_one(lc, st)) return rc;
   }
   for (int i = 0; i < (stream_forked ? std::min(h->n_side, 2) : nside); ++i) {
     HIPCHK(h, hipEventRecord(h->join[i], h->side[i]));
@@ -813,7 +807,7 @@ size_t cost_x_off(const Layout& L, int acc) {
   return acc == 1 ? (size_t)((L.cost_nslot + 1) & ~1) : acc == 2 ? 3 * n_pad : 0;
 }
 size_t cost_red_off(const Layout& L, int acc) {   // ... after x and the node table: acc 1's slot tables (16-byte units)
-  const size_t tabs = acc == 1 ? 2 * ((size_t)(L.cost_nslot + 7) / 8 + (size_t)(L.n + 4) / 4) : 0;
+  const size_t tabs = acc == 1 ? 2 * ((size_t)(L.cost_nslot + 7) / 8 + (size_t)(L.n + 8) / 8) : 0;
   return cost_x_off(L, acc) + (size_t)((L.n + 2) & ~1) + (L.nodecol.size() + 3) / 4 * 2 + tabs;
 }
 size_t cost_lds_bytes(const Layout& L, int acc) { return sizeof(double) * (cost_red_off(L, acc) + kCostBlock / 64 + 2); }
@@ -861,8 +855,8 @@ int launch_cost(towr_gpu_handle h, int B, const double* X, int64_t ldx, double* 
   P.c_cptr = h->d_c_cptr; P.c_cslot = h->d_c_cslot; P.c_nslot = L.cost_nslot;
   P.F = F; P.GR = GR; P.ldgr = ldgr;
   void* args[] = {&P};
-  HIPCHK(h, launch_kernel(cost_kernel_for(L.gait, acc, L.rotvec), dim3((unsigned)B), dim3(kCostBlock), args,
-                            cost_lds_bytes(L, acc), s));
+  HIPCHK(h, launch_kernel(cost_kernel_for(L.gait, acc, L.rotvec), dim3((unsigned)std::min(B, h->cost_grid[acc])),
+                            dim3(kCostBlock), args, cost_lds_bytes(L, acc), s));
   return h->soft ? scratch_release(h, s) : TOWR_OK;
 }
 
@@ -1253,10 +1247,9 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
       (r = upload(h, &h->d_misc, L.misc_tiles)) || (r = upload(h, &h->d_misc_lds, L.misc_lds)) || (r = upload(h, &h->d_xspan, L.misc_xspan)) || (r = upload(h, &h->d_eelin, L.eelin)) ||
       (r = upload(h, &h->d_lin, L.lin)) ||
       (r = upload(h, &h->d_citems, L.cost_items)) || (r = upload(h, &h->d_cq, L.cost_q)) ||
-      (r = upload(h, &h->d_c_cptr, padded(L.cost_cptr, 4))) || (r = upload(h, &h->d_c_cslot, cost_slot_table(L))) || (r = upload(h, &h->d_gtab, gait_blob(L))) ||
+      (r = upload(h, &h->d_c_cptr, padded(L.cost_cptr, 8))) || (r = upload(h, &h->d_c_cslot, cost_slot_table(L))) || (r = upload(h, &h->d_gtab, gait_blob(L))) ||
       (r = upload(h, &h->d_idir, L.idirect)) || (r = upload(h, &h->d_fsb, L.fs_blocks)) || (r = upload(h, &h->d_fs_t, L.fs_t)) ||
       (r = upload(h, &h->d_fs_tmpl, L.fs_tmpl)) || (r = upload(h, &h->d_fs_ws, L.fs_ws)) ||
-      (r = upload(h, &h->d_ff_geo, L.ff_geo)) || (r = upload(h, &h->d_ff_blob, L.ff_blob)) ||
       (r = upload(h, &h->d_fs_iee, L.fs_iee)) || (r = upload(h, &h->d_fs_irow, L.fs_irow)) || (r = upload(h, &h->d_fs_iblk, L.fs_iblk)) ||
       (r = upload(h, &h->d_gs_geo, L.gs_geo)) || (r = upload(h, &h->d_gs_tmpl, L.gs_tmpl)) || (r = upload(h, &h->d_gs_pcode, L.gs_pcode)) ||
       (r = upload(h, &h->d_gs_blk[GS_ROM], L.gs_blocks[GS_ROM])) || (r = upload(h, &h->d_gs_blk[GS_DYN], L.gs_blocks[GS_DYN])) ||
@@ -1325,11 +1318,12 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
     // streaming path) one or two side streams: the write-bound compose launches run beside the latency-bound
     // record work (launch_stream_path).
     const bool streamed = h->L.gait && (h->L.fstream || h->L.gstream[GS_TQ]);
-    const char* rvo = std::getenv("TOWR_GPU_ROTVEC_OVERLAP");
-    h->rv_overlap = h->L.rotvec && !(rvo && std::strcmp(rvo, "0") == 0);
+    h->rv_overlap = h->L.rotvec;
     const int want = ns ? std::atoi(ns) - 1 : streamed ? (h->L.gstream[GS_TQ] ? 2 : 1) : (h->n_fuse > 0 || h->rv_overlap) ? 1 : 0;
     h->n_side = std::max(0, std::min(towr_gpu_handle_s::kMaxSide, want));
-    if (h->n_side > 0 && hipEventCreateWithFlags(&h->fork, hipEventDisableTiming) != hipSuccess) { h->err = "hipEventCreate failed"; return bail(TOWR_ERR_HIP); }
+    if (h->n_side > 0 && hipEventCreateWithFlags(&h->fork, hipEventDisableTiming) != hipSuccess) {
+      h->err = "hipEventCreate failed"; return bail(TOWR_ERR_HIP);
+    }
     // side streams at the device's greatest priority: the streaming path runs its critical chains there (the
     // FDISC / TQDISC records, whose blocks must not wait behind the other chain's, see launch_stream_path;
     // ANYmal gait + Torque, B = 1024: the TQDISC records on a low-priority stream took 730 us instead of ~50)
@@ -1368,14 +1362,6 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
       h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
     }
   }
-  {
-    const char* ffe = std::getenv("TOWR_GPU_FDISC_FUSED");
-    h->ff = L.fstream && !L.ff_geo.empty() && ffe && std::strcmp(ffe, "1") == 0 && ff_lds(L, nullptr) <= kLdsMax;
-    if (h->ff && ff_lds(L, nullptr) > 64 * 1024 &&
-        hipFuncSetAttribute(fdisc_fused_kernel(), hipFuncAttributeMaxDynamicSharedMemorySize, (int)ff_lds(L, nullptr)) != hipSuccess) {
-      h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
-    }
-  }
   if (L.fstream || L.gstream[GS_ROM] || L.gstream[GS_DYN] || L.gstream[GS_TQ]) {   // the record kernels share fs_inst_lds_bytes' layout
     // (fixed-gait RotVec also uses scratch, for its coefficient pre-pass, but launches no record kernel)
     const size_t lds = fs_inst_lds_bytes(L);
@@ -1391,13 +1377,28 @@ int towr_gpu_create_ex(const towr_problem_desc_t* desc, int32_t n_data, const to
     }
   }
   {
+    // the cost kernel's persistent grid: as many blocks as the device holds at once (cost_traj.hip)
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || cus <= 0) cus = 256;
     for (int g = 0; g < 2; ++g) {
       const int acc = cost_acc(L, g != 0);
       const size_t lds = cost_lds_bytes(L, acc);
+      const void* fn = cost_kernel_for(L.gait, acc, L.rotvec);
       if (lds > 160 * 1024) { h->err = "problem too large for the cost kernel's LDS gradient"; return bail(TOWR_ERR_UNSUPPORTED); }
-      if (lds > 64 * 1024 && hipFuncSetAttribute(cost_kernel_for(L.gait, acc, L.rotvec), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+      if (lds > 64 * 1024 && hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
         h->err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; return bail(TOWR_ERR_HIP);
       }
+      // blocks per CU: 160 kB of LDS, and the waves per SIMD the registers allow (512 VGPRs per lane and SIMD,
+      // granules of 8; a block of kCostBlock threads puts kCostBlock / 256 waves on each SIMD)
+      hipFuncAttributes fa{};
+      int per_cu = 1;
+      if (hipFuncGetAttributes(&fa, fn) == hipSuccess && fa.numRegs > 0) {
+        const int by_regs = 512 / ((fa.numRegs + 7) / 8 * 8) / std::max(1, kCostBlock / 256);
+        const int by_lds = (int)(160 * 1024 / std::max<size_t>(lds, 1));
+        per_cu = std::max(1, std::min({by_regs, by_lds, 8}));
+      }
+      h->cost_grid[acc] = per_cu * cus;
+      if (launch_log_on()) std::fprintf(stderr, "towr-cost acc %d regs %d lds %zu blocks/CU %d\n", acc, fa.numRegs, lds, per_cu);
     }
   }
   *out = h;
@@ -1409,7 +1410,7 @@ int towr_gpu_destroy(towr_gpu_handle h) {
   void* dev[] = {h->d_items, h->d_slots, h->d_tiles, h->d_nodecol, h->d_spl, h->d_dur, h->d_segs, h->d_terrain,
                  h->d_pinfo, h->d_pcols, h->d_pact, h->d_sched, h->d_misc, h->d_misc_lds, h->d_misc_wave, h->d_misc_items, h->d_xspan, h->d_eelin, h->d_gtab, h->d_idir, h->d_citems, h->d_cq, h->fuse[0].d_units, h->fuse[1].d_units,
                  h->d_bterrain, h->d_x, h->d_g, h->d_v, h->d_f, h->d_grad,
-                 h->d_traj_pd, h->d_traj_n, h->d_traj_c0, h->d_traj_t, h->d_fsb, h->d_fs_t, h->d_fs_tmpl, h->d_fs_ws, h->d_ff_geo, h->d_ff_blob,
+                 h->d_traj_pd, h->d_traj_n, h->d_traj_c0, h->d_traj_t, h->d_fsb, h->d_fs_t, h->d_fs_tmpl, h->d_fs_ws, 
                  h->d_fs_iee, h->d_fs_irow, h->d_fs_iblk, h->d_fsrec, h->d_lin, h->d_soft_b, h->d_soft_cptr, h->d_soft_cent, h->d_c_cptr, h->d_c_cslot, h->d_sg, h->d_sv,
                  h->single.d_units, h->d_gs_geo, h->d_gs_tmpl, h->d_gs_pcode, h->d_gs_blk[0], h->d_gs_blk[1], h->d_gs_blk[2],
                  h->d_gs_inst[0], h->d_gs_inst[1], h->d_gs_inst[2], h->d_gsrec, h->d_rvc, h->d_rvi, h->d_gs_segs, h->d_gs_tseg, h->d_gs_vmap, h->d_gs_ws, h->d_gs_blob};
