@@ -255,6 +255,14 @@ int towr_gpu_eval_g(towr_gpu_handle h, const double* x, double* g);
 int towr_gpu_eval_jac_values(towr_gpu_handle h, const double* x, double* values);
 /* both at once (one fused launch)                                                                */
 int towr_gpu_eval_g_jac(towr_gpu_handle h, const double* x, double* g, double* values);
+/* IPOPT's callback pair without a second evaluation: eval_g_keep_jac evaluates g and the Jacobian at x
+ * into the handle's device staging and returns g; the values stay on the device with a copy of x.
+ * eval_jac_values_kept(x) copies them into `values` (a DMA in place when `values` is registered) when x
+ * is bit-identical to the kept x, else it evaluates the values as towr_gpu_eval_jac_values does. Any
+ * other host-pointer evaluation on the handle drops the kept values. (ifopt IpoptAdapter::eval_g /
+ * eval_jac_g, hopper_example.cc:175-180)                                                           */
+int towr_gpu_eval_g_keep_jac(towr_gpu_handle h, const double* x, double* g);
+int towr_gpu_eval_jac_values_kept(towr_gpu_handle h, const double* x, double* values);
 /* Objective (IpoptAdapter::eval_f = Problem::EvaluateCostFunction, the sum of every cost term's
  * GetCost) and its dense gradient (eval_grad_f = Problem::EvaluateCostFunctionGradient). A problem
  * without cost terms has f = 0 and a zero gradient.                                               */

@@ -617,3 +617,27 @@ def test_batch_device_g_or_jac_only(name):
     p.eval_batch_device(Xd, None, Vd, want_g=False, want_jac=True)
     torch.cuda.synchronize()
     assert np.array_equal(Gd.cpu().numpy(), G) and np.array_equal(Vd.cpu().numpy()[:, :p.nnz], V)
+
+
+@pytest.mark.parametrize("name", ["anymal_trot_2p4s", "anymal_stairs_gaitopt"])
+def test_keep_jacobian_pair(name):
+    """IPOPT's pair through towr_gpu_eval_g_keep_jac + towr_gpu_eval_jac_values_kept: bit-identical to the one-call
+    evaluation at the same x; at another x (or after another host-pointer evaluation dropped the kept values) the
+    values are evaluated afresh, never served from the kept x."""
+    desc = CONFIGS[name]
+    o = Oracle(desc)
+    p = TowrGpuProblem(desc, device=0)
+    xa, xb = _perturb(o.initial_x(), 61), _perturb(o.initial_x(), 62)
+    ga, va = p.eval_g_jac(xa)
+    gb, vb = p.eval_g_jac(xb)
+    np.testing.assert_array_equal(p.eval_g_keep_jac(xa), ga)
+    np.testing.assert_array_equal(p.eval_jac_values_kept(xa), va)
+    np.testing.assert_array_equal(p.eval_jac_values_kept(xa), va)   # served again from the kept values
+    np.testing.assert_array_equal(p.eval_jac_values_kept(xb), vb)   # another x: evaluated
+    np.testing.assert_array_equal(p.eval_g_keep_jac(xb), gb)
+    p.eval_g(xa)                                                       # any other evaluation drops the kept values
+    np.testing.assert_array_equal(p.eval_jac_values_kept(xb), vb)
+    xc = xb.copy()
+    xc[7] = np.nextafter(xc[7], np.inf)                               # one ulp away: not the kept x
+    np.testing.assert_array_equal(p.eval_g_keep_jac(xb), gb)
+    np.testing.assert_array_equal(p.eval_jac_values_kept(xc), p.eval_jac_values(xc))

@@ -125,6 +125,8 @@ SYMBOLS = {
     "towr_gpu_eval_g": (C.c_int, [_HANDLE, _DP, _DP]),
     "towr_gpu_eval_jac_values": (C.c_int, [_HANDLE, _DP, _DP]),
     "towr_gpu_eval_g_jac": (C.c_int, [_HANDLE, _DP, _DP, _DP]),
+    "towr_gpu_eval_g_keep_jac": (C.c_int, [_HANDLE, _DP, _DP]),
+    "towr_gpu_eval_jac_values_kept": (C.c_int, [_HANDLE, _DP, _DP]),
     "towr_gpu_eval_f": (C.c_int, [_HANDLE, _DP, _DP]),
     "towr_gpu_eval_grad_f": (C.c_int, [_HANDLE, _DP, _DP]),
     "towr_gpu_eval_cost_batch_device": (C.c_int, [_HANDLE, C.c_int32, C.c_void_p, C.c_int64, C.c_void_p,

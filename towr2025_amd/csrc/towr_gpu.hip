@@ -96,6 +96,10 @@ struct towr_gpu_handle_s {
   hipStream_t scr_stream = nullptr;
   bool scr_used = false;
   bool sync_call = false;   // host_eval: the call synchronises its stream before returning (no event needed)
+  // towr_gpu_eval_g_keep_jac: the Jacobian of kept_x waits in the device staging d_v (kept: until any other
+  // host-pointer evaluation reuses the staging)
+  bool kept = false;
+  std::vector<double> kept_x;
   // fusion groups (TOWR_GPU_FUSE, see towr_step_kernel): classes that run in one launch
   struct FuseGroup {
     uint32_t mask = 0;        // bit lc: launch class lc belongs to the group
@@ -995,6 +999,7 @@ int ensure_events(towr_gpu_handle h, size_t n) {
 //     the host thread copies finished chunks out of the staging in parallel with both. Outputs in
 //     registered caller memory are DMA'd in place (no host copy at all).
 int host_eval(towr_gpu_handle h, int B, const double* X, double* G, double* V, bool single) {
+  h->kept = false;   // (the staging below may be overwritten)
   const towr_terrain_t* ter;
   int per;
   if (int rc = batch_terrain(h, B, single, &ter, &per)) return rc;
@@ -1497,6 +1502,62 @@ int towr_gpu_eval_g_jac(towr_gpu_handle h, const double* x, double* g, double* v
   if (!h || !x || !g || !values) return fail(h, TOWR_ERR_INVALID, "null argument");
   if (int rc = bind(h)) return rc;
   return host_eval(h, 1, x, g, values, true);
+}
+
+// IPOPT's callback pair at one x (eval_g, then eval_jac_g): towr_gpu_eval_g_keep_jac evaluates g AND the Jacobian
+// into the device staging (HBM, no PCIe traffic for the values: the composers / the single launch write at device
+// speed), returns g, and keeps the values with a copy of x; towr_gpu_eval_jac_values_kept then DMAs them into the
+// caller's array (in place when it is registered) if x is bit-identical, else it evaluates afresh. IPOPT's values
+// array is written only inside eval_jac_g, for the x it asked for. (Round 5's pair: g alone, then the Jacobian
+// zero-copy over PCIe into IPOPT's registered array: 111.5 us for ANYmal gait, B = 1.)
+int eval_single_kept(towr_gpu_handle h, const double* x, double* g) {
+  h->kept = false;
+  const towr_terrain_t* ter;
+  int per;
+  if (int rc = batch_terrain(h, 1, true, &ter, &per)) return rc;
+  if (int rc = ensure_stage(h, 1)) return rc;
+  const Layout& L = h->L;
+  const size_t xb = sizeof(double) * (size_t)L.n, gp = sizeof(double) * (size_t)L.m;
+  const double* xd = device_view(h, x, xb);
+  if (!xd) { std::memcpy(h->h_x, x, xb); xd = h->hd_x; }
+  h->sync_call = true;   // (the scratch event: this call ends with a synchronisation below)
+  const bool scr = uses_scratch(L);
+  if (scr && h->single.n_units > 0)
+    if (int rc = scratch_acquire(h, h->stream)) { h->sync_call = false; return rc; }
+  int rc = h->single.n_units > 0
+               ? launch_fused(h, h->single, 1, xd, L.n, h->d_g, L.m, h->d_v, L.nnz, 1, 1, h->stream, ter, per)
+               : launch(h, 1, xd, L.n, h->d_g, L.m, h->d_v, L.nnz, 1, 1, h->stream, ter, per, -1);
+  if (scr && h->single.n_units > 0) (void)scratch_release(h, h->stream);
+  h->sync_call = false;
+  double* gdst = is_registered(h, g, gp) ? g : h->h_g;
+  if (rc == TOWR_OK && hipMemcpyAsync(gdst, h->d_g, gp, hipMemcpyDeviceToHost, h->stream) != hipSuccess)
+    rc = fail(h, TOWR_ERR_HIP, "hipMemcpyAsync (g) failed");
+  if (hipStreamSynchronize(h->stream) != hipSuccess && rc == TOWR_OK) rc = fail(h, TOWR_ERR_HIP, "hipStreamSynchronize failed");
+  if (rc) return rc;
+  if (gdst != g) std::memcpy(g, h->h_g, gp);
+  h->kept_x.assign(x, x + L.n);
+  h->kept = true;
+  return TOWR_OK;
+}
+
+int towr_gpu_eval_g_keep_jac(towr_gpu_handle h, const double* x, double* g) {
+  if (!h || !x || !g) return fail(h, TOWR_ERR_INVALID, "null argument");
+  if (int rc = bind(h)) return rc;
+  return eval_single_kept(h, x, g);
+}
+
+int towr_gpu_eval_jac_values_kept(towr_gpu_handle h, const double* x, double* values) {
+  if (!h || !x || !values) return fail(h, TOWR_ERR_INVALID, "null argument");
+  if (int rc = bind(h)) return rc;
+  const Layout& L = h->L;
+  if (!h->kept || h->kept_x.size() != (size_t)L.n || std::memcmp(h->kept_x.data(), x, sizeof(double) * (size_t)L.n) != 0)
+    return host_eval(h, 1, x, nullptr, values, true);
+  const size_t vp = sizeof(double) * (size_t)L.nnz;
+  const bool vr = is_registered(h, values, vp);
+  HIPCHK(h, hipMemcpyAsync(vr ? values : h->h_v, h->d_v, vp, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (!vr) par_copy(values, h->h_v, vp);
+  return TOWR_OK;
 }
 
 // one problem through the staging buffers: x -> HBM, cost launch, f (and gradient) -> host

@@ -57,6 +57,9 @@ class Engine {
   void EvalConstraints(const double* x, double* g) const { Check(towr_gpu_eval_g(h_, x, g)); }
   void EvalNonzerosOfJacobian(const double* x, double* values) const { Check(towr_gpu_eval_jac_values(h_, x, values)); }
   void EvalConstraintsAndJacobian(const double* x, double* g, double* values) const { Check(towr_gpu_eval_g_jac(h_, x, g, values)); }
+  // g at x, with the Jacobian at x kept on the device; then the values at x from it (or evaluated, for another x)
+  void EvalConstraintsKeepJacobian(const double* x, double* g) const { Check(towr_gpu_eval_g_keep_jac(h_, x, g)); }
+  void EvalNonzerosOfJacobianKept(const double* x, double* values) const { Check(towr_gpu_eval_jac_values_kept(h_, x, values)); }
   // objective (ifopt Problem::EvaluateCostFunction) and its dense gradient
   double EvalCostFunction(const double* x) const { double f = 0.0; Check(towr_gpu_eval_f(h_, x, &f)); return f; }
   void EvalCostFunctionGradient(const double* x, double* grad) const { Check(towr_gpu_eval_grad_f(h_, x, grad)); }
@@ -94,24 +97,33 @@ class Engine {
 // The eval_f / eval_grad_f / eval_g / eval_jac_g callbacks of an IPOPT TNLP (Index = int,
 // Number = double), as ifopt's IpoptAdapter implements them for towr, served by the engine.
 //
-// Zero-copy Jacobian. eval_jac_g evaluates the values straight into IPOPT's own `values` array: the array is
-// page-locked for the engine (towr_gpu_register_host) the first time it is seen, and the engine's B = 1 launch
-// writes every value into it over PCIe, so no copy of the nnz values happens on the host (ifopt's IpoptAdapter
-// copies its sparse matrix there, ipopt_adapter.cc; at nnz = 241,250 that copy took longer than the evaluation).
-// IPOPT's TNLPAdapter passes the same array on every call (its jac_g_ member, allocated once), so registration
-// happens once per solve; when a different pointer arrives, the old one is unregistered and the new one
-// registered. If registration fails (the range overlaps one already registered, or the array is too short to
-// matter) the values go through the page-locked cache and a copy, as before.
-// eval_g evaluates g alone (into the page-locked g cache, then m doubles to IPOPT's g), unless eval_jac_g came first
-// at this x: then one launch formed both and eval_g serves the cached g. The Jacobian is written only when IPOPT asks
-// for it, so IPOPT's array never holds values of an x it did not request (its adapter reuses the array without
-// re-asking when the x tag it last evaluated matches).
-// finalize_solution (or the destructor) unregisters IPOPT's array.
+// One evaluation per x. eval_g at a new x evaluates g AND the Jacobian into the engine's device staging
+// (towr_gpu_eval_g_keep_jac) and returns g; eval_jac_g at that x then only moves the kept values into IPOPT's own
+// `values` array (towr_gpu_eval_jac_values_kept: one DMA, in place, because the array is page-locked for the engine
+// the first time it is seen), so no copy of the nnz values happens on the host (ifopt's IpoptAdapter copies its
+// sparse matrix there, ipopt_adapter.cc; at nnz = 241,250 that copy took longer than the evaluation). The values
+// are written into IPOPT's array only when IPOPT asks for them, and only for the x it asks about (the engine checks
+// x bit for bit), so the array never holds values of an x it did not request (its adapter reuses the array without
+// re-asking when the x tag it last evaluated matches). eval_jac_g first at a new x: one launch forms both, straight
+// into IPOPT's array, and eval_g serves the cached g.
+// IPOPT's TNLPAdapter passes the same array on every call (its jac_g_ member, allocated once per solve), so
+// registration happens once per solve; when a different pointer or length arrives, the old one is unregistered and the
+// new one registered. If registration fails (the range overlaps one already registered) the values go through the
+// page-locked cache and a copy.
+// A small Jacobian (below kSmallJacBytes, e.g. ANYmal with fixed phase durations: 225 kB) takes the round-4 path
+// instead: eval_g evaluates both in one launch into the page-locked caches, eval_jac_g copies the cached values
+// (MI355X, ANYmal, B = 1: 37.6 us per pair against 42.0 through the device staging; ANYmal gait, 1.93 MB of values:
+// 92.4 us through the device staging against 148.6 cached and 111.5 for round 5's g-alone + zero-copy Jacobian).
+// finalize_solution() is mandatory at the end of a solve (TNLP::finalize_solution; or destroy the callbacks): it
+// unregisters IPOPT's array before IPOPT frees it. A solve whose integration does not forward finalize_solution
+// would leave a registration of freed memory behind.
 class NlpCallbacks {
  public:
   // Lifetime: the Engine must outlive these callbacks (declare the Engine first): the destructor
   // unregisters through the Engine's handle.
-  explicit NlpCallbacks(Engine& e) : e_(e), g_(e.GetNumberOfConstraints()) {
+  static constexpr size_t kSmallJacBytes = 1u << 20;
+  explicit NlpCallbacks(Engine& e)
+      : e_(e), g_(e.GetNumberOfConstraints()), small_(e.GetNumberOfJacobianNonzeros() * sizeof(double) < kSmallJacBytes) {
     pin_g_ = !g_.empty() && e_.RegisterHost(g_.data(), g_.size() * sizeof(double)) == TOWR_OK;
   }
   ~NlpCallbacks() {
@@ -144,8 +156,16 @@ class NlpCallbacks {
   bool eval_g(int n, const double* x, bool new_x, int m, double* g) {
     if (n != e_.GetNumberOfOptimizationVariables() || m != e_.GetNumberOfConstraints()) return false;
     NewX(new_x);
-    if (!g_valid_) {   // g alone (the Jacobian is evaluated when IPOPT asks for it)
-      try { e_.EvalConstraints(x, g_.data()); } catch (const std::exception&) { return false; }
+    if (!g_valid_) {   // g, with the Jacobian kept for eval_jac_g at this x (on the device, or in the cache)
+      try {
+        if (small_) {
+          CacheValues();
+          e_.EvalConstraintsAndJacobian(x, g_.data(), v_.data());
+          v_valid_ = true;
+        } else {
+          e_.EvalConstraintsKeepJacobian(x, g_.data());
+        }
+      } catch (const std::exception&) { return false; }
       g_valid_ = true;
     }
     for (int i = 0; i < m; ++i) g[i] = g_[i];
@@ -160,9 +180,13 @@ class NlpCallbacks {
       return true;
     }
     NewX(new_x);
+    if (small_ && g_valid_ && v_valid_) {   // the cached values of this x
+      for (int k = 0; k < nele_jac; ++k) values[k] = v_[k];
+      return true;
+    }
     double* dst = Values(values, nele_jac);   // IPOPT's array when registered, else the page-locked cache
     try {
-      if (g_valid_) e_.EvalNonzerosOfJacobian(x, dst);
+      if (g_valid_) e_.EvalNonzerosOfJacobianKept(x, dst);   // the values eval_g kept (or evaluated, another x)
       else e_.EvalConstraintsAndJacobian(x, g_.data(), dst);   // first callback at this x: g comes along
     } catch (const std::exception&) { g_valid_ = false; return false; }
     g_valid_ = true;
@@ -175,16 +199,25 @@ class NlpCallbacks {
 
   // introspection for tests: whether the last eval_jac_g wrote IPOPT's array directly, registrations so far
   bool values_zero_copy() const { return reg_ != nullptr; }
+  bool small_jacobian() const { return small_; }   // the cached path (kSmallJacBytes)
   int values_registrations() const { return n_reg_; }
 
  private:
-  // IPOPT's new_x == true on the first callback at a new x (whichever it is) invalidates the cached g
-  void NewX(bool new_x) { if (new_x) g_valid_ = false; }
+  // IPOPT's new_x == true on the first callback at a new x (whichever it is) invalidates the cached g (and values)
+  void NewX(bool new_x) { if (new_x) g_valid_ = v_valid_ = false; }
+  void CacheValues() {   // the page-locked values cache (small Jacobians, and the fallback of Values)
+    const size_t nele = (size_t)e_.GetNumberOfJacobianNonzeros();
+    if (v_.size() == nele) return;
+    if (pin_v_) e_.UnregisterHost(v_.data());
+    v_.assign(nele, 0.0);
+    pin_v_ = nele > 0 && e_.RegisterHost(v_.data(), v_.size() * sizeof(double)) == TOWR_OK;
+  }
   double* Values(double* values, int nele) {
-    if (values == reg_) return values;
+    if (values == reg_ && nele == reg_n_) return values;
     ReleaseValues();
     if (nele > 0 && e_.RegisterHost(values, (size_t)nele * sizeof(double)) == TOWR_OK) {
       reg_ = values;
+      reg_n_ = nele;
       ++n_reg_;
       return values;
     }
@@ -198,12 +231,15 @@ class NlpCallbacks {
   void ReleaseValues() {
     if (reg_) e_.UnregisterHost(reg_);
     reg_ = nullptr;
+    reg_n_ = 0;
   }
   Engine& e_;
   std::vector<double> g_, v_;
   bool pin_g_ = false, pin_v_ = false;
-  bool g_valid_ = false;
-  double* reg_ = nullptr;   // IPOPT's values array, registered
+  bool g_valid_ = false, v_valid_ = false;
+  const bool small_;
+  double* reg_ = nullptr;   // IPOPT's values array, registered (reg_n_ values)
+  int reg_n_ = 0;
   int n_reg_ = 0;
 };
 

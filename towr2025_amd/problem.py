@@ -138,6 +138,20 @@ class TowrGpuProblem:
         self._check(self._lib.towr_gpu_eval_g_jac(self._h, capi.dptr(x), capi.dptr(g), capi.dptr(v)))
         return g, v
 
+    def eval_g_keep_jac(self, x) -> np.ndarray:
+        """g at x, the Jacobian kept on the device for eval_jac_values_kept (IPOPT's eval_g at a new x)."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        g = np.zeros(self.m)
+        self._check(self._lib.towr_gpu_eval_g_keep_jac(self._h, capi.dptr(x), capi.dptr(g)))
+        return g
+
+    def eval_jac_values_kept(self, x) -> np.ndarray:
+        """The Jacobian values at x: the kept ones when x is bit-identical to eval_g_keep_jac's, else evaluated."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        v = np.zeros(self.nnz)
+        self._check(self._lib.towr_gpu_eval_jac_values_kept(self._h, capi.dptr(x), capi.dptr(v)))
+        return v
+
     def eval_g_jac_into(self, x, g, v):
         """eval_g + eval_jac_g into caller arrays (contiguous float64): with x, g, v registered
         (register_host) the transfers run in place, as an IPOPT driver reusing its buffers would."""
