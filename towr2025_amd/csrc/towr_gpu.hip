@@ -1509,7 +1509,9 @@ int towr_gpu_eval_g_jac(towr_gpu_handle h, const double* x, double* g, double* v
 // speed), returns g, and keeps the values with a copy of x; towr_gpu_eval_jac_values_kept then DMAs them into the
 // caller's array (in place when it is registered) if x is bit-identical, else it evaluates afresh. IPOPT's values
 // array is written only inside eval_jac_g, for the x it asked for. (Round 5's pair: g alone, then the Jacobian
-// zero-copy over PCIe into IPOPT's registered array: 111.5 us for ANYmal gait, B = 1.)
+// zero-copy over PCIe into IPOPT's registered array: 111.5 us for ANYmal gait, B = 1; this pair 91.1 us. Returning g
+// before the compose launch ends, with the small kinds in a launch of their own and g copied on the copy stream after an
+// event between the record and compose launches: 105.6 us, a cross-stream event costs more than the overlap gains.)
 int eval_single_kept(towr_gpu_handle h, const double* x, double* g) {
   h->kept = false;
   const towr_terrain_t* ter;
