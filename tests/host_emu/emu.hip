@@ -214,6 +214,7 @@ extern "C" int emu_cost_stats(const towr_problem_desc_t* d, const double* x) {
   c.eelin = L.eelin.data(); c.rotvec = L.rotvec; c.cq = L.cost_q.data();
   long n_t[CT_COUNT] = {}, em_t[CT_COUNT] = {}, pr_t[CT_COUNT] = {}, mx_t[CT_COUNT] = {};
   for (const CostItem& it : L.cost_items) {
+    if (it.type >= CT_COUNT) continue;   // a no-op lane of the wave schedule
     c.seg = it.seg >= 0 ? L.segs.data() + (size_t)it.seg * L.spl.size() : nullptr;
     CountEmit em{}; em.colcnt = &colcnt;
     eval_cost_item(c, it, em);

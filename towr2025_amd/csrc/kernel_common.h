@@ -431,13 +431,10 @@ const void* cost_kernel_for(bool gait, int acc, bool rotvec);   // acc: 0 f only
 const void* traj_kernel_for(bool gait);
 const void* rv_coef_kernel();
 constexpr int kRvCoefBlock = 256;   // the RotVec coefficient pre-pass: 4 waves, one component each
-// objective kernel: persistent blocks, one problem at a time per block. 512 threads: one block per CU (8 waves, the
-// 2 per SIMD its registers allow) with the CU's whole LDS for the slot gradient (ANYmal + every cost kind: 84 kB, more
-// than half a CU's 160 kB, so 256-thread blocks ran one per CU: 0.207 ms per 4096 problems)
-#ifndef TOWR_COST_BLOCK   // (experiment builds: -DTOWR_COST_BLOCK=256)
-#define TOWR_COST_BLOCK 256
-#endif
-constexpr int kCostBlock = TOWR_COST_BLOCK;
+// objective kernel: persistent blocks of 256 threads, one problem at a time per block (Layout's wave schedule of
+// the cost items assumes kCostLanes threads). (512-thread blocks, one per CU with the CU's whole LDS: 0.179 vs 0.130
+// ms per 4096 problems.)
+constexpr int kCostBlock = kCostLanes;
 constexpr int kTrajBlock = 64;    // trajectory kernel: one block per (problem, 64 sample times)
 
 // The heavy kinds read spline nodes through the segment records; with phase-duration optimisation

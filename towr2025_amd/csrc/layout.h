@@ -271,7 +271,6 @@ struct Layout {
   // cost terms (eval_f / eval_grad_f): work items sorted by CostType, one block per problem
   std::vector<CostItem> cost_items;
   std::vector<double> cost_q;        // CT_ENERGYQ Gram matrices, 16 doubles per item (CostItem::q)
-  int32_t cost_type0[CT_COUNT + 1] = {};
   // Deterministic gradient (fixed phase durations): every present gradient entry of every cost item has an
   // LDS contribution slot, ordered by column (layout.hip build_cost_slots): entry k of item i goes to slot
   // cost_cslot[CostItem::cslot + k], and column j sums slots [cost_cptr[j], cost_cptr[j + 1]) in order.
@@ -290,6 +289,7 @@ struct Layout {
 #define TOWR_COST_SLOT_MAX 8192
 #endif
 constexpr int kCostSlotMax = TOWR_COST_SLOT_MAX;   // contribution slots of the cost kernel's LDS (64 KB)
+constexpr int kCostLanes = 256;   // threads of the cost kernel's blocks (kCostBlock, its wave schedule)
 constexpr int kMiscWaves = 4;   // one-wave small-kind tiles per group (block)
 constexpr int kSlotSpare = 4;   // spare slot groups per lane: the kernels prefetch up to this many ahead
 constexpr bool is_misc_kind(int t) { return t != IT_DYN && t != IT_ROM && t != IT_FDISC && t != IT_TQDISC; }

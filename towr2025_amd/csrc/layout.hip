@@ -309,6 +309,56 @@ int push_seg_row(Layout& L, double t) {
 
 // cost work items (NlpFormulation::GetCosts, nlp_formulation.cc:604-680), grouped by type
 constexpr int kNodeChunk = 4;   // NodeCost nodes per work item
+// The cost kernel's wave schedule (cost_traj.hip: item i runs on lane i % kCostLanes in round i / kCostLanes, so in
+// wave (i % kCostLanes) / 64). A wave's time is the sum over its rounds of its slowest item, and a wave whose lanes
+// hold two kinds runs both paths. So each kind's items (sorted by kind) go in chunks of 64 lanes, one chunk per
+// (round, wave), and the chunks are dealt to the waves heaviest first, each to the wave with the least work so far
+// (longest processing time first): every wave runs one kind per round and the waves' loads are level. Lanes left
+// over hold a no-op item (type CT_COUNT). The relative latencies per kind are from tools/cost_timing.py (MI355X,
+// ANYmal, f + gradient of each kind alone).
+std::vector<CostItem> cost_wave_schedule(const std::vector<CostItem>& items) {
+#if defined(TOWR_COST_SCHED) && TOWR_COST_SCHED == 0   // (experiment builds: the items in kind order, round-robin)
+  return items;
+#endif
+  constexpr int W = kCostLanes / 64;
+  auto weight = [](int type) {
+    switch (type) {
+      case CT_EEBP: return 5.0;
+      case CT_ANGMOM: return 3.0;
+      case CT_ENERGY: return 3.0;
+      case CT_BHC: return 2.0;
+      case CT_ENERGYQ: return 1.5;
+      default: return 1.0;
+    }
+  };
+  struct Chunk { size_t i0, n; double w; };
+  std::vector<Chunk> chunks;
+  for (size_t i = 0; i < items.size();) {
+    size_t j = i;
+    while (j < items.size() && items[j].type == items[i].type && j - i < 64) ++j;
+    chunks.push_back({i, j - i, weight(items[i].type)});
+    i = j;
+  }
+  std::stable_sort(chunks.begin(), chunks.end(), [](const Chunk& a, const Chunk& b) { return a.w > b.w; });
+  std::vector<std::vector<const Chunk*>> per(W);
+  double load[W] = {};
+  for (const Chunk& c : chunks) {
+    const int w = (int)(std::min_element(load, load + W) - load);
+    per[w].push_back(&c);
+    load[w] += c.w;
+  }
+  size_t rounds = 0;
+  for (const auto& v : per) rounds = std::max(rounds, v.size());
+  CostItem none{};
+  none.type = CT_COUNT; none.seg = -1;
+  std::vector<CostItem> out(rounds * kCostLanes, none);
+  for (int w = 0; w < W; ++w)
+    for (size_t r = 0; r < per[w].size(); ++r)
+      for (size_t l = 0; l < per[w][r]->n; ++l) out[r * kCostLanes + (size_t)w * 64 + l] = items[per[w][r]->i0 + l];
+  while (!out.empty() && out.back().type == CT_COUNT) out.pop_back();
+  return out;
+}
+
 int build_costs(const towr_problem_desc_t& d, const std::vector<double>& base_d, Layout& L, std::string& err) {
   const int E = d.robot.n_ee;
   if (d.n_costs < 0 || d.n_costs > TOWR_MAX_COSTS) { err = "n_costs out of range"; return TOWR_ERR_INVALID; }
@@ -435,12 +485,7 @@ int build_costs(const towr_problem_desc_t& d, const std::vector<double>& base_d,
     }
   }
   std::stable_sort(items.begin(), items.end(), [](const CostItem& a, const CostItem& b) { return a.type < b.type; });
-  L.cost_items.swap(items);
-  for (int t = 0; t <= CT_COUNT; ++t) {
-    int k = 0;
-    while (k < (int)L.cost_items.size() && L.cost_items[k].type < t) ++k;
-    L.cost_type0[t] = k;
-  }
+  L.cost_items = cost_wave_schedule(items);
   return TOWR_OK;
 }
 
