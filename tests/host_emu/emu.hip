@@ -376,3 +376,30 @@ extern "C" int emu_traj(const towr_problem_desc_t* d, const double* x, double dt
     if (k < max_rows) traj_row(c, ph, t, out + (size_t)k * cols, 1);
   return k;
 }
+
+// whether every polynomial's active-window PhaseCols (pact window, then up to kGsAct entries: n, ids, derivs) coincide
+// over the three dimensions, per spline (experiment aid: the record composers' window sums per dimension)
+extern "C" int emu_window_dims(const towr_problem_desc_t* d) {
+  Layout L; std::string e;
+  if (build_layout(*d, L, e)) return -1;
+  for (size_t s = 0; s < L.spl.size(); ++s) {
+    const SplineMeta& m = L.spl[s];
+    if (m.ee < 0) continue;
+    int same = 1;
+    for (int p = 0; p < m.n_polys && same; ++p) {
+      int a[3], z[3];
+      for (int k = 0; k < 3; ++k) { a[k] = L.pact[m.pact_off + 2 * (k * m.n_polys + p)]; z[k] = L.pact[m.pact_off + 2 * (k * m.n_polys + p) + 1]; }
+      for (int k = 1; k < 3 && same; ++k) {
+        if (z[k] - a[k] != z[0] - a[0]) { same = 0; break; }
+        for (int q = 0; q < kGsAct && a[0] + q <= z[0]; ++q) {
+          const PhaseCol& c0 = L.pcols[m.pcol_off[0] + a[0] + q];
+          const PhaseCol& ck = L.pcols[m.pcol_off[k] + a[k] + q];
+          if (c0.n != ck.n) { same = 0; break; }
+          for (int j = 0; j < c0.n; ++j) if (c0.id[j] != ck.id[j] || c0.deriv[j] != ck.deriv[j]) same = 0;
+        }
+      }
+    }
+    std::printf("spline %zu ee %d: dims coincide %d\n", s, m.ee, same);
+  }
+  return 0;
+}

@@ -124,7 +124,7 @@ struct TqCls {
     const int kind = sg.kind, e = (t >> 22) & 3, q = t & 0x3FFFFF;   // torque (kind 2) or force (1) PhaseCol
     const unsigned rel = (unsigned)(q - ci[2 * (kind == 2 ? 1 + e : 4 + e)]);
     if (rel >= (unsigned)kGsAct) return 0.0;
-    const double sum = d[(kind == 2 ? 24 : 36) + e * kGsAct + rel];
+    const double sum = d[(kind == 2 ? 24 : 28) + rel];   // (one set for the three dimensions, layout.h)
     return (kind == 2 ? tb(d, r, e) : d[9 + e]) * sum;   // emit_dim: scale * basis sum
   }
 };
@@ -159,22 +159,19 @@ TG_HD void tq_record(const Ctx& c, const GsInst& gi, Put&& put, double g[4]) {
   put(kTqND, gs_int(Jt.cur));
   double H[4], sums[3][kGsAct];
   int qa[3];
+  // (the window sums of the three dimensions coincide: the layout checked the PhaseCols, spline_dims_coincide)
   spline_basis(Tq, kPos, H);   // AccumulateLinearFormJacobian of the torque spline (:147-155)
   gs_window(c, sp_torque(ee), Tq.poly, H, sums, qa);
 #pragma unroll
-  for (int e = 0; e < 3; ++e) {
-    put(kTqND + 1 + e, gs_int(qa[e]));
+  for (int e = 0; e < 3; ++e) put(kTqND + 1 + e, gs_int(qa[e]));
 #pragma unroll
-    for (int q = 0; q < kGsAct; ++q) put(24 + e * kGsAct + q, sums[e][q]);
-  }
+  for (int q = 0; q < kGsAct; ++q) put(24 + q, sums[0][q]);
   spline_basis(F, kPos, H);    // ... of the force spline into the normal-torque rows (:158-163)
   gs_window(c, sp_force(ee), F.poly, H, sums, qa);
 #pragma unroll
-  for (int e = 0; e < 3; ++e) {
-    put(kTqND + 4 + e, gs_int(qa[e]));
+  for (int e = 0; e < 3; ++e) put(kTqND + 4 + e, gs_int(qa[e]));
 #pragma unroll
-    for (int q = 0; q < kGsAct; ++q) put(36 + e * kGsAct + q, sums[e][q]);
-  }
+  for (int q = 0; q < kGsAct; ++q) put(28 + q, sums[0][q]);
   put(kTqND + 7, gs_int(Tq.poly));
   put(kTqND + 8, gs_int(F.poly));
 }

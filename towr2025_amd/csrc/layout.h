@@ -136,14 +136,17 @@ struct GsInst { double t; int32_t seg, row0; int16_t ee, kk, nb, reserved; doubl
 //                  endeffector Fp[3] | rv[3] | Jf.dx v[6] | Jx.dx v[6] | sums[kind][dim][4] (36);
 //                  ints per endeffector curF | curX | qa[kind][dim] (9) | poly[kind] (3)
 //   TorqueConstraintDiscretized: t1[3] | t2[3] | n[3] | b[3] (= -k mu n) | Jt.dx v[6] | Jf.dx v[6] |
-//                  torque sums[dim][4] (12) | force sums[dim][4] (12); ints cur | qaT[3] | qaF[3] | polyT | polyF
+//                  torque sums[4] | force sums[4]; ints cur | qaT[3] | qaF[3] | polyT | polyF. The sums are
+//                  the same for the three dimensions (the layout streams TQDISC only when the torque and force
+//                  splines' active windows hold PhaseCols of one structure in every dimension, spline_dims_coincide),
+//                  so one set of 4 per spline: 41 fields instead of round 5's 57
 //                  (torque_constraint_discretized.cc:139-235 without the motion block: a terrain
 //                  without curvature, where every motion scale is exactly 0.0 and the block is skipped, :57)
 // (kind 0 motion, 1 force, 2 torque; sums / qa: the active-window basis sums of the PhaseSpline, the
 // first active PhaseCol of each dimension and the basis sums of up to kGsAct PhaseCols from it)
 constexpr int kRomND = 44, kRomNI = 5;
 constexpr int kDynBaseND = 53, kDynEeND = 54, kDynEeNI = 14;
-constexpr int kTqND = 48, kTqNI = 9;
+constexpr int kTqND = 32, kTqNI = 9;
 TG_HD constexpr int gs_rec_nd(int cls, int E) { return cls == GS_ROM ? kRomND : cls == GS_TQ ? kTqND : kDynBaseND + kDynEeND * E; }
 TG_HD constexpr int gs_rec_ni(int cls, int E) { return cls == GS_ROM ? kRomNI : cls == GS_TQ ? kTqNI : kDynEeNI * E; }
 TG_HD constexpr int gs_rec_fields(int cls, int E) { return gs_rec_nd(cls, E) + gs_rec_ni(cls, E); }

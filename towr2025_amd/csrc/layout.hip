@@ -681,6 +681,28 @@ namespace {
 struct BaseDec { int8_t s = -1, deriv = 0, dim = 0; int32_t node = 0; };   // base node-set column
 struct PhaseDec { int8_t kind = -1, ee = 0, dim = 0; int32_t q = 0; };     // PhaseSpline column (kind 0 motion, 1 force, 2 torque)
 
+// Whether every polynomial's active window (Layout::pact) of PhaseSpline s holds PhaseCols of one structure (count,
+// node ids, derivatives) in all three dimensions: then its kGsAct window basis sums are the same in every dimension
+// (gs_window), and a record keeps one set (the TQDISC record, layout.h).
+bool spline_dims_coincide(const Layout& L, int s) {
+  const SplineMeta& m = L.spl[s];
+  for (int p = 0; p < m.n_polys; ++p) {
+    const int32_t* w0 = L.pact.data() + m.pact_off + 2 * p;
+    for (int k = 1; k < 3; ++k) {
+      const int32_t* wk = L.pact.data() + m.pact_off + 2 * (k * m.n_polys + p);
+      if (wk[1] - wk[0] != w0[1] - w0[0]) return false;
+      for (int q = 0; q < kGsAct && w0[0] + q <= w0[1]; ++q) {
+        const PhaseCol& a = L.pcols[(size_t)m.pcol_off[0] + w0[0] + q];
+        const PhaseCol& b = L.pcols[(size_t)m.pcol_off[k] + wk[0] + q];
+        if (a.n != b.n) return false;
+        for (int j = 0; j < a.n; ++j)
+          if (a.id[j] != b.id[j] || a.deriv[j] != b.deriv[j]) return false;
+      }
+    }
+  }
+  return true;
+}
+
 bool build_gstream_class(Layout& L, int cls, const std::vector<BaseDec>& bdec, const std::vector<PhaseDec>& pdec,
                          const std::vector<int>& sdec_ee, const std::vector<int>& sdec_j, std::string& why) {
   const int nspl = (int)L.spl.size();
@@ -690,6 +712,13 @@ bool build_gstream_class(Layout& L, int cls, const std::vector<BaseDec>& bdec, c
   const bool per_ee = cls != GS_DYN;   // one endeffector's constraint (RangeOfMotion, TQDISC)
   // TQDISC on curved terrain adds its motion block only where a scale is non-zero (:57): data-dependent, tiles
   if (cls == GS_TQ && L.fdisc_motion) { why = "motion block on curved terrain"; return false; }
+  if (cls == GS_TQ)   // one set of window sums per spline in the record
+    for (const ConsInfo& cs : L.cons)
+      if (cs.kind == TOWR_C_TORQUE_DISCRETIZED && cs.rows > 0 &&
+          (!spline_dims_coincide(L, sp_torque(cs.ee)) || !spline_dims_coincide(L, sp_force(cs.ee)))) {
+        why = "window structure differs by dimension";
+        return false;
+      }
   std::vector<GsGeo> geos;
   std::vector<GsBlock> blocks;
   std::vector<GsInst> insts;
