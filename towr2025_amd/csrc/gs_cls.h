@@ -95,7 +95,7 @@ struct DynCls {
     const int kind = sg.kind, e = (t >> 22) & 3, q = t & 0x3FFFFF;
     const unsigned rel = (unsigned)(q - ii[2 * (2 + 3 * kind + e)]);
     if (rel >= (unsigned)kGsAct) return 0.0;
-    const double v = de[18 + (kind * 3 + e) * kGsAct + rel];
+    const double v = de[dyn_sum_field(kind, e, rel)];
     // emit_dim scales: motion Cross(f)[r][e]; force Cross(rv)[r][e] (angular) or -1 (linear); torque -1
     const double sc = kind == 0 ? cross_el(de, r, e) : kind == 1 ? (r < 3 ? cross_el(de + 3, r, e) : -1.0) : -1.0;
     return sc * v;

@@ -211,8 +211,9 @@ __device__ __forceinline__ void gs_records(const KParams& P, const GsRecArgs& A,
 #pragma unroll
         for (int e = 0; e < 3; ++e) {
           put(fi + 2 + 3 * kind + e, gs_int(qa[e]));
+          if (kind == 0 || e == 0)   // force and torque: one set for the three dimensions (layout.h)
 #pragma unroll
-          for (int q = 0; q < kGsAct; ++q) put(fd + 18 + (3 * kind + e) * kGsAct + q, sums[e][q]);
+            for (int q = 0; q < kGsAct; ++q) put(fd + dyn_sum_field(kind, e, q), sums[e][q]);
         }
       }
       if (kind < 2) {   // force and ee-position schedule terms (dynamic_constraint.cc:116-122; no torque term)

@@ -133,8 +133,10 @@ struct GsInst { double t; int32_t seg, row0; int16_t ee, kk, nb, reserved; doubl
 //   RangeOfMotion: R[9] | HL[4] | Ag[axis][r] (9) | HA[4] | Jx.dx[3] v[3] | sums[dim][4] (12);
 //                  ints cur | qa[dim] (3) | poly
 //   Dynamic:       fs[3] | Lp[3] | HpL[4] | HaL[4] | A[axis][p v a][r] (27) | HpA HvA HaA (12), then per
-//                  endeffector Fp[3] | rv[3] | Jf.dx v[6] | Jx.dx v[6] | sums[kind][dim][4] (36);
-//                  ints per endeffector curF | curX | qa[kind][dim] (9) | poly[kind] (3)
+//                  endeffector Fp[3] | rv[3] | Jf.dx v[6] | Jx.dx v[6] | motion sums[dim][4] (12) | force sums[4] |
+//                  torque sums[4]; ints per endeffector curF | curX | qa[kind][dim] (9) | poly[kind] (3). The force
+//                  and torque sums are one set for the three dimensions, as TQDISC's below (the layout streams Dynamic
+//                  only when they coincide, spline_dims_coincide): 38 doubles per endeffector instead of round 5's 54
 //   TorqueConstraintDiscretized: t1[3] | t2[3] | n[3] | b[3] (= -k mu n) | Jt.dx v[6] | Jf.dx v[6] |
 //                  torque sums[4] | force sums[4]; ints cur | qaT[3] | qaF[3] | polyT | polyF. The sums are
 //                  the same for the three dimensions (the layout streams TQDISC only when the torque and force
@@ -145,7 +147,9 @@ struct GsInst { double t; int32_t seg, row0; int16_t ee, kk, nb, reserved; doubl
 // (kind 0 motion, 1 force, 2 torque; sums / qa: the active-window basis sums of the PhaseSpline, the
 // first active PhaseCol of each dimension and the basis sums of up to kGsAct PhaseCols from it)
 constexpr int kRomND = 44, kRomNI = 5;
-constexpr int kDynBaseND = 53, kDynEeND = 54, kDynEeNI = 14;
+constexpr int kDynBaseND = 53, kDynEeND = 38, kDynEeNI = 14;
+// field of the window sum q of kind (0 motion, 1 force, 2 torque) and dimension e in a Dynamic record's endeffector part
+TG_HD constexpr int dyn_sum_field(int kind, int e, int q) { return kind == 0 ? 18 + e * kGsAct + q : 26 + kind * kGsAct + q; }
 constexpr int kTqND = 32, kTqNI = 9;
 TG_HD constexpr int gs_rec_nd(int cls, int E) { return cls == GS_ROM ? kRomND : cls == GS_TQ ? kTqND : kDynBaseND + kDynEeND * E; }
 TG_HD constexpr int gs_rec_ni(int cls, int E) { return cls == GS_ROM ? kRomNI : cls == GS_TQ ? kTqNI : kDynEeNI * E; }

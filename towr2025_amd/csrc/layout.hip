@@ -719,6 +719,12 @@ bool build_gstream_class(Layout& L, int cls, const std::vector<BaseDec>& bdec, c
         why = "window structure differs by dimension";
         return false;
       }
+  if (cls == GS_DYN)   // one set of force and torque window sums per endeffector
+    for (int ee = 0; ee < L.rb.n_ee; ++ee)
+      if (!spline_dims_coincide(L, sp_torque(ee)) || !spline_dims_coincide(L, sp_force(ee))) {
+        why = "window structure differs by dimension";
+        return false;
+      }
   std::vector<GsGeo> geos;
   std::vector<GsBlock> blocks;
   std::vector<GsInst> insts;
