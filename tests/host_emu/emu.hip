@@ -75,7 +75,7 @@ extern "C" int emu_eval_ex(const towr_problem_desc_t* d, int n_data, const towr_
       for (int k = 0; k < fb.n_inst; ++k) {
         c.seg = nullptr;
         fdisc_instant(c, fb.ee, L.fs_t[fb.t0 + k], in[k]);
-        ws[k] = L.fs_ws[2 * (fb.wsoff + in[k].poly)];   // (window start, dimension codes) pairs
+        ws[k] = L.fs_ws[3 * (fb.wsoff + in[k].poly)];   // (window start, dimension codes, slot codes) triples
         for (int i = 0; i < 5; ++i) g[fb.r0 + 5 * k + i] = in[k].g[i];
       }
       for (int e = 0; e < fb.nv; ++e) {

@@ -63,18 +63,18 @@ __device__ __forceinline__ void fdisc_record(const KParams& P, const FsTabs& T, 
     for (int i = 0; i < 5; ++i) __builtin_nontemporal_store(o.g[i], Gb + row + i);
   TG_STAMP(P, 5);
   const int poly = o.poly;
-  const int ws = T.ws[2 * (fb.wsoff + poly)], wd = T.ws[2 * (fb.wsoff + poly) + 1];
+  const int ws = T.ws[3 * (fb.wsoff + poly)], wd = T.ws[3 * (fb.wsoff + poly) + 1], wq = T.ws[3 * (fb.wsoff + poly) + 2];
   put(kFsND, fs_int(ws));
   put(kFsND + 1, fs_int(wd));
+  put(kFsND + 3, fs_int(wq));
   double h0 = o.H[0], h1 = o.H[1], h2 = o.H[2], h3 = o.H[3];
   asm volatile("" : "+v"(h0), "+v"(h1), "+v"(h2), "+v"(h3));
-  const int32_t* tm = T.tmpl + fb.tmpl;
-#pragma unroll 4
-  for (int q = 0; q < kFsWin; ++q) {   // the window's basis sums (schedule entries: never read, 0)
-    const int pos = ws + q;
-    const int32_t te = pos < fb.L ? tm[pos] : -1;
-    put(q, te >= 0 ? phase_basis_sum(c.pcols[te & 0xFFFFFF], poly, h0, h1, h2, h3) : 0.0);
-  }
+  const SplineMeta m = c.spl[sp_force(P.fs_iee[k])];
+  const int32_t* aw = c.pact + m.pact_off + 2 * poly;   // dimension 0's active window
+  const int a = aw[0], z = aw[1];
+#pragma unroll
+  for (int q = 0; q < kFsS; ++q)   // the active window's basis sums (one set: the dimensions coincide)
+    put(q, a + q <= z ? phase_basis_sum(c.pcols[m.pcol_off[0] + a + q], poly, h0, h1, h2, h3) : 0.0);
   TG_STAMP(P, 6);
 }
 __device__ __forceinline__ void fdisc_records(const KParams& P, const FsTabs& T, const Ctx& c, int b, double* rec, int64_t ldr, int32_t k0,
@@ -425,12 +425,12 @@ constexpr int kFsUnits = TOWR_FS_UNITS;
 template <int BLOCK>
 __device__ __forceinline__ void fs_rows(const FsBlock& fb, const double* cd, double* rowv, int32_t* wsr) {
   const int tid = threadIdx.x, nr = 5 * fb.n_inst;
-  auto ci = [&](int k, int f) -> int { return *reinterpret_cast<const int32_t*>(cd + k * kFsCS + kFsND + f); };   // ws, wd, cur
+  auto ci = [&](int k, int f) -> int { return *reinterpret_cast<const int32_t*>(cd + k * kFsCS + kFsND + f); };   // ws, wd, cur, wq
   for (int t = tid; t < nr * kFsWin; t += BLOCK) {
     const int r = t / kFsWin, q = t - r * kFsWin;
     const int k = r / 5, i = r - 5 * k;
-    const double v = cd[k * kFsCS + q];
-    const int ed = (ci(k, 1) >> (2 * q)) & 3;
+    const int ed = (ci(k, 1) >> (2 * q)) & 3;   // 3: not an active column
+    const double v = ed == 3 ? 0.0 : cd[k * kFsCS + ((ci(k, 3) >> (2 * q)) & 3)];
     rowv[t] = v == 0.0 ? 0.0 : cd[k * kFsCS + kFsB + 3 * i + ed] * v;
   }
   for (int t = tid; t < nr; t += BLOCK) wsr[t] = ci(t / 5, 0);

@@ -55,10 +55,14 @@ constexpr int kFsWin = 12;
 // (e / L) 2^-23 < 0.5 / L, i.e. for e < 2^22. The layout keeps every block range below half that bound
 // (build_fstream, build_gstream_class: fewer instants per block, or the tile path).
 constexpr int kFloatDivMax = 1 << 21;
-// FDISC record (gstream.hip fdisc_records -> the composer): Hv[kFsWin] | b[5][3] | Jf.dx[3] |
-// Jf.v[3] | ints ws, wd, cur (64-bit integer bit patterns)
-constexpr int kFsB = kFsWin, kFsDx = kFsWin + 15, kFsV = kFsWin + 18, kFsND = kFsWin + 21;
-constexpr int kFsRS = kFsND + 3, kFsCS = kFsRS | 1;   // record fields; LDS stride per instant
+// FDISC record (gstream.hip fdisc_records -> the composer): S[kFsS] | b[5][3] | Jf.dx[3] | Jf.v[3] | ints ws, wd,
+// cur, wq (64-bit integer bit patterns). S = the basis sums of the force polynomial's active window in dimension 0;
+// the three dimensions' windows hold PhaseCols of one structure (build_fstream checks it), so window position q
+// holds S[slot q] (wq: 2 bits per position) times b[row][dim q] (wd: 2 bits per position, 3 = not an active column:
+// 0). Round 5's record kept the 12 window positions' sums (36 fields instead of 29).
+constexpr int kFsS = 4;   // = kGsAct (below)
+constexpr int kFsB = kFsS, kFsDx = kFsS + 15, kFsV = kFsS + 18, kFsND = kFsS + 21;
+constexpr int kFsRS = kFsND + 4, kFsCS = kFsRS | 1;   // record fields; LDS stride per instant
 struct FsBlock {
   int32_t ee, n_inst, t0, r0;   // endeffector, instants, first instant's time index (fs_t), first row
   int32_t v0, nv, L, tmpl;      // CSR range [v0, v0 + nv), row length, template offset (fs_tmpl)
@@ -86,6 +90,7 @@ static_assert(sizeof(FsBlock) % 4 == 0, "FsBlock is staged to LDS as int32 words
 enum GsClass { GS_ROM = 0, GS_DYN = 1, GS_TQ = 2, GS_COUNT = 3 };   // GS_TQ: TorqueConstraintDiscretized (no base prefix)
 constexpr int kGsRowTypes = 6;
 constexpr int kGsAct = 4;
+static_assert(kFsS == kGsAct, "the FDISC record's window sums are one active window");
 // The composer launch (gstream.hip towr_gait_compose_kernel): the ForceConstraintDiscretized,
 // RangeOfMotion and Dynamic compose blocks of every problem in one grid, kComposeBlock threads each.
 // (experiment builds: -DTOWR_COMPOSE_BLOCK / -DTOWR_COMPOSE_BLOCK_RD. Round 5, ANYmal gait, B = 1024, one box, ms per step

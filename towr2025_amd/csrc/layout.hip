@@ -578,6 +578,28 @@ int64_t pattern_outside_host(const Layout& L, const double* x, const towr_terrai
 // in chunks of <= kFsInst, provided every row of the constraint holds the same column list, each column
 // is a force-set PhaseSpline column or a schedule column of the constraint's endeffector, and each force
 // polynomial's columns fit a kFsWin window of the row. Otherwise the tile path stays.
+// Whether every polynomial's active window (Layout::pact) of PhaseSpline s holds PhaseCols of one structure (count,
+// node ids, derivatives) in all three dimensions: then its kGsAct window basis sums are the same in every dimension
+// (gs_window), and a record keeps one set (the TQDISC record, layout.h).
+bool spline_dims_coincide(const Layout& L, int s) {
+  const SplineMeta& m = L.spl[s];
+  for (int p = 0; p < m.n_polys; ++p) {
+    const int32_t* w0 = L.pact.data() + m.pact_off + 2 * p;
+    for (int k = 1; k < 3; ++k) {
+      const int32_t* wk = L.pact.data() + m.pact_off + 2 * (k * m.n_polys + p);
+      if (wk[1] - wk[0] != w0[1] - w0[0]) return false;
+      for (int q = 0; q < kGsAct && w0[0] + q <= w0[1]; ++q) {
+        const PhaseCol& a = L.pcols[(size_t)m.pcol_off[0] + w0[0] + q];
+        const PhaseCol& b = L.pcols[(size_t)m.pcol_off[k] + wk[0] + q];
+        if (a.n != b.n) return false;
+        for (int j = 0; j < a.n; ++j)
+          if (a.id[j] != b.id[j] || a.deriv[j] != b.deriv[j]) return false;
+      }
+    }
+  }
+  return true;
+}
+
 int build_fstream(Layout& L, std::string& err) {
   L.fstream = false;
   L.fs_blocks.clear(); L.fs_t.clear(); L.fs_tmpl.clear(); L.fs_ws.clear(); L.fs_iee.clear(); L.fs_irow.clear(); L.fs_iblk.clear(); L.fs_tmpl_max = 0;
@@ -622,8 +644,9 @@ int build_fstream(Layout& L, std::string& err) {
       tmpl.push_back(code);
     }
     if (nsch != si.n_phases - 1) return TOWR_OK;
+    if (!spline_dims_coincide(L, fs)) return TOWR_OK;   // the record's one set of window sums (layout.h)
     // window start of each force polynomial: the columns it touches (pact ranges of its 3 dims)
-    const int wsoff = (int)wsv.size() / 2;
+    const int wsoff = (int)wsv.size() / 3;
     for (int p = 0; p < m.n_polys; ++p) {
       int lo = INT32_MAX, hi = -1;
       for (int e = 0; e < 3; ++e) {
@@ -636,11 +659,24 @@ int build_fstream(Layout& L, std::string& err) {
       }
       if (hi >= 0 && hi - lo >= kFsWin) return TOWR_OK;
       const int ws = hi >= 0 ? lo : 0;
-      int32_t wd = 0;   // dimension code of each window position (the stream kernel's prologue reads it once)
-      for (int q = 0; q < kFsWin; ++q)
-        if (ws + q < L0) wd |= ((tmpl[toff + ws + q] >> 24) & 3) << (2 * q);
+      // per window position: its dimension (3: not a PhaseCol active on p, its value is 0) and its slot in the active
+      // window of that dimension (the record keeps dimension 0's sums: the dimensions' windows coincide, checked above)
+      int32_t wd = 0, wq = 0;
+      for (int q = 0; q < kFsWin; ++q) {
+        int dim = 3, slot = 0;
+        const int32_t te = ws + q < L0 ? tmpl[toff + ws + q] : -1;
+        if (te >= 0) {
+          const int e = (te >> 24) & 3, li = (te & 0xFFFFFF) - m.pcol_off[e];
+          const int32_t* r = L.pact.data() + m.pact_off + 2 * (e * m.n_polys + p);
+          if (li >= r[0] && li <= r[1]) { dim = e; slot = li - r[0]; }
+        }
+        if (slot >= kGsAct) return TOWR_OK;
+        wd |= dim << (2 * q);
+        wq |= slot << (2 * q);
+      }
       wsv.push_back(ws);
       wsv.push_back(wd);
+      wsv.push_back(wq);
     }
     lmax = std::max(lmax, (int)L0);
     // the constraint's instants, in row order (one instant per 5 rows)
@@ -680,28 +716,6 @@ int build_fstream(Layout& L, std::string& err) {
 namespace {
 struct BaseDec { int8_t s = -1, deriv = 0, dim = 0; int32_t node = 0; };   // base node-set column
 struct PhaseDec { int8_t kind = -1, ee = 0, dim = 0; int32_t q = 0; };     // PhaseSpline column (kind 0 motion, 1 force, 2 torque)
-
-// Whether every polynomial's active window (Layout::pact) of PhaseSpline s holds PhaseCols of one structure (count,
-// node ids, derivatives) in all three dimensions: then its kGsAct window basis sums are the same in every dimension
-// (gs_window), and a record keeps one set (the TQDISC record, layout.h).
-bool spline_dims_coincide(const Layout& L, int s) {
-  const SplineMeta& m = L.spl[s];
-  for (int p = 0; p < m.n_polys; ++p) {
-    const int32_t* w0 = L.pact.data() + m.pact_off + 2 * p;
-    for (int k = 1; k < 3; ++k) {
-      const int32_t* wk = L.pact.data() + m.pact_off + 2 * (k * m.n_polys + p);
-      if (wk[1] - wk[0] != w0[1] - w0[0]) return false;
-      for (int q = 0; q < kGsAct && w0[0] + q <= w0[1]; ++q) {
-        const PhaseCol& a = L.pcols[(size_t)m.pcol_off[0] + w0[0] + q];
-        const PhaseCol& b = L.pcols[(size_t)m.pcol_off[k] + wk[0] + q];
-        if (a.n != b.n) return false;
-        for (int j = 0; j < a.n; ++j)
-          if (a.id[j] != b.id[j] || a.deriv[j] != b.deriv[j]) return false;
-      }
-    }
-  }
-  return true;
-}
 
 bool build_gstream_class(Layout& L, int cls, const std::vector<BaseDec>& bdec, const std::vector<PhaseDec>& pdec,
                          const std::vector<int>& sdec_ee, const std::vector<int>& sdec_j, std::string& why) {
