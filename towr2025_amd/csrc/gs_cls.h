@@ -9,8 +9,11 @@
 
 namespace tg {
 
-// an int field of a record: its 64-bit integer bit pattern (the composer reads the low dword in place)
-TG_HD double gs_int(int v) { return __builtin_bit_cast(double, (long long)v); }
+// two int fields of a record in one double: lo is dword 2 j, hi dword 2 j + 1 of the record's int area (the composer
+// reads them in place)
+TG_HD double gs_int2(int lo, int hi) {
+  return __builtin_bit_cast(double, (unsigned long long)(uint32_t)lo | ((unsigned long long)(uint32_t)hi << 32));
+}
 
 // The active-window basis sums of one PhaseSpline at one instant, from the block's PhaseSpline tables
 // (Ctx: SplineMeta, pact, PhaseCol in LDS): sums[e][q] = emit_dim's basis sum of the dimension's PhaseCol
@@ -39,11 +42,11 @@ TG_HD double gs_sched_val(const double* dx, const double* v, int cur, int n, int
   return 0.0;
 }
 // Per-class pieces of the composer (gs_compose): an instant's record in LDS is its RS fields
-// (stride RS | 1, layout.h record format); ci = its int fields, field j at ci[2 j] (gs_int);
+// (stride RS | 1, layout.h record format); ci = its int fields, int j at ci[j] (gs_int2);
 //   poly(): the active polynomial of a PhaseSpline segment's spline at the instant;
 //   value(): value q of a segment at the instant (the tile path's expression for that entry).
 struct RomCls {
-  TG_HD static int poly(const int32_t* ci, int, int) { return ci[8]; }
+  TG_HD static int poly(const int32_t* ci, int, int) { return ci[4]; }
   TG_HD static double value(const RobotC& rb, const int32_t* tmpl, const GsSeg& sg, int pos, const double* d, const int32_t* ci,
                                  const uint8_t* pcl, int nph) {
     const int r = sg.r;
@@ -60,13 +63,14 @@ struct RomCls {
              d[6 + r] * gs_sched_val(d + 26, d + 29, cur, nph, 2, col);
     }
     const int e = (t >> 22) & 3, q = t & 0x3FFFFF;   // motion PhaseCol: R[e][r] * basis sum (emit_dim)
-    const unsigned rel = (unsigned)(q - ci[2 + 2 * e]);
+    const unsigned rel = (unsigned)(q - ci[1 + e]);
     return rel < (unsigned)kGsAct ? d[3 * e + r] * d[32 + e * kGsAct + rel] : 0.0;
   }
 };
 
 struct DynCls {
-  TG_HD static int poly(const int32_t* ci, int kind, int ee) { return ci[2 * (ee * kDynEeNI + 11 + kind)]; }
+  // an endeffector's ints (layout.h): curX | qaX[3] | polyX | - | curF | qaF | polyF | - | qaT | polyT
+  TG_HD static int poly(const int32_t* ci, int kind, int ee) { return ci[2 * ee * kDynEeNI + (kind == 0 ? 4 : kind == 1 ? 8 : 11)]; }
   TG_HD static double value(const RobotC& rb, const int32_t* tmpl, const GsSeg& sg, int pos, const double* d, const int32_t* ci,
                                  const uint8_t* pcl, const int32_t* nph) {
     const int r = sg.r;
@@ -84,16 +88,16 @@ struct DynCls {
     const int32_t* ii = ci + 2 * ee * kDynEeNI;
     if (sg.type == 2) {   // d/d ee schedule (eval_dyn, dynamic_constraint.cc:116-122)
       const int col = t & 0xFFFF, n = nph[ee];
-      if (r >= 3) return -gs_sched_val(de + 6, de + 9, ii[0], n, r - 3, col);
+      if (r >= 3) return -gs_sched_val(de + 6, de + 9, ii[6], n, r - 3, col);
       const int e1 = r == 2 ? 0 : r + 1, e2 = r == 0 ? 2 : r - 1;
-      const double a = cross_el(de + 3, r, e1) * gs_sched_val(de + 6, de + 9, ii[0], n, e1, col) +
-                       cross_el(de + 3, r, e2) * gs_sched_val(de + 6, de + 9, ii[0], n, e2, col);
-      const double bq = cross_el(de, r, e1) * gs_sched_val(de + 12, de + 15, ii[2], n, e1, col) +
-                        cross_el(de, r, e2) * gs_sched_val(de + 12, de + 15, ii[2], n, e2, col);
+      const double a = cross_el(de + 3, r, e1) * gs_sched_val(de + 6, de + 9, ii[6], n, e1, col) +
+                       cross_el(de + 3, r, e2) * gs_sched_val(de + 6, de + 9, ii[6], n, e2, col);
+      const double bq = cross_el(de, r, e1) * gs_sched_val(de + 12, de + 15, ii[0], n, e1, col) +
+                        cross_el(de, r, e2) * gs_sched_val(de + 12, de + 15, ii[0], n, e2, col);
       return a + bq;
     }
     const int kind = sg.kind, e = (t >> 22) & 3, q = t & 0x3FFFFF;
-    const unsigned rel = (unsigned)(q - ii[2 * (2 + 3 * kind + e)]);
+    const unsigned rel = (unsigned)(q - ii[kind == 0 ? 1 + e : kind == 1 ? 7 : 10]);
     if (rel >= (unsigned)kGsAct) return 0.0;
     const double v = de[dyn_sum_field(kind, e, rel)];
     // emit_dim scales: motion Cross(f)[r][e]; force Cross(rv)[r][e] (angular) or -1 (linear); torque -1
@@ -105,7 +109,7 @@ struct DynCls {
 // TorqueConstraintDiscretized rows r = 0..3 scale the torque window by tb[r] = t1, t2, n, -n and (rows 2,
 // 3) the force window by b = -k mu n; a schedule column is eval_tqdisc's sum of the two linear forms
 struct TqCls {
-  TG_HD static int poly(const int32_t* ci, int kind, int) { return ci[2 * (kind == 2 ? 7 : 8)]; }
+  TG_HD static int poly(const int32_t* ci, int kind, int) { return ci[kind == 2 ? 3 : 4]; }   // cur | qaT | qaF | polyT | polyF
   TG_HD static double tb(const double* d, int r, int e) { return r == 3 ? -d[6 + e] : d[3 * r + e]; }
   TG_HD static double value(const RobotC& rb, const int32_t* tmpl, const GsSeg& sg, int pos, const double* d, const int32_t* ci,
                                  const uint8_t*, int nph) {
@@ -122,7 +126,7 @@ struct TqCls {
       return v;
     }
     const int kind = sg.kind, e = (t >> 22) & 3, q = t & 0x3FFFFF;   // torque (kind 2) or force (1) PhaseCol
-    const unsigned rel = (unsigned)(q - ci[2 * (kind == 2 ? 1 + e : 4 + e)]);
+    const unsigned rel = (unsigned)(q - ci[kind == 2 ? 1 : 2]);   // (one first PhaseCol for the three dimensions)
     if (rel >= (unsigned)kGsAct) return 0.0;
     const double sum = d[(kind == 2 ? 24 : 28) + rel];   // (one set for the three dimensions, layout.h)
     return (kind == 2 ? tb(d, r, e) : d[9 + e]) * sum;   // emit_dim: scale * basis sum
@@ -156,24 +160,21 @@ TG_HD void tq_record(const Ctx& c, const GsInst& gi, Put&& put, double g[4]) {
   sched_jac(c, sp_force(ee), t, F, Jf);
 #pragma unroll
   for (int e = 0; e < 3; ++e) { put(12 + e, Jt.dx[e]); put(15 + e, Jt.v[e]); put(18 + e, Jf.dx[e]); put(21 + e, Jf.v[e]); }
-  put(kTqND, gs_int(Jt.cur));
   double H[4], sums[3][kGsAct];
-  int qa[3];
+  int qa[3], qaT;
   // (the window sums of the three dimensions coincide: the layout checked the PhaseCols, spline_dims_coincide)
   spline_basis(Tq, kPos, H);   // AccumulateLinearFormJacobian of the torque spline (:147-155)
   gs_window(c, sp_torque(ee), Tq.poly, H, sums, qa);
-#pragma unroll
-  for (int e = 0; e < 3; ++e) put(kTqND + 1 + e, gs_int(qa[e]));
+  qaT = qa[0];
+  put(kTqND, gs_int2(Jt.cur, qaT));
 #pragma unroll
   for (int q = 0; q < kGsAct; ++q) put(24 + q, sums[0][q]);
   spline_basis(F, kPos, H);    // ... of the force spline into the normal-torque rows (:158-163)
   gs_window(c, sp_force(ee), F.poly, H, sums, qa);
 #pragma unroll
-  for (int e = 0; e < 3; ++e) put(kTqND + 4 + e, gs_int(qa[e]));
-#pragma unroll
   for (int q = 0; q < kGsAct; ++q) put(28 + q, sums[0][q]);
-  put(kTqND + 7, gs_int(Tq.poly));
-  put(kTqND + 8, gs_int(F.poly));
+  put(kTqND + 1, gs_int2(qa[0], Tq.poly));
+  put(kTqND + 2, gs_int2(F.poly, 0));
 }
 
 }  // namespace tg

@@ -38,7 +38,6 @@ namespace {
 // FsBlock (field f of the block's instant kk at kFsRS t0 + f n + kk), so a compose block's prologue is
 // one contiguous copy.
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ double fs_int(int v) { return __longlong_as_double((long long)v); }
 // FDISC instant k (fs_t order) of the problem in c: its record fields through put(field, value) and its 5 g
 // rows (when wanted) straight to Gb
 // the FDISC tables a record lane reads after its instant: in LDS (staged by towr_gait_frec_kernel) or global memory
@@ -57,16 +56,14 @@ __device__ __forceinline__ void fdisc_record(const KParams& P, const FsTabs& T, 
     for (int e = 0; e < 3; ++e) put(kFsB + 3 * i + e, o.b[i][e]);
 #pragma unroll
   for (int e = 0; e < 3; ++e) { put(kFsDx + e, o.Jf.dx[e]); put(kFsV + e, o.Jf.v[e]); }
-  put(kFsND + 2, fs_int(o.Jf.cur));
   if (P.want_g)
 #pragma unroll
     for (int i = 0; i < 5; ++i) __builtin_nontemporal_store(o.g[i], Gb + row + i);
   TG_STAMP(P, 5);
   const int poly = o.poly;
   const int ws = T.ws[3 * (fb.wsoff + poly)], wd = T.ws[3 * (fb.wsoff + poly) + 1], wq = T.ws[3 * (fb.wsoff + poly) + 2];
-  put(kFsND, fs_int(ws));
-  put(kFsND + 1, fs_int(wd));
-  put(kFsND + 3, fs_int(wq));
+  put(kFsND, gs_int2(ws, wd));
+  put(kFsND + 1, gs_int2(o.Jf.cur, wq));
   double h0 = o.H[0], h1 = o.H[1], h2 = o.H[2], h3 = o.H[3];
   asm volatile("" : "+v"(h0), "+v"(h1), "+v"(h2), "+v"(h3));
   const SplineMeta m = c.spl[sp_force(P.fs_iee[k])];
@@ -202,30 +199,36 @@ __device__ __forceinline__ void gs_records(const KParams& P, const GsRecArgs& A,
       for (int e = 0; e < 3; ++e) sk[e] = Sp.p[e];
       const int fd = kDynBaseND + kDynEeND * ee, fi = NDd + kDynEeNI * ee;
       auto put = [&](int f, double v) { *gs_field(Rd, RSd, k, gi, f) = v; };
+      int qa[3];
       {   // the active window's basis sums
         double H[4], sums[3][kGsAct];
-        int qa[3];
         spline_basis(Sp, kPos, H);
         gs_window(c, sp, Sp.poly, H, sums, qa);
-        put(fi + 11 + kind, gs_int(Sp.poly));
 #pragma unroll
-        for (int e = 0; e < 3; ++e) {
-          put(fi + 2 + 3 * kind + e, gs_int(qa[e]));
+        for (int e = 0; e < 3; ++e)
           if (kind == 0 || e == 0)   // force and torque: one set for the three dimensions (layout.h)
 #pragma unroll
             for (int q = 0; q < kGsAct; ++q) put(fd + dyn_sum_field(kind, e, q), sums[e][q]);
-        }
       }
+      // the lane's ints (layout.h: curX | qaX[3] | polyX | - | curF | qaF | polyF | - | qaT | polyT)
       if (kind < 2) {   // force and ee-position schedule terms (dynamic_constraint.cc:116-122; no torque term)
         SchedJac J;
         sched_jac(c, sp, t, Sp, J);
         const int o = kind == 1 ? 6 : 12;
 #pragma unroll
         for (int e = 0; e < 3; ++e) { put(fd + o + e, J.dx[e]); put(fd + o + 3 + e, J.v[e]); }
-        put(fi + (kind == 1 ? 0 : 1), gs_int(J.cur));
-        if (kind == 1)
+        if (kind == 1) {
 #pragma unroll
           for (int e = 0; e < 3; ++e) put(fd + e, Sp.p[e]);
+          put(fi + 3, gs_int2(J.cur, qa[0]));
+          put(fi + 4, gs_int2(Sp.poly, 0));
+        } else {
+          put(fi, gs_int2(J.cur, qa[0]));
+          put(fi + 1, gs_int2(qa[1], qa[2]));
+          put(fi + 2, gs_int2(Sp.poly, 0));
+        }
+      } else {
+        put(fi + 5, gs_int2(qa[0], Sp.poly));
       }
     } else if (i >= r0) {   // RangeOfMotion instant
       const int k = i - r0;
@@ -274,23 +277,22 @@ __device__ __forceinline__ void gs_records(const KParams& P, const GsRecArgs& A,
       for (int bb = 0; bb < 4; ++bb) put(22 + bb, HA[bb]);
       double H[4];
       spline_basis(M, kPos, H);
+      int qa[3];
       {
         double sums[3][kGsAct];
-        int qa[3];
         gs_window(c, sp_motion(gi.ee), M.poly, H, sums, qa);
 #pragma unroll
-        for (int e = 0; e < 3; ++e) {
-          put(kRomND + 1 + e, gs_int(qa[e]));
+        for (int e = 0; e < 3; ++e)
 #pragma unroll
           for (int qq = 0; qq < kGsAct; ++qq) put(32 + e * kGsAct + qq, sums[e][qq]);
-        }
       }
       SchedJac Jx;
       sched_jac(c, sp_motion(gi.ee), t, M, Jx);   // b_R_w * d pos / d schedule (:123-130)
 #pragma unroll
       for (int e = 0; e < 3; ++e) { put(26 + e, Jx.dx[e]); put(29 + e, Jx.v[e]); }
-      put(kRomND, gs_int(Jx.cur));
-      put(kRomND + 4, gs_int(M.poly));
+      put(kRomND, gs_int2(Jx.cur, qa[0]));   // ints cur | qa[3] | poly
+      put(kRomND + 1, gs_int2(qa[1], qa[2]));
+      put(kRomND + 2, gs_int2(M.poly, 0));
     }
   }
   if (Kd == 0 || part == 2) return;
@@ -425,7 +427,7 @@ constexpr int kFsUnits = TOWR_FS_UNITS;
 template <int BLOCK>
 __device__ __forceinline__ void fs_rows(const FsBlock& fb, const double* cd, double* rowv, int32_t* wsr) {
   const int tid = threadIdx.x, nr = 5 * fb.n_inst;
-  auto ci = [&](int k, int f) -> int { return *reinterpret_cast<const int32_t*>(cd + k * kFsCS + kFsND + f); };   // ws, wd, cur, wq
+  auto ci = [&](int k, int f) -> int { return reinterpret_cast<const int32_t*>(cd + k * kFsCS + kFsND)[f]; };   // ws, wd, cur, wq
   for (int t = tid; t < nr * kFsWin; t += BLOCK) {
     const int r = t / kFsWin, q = t - r * kFsWin;
     const int k = r / 5, i = r - 5 * k;
@@ -449,7 +451,7 @@ __device__ __forceinline__ void fs_stream(const KParams& P, const FsBlock& fb, i
   const int tid = threadIdx.x;
   const int Lr = fb.L, js0 = fb.js0, ns1 = fb.ns1;
   const float invL = 1.0f / (float)Lr;   // exact row for block ranges below kFloatDivMax (layout.h, checked by build_fstream)
-  auto ci = [&](int k, int f) -> int { return *reinterpret_cast<const int32_t*>(cd + k * kFsCS + kFsND + f); };
+  auto ci = [&](int k, int f) -> int { return reinterpret_cast<const int32_t*>(cd + k * kFsCS + kFsND)[f]; };
   // entry j of row r (instant k = r / 5, pyramid row i): eval_fdisc's value (see fdisc_sched_value / emit_dim)
   auto entry = [&](int r, int j) -> double {
 #pragma clang fp contract(off)   // (lambda bodies: the enclosing function's pragma is not relied on)

@@ -56,13 +56,13 @@ constexpr int kFsWin = 12;
 // (build_fstream, build_gstream_class: fewer instants per block, or the tile path).
 constexpr int kFloatDivMax = 1 << 21;
 // FDISC record (gstream.hip fdisc_records -> the composer): S[kFsS] | b[5][3] | Jf.dx[3] | Jf.v[3] | ints ws, wd,
-// cur, wq (64-bit integer bit patterns). S = the basis sums of the force polynomial's active window in dimension 0;
+// cur, wq (two 32-bit ints per double, gs_int2). S = the basis sums of the force polynomial's active window in dimension 0;
 // the three dimensions' windows hold PhaseCols of one structure (build_fstream checks it), so window position q
 // holds S[slot q] (wq: 2 bits per position) times b[row][dim q] (wd: 2 bits per position, 3 = not an active column:
 // 0). Round 5's record kept the 12 window positions' sums (36 fields instead of 29).
 constexpr int kFsS = 4;   // = kGsAct (below)
 constexpr int kFsB = kFsS, kFsDx = kFsS + 15, kFsV = kFsS + 18, kFsND = kFsS + 21;
-constexpr int kFsRS = kFsND + 4, kFsCS = kFsRS | 1;   // record fields; LDS stride per instant
+constexpr int kFsRS = kFsND + 2, kFsCS = kFsRS | 1;   // record fields; LDS stride per instant
 struct FsBlock {
   int32_t ee, n_inst, t0, r0;   // endeffector, instants, first instant's time index (fs_t), first row
   int32_t v0, nv, L, tmpl;      // CSR range [v0, v0 + nv), row length, template offset (fs_tmpl)
@@ -132,30 +132,32 @@ struct GsBlock { int32_t geo, k0, n_inst, v0, nv, reserved[3]; };   // instants 
 // p0: TorqueConstraintDiscretized's k_friction (ItemDesc::p0)
 struct GsInst { double t; int32_t seg, row0; int16_t ee, kk, nb, reserved; double p0; };
 // Records (gstream.hip gs_records): per instant RS fields, the composer's view of the instant —
-// ND doubles then NI ints (stored as doubles) — so that a composer block's prologue is one contiguous
+// ND doubles then NI doubles of ints, two 32-bit ints per double (gs_int2; int j is dword j of that area) — so that a composer block's prologue is one contiguous
 // copy. The fields of the GsBlock of instants [k0, k0 + n) form one chunk at RS * k0 (class-global
 // instant index), field-major inside it (field f of instant k0 + kk at RS * k0 + f * n + kk).
 //   RangeOfMotion: R[9] | HL[4] | Ag[axis][r] (9) | HA[4] | Jx.dx[3] v[3] | sums[dim][4] (12);
-//                  ints cur | qa[dim] (3) | poly
+//                  ints cur | qa[dim] (3) | poly (3 doubles)
 //   Dynamic:       fs[3] | Lp[3] | HpL[4] | HaL[4] | A[axis][p v a][r] (27) | HpA HvA HaA (12), then per
 //                  endeffector Fp[3] | rv[3] | Jf.dx v[6] | Jx.dx v[6] | motion sums[dim][4] (12) | force sums[4] |
-//                  torque sums[4]; ints per endeffector curF | curX | qa[kind][dim] (9) | poly[kind] (3). The force
+//                  torque sums[4]; ints per endeffector (6 doubles, each pair written by one record lane): curX | qaX[3] |
+//                  polyX | - | curF | qaF | polyF | - | qaT | polyT (the force and torque windows start at one PhaseCol
+//                  index in every dimension, spline_dims_coincide; round 5: 14 ints in 14 doubles). The force
 //                  and torque sums are one set for the three dimensions, as TQDISC's below (the layout streams Dynamic
 //                  only when they coincide, spline_dims_coincide): 38 doubles per endeffector instead of round 5's 54
 //   TorqueConstraintDiscretized: t1[3] | t2[3] | n[3] | b[3] (= -k mu n) | Jt.dx v[6] | Jf.dx v[6] |
-//                  torque sums[4] | force sums[4]; ints cur | qaT[3] | qaF[3] | polyT | polyF. The sums are
+//                  torque sums[4] | force sums[4]; ints cur | qaT | qaF | polyT | polyF (3 doubles). The sums and qa are
 //                  the same for the three dimensions (the layout streams TQDISC only when the torque and force
 //                  splines' active windows hold PhaseCols of one structure in every dimension, spline_dims_coincide),
-//                  so one set of 4 per spline: 41 fields instead of round 5's 57
+//                  so one set of 4 per spline: 35 fields instead of round 5's 57
 //                  (torque_constraint_discretized.cc:139-235 without the motion block: a terrain
 //                  without curvature, where every motion scale is exactly 0.0 and the block is skipped, :57)
 // (kind 0 motion, 1 force, 2 torque; sums / qa: the active-window basis sums of the PhaseSpline, the
 // first active PhaseCol of each dimension and the basis sums of up to kGsAct PhaseCols from it)
-constexpr int kRomND = 44, kRomNI = 5;
-constexpr int kDynBaseND = 53, kDynEeND = 38, kDynEeNI = 14;
+constexpr int kRomND = 44, kRomNI = 3;
+constexpr int kDynBaseND = 53, kDynEeND = 38, kDynEeNI = 6;
 // field of the window sum q of kind (0 motion, 1 force, 2 torque) and dimension e in a Dynamic record's endeffector part
 TG_HD constexpr int dyn_sum_field(int kind, int e, int q) { return kind == 0 ? 18 + e * kGsAct + q : 26 + kind * kGsAct + q; }
-constexpr int kTqND = 32, kTqNI = 9;
+constexpr int kTqND = 32, kTqNI = 3;
 TG_HD constexpr int gs_rec_nd(int cls, int E) { return cls == GS_ROM ? kRomND : cls == GS_TQ ? kTqND : kDynBaseND + kDynEeND * E; }
 TG_HD constexpr int gs_rec_ni(int cls, int E) { return cls == GS_ROM ? kRomNI : cls == GS_TQ ? kTqNI : kDynEeNI * E; }
 TG_HD constexpr int gs_rec_fields(int cls, int E) { return gs_rec_nd(cls, E) + gs_rec_ni(cls, E); }

@@ -579,15 +579,15 @@ int64_t pattern_outside_host(const Layout& L, const double* x, const towr_terrai
 // is a force-set PhaseSpline column or a schedule column of the constraint's endeffector, and each force
 // polynomial's columns fit a kFsWin window of the row. Otherwise the tile path stays.
 // Whether every polynomial's active window (Layout::pact) of PhaseSpline s holds PhaseCols of one structure (count,
-// node ids, derivatives) in all three dimensions: then its kGsAct window basis sums are the same in every dimension
-// (gs_window), and a record keeps one set (the TQDISC record, layout.h).
+// node ids, derivatives) from one PhaseCol index in all three dimensions: then its kGsAct window basis sums and its first
+// active PhaseCol are the same in every dimension (gs_window), and a record keeps one set (the TQDISC record, layout.h).
 bool spline_dims_coincide(const Layout& L, int s) {
   const SplineMeta& m = L.spl[s];
   for (int p = 0; p < m.n_polys; ++p) {
     const int32_t* w0 = L.pact.data() + m.pact_off + 2 * p;
     for (int k = 1; k < 3; ++k) {
       const int32_t* wk = L.pact.data() + m.pact_off + 2 * (k * m.n_polys + p);
-      if (wk[1] - wk[0] != w0[1] - w0[0]) return false;
+      if (wk[0] != w0[0] || wk[1] != w0[1]) return false;   // one first PhaseCol index: the records keep one qa
       for (int q = 0; q < kGsAct && w0[0] + q <= w0[1]; ++q) {
         const PhaseCol& a = L.pcols[(size_t)m.pcol_off[0] + w0[0] + q];
         const PhaseCol& b = L.pcols[(size_t)m.pcol_off[k] + wk[0] + q];
