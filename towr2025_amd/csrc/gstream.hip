@@ -641,8 +641,11 @@ __device__ __forceinline__ void gs_compose(const KParams& P, const GsBlock* blks
     // (2 or 4 values per thread formed before their LDS stores, so that their load chains overlap: the value phase is
     // 3.6 / 5.6 of a 15 / 19 us Dynamic / RangeOfMotion block (tools/stamps.py), but the gait step measured 0.595-0.603
     // vs 0.594-0.607 ms and + Torque 1.19-1.20 vs 1.16 ms: not kept)
-    for (int t = tid; t < n * vt; t += BLOCK) {   // every value of every instant, once
-      const int kk = t / vt, v = t - kk * vt;
+    // every value of every instant, once; instant-fastest lanes (t = v n + kk), so that a wave's lanes share a few value
+    // slots and with them one segment's code path (instant-major lanes mixed 2-3 segment kinds in most waves)
+    const float invn = 1.0f / (float)n;   // exact: n vt < kFloatDivMax (build_gstream_class's encodings)
+    for (int t = tid; t < n * vt; t += BLOCK) {
+      const int v = (int)(((float)t + 0.5f) * invn), kk = t - v * n;
       const uint32_t vm = vmap[v];
       const int sid = (int)(vm >> 16), q = (int)(vm & 0xFFFF);
       const GsSeg sg = segs[sid];
@@ -654,7 +657,7 @@ __device__ __forceinline__ void gs_compose(const KParams& P, const GsBlock* blks
         if constexpr (CLS == GS_DYN) x = C::value(P.rb, tmpl, sg, pos, d, ci, pcl + kk * g.Psum, nph);
         else x = C::value(P.rb, tmpl, sg, pos, d, ci, pcl + kk * g.Psum, nph[g.ee]);
       }
-      val[t] = x;
+      val[kk * vt + v] = x;
     }
     __syncthreads();
     if (it == 0) TG_STAMP(P, 3);
